@@ -1,0 +1,405 @@
+#!/usr/bin/env python3
+"""bench.py -- batched CRDT merge throughput on MI355X (driver contract).
+
+    python bench.py --gpus N --steps K --warmup W [--workload NAME]
+
+Default workload = BASELINE.json configs[1]: G-Counter join of 1M replicas x
+64 nodes uint64 per GPU (out = max(A, B) elementwise).  One "step" = one
+pass of the hot path over one batch; inputs are generated in HBM before the
+timed region.  N>1: one process per GPU (torchrun), each rank joins its own
+replica shard (weak scaling, no data-path collective: pairwise joins of
+independent replicas have no exchange step).  The sharded whole-population
+join with its real exchange step (fold + RCCL all-reduce(max)) is
+--workload shard_fold (configs[4]).
+
+Prints ONE JSON line (rank 0) with value = whole-job units/s, a roofline
+object for the dominant kernel (HIP-event-timed on the launch stream) and a
+cpu_baseline object (the oracle restatement on this host's cores, rank 0 at
+N=1 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from crdt_amd import engine as E  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+METRIC = "replica-merges/sec + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
+
+
+def dist_init():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: int, world: int, dev) -> int:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+# --------------------------------------------------------------------------- workloads
+class Workload:
+    """setup() allocates device inputs; step() enqueues one pass of the hot path."""
+    name = ""
+    unit = "replica-merges/s"
+    dtype = "u64"
+    kernel = ""           # dominant kernel name (for the rocprof cross-check)
+    config: dict = {}
+
+    def units(self) -> int: ...
+    def bytes_per_launch(self) -> int: ...
+    def step(self): ...
+
+
+class GCounterJoin(Workload):
+    name = "gcounter_join"
+    kernel = "k_join"
+
+    def __init__(self, eng, rank, world, rows, nodes, seed=2024):
+        self.eng, self.rows, self.nodes = eng, rows, nodes
+        base = rank * rows                       # weak scaling: each rank its own replicas
+        self.a = eng.synth_counters(seed, 1, rows, nodes, row_base=base)
+        self.b = eng.synth_counters(seed, 2, rows, nodes, row_base=base)
+        self.out = torch.empty_like(self.a)
+        self.config = {"workload": f"G-Counter join, {rows} replicas x {nodes} nodes uint64 per GPU "
+                                   "(BASELINE configs[1])", "rows_per_gpu": rows, "nodes": nodes,
+                       "parallelism": f"replica-shard x{world}"}
+
+    def units(self):
+        return self.rows
+
+    def bytes_per_launch(self):
+        return 3 * self.rows * self.nodes * 8    # read A, read B, write out once
+
+    def step(self):
+        self.eng.gcounter_join(self.a, self.b, out=self.out)
+
+    def cpu_baseline(self, seconds, threads):
+        from oracle import oracle
+        rows = min(self.rows, 250_000)
+        a = E.as_u64(self.a[:rows]).reshape(rows, self.nodes)
+        b = E.as_u64(self.b[:rows]).reshape(rows, self.nodes)
+        # parity spot-check of the sample before timing it
+        assert np.array_equal(oracle.gcounter_join(a, b, threads), E.as_u64(self.out[:rows]).reshape(rows, self.nodes))
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.gcounter_join(a, b, threads)
+            done += rows
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle/crdt_oracle.c oc_gcounter_join (C restatement, not the Go reference: no Go "
+                          f"toolchain), {rows} replicas x {self.nodes} nodes from the same device inputs, "
+                          f"repeated {done // rows}x over {dt:.1f}s, {threads} pthreads"}
+
+
+class PNCounterJoin(GCounterJoin):
+    name = "pncounter_join"
+    kernel = "k_join_pn"
+
+    def __init__(self, eng, rank, world, rows, nodes, seed=2024):
+        super().__init__(eng, rank, world, rows, nodes, seed)
+        base = rank * rows
+        self.na = eng.synth_counters(seed, 3, rows, nodes, row_base=base)
+        self.nb = eng.synth_counters(seed, 4, rows, nodes, row_base=base)
+        self.nout = torch.empty_like(self.na)
+        self.config = dict(self.config, workload=f"PN-Counter join, {rows} replicas x {nodes} nodes (P,N) uint64")
+
+    def bytes_per_launch(self):
+        return 6 * self.rows * self.nodes * 8
+
+    def step(self):
+        self.eng.pncounter_join(self.a, self.na, self.b, self.nb, self.out, self.nout)
+
+    def cpu_baseline(self, seconds, threads):
+        return None
+
+
+class VClockClassify(Workload):
+    name = "vclock_classify"
+    unit = "pairs/s"
+    kernel = "k_vclock"
+
+    def __init__(self, eng, rank, world, pairs, nodes, seed=2024):
+        self.eng, self.pairs, self.nodes = eng, pairs, nodes
+        self.a, self.b = eng.synth_vclock_pairs(seed, pairs, nodes, pair_base=rank * pairs)
+        self.cls = torch.empty(pairs, dtype=torch.uint8, device=eng.device)
+        self.config = {"workload": f"vector-clock classify, {pairs} pairs x {nodes} nodes (BASELINE configs[2])",
+                       "pairs_per_gpu": pairs, "nodes": nodes, "parallelism": f"replicas x{world}"}
+
+    def units(self):
+        return self.pairs
+
+    def bytes_per_launch(self):
+        return self.pairs * (2 * self.nodes * 8 + 1)
+
+    def step(self):
+        self.eng.vclock_classify(self.a, self.b, out=self.cls)
+
+    def cpu_baseline(self, seconds, threads):
+        from oracle import oracle
+        n = min(self.pairs, 200_000)
+        a, b = E.as_u64(self.a[:n]), E.as_u64(self.b[:n])
+        assert np.array_equal(oracle.vclock_classify(a, b, threads), self.cls[:n].cpu().numpy())
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.vclock_classify(a, b, threads)
+            done += n
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oc_vclock_classify, {n} pairs x {self.nodes} nodes, {dt:.1f}s, {threads} pthreads"}
+
+
+class SetMerge(Workload):
+    unit = "input-tuples/s"
+    kernel = "k_set_tile"
+
+    def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
+        self.eng, self.n, self.lww = eng, n, lww
+        self.name = "lww_merge" if lww else "orset_merge"
+        s = seed + 7919 * rank
+        self.A = eng.synth_set_tuples(s, 0, n, key_space)
+        self.B = eng.synth_set_tuples(s, 1, n, key_space)
+        self.out = E.TupleSet.empty(2 * n, eng.device)
+        self.count = torch.zeros(1, dtype=torch.int64, device=eng.device)
+        fn = eng.lww_merge if lww else eng.orset_merge
+        fn(self.A, self.B, out=self.out, count=self.count, trim=False)
+        torch.cuda.synchronize()
+        self.n_out = int(self.count.item())
+        self.config = {"workload": f"{'LWW-Element-Set' if lww else 'OR-Set'} merge, {n} tuples per side, "
+                                   f"key space {key_space}, pre-sorted (BASELINE configs[3], D1)",
+                       "tuples_per_side": n, "key_space": key_space, "n_out": self.n_out,
+                       "parallelism": f"replicas x{world}"}
+        self._fn = fn
+
+    def units(self):
+        return 2 * self.n
+
+    def bytes_per_launch(self):
+        return 21 * 2 * self.n + 21 * self.n_out
+
+    def step(self):
+        self._fn(self.A, self.B, out=self.out, count=self.count, trim=False)
+
+    def cpu_baseline(self, seconds, threads):
+        from oracle import oracle
+        a = self.A.to_numpy()
+        b = self.B.to_numpy()
+        fn = oracle.lww_merge if self.lww else oracle.orset_merge
+        done, t0 = 0, time.perf_counter()
+        while True:
+            fn(a, b)
+            done += 2 * self.n
+            if time.perf_counter() - t0 > seconds:
+                break
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": 1, "kind": "port",
+                "sample": f"oc_{self.name} (serial merge), {self.n} tuples per side, {done // (2 * self.n)} reps"}
+
+
+class ShardFold(Workload):
+    """configs[4]: R replicas sharded over the ranks; fold + all-reduce(max)."""
+    name = "shard_fold"
+    unit = "replica-merges/s"
+    kernel = "k_fold_pow2"
+
+    def __init__(self, eng, rank, world, total_rows, nodes, seed=2024):
+        import ctypes as C
+        from crdt_amd import _lib
+        self.eng, self.world, self.nodes, self.total = eng, world, nodes, total_rows
+        b, e = C.c_uint64(), C.c_uint64()
+        _lib.call("crdt_shard_range", total_rows, world, rank, C.byref(b), C.byref(e))
+        self.rows = e.value - b.value
+        self.a = eng.synth_counters(seed, 1, self.rows, nodes, row_base=b.value)
+        self.fold = torch.empty(nodes, dtype=torch.int64, device=eng.device)
+        self.ordered = torch.empty(nodes, dtype=torch.int64, device=eng.device)
+        self.config = {"workload": f"sharded fold, {total_rows} replicas x {nodes} nodes total, "
+                                   f"fold + all-reduce(max) (BASELINE configs[4])",
+                       "total_rows": total_rows, "rows_per_gpu": self.rows, "nodes": nodes,
+                       "parallelism": f"row-shard x{world} + RCCL all-reduce(max)"}
+
+    def units(self):
+        return self.rows
+
+    def bytes_per_launch(self):
+        return self.rows * self.nodes * 8
+
+    def step(self):
+        self.eng.gcounter_fold(self.a, out=self.fold)
+        if self.world > 1:
+            import torch.distributed as dist
+            self.eng.u64_to_ordered_i64(self.fold, out=self.ordered)
+            dist.all_reduce(self.ordered, op=dist.ReduceOp.MAX)
+            self.eng.ordered_i64_to_u64(self.ordered, out=self.fold)
+
+    def cpu_baseline(self, seconds, threads):
+        return None
+
+
+def make_workload(name, eng, rank, world, args):
+    if name == "gcounter_join":
+        return GCounterJoin(eng, rank, world, args.rows, args.nodes)
+    if name == "pncounter_join":
+        return PNCounterJoin(eng, rank, world, args.rows, args.nodes)
+    if name == "vclock_classify":
+        return VClockClassify(eng, rank, world, args.pairs, 128)
+    if name in ("lww_merge", "orset_merge"):
+        return SetMerge(eng, rank, world, args.set_n, args.key_space, lww=(name == "lww_merge"))
+    if name == "shard_fold":
+        return ShardFold(eng, rank, world, args.total_rows, args.nodes)
+    raise SystemExit(f"unknown workload {name}")
+
+
+def load_traffic(workload: Workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f).get(workload.name)
+    except (OSError, ValueError):
+        return None
+    if not d or d.get("bytes_per_launch_algorithmic") != workload.bytes_per_launch():
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="gcounter_join",
+                    choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
+                             "shard_fold"])
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--nodes", type=int, default=64)
+    ap.add_argument("--pairs", type=int, default=10_000_000)
+    ap.add_argument("--set-n", type=int, default=10_000_000)
+    ap.add_argument("--key-space", type=int, default=8_000_000)
+    ap.add_argument("--total-rows", type=int, default=100_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--option", action="append", default=[], help="name=value kernel knob (crdt_set_option)")
+    args = ap.parse_args()
+
+    world, rank, local = dist_init()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    for o in args.option:
+        k, v = o.split("=")
+        from crdt_amd import _lib
+        _lib.call("crdt_set_option", k.encode(), int(v))
+
+    eng = E.Engine(local)
+    wl = make_workload(args.workload, eng, rank, world, args)
+    dev = eng.device
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for k in range(args.steps):
+        wl.step()
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+
+    step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+    gpu_s = sum(step_ms) / 1e3
+    elapsed = max_over_ranks(wall, world, dev)
+    total_units = sum_over_ranks(wl.units() * args.steps, world, dev)
+    value = total_units / elapsed
+
+    out = None
+    if rank == 0:
+        avg_ms = float(np.mean(step_ms))
+        med_ms = float(np.median(step_ms))
+        achieved = wl.bytes_per_launch() / (avg_ms / 1e3) / 1e9
+        traffic = load_traffic(wl)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": wl.kernel, "bytes_per_launch": wl.bytes_per_launch(),
+                "avg_launch_us": round(avg_ms * 1e3, 2), "median_launch_us": round(med_ms * 1e3, 2),
+                "timing": "HIP events on the launch stream, per step"}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and hasattr(wl, "cpu_baseline"):
+            threads = min(16, os.cpu_count() or 1)
+            cpu = wl.cpu_baseline(args.cpu_seconds, threads)
+            if cpu is not None:
+                cpu["value"] = round(cpu["value"], 1)
+                cpu["host_cpu"] = _cpu_model()
+                cpu["nproc"] = os.cpu_count()
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": wl.unit, "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak" if wl.name != "shard_fold" else "strong",
+            "vs_baseline": None, "dtype": wl.dtype,
+            "data": "synthetic (SplitMix64-seeded, generated in HBM)",
+            "config": wl.config, "roofline": roof, "cpu_baseline": cpu,
+            "gpu_time_s": round(gpu_s, 6),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    eng.close()
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+"""ctypes binding of libcrdt_amd.so -- the C-ABI declared in include/crdt_amd.h.
+
+The shared library is built in-tree (``crdt_amd/libcrdt_amd.so``) by
+``__graft_entry__.build()``.  There is deliberately NO fallback: if the
+library is missing or cannot be loaded, every product entry point raises
+:class:`CrdtLibraryError` (a CPU path would void the parity claims).
+
+``torch`` is imported before the library is opened so that the library's
+``libamdhip64.so.7`` dependency resolves to the HIP runtime torch already
+loaded (same SONAME): one HIP runtime per process, so torch's device
+pointers and streams are valid inside the library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (load order: torch's HIP runtime first)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcrdt_amd.so")
+
+CRDT_OK = 0
+STATUS_NAMES = {
+    0: "CRDT_OK",
+    -1: "CRDT_E_INVAL",
+    -2: "CRDT_E_HIP",
+    -3: "CRDT_E_NOMEM",
+    -4: "CRDT_E_NODEV",
+    -5: "CRDT_E_UNSORTED",
+    -6: "CRDT_E_RANGE",
+}
+
+
+class CrdtLibraryError(RuntimeError):
+    """libcrdt_amd.so is missing or failed to load (no silent fallback)."""
+
+
+class CrdtError(RuntimeError):
+    """A C-ABI call returned a negative crdt_status."""
+
+    def __init__(self, fn: str, status: int, hip_error: int = 0):
+        self.status = status
+        self.hip_error = hip_error
+        name = STATUS_NAMES.get(status, str(status))
+        msg = f"{fn} failed: {name}"
+        if hip_error:
+            msg += f" (hipError {hip_error})"
+        super().__init__(msg)
+
+
+class crdt_tuples(C.Structure):
+    _fields_ = [("key", C.c_void_p), ("ts", C.c_void_p), ("rep", C.c_void_p), ("tomb", C.c_void_p)]
+
+
+class crdt_refmerge_in(C.Structure):
+    _fields_ = [
+        ("replicas", C.c_uint32), ("n_slots", C.c_uint32),
+        ("n_l", C.c_uint64), ("n_r", C.c_uint64), ("n_kv", C.c_uint64), ("n_str", C.c_uint64),
+        ("l_off", C.c_void_p), ("l_ts", C.c_void_p), ("l_origin", C.c_void_p), ("l_kv", C.c_void_p),
+        ("r_off", C.c_void_p), ("r_ts", C.c_void_p), ("r_kv", C.c_void_p),
+        ("kv_key", C.c_void_p), ("kv_val", C.c_void_p),
+        ("str_bytes", C.c_void_p), ("str_off", C.c_void_p),
+    ]
+
+
+class crdt_refmerge_out(C.Structure):
+    _fields_ = [
+        ("off", C.c_void_p), ("ts", C.c_void_p), ("origin", C.c_void_p), ("src", C.c_void_p),
+        ("st_kind", C.c_void_p), ("st_str", C.c_void_p), ("st_sum", C.c_void_p),
+    ]
+
+
+_P = C.c_void_p
+_SZ = C.c_size_t
+_U64 = C.c_uint64
+_I = C.c_int
+_CTX = C.c_void_p
+
+# name -> (restype, argtypes); exactly the functions include/crdt_amd.h declares.
+SIGNATURES = {
+    "crdt_abi_version": (_I, []),
+    "crdt_status_str": (C.c_char_p, [_I]),
+    "crdt_device_count": (_I, [C.POINTER(_I)]),
+    "crdt_ctx_create": (_I, [_I, _P, C.POINTER(_P)]),
+    "crdt_ctx_destroy": (_I, [_CTX]),
+    "crdt_ctx_set_stream": (_I, [_CTX, _P]),
+    "crdt_ctx_sync": (_I, [_CTX]),
+    "crdt_ctx_last_hip_error": (_I, [_CTX]),
+    "crdt_ctx_reserve": (_I, [_CTX, _SZ]),
+    "crdt_set_option": (_I, [C.c_char_p, C.c_int64]),
+    "crdt_dev_alloc": (_I, [_CTX, _SZ, C.POINTER(_P)]),
+    "crdt_dev_free": (_I, [_CTX, _P]),
+    "crdt_memcpy_h2d": (_I, [_CTX, _P, _P, _SZ]),
+    "crdt_memcpy_d2h": (_I, [_CTX, _P, _P, _SZ]),
+    "crdt_memset": (_I, [_CTX, _P, _I, _SZ]),
+    "crdt_compare_int64": (_I, [C.c_int64, C.c_int64]),
+    "crdt_gcounter_join": (_I, [_CTX, _P, _P, _P, _SZ, _SZ]),
+    "crdt_gcounter_fold": (_I, [_CTX, _P, _SZ, _SZ, _P]),
+    "crdt_gcounter_value": (_I, [_CTX, _P, _SZ, _SZ, _P]),
+    "crdt_pncounter_join": (_I, [_CTX, _P, _P, _P, _P, _P, _P, _SZ, _SZ]),
+    "crdt_pncounter_value": (_I, [_CTX, _P, _P, _P, _SZ, _SZ]),
+    "crdt_vclock_classify": (_I, [_CTX, _P, _P, _P, _SZ, _SZ]),
+    "crdt_lww_merge": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                            C.POINTER(crdt_tuples), _P]),
+    "crdt_orset_merge": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                              C.POINTER(crdt_tuples), _P]),
+    "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),
+    "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
+    "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
+    "crdt_shard_range": (_I, [_U64, _I, _I, C.POINTER(_U64), C.POINTER(_U64)]),
+    "crdt_u64_to_ordered_i64": (_I, [_CTX, _P, _P, _SZ]),
+    "crdt_ordered_i64_to_u64": (_I, [_CTX, _P, _P, _SZ]),
+    "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
+    "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),
+    "crdt_synth_set_tuples": (_I, [_CTX, _U64, C.c_uint32, C.POINTER(crdt_tuples), _SZ, _U64]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib() -> C.CDLL:
+    """Open libcrdt_amd.so once; raise CrdtLibraryError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise CrdtLibraryError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(make -C crdt_amd/csrc). There is no CPU fallback.")
+        try:
+            handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise CrdtLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+        return _lib
+
+
+def check(fn: str, status: int, ctx=None) -> None:
+    if status != CRDT_OK:
+        hip = lib().crdt_ctx_last_hip_error(ctx) if ctx else 0
+        raise CrdtError(fn, status, hip)
+
+
+def call(fn: str, *args, ctx=None) -> int:
+    st = getattr(lib(), fn)(*args)
+    if isinstance(st, int) and st < 0:
+        check(fn, st, ctx)
+    return st

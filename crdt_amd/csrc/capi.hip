@@ -1,0 +1,207 @@
+// capi.hip -- context lifecycle, memory helpers, options, small host-side
+// entry points of the C-ABI (include/crdt_amd.h).
+#include <string.h>
+
+#include "common.hpp"
+
+namespace crdt {
+JoinTuning g_join;
+int g_vclock_pairs_per_wave = 4;
+int g_sets_items = 8;
+
+int ws_reserve(crdt_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->ws_bytes) return CRDT_OK;
+    size_t want = bytes + bytes / 4;                  // grow with headroom
+    want = (want + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    hipError_t e;
+    if (ctx->ws) {
+        e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        e = hipFree(ctx->ws);
+        ctx->ws = nullptr;
+        ctx->ws_bytes = 0;
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
+    e = hipMalloc(&ctx->ws, want);
+    if (e != hipSuccess) {
+        ctx->ws = nullptr;
+        return hip_fail(ctx, e);
+    }
+    ctx->ws_bytes = want;
+    return CRDT_OK;
+}
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_abi_version(void) { return CRDT_AMD_ABI_VERSION; }
+
+extern "C" const char *crdt_status_str(int s) {
+    switch (s) {
+        case CRDT_OK: return "ok";
+        case CRDT_E_INVAL: return "invalid argument";
+        case CRDT_E_HIP: return "HIP runtime error";
+        case CRDT_E_NOMEM: return "device out of memory";
+        case CRDT_E_NODEV: return "no gfx950 device";
+        case CRDT_E_UNSORTED: return "input not sorted";
+        case CRDT_E_RANGE: return "size exceeds kernel index range";
+        default: return "unknown status";
+    }
+}
+
+extern "C" int crdt_device_count(int *count) {
+    if (!count) return CRDT_E_INVAL;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *count = 0; return CRDT_E_NODEV; }
+    *count = n;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_ctx_create(int device, void *stream, crdt_ctx **out) {
+    if (!out) return CRDT_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CRDT_E_NODEV;
+    if (device < 0 || device >= n) return CRDT_E_INVAL;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return CRDT_E_NODEV;
+    // gfx950 only: the kernels are compiled for nothing else.
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CRDT_E_NODEV;
+    crdt_ctx *ctx = new (std::nothrow) crdt_ctx();
+    if (!ctx) return CRDT_E_NOMEM;
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    if (stream) {
+        ctx->stream = (hipStream_t)stream;
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { int rc = hip_fail(ctx, e); delete ctx; return rc; }
+        ctx->own_stream = true;
+    }
+    *out = ctx;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
+    if (!ctx) return CRDT_OK;
+    (void)bind(ctx);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream) {
+    if (!ctx) return CRDT_E_INVAL;
+    if (!stream) return CRDT_E_INVAL;
+    if (ctx->own_stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+        ctx->own_stream = false;
+    }
+    ctx->stream = (hipStream_t)stream;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_ctx_sync(crdt_ctx *ctx) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+extern "C" int crdt_ctx_last_hip_error(const crdt_ctx *ctx) { return ctx ? ctx->last_hip_error : 0; }
+
+extern "C" int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    return ws_reserve(ctx, bytes);
+}
+
+extern "C" int crdt_set_option(const char *name, int64_t v) {
+    if (!name) return CRDT_E_INVAL;
+    if (!strcmp(name, "join.unroll")) {
+        if (v != 1 && v != 2 && v != 4 && v != 8) return CRDT_E_INVAL;
+        g_join.unroll = (int)v;
+    } else if (!strcmp(name, "join.nontemporal")) {
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_join.nontemporal = (int)v;
+    } else if (!strcmp(name, "join.blocks_per_cu")) {
+        if (v < 1 || v > 64) return CRDT_E_INVAL;
+        g_join.blocks_per_cu = (int)v;
+    } else if (!strcmp(name, "vclock.pairs_per_wave")) {
+        if (v != 1 && v != 2 && v != 4 && v != 8) return CRDT_E_INVAL;
+        g_vclock_pairs_per_wave = (int)v;
+    } else if (!strcmp(name, "sets.items")) {
+        if (v != 4 && v != 8) return CRDT_E_INVAL;
+        g_sets_items = (int)v;
+    } else {
+        return CRDT_E_INVAL;
+    }
+    return CRDT_OK;
+}
+
+extern "C" int crdt_dev_alloc(crdt_ctx *ctx, size_t bytes, void **dev) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!dev) return CRDT_E_INVAL;
+    *dev = nullptr;
+    if (bytes == 0) return CRDT_OK;
+    hipError_t e = hipMalloc(dev, bytes);
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+extern "C" int crdt_dev_free(crdt_ctx *ctx, void *dev) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!dev) return CRDT_OK;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipFree(dev);
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+extern "C" int crdt_memcpy_h2d(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (bytes == 0) return CRDT_OK;
+    if (!dst || !src) return CRDT_E_INVAL;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+extern "C" int crdt_memcpy_d2h(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (bytes == 0) return CRDT_OK;
+    if (!dst || !src) return CRDT_E_INVAL;
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);   // host buffer valid on return
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+extern "C" int crdt_memset(crdt_ctx *ctx, void *dst, int byte, size_t bytes) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (bytes == 0) return CRDT_OK;
+    if (!dst) return CRDT_E_INVAL;
+    hipError_t e = hipMemsetAsync(dst, byte, bytes, ctx->stream);
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+// utils.Int64Comparator (gods v1.18.1; main.go:106-107): signed order.
+extern "C" int crdt_compare_int64(int64_t a, int64_t b) { return a < b ? -1 : (a > b ? 1 : 0); }
+
+extern "C" int crdt_shard_range(uint64_t rows, int world, int rank, uint64_t *begin, uint64_t *end) {
+    if (world <= 0 || rank < 0 || rank >= world || !begin || !end) return CRDT_E_INVAL;
+    // Balanced contiguous split: the first (rows % world) ranks take one extra row.
+    const uint64_t q = rows / (uint64_t)world, r = rows % (uint64_t)world;
+    const uint64_t k = (uint64_t)rank;
+    *begin = k * q + (k < r ? k : r);
+    *end = *begin + q + (k < r ? 1 : 0);
+    return CRDT_OK;
+}

@@ -1,0 +1,106 @@
+// common.hpp -- shared internals of libcrdt_amd (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/crdt_amd.h"
+
+struct crdt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 256;
+    int last_hip_error = 0;
+    void *ws = nullptr;      // device workspace, grown on demand (crdt_ctx_reserve)
+    size_t ws_bytes = 0;
+};
+
+namespace crdt {
+
+constexpr int kWave = 64;     // CDNA wavefront width (never 32)
+
+inline int hip_fail(crdt_ctx *ctx, hipError_t e) {
+    if (ctx) ctx->last_hip_error = (int)e;
+    return e == hipErrorOutOfMemory ? CRDT_E_NOMEM : CRDT_E_HIP;
+}
+
+// Process-wide kernel tuning knobs (crdt_set_option); defined in capi.hip.
+struct JoinTuning {
+    int unroll = 4;         // 16-B vectors in flight per lane per operand
+    int nontemporal = 1;    // nt loads/stores for once-touched streams
+    int blocks_per_cu = 8;  // grid = CUs * blocks_per_cu (grid-stride beyond)
+};
+extern JoinTuning g_join;
+extern int g_vclock_pairs_per_wave;
+extern int g_sets_items;
+
+// Make the context's device current for this host thread.
+inline int bind(crdt_ctx *ctx) {
+    if (!ctx) return CRDT_E_INVAL;
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (cur != ctx->device) {
+        e = hipSetDevice(ctx->device);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
+    return CRDT_OK;
+}
+
+inline int check_launch(crdt_ctx *ctx) {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+// Grow the workspace to at least `bytes` (synchronises the stream first so
+// that in-flight kernels never see the old buffer freed).
+int ws_reserve(crdt_ctx *ctx, size_t bytes);
+
+// Bump allocator over the workspace (256-B aligned carve-outs).
+struct Carve {
+    char *base;
+    size_t used = 0;
+    explicit Carve(void *b) : base((char *)b) {}
+    template <class T> T *take(size_t n) {
+        used = (used + 255) & ~(size_t)255;
+        T *p = (T *)(base + used);
+        used += n * sizeof(T);
+        return p;
+    }
+    static size_t round(size_t b) { return (b + 255) & ~(size_t)255; }
+};
+
+inline bool mul_overflows(size_t a, size_t b) {
+    return a != 0 && b > SIZE_MAX / a;
+}
+
+inline unsigned grid_for(size_t work_items, unsigned block, unsigned cap) {
+    size_t g = (work_items + block - 1) / block;
+    if (g > cap) g = cap;
+    if (g == 0) g = 1;
+    return (unsigned)g;
+}
+
+// Device-wide exclusive scan of n uint32 flags/counts into uint64 offsets;
+// out[n] receives the total.  Workspace from `tmp` (scan_tmp_bytes(n)).
+size_t scan_tmp_bytes(size_t n);
+int exclusive_scan_u32(crdt_ctx *ctx, const uint32_t *in, uint64_t *out, size_t n, void *tmp);
+
+// ---- SplitMix64 (Steele, Lea, Flood 2014): the seeded synthetic generator.
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+__host__ __device__ inline uint64_t stream_key(uint64_t seed, uint64_t stream) {
+    return splitmix64(seed ^ splitmix64(stream));
+}
+// i-th output of a SplitMix64 sequence started at state k.
+__host__ __device__ inline uint64_t rnd(uint64_t k, uint64_t i) {
+    return splitmix64(k + i * 0x9E3779B97F4A7C15ULL);
+}
+
+}  // namespace crdt

@@ -1,0 +1,312 @@
+"""Device-level host API over the C-ABI (include/crdt_amd.h).
+
+PyTorch is plumbing here: it owns device memory (tensors in HBM) and the
+stream; every merge/compare computation runs in libcrdt_amd.so's gfx950 HIP
+kernels.  uint64 state is carried in int64 tensors (same bits); use
+:func:`as_u64` to view a host copy as numpy uint64.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, crdt_refmerge_in, crdt_refmerge_out, crdt_tuples
+
+VC_EQUAL, VC_BEFORE, VC_AFTER, VC_CONCURRENT = 0, 1, 2, 3
+
+
+def as_u64(t: torch.Tensor) -> np.ndarray:
+    """Host numpy uint64 view of an 8-byte integer tensor (any device)."""
+    return t.detach().cpu().contiguous().numpy().view(np.uint64)
+
+
+def u64_tensor(a, device) -> torch.Tensor:
+    """numpy uint64 (or int64) array -> int64 tensor with the same bits."""
+    a = np.ascontiguousarray(a)
+    if a.dtype != np.int64:
+        a = a.view(np.int64) if a.dtype.itemsize == 8 else a.astype(np.int64)
+    return torch.from_numpy(a.copy()).to(device)
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class TupleSet:
+    """SoA (key u64, ts u64, rep u32, tomb u8) tuples, sorted by (key, ts, rep)."""
+
+    key: torch.Tensor   # int64 storage of uint64 keys
+    ts: torch.Tensor    # int64 storage of uint64 timestamps
+    rep: torch.Tensor   # int32 storage of uint32 replica ids
+    tomb: torch.Tensor  # uint8 0/1
+
+    def __len__(self) -> int:
+        return int(self.key.numel())
+
+    @staticmethod
+    def empty(n: int, device) -> "TupleSet":
+        return TupleSet(torch.empty(n, dtype=torch.int64, device=device),
+                        torch.empty(n, dtype=torch.int64, device=device),
+                        torch.empty(n, dtype=torch.int32, device=device),
+                        torch.empty(n, dtype=torch.uint8, device=device))
+
+    def c(self) -> crdt_tuples:
+        return crdt_tuples(self.key.data_ptr(), self.ts.data_ptr(), self.rep.data_ptr(), self.tomb.data_ptr())
+
+    def slice(self, n: int) -> "TupleSet":
+        return TupleSet(self.key[:n], self.ts[:n], self.rep[:n], self.tomb[:n])
+
+    def to_numpy(self):
+        return (as_u64(self.key), as_u64(self.ts), self.rep.cpu().numpy().view(np.uint32),
+                self.tomb.cpu().numpy())
+
+    @staticmethod
+    def from_numpy(key, ts, rep, tomb, device) -> "TupleSet":
+        return TupleSet(u64_tensor(key, device), u64_tensor(ts, device),
+                        torch.from_numpy(np.ascontiguousarray(rep).view(np.int32).copy()).to(device),
+                        torch.from_numpy(np.ascontiguousarray(tomb).astype(np.uint8)).to(device))
+
+
+class Engine:
+    """One crdt_ctx bound to one GPU and to torch's current stream."""
+
+    def __init__(self, device: int | torch.device = 0):
+        if not torch.cuda.is_available():
+            raise _lib.CrdtLibraryError("no GPU visible: the crdt_amd engine has no CPU path")
+        self.device = torch.device("cuda", device if isinstance(device, int) else device.index or 0)
+        lib = _lib.lib()
+        self._stream = torch.cuda.current_stream(self.device).cuda_stream
+        ctx = C.c_void_p()
+        call("crdt_ctx_create", self.device.index, self._stream, C.byref(ctx))
+        self.ctx = ctx
+        self._lib = lib
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self._lib.crdt_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _bind(self) -> None:
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream:
+            call("crdt_ctx_set_stream", self.ctx, s, ctx=self.ctx)
+            self._stream = s
+
+    def _call(self, fn: str, *args) -> None:
+        self._bind()
+        call(fn, self.ctx, *args, ctx=self.ctx)
+
+    def _check(self, *ts: torch.Tensor, itemsize: int | None = None) -> None:
+        for t in ts:
+            if t.device != self.device:
+                raise ValueError(f"tensor on {t.device}, engine on {self.device}")
+            if not t.is_contiguous():
+                raise ValueError("tensors must be contiguous")
+            if itemsize is not None and t.element_size() != itemsize:
+                raise ValueError(f"expected {itemsize}-byte elements, got {t.dtype}")
+
+    def sync(self) -> None:
+        self._call("crdt_ctx_sync")
+
+    def reserve(self, nbytes: int) -> None:
+        self._call("crdt_ctx_reserve", nbytes)
+
+    # ------------------------------------------------------------ counters (a6)
+    def gcounter_join(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """out = max(a, b) elementwise (uint64); a, b: [rows, nodes]."""
+        if a.shape != b.shape or a.dim() != 2:
+            raise ValueError("a and b must be [rows, nodes] of equal shape")
+        out = torch.empty_like(a) if out is None else out
+        self._check(a, b, out, itemsize=8)
+        if out.shape != a.shape:
+            raise ValueError("out shape mismatch")
+        self._call("crdt_gcounter_join", a.data_ptr(), b.data_ptr(), out.data_ptr(), a.shape[0], a.shape[1])
+        return out
+
+    vclock_join = gcounter_join
+
+    def gcounter_fold(self, a: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """out[n] = max over rows of a[:, n]."""
+        rows, nodes = a.shape
+        out = torch.empty(nodes, dtype=torch.int64, device=self.device) if out is None else out
+        self._check(a, out, itemsize=8)
+        self._call("crdt_gcounter_fold", a.data_ptr(), rows, nodes, out.data_ptr())
+        return out
+
+    def gcounter_value(self, a: torch.Tensor) -> torch.Tensor:
+        rows, nodes = a.shape
+        out = torch.empty(rows, dtype=torch.int64, device=self.device)
+        self._check(a, out, itemsize=8)
+        self._call("crdt_gcounter_value", a.data_ptr(), rows, nodes, out.data_ptr())
+        return out
+
+    def pncounter_join(self, pa, na, pb, nb, pout=None, nout=None):
+        pout = torch.empty_like(pa) if pout is None else pout
+        nout = torch.empty_like(na) if nout is None else nout
+        for t in (na, pb, nb, pout, nout):
+            if t.shape != pa.shape:
+                raise ValueError("PN-Counter operands must share one [rows, nodes] shape")
+        self._check(pa, na, pb, nb, pout, nout, itemsize=8)
+        rows, nodes = pa.shape
+        self._call("crdt_pncounter_join", pa.data_ptr(), na.data_ptr(), pb.data_ptr(), nb.data_ptr(),
+                   pout.data_ptr(), nout.data_ptr(), rows, nodes)
+        return pout, nout
+
+    def pncounter_value(self, p: torch.Tensor, n: torch.Tensor) -> torch.Tensor:
+        if p.shape != n.shape:
+            raise ValueError("P and N must share one shape")
+        rows, nodes = p.shape
+        out = torch.empty(rows, dtype=torch.int64, device=self.device)
+        self._check(p, n, out, itemsize=8)
+        self._call("crdt_pncounter_value", p.data_ptr(), n.data_ptr(), out.data_ptr(), rows, nodes)
+        return out
+
+    # ------------------------------------------------------------ vector clocks (a7)
+    def vclock_classify(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if a.shape != b.shape or a.dim() != 2:
+            raise ValueError("a and b must be [pairs, nodes] of equal shape")
+        pairs, nodes = a.shape
+        out = torch.empty(pairs, dtype=torch.uint8, device=self.device) if out is None else out
+        self._check(a, b, itemsize=8)
+        self._check(out, itemsize=1)
+        self._call("crdt_vclock_classify", a.data_ptr(), b.data_ptr(), out.data_ptr(), pairs, nodes)
+        return out
+
+    # ------------------------------------------------------------ sets (a8)
+    def _set_merge(self, fn: str, a: TupleSet, b: TupleSet, out: TupleSet | None,
+                   count: torch.Tensor | None, trim: bool):
+        na, nb = len(a), len(b)
+        out = TupleSet.empty(max(na + nb, 1), self.device) if out is None else out
+        count = torch.empty(1, dtype=torch.int64, device=self.device) if count is None else count
+        for s in (a, b, out):
+            self._check(s.key, s.ts, itemsize=8)
+            self._check(s.rep, itemsize=4)
+            self._check(s.tomb, itemsize=1)
+        ca, cb, co = a.c(), b.c(), out.c()
+        self._call(fn, C.byref(ca), na, C.byref(cb), nb, C.byref(co), count.data_ptr())
+        if trim:
+            return out.slice(int(count.item()))
+        return out, count
+
+    def lww_merge(self, a: TupleSet, b: TupleSet, out: TupleSet | None = None,
+                  count: torch.Tensor | None = None, trim: bool = True):
+        """LWW-Element-Set merge; a is the local (tie-winning) operand."""
+        return self._set_merge("crdt_lww_merge", a, b, out, count, trim)
+
+    def orset_merge(self, a: TupleSet, b: TupleSet, out: TupleSet | None = None,
+                    count: torch.Tensor | None = None, trim: bool = True):
+        """OR-Set merge: union of tags, tombstones OR-ed."""
+        return self._set_merge("crdt_orset_merge", a, b, out, count, trim)
+
+    def count_unsorted(self, t: TupleSet) -> int:
+        bad = torch.empty(1, dtype=torch.int64, device=self.device)
+        ct = t.c()
+        self._call("crdt_tuples_count_unsorted", C.byref(ct), len(t), bad.data_ptr())
+        return int(bad.item())
+
+    # ------------------------------------------------------------ RefMerge (a1-a3)
+    def refmerge_batch(self, packed: dict) -> dict:
+        """Run the batched bit-exact reference merge on a packed batch.
+
+        ``packed`` holds device tensors produced by
+        :func:`crdt_amd.refmerge.pack_batch`; returns device output tensors.
+        """
+        d = packed
+        n_l, n_r = d["l_ts"].numel(), d["r_ts"].numel()
+        n_slots = int(d["n_slots"])
+        dev = self.device
+        out = {
+            "off": torch.empty(d["replicas"] + 1, dtype=torch.int64, device=dev),
+            "ts": torch.empty(max(n_l + n_r, 1), dtype=torch.int64, device=dev),
+            "origin": torch.empty(max(n_l + n_r, 1), dtype=torch.uint8, device=dev),
+            "src": torch.empty(max(n_l + n_r, 1), dtype=torch.int64, device=dev),
+            "st_kind": torch.empty(max(n_slots, 1), dtype=torch.uint8, device=dev),
+            "st_str": torch.empty(max(n_slots, 1), dtype=torch.int32, device=dev),
+            "st_sum": torch.empty(max(n_slots, 1), dtype=torch.int64, device=dev),
+        }
+        cin = crdt_refmerge_in(
+            d["replicas"], n_slots, n_l, n_r, d["kv_key"].numel(), d["str_off"].numel() - 1,
+            _ptr(d["l_off"]), _ptr(d["l_ts"]), _ptr(d["l_origin"]), _ptr(d["l_kv"]),
+            _ptr(d["r_off"]), _ptr(d["r_ts"]), _ptr(d["r_kv"]),
+            _ptr(d["kv_key"]), _ptr(d["kv_val"]), _ptr(d["str_bytes"]), _ptr(d["str_off"]))
+        cout = crdt_refmerge_out(*(out[k].data_ptr() for k in
+                                   ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum")))
+        self._call("crdt_refmerge_batch", C.byref(cin), C.byref(cout))
+        return out
+
+    def atoi_batch(self, str_bytes: torch.Tensor, str_off: torch.Tensor):
+        n = str_off.numel() - 1
+        ok = torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
+        val = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        self._call("crdt_atoi_batch", str_bytes.data_ptr(), str_off.data_ptr(), n, ok.data_ptr(), val.data_ptr())
+        return ok[:n], val[:n]
+
+    # ------------------------------------------------------------ sharding helpers (a9)
+    def u64_to_ordered_i64(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        out = torch.empty_like(x) if out is None else out
+        self._call("crdt_u64_to_ordered_i64", x.data_ptr(), out.data_ptr(), x.numel())
+        return out
+
+    def ordered_i64_to_u64(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        out = torch.empty_like(x) if out is None else out
+        self._call("crdt_ordered_i64_to_u64", x.data_ptr(), out.data_ptr(), x.numel())
+        return out
+
+    # ------------------------------------------------------------ synthetic state
+    def synth_counters(self, seed: int, stream: int, rows: int, nodes: int, row_base: int = 0,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+        out = torch.empty(rows, nodes, dtype=torch.int64, device=self.device) if out is None else out
+        self._call("crdt_synth_counters", seed, stream, out.data_ptr(), rows * nodes, row_base * nodes)
+        return out
+
+    def synth_vclock_pairs(self, seed: int, pairs: int, nodes: int, pair_base: int = 0):
+        a = torch.empty(pairs, nodes, dtype=torch.int64, device=self.device)
+        b = torch.empty(pairs, nodes, dtype=torch.int64, device=self.device)
+        self._call("crdt_synth_vclock_pairs", seed, a.data_ptr(), b.data_ptr(), pairs, nodes, pair_base)
+        return a, b
+
+    def synth_set_tuples(self, seed: int, side: int, n: int, key_space: int, sort: bool = True) -> TupleSet:
+        t = TupleSet.empty(n, self.device)
+        ct = t.c()
+        self._call("crdt_synth_set_tuples", seed, side, C.byref(ct), n, key_space)
+        if sort:
+            t = sort_tuples(t)
+        return t
+
+
+def sort_tuples(t: TupleSet) -> TupleSet:
+    """Stable sort by (key, ts, rep): input preparation for the D1 config.
+
+    Input prep only (not the measured path): the synthetic fields fit one
+    int64 composite (key < 2^37, ts < 2^20, rep < 2^6).
+    """
+    if len(t) == 0:
+        return t
+    kmax = int(t.key.max().item())
+    tmax = int(t.ts.max().item())
+    rmax = int(t.rep.max().item())
+    if kmax >= (1 << 37) or tmax >= (1 << 20) or rmax >= (1 << 6) or min(
+            int(t.key.min().item()), int(t.ts.min().item()), int(t.rep.min().item())) < 0:
+        # general case: three stable passes, least significant field first;
+        # uint64 fields are sign-flipped so signed argsort gives unsigned order
+        flip = torch.iinfo(torch.int64).min
+        order = torch.argsort(t.rep.to(torch.int64) & 0xFFFFFFFF, stable=True)
+        for f in (t.ts, t.key):
+            g = f[order] ^ flip
+            order = order[torch.argsort(g, stable=True)]
+    else:
+        comp = (t.key << 26) | (t.ts << 6) | t.rep.to(torch.int64)
+        order = torch.argsort(comp, stable=True)
+    return TupleSet(t.key[order].contiguous(), t.ts[order].contiguous(), t.rep[order].contiguous(),
+                    t.tomb[order].contiguous())

@@ -1,0 +1,205 @@
+/*
+ * crdt_amd.h -- C-ABI of the MI355X-native batched CRDT merge engine.
+ *
+ * This is the drop-in boundary for the merge/compare path of
+ * anuragsarkar97/crdt (/root/reference/main.go).  The reference exposes no
+ * FFI: its path is the unexported Go method `func (server *Server) merge()`
+ * (main.go:35-100) over a gods treemap ordered by `utils.Int64Comparator`
+ * (main.go:106-107).  Every entry point below names the reference interface
+ * it replaces; INTEGRATION.md shows the cgo binding a maintainer would add.
+ *
+ * Conventions:
+ *   - plain pointers and sizes; no C++/torch types cross the boundary;
+ *   - every call returns int: 0 = CRDT_OK, < 0 = crdt_status (never aborts,
+ *     never throws);
+ *   - "dev" pointers are device (HBM) addresses; work is enqueued on the
+ *     context's stream and is asynchronous unless the name says _sync/_host;
+ *   - the library never retains caller pointers past a call (cgo rule);
+ *   - a context is single-stream and not thread-safe: one context per
+ *     Server/goroutine, mirroring the reference's one mutex per Server
+ *     (main.go:32, :43-44).
+ */
+#ifndef CRDT_AMD_H
+#define CRDT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRDT_AMD_ABI_VERSION 1
+
+typedef enum crdt_status {
+    CRDT_OK = 0,
+    CRDT_E_INVAL = -1,      /* bad argument (null pointer, size overflow, bad option) */
+    CRDT_E_HIP = -2,        /* HIP runtime error; see crdt_ctx_last_hip_error() */
+    CRDT_E_NOMEM = -3,      /* device allocation failed */
+    CRDT_E_NODEV = -4,      /* no usable gfx950 device */
+    CRDT_E_UNSORTED = -5,   /* input violates the documented sort order */
+    CRDT_E_RANGE = -6       /* an index/size does not fit the kernel's integer width */
+} crdt_status;
+
+typedef struct crdt_ctx crdt_ctx;
+
+/* ---------------------------------------------------------------- library */
+int         crdt_abi_version(void);
+const char *crdt_status_str(int status);
+int         crdt_device_count(int *count);
+
+/* ---------------------------------------------------------------- context */
+/* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or
+ * NULL for a library-owned non-blocking stream. */
+int crdt_ctx_create(int device, void *stream, crdt_ctx **out);
+int crdt_ctx_destroy(crdt_ctx *ctx);
+int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream);
+int crdt_ctx_sync(crdt_ctx *ctx);
+int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
+/* Pre-size the context's device workspace so that later calls never
+ * allocate (needed before graph capture). */
+int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
+/* Kernel tuning knobs (process-wide), for A/B runs: "join.unroll" (1,2,4,8),
+ * "join.nontemporal" (0/1), "join.blocks_per_cu" (1..64),
+ * "vclock.pairs_per_wave" (1,2,4,8), "sets.items" (4,8).
+ * Returns CRDT_E_INVAL for an unknown name or value. */
+int crdt_set_option(const char *name, int64_t value);
+
+/* Device memory for hosts without an allocator of their own (the Go side). */
+int crdt_dev_alloc(crdt_ctx *ctx, size_t bytes, void **dev);
+int crdt_dev_free(crdt_ctx *ctx, void *dev);
+int crdt_memcpy_h2d(crdt_ctx *ctx, void *dev_dst, const void *host_src, size_t bytes);
+int crdt_memcpy_d2h(crdt_ctx *ctx, void *host_dst, const void *dev_src, size_t bytes);
+int crdt_memset(crdt_ctx *ctx, void *dev_dst, int byte, size_t bytes);
+
+/* ------------------------------------------------------- compare (a2)
+ * utils.Int64Comparator (main.go:106-107): signed total order, -1/0/+1. */
+int crdt_compare_int64(int64_t a, int64_t b);
+
+/* ------------------------------------------------ G-Counter / PN-Counter (a6)
+ * Replica population state: row-major [rows x nodes] uint64 in HBM.
+ * No reference code: build-defined state-based CRDT joins. */
+
+/* out[r][n] = max(a[r][n], b[r][n]) (unsigned).  out may alias a or b. */
+int crdt_gcounter_join(crdt_ctx *ctx, const uint64_t *a_dev, const uint64_t *b_dev,
+                       uint64_t *out_dev, size_t rows, size_t nodes);
+/* out[n] = max_r a[r][n]  (the join of a whole population; identity 0). */
+int crdt_gcounter_fold(crdt_ctx *ctx, const uint64_t *a_dev, size_t rows, size_t nodes,
+                       uint64_t *out_dev);
+/* out[r] = sum_n a[r][n] (uint64 wrap): the G-Counter value of every replica. */
+int crdt_gcounter_value(crdt_ctx *ctx, const uint64_t *a_dev, size_t rows, size_t nodes,
+                        uint64_t *out_dev);
+/* PN-Counter = (P, N) pair: both joined in one launch.  Outputs may alias. */
+int crdt_pncounter_join(crdt_ctx *ctx, const uint64_t *pa_dev, const uint64_t *na_dev,
+                        const uint64_t *pb_dev, const uint64_t *nb_dev,
+                        uint64_t *pout_dev, uint64_t *nout_dev, size_t rows, size_t nodes);
+/* out[r] = (int64)(sum_n P[r][n] - sum_n N[r][n]) with uint64 wrap (main.go:95). */
+int crdt_pncounter_value(crdt_ctx *ctx, const uint64_t *p_dev, const uint64_t *n_dev,
+                         int64_t *out_dev, size_t rows, size_t nodes);
+
+/* ------------------------------------------------------ vector clocks (a7) */
+typedef enum crdt_vc_class {
+    CRDT_VC_EQUAL = 0,      /* a == b                  */
+    CRDT_VC_BEFORE = 1,     /* a <  b  (a happened-before b) */
+    CRDT_VC_AFTER = 2,      /* a >  b                  */
+    CRDT_VC_CONCURRENT = 3  /* neither dominates        */
+} crdt_vc_class;
+/* Join of vector clocks is the elementwise max: crdt_gcounter_join. */
+/* cls[p] = classify(a[p], b[p]) for [pairs x nodes] uint64 clocks.  With
+ * nodes == 1 this is the sign of Int64Comparator (main.go:106) on unsigned
+ * values, mapped EQUAL/BEFORE/AFTER. */
+int crdt_vclock_classify(crdt_ctx *ctx, const uint64_t *a_dev, const uint64_t *b_dev,
+                         uint8_t *cls_dev, size_t pairs, size_t nodes);
+
+/* ---------------------------------------------- LWW-Element-Set / OR-Set (a8)
+ * Structure-of-arrays tuples, sorted ascending by (key, ts, rep).
+ * Tie rule: on an exactly equal (ts, rep) the left operand (a, the local
+ * replica) wins, as the reference keeps the local value on an equal
+ * timestamp (main.go:54-65). */
+typedef struct crdt_tuples {
+    uint64_t *key;
+    uint64_t *ts;
+    uint32_t *rep;
+    uint8_t  *tomb;
+} crdt_tuples;
+
+/* LWW: one tuple per distinct key = the max (ts, rep) element (left wins an
+ * exact tie; tombstoned winners are kept).  out capacity >= na + nb;
+ * *out_count_dev (device uint64) receives the output length. */
+int crdt_lww_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                   size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
+/* OR-Set: union of unique tags (key, ts, rep); tomb OR-ed over equal tags. */
+int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                     size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
+/* Sortedness check (host-facing validation): *bad_dev = number of adjacent
+ * pairs with t[i] > t[i+1]. */
+int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
+                               uint64_t *bad_dev);
+
+/* ------------------------------------------------ RefMerge (a1-a5)
+ * Batched, bit-exact (*Server).merge() (main.go:35-100) for many replicas.
+ * Each replica's Diff (L) and RemoteDiff (R) are ascending unique int64 ts
+ * arrays (treemap keys under Int64Comparator, main.go:106), concatenated
+ * over replicas with CSR offsets.  Entry e owns key/value pairs
+ * [kv_off[e], kv_off[e+1]) of one kv arena (L entries' ranges and R
+ * entries' ranges both index it).  kv_key is a key SLOT: the host interns
+ * each replica's key strings into its own disjoint slot range.  kv_val is a
+ * value string id into (str_bytes, str_off).
+ * origin: 1 = local write (*Command, main.go:187) -- skipped by the replay
+ * (main.go:80); 0 = remote map (main.go:245-255). */
+typedef struct crdt_refmerge_in {
+    uint32_t replicas;
+    uint32_t n_slots;
+    uint64_t n_l, n_r, n_kv, n_str;
+    const uint64_t *l_off;      /* [replicas+1] */
+    const int64_t  *l_ts;       /* [n_l] */
+    const uint8_t  *l_origin;   /* [n_l] */
+    const uint64_t *l_kv;       /* [n_l+1] */
+    const uint64_t *r_off;      /* [replicas+1] */
+    const int64_t  *r_ts;       /* [n_r] */
+    const uint64_t *r_kv;       /* [n_r+1] */
+    const uint32_t *kv_key;     /* [n_kv] slot id < n_slots */
+    const uint32_t *kv_val;     /* [n_kv] string id < n_str */
+    const uint8_t  *str_bytes;
+    const uint64_t *str_off;    /* [n_str+1] */
+} crdt_refmerge_in;
+
+typedef struct crdt_refmerge_out {
+    uint64_t *off;      /* [replicas+1] new Diff ranges */
+    int64_t  *ts;       /* capacity n_l + n_r: new Diff keys, ascending per replica */
+    uint8_t  *origin;   /* origin of each new Diff entry */
+    int64_t  *src;      /* >= 0: index into L; < 0: R index j encoded as -(j+1) */
+    uint8_t  *st_kind;  /* [n_slots] CurrentState: 0 absent, 1 verbatim, 2 sum */
+    uint32_t *st_str;   /* [n_slots] verbatim value string id (kind 1) */
+    int64_t  *st_sum;   /* [n_slots] Itoa() operand (kind 2) */
+} crdt_refmerge_out;
+
+/* All pointers in `in` / `out` are device pointers. */
+int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out);
+/* Go strconv.Atoi over a string arena: ok[s] = parsable, val[s] = value. */
+int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *str_bytes_dev, const uint64_t *str_off_dev,
+                    uint64_t n_str, uint8_t *ok_dev, int64_t *val_dev);
+
+/* ------------------------------------------------ sharding (a9)
+ * Contiguous row range [*begin, *end) of rank `rank` in a world of `world`
+ * ranks (replica populations shard by contiguous rows). */
+int crdt_shard_range(uint64_t rows, int world, int rank, uint64_t *begin, uint64_t *end);
+/* Order-preserving map between uint64 and int64 (x ^ 2^63): lets a signed
+ * int64 MAX all-reduce (RCCL/gloo) compute the unsigned max exactly. */
+int crdt_u64_to_ordered_i64(crdt_ctx *ctx, const uint64_t *in_dev, int64_t *out_dev, size_t n);
+int crdt_ordered_i64_to_u64(crdt_ctx *ctx, const int64_t *in_dev, uint64_t *out_dev, size_t n);
+
+/* ------------------------------------------------ synthetic state (bench/tests)
+ * SplitMix64-seeded generators; identical to the numpy
+ * restatement in crdt_amd/synth.py. */
+int crdt_synth_counters(crdt_ctx *ctx, uint64_t seed, uint32_t stream, uint64_t *out_dev,
+                        size_t n, uint64_t index_base);
+int crdt_synth_vclock_pairs(crdt_ctx *ctx, uint64_t seed, uint64_t *a_dev, uint64_t *b_dev,
+                            size_t pairs, size_t nodes, uint64_t pair_base);
+int crdt_synth_set_tuples(crdt_ctx *ctx, uint64_t seed, uint32_t side, const crdt_tuples *out,
+                          size_t n, uint64_t key_space);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRDT_AMD_H */

@@ -1,0 +1,112 @@
+"""GPU parity: G-Counter / PN-Counter / vector-clock join kernels vs the oracle.
+
+Bit-exact (integer) comparisons through the C-ABI.  Reference parity is
+unpinned for these build-defined types; the oracle
+restatement is pinned by tests/golden/counters_kat.json.
+"""
+import numpy as np
+import pytest
+import torch
+
+from crdt_amd import synth
+from crdt_amd.engine import as_u64, u64_tensor
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+EDGE = np.array([0, 1, 2**63 - 1, 2**63, 2**64 - 2, 2**64 - 1], dtype=np.uint64)
+
+
+def _edge_pairs(nodes):
+    a = np.repeat(EDGE, len(EDGE))
+    b = np.tile(EDGE, len(EDGE))
+    n = (len(a) + nodes - 1) // nodes * nodes
+    a = np.resize(a, n).reshape(-1, nodes)
+    b = np.resize(b, n).reshape(-1, nodes)
+    return a, b
+
+
+@pytest.mark.parametrize("rows,nodes", [(1, 64), (3, 64), (1000, 64), (777, 63), (5, 1), (100, 128), (33, 7)])
+def test_join_matches_oracle(eng, rows, nodes):
+    a = synth.counters(1, 1, rows * nodes).reshape(rows, nodes)
+    b = synth.counters(1, 2, rows * nodes).reshape(rows, nodes)
+    out = eng.gcounter_join(u64_tensor(a, eng.device), u64_tensor(b, eng.device))
+    np.testing.assert_array_equal(as_u64(out), oracle.gcounter_join(a, b))
+
+
+def test_join_edge_values_unsigned(eng):
+    a, b = _edge_pairs(64)
+    out = as_u64(eng.gcounter_join(u64_tensor(a, eng.device), u64_tensor(b, eng.device)))
+    np.testing.assert_array_equal(out, np.maximum(a, b))
+
+
+def test_join_in_place_alias(eng):
+    a = synth.counters(3, 1, 4096 * 64).reshape(4096, 64)
+    b = synth.counters(3, 2, 4096 * 64).reshape(4096, 64)
+    ta = u64_tensor(a, eng.device)
+    eng.gcounter_join(ta, u64_tensor(b, eng.device), out=ta)
+    np.testing.assert_array_equal(as_u64(ta), oracle.gcounter_join(a, b))
+
+
+def test_join_full_config_b(eng):
+    """configs[1] at full size: 1M replicas x 64 nodes, device-generated."""
+    rows, nodes = 1_000_000, 64
+    ta = eng.synth_counters(7, 1, rows, nodes)
+    tb = eng.synth_counters(7, 2, rows, nodes)
+    out = eng.gcounter_join(ta, tb)
+    a, b, o = as_u64(ta), as_u64(tb), as_u64(out)
+    # device generator == host generator on a head and a tail window
+    flat = a.reshape(-1)
+    np.testing.assert_array_equal(flat[:64000], synth.counters(7, 1, 64000))
+    np.testing.assert_array_equal(flat[-64000:], synth.counters(7, 1, 64000, rows * nodes - 64000))
+    np.testing.assert_array_equal(o, oracle.gcounter_join(a, b, threads=8))
+    # idempotent / commutative
+    np.testing.assert_array_equal(as_u64(eng.gcounter_join(out, out)), o)
+    np.testing.assert_array_equal(as_u64(eng.gcounter_join(tb, ta)), o)
+
+
+def test_device_generator_matches_host(eng):
+    n = 64 * 5000
+    dev = as_u64(eng.synth_counters(11, 3, 5000, 64)).reshape(-1)
+    np.testing.assert_array_equal(dev, synth.counters(11, 3, n))
+    base = 123457
+    dev2 = as_u64(eng.synth_counters(11, 3, 10, 64, row_base=base)).reshape(-1)
+    np.testing.assert_array_equal(dev2, synth.counters(11, 3, 640, base * 64))
+
+
+@pytest.mark.parametrize("rows,nodes", [(1, 64), (1000, 64), (100_003, 64), (999, 63), (10, 1024), (4, 3), (257, 128)])
+def test_fold_matches_oracle(eng, rows, nodes):
+    a = synth.counters(5, 4, rows * nodes).reshape(rows, nodes)
+    out = eng.gcounter_fold(u64_tensor(a, eng.device))
+    np.testing.assert_array_equal(as_u64(out), oracle.gcounter_fold(a))
+
+
+def test_fold_empty_rows_is_identity(eng):
+    a = torch.empty(0, 64, dtype=torch.int64, device=eng.device)
+    out = eng.gcounter_fold(a)
+    assert (as_u64(out) == 0).all()
+
+
+@pytest.mark.parametrize("rows,nodes", [(1, 64), (5000, 64), (333, 128), (77, 32), (50, 16), (40, 5), (9, 200)])
+def test_pncounter_value_and_join(eng, rows, nodes):
+    p = synth.counters(9, 1, rows * nodes).reshape(rows, nodes)
+    n = synth.counters(9, 2, rows * nodes).reshape(rows, nodes)
+    tp, tn = u64_tensor(p, eng.device), u64_tensor(n, eng.device)
+    v = eng.pncounter_value(tp, tn)
+    np.testing.assert_array_equal(v.cpu().numpy(), oracle.pncounter_value(p, n))
+    g = eng.gcounter_value(tp)
+    np.testing.assert_array_equal(as_u64(g), oracle.pncounter_value(p, np.zeros_like(p)).view(np.uint64))
+    p2 = synth.counters(9, 3, rows * nodes).reshape(rows, nodes)
+    n2 = synth.counters(9, 4, rows * nodes).reshape(rows, nodes)
+    po, no = eng.pncounter_join(tp, tn, u64_tensor(p2, eng.device), u64_tensor(n2, eng.device))
+    np.testing.assert_array_equal(as_u64(po), oracle.gcounter_join(p, p2))
+    np.testing.assert_array_equal(as_u64(no), oracle.gcounter_join(n, n2))
+
+
+def test_ordered_i64_roundtrip(eng):
+    x = np.concatenate([EDGE, synth.counters(2, 2, 1000)])
+    t = u64_tensor(x, eng.device)
+    o = eng.u64_to_ordered_i64(t)
+    # signed order of the mapped values == unsigned order of the originals
+    assert (np.argsort(o.cpu().numpy(), kind="stable") == np.argsort(x, kind="stable")).all()
+    np.testing.assert_array_equal(as_u64(eng.ordered_i64_to_u64(o)), x)

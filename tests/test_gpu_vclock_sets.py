@@ -1,0 +1,126 @@
+"""GPU parity: vector-clock classification and LWW / OR-Set merges vs the oracle.
+
+Build-defined types (no reference code): bit-exact against
+oracle/crdt_oracle.c, whose semantics are pinned by tests/golden KATs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from crdt_amd import synth
+from crdt_amd.engine import TupleSet, as_u64, u64_tensor
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("pairs,nodes", [(1, 128), (7, 128), (20_000, 128), (5000, 64), (3000, 32),
+                                         (1000, 100), (100, 1), (50, 3), (10, 513)])
+def test_vclock_matches_oracle(eng, pairs, nodes):
+    a, b = synth.vclock_pairs(21, pairs, nodes)
+    cls = eng.vclock_classify(u64_tensor(a, eng.device), u64_tensor(b, eng.device))
+    exp = oracle.vclock_classify(a, b)
+    np.testing.assert_array_equal(cls.cpu().numpy(), exp)
+    # antisymmetry: classify(b, a) swaps BEFORE/AFTER
+    rev = eng.vclock_classify(u64_tensor(b, eng.device), u64_tensor(a, eng.device)).cpu().numpy()
+    np.testing.assert_array_equal(rev, np.array([0, 2, 1, 3], np.uint8)[exp])
+
+
+def test_vclock_full_config_c_sample(eng):
+    """configs[2]-shaped (128 nodes) at 2M pairs (16 MB per 1k... 4 GB total)."""
+    pairs, nodes = 2_000_000, 128
+    ta, tb = eng.synth_vclock_pairs(99, pairs, nodes)
+    cls = eng.vclock_classify(ta, tb).cpu().numpy()
+    a, b = as_u64(ta), as_u64(tb)
+    np.testing.assert_array_equal(cls, oracle.vclock_classify(a, b, threads=8))
+    ha, hb = synth.vclock_pairs(99, 1000, nodes, pair_base=pairs - 1000)
+    np.testing.assert_array_equal(a[-1000:], ha)
+    np.testing.assert_array_equal(b[-1000:], hb)
+    frac = np.bincount(cls, minlength=4) / pairs
+    assert np.all(np.abs(frac - 0.25) < 0.01), frac
+
+
+def test_vclock_edges(eng):
+    M = 2**64 - 1
+    rows = [
+        ([0, 0], [0, 0], 0), ([M, 0], [M, 0], 0), ([0, M], [1, M], 1), ([M, 1], [M - 1, 1], 2),
+        ([2**63, 0], [2**63 - 1, 1], 3), ([2**63, 5], [2**63, 5], 0),
+    ]
+    a = np.array([r[0] for r in rows], dtype=np.uint64)
+    b = np.array([r[1] for r in rows], dtype=np.uint64)
+    cls = eng.vclock_classify(u64_tensor(a, eng.device), u64_tensor(b, eng.device)).cpu().numpy()
+    np.testing.assert_array_equal(cls, [r[2] for r in rows])
+
+
+def _sets(seed, na, nb, key_space):
+    sa = synth.sort_tuples_np(*synth.set_tuples(seed, 0, na, key_space))
+    sb = synth.sort_tuples_np(*synth.set_tuples(seed, 1, nb, key_space))
+    return sa, sb
+
+
+def _check(eng, sa, sb):
+    A = TupleSet.from_numpy(*sa, eng.device)
+    B = TupleSet.from_numpy(*sb, eng.device)
+    for fn, ref in ((eng.lww_merge, oracle.lww_merge), (eng.orset_merge, oracle.orset_merge)):
+        got = fn(A, B).to_numpy()
+        exp = ref(sa, sb)
+        for g, e, f in zip(got, exp, ("key", "ts", "rep", "tomb")):
+            np.testing.assert_array_equal(g, e, err_msg=f"{fn.__name__}.{f}")
+
+
+@pytest.mark.parametrize("na,nb,key_space", [
+    (1, 1, 1), (0, 10, 5), (10, 0, 5), (2048, 2048, 100), (2047, 2049, 10), (5000, 3, 1000),
+    (100_000, 100_000, 1), (100_000, 100_000, 7), (100_000, 100_000, 50_000), (300_000, 200_000, 10**9),
+])
+def test_sets_match_oracle(eng, na, nb, key_space):
+    _check(eng, *_sets(31 + na + nb, na, nb, key_space))
+
+
+def test_sets_identical_inputs_idempotent(eng):
+    sa, _ = _sets(5, 50_000, 1, 20_000)
+    _check(eng, sa, sa)
+    A = TupleSet.from_numpy(*sa, eng.device)
+    got = eng.orset_merge(A, A).to_numpy()
+    dedup = oracle.orset_merge(sa, (sa[0][:0], sa[1][:0], sa[2][:0], sa[3][:0]))
+    for g, e in zip(got, dedup):
+        np.testing.assert_array_equal(g, e)
+
+
+def test_sets_long_runs_cross_tiles(eng):
+    # one key with 20k versions on each side: key runs and equal-tag runs cross many tiles
+    n = 20_000
+    ka = np.zeros(n, np.uint64)
+    ta = np.repeat(np.arange(n // 4, dtype=np.uint64), 4)
+    ra = np.tile(np.array([0, 0, 1, 1], np.uint32), n // 4)
+    tomba = (np.arange(n) % 3 == 0).astype(np.uint8)
+    sa = (ka, ta, ra, tomba)
+    sb = (ka.copy(), ta.copy(), ra.copy(), (np.arange(n) % 5 == 0).astype(np.uint8))
+    _check(eng, sa, sb)
+
+
+def test_sets_uint64_extremes(eng):
+    key = np.array([0, 5, 2**63, 2**64 - 1], np.uint64)
+    ts = np.array([2**64 - 1, 0, 2**63, 1], np.uint64)
+    rep = np.array([0, 2**32 - 1, 7, 7], np.uint32)
+    tomb = np.array([0, 1, 0, 1], np.uint8)
+    sa = (key, ts, rep, tomb)
+    sb = (key.copy(), ts.copy(), rep.copy(), 1 - tomb)
+    _check(eng, sa, sb)
+
+
+def test_sets_full_config_d(eng):
+    """configs[3] at full size: 10M tuples per side, device generated + sorted."""
+    n, ks = 10_000_000, 8_000_000
+    A = eng.synth_set_tuples(2024, 0, n, ks)
+    B = eng.synth_set_tuples(2024, 1, n, ks)
+    assert eng.count_unsorted(A) == 0 and eng.count_unsorted(B) == 0
+    sa, sb = A.to_numpy(), B.to_numpy()
+    ha = synth.sort_tuples_np(*synth.set_tuples(2024, 0, n, ks))
+    for g, e in zip(sa, ha):
+        np.testing.assert_array_equal(g, e)
+    for fn, ref in ((eng.lww_merge, oracle.lww_merge), (eng.orset_merge, oracle.orset_merge)):
+        got = fn(A, B).to_numpy()
+        exp = ref(sa, sb)
+        for g, e in zip(got, exp):
+            np.testing.assert_array_equal(g, e)
+    torch.cuda.synchronize()
