@@ -85,6 +85,8 @@ SIGNATURES = {
     "crdt_ctx_create": (_I, [_I, _P, C.POINTER(_P)]),
     "crdt_ctx_destroy": (_I, [_CTX]),
     "crdt_ctx_set_stream": (_I, [_CTX, _P]),
+    "crdt_stream_create": (_I, [_I, C.POINTER(_P)]),
+    "crdt_stream_destroy": (_I, [_P]),
     "crdt_ctx_sync": (_I, [_CTX]),
     "crdt_ctx_last_hip_error": (_I, [_CTX]),
     "crdt_ctx_reserve": (_I, [_CTX, _SZ]),

@@ -75,15 +75,36 @@ extern "C" int crdt_ctx_create(int device, void *stream, crdt_ctx **out) {
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != device) (void)hipSetDevice(device);
-    if (stream) {
-        ctx->stream = (hipStream_t)stream;
-    } else {
-        hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-        if (e != hipSuccess) { int rc = hip_fail(ctx, e); delete ctx; return rc; }
-        ctx->own_stream = true;
-    }
+    // NULL is the device's default (null) stream -- what torch's default
+    // current stream reports as cuda_stream == 0 -- never a private stream:
+    // work must stay ordered with the caller's copies on that stream.
+    ctx->stream = (hipStream_t)stream;
     *out = ctx;
     return CRDT_OK;
+}
+
+extern "C" int crdt_stream_create(int device, void **stream) {
+    if (!stream) return CRDT_E_INVAL;
+    *stream = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CRDT_E_NODEV;
+    if (device < 0 || device >= n) return CRDT_E_INVAL;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (cur != device && cur >= 0) (void)hipSetDevice(cur);
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? CRDT_E_NOMEM : CRDT_E_HIP;
+    *stream = (void *)s;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_stream_destroy(void *stream) {
+    if (!stream) return CRDT_OK;
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamDestroy((hipStream_t)stream);
+    return e == hipSuccess ? CRDT_OK : CRDT_E_HIP;
 }
 
 extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
@@ -98,7 +119,6 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
 
 extern "C" int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream) {
     if (!ctx) return CRDT_E_INVAL;
-    if (!stream) return CRDT_E_INVAL;
     if (ctx->own_stream) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamDestroy(ctx->stream);

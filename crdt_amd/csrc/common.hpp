@@ -28,9 +28,9 @@ inline int hip_fail(crdt_ctx *ctx, hipError_t e) {
 
 // Process-wide kernel tuning knobs (crdt_set_option); defined in capi.hip.
 struct JoinTuning {
-    int unroll = 4;         // 16-B vectors in flight per lane per operand
+    int unroll = 1;         // 16-B vectors in flight per lane per operand (tuned: tools/tune_join.py)
     int nontemporal = 1;    // nt loads/stores for once-touched streams
-    int blocks_per_cu = 8;  // grid = CUs * blocks_per_cu (grid-stride beyond)
+    int blocks_per_cu = 2;  // grid = CUs * blocks_per_cu (grid-stride beyond); ~16 KiB in flight per CU
 };
 extern JoinTuning g_join;
 extern int g_vclock_pairs_per_wave;

@@ -49,11 +49,16 @@ const char *crdt_status_str(int status);
 int         crdt_device_count(int *count);
 
 /* ---------------------------------------------------------------- context */
-/* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or
- * NULL for a library-owned non-blocking stream. */
+/* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream), or
+ * NULL for the device's default (null) stream.  The context never creates a
+ * stream of its own: its work is ordered with the caller's copies. */
 int crdt_ctx_create(int device, void *stream, crdt_ctx **out);
 int crdt_ctx_destroy(crdt_ctx *ctx);
 int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream);
+/* A non-blocking stream for hosts that want one (e.g. to overlap merges with
+ * copies); pass it to crdt_ctx_create / crdt_ctx_set_stream. */
+int crdt_stream_create(int device, void **stream);
+int crdt_stream_destroy(void *stream);
 int crdt_ctx_sync(crdt_ctx *ctx);
 int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 /* Pre-size the context's device workspace so that later calls never
