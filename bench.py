@@ -262,12 +262,10 @@ class ShardFold(Workload):
         return self.rows * self.nodes * 8
 
     def step(self):
+        from crdt_amd import shard
         self.eng.gcounter_fold(self.a, out=self.fold)
         if self.world > 1:
-            import torch.distributed as dist
-            self.eng.u64_to_ordered_i64(self.fold, out=self.ordered)
-            dist.all_reduce(self.ordered, op=dist.ReduceOp.MAX)
-            self.eng.ordered_i64_to_u64(self.ordered, out=self.fold)
+            shard.allreduce_max_u64(self.fold, self.eng)     # RCCL all-reduce(max), 512 B
 
     def cpu_baseline(self, seconds, threads):
         return None

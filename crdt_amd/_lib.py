@@ -110,6 +110,20 @@ SIGNATURES = {
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),
     "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
+    "crdt_server_new": (_I, [_CTX, _I, C.POINTER(_P)]),
+    "crdt_server_free": (_I, [_P]),
+    "crdt_server_init_state": (_I, [_P, _P, _P, _P, _P, _SZ]),
+    "crdt_server_diff_put": (_I, [_P, C.c_int64, _I, _P, _P, _P, _P, _SZ]),
+    "crdt_server_remote_put": (_I, [_P, C.c_int64, _P, _P, _P, _P, _SZ]),
+    "crdt_server_add_command": (_I, [_P, C.c_int64, _P, _P, _P, _P, _SZ, C.POINTER(_I)]),
+    "crdt_server_merge": (_I, [_P]),
+    "crdt_servers_merge": (_I, [C.POINTER(_P), _SZ]),
+    "crdt_server_diff_len": (_I, [_P, C.POINTER(_SZ)]),
+    "crdt_server_remote_len": (_I, [_P, C.POINTER(_SZ)]),
+    "crdt_server_diff_keys": (_I, [_P, _P, _P, _SZ, C.POINTER(_SZ)]),
+    "crdt_server_state_len": (_I, [_P, C.POINTER(_SZ)]),
+    "crdt_server_state_at": (_I, [_P, _SZ, C.POINTER(C.c_void_p), C.POINTER(_SZ), C.POINTER(C.c_void_p),
+                                  C.POINTER(_SZ)]),
     "crdt_shard_range": (_I, [_U64, _I, _I, C.POINTER(_U64), C.POINTER(_U64)]),
     "crdt_u64_to_ordered_i64": (_I, [_CTX, _P, _P, _SZ]),
     "crdt_ordered_i64_to_u64": (_I, [_CTX, _P, _P, _SZ]),

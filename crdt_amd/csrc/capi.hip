@@ -112,6 +112,7 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
     (void)bind(ctx);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->io) (void)hipFree(ctx->io);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return CRDT_OK;

@@ -15,6 +15,8 @@ struct crdt_ctx {
     int last_hip_error = 0;
     void *ws = nullptr;      // device workspace, grown on demand (crdt_ctx_reserve)
     size_t ws_bytes = 0;
+    void *io = nullptr;      // device staging for host-facing calls (crdt_server_*)
+    size_t io_bytes = 0;
 };
 
 namespace crdt {

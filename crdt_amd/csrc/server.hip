@@ -1,0 +1,437 @@
+// server.hip -- C++ host mirror of the reference's Server (main.go:23-113),
+// with merge() routed to the batched gfx950 RefMerge (refmerge.hip).
+//
+// The reference's Go API surface this replaces:
+//   type Server struct { InitialState, CurrentState Data; Diff, RemoteDiff
+//                        treemap.Map; Port int; LastReceived int64;
+//                        FriendList []string; Alive bool; Lock sync.Mutex }
+//                                                            main.go:23-33
+//   func NewServer(port int, initialState Data, friendList []string) *Server
+//                                                            main.go:102-113
+//   func (server *Server) merge()                            main.go:35-100
+//   Diff.Put(time.Now().UnixMilli(), &data)   (local write)  main.go:187
+//   RemoteDiff.Put(int64(atoi), value)        (gossip ingest) main.go:255
+// The host keeps the treemaps (std::map under the signed int64 order of
+// utils.Int64Comparator, main.go:106); merge() packs every participating
+// server into one CSR batch, runs ONE device call, and rebuilds Diff and
+// CurrentState from the device result.  There is no CPU merge path.
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "common.hpp"
+
+namespace crdt {
+
+struct Value {                       // map[string]string or *Command
+    bool local = false;              // true: *Command (main.go:187), skipped by the replay
+    std::vector<std::pair<std::string, std::string>> kv;   // unique keys
+};
+
+struct Server {
+    crdt_ctx *ctx = nullptr;
+    std::map<std::string, std::string> InitialState;        // main.go:24
+    std::map<std::string, std::string> CurrentState;        // main.go:25 (aliases InitialState, :104-105)
+    std::map<int64_t, std::shared_ptr<const Value>> Diff;   // main.go:26
+    std::map<int64_t, std::shared_ptr<const Value>> RemoteDiff;  // main.go:27
+    int Port = 0;                                           // main.go:28
+    int64_t LastReceived = 0;                               // main.go:29 (unused by the reference)
+    std::vector<std::string> FriendList;                    // main.go:30
+    bool Alive = true;                                      // main.go:31
+    std::mutex Lock;                                        // main.go:32
+    std::vector<std::pair<std::string, std::string>> state_view;   // CurrentState snapshot for iteration
+};
+
+static int io_reserve(crdt_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->io_bytes) return CRDT_OK;
+    size_t want = (bytes + bytes / 4 + (1u << 20)) & ~(size_t)((1u << 20) - 1);
+    hipError_t e;
+    if (ctx->io) {
+        e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        (void)hipFree(ctx->io);
+        ctx->io = nullptr;
+        ctx->io_bytes = 0;
+    }
+    e = hipMalloc(&ctx->io, want);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    ctx->io_bytes = want;
+    return CRDT_OK;
+}
+
+// One host-side batch of replicas in the crdt_refmerge_in layout.
+struct Batch {
+    std::vector<uint64_t> l_off{0}, l_kv, r_off{0}, r_kv, str_off{0};
+    std::vector<int64_t> l_ts, r_ts;
+    std::vector<uint8_t> l_origin;
+    std::vector<uint32_t> kv_key, kv_val;
+    std::vector<uint32_t> slot_off{0};
+    std::vector<const std::string *> slot_name;
+    std::vector<std::shared_ptr<const Value>> l_val, r_val;
+    std::string blob;
+    std::unordered_map<std::string, uint32_t> sid;
+    std::vector<std::pair<uint32_t, uint32_t>> l_pairs, r_pairs;   // (slot, string) before arena layout
+    std::vector<uint64_t> l_cnt, r_cnt;
+
+    uint32_t str_id(const std::string &s) {
+        auto it = sid.find(s);
+        if (it != sid.end()) return it->second;
+        uint32_t id = (uint32_t)(str_off.size() - 1);
+        sid.emplace(s, id);
+        blob += s;
+        str_off.push_back(blob.size());
+        return id;
+    }
+
+    void add(Server &s) {
+        std::unordered_map<std::string, uint32_t> slots;
+        auto slot = [&](const std::string &k) {
+            auto it = slots.find(k);
+            if (it != slots.end()) return it->second;
+            uint32_t id = (uint32_t)slot_name.size();
+            slots.emplace(k, id);
+            slot_name.push_back(&k);
+            return id;
+        };
+        for (auto &e : s.Diff) {
+            l_ts.push_back(e.first);
+            l_origin.push_back(e.second->local ? 1 : 0);
+            l_val.push_back(e.second);
+            l_cnt.push_back(e.second->kv.size());
+            for (auto &kv : e.second->kv) l_pairs.emplace_back(slot(kv.first), str_id(kv.second));
+        }
+        for (auto &e : s.RemoteDiff) {
+            r_ts.push_back(e.first);
+            r_val.push_back(e.second);
+            r_cnt.push_back(e.second->kv.size());
+            for (auto &kv : e.second->kv) r_pairs.emplace_back(slot(kv.first), str_id(kv.second));
+        }
+        l_off.push_back(l_ts.size());
+        r_off.push_back(r_ts.size());
+        slot_off.push_back((uint32_t)slot_name.size());
+    }
+
+    void finish() {
+        // kv arena: every L entry's pairs, then every R entry's pairs
+        l_kv.reserve(l_cnt.size() + 1);
+        uint64_t q = 0;
+        for (auto c : l_cnt) { l_kv.push_back(q); q += c; }
+        l_kv.push_back(q);
+        for (auto c : r_cnt) { r_kv.push_back(q); q += c; }
+        r_kv.push_back(q);
+        kv_key.reserve(q);
+        kv_val.reserve(q);
+        for (auto &p : l_pairs) { kv_key.push_back(p.first); kv_val.push_back(p.second); }
+        for (auto &p : r_pairs) { kv_key.push_back(p.first); kv_val.push_back(p.second); }
+        if (blob.empty()) blob.push_back('\0');
+    }
+};
+
+template <class T> static size_t vbytes(const std::vector<T> &v) { return v.size() * sizeof(T); }
+
+// merge() for a set of servers whose locks the caller holds.
+static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
+    Batch b;
+    for (size_t i = 0; i < n; ++i) b.add(*srv[i]);
+    b.finish();
+    const uint64_t n_l = b.l_ts.size(), n_r = b.r_ts.size(), n_kv = b.kv_key.size();
+    const uint64_t n_str = b.str_off.size() - 1, n_slots = b.slot_name.size();
+    if (n_slots >= 0xFFFFFFFFull || n_str >= 0xFFFFFFFFull) return CRDT_E_RANGE;
+    const uint64_t n_out = n_l + n_r;
+
+    // device layout: inputs then outputs, 256-B aligned carve-outs
+    struct Piece { const void *src; size_t bytes; size_t off; };
+    std::vector<Piece> in = {
+        {b.l_off.data(), vbytes(b.l_off), 0}, {b.l_ts.data(), vbytes(b.l_ts), 0},
+        {b.l_origin.data(), vbytes(b.l_origin), 0}, {b.l_kv.data(), vbytes(b.l_kv), 0},
+        {b.r_off.data(), vbytes(b.r_off), 0}, {b.r_ts.data(), vbytes(b.r_ts), 0},
+        {b.r_kv.data(), vbytes(b.r_kv), 0}, {b.kv_key.data(), vbytes(b.kv_key), 0},
+        {b.kv_val.data(), vbytes(b.kv_val), 0}, {b.blob.data(), b.blob.size(), 0},
+        {b.str_off.data(), vbytes(b.str_off), 0},
+    };
+    size_t off = 0;
+    for (auto &p : in) { p.off = off; off += Carve::round(p.bytes ? p.bytes : 1); }
+    const size_t o_off = off;            off += Carve::round((n + 1) * 8);
+    const size_t o_ts = off;             off += Carve::round(n_out * 8 + 8);
+    const size_t o_origin = off;         off += Carve::round(n_out + 1);
+    const size_t o_src = off;            off += Carve::round(n_out * 8 + 8);
+    const size_t o_kind = off;           off += Carve::round(n_slots + 1);
+    const size_t o_str = off;            off += Carve::round(n_slots * 4 + 4);
+    const size_t o_sum = off;            off += Carve::round(n_slots * 8 + 8);
+    int rc = io_reserve(ctx, off);
+    if (rc) return rc;
+    char *d = (char *)ctx->io;
+    for (auto &p : in)
+        if (p.bytes) {
+            hipError_t e = hipMemcpyAsync(d + p.off, p.src, p.bytes, hipMemcpyHostToDevice, ctx->stream);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+        }
+    crdt_refmerge_in ri;
+    ri.replicas = (uint32_t)n;
+    ri.n_slots = (uint32_t)n_slots;
+    ri.n_l = n_l; ri.n_r = n_r; ri.n_kv = n_kv; ri.n_str = n_str;
+    ri.l_off = (const uint64_t *)(d + in[0].off);
+    ri.l_ts = (const int64_t *)(d + in[1].off);
+    ri.l_origin = (const uint8_t *)(d + in[2].off);
+    ri.l_kv = (const uint64_t *)(d + in[3].off);
+    ri.r_off = (const uint64_t *)(d + in[4].off);
+    ri.r_ts = (const int64_t *)(d + in[5].off);
+    ri.r_kv = (const uint64_t *)(d + in[6].off);
+    ri.kv_key = (const uint32_t *)(d + in[7].off);
+    ri.kv_val = (const uint32_t *)(d + in[8].off);
+    ri.str_bytes = (const uint8_t *)(d + in[9].off);
+    ri.str_off = (const uint64_t *)(d + in[10].off);
+    crdt_refmerge_out ro;
+    ro.off = (uint64_t *)(d + o_off);
+    ro.ts = (int64_t *)(d + o_ts);
+    ro.origin = (uint8_t *)(d + o_origin);
+    ro.src = (int64_t *)(d + o_src);
+    ro.st_kind = (uint8_t *)(d + o_kind);
+    ro.st_str = (uint32_t *)(d + o_str);
+    ro.st_sum = (int64_t *)(d + o_sum);
+    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    if (rc) return rc;
+
+    std::vector<uint64_t> h_off(n + 1);
+    std::vector<int64_t> h_ts(n_out), h_src(n_out);
+    std::vector<uint8_t> h_kind(n_slots);
+    std::vector<uint32_t> h_str(n_slots);
+    std::vector<int64_t> h_sum(n_slots);
+    struct Back { void *dst; size_t src; size_t bytes; };
+    const Back back[] = {{h_off.data(), o_off, vbytes(h_off)}, {h_ts.data(), o_ts, vbytes(h_ts)},
+                         {h_src.data(), o_src, vbytes(h_src)}, {h_kind.data(), o_kind, vbytes(h_kind)},
+                         {h_str.data(), o_str, vbytes(h_str)}, {h_sum.data(), o_sum, vbytes(h_sum)}};
+    for (auto &x : back)
+        if (x.bytes) {
+            hipError_t e = hipMemcpyAsync(x.dst, d + x.src, x.bytes, hipMemcpyDeviceToHost, ctx->stream);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+        }
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+
+    for (size_t p = 0; p < n; ++p) {
+        Server &s = *srv[p];
+        std::map<int64_t, std::shared_ptr<const Value>> nd;
+        for (uint64_t o = h_off[p]; o < h_off[p + 1]; ++o) {
+            const int64_t src = h_src[o];
+            nd.emplace_hint(nd.end(), h_ts[o], src >= 0 ? b.l_val[(size_t)src] : b.r_val[(size_t)(-src - 1)]);
+        }
+        std::map<std::string, std::string> st;                 // main.go:76: rebuilt from empty
+        for (uint32_t sl = b.slot_off[p]; sl < b.slot_off[p + 1]; ++sl) {
+            if (h_kind[sl] == 1) {
+                const uint32_t id = h_str[sl];
+                st.emplace(*b.slot_name[sl], b.blob.substr(b.str_off[id], b.str_off[id + 1] - b.str_off[id]));
+            } else if (h_kind[sl] == 2) {
+                st.emplace(*b.slot_name[sl], std::to_string((long long)h_sum[sl]));   // strconv.Itoa
+            }
+        }
+        s.Diff.swap(nd);
+        s.RemoteDiff.clear();                                    // main.go:75
+        s.CurrentState.swap(st);
+        s.state_view.clear();
+        s.Alive = true;                                          // main.go:99
+    }
+    return CRDT_OK;
+}
+
+static std::shared_ptr<const Value> make_value(bool local, const char *const *keys, const size_t *klen,
+                                               const char *const *vals, const size_t *vlen, size_t n) {
+    auto v = std::make_shared<Value>();
+    v->local = local;
+    std::map<std::string, std::string> m;                       // map semantics: a repeated key overwrites
+    for (size_t i = 0; i < n; ++i) m[std::string(keys[i], klen[i])] = std::string(vals[i], vlen[i]);
+    v->kv.assign(m.begin(), m.end());
+    return v;
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+struct crdt_server { Server s; };
+
+extern "C" int crdt_server_new(crdt_ctx *ctx, int port, crdt_server **out) {
+    if (!ctx || !out) return CRDT_E_INVAL;
+    crdt_server *p = new (std::nothrow) crdt_server();
+    if (!p) return CRDT_E_NOMEM;
+    p->s.ctx = ctx;
+    p->s.Port = port;
+    *out = p;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_server_free(crdt_server *srv) {
+    delete srv;
+    return CRDT_OK;
+}
+
+static bool kv_args_ok(const char *const *keys, const size_t *klen, const char *const *vals, const size_t *vlen,
+                       size_t n) {
+    if (n == 0) return true;
+    if (!keys || !klen || !vals || !vlen) return false;
+    for (size_t i = 0; i < n; ++i)
+        if ((!keys[i] && klen[i]) || (!vals[i] && vlen[i])) return false;
+    return true;
+}
+
+extern "C" int crdt_server_diff_put(crdt_server *srv, int64_t ts, int local, const char *const *keys,
+                                    const size_t *klen, const char *const *vals, const size_t *vlen, size_t n) {
+    if (!srv || !kv_args_ok(keys, klen, vals, vlen, n)) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    srv->s.Diff[ts] = make_value(local != 0, keys, klen, vals, vlen, n);   // treemap Put replaces
+    return CRDT_OK;
+}
+
+extern "C" int crdt_server_remote_put(crdt_server *srv, int64_t ts, const char *const *keys, const size_t *klen,
+                                      const char *const *vals, const size_t *vlen, size_t n) {
+    if (!srv || !kv_args_ok(keys, klen, vals, vlen, n)) return CRDT_E_INVAL;
+    // main.go:255 writes RemoteDiff from the gossip goroutine without the lock;
+    // here the lock is taken so concurrent callers stay safe.
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    srv->s.RemoteDiff[ts] = make_value(false, keys, klen, vals, vlen, n);
+    return CRDT_OK;
+}
+
+extern "C" int crdt_servers_merge(crdt_server *const *srvs, size_t n) {
+    if (n == 0) return CRDT_OK;
+    if (!srvs) return CRDT_E_INVAL;
+    std::vector<Server *> v;
+    v.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (!srvs[i]) return CRDT_E_INVAL;
+        v.push_back(&srvs[i]->s);
+    }
+    std::vector<Server *> order(v);
+    std::sort(order.begin(), order.end());
+    if (std::adjacent_find(order.begin(), order.end()) != order.end()) return CRDT_E_INVAL;   // duplicates
+    crdt_ctx *ctx = v[0]->ctx;
+    for (auto *s : v)
+        if (s->ctx->device != ctx->device) return CRDT_E_INVAL;
+    int rc = bind(ctx);
+    if (rc) return rc;
+    for (auto *s : v) s->Alive = false;                         // main.go:41
+    for (auto *s : order) s->Lock.lock();                       // main.go:43 (address order: no deadlock)
+    rc = merge_locked(ctx, v.data(), v.size());
+    for (auto *s : v) s->Alive = true;
+    for (auto it = order.rbegin(); it != order.rend(); ++it) (*it)->Lock.unlock();
+    return rc;
+}
+
+extern "C" int crdt_server_merge(crdt_server *srv) {
+    if (!srv) return CRDT_E_INVAL;
+    return crdt_servers_merge(&srv, 1);
+}
+
+// NewServer's initialState (main.go:102-105): CurrentState starts as it.
+extern "C" int crdt_server_init_state(crdt_server *srv, const char *const *keys, const size_t *klen,
+                                      const char *const *vals, const size_t *vlen, size_t n) {
+    if (!srv || !kv_args_ok(keys, klen, vals, vlen, n)) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    srv->s.InitialState.clear();
+    for (size_t i = 0; i < n; ++i) srv->s.InitialState[std::string(keys[i], klen[i])] = std::string(vals[i], vlen[i]);
+    srv->s.CurrentState = srv->s.InitialState;
+    srv->s.state_view.clear();
+    return CRDT_OK;
+}
+
+// AddCommand (main.go:173-215) after the JSON decode: Diff.Put(ts, &data)
+// (main.go:187), then the local apply (main.go:188-207) in key order (Go's
+// map order is random; key order is one of its legal executions): a key not
+// yet in CurrentState is set verbatim and the handler RETURNS (main.go:189-193);
+// otherwise Atoi both sides (500 on error, main.go:195-204) and store
+// Itoa(sum) (main.go:205-206).  *http_status = 200 / 500 / 502 (dead replica).
+extern "C" int crdt_server_add_command(crdt_server *srv, int64_t ts_ms, const char *const *keys, const size_t *klen,
+                                       const char *const *vals, const size_t *vlen, size_t n, int *http_status) {
+    if (!srv || !http_status || !kv_args_ok(keys, klen, vals, vlen, n)) return CRDT_E_INVAL;
+    Server &s = srv->s;
+    std::lock_guard<std::mutex> g(s.Lock);
+    if (!s.Alive) { *http_status = 502; return CRDT_OK; }
+    auto v = make_value(true, keys, klen, vals, vlen, n);
+    s.Diff[ts_ms] = v;                                     // same-ms writes overwrite
+    s.state_view.clear();
+    *http_status = 200;
+    for (auto &kv : v->kv) {
+        auto it = s.CurrentState.find(kv.first);
+        if (it == s.CurrentState.end()) {
+            s.CurrentState.emplace(kv.first, kv.second);
+            return CRDT_OK;                                 // "Inserted", early return (main.go:192-193)
+        }
+        long long curr, change;
+        auto atoi = [](const std::string &x, long long *out) {
+            if (x.empty()) return false;
+            size_t i = 0;
+            bool neg = false;
+            if (x[0] == '+' || x[0] == '-') { neg = x[0] == '-'; i = 1; if (x.size() == 1) return false; }
+            unsigned long long acc = 0;
+            for (; i < x.size(); ++i) {
+                unsigned d = (unsigned char)x[i] - (unsigned)'0';
+                if (d > 9 || acc > (0xFFFFFFFFFFFFFFFFULL - d) / 10) return false;
+                acc = acc * 10 + d;
+            }
+            if ((!neg && acc >= 0x8000000000000000ULL) || (neg && acc > 0x8000000000000000ULL)) return false;
+            *out = neg ? (long long)(0 - acc) : (long long)acc;
+            return true;
+        };
+        if (!atoi(it->second, &curr) || !atoi(kv.second, &change)) { *http_status = 500; return CRDT_OK; }
+        it->second = std::to_string((long long)((unsigned long long)curr + (unsigned long long)change));
+    }
+    return CRDT_OK;
+}
+
+extern "C" int crdt_server_diff_len(crdt_server *srv, size_t *n) {
+    if (!srv || !n) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    *n = srv->s.Diff.size();
+    return CRDT_OK;
+}
+
+extern "C" int crdt_server_remote_len(crdt_server *srv, size_t *n) {
+    if (!srv || !n) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    *n = srv->s.RemoteDiff.size();
+    return CRDT_OK;
+}
+
+// Ascending Diff keys (Diff.Keys(), main.go:45) with their origin; either
+// output may be NULL.  Writes min(cap, len) entries.
+extern "C" int crdt_server_diff_keys(crdt_server *srv, int64_t *ts, uint8_t *local, size_t cap, size_t *n) {
+    if (!srv || !n) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    size_t i = 0;
+    for (auto &e : srv->s.Diff) {
+        if (i >= cap) break;
+        if (ts) ts[i] = e.first;
+        if (local) local[i] = e.second->local ? 1 : 0;
+        ++i;
+    }
+    *n = srv->s.Diff.size();
+    return CRDT_OK;
+}
+
+extern "C" int crdt_server_state_len(crdt_server *srv, size_t *n) {
+    if (!srv || !n) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    *n = srv->s.CurrentState.size();
+    return CRDT_OK;
+}
+
+// i-th CurrentState entry in key order.  The returned pointers stay valid
+// until the next mutation of this server.
+extern "C" int crdt_server_state_at(crdt_server *srv, size_t i, const char **key, size_t *klen, const char **val,
+                                    size_t *vlen) {
+    if (!srv || !key || !klen || !val || !vlen) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    Server &s = srv->s;
+    if (s.state_view.size() != s.CurrentState.size()) s.state_view.assign(s.CurrentState.begin(), s.CurrentState.end());
+    if (i >= s.state_view.size()) return CRDT_E_INVAL;
+    *key = s.state_view[i].first.data();
+    *klen = s.state_view[i].first.size();
+    *val = s.state_view[i].second.data();
+    *vlen = s.state_view[i].second.size();
+    return CRDT_OK;
+}

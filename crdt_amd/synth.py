@@ -89,6 +89,58 @@ def set_tuples(seed: int, side: int, n: int, key_space: int):
     return key.astype(np.uint64), ts.astype(np.uint64), rep.astype(np.uint32), tomb
 
 
+ALPHABET = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ1234567890"   # main.go:274
+_ODD_VALUES = ["+5", "007", "-0", "x", "", "9223372036854775807", "-9223372036854775808",
+               "9223372036854775808", "1_0", " 3", "00000000000000000000042", "+", "--1"]
+
+
+def refmerge_demo(seed: int, replicas: int = 5, entries: int = 10_000, multi_key: float = 0.0):
+    """Config A (BASELINE configs[0]): the reference demo's workload shape.
+
+    Per replica: a local Diff of `entries` ts with gaps U[1,4] (UnixMilli-like
+    start), half local writes (*Command, main.go:187) and half previously
+    merged remote maps; a RemoteDiff from a peer with ~5% ts collisions with
+    the local log and ~10% of its ts above max(L).  Each entry holds one key
+    of the 62-char alphabet (main.go:274) with a value in [-20, -11]
+    (main.go:282), ~1% non-canonical / unparsable strings, and a
+    `multi_key` fraction of entries hold 2-4 keys.
+    Returns [(diff, remote), ...] with crdt_amd.refmerge.Command marking
+    local writes.
+    """
+    from .refmerge import Command
+    out = []
+    for p in range(replicas):
+        rng = np.random.default_rng([seed, p])
+
+        def kv():
+            nk = int(rng.integers(2, 5)) if rng.random() < multi_key else 1
+            d = {}
+            for _ in range(nk):
+                k = ALPHABET[int(rng.integers(0, len(ALPHABET)))]
+                if rng.random() < 0.01:
+                    d[k] = _ODD_VALUES[int(rng.integers(0, len(_ODD_VALUES)))]
+                else:
+                    d[k] = str(int(rng.integers(0, 10)) + 2 * (-10))
+            return d
+
+        t0 = 1_700_000_000_000 + int(rng.integers(0, 1000))
+        lts = t0 + np.cumsum(rng.integers(1, 5, size=entries))
+        diff = {}
+        for t in lts.tolist():
+            diff[t] = Command(kv()) if rng.random() < 0.5 else kv()
+        n_r = entries
+        hi = int(lts[-1]) if entries else t0
+        n_above = int(round(0.10 * n_r))
+        n_coll = int(round(0.05 * n_r))
+        rts = set((t0 + np.cumsum(rng.integers(1, 5, size=n_r - n_above - n_coll))).tolist())
+        if entries:
+            rts |= set(rng.choice(lts, size=min(n_coll, entries), replace=False).tolist())
+        rts |= set((hi + np.cumsum(rng.integers(1, 5, size=n_above))).tolist())
+        remote = {int(t): kv() for t in sorted(rts)}
+        out.append((diff, remote))
+    return out
+
+
 def sort_tuples_np(key, ts, rep, tomb):
     """Stable (key, ts, rep) sort of numpy SoA tuples."""
     order = np.lexsort((rep, ts, key))  # lexsort is stable; last key is primary

@@ -185,6 +185,45 @@ int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_re
 int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *str_bytes_dev, const uint64_t *str_off_dev,
                     uint64_t n_str, uint8_t *ok_dev, int64_t *val_dev);
 
+/* ------------------------------------------------ Server (a4): host mirror
+ * The reference's state holder (main.go:23-33) kept on the host, with
+ * merge() routed to crdt_refmerge_batch.  Key/value arguments are parallel
+ * arrays of (pointer, length) byte strings; a repeated key overwrites (Go
+ * map semantics).  All functions lock the server's mutex (main.go:32). */
+typedef struct crdt_server crdt_server;
+/* NewServer(port, initialState, friendList) (main.go:102-113). */
+int crdt_server_new(crdt_ctx *ctx, int port, crdt_server **out);
+int crdt_server_free(crdt_server *srv);
+int crdt_server_init_state(crdt_server *srv, const char *const *keys, const size_t *key_lens,
+                           const char *const *vals, const size_t *val_lens, size_t n);
+/* Diff.Put(ts, value): local != 0 stores a *Command (main.go:187), else a
+ * remote map (as merge inserts it, main.go:68).  Replaces an equal ts. */
+int crdt_server_diff_put(crdt_server *srv, int64_t ts, int local, const char *const *keys,
+                         const size_t *key_lens, const char *const *vals, const size_t *val_lens,
+                         size_t n);
+/* RemoteDiff.Put(int64(atoi(key)), value): gossip ingest (main.go:250-256). */
+int crdt_server_remote_put(crdt_server *srv, int64_t ts, const char *const *keys,
+                           const size_t *key_lens, const char *const *vals,
+                           const size_t *val_lens, size_t n);
+/* AddCommand after JSON decode (main.go:173-215): Diff.Put(ts_ms, &data) and
+ * the local apply; *http_status = 200, 500 or 502. */
+int crdt_server_add_command(crdt_server *srv, int64_t ts_ms, const char *const *keys,
+                            const size_t *key_lens, const char *const *vals,
+                            const size_t *val_lens, size_t n, int *http_status);
+/* (*Server).merge() (main.go:35-100) on the GPU. */
+int crdt_server_merge(crdt_server *srv);
+/* merge() of n distinct servers (same device) in ONE batched device call. */
+int crdt_servers_merge(crdt_server *const *servers, size_t n);
+int crdt_server_diff_len(crdt_server *srv, size_t *n);
+int crdt_server_remote_len(crdt_server *srv, size_t *n);
+/* Ascending Diff keys and origins (1 = *Command); writes min(cap, len). */
+int crdt_server_diff_keys(crdt_server *srv, int64_t *ts, uint8_t *local, size_t cap, size_t *n);
+int crdt_server_state_len(crdt_server *srv, size_t *n);
+/* i-th CurrentState entry in key order; pointers valid until the next
+ * mutation of the server. */
+int crdt_server_state_at(crdt_server *srv, size_t i, const char **key, size_t *key_len,
+                         const char **val, size_t *val_len);
+
 /* ------------------------------------------------ sharding (a9)
  * Contiguous row range [*begin, *end) of rank `rank` in a world of `world`
  * ranks (replica populations shard by contiguous rows). */

@@ -1,0 +1,94 @@
+"""CPU: libcrdt_amd.so loads and exports every symbol include/crdt_amd.h
+declares; host-only entry points behave; the product fails loudly without a
+GPU (there is no CPU fallback)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from crdt_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    with open(os.path.join(ROOT, "include", "crdt_amd.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(crdt_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ("crdt_gcounter_join", "crdt_vclock_classify", "crdt_lww_merge", "crdt_orset_merge",
+                 "crdt_refmerge_batch", "crdt_compare_int64", "crdt_shard_range", "crdt_server_merge"):
+        assert must in names, must
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_ctypes_table_matches_header():
+    assert sorted(_lib.SIGNATURES) == declared_functions()
+
+
+def test_abi_version_and_status_strings():
+    lib = _lib.lib()
+    assert lib.crdt_abi_version() == 1
+    assert lib.crdt_status_str(0) == b"ok"
+    assert lib.crdt_status_str(-5) == b"input not sorted"
+    assert lib.crdt_status_str(-99) == b"unknown status"
+
+
+@pytest.mark.parametrize("a,b,r", [(1, 2, -1), (2, 1, 1), (5, 5, 0), (-(2**63), 2**63 - 1, -1), (-1, 0, -1)])
+def test_compare_is_signed_int64_comparator(a, b, r):
+    # utils.Int64Comparator, main.go:106-107
+    assert _lib.lib().crdt_compare_int64(a, b) == r
+
+
+@pytest.mark.parametrize("rows,world", [(0, 1), (10, 3), (100_000_000, 8), (7, 8), (2**40 + 3, 7)])
+def test_shard_range_partitions_rows(rows, world):
+    lib = _lib.lib()
+    prev = 0
+    sizes = []
+    for r in range(world):
+        b, e = C.c_uint64(), C.c_uint64()
+        assert lib.crdt_shard_range(rows, world, r, C.byref(b), C.byref(e)) == 0
+        assert b.value == prev
+        prev = e.value
+        sizes.append(e.value - b.value)
+    assert prev == rows and max(sizes) - min(sizes) <= 1
+
+
+def test_shard_range_rejects_bad_args():
+    lib = _lib.lib()
+    b, e = C.c_uint64(), C.c_uint64()
+    assert lib.crdt_shard_range(10, 0, 0, C.byref(b), C.byref(e)) == -1
+    assert lib.crdt_shard_range(10, 2, 2, C.byref(b), C.byref(e)) == -1
+
+
+def test_set_option_validation():
+    lib = _lib.lib()
+    assert lib.crdt_set_option(b"join.unroll", 3) == -1
+    assert lib.crdt_set_option(b"no.such.knob", 1) == -1
+    assert lib.crdt_set_option(b"join.unroll", 1) == 0
+
+
+def test_null_context_is_invalid_not_a_crash():
+    lib = _lib.lib()
+    assert lib.crdt_gcounter_join(None, None, None, None, 1, 1) == -1
+    assert lib.crdt_ctx_sync(None) == -1
+
+
+@pytest.mark.skipif(__import__("torch").cuda.is_available(), reason="needs a host without a GPU")
+def test_no_gpu_fails_loudly():
+    import torch  # noqa: F401
+    from crdt_amd.engine import Engine
+    with pytest.raises(_lib.CrdtLibraryError):
+        Engine(0)
+    ctx = C.c_void_p()
+    assert _lib.lib().crdt_ctx_create(0, None, C.byref(ctx)) == -4   # CRDT_E_NODEV

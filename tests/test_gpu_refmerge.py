@@ -1,0 +1,119 @@
+"""GPU parity for RefMerge: the bit-exact (*Server).merge() of main.go:35-100.
+
+Pinned twice: every hand-derived KAT (tests/golden/refmerge_kat.json) must
+come out of the GPU path exactly, and seeded config-A workloads must match the
+C oracle (oracle/crdt_oracle.c) replica by replica -- same new Diff (same
+keys, same value objects), same CurrentState strings.
+"""
+import numpy as np
+import pytest
+import torch
+
+from crdt_amd import refmerge, synth
+from crdt_amd.server import Command, NewServer, Server, merge_servers
+from oracle import oracle, pyref
+from refmerge_util import diff_signature, kat_inputs, load_kats, oracle_merge
+
+pytestmark = pytest.mark.gpu
+KATS = load_kats()
+
+
+def _server_from(eng, diff, remote, port=8080):
+    s = Server(eng, port)
+    for ts, v in diff.items():
+        s.Diff.Put(ts, v)
+    for ts, v in remote.items():
+        s.RemoteDiff.Put(ts, v)
+    return s
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_server_merge_kat(eng, kat):
+    diff, remote = kat_inputs(kat)
+    s = _server_from(eng, diff, remote)
+    s.merge()
+    assert s.DiffSignature == kat["diff"]
+    assert s.CurrentState == kat["state"]
+    assert s.RemoteDiff.Size() == 0          # RemoteDiff.Clear() (main.go:75)
+    s.close()
+
+
+def test_all_kats_in_one_batch(eng):
+    res = refmerge.merge_batch(eng, [kat_inputs(k) for k in KATS])
+    for k, (d, st) in zip(KATS, res):
+        assert diff_signature(d) == k["diff"], k["name"]
+        assert st == k["state"], k["name"]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_config_a_demo_matches_oracle(eng, seed):
+    reps = synth.refmerge_demo(seed, replicas=5, entries=10_000, multi_key=0.1)
+    res = refmerge.merge_batch(eng, reps)
+    for (diff, remote), (d_gpu, s_gpu) in zip(reps, res):
+        d_or, s_or = oracle_merge(diff, remote)
+        assert list(d_gpu) == list(d_or)
+        assert all(d_gpu[t] is d_or[t] for t in d_or)
+        assert s_gpu == s_or
+
+
+def test_large_batch_matches_oracle(eng):
+    reps = synth.refmerge_demo(77, replicas=400, entries=600, multi_key=0.3)
+    res = refmerge.merge_batch(eng, reps)
+    for (diff, remote), (d_gpu, s_gpu) in zip(reps, res):
+        d_or, s_or = oracle_merge(diff, remote)
+        assert list(d_gpu) == list(d_or)
+        assert s_gpu == s_or
+
+
+def test_servers_batched_equals_single(eng):
+    reps = synth.refmerge_demo(5, replicas=6, entries=2000, multi_key=0.2)
+    batch = [_server_from(eng, d, r, 8080 + i) for i, (d, r) in enumerate(reps)]
+    single = [_server_from(eng, d, r, 9080 + i) for i, (d, r) in enumerate(reps)]
+    merge_servers(batch)
+    for s in single:
+        s.merge()
+    for a, b, (d, r) in zip(batch, single, reps):
+        _, st = pyref.merge(d, r)
+        assert a.DiffSignature == b.DiffSignature
+        assert a.CurrentState == b.CurrentState == st
+
+
+def test_merge_idempotent_and_empty(eng):
+    diff, remote = synth.refmerge_demo(9, replicas=1, entries=3000)[0]
+    s = _server_from(eng, diff, remote)
+    s.merge()
+    sig, st = s.DiffSignature, s.CurrentState
+    for ts, v in remote.items():            # re-gossip the same R (KAT-5 at scale)
+        s.RemoteDiff.Put(ts, v)
+    s.merge()
+    assert s.DiffSignature == sig and s.CurrentState == st
+    e = Server(eng, 1)
+    e.merge()                               # empty Diff and RemoteDiff
+    assert e.DiffSignature == [] and e.CurrentState == {}
+
+
+def test_add_command_local_apply(eng):
+    s = NewServer(8080, {}, [], eng=eng)
+    assert s.AddCommand(100, {"a": "5"}) == 200          # new key: inserted, early return
+    assert s.CurrentState == {"a": "5"}
+    assert s.AddCommand(101, {"a": "-3"}) == 200
+    assert s.CurrentState == {"a": "2"}
+    assert s.AddCommand(102, {"a": "x"}) == 500          # Atoi(value) error
+    assert s.AddCommand(103, {"b": "1", "c": "2"}) == 200  # returns after the first new key
+    assert s.CurrentState == {"a": "2", "b": "1"}
+    assert s.AddCommand(103, {"a": "1"}) == 200          # same-ms write overwrites the Diff entry
+    assert s.DiffSignature == [[100, "local"], [101, "local"], [102, "local"], [103, "local"]]
+    s.merge()                                            # local entries are excluded from the replay
+    assert s.CurrentState == {}
+
+
+def test_device_atoi_matches_go(eng):
+    cases = ["0", "-0", "+7", "007", "9223372036854775807", "-9223372036854775808", "9223372036854775808",
+             "", "+", "-", "1_0", "0x1", " 1", "1 ", "18446744073709551616", "00000000000000000000000000042",
+             "-00000000000000000000001", "--1", "12a", "99999999999999999999", "-9223372036854775809"]
+    blob = b"".join(c.encode() for c in cases)
+    off = np.concatenate([[0], np.cumsum([len(c.encode()) for c in cases])]).astype(np.int64)
+    ok, val = eng.atoi_batch(torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).to(eng.device),
+                             torch.from_numpy(off).to(eng.device))
+    for c, o, v in zip(cases, ok.cpu().tolist(), val.cpu().tolist()):
+        assert (bool(o), v if o else 0) == oracle.go_atoi(c), c

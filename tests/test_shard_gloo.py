@@ -1,0 +1,82 @@
+"""CPU, world_size 2 (gloo): the multi-GPU exchange protocol of crdt_amd.shard.
+
+The per-rank compute here is the oracle (no GPU in this container); what is
+under test is the exchange: shard planning, the order-preserving uint64 MAX
+all-reduce, and the key-range all-gather-v assembling a sorted merged set.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from crdt_amd import shard, synth
+from oracle import oracle
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # --- counters: 10_001 rows x 64 sharded, fold + all-reduce(max)
+        rows, nodes = 10_001, 64
+        b, e = shard.shard_range(rows, world, rank)
+        full = synth.counters(3, 1, rows * nodes).reshape(rows, nodes)
+        full[5, 7] = np.uint64(2**64 - 1) if rank == 1 else full[5, 7]   # unsigned edge on one rank
+        local = oracle.gcounter_fold(full[b:e])
+        t = torch.from_numpy(local.view(np.int64).copy())
+        shard.allreduce_max_u64(t)
+        got_fold = t.numpy().view(np.uint64).copy()
+        full[5, 7] = np.uint64(2**64 - 1)
+        exp_fold = oracle.gcounter_fold(full)
+
+        # --- sets: key-range partition, local merge, all-gather-v
+        ks = 5000
+        sa = synth.sort_tuples_np(*synth.set_tuples(8, 0, 20000, ks))
+        sb = synth.sort_tuples_np(*synth.set_tuples(8, 1, 20000, ks))
+        spl = shard.key_splitters(ks, world)
+        lo, hi = spl[rank], spl[rank + 1]
+
+        def part(s):
+            i, j = np.searchsorted(s[0], lo), np.searchsorted(s[0], hi)
+            return tuple(x[i:j] for x in s)
+
+        m = oracle.lww_merge(part(sa), part(sb))
+        keys = shard.allgather_v(torch.from_numpy(m[0].view(np.int64).copy())).numpy().view(np.uint64)
+        tss = shard.allgather_v(torch.from_numpy(m[1].view(np.int64).copy())).numpy().view(np.uint64)
+        full_m = oracle.lww_merge(sa, sb)
+        q.put((rank, np.array_equal(got_fold, exp_fold), np.array_equal(keys, full_m[0]),
+               np.array_equal(tss, full_m[1]), (b, e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_exchange(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    for rank, fold_ok, keys_ok, ts_ok, _ in res:
+        assert fold_ok, f"rank {rank}: sharded fold != oracle fold"
+        assert keys_ok and ts_ok, f"rank {rank}: gathered LWW merge != oracle"
+    assert res[0][4][1] == res[1][4][0]      # contiguous shards
