@@ -258,7 +258,7 @@ extern "C" int crdt_pncounter_join(crdt_ctx *ctx, const uint64_t *pa, const uint
     const size_t n2 = n / 2;
     const unsigned grid = grid_for(n2, 256, (unsigned)(ctx->num_cus * g_join.blocks_per_cu));
     if (n2)
-        k_join_pn<2, true><<<grid, 256, 0, ctx->stream>>>(
+        k_join_pn<1, true><<<grid, 256, 0, ctx->stream>>>(
             (const u64x2 *)pa, (const u64x2 *)na, (const u64x2 *)pb, (const u64x2 *)nb,
             (u64x2 *)po, (u64x2 *)no, n2);
     if (n & 1) {
