@@ -8,6 +8,8 @@ namespace crdt {
 JoinTuning g_join;
 int g_vclock_pairs_per_wave = 4;
 int g_sets_items = 8;
+int g_sets_ablate = 0;
+int g_sets_stamps = 0;
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -161,6 +163,12 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.items")) {
         if (v != 4 && v != 8) return CRDT_E_INVAL;
         g_sets_items = (int)v;
+    } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_sets_stamps = (int)v;
+    } else if (!strcmp(name, "sets.ablate")) {      // diagnostic timing builds only (wrong output)
+        if (v < 0 || v > 7 || ((v & 4) && !(v & 1))) return CRDT_E_INVAL;   // 4 requires 1 (no waits)
+        g_sets_ablate = (int)v;
     } else {
         return CRDT_E_INVAL;
     }

@@ -140,6 +140,10 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
  * pairs with t[i] > t[i+1]. */
 int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
                                uint64_t *bad_dev);
+/* Diagnostic: after crdt_set_option("sets.stamps", 1), the last set merge
+ * records 8 s_memtime stamps per tile at its phase boundaries; copies
+ * min(cap, *n) of them to host memory. */
+int crdt_debug_set_stamps(crdt_ctx *ctx, uint64_t *host, size_t cap, size_t *n);
 
 /* ------------------------------------------------ RefMerge (a1-a5)
  * Batched, bit-exact (*Server).merge() (main.go:35-100) for many replicas.

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the set-merge kernel from in-kernel s_memtime stamps.
+
+Diagnostic build path (crdt_set_option("sets.stamps", 1)): per tile, 8 stamps
+at the phase boundaries of k_set_merge.  Prints the median / p90 cycles of
+each phase and the tile start skew.  Read SHARES, not absolute time: the
+stamp path adds a drain and a barrier at the end of every tile.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from crdt_amd import _lib  # noqa: E402
+from crdt_amd.engine import Engine, TupleSet  # noqa: E402
+
+# stamp index pairs per phase, in kernel order (see STAMP(i) in csrc/sets.hip)
+PAIRS = {"load+edges": (0, 1), "rank-merge": (1, 2), "emit+scan": (2, 3), "resolve": (3, 5),
+         "stage": (5, 6), "look-back": (6, 4), "store": (4, 7)}
+
+
+def main():
+    mode = sys.argv[1] if len(sys.argv) > 1 else "lww"
+    n, ks = 10_000_000, 8_000_000
+    eng = Engine(0)
+    A = eng.synth_set_tuples(2024, 0, n, ks)
+    B = eng.synth_set_tuples(2024, 1, n, ks)
+    out = TupleSet.empty(2 * n, eng.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=eng.device)
+    fn = eng.lww_merge if mode == "lww" else eng.orset_merge
+    for _ in range(3):
+        fn(A, B, out=out, count=cnt, trim=False)
+    _lib.call("crdt_set_option", b"sets.stamps", 1)
+    fn(A, B, out=out, count=cnt, trim=False)
+    torch.cuda.synchronize()
+    m = C.c_size_t()
+    _lib.call("crdt_debug_set_stamps", eng.ctx, None, 0, C.byref(m))
+    buf = np.zeros(m.value, dtype=np.uint64)
+    _lib.call("crdt_debug_set_stamps", eng.ctx, buf.ctypes.data, m.value, C.byref(m))
+    _lib.call("crdt_set_option", b"sets.stamps", 0)
+    st = buf.reshape(-1, 8).astype(np.int64)
+    print(f"{mode}: tiles={st.shape[0]}")
+    for p, (a, b) in PAIRS.items():
+        d = st[:, b] - st[:, a]
+        print(f"  {p:12s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f} cycles")
+    tot = st[:, 7] - st[:, 0]
+    print(f"  {'total':12s} median {np.median(tot):9.0f}  p90 {np.percentile(tot, 90):9.0f}")
+    span = st[:, 7].max() - st[:, 0].min()
+    print(f"  kernel span {span} cycles; sum(tile)/span = {tot.sum() / span:.1f} tiles in flight on average")
+
+
+if __name__ == "__main__":
+    main()
