@@ -38,17 +38,23 @@ METRIC = "replica-merges/sec + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
 
 
 def dist_init():
+    """One process per GPU.  Backend "nccl" (= RCCL over xGMI on ROCm).
+    CRDT_BENCH_BACKEND=gloo lets several ranks share one GPU to rehearse the
+    multi-rank path on a 1-GPU box (never used for reported numbers)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("CRDT_BENCH_BACKEND", "nccl")
+    dev = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    return world, rank, local
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, dev
 
 
 def barrier(world):
@@ -271,7 +277,78 @@ class ShardFold(Workload):
         return None
 
 
+class RefMergeBatch(Workload):
+    """configs[0]'s merge (main.go:35-100) batched: P replicas x E entries."""
+    name = "refmerge"
+    unit = "remote-entries/s"
+    dtype = "int64"
+    kernel = "k_replay"
+
+    def __init__(self, eng, rank, world, replicas, entries, seed=2024):
+        from crdt_amd import refmerge, synth
+        self.eng = eng
+        self.host = synth.refmerge_packed(seed + rank, replicas, entries)
+        self.dev = refmerge.to_device(self.host, eng.device)
+        out = eng.refmerge_batch(self.dev)
+        torch.cuda.synchronize()
+        self.n_out = int(out["off"][-1].item())
+        h = self.host
+        self.n_l, self.n_r, self.n_kv = len(h["l_ts"]), len(h["r_ts"]), len(h["kv_key"])
+        self.config = {"workload": f"RefMerge (main.go:35-100) batched: {replicas} replicas x {entries} "
+                                   f"Diff entries + ~{entries} RemoteDiff entries each (BASELINE configs[0] "
+                                   "shape at scale)", "replicas": replicas, "entries": entries,
+                       "n_remote": self.n_r, "n_new_diff": self.n_out, "parallelism": f"replicas x{world}"}
+
+    def units(self):
+        return self.n_r
+
+    def bytes_per_launch(self):
+        # compulsory: every input once, every output once
+        return (self.n_l * 17 + self.n_r * 16 + self.n_kv * 8 + self.n_out * 17
+                + self.host["n_slots"] * 13 + int(self.host["str_off"][-1]))
+
+    def step(self):
+        self.eng.refmerge_batch(self.dev)
+
+    def cpu_baseline(self, seconds, threads):
+        """oc_refmerge, one replica per call (the reference merges under one
+        mutex per Server, main.go:43-44), independent replicas on `threads`
+        host threads like the reference's goroutine-per-replica (main.go:321).
+        Per-replica compact arrays are prepared before the timed region."""
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle
+        h = self.host
+        kvk, kvv = h["kv_key"].view(np.uint32), h["kv_val"].view(np.uint32)
+        jobs = []
+        for p in range(min(h["replicas"], 4 * threads)):
+            lb, le = int(h["l_off"][p]), int(h["l_off"][p + 1])
+            rb, re_ = int(h["r_off"][p]), int(h["r_off"][p + 1])
+            lk0, lk1 = int(h["l_kv"][lb]), int(h["l_kv"][le])
+            rk0, rk1 = int(h["r_kv"][rb]), int(h["r_kv"][re_])
+            kv_key = np.concatenate([kvk[lk0:lk1], kvk[rk0:rk1]]) - np.uint32(p * 62)
+            kv_val = np.concatenate([kvv[lk0:lk1], kvv[rk0:rk1]])
+            l_kv = (h["l_kv"][lb:le + 1] - lk0).astype(np.uint32)
+            r_kv = (h["r_kv"][rb:re_ + 1] - rk0 + (lk1 - lk0)).astype(np.uint32)
+            jobs.append((h["l_ts"][lb:le].copy(), h["l_origin"][lb:le].copy(), l_kv, h["r_ts"][rb:re_].copy(),
+                         r_kv, kv_key, kv_val, re_ - rb))
+
+        def run(j):
+            oracle.refmerge_packed(j[0], j[1], j[2], j[3], j[4], j[5], j[6], h["str_bytes"], h["str_off"], 62)
+            return j[7]
+
+        done, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            while time.perf_counter() - t0 < seconds:
+                done += sum(ex.map(run, jobs))
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oc_refmerge (C restatement of main.go:35-100), one replica per call, {len(jobs)} "
+                          f"replicas of the same batch on {threads} threads, {dt:.1f}s"}
+
+
 def make_workload(name, eng, rank, world, args):
+    if name == "refmerge":
+        return RefMergeBatch(eng, rank, world, args.replicas, args.entries)
     if name == "gcounter_join":
         return GCounterJoin(eng, rank, world, args.rows, args.nodes)
     if name == "pncounter_join":
@@ -305,13 +382,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gcounter_join",
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
-                             "shard_fold"])
+                             "shard_fold", "refmerge"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)
     ap.add_argument("--set-n", type=int, default=10_000_000)
     ap.add_argument("--key-space", type=int, default=8_000_000)
     ap.add_argument("--total-rows", type=int, default=100_000_000)
+    ap.add_argument("--replicas", type=int, default=1000)
+    ap.add_argument("--entries", type=int, default=10_000)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--option", action="append", default=[], help="name=value kernel knob (crdt_set_option)")

@@ -141,6 +141,60 @@ def refmerge_demo(seed: int, replicas: int = 5, entries: int = 10_000, multi_key
     return out
 
 
+def refmerge_packed(seed: int, replicas: int, entries: int):
+    """Config A's workload shape at scale, generated directly in the packed
+    CSR layout of crdt_refmerge_in (vectorised; one kv per entry as the
+    reference's load generator sends, main.go:281-286).
+
+    Per replica: L = `entries` ts with gaps U[1,4], origin local w.p. 1/2;
+    R = `entries` ts: 85% own-clock, 5% colliding with L, 10% above max(L).
+    Values: "-20".."-11" (main.go:282) plus ~1% odd strings; keys: 62 slots
+    per replica (main.go:274).  Returns the dict Engine.refmerge_batch takes
+    (numpy arrays; move with refmerge.to_device).
+    """
+    rng = np.random.default_rng(seed)
+    P, E = replicas, entries
+    strs = [str(v) for v in range(-20, -10)] + _ODD_VALUES
+    blob = "".join(strs).encode()
+    str_off = np.zeros(len(strs) + 1, np.int64)
+    str_off[1:] = np.cumsum([len(s.encode()) for s in strs])
+    t0 = 1_700_000_000_000 + rng.integers(0, 1000, size=(P, 1))
+    l_ts = t0 + np.cumsum(rng.integers(1, 5, size=(P, E)), axis=1)
+    l_origin = (rng.random((P, E)) < 0.5).astype(np.uint8)
+    n_above, n_coll = E // 10, E // 20
+    n_own = E - n_above - n_coll
+    own = t0 + np.cumsum(rng.integers(1, 5, size=(P, n_own)), axis=1)
+    coll = np.take_along_axis(l_ts, rng.integers(0, E, size=(P, n_coll)), axis=1)
+    above = l_ts[:, -1:] + np.cumsum(rng.integers(1, 5, size=(P, n_above)), axis=1)
+    r_all = np.sort(np.concatenate([own, coll, above], axis=1), axis=1)
+    # unique per replica: bump duplicates by rebuilding each row's unique set
+    r_rows = [np.unique(r) for r in r_all]
+    r_off = np.zeros(P + 1, np.int64)
+    r_off[1:] = np.cumsum([len(r) for r in r_rows])
+    r_ts = np.concatenate(r_rows).astype(np.int64)
+    n_l, n_r = P * E, int(r_off[-1])
+
+    def vals(n):
+        v = rng.integers(0, 10, size=n)
+        odd = rng.random(n) < 0.01
+        v[odd] = 10 + rng.integers(0, len(_ODD_VALUES), size=int(odd.sum()))
+        return v.astype(np.uint32)
+
+    l_rep = np.repeat(np.arange(P, dtype=np.int64), E)
+    r_rep = np.repeat(np.arange(P, dtype=np.int64), np.diff(r_off))
+    kv_key = np.concatenate([l_rep * 62 + rng.integers(0, 62, size=n_l),
+                             r_rep * 62 + rng.integers(0, 62, size=n_r)]).astype(np.uint32)
+    kv_val = np.concatenate([vals(n_l), vals(n_r)])
+    return {
+        "replicas": P, "n_slots": P * 62,
+        "l_off": np.arange(0, n_l + 1, E, dtype=np.int64), "l_ts": l_ts.reshape(-1).astype(np.int64),
+        "l_origin": l_origin.reshape(-1), "l_kv": np.arange(n_l + 1, dtype=np.int64),
+        "r_off": r_off, "r_ts": r_ts, "r_kv": np.arange(n_l, n_l + n_r + 1, dtype=np.int64),
+        "kv_key": kv_key.view(np.int32), "kv_val": kv_val.view(np.int32),
+        "str_bytes": np.frombuffer(blob, np.uint8).copy(), "str_off": str_off,
+    }
+
+
 def sort_tuples_np(key, ts, rep, tomb):
     """Stable (key, ts, rep) sort of numpy SoA tuples."""
     order = np.lexsort((rep, ts, key))  # lexsort is stable; last key is primary

@@ -25,6 +25,21 @@ def diff_signature(diff):
     return [[ts, "local" if type(v).__name__ == "Command" else "remote"] for ts, v in sorted(diff.items())]
 
 
+def oracle_packed_replica(h, p, slots_per_replica=62):
+    """Oracle merge of replica p of a packed batch (crdt_amd.synth.refmerge_packed).
+    Returns (diff_ts, diff_origin, diff_src_global, kind, str, sum) with src
+    rebased to the batch's global L / R indices like the device output."""
+    lb, le = int(h["l_off"][p]), int(h["l_off"][p + 1])
+    rb, re_ = int(h["r_off"][p]), int(h["r_off"][p + 1])
+    kv_key = (h["kv_key"].view(np.uint32).astype(np.int64) - p * slots_per_replica).astype(np.uint32)
+    o_ts, o_or, o_src, kind, sstr, ssum = oracle.refmerge_packed(
+        h["l_ts"][lb:le], h["l_origin"][lb:le], h["l_kv"][lb:le + 1].astype(np.uint32),
+        h["r_ts"][rb:re_], h["r_kv"][rb:re_ + 1].astype(np.uint32), kv_key, h["kv_val"].view(np.uint32),
+        h["str_bytes"], h["str_off"], slots_per_replica)
+    src = np.where(o_src >= 0, o_src + lb, o_src - rb)
+    return o_ts, o_or, src, kind, sstr, ssum
+
+
 def oracle_merge(diff, remote):
     """(new_diff, state) of one replica through oracle/crdt_oracle.c."""
     pk = Packer()

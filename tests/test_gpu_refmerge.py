@@ -65,6 +65,28 @@ def test_large_batch_matches_oracle(eng):
         assert s_gpu == s_or
 
 
+def test_packed_batch_matches_oracle(eng):
+    """The bench's packed config-A-at-scale batch: every replica checked."""
+    from refmerge_util import oracle_packed_replica
+    h = synth.refmerge_packed(11, 48, 5000)
+    out = eng.refmerge_batch(refmerge.to_device(h, eng.device))
+    off = out["off"].cpu().numpy()
+    ts, org, src = (out[k].cpu().numpy() for k in ("ts", "origin", "src"))
+    kind, sstr, ssum = (out[k].cpu().numpy() for k in ("st_kind", "st_str", "st_sum"))
+    for p in range(h["replicas"]):
+        o_ts, o_or, o_src, k, s, v = oracle_packed_replica(h, p)
+        a, b = int(off[p]), int(off[p + 1])
+        np.testing.assert_array_equal(ts[a:b], o_ts)
+        np.testing.assert_array_equal(org[a:b], o_or)
+        np.testing.assert_array_equal(src[a:b], o_src)
+        sl = slice(p * 62, (p + 1) * 62)
+        np.testing.assert_array_equal(kind[sl], k)
+        m = k > 0
+        np.testing.assert_array_equal(sstr[sl].view(np.uint32)[k == 1], s[k == 1])
+        np.testing.assert_array_equal(ssum[sl][k == 2], v[k == 2])
+        assert m.sum() > 0
+
+
 def test_servers_batched_equals_single(eng):
     reps = synth.refmerge_demo(5, replicas=6, entries=2000, multi_key=0.2)
     batch = [_server_from(eng, d, r, 8080 + i) for i, (d, r) in enumerate(reps)]
