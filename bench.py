@@ -195,7 +195,7 @@ class VClockClassify(Workload):
 
 class SetMerge(Workload):
     unit = "input-tuples/s"
-    kernel = "k_set_tile"
+    kernel = "k_partition+k_set_merge"
 
     def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
         self.eng, self.n, self.lww = eng, n, lww

@@ -109,6 +109,7 @@ SIGNATURES = {
                               C.POINTER(crdt_tuples), _P]),
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),
     "crdt_debug_set_stamps": (_I, [_CTX, _P, _SZ, C.POINTER(_SZ)]),
+    "crdt_debug_set_grid": (_I, [C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
     "crdt_server_new": (_I, [_CTX, _I, C.POINTER(_P)]),

@@ -7,9 +7,9 @@
 namespace crdt {
 JoinTuning g_join;
 int g_vclock_pairs_per_wave = 4;
-int g_sets_items = 8;
-int g_sets_ablate = 0;
 int g_sets_stamps = 0;
+int g_sets_grid_per_cu = 0;
+int g_sets_diag = 0;
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -160,15 +160,15 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "vclock.pairs_per_wave")) {
         if (v != 1 && v != 2 && v != 4 && v != 8) return CRDT_E_INVAL;
         g_vclock_pairs_per_wave = (int)v;
-    } else if (!strcmp(name, "sets.items")) {
-        if (v != 4 && v != 8) return CRDT_E_INVAL;
-        g_sets_items = (int)v;
+    } else if (!strcmp(name, "sets.grid_per_cu")) { // 0 = occupancy query (co-residency required)
+        if (v < 0 || v > 16) return CRDT_E_INVAL;
+        g_sets_grid_per_cu = (int)v;
+    } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic: WRONG output order
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_sets_diag = (int)v;
     } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sets_stamps = (int)v;
-    } else if (!strcmp(name, "sets.ablate")) {      // diagnostic timing builds only (wrong output)
-        if (v < 0 || v > 7 || ((v & 4) && !(v & 1))) return CRDT_E_INVAL;   // 4 requires 1 (no waits)
-        g_sets_ablate = (int)v;
     } else {
         return CRDT_E_INVAL;
     }

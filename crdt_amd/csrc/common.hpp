@@ -36,8 +36,8 @@ struct JoinTuning {
 };
 extern JoinTuning g_join;
 extern int g_vclock_pairs_per_wave;
-extern int g_sets_items;
-extern int g_sets_ablate;   // diagnostic only: 1 = skip look-back, 2 = skip output stores, 4 = static tile ids
+extern int g_sets_grid_per_cu; // persistent set-merge workgroups per CU (0 = occupancy query)
+extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
 extern int g_sets_stamps;   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
 
 // Make the context's device current for this host thread.

@@ -15,17 +15,20 @@
 //   1. k_partition: 16-ary searches, four tile diagonals per wave (one per
 //      16-lane group), comparing keys first and loading ts/rep only on a key
 //      tie.
-//   2. k_set_merge: each workgroup takes the next tile id from an atomic
-//      counter (a look-back then never waits on a tile that no running
-//      workgroup owns), issues all of the tile's A/B loads before any LDS
-//      store, finds its lane's merge-path split in LDS and merges ITEMS
-//      elements keeping the merged tags in REGISTERS (the two heads are the
-//      only LDS reads per step), derives emit flags / LWW winners / OR-Set
-//      tomb-ORs from registers (runs that cross a lane, tile edge continue
-//      through the merged-order index in LDS and then global memory: rare),
-//      publishes its count and looks back 256 predecessors per round trip
-//      ({flag, count} 8-byte agent-scope atomics: the data is the flag),
-//      stages the output in LDS and writes it with coalesced stores.
+//   2. k_set_merge: a persistent grid of ND data waves + 1 control wave.
+//      The control wave claims tiles one iteration ahead (one atomic), loads
+//      their splits, warms the cache with the next tile's lines, publishes each tile's count and runs the
+//      decoupled look-back (256 predecessors per round trip; {flag, count}
+//      8-byte agent-scope atomics: the data is the flag) with an iteration
+//      of slack: the data waves hold a tile's staged output in registers and
+//      write it out after the NEXT tile's loads.  Per tile the data waves
+//      find each lane's merge-path split in LDS and merge ITEMS elements
+//      keeping the merged tags in registers, derive emit flags / LWW winners /
+//      OR-Set tomb-ORs from registers (runs that cross a lane or tile edge
+//      continue through the merged-order index in LDS and then global
+//      memory: rare), stage in LDS and read back in coalesced copy-out order.
+#include <algorithm>
+
 #include "scan.hpp"
 
 namespace crdt {
@@ -43,6 +46,10 @@ __device__ __forceinline__ bool tag_le(const Tag &a, const Tag &b) {
 }
 __device__ __forceinline__ bool tag_eq(const Tag &a, const Tag &b) {
     return a.k == b.k && a.t == b.t && a.r == b.r;
+}
+// Field-wise select (a ternary on Tag objects lowers to a scratch alloca).
+__device__ __forceinline__ Tag tag_sel(bool c, const Tag &x, const Tag &y) {
+    return Tag{c ? x.k : y.k, c ? x.t : y.t, c ? x.r : y.r};
 }
 __device__ __forceinline__ Tag gtag(const crdt_tuples &s, size_t i) { return Tag{s.key[i], s.ts[i], s.rep[i]}; }
 
@@ -102,14 +109,15 @@ __device__ __forceinline__ void st_status(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Called by the WHOLE 256-lane block (contains barriers; every loop decision
-// is block-uniform).  Exclusive prefix of tile t = sum of the counts of tiles
-// 0..t-1.  One round trip reads 1024 predecessors (4 per lane, nearest
-// first); it stops at the nearest inclusive prefix and spins only while a
-// nearer predecessor has not published its count.  Bounded: sets *err.
-__device__ uint64_t block_look_back(const uint64_t *status, uint32_t t, uint32_t *err, int *s_fi, int *s_fv,
-                                    uint64_t *s_part) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// Called by ONE whole wave (the control wave; no barriers inside).
+// Exclusive prefix of tile t = sum of the counts of tiles 0..t-1.  One round
+// trip reads 256 predecessors (4 per lane, nearest first); it stops at the
+// nearest inclusive prefix and spins only while a nearer predecessor has not
+// published its count.  The {flag, count} word is one 8-byte agent-scope
+// atomic: the data is the flag.  Bounded: sets *err.
+__device__ uint64_t wave_look_back(const uint64_t *status, uint32_t t, uint32_t *err, uint32_t *nspin = nullptr,
+                                   uint32_t *nround = nullptr) {
+    const int lane = threadIdx.x & 63;
     uint64_t excl = 0;
     int64_t base = (int64_t)t - 1;
     unsigned spins = 0;
@@ -117,25 +125,21 @@ __device__ uint64_t block_look_back(const uint64_t *status, uint32_t t, uint32_t
         uint64_t s[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int64_t idx = base - (w * 256 + j * 64 + lane);
+            const int64_t idx = base - (j * 64 + lane);
             s[j] = idx >= 0 ? ld_status(status + idx) : kFlagInc;   // virtual inclusive 0 before tile 0
         }
-        int fi = 1024, fv = 1024;
+        int fi = 256, fv = 256;
 #pragma unroll
         for (int j = 3; j >= 0; --j) {
             const uint64_t inc = __ballot((s[j] >> 62) == 2), inv = __ballot((s[j] >> 62) == 0);
-            if (inc) fi = w * 256 + j * 64 + __ffsll((unsigned long long)inc) - 1;
-            if (inv) fv = w * 256 + j * 64 + __ffsll((unsigned long long)inv) - 1;
+            if (inc) fi = j * 64 + __ffsll((unsigned long long)inc) - 1;
+            if (inv) fv = j * 64 + __ffsll((unsigned long long)inv) - 1;
         }
-        if (lane == 0) { s_fi[w] = fi; s_fv[w] = fv; }
-        __syncthreads();
-        int FI = s_fi[0], FV = s_fv[0];
-#pragma unroll
-        for (int k = 1; k < 4; ++k) { FI = s_fi[k] < FI ? s_fi[k] : FI; FV = s_fv[k] < FV ? s_fv[k] : FV; }
-        __syncthreads();
-        if (FV < FI) {                               // a nearer predecessor has not published yet
+        if (nround) ++*nround;
+        if (fv < fi) {                               // a nearer predecessor has not published yet
+            if (nspin) ++*nspin;
             if (++spins > (1u << 22)) {
-                if (threadIdx.x == 0) atomicOr(err, 1u);
+                if (lane == 0) atomicOr(err, 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -143,309 +147,603 @@ __device__ uint64_t block_look_back(const uint64_t *status, uint32_t t, uint32_t
         }
         uint64_t v = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v += (w * 256 + j * 64 + lane <= FI) ? (s[j] & kValMask) : 0;
+        for (int j = 0; j < 4; ++j) v += (j * 64 + lane <= fi) ? (s[j] & kValMask) : 0;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-        if (lane == 0) s_part[w] = v;
-        __syncthreads();
-        excl += s_part[0] + s_part[1] + s_part[2] + s_part[3];
-        __syncthreads();
-        if (FI < 1024) break;
-        base -= 1024;
+        excl += v;
+        if (fi < 256) break;
+        base -= 256;
     }
     return excl;
 }
 
 // ---------------------------------------------------------------- tile merge
-template <int MODE, int ITEMS>
-__global__ __launch_bounds__(256) void k_set_merge(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
-                                                   const uint64_t *__restrict__ split, uint64_t *status,
-                                                   uint32_t *tile_ctr, uint32_t *err, uint32_t ntiles, int ablate,
-                                                   crdt_tuples out, uint64_t *__restrict__ out_count,
-                                                   uint64_t *stamps) {
-    // Diagnostic build only (stamps != nullptr): per-tile s_memtime at phase
-    // boundaries, written to a buffer nothing else reads.
-#define STAMP(i) \
-    do { if (stamps && threadIdx.x == 0) stamps[(size_t)s_tile * 8 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
-    constexpr int TILE = 256 * ITEMS;
-    __shared__ uint64_t skey[TILE];
-    __shared__ uint64_t sts[TILE];
-    __shared__ uint32_t srep[TILE];
-    __shared__ uint8_t stomb[TILE];
+// Workgroup of k_set_merge: warp-specialised, 8 waves.
+//   waves 0..ND-1 : data waves -- merge a tile that is already in LDS
+//   wave  ND      : loader    -- claims tiles, loads their split and edge
+//                               candidates, DMAs the tile into the free LDS
+//                               buffer (global_load_lds, no registers)
+//   wave  ND+1    : look-back -- turns each tile's count into its offset
+// 8 waves of <= 128 VGPRs pack exactly two workgroups per CU (2 waves per
+// SIMD each); two double-buffered tiles per workgroup fill the 160 KB LDS.
+constexpr int ND = 6;                  // data waves
+constexpr int NDL = ND * 64;           // data lanes
+constexpr int SET_BLOCK = NDL + 128;
+constexpr int SET_ITEMS = 4;           // merged elements per data lane
+constexpr int TILE = NDL * SET_ITEMS;  // 1536 merged elements per tile
+
+// A wave-uniform 64-bit LDS value in scalar registers.
+__device__ __forceinline__ uint64_t uread64(const uint64_t &v) {
+    const uint64_t x = v;
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+// One tile's bounds in A and B, from the partition.
+struct TileBounds {
+    size_t d0, i0, i1, j0, j1;
+    int len, na_t, nb_t;
+};
+__device__ __forceinline__ TileBounds tile_bounds(uint32_t t, uint64_t i0, uint64_t i1, size_t n) {
+    TileBounds b;
+    b.d0 = (size_t)t * TILE;
+    const size_t d1 = b.d0 + TILE < n ? b.d0 + TILE : n;
+    b.i0 = i0;
+    b.i1 = i1;
+    b.j0 = b.d0 - i0;
+    b.j1 = d1 - i1;
+    b.len = (int)(d1 - b.d0);
+    b.na_t = (int)(i1 - i0);
+    b.nb_t = b.len - b.na_t;
+    return b;
+}
+
+// One LDS tile buffer.  Each array holds A's part of the tile, then B's,
+// each DMA'd in 16-byte chunks from its 16-byte aligned-down start, so a
+// part's element 0 sits at byte offset o[A|B] of its array (its global
+// misalignment past a 16-byte boundary); the chunks never overlap.  After
+// the merge the arrays are reused, from 0, as the output staging area.
+struct TileBuf {
+    alignas(16) uint64_t key[TILE + 8];
+    alignas(16) uint64_t ts[TILE + 8];
+    alignas(16) uint32_t rep[TILE + 16];
+    alignas(16) uint8_t tomb[TILE + 64];
+    uint64_t ek[4], et[4];             // edge candidates A[i0-1], B[j0-1], A[i1], B[j1]
+    uint32_t er[4], ev[4];
+    uint32_t tile;
+    uint32_t ok[2], ot[2], orr[2], om[2];   // byte offsets of A's / B's element 0
+    uint64_t i0, i1;                   // the tile's split
+};
+
+// LDS hand-off between waves of one workgroup: payload stores, then the
+// tag (LDS accesses of one wave complete in order); the reader polls the tag
+// and reads the payload after it.
+__device__ __forceinline__ void lds_publish(uint32_t *tag, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(tag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(const uint32_t *tag, uint32_t v) {
+    while (__hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+// Barrier among the ND data waves only (the loader and look-back waves run
+// on): an LDS arrival counter; gen advances by ND per use.
+__device__ __forceinline__ void data_barrier(uint32_t *cnt, uint32_t &gen) {
+    gen += ND;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's LDS accesses are done
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+// Loader wave: DMA elements src[0, cnt) into the LDS array `dst` at the
+// 16-byte aligned byte offset `at`, in 16-byte chunks from src's aligned-down
+// address (1 KB per wave instruction, no registers held; the last chunk reads
+// at most 15 bytes past the part, inside the same 16-byte block, never past a
+// page).  Returns the byte offset of element 0; *at advances past the chunks.
+template <typename E>
+__device__ __forceinline__ uint32_t dma_part(const E *src, uint32_t cnt, void *dst, uint32_t *at, int lane) {
+    const uint32_t sh = (uint32_t)((uintptr_t)src & 15);
+    const uint32_t o = *at + sh;
+    if (cnt == 0) return o;
+    const uint32_t bytes = (sh + cnt * (uint32_t)sizeof(E) + 15) & ~15u;
+    const char *g = (const char *)src - sh;
+    char *d = (char *)dst + *at;
+    for (uint32_t off = 0; off < bytes; off += 1024) {
+        if (off + 16u * (uint32_t)lane < bytes)
+            __builtin_amdgcn_global_load_lds((const void *)(g + off + 16 * lane),
+                                             (__attribute__((address_space(3))) void *)(d + off), 16, 0, 0);
+    }
+    *at += bytes;
+    return o;
+}
+
+// Persistent, warp-specialised merge.  For iteration k of a workgroup
+// (tile t_k, LDS buffer k & 1):
+//   loader     : claim t_k (one atomic), load its split, wait until the data
+//                waves are done with buffer k & 1 (iteration k-2), hand t_k to
+//                the look-back wave, DMA the tile and its edge candidates in,
+//                publish it
+//   look-back  : look back for t_k's offset as soon as it is claimed (only
+//                the predecessors' counts are needed), then wait for t_k's
+//                count and publish its inclusive prefix and its offset
+//   data waves : merge t_k from LDS | publish its count (globally: the
+//                look-back's aggregate; and to the look-back wave) | write
+//                t_{k-2}'s output, held in registers, at its offset | resolve
+//                tombs, stage in LDS, read back into the hold registers |
+//                release the buffer
+// Only the data waves synchronise with each other (LDS counter); the other
+// two roles communicate by tagged LDS words.  Loads of t_{k+1} overlap the
+// merge of t_k, and a late look-back delays only this workgroup's copy-out,
+// two iterations later, never the next tile's count, so look-back latency
+// does not chain across the grid.  Tiles are claimed at the loader's pace,
+// which tracks the data waves' (two buffers), so claim order tracks
+// processing order; a workgroup that is not resident owns no tile, so every
+// look-back makes progress.
+template <int MODE>
+__global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
+    crdt_tuples A, crdt_tuples B, size_t na, size_t nb, const uint64_t *__restrict__ split, uint64_t *status,
+    uint32_t *tile_ctr, uint32_t *err, uint32_t ntiles, crdt_tuples out, uint64_t *__restrict__ out_count,
+    uint64_t *stamps, int diag) {
+    __shared__ TileBuf buf[2];
     __shared__ uint16_t smi[TILE];
-    __shared__ uint64_t s_edge_k[2], s_edge_t[2];
-    __shared__ uint32_t s_edge_r[2];
-    __shared__ int s_has[2];
-    __shared__ uint32_t s_tile;
-    __shared__ int s_fi[4], s_fv[4];
-    __shared__ uint64_t s_part[4];
+    __shared__ uint32_t s_wsum[ND];
+    __shared__ uint64_t s_wf_k[ND], s_wf_t[ND], s_wl_k[ND], s_wl_t[ND];   // first / last item of each
+    __shared__ uint32_t s_wf_r[ND], s_wl_r[ND];                            //   data wave
+    __shared__ uint32_t s_dbar;                      // data-wave soft barrier counter
+    __shared__ uint32_t s_load_tag[2];               // loader -> data: buffer holds iteration k (k+1)
+    __shared__ uint32_t s_free_tag[2];               // data -> loader: iteration k done with it (k+1)
+    // rings of 4 (slot k & 3): data waves lag the look-back by up to two
+    // iterations (they write tile k-2 out in iteration k)
+    __shared__ uint32_t s_lb_tile[4], s_lb_tag[4];   // loader -> look-back: tile of iteration k
+    __shared__ uint32_t s_tot[4], s_tot_tag[4];      // data -> look-back: count of iteration k
+    __shared__ uint64_t s_off[4];                    // look-back -> data: offset of iteration k
+    __shared__ uint32_t s_off_tag[4];
 
-    const int tid = threadIdx.x;
-    if (tid == 0) s_tile = (ablate & 4) ? blockIdx.x : atomicAdd(tile_ctr, 1u);   // 4: timing only, with 1
-    __syncthreads();
-    const uint32_t t = s_tile;
-    STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63;
     const size_t n = na + nb;
-    const size_t d0 = (size_t)t * TILE;
-    const size_t d1 = d0 + TILE < n ? d0 + TILE : n;
-    const size_t i0 = split[t], i1 = split[t + 1];
-    const size_t j0 = d0 - i0, j1 = d1 - i1;
-    const int na_t = (int)(i1 - i0), len = (int)(d1 - d0);
-    const int nb_t = len - na_t;
+    const int role = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: separate loops
+    // Diagnostic build only (stamps != nullptr): s_memtime at phase
+    // boundaries of each tile, written to a buffer nothing else reads.
+#define STAMP(t, i) \
+    do { if (stamps && tid == 0) stamps[(size_t)(t) * 16 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define WSTAMP(t, i, v) \
+    do { if (stamps && lane == 0) stamps[(size_t)(t) * 16 + (i)] = (v); } while (0)
 
-    // ---- issue every load of the tile (and its edge neighbours) before any LDS store
-    uint64_t rk[ITEMS], rt[ITEMS];     // this lane's tile elements x = u*256 + tid (kept for the rank search)
-    uint32_t rr[ITEMS];
-    {
-        uint8_t rb[ITEMS];
-#pragma unroll
-        for (int u = 0; u < ITEMS; ++u) {
-            const int x = u * 256 + tid;
-            if (x < len) {
-                const bool fa = x < na_t;
-                const size_t g = fa ? i0 + x : j0 + (x - na_t);
-                rk[u] = (fa ? A.key : B.key)[g];
-                rt[u] = (fa ? A.ts : B.ts)[g];
-                rr[u] = (fa ? A.rep : B.rep)[g];
-                rb[u] = (fa ? A.tomb : B.tomb)[g];
-            }
-        }
-        if (tid == 0 || tid == 64) {                  // merged positions d0-1 (prev) and d1 (next)
-            const bool prev = tid == 0;
-            int has = 0;
-            Tag e{0, 0, 0};
-            if (prev && d0 > 0) {
-                has = 1;
-                if (i0 > 0 && j0 > 0) {
-                    const Tag a = gtag(A, i0 - 1), b = gtag(B, j0 - 1);
-                    const bool lb = tag_le(a, b);      // the later one in merged order
-                    e = Tag{lb ? b.k : a.k, lb ? b.t : a.t, lb ? b.r : a.r};
-                } else if (i0 > 0) {
-                    e = gtag(A, i0 - 1);
-                } else {
-                    e = gtag(B, j0 - 1);
-                }
-            } else if (!prev && d1 < n) {
-                has = 1;
-                if (i1 < na && j1 < nb) {
-                    const Tag a = gtag(A, i1), b = gtag(B, j1);
-                    const bool la = tag_le(a, b);      // the earlier one in merged order
-                    e = Tag{la ? a.k : b.k, la ? a.t : b.t, la ? a.r : b.r};
-                } else if (i1 < na) {
-                    e = gtag(A, i1);
-                } else {
-                    e = gtag(B, j1);
-                }
-            }
-            const int w = prev ? 0 : 1;
-            s_has[w] = has;
-            s_edge_k[w] = e.k;
-            s_edge_t[w] = e.t;
-            s_edge_r[w] = e.r;
-        }
-#pragma unroll
-        for (int u = 0; u < ITEMS; ++u) {
-            const int x = u * 256 + tid;
-            if (x < len) {
-                skey[x] = rk[u];
-                sts[x] = rt[u];
-                srep[x] = rr[u];
-                stomb[x] = rb[u];
-            }
-        }
+    if (tid < 2) {
+        s_load_tag[tid] = 0;
+        s_free_tag[tid] = 0;
     }
-    __syncthreads();
-    STAMP(1);
+    if (tid < 4) {
+        s_lb_tag[tid] = 0;
+        s_tot_tag[tid] = 0;
+        s_off_tag[tid] = 0;
+    }
+    if (tid == 0) s_dbar = 0;
+    __syncthreads();                          // the only workgroup-wide barrier
 
-#define LTAG(x) Tag{skey[(x)], sts[(x)], srep[(x)]}
-    // ---- merge path: this lane owns merged positions [dd, dd + nv); the
-    // merged tags stay in registers, the two heads are the only LDS reads
-    // per serial step.  (A per-element ILP rank search was measured 3.6x
-    // slower here: 12 x 3 scattered LDS probes per element.)
-    const int dd = tid * ITEMS < len ? tid * ITEMS : len;
-    const int nv = len - dd < ITEMS ? len - dd : ITEMS;
-    Tag it[ITEMS];
-    uint8_t tb[ITEMS];
-    {
-        int lo = dd > nb_t ? dd - nb_t : 0, hi = dd < na_t ? dd : na_t;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            const int mb = na_t + dd - 1 - mid;
-            bool le;
-            const uint64_t ka = skey[mid], kb = skey[mb];
-            if (ka != kb) le = ka < kb;
-            else le = tag_le(LTAG(mid), LTAG(mb));
-            if (le) lo = mid + 1;
-            else hi = mid;
+    if (role == ND) {
+        // ============================================================ loader wave
+        for (uint32_t k = 0;; ++k) {
+            const int bi = k & 1;
+            uint32_t a = 0;
+            if (lane == 0) a = atomicAdd(tile_ctr, 1u);
+            const uint32_t t = __shfl(a, 0);
+            uint64_t sp = 0;
+            if (lane < 2 && t < ntiles) sp = split[t + lane];
+            const uint64_t i0 = __shfl(sp, 0), i1 = __shfl(sp, 1);
+            if (k >= 2) lds_wait(&s_free_tag[bi], k - 1);     // iteration k-2 released the buffer
+            if (lane == 0) {                  // the look-back can start now (its slot's last
+                s_lb_tile[k & 3] = t;         // reader, iteration k-4, is done: the data waves
+                lds_publish(&s_lb_tag[k & 3], k + 1);   // wrote k-4 out in iteration k-2)
+            }
+            TileBuf &tb = buf[bi];
+            if (t < ntiles) {
+                WSTAMP(t, 12, __builtin_amdgcn_s_memtime());
+                const TileBounds b = tile_bounds(t, i0, i1, n);
+                uint32_t ak = 0, at = 0, ar = 0, am = 0;
+                const uint32_t okA = dma_part(A.key + b.i0, b.na_t, tb.key, &ak, lane);
+                const uint32_t okB = dma_part(B.key + b.j0, b.nb_t, tb.key, &ak, lane);
+                const uint32_t otA = dma_part(A.ts + b.i0, b.na_t, tb.ts, &at, lane);
+                const uint32_t otB = dma_part(B.ts + b.j0, b.nb_t, tb.ts, &at, lane);
+                const uint32_t orA = dma_part(A.rep + b.i0, b.na_t, tb.rep, &ar, lane);
+                const uint32_t orB = dma_part(B.rep + b.j0, b.nb_t, tb.rep, &ar, lane);
+                const uint32_t omA = dma_part(A.tomb + b.i0, b.na_t, tb.tomb, &am, lane);
+                const uint32_t omB = dma_part(B.tomb + b.j0, b.nb_t, tb.tomb, &am, lane);
+                if (lane < 4) {               // merged neighbours' candidates
+                    const bool isA = (lane & 1) == 0;
+                    const size_t g = lane == 0 ? b.i0 - 1 : lane == 1 ? b.j0 - 1 : lane == 2 ? b.i1 : b.j1;
+                    const uint32_t ev = lane == 0 ? b.i0 > 0 : lane == 1 ? b.j0 > 0 : lane == 2 ? b.i1 < na : b.j1 < nb;
+                    uint64_t ek = 0, et = 0;
+                    uint32_t er = 0;
+                    if (ev) {
+                        ek = (isA ? A.key : B.key)[g];
+                        et = (isA ? A.ts : B.ts)[g];
+                        er = (isA ? A.rep : B.rep)[g];
+                    }
+                    tb.ek[lane] = ek;
+                    tb.et[lane] = et;
+                    tb.er[lane] = er;
+                    tb.ev[lane] = ev;
+                }
+                if (lane == 0) {
+                    tb.ok[0] = okA;
+                    tb.ok[1] = okB;
+                    tb.ot[0] = otA;
+                    tb.ot[1] = otB;
+                    tb.orr[0] = orA;
+                    tb.orr[1] = orB;
+                    tb.om[0] = omA;
+                    tb.om[1] = omB;
+                    tb.i0 = i0;
+                    tb.i1 = i1;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA has landed in LDS
+                WSTAMP(t, 13, __builtin_amdgcn_s_memtime());
+            }
+            if (lane == 0) {
+                tb.tile = t;
+                lds_publish(&s_load_tag[bi], k + 1);
+            }
+            if (t >= ntiles) break;
         }
-        int ia = lo, ib = dd - lo;
-        Tag ha = ia < na_t ? LTAG(ia) : Tag{0, 0, 0};
-        Tag hb = ib < nb_t ? LTAG(na_t + ib) : Tag{0, 0, 0};
+        return;
+    }
+
+    if (role == ND + 1) {
+        // ============================================================ look-back wave
+        // Looks back as soon as the loader has claimed the tile (it needs
+        // only the predecessors' counts), then waits for the tile's own count
+        // to publish its inclusive prefix.
+        for (uint32_t k = 0;; ++k) {
+            const int si = k & 3;
+            lds_wait(&s_lb_tag[si], k + 1);
+            const uint32_t t = __builtin_amdgcn_readfirstlane(s_lb_tile[si]);
+            if (t >= ntiles) break;
+            uint64_t P = 0;
+            uint32_t nsp = 0, nrd = 0;
+            WSTAMP(t, 8, __builtin_amdgcn_s_memtime());
+            if (diag) P = (uint64_t)t * TILE;  // timing diagnostic only: no look-back, scrambled output
+            else if (t > 0) P = wave_look_back(status, t, err, &nsp, &nrd);
+            WSTAMP(t, 9, __builtin_amdgcn_s_memtime());
+            WSTAMP(t, 10, nsp);
+            WSTAMP(t, 11, nrd);
+            lds_wait(&s_tot_tag[si], k + 1);
+            const uint32_t total = s_tot[si];
+            if (lane == 0) {
+                if (t > 0 && !diag) st_status(status + t, kFlagInc | (P + total));
+                if (t == ntiles - 1) *out_count = P + total;
+                s_off[si] = P;
+                lds_publish(&s_off_tag[si], k + 1);
+            }
+        }
+        return;
+    }
+
+    // ================================================================ data waves
+    // the output of t_{k-1} (h1) and t_{k-2} (h2), held in registers in
+    // copy-out order until its offset is known; t_{k-2}'s is written out in
+    // iteration k, so a look-back has two iterations of slack
+    uint64_t h1k[SET_ITEMS], h1t[SET_ITEMS], h2k[SET_ITEMS], h2t[SET_ITEMS];
+    uint32_t h1r[SET_ITEMS], h2r[SET_ITEMS];
+    uint8_t h1b[SET_ITEMS], h2b[SET_ITEMS];
+    uint32_t held1 = 0, held2 = 0;            // their counts (0: nothing held)
+    uint32_t dgen = 0;                        // data-wave soft-barrier generation
+    uint32_t k = 0;
+    for (;; ++k) {
+        // Opaque per-iteration copy of the lane id: keeps LICM from hoisting
+        // lane-dependent address arithmetic out of the loop.
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        const int bi = k & 1;
+        TileBuf &T = buf[bi];
+        lds_wait(&s_load_tag[bi], k + 1);
+        const uint32_t cur = __builtin_amdgcn_readfirstlane(T.tile);
+        if (cur >= ntiles) break;
+        STAMP(cur, 0);
+        const TileBounds b = tile_bounds(cur, uread64(T.i0), uread64(T.i1), n);
+        // tile element x: A part (x < na_t) through *A, B part through *B
+        const uint64_t *KA = (const uint64_t *)((const char *)T.key + __builtin_amdgcn_readfirstlane(T.ok[0]));
+        const uint64_t *KB = (const uint64_t *)((const char *)T.key + __builtin_amdgcn_readfirstlane(T.ok[1])) - b.na_t;
+        const uint64_t *TA = (const uint64_t *)((const char *)T.ts + __builtin_amdgcn_readfirstlane(T.ot[0]));
+        const uint64_t *TB = (const uint64_t *)((const char *)T.ts + __builtin_amdgcn_readfirstlane(T.ot[1])) - b.na_t;
+        const uint32_t *RA = (const uint32_t *)((const char *)T.rep + __builtin_amdgcn_readfirstlane(T.orr[0]));
+        const uint32_t *RB = (const uint32_t *)((const char *)T.rep + __builtin_amdgcn_readfirstlane(T.orr[1])) - b.na_t;
+        const uint8_t *tombA = T.tomb + __builtin_amdgcn_readfirstlane(T.om[0]);
+        const uint8_t *tombB = T.tomb + __builtin_amdgcn_readfirstlane(T.om[1]) - b.na_t;
+#define LTAG_A(x) Tag{KA[(x)], TA[(x)], RA[(x)]}
+#define LTAG_B(x) Tag{KB[(x)], TB[(x)], RB[(x)]}
+#define LTAG(x) ((x) < b.na_t ? LTAG_A(x) : LTAG_B(x))
+#define LTOMB(x) ((x) < b.na_t ? tombA[(x)] : tombB[(x)])
+
+        // ---- merge path.  This lane owns merged positions [dd, dd + nv); the
+        // merged tags stay in registers, the two heads are the only LDS reads
+        // per serial step.  (The phase is bound by LDS throughput, not by
+        // latency: an 8-ary search with 7 parallel probes per step was 1.5x
+        // slower than this binary search.)
+        Tag it[SET_ITEMS];
+        uint8_t tbm[SET_ITEMS];
+        const int dd = tid * SET_ITEMS < b.len ? tid * SET_ITEMS : b.len;
+        const int nv = b.len - dd < SET_ITEMS ? b.len - dd : SET_ITEMS;
+        {
+            int lo = dd > b.nb_t ? dd - b.nb_t : 0, hi = dd < b.na_t ? dd : b.na_t;
+            const int jb = b.na_t + dd - 1;   // B index paired with A index i: jb - i
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const uint64_t ka = KA[mid], kb = KB[jb - mid];
+                const bool le = ka != kb ? ka < kb : tag_le(LTAG_A(mid), LTAG_B(jb - mid));
+                if (le) lo = mid + 1;
+                else hi = mid;
+            }
+            int ia = lo, ib = b.na_t + dd - lo;               // tile indices of the heads
+            const int ie = b.na_t, je = b.len;
+            Tag ha = ia < ie ? LTAG_A(ia) : Tag{0, 0, 0};
+            Tag hb_ = ib < je ? LTAG_B(ib) : Tag{0, 0, 0};
 #pragma unroll
-        for (int u = 0; u < ITEMS; ++u) {
+            for (int u = 0; u < SET_ITEMS; ++u) {
+                if (u < nv) {
+                    const bool takeA = ib >= je || (ia < ie && tag_le(ha, hb_));
+                    const int src = takeA ? ia : ib;
+                    it[u] = tag_sel(takeA, ha, hb_);
+                    smi[dd + u] = (uint16_t)src;
+                    tbm[u] = takeA ? tombA[src] : tombB[src];
+                    if (takeA) {
+                        ++ia;
+                        if (ia < ie) ha = LTAG_A(ia);
+                    } else {
+                        ++ib;
+                        if (ib < je) hb_ = LTAG_B(ib);
+                    }
+                } else {
+                    it[u] = Tag{0, 0, 0};
+                    tbm[u] = 0;
+                }
+            }
+        }
+        // wave-edge items for the neighbour exchange (lane 63's last item is
+        // real whenever a next wave has items)
+        const int w = tid >> 6;
+        if (lane == 0) {
+            s_wf_k[w] = it[0].k;
+            s_wf_t[w] = it[0].t;
+            s_wf_r[w] = it[0].r;
+        }
+        if (lane == 63) {
+            s_wl_k[w] = it[SET_ITEMS - 1].k;
+            s_wl_t[w] = it[SET_ITEMS - 1].t;
+            s_wl_r[w] = it[SET_ITEMS - 1].r;
+        }
+        data_barrier(&s_dbar, dgen);                                       // smi, wave edges
+        STAMP(cur, 1);
+
+        // ---- merged neighbours of this lane's run (lane +-1 by shuffles),
+        // emit flags, block count
+        const Tag up{(uint64_t)__shfl_up((unsigned long long)it[SET_ITEMS - 1].k, 1, 64),
+                     (uint64_t)__shfl_up((unsigned long long)it[SET_ITEMS - 1].t, 1, 64),
+                     (uint32_t)__shfl_up((int)it[SET_ITEMS - 1].r, 1, 64)};
+        const Tag dn{(uint64_t)__shfl_down((unsigned long long)it[0].k, 1, 64),
+                     (uint64_t)__shfl_down((unsigned long long)it[0].t, 1, 64),
+                     (uint32_t)__shfl_down((int)it[0].r, 1, 64)};
+        bool hp = false, hn = false;
+        Tag pv{0, 0, 0}, nx{0, 0, 0};
+        if (nv > 0) {
+            if (dd > 0) {
+                pv = lane > 0 ? up : Tag{s_wl_k[w - 1], s_wl_t[w - 1], s_wl_r[w - 1]};
+                hp = true;
+            } else {                          // d0-1 = the later of A[i0-1], B[j0-1] (A first on equal)
+                const Tag a{T.ek[0], T.et[0], T.er[0]}, bb{T.ek[1], T.et[1], T.er[1]};
+                const bool va = T.ev[0] != 0, vb = T.ev[1] != 0;
+                hp = va || vb;
+                pv = tag_sel(va && vb ? tag_le(a, bb) : !va, bb, a);
+            }
+            if (dd + nv < b.len) {
+                nx = lane < 63 ? dn : Tag{s_wf_k[w + 1], s_wf_t[w + 1], s_wf_r[w + 1]};
+                hn = true;
+            } else {                          // d1 = the earlier of A[i1], B[j1]
+                const Tag a{T.ek[2], T.et[2], T.er[2]}, bb{T.ek[3], T.et[3], T.er[3]};
+                const bool va = T.ev[2] != 0, vb = T.ev[3] != 0;
+                hn = va || vb;
+                nx = tag_sel(va && vb ? !tag_le(a, bb) : !va, bb, a);
+            }
+        }
+        // OR: first of a tag run; LWW: last of a key run
+        uint32_t emask = 0;
+#pragma unroll
+        for (int u = 0; u < SET_ITEMS; ++u) {
             if (u < nv) {
-                const bool takeA = ib >= nb_t || (ia < na_t && tag_le(ha, hb));
-                const int src = takeA ? ia : na_t + ib;
-                it[u] = takeA ? ha : hb;
-                smi[dd + u] = (uint16_t)src;
-                tb[u] = stomb[src];
-                if (takeA) {
-                    ++ia;
-                    if (ia < na_t) ha = LTAG(ia);
+                bool emit;
+                if constexpr (MODE == SET_OR) {
+                    emit = u > 0 ? !tag_eq(it[u - 1], it[u]) : !(hp && tag_eq(pv, it[0]));
                 } else {
-                    ++ib;
-                    if (ib < nb_t) hb = LTAG(na_t + ib);
+                    emit = (u + 1 < nv) ? it[u + 1].k != it[u].k : !(hn && nx.k == it[u].k);
                 }
-            } else {
-                it[u] = Tag{0, 0, 0};
-                tb[u] = 0;
+                emask |= emit ? (1u << u) : 0u;
             }
         }
-    }
-    __syncthreads();
-    STAMP(2);
-
-    // ---- neighbours of this lane's run: merged positions dd-1 and dd+nv
-    const Tag eprev{s_edge_k[0], s_edge_t[0], s_edge_r[0]};
-    const Tag enext{s_edge_k[1], s_edge_t[1], s_edge_r[1]};
-    const bool has_prev_edge = s_has[0] != 0, has_next_edge = s_has[1] != 0;
-    bool hp = false, hn = false;
-    Tag pv{0, 0, 0}, nx{0, 0, 0};
-    if (nv > 0) {
-        if (dd > 0) { pv = LTAG(smi[dd - 1]); hp = true; }
-        else if (has_prev_edge) { pv = eprev; hp = true; }
-        if (dd + nv < len) { nx = LTAG(smi[dd + nv]); hn = true; }
-        else if (has_next_edge) { nx = enext; hn = true; }
-    }
-
-    // ---- emit flags from registers (OR: first of a tag run; LWW: last of a key run)
-    uint32_t emask = 0;
+        uint32_t woff;
+        {
+            uint32_t x = (uint32_t)__popc(emask);
 #pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-        if (u < nv) {
-            bool emit;
-            if constexpr (MODE == SET_OR) {
-                emit = u > 0 ? !tag_eq(it[u - 1], it[u]) : !(hp && tag_eq(pv, it[0]));
-            } else {
-                emit = (u + 1 < nv) ? it[u + 1].k != it[u].k : !(hn && nx.k == it[u].k);
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                if (lane >= d) x += y;
             }
-            emask |= emit ? (1u << u) : 0u;
+            woff = x - (uint32_t)__popc(emask);
+            if (lane == 63) s_wsum[w] = x;
         }
-    }
-    uint64_t total;
-    const uint64_t local_off = block_exclusive_scan_u64((uint64_t)__popc(emask), &total);
-    STAMP(3);
-
-    // ---- publish this tile's count now; its successors can look past it
-    // while this tile resolves and stages (the look-back itself comes last)
-    if (tid == 0) st_status(status + t, (t == 0 ? kFlagInc : kFlagAgg) | total);
-
-    // ---- output tombs from registers; runs crossing this lane's edge are rare
-    uint8_t ot[ITEMS];
-    if constexpr (MODE == SET_OR) {
-        // tomb-OR over the run that starts at each emitter (backward sweep)
-        uint8_t carry = 0;
-        Tag last = it[0];                                       // it[nv-1] without a runtime index
+        data_barrier(&s_dbar, dgen);                                       // wave sums
+        STAMP(cur, 2);
+        uint32_t total = 0, local_off = woff;
 #pragma unroll
-        for (int u = 1; u < ITEMS; ++u)
-            if (u < nv) last = it[u];
-        if (nv > 0 && hn && tag_eq(nx, last)) {                 // run continues past this lane
-            const Tag tg = last;
-            int m = dd + nv;
-            while (m < len && tag_eq(LTAG(smi[m]), tg)) carry |= stomb[smi[m++]];
-            if (m == len) {
-                for (size_t x = i1; x < na && tag_eq(gtag(A, x), tg); ++x) carry |= A.tomb[x];
-                for (size_t y = j1; y < nb && tag_eq(gtag(B, y), tg); ++y) carry |= B.tomb[y];
-            }
+        for (int q = 0; q < ND; ++q) {
+            const uint32_t ws = s_wsum[q];
+            total += ws;
+            local_off += (q < w) ? ws : 0;
         }
+        // publish t_k's count (the look-back's aggregate) right away, and
+        // hand it to the look-back wave for t_k's own offset
+        if (tid == 0) {
+            st_status(status + cur, (cur == 0 ? kFlagInc : kFlagAgg) | total);
+            s_tot[k & 3] = total;
+            lds_publish(&s_tot_tag[k & 3], k + 1);
+        }
+        // ---- t_{k-2} out at its offset (coalesced rows)
+        if (held2) {
+            lds_wait(&s_off_tag[(k - 2) & 3], k - 1);
+            const uint64_t P = uread64(s_off[(k - 2) & 3]);
 #pragma unroll
-        for (int u = ITEMS - 1; u >= 0; --u) {
-            if (u < nv) {
-                const bool cont = (u + 1 < nv) ? tag_eq(it[u + 1], it[u]) : true;   // last valid: carry
-                const uint8_t c = (u + 1 < nv) ? (cont ? ot[u + 1] : (uint8_t)0) : carry;
-                ot[u] = (uint8_t)(tb[u] | c);
-            } else {
-                ot[u] = 0;
+            for (int u = 0; u < SET_ITEMS; ++u) {
+                const int x = u * NDL + tid;
+                if (x < (int)held2) {
+                    out.key[P + x] = h2k[u];
+                    out.ts[P + x] = h2t[u];
+                    out.rep[P + x] = h2r[u];
+                    out.tomb[P + x] = h2b[u];
+                }
             }
         }
-    } else {
-        // LWW winner = earliest element carrying the emitter's tag (forward sweep)
-        uint8_t first = 0;
-        if (nv > 0 && hp && tag_eq(pv, it[0])) {                 // tag group began before this lane
-            const Tag tg = it[0];
-            int m = dd - 1;
-            while (m > 0 && tag_eq(LTAG(smi[m - 1]), tg)) --m;
-            first = (dd > 0) ? stomb[smi[m]] : 0;
-            if ((dd == 0 || m == 0) && has_prev_edge && tag_eq(eprev, tg)) {   // ... or before the tile
-                if (i0 > 0 && tag_eq(gtag(A, i0 - 1), tg)) {
-                    size_t x = i0 - 1;
-                    while (x > 0 && tag_eq(gtag(A, x - 1), tg)) --x;
-                    first = A.tomb[x];
+        STAMP(cur, 3);
+
+        // ---- output tombs (runs crossing this lane's edge are rare)
+        uint8_t ot[SET_ITEMS];
+        if constexpr (MODE == SET_OR) {
+            // tomb-OR over the run that starts at each emitter (backward sweep)
+            uint8_t carry = 0;
+            Tag last = it[0];                                       // it[nv-1] without a runtime index
+#pragma unroll
+            for (int u = 1; u < SET_ITEMS; ++u)
+                if (u < nv) last = it[u];
+            if (nv > 0 && hn && tag_eq(nx, last)) {                 // run continues past this lane
+                const Tag tg = last;
+                int m = dd + nv;
+                while (m < b.len && tag_eq(LTAG(smi[m]), tg)) {
+                    carry |= LTOMB(smi[m]);
+                    ++m;
+                }
+                if (m == b.len) {
+                    for (size_t x = b.i1; x < na && tag_eq(gtag(A, x), tg); ++x) carry |= A.tomb[x];
+                    for (size_t y = b.j1; y < nb && tag_eq(gtag(B, y), tg); ++y) carry |= B.tomb[y];
+                }
+            }
+#pragma unroll
+            for (int u = SET_ITEMS - 1; u >= 0; --u) {
+                if (u < nv) {
+                    const bool cont = (u + 1 < nv) ? tag_eq(it[u + 1], it[u]) : true;
+                    const uint8_t c = (u + 1 < nv) ? (cont ? ot[u + 1] : (uint8_t)0) : carry;
+                    ot[u] = (uint8_t)(tbm[u] | c);
                 } else {
-                    size_t y = j0 - 1;
-                    while (y > 0 && tag_eq(gtag(B, y - 1), tg)) --y;
-                    first = B.tomb[y];
+                    ot[u] = 0;
                 }
             }
         } else {
-            first = tb[0];
-        }
+            // LWW winner = earliest element carrying the emitter's tag (forward sweep)
+            uint8_t first = 0;
+            if (nv > 0 && hp && tag_eq(pv, it[0])) {                 // tag group began before this lane
+                const Tag tg = it[0];
+                int m = dd - 1;
+                while (m > 0 && tag_eq(LTAG(smi[m - 1]), tg)) --m;
+                first = (dd > 0) ? LTOMB(smi[m]) : 0;
+                if (dd == 0 || m == 0) {                             // ... or before the tile
+                    if (b.i0 > 0 && tag_eq(gtag(A, b.i0 - 1), tg)) {
+                        size_t x = b.i0 - 1;
+                        while (x > 0 && tag_eq(gtag(A, x - 1), tg)) --x;
+                        first = A.tomb[x];
+                    } else if (b.j0 > 0 && tag_eq(gtag(B, b.j0 - 1), tg)) {
+                        size_t y = b.j0 - 1;
+                        while (y > 0 && tag_eq(gtag(B, y - 1), tg)) --y;
+                        first = B.tomb[y];
+                    }
+                }
+            } else {
+                first = tbm[0];
+            }
 #pragma unroll
-        for (int u = 0; u < ITEMS; ++u) {
-            if (u == 0) ot[0] = first;
-            else ot[u] = (u < nv && tag_eq(it[u - 1], it[u])) ? ot[u - 1] : tb[u];
+            for (int u = 0; u < SET_ITEMS; ++u) {
+                if (u == 0) ot[0] = first;
+                else ot[u] = (u < nv && tag_eq(it[u - 1], it[u])) ? ot[u - 1] : tbm[u];
+            }
         }
-    }
 #undef LTAG
-    __syncthreads();                                          // inputs in LDS are dead from here
-    STAMP(5);
+#undef LTAG_A
+#undef LTAG_B
+#undef LTOMB
+        data_barrier(&s_dbar, dgen);                                       // inputs dead
 
-    // ---- stage the tile's output in LDS at its local offsets, then copy out coalesced
-    {
-        uint32_t o = (uint32_t)local_off;
+        // ---- stage t_k's output in this buffer at its local offsets
+        {
+            uint32_t o = local_off;
 #pragma unroll
-        for (int u = 0; u < ITEMS; ++u) {
-            if (emask & (1u << u)) {
-                skey[o] = it[u].k;
-                sts[o] = it[u].t;
-                srep[o] = it[u].r;
-                stomb[o] = ot[u];
-                ++o;
+            for (int u = 0; u < SET_ITEMS; ++u) {
+                if (emask & (1u << u)) {
+                    T.key[o] = it[u].k;
+                    T.ts[o] = it[u].t;
+                    T.rep[o] = it[u].r;
+                    T.tomb[o] = ot[u];
+                    ++o;
+                }
+            }
+        }
+        data_barrier(&s_dbar, dgen);                                       // staged
+        STAMP(cur, 4);
+        // ---- hold it in registers in copy-out order (written out next iteration)
+#pragma unroll
+        for (int u = 0; u < SET_ITEMS; ++u) {
+            h2k[u] = h1k[u];
+            h2t[u] = h1t[u];
+            h2r[u] = h1r[u];
+            h2b[u] = h1b[u];
+            const int x = u * NDL + tid;
+            if (x < (int)total) {
+                h1k[u] = T.key[x];
+                h1t[u] = T.ts[x];
+                h1r[u] = T.rep[x];
+                h1b[u] = T.tomb[x];
+            }
+        }
+        held2 = held1;
+        held1 = total;
+        data_barrier(&s_dbar, dgen);                                       // staged copy read
+        if (tid == 0) lds_publish(&s_free_tag[bi], k + 1);                 // the loader may refill it
+        STAMP(cur, 5);
+    }
+    // the last two tiles' output (iterations k-2 and k-1)
+    if (held2) {
+        lds_wait(&s_off_tag[(k - 2) & 3], k - 1);
+        const uint64_t P = uread64(s_off[(k - 2) & 3]);
+#pragma unroll
+        for (int u = 0; u < SET_ITEMS; ++u) {
+            const int x = u * NDL + tid;
+            if (x < (int)held2) {
+                out.key[P + x] = h2k[u];
+                out.ts[P + x] = h2t[u];
+                out.rep[P + x] = h2r[u];
+                out.tomb[P + x] = h2b[u];
             }
         }
     }
-    __syncthreads();
-    STAMP(6);
-    // ---- output offset: decoupled look-back by the whole block (1024 predecessors per round trip)
-    uint64_t P = 0;
-    if (t > 0) {
-        P = (ablate & 1) ? 0 : block_look_back(status, t, err, s_fi, s_fv, s_part);
-        if (tid == 0) st_status(status + t, kFlagInc | (P + total));
-    }
-    if (tid == 0 && t == ntiles - 1) *out_count = P + total;
-    STAMP(4);
-    const int T = (int)total;
-    if (!(ablate & 2)) {
+    if (held1) {
+        lds_wait(&s_off_tag[(k - 1) & 3], k);
+        const uint64_t P = uread64(s_off[(k - 1) & 3]);
 #pragma unroll
-        for (int u = 0; u < ITEMS; ++u) {
-            const int x = u * 256 + tid;
-            if (x < T) {
-                out.key[P + x] = skey[x];
-                out.ts[P + x] = sts[x];
-                out.rep[P + x] = srep[x];
-                out.tomb[P + x] = stomb[x];
+        for (int u = 0; u < SET_ITEMS; ++u) {
+            const int x = u * NDL + tid;
+            if (x < (int)held1) {
+                out.key[P + x] = h1k[u];
+                out.ts[P + x] = h1t[u];
+                out.rep[P + x] = h1r[u];
+                out.tomb[P + x] = h1b[u];
             }
         }
-    }
-    if (stamps) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        STAMP(7);
     }
 #undef STAMP
+#undef WSTAMP
 }
 
-uint64_t *g_last_stamps = nullptr;   // diagnostic: stamps of the last set merge (8 per tile)
+size_t g_last_grid = 0;              // diagnostic: persistent grid of the last set merge
+int g_last_occ = 0;
+uint64_t *g_last_stamps = nullptr;   // diagnostic: stamps of the last set merge (16 per tile)
 size_t g_last_stamps_n = 0;
 
 // Adjacent pairs out of (key, ts, rep) order.
@@ -456,17 +754,20 @@ __global__ void k_count_unsorted(crdt_tuples T, size_t n, unsigned long long *ba
     if (c) atomicAdd(bad, c);
 }
 
-template <int MODE, int ITEMS>
+template <int MODE>
 static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
                           const crdt_tuples &O, uint64_t *out_count) {
-    constexpr size_t TILE = 256 * ITEMS;
     const size_t n = na + nb;
     const size_t ntiles = (n + TILE - 1) / TILE;
     if (ntiles >= 0x7fffffffULL || n >= (1ULL << 62)) return CRDT_E_RANGE;
+    // the LDS-DMA copies key/ts/rep in whole dwords: naturally aligned arrays
+    const crdt_tuples *sides[2] = {&A, &B};
+    for (const crdt_tuples *t : sides)
+        if (((uintptr_t)t->key | (uintptr_t)t->ts) & 7 || (uintptr_t)t->rep & 3) return CRDT_E_INVAL;
     // status words + tile counter + error word first (one memset), split after
     const size_t b_status = Carve::round((ntiles + 4) * sizeof(uint64_t));
     const size_t b_split = Carve::round((ntiles + 1) * sizeof(uint64_t));
-    const size_t b_stamps = g_sets_stamps ? Carve::round(ntiles * 8 * sizeof(uint64_t)) : 0;
+    const size_t b_stamps = g_sets_stamps ? Carve::round(ntiles * 16 * sizeof(uint64_t)) : 0;
     int rc = ws_reserve(ctx, b_status + b_split + b_stamps + 768);
     if (rc) return rc;
     Carve w(ctx->ws);
@@ -474,17 +775,35 @@ static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const 
     uint32_t *ctr = (uint32_t *)(status + ntiles);        // status[ntiles]: tile counter + error word
     uint32_t *err = ctr + 1;
     uint64_t *split = w.take<uint64_t>(ntiles + 1);
-    uint64_t *stamps = g_sets_stamps ? w.take<uint64_t>(ntiles * 8) : nullptr;
+    uint64_t *stamps = g_sets_stamps ? w.take<uint64_t>(ntiles * 16) : nullptr;
     g_last_stamps = stamps;
-    g_last_stamps_n = stamps ? ntiles * 8 : 0;
+    g_last_stamps_n = stamps ? ntiles * 16 : 0;
     const hipStream_t s = ctx->stream;
     hipError_t e = hipMemsetAsync(status, 0, b_status, s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     const size_t diags = ntiles + 1;                      // 4 diagonals per wave, 16 per block
     k_partition<<<(unsigned)((diags + 15) / 16), 256, 0, s>>>(A, B, na, nb, TILE, ntiles, split);
-    k_set_merge<MODE, ITEMS><<<(unsigned)ntiles, 256, 0, s>>>(A, B, na, nb, split, status, ctr, err,
-                                                              (uint32_t)ntiles, g_sets_ablate, O, out_count,
-                                                              stamps);
+    // persistent grid: CUs x the occupancy query (tiles are claimed
+    // dynamically, so a workgroup that is not resident owns nothing and any
+    // grid is correct; a spilling build is refused: its scratch traffic
+    // would defeat the design)
+    static int occ = 0;
+    if (occ == 0) {
+        hipFuncAttributes fa{};
+        e = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_set_merge<MODE>));
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_set_merge<MODE>, SET_BLOCK, 0);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        if (fa.localSizeBytes != 0 || occ < 1) {
+            occ = 0;
+            return CRDT_E_RANGE;
+        }
+    }
+    const int per_cu = g_sets_grid_per_cu > 0 ? g_sets_grid_per_cu : occ;
+    const size_t grid = std::min(ntiles, (size_t)ctx->num_cus * (size_t)per_cu);
+    g_last_grid = grid;
+    g_last_occ = occ;
+    k_set_merge<MODE><<<(unsigned)grid, SET_BLOCK, 0, s>>>(A, B, na, nb, split, status, ctr, err, (uint32_t)ntiles,
+                                                           O, out_count, stamps, g_sets_diag);
     return check_launch(ctx);
 }
 
@@ -504,8 +823,7 @@ static int set_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
     crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples &A = na ? *a : empty;
     const crdt_tuples &B = nb ? *b : empty;
-    if (g_sets_items == 4) return set_merge_impl<MODE, 4>(ctx, A, na, B, nb, *out, out_count);
-    return set_merge_impl<MODE, 8>(ctx, A, na, B, nb, *out, out_count);
+    return set_merge_impl<MODE>(ctx, A, na, B, nb, *out, out_count);
 }
 
 }  // namespace crdt
@@ -522,8 +840,8 @@ extern "C" int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, 
     return set_merge<SET_OR>(ctx, a, na, b, nb, out, out_count_dev);
 }
 
-// Diagnostic: copy the phase stamps of the last set merge (8 s_memtime values
-// per tile) to host memory.  Enabled by crdt_set_option("sets.stamps", 1).
+// Diagnostic: copy the phase stamps of the last set merge (16 values per
+// tile: 8 data-wave phase stamps, then control-wave stamps / counters) to host memory.  Enabled by crdt_set_option("sets.stamps", 1).
 extern "C" int crdt_debug_set_stamps(crdt_ctx *ctx, uint64_t *host, size_t cap, size_t *n) {
     int rc = bind(ctx);
     if (rc) return rc;
@@ -534,6 +852,14 @@ extern "C" int crdt_debug_set_stamps(crdt_ctx *ctx, uint64_t *host, size_t cap, 
     hipError_t e = hipMemcpyAsync(host, g_last_stamps, m * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+
+// Diagnostic: grid size and occupancy-query answer of the last set merge.
+extern "C" int crdt_debug_set_grid(size_t *grid, int *occ) {
+    if (!grid || !occ) return CRDT_E_INVAL;
+    *grid = g_last_grid;
+    *occ = g_last_occ;
+    return CRDT_OK;
 }
 
 extern "C" int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n, uint64_t *bad) {

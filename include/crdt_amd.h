@@ -66,7 +66,8 @@ int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
 /* Kernel tuning knobs (process-wide), for A/B runs: "join.unroll" (1,2,4,8),
  * "join.nontemporal" (0/1), "join.blocks_per_cu" (1..64),
- * "vclock.pairs_per_wave" (1,2,4,8), "sets.items" (4,8).
+ * "vclock.pairs_per_wave" (1,2,4,8), "sets.grid_per_cu" (0 = occupancy query);
+ * diagnostics: "sets.stamps" (0/1), "sets.diag_no_lookback" (0/1, WRONG output).
  * Returns CRDT_E_INVAL for an unknown name or value. */
 int crdt_set_option(const char *name, int64_t value);
 
@@ -144,6 +145,8 @@ int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
  * records 8 s_memtime stamps per tile at its phase boundaries; copies
  * min(cap, *n) of them to host memory. */
 int crdt_debug_set_stamps(crdt_ctx *ctx, uint64_t *host, size_t cap, size_t *n);
+/* Diagnostic: persistent grid size and occupancy answer of the last set merge. */
+int crdt_debug_set_grid(size_t *grid, int *occ);
 
 /* ------------------------------------------------ RefMerge (a1-a5)
  * Batched, bit-exact (*Server).merge() (main.go:35-100) for many replicas.

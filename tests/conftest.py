@@ -18,5 +18,11 @@ def eng():
     from crdt_amd.engine import Engine
     assert torch.cuda.is_available(), "gpu-marked test without a GPU"
     e = Engine(0)
+    # CRDT_TEST_OPTIONS="sets.grid_per_cu=1,join.unroll=2": run the GPU suite
+    # under non-default kernel knobs (crdt_set_option)
+    from crdt_amd import _lib
+    for opt in filter(None, os.environ.get("CRDT_TEST_OPTIONS", "").split(",")):
+        k, v = opt.split("=")
+        _lib.call("crdt_set_option", k.strip().encode(), int(v))
     yield e
     e.close()

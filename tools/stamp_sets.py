@@ -18,12 +18,15 @@ from crdt_amd import _lib  # noqa: E402
 from crdt_amd.engine import Engine, TupleSet  # noqa: E402
 
 # stamp index pairs per phase, in kernel order (see STAMP(i) in csrc/sets.hip)
-PAIRS = {"load+edges": (0, 1), "rank-merge": (1, 2), "emit+scan": (2, 3), "resolve": (3, 5),
-         "stage": (5, 6), "look-back": (6, 4), "store": (4, 7)}
+PAIRS = {"merge": (0, 1), "emit+scan": (1, 2), "copy-out k-1": (2, 3), "resolve+stage": (3, 4),
+         "hold+release": (4, 5)}
 
 
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "lww"
+    for opt in sys.argv[2:]:                      # name=value kernel knobs
+        k, v = opt.split("=")
+        _lib.call("crdt_set_option", k.encode(), int(v))
     n, ks = 10_000_000, 8_000_000
     eng = Engine(0)
     A = eng.synth_set_tuples(2024, 0, n, ks)
@@ -41,14 +44,24 @@ def main():
     buf = np.zeros(m.value, dtype=np.uint64)
     _lib.call("crdt_debug_set_stamps", eng.ctx, buf.ctypes.data, m.value, C.byref(m))
     _lib.call("crdt_set_option", b"sets.stamps", 0)
-    st = buf.reshape(-1, 8).astype(np.int64)
+    g, o = C.c_size_t(), C.c_int()
+    _lib.call("crdt_debug_set_grid", C.byref(g), C.byref(o))
+    print(f"grid {g.value} workgroups (occupancy query {o.value} per CU)")
+    st = buf.reshape(-1, 16).astype(np.int64)
     print(f"{mode}: tiles={st.shape[0]}")
     for p, (a, b) in PAIRS.items():
         d = st[:, b] - st[:, a]
         print(f"  {p:12s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f} cycles")
-    tot = st[:, 7] - st[:, 0]
+    lb = st[:, 9] - st[:, 8]
+    print(f"  {'ctl look-back':12s} median {np.median(lb):9.0f}  p90 {np.percentile(lb, 90):9.0f} cycles; "
+          f"rounds median {np.median(st[:, 11]):.0f} max {st[:, 11].max()}, spinning rounds median "
+          f"{np.median(st[:, 10]):.0f} p90 {np.percentile(st[:, 10], 90):.0f}")
+    for nm, (x, y) in {"loader DMA": (12, 13)}.items():
+        d = st[:, y] - st[:, x]
+        print(f"  {nm:12s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}")
+    tot = st[:, 5] - st[:, 0]
     print(f"  {'total':12s} median {np.median(tot):9.0f}  p90 {np.percentile(tot, 90):9.0f}")
-    span = st[:, 7].max() - st[:, 0].min()
+    span = st[:, 5].max() - st[:, 0].min()
     print(f"  kernel span {span} cycles; sum(tile)/span = {tot.sum() / span:.1f} tiles in flight on average")
 
 
