@@ -65,6 +65,8 @@ __device__ __forceinline__ bool g_le_lazy(const crdt_tuples &A, size_t i, const 
 // ---------------------------------------------------------------- partition
 // split[t] = number of A elements among the first min(t*TILE, n) merged
 // elements.  P(i) = A[i] <= B[d-1-i] is true for i < answer, false after.
+// (One diagonal per wave with 64 probes per round was 2x slower: four times
+// the waves, and a key tie in any lane stalls the whole wave's round.)
 __global__ __launch_bounds__(256) void k_partition(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
                                                    size_t tile, size_t ntiles, uint64_t *__restrict__ split) {
     const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
@@ -462,7 +464,9 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
         // merged tags stay in registers, the two heads are the only LDS reads
         // per serial step.  (The phase is bound by LDS throughput, not by
         // latency: an 8-ary search with 7 parallel probes per step was 1.5x
-        // slower than this binary search.)
+        // slower than this binary search.  Writing the output straight from
+        // these registers, without the LDS staging below, was 1.2x slower:
+        // per-lane runs make each store instruction touch many lines.)
         Tag it[SET_ITEMS];
         uint8_t tbm[SET_ITEMS];
         const int dd = tid * SET_ITEMS < b.len ? tid * SET_ITEMS : b.len;

@@ -18,7 +18,7 @@ from crdt_amd import _lib  # noqa: E402
 from crdt_amd.engine import Engine, TupleSet  # noqa: E402
 
 # stamp index pairs per phase, in kernel order (see STAMP(i) in csrc/sets.hip)
-PAIRS = {"merge": (0, 1), "emit+scan": (1, 2), "copy-out k-1": (2, 3), "resolve+stage": (3, 4),
+PAIRS = {"merge": (0, 1), "emit+scan": (1, 2), "copy-out k-2": (2, 3), "resolve+stage": (3, 4),
          "hold+release": (4, 5)}
 
 
