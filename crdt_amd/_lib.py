@@ -88,6 +88,7 @@ SIGNATURES = {
     "crdt_stream_create": (_I, [_I, C.POINTER(_P)]),
     "crdt_stream_destroy": (_I, [_P]),
     "crdt_ctx_sync": (_I, [_CTX]),
+    "crdt_ctx_device_status": (_I, [_CTX, C.POINTER(C.c_uint32), C.c_int]),
     "crdt_ctx_last_hip_error": (_I, [_CTX]),
     "crdt_ctx_reserve": (_I, [_CTX, _SZ]),
     "crdt_set_option": (_I, [C.c_char_p, C.c_int64]),

@@ -81,6 +81,13 @@ extern "C" int crdt_ctx_create(int device, void *stream, crdt_ctx **out) {
     // current stream reports as cuda_stream == 0 -- never a private stream:
     // work must stay ordered with the caller's copies on that stream.
     ctx->stream = (hipStream_t)stream;
+    hipError_t e = hipMalloc((void **)&ctx->dev_status, 256);
+    if (e == hipSuccess) e = hipMemset(ctx->dev_status, 0, 256);
+    if (e != hipSuccess) {
+        if (ctx->dev_status) (void)hipFree(ctx->dev_status);
+        delete ctx;
+        return e == hipErrorOutOfMemory ? CRDT_E_NOMEM : CRDT_E_HIP;
+    }
     *out = ctx;
     return CRDT_OK;
 }
@@ -115,6 +122,7 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->io) (void)hipFree(ctx->io);
+    if (ctx->dev_status) (void)hipFree(ctx->dev_status);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return CRDT_OK;
@@ -128,6 +136,19 @@ extern "C" int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream) {
         ctx->own_stream = false;
     }
     ctx->stream = (hipStream_t)stream;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_ctx_device_status(crdt_ctx *ctx, uint32_t *flags, int clear) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!flags) return CRDT_E_INVAL;
+    uint32_t v = 0;
+    hipError_t e = hipMemcpyAsync(&v, ctx->dev_status, sizeof(v), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess && clear && v) e = hipMemsetAsync(ctx->dev_status, 0, sizeof(v), ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    *flags = v;
     return CRDT_OK;
 }
 

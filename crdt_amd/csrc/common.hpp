@@ -17,6 +17,7 @@ struct crdt_ctx {
     size_t ws_bytes = 0;
     void *io = nullptr;      // device staging for host-facing calls (crdt_server_*)
     size_t io_bytes = 0;
+    uint32_t *dev_status = nullptr;   // device-side failure flags (CRDT_DEV_*), read by crdt_ctx_device_status
 };
 
 namespace crdt {

@@ -141,7 +141,7 @@ __device__ uint64_t wave_look_back(const uint64_t *status, uint32_t t, uint32_t 
         if (fv < fi) {                               // a nearer predecessor has not published yet
             if (nspin) ++*nspin;
             if (++spins > (1u << 22)) {
-                if (lane == 0) atomicOr(err, 1u);
+                if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -768,7 +768,7 @@ static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const 
     const crdt_tuples *sides[2] = {&A, &B};
     for (const crdt_tuples *t : sides)
         if (((uintptr_t)t->key | (uintptr_t)t->ts) & 7 || (uintptr_t)t->rep & 3) return CRDT_E_INVAL;
-    // status words + tile counter + error word first (one memset), split after
+    // status words + tile counter first (one memset), split after
     const size_t b_status = Carve::round((ntiles + 4) * sizeof(uint64_t));
     const size_t b_split = Carve::round((ntiles + 1) * sizeof(uint64_t));
     const size_t b_stamps = g_sets_stamps ? Carve::round(ntiles * 16 * sizeof(uint64_t)) : 0;
@@ -776,8 +776,8 @@ static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const 
     if (rc) return rc;
     Carve w(ctx->ws);
     uint64_t *status = w.take<uint64_t>(ntiles + 4);
-    uint32_t *ctr = (uint32_t *)(status + ntiles);        // status[ntiles]: tile counter + error word
-    uint32_t *err = ctr + 1;
+    uint32_t *ctr = (uint32_t *)(status + ntiles);        // status[ntiles]: tile counter
+    uint32_t *err = ctx->dev_status;                      // CRDT_DEV_LOOKBACK (crdt_ctx_device_status)
     uint64_t *split = w.take<uint64_t>(ntiles + 1);
     uint64_t *stamps = g_sets_stamps ? w.take<uint64_t>(ntiles * 16) : nullptr;
     g_last_stamps = stamps;

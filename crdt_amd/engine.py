@@ -119,6 +119,18 @@ class Engine:
     def sync(self) -> None:
         self._call("crdt_ctx_sync")
 
+    def device_status(self, clear: bool = True) -> int:
+        """Kernel-raised failure flags (CRDT_DEV_*) since the last clear; syncs."""
+        v = C.c_uint32()
+        self._call("crdt_ctx_device_status", C.byref(v), 1 if clear else 0)
+        return v.value
+
+    def check_device(self) -> None:
+        """Raise if a kernel reported a device-side failure (its output is invalid)."""
+        flags = self.device_status(clear=True)
+        if flags:
+            raise _lib.CrdtLibraryError(f"device-side failure flags 0x{flags:x} (CRDT_DEV_*): output invalid")
+
     def reserve(self, nbytes: int) -> None:
         self._call("crdt_ctx_reserve", nbytes)
 
@@ -195,7 +207,8 @@ class Engine:
             self._check(s.tomb, itemsize=1)
         ca, cb, co = a.c(), b.c(), out.c()
         self._call(fn, C.byref(ca), na, C.byref(cb), nb, C.byref(co), count.data_ptr())
-        if trim:
+        if trim:                              # synchronises anyway: check the look-back's flag too
+            self.check_device()
             return out.slice(int(count.item()))
         return out, count
 

@@ -60,6 +60,13 @@ int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream);
 int crdt_stream_create(int device, void **stream);
 int crdt_stream_destroy(void *stream);
 int crdt_ctx_sync(crdt_ctx *ctx);
+/* Device-side failure flags raised by kernels since the last clear (the
+ * kernels cannot return an error): synchronises the context's stream, then
+ * *flags = CRDT_DEV_* bits; clear != 0 resets them.  A set merge whose
+ * decoupled look-back exceeded its bounded wait (a scheduling fault, never
+ * expected) raises CRDT_DEV_LOOKBACK and its output is invalid. */
+#define CRDT_DEV_LOOKBACK 1u
+int crdt_ctx_device_status(crdt_ctx *ctx, uint32_t *flags, int clear);
 int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 /* Pre-size the context's device workspace so that later calls never
  * allocate (needed before graph capture). */
