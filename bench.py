@@ -282,7 +282,7 @@ class RefMergeBatch(Workload):
     name = "refmerge"
     unit = "remote-entries/s"
     dtype = "int64"
-    kernel = "k_replay"
+    kernel = "refmerge (whole op: walk, scan, scatters, replay)"
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         from crdt_amd import refmerge, synth

@@ -16,8 +16,12 @@
 //    as parallel atomics instead of the reference's serial descending loop.
 //
 // Kernels: atoi over the string arena; walk flags (binary search per R
-// entry); device scan of the flags; L and R scatters into the new Diff; slot
-// accumulate (atomicMax ts, atomicAdd sum/count); base pick; finalize.
+// entry); device scan of the flags; L and R scatters into the new Diff;
+// per-replica replay over the new Diff with LDS accumulators (k_replay).
+// (Workgroup-per-replica and chunk-parallel walk/scatter variants measured
+// no faster: every variant is bound by chains of dependent global loads.)
+#include <algorithm>
+
 #include "scan.hpp"
 
 namespace crdt {
@@ -116,84 +120,155 @@ __global__ void k_scatter_r(crdt_refmerge_in in, const uint32_t *__restrict__ fl
     }
 }
 
-struct SlotAcc {
-    long long *maxts;
+// ---------------------------------------------------------------- replay
+// One workgroup per replica, over the replica's NEW Diff (already written by
+// the scatters, ascending ts): an entry's position o in it orders the
+// entries by ts, so the base holder of a key (its max-ts entry) is the one
+// with the largest (o << 32 | string id) -- a single 64-bit max, reduced in
+// the same pass as the sums and counts.  The per-key accumulators live in an
+// LDS hash table (slots of different replicas are disjoint, so the workgroup
+// owns every slot it touches: no global atomics); a replica with more
+// distinct keys than the table holds is redone by the same workgroup through
+// its slice of slot-indexed global accumulators.  (Four contended global
+// atomics per key plus a second base pass took 4x longer; chunk-parallel
+// workgroups with a table flush were 1.4x slower than this.)
+constexpr int RT = 1024;                  // LDS table entries per workgroup
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+struct SlotAcc {                          // global fallback, indexed by slot
+    unsigned long long *best;
     unsigned *nent;
     unsigned long long *sum;
     unsigned *npar;
-    uint32_t *base;
 };
 
-__global__ void k_slot_init(SlotAcc acc, uint32_t n) {
+__global__ void k_slot_clear(crdt_refmerge_out out, SlotAcc acc, uint32_t n) {
     for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
-        acc.maxts[s] = (long long)0x8000000000000000ULL;
+        out.st_kind[s] = 0;               // untouched slot: key absent from CurrentState
+        out.st_str[s] = 0;
+        out.st_sum[s] = 0;
+        acc.best[s] = 0;
         acc.nent[s] = 0;
         acc.sum[s] = 0;
         acc.npar[s] = 0;
-        acc.base[s] = 0;
     }
 }
 
-// Entry e in [0, n_l + n_r): L entries first, then R entries.  Remote-origin
-// entries of the new Diff only: L entries with origin 0, included R entries.
-template <bool BASE>
-__global__ void k_replay(crdt_refmerge_in in, const uint32_t *__restrict__ flag, const uint8_t *__restrict__ ok,
-                         const int64_t *__restrict__ val, SlotAcc acc) {
-    const uint64_t n = in.n_l + in.n_r;
-    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256) {
-        int64_t ts;
-        uint64_t kb, ke;
-        if (e < in.n_l) {
-            if (in.l_origin[e]) continue;                // *Command: skipped (main.go:80)
-            ts = in.l_ts[e];
-            kb = in.l_kv[e];
-            ke = in.l_kv[e + 1];
-        } else {
-            const uint64_t g = e - in.n_l;
-            if (!flag[g]) continue;                      // not in the new Diff
-            ts = in.r_ts[g];
-            kb = in.r_kv[g];
-            ke = in.r_kv[g + 1];
+// kv range of new-Diff entry o, clamped to the arena
+__device__ __forceinline__ void entry_kv(const crdt_refmerge_in &in, const crdt_refmerge_out &out, uint64_t o,
+                                         uint64_t *kb, uint64_t *ke) {
+    const int64_t src = out.src[o];
+    if (src >= 0) {
+        *kb = in.l_kv[src];
+        *ke = in.l_kv[src + 1];
+    } else {
+        const uint64_t g = (uint64_t)(-(src + 1));
+        *kb = in.r_kv[g];
+        *ke = in.r_kv[g + 1];
+    }
+    if (*ke > in.n_kv) *ke = in.n_kv;     // malformed ranges never read out of bounds
+}
+
+// Per-key closed form (main.go:82-96): verbatim base unless the base parses
+// AND another holder's value parses; then Itoa(sum) with int64 wrap.
+__device__ __forceinline__ void slot_final(const crdt_refmerge_out &out, const uint8_t *ok, uint32_t slot,
+                                           unsigned long long best, unsigned npar, unsigned long long sum) {
+    const uint32_t str = (uint32_t)best;
+    const bool sum_form = ok[str] && npar >= 2;
+    out.st_kind[slot] = sum_form ? 2 : 1;
+    out.st_str[slot] = str;
+    out.st_sum[slot] = sum_form ? (int64_t)sum : 0;
+}
+
+__global__ __launch_bounds__(256) void k_replay(crdt_refmerge_in in, const uint8_t *__restrict__ ok,
+                                                const int64_t *__restrict__ val, crdt_refmerge_out out,
+                                                SlotAcc acc) {
+    __shared__ uint32_t t_slot[RT];
+    __shared__ unsigned long long t_best[RT];
+    __shared__ unsigned long long t_sum[RT];
+    __shared__ uint32_t t_nent[RT], t_npar[RT];
+    __shared__ int s_over;
+    const int tid = threadIdx.x;
+    for (uint32_t p = blockIdx.x; p < in.replicas; p += gridDim.x) {
+        for (int h = tid; h < RT; h += 256) {
+            t_slot[h] = kEmpty;
+            t_best[h] = 0;
+            t_sum[h] = 0;
+            t_nent[h] = 0;
+            t_npar[h] = 0;
         }
-        if (ke > in.n_kv) ke = in.n_kv;                  // malformed ranges never read out of bounds
-        for (uint64_t q = kb; q < ke; ++q) {
-            const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
-            if (slot >= in.n_slots || v >= in.n_str) continue;
-            if constexpr (!BASE) {
-                atomicMax(&acc.maxts[slot], (long long)ts);
-                atomicAdd(&acc.nent[slot], 1u);
-                if (ok[v]) {
-                    atomicAdd(&acc.sum[slot], (unsigned long long)val[v]);   // mod 2^64 (main.go:95)
-                    atomicAdd(&acc.npar[slot], 1u);
+        if (tid == 0) s_over = 0;
+        __syncthreads();
+        const uint64_t ob = out.off[p], oe = out.off[p + 1];
+        for (uint64_t o = ob + tid; o < oe; o += 256) {
+            if (out.origin[o]) continue;                 // *Command: skipped (main.go:80)
+            uint64_t kb, ke;
+            entry_kv(in, out, o, &kb, &ke);
+            const unsigned long long pos = (unsigned long long)(o - ob) << 32;
+            for (uint64_t q = kb; q < ke; ++q) {
+                const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
+                if (slot >= in.n_slots || v >= in.n_str) continue;
+                uint32_t h = (slot * 2654435761u) >> 22;   // 10-bit hash
+                int idx = -1;
+                for (int probe = 0; probe < 32; ++probe, h = (h + 1) & (RT - 1)) {
+                    const uint32_t c = atomicCAS(&t_slot[h], kEmpty, slot);
+                    if (c == kEmpty || c == slot) {
+                        idx = (int)h;
+                        break;
+                    }
                 }
-            } else {
-                // ts are unique per replica and slots are per replica: one writer
-                if (__hip_atomic_load(&acc.maxts[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ts)
-                    acc.base[slot] = v;
+                if (idx < 0) {
+                    s_over = 1;
+                    continue;
+                }
+                atomicMax(&t_best[idx], pos | v);
+                atomicAdd(&t_nent[idx], 1u);
+                if (ok[v]) {
+                    atomicAdd(&t_sum[idx], (unsigned long long)val[v]);   // mod 2^64 (main.go:95)
+                    atomicAdd(&t_npar[idx], 1u);
+                }
             }
         }
-    }
-}
-
-__global__ void k_slot_final(SlotAcc acc, uint32_t n, const uint8_t *__restrict__ ok, crdt_refmerge_out out) {
-    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
-        uint8_t kind = 0;
-        uint32_t str = 0;
-        int64_t sum = 0;
-        if (acc.nent[s]) {
-            str = acc.base[s];
-            const bool base_ok = ok[str];
-            // verbatim unless the base parses AND another holder's value parses
-            if (base_ok && acc.npar[s] >= 2) {
-                kind = 2;
-                sum = (int64_t)acc.sum[s];
-            } else {
-                kind = 1;
+        __syncthreads();
+        if (!s_over) {
+            for (int h = tid; h < RT; h += 256)
+                if (t_slot[h] != kEmpty) slot_final(out, ok, t_slot[h], t_best[h], t_npar[h], t_sum[h]);
+        } else {
+            // too many distinct keys for the table: this replica again through
+            // its own (disjoint) slice of the global accumulators
+            for (uint64_t o = ob + tid; o < oe; o += 256) {
+                if (out.origin[o]) continue;
+                uint64_t kb, ke;
+                entry_kv(in, out, o, &kb, &ke);
+                const unsigned long long pos = (unsigned long long)(o - ob) << 32;
+                for (uint64_t q = kb; q < ke; ++q) {
+                    const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
+                    if (slot >= in.n_slots || v >= in.n_str) continue;
+                    atomicMax(&acc.best[slot], pos | v);
+                    atomicAdd(&acc.nent[slot], 1u);
+                    if (ok[v]) {
+                        atomicAdd(&acc.sum[slot], (unsigned long long)val[v]);
+                        atomicAdd(&acc.npar[slot], 1u);
+                    }
+                }
+            }
+            __threadfence();
+            __syncthreads();
+            for (uint64_t o = ob + tid; o < oe; o += 256) {
+                if (out.origin[o]) continue;
+                uint64_t kb, ke;
+                entry_kv(in, out, o, &kb, &ke);
+                for (uint64_t q = kb; q < ke; ++q) {
+                    const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
+                    if (slot >= in.n_slots || v >= in.n_str) continue;
+                    slot_final(out, ok, slot,
+                               __hip_atomic_load(&acc.best[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __hip_atomic_load(&acc.npar[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __hip_atomic_load(&acc.sum[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                }
             }
         }
-        out.st_kind[s] = kind;
-        out.st_str[s] = str;
-        out.st_sum[s] = sum;
+        __syncthreads();                                 // table reused by the next replica
     }
 }
 
@@ -231,7 +306,7 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
     const size_t nr = in.n_r, ns = in.n_slots, nstr = in.n_str;
     const size_t need = Carve::round((nr + 1) * 4) + Carve::round(nr * 8 + 8) + Carve::round((nr + 1) * 8) +
                         scan_tmp_bytes(nr) + Carve::round(nstr + 1) + Carve::round(nstr * 8 + 8) +
-                        Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) * 3 + 4096;
+                        Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) * 2 + 4096;
     rc = ws_reserve(ctx, need);
     if (rc) return rc;
     Carve w(ctx->ws);
@@ -242,11 +317,10 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
     uint8_t *ok = w.take<uint8_t>(nstr + 1);
     int64_t *val = w.take<int64_t>(nstr + 1);
     SlotAcc acc;
-    acc.maxts = w.take<long long>(ns + 1);
+    acc.best = w.take<unsigned long long>(ns + 1);
     acc.sum = w.take<unsigned long long>(ns + 1);
     acc.nent = w.take<unsigned>(ns + 1);
     acc.npar = w.take<unsigned>(ns + 1);
-    acc.base = w.take<uint32_t>(ns + 1);
 
     const hipStream_t s = ctx->stream;
     const unsigned cap = (unsigned)ctx->num_cus * 8;
@@ -260,13 +334,9 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
     if (in.n_l) k_scatter_l<<<grid_for(in.n_l, 256, cap), 256, 0, s>>>(in, ib, out);
     if (nr) k_scatter_r<<<grid_for(nr, 256, cap), 256, 0, s>>>(in, flag, rpos, ib, out);
     if (ns) {
-        k_slot_init<<<grid_for(ns, 256, cap), 256, 0, s>>>(acc, (uint32_t)ns);
-        const size_t ne = in.n_l + nr;
-        if (ne) {
-            k_replay<false><<<grid_for(ne, 256, cap), 256, 0, s>>>(in, flag, ok, val, acc);
-            k_replay<true><<<grid_for(ne, 256, cap), 256, 0, s>>>(in, flag, ok, val, acc);
-        }
-        k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(acc, (uint32_t)ns, ok, out);
+        k_slot_clear<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, (uint32_t)ns);
+        if (in.n_l + nr) k_replay<<<std::min<unsigned>(in.replicas, (unsigned)ctx->num_cus * 4), 256, 0, s>>>(
+            in, ok, val, out, acc);
     }
     return check_launch(ctx);
 }

@@ -139,3 +139,29 @@ def test_device_atoi_matches_go(eng):
                              torch.from_numpy(off).to(eng.device))
     for c, o, v in zip(cases, ok.cpu().tolist(), val.cpu().tolist()):
         assert (bool(o), v if o else 0) == oracle.go_atoi(c), c
+
+
+def test_many_keys_per_replica_matches_oracle(eng):
+    """Replicas with ~2500 distinct keys overflow the replay's 1024-entry LDS
+    table and take the per-replica global-accumulator path; mixed in one
+    batch with small replicas that stay in LDS."""
+    rng = np.random.default_rng(5)
+    reps = []
+    for r, nkeys in enumerate((2500, 40, 3000)):
+        diff, remote, ts = {}, {}, 0
+        for _ in range(4000):
+            ts += int(rng.integers(1, 4))
+            m = {}
+            for _ in range(int(rng.integers(1, 4))):
+                v = int(rng.integers(-50, 50))
+                m[f"key{int(rng.integers(0, nkeys))}"] = str(v) if rng.random() > 0.05 else f"x{v}"
+            if rng.random() < 0.5:
+                diff[ts] = Command(m) if rng.random() < 0.3 else m
+            else:
+                remote[ts] = m
+        reps.append((diff, remote))
+    res = refmerge.merge_batch(eng, reps)
+    for (diff, remote), (d_gpu, s_gpu) in zip(reps, res):
+        d_or, s_or = oracle_merge(diff, remote)
+        assert list(d_gpu) == list(d_or)
+        assert s_gpu == s_or
