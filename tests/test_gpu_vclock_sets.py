@@ -124,3 +124,29 @@ def test_sets_full_config_d(eng):
         for g, e in zip(got, exp):
             np.testing.assert_array_equal(g, e)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("na,nb", [(1535, 1), (1536, 1536), (1537, 1535), (3071, 3073), (4608, 0), (0, 4609)])
+def test_sets_tile_boundaries(eng, na, nb):
+    """Sizes around the 1536-element merge tile."""
+    _check(eng, *_sets(900 + na + nb, na, nb, max(1, (na + nb) // 3)))
+
+
+@pytest.mark.parametrize("off_a,off_b", [(1, 0), (3, 5), (7, 2), (13, 11)])
+def test_sets_unaligned_views(eng, off_a, off_b):
+    """Inputs that start mid-allocation: every segment the LDS-DMA loader
+    copies then begins off a 16-byte boundary (and tombs off a 4-byte one)."""
+    n = 20_000
+    sa = _sets(41 + off_a, n + off_a, 0, 9_000)[0]
+    sb = _sets(43 + off_b, n + off_b, 0, 9_000)[0]
+    Afull = TupleSet.from_numpy(*sa, eng.device)
+    Bfull = TupleSet.from_numpy(*sb, eng.device)
+    A = TupleSet(Afull.key[off_a:], Afull.ts[off_a:], Afull.rep[off_a:], Afull.tomb[off_a:])
+    B = TupleSet(Bfull.key[off_b:], Bfull.ts[off_b:], Bfull.rep[off_b:], Bfull.tomb[off_b:])
+    ha = tuple(x[off_a:] for x in sa)
+    hb = tuple(x[off_b:] for x in sb)
+    for fn, ref in ((eng.lww_merge, oracle.lww_merge), (eng.orset_merge, oracle.orset_merge)):
+        got = fn(A, B).to_numpy()
+        exp = ref(ha, hb)
+        for g, e, f in zip(got, exp, ("key", "ts", "rep", "tomb")):
+            np.testing.assert_array_equal(g, e, err_msg=f"{fn.__name__}.{f}")
