@@ -138,7 +138,7 @@ class GCounterJoin(Workload):
 
 class PNCounterJoin(GCounterJoin):
     name = "pncounter_join"
-    kernel = "k_join_pn"
+    kernel = "k_join (P pass, N pass)"
 
     def __init__(self, eng, rank, world, rows, nodes, seed=2024):
         super().__init__(eng, rank, world, rows, nodes, seed)
@@ -277,6 +277,49 @@ class ShardFold(Workload):
         return None
 
 
+class ShardJoin(Workload):
+    """configs[4] E2: every rank holds a DIVERGENT full copy of the
+    [rows, nodes] counter state; the join is one RCCL all-reduce(MAX) over
+    xGMI (uint64 through the order-preserving map x ^ 2^63, crdt_amd.shard).
+    The bound is xGMI, reported as bus bandwidth 2(G-1)/G * S / t."""
+    name = "shard_join"
+    unit = "replica-merges/s"
+    kernel = "RCCL all-reduce(max) + 2 order-map passes"
+
+    def __init__(self, eng, rank, world, rows, nodes, seed=2024):
+        self.eng, self.world, self.rows, self.nodes = eng, world, rows, nodes
+        self.state = eng.synth_counters(seed, 100 + rank, rows, nodes)    # divergent per rank
+        self.buf = torch.empty_like(self.state)
+        self.config = {"workload": f"divergent full-state join, {rows} replicas x {nodes} nodes uint64 "
+                                   f"({rows * nodes * 8 / 1e9:.3f} GB) per rank, all-reduce(max) "
+                                   "(BASELINE configs[4], E2)" + ("" if world > 1 else "; single rank: no exchange"),
+                       "rows": rows, "nodes": nodes, "parallelism": f"state-replica x{world} + RCCL all-reduce(max)"}
+
+    def units(self):
+        return self.rows            # each rank's copy of every replica row merged once per step
+
+    def bytes_per_launch(self):
+        return 4 * self.rows * self.nodes * 8   # the two order-map passes (read + write each)
+
+    def step(self):
+        self.eng.u64_to_ordered_i64(self.state, out=self.buf)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.buf, op=dist.ReduceOp.MAX)
+        self.eng.ordered_i64_to_u64(self.buf, out=self.state)
+
+    def extra(self, avg_ms):
+        S = self.rows * self.nodes * 8
+        g = self.world
+        bus = 2 * (g - 1) / g * S / (avg_ms / 1e3) / 1e9 if g > 1 else 0.0
+        return {"xgmi": {"bus_bw": round(bus, 1), "unit": "GB/s", "bytes_per_rank": S,
+                         "link_peak": 153.0, "links_per_gpu": 7,
+                         "note": "ring all-reduce busBW = 2(G-1)/G * S / t; per-link bound"}}
+
+    def cpu_baseline(self, seconds, threads):
+        return None
+
+
 class RefMergeBatch(Workload):
     """configs[0]'s merge (main.go:35-100) batched: P replicas x E entries."""
     name = "refmerge"
@@ -359,6 +402,8 @@ def make_workload(name, eng, rank, world, args):
         return SetMerge(eng, rank, world, args.set_n, args.key_space, lww=(name == "lww_merge"))
     if name == "shard_fold":
         return ShardFold(eng, rank, world, args.total_rows, args.nodes)
+    if name == "shard_join":
+        return ShardJoin(eng, rank, world, args.rows, args.nodes)
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -382,7 +427,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gcounter_join",
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
-                             "shard_fold", "refmerge"])
+                             "shard_fold", "shard_join", "refmerge"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)
@@ -460,6 +505,8 @@ def main():
             "config": wl.config, "roofline": roof, "cpu_baseline": cpu,
             "gpu_time_s": round(gpu_s, 6),
         }
+        if hasattr(wl, "extra"):
+            out.update(wl.extra(avg_ms))
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
