@@ -240,6 +240,43 @@ class SetMerge(Workload):
                 "sample": f"oc_{self.name} (serial merge), {self.n} tuples per side, {done // (2 * self.n)} reps"}
 
 
+class SetMergeUnsorted(SetMerge):
+    """configs[3] D2: both sides arrive UNSORTED; a step is the device sort
+    of each side (crdt_tuples_sort: LSD radix over the packed composite)
+    followed by the merge.  Algorithmic bytes are those of the merge itself
+    (inputs read once, output written once); the sort's passes are the
+    price of unsorted input, so frac reads against that."""
+    kernel = "k_sort_* (2 sides) + k_partition + k_set_merge"
+
+    def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
+        self.eng, self.n, self.lww = eng, n, lww
+        self.name = ("lww_merge" if lww else "orset_merge") + "_d2"
+        s = seed + 7919 * rank
+        self.UA = eng.synth_set_tuples(s, 0, n, key_space, sort=False)
+        self.UB = eng.synth_set_tuples(s, 1, n, key_space, sort=False)
+        self.A = E.TupleSet.empty(n, eng.device)
+        self.B = E.TupleSet.empty(n, eng.device)
+        self.out = E.TupleSet.empty(2 * n, eng.device)
+        self.count = torch.zeros(1, dtype=torch.int64, device=eng.device)
+        self._fn = eng.lww_merge if lww else eng.orset_merge
+        self.step()
+        torch.cuda.synchronize()
+        self.n_out = int(self.count.item())
+        self.config = {"workload": f"{'LWW-Element-Set' if lww else 'OR-Set'} merge, {n} tuples per side, "
+                                   f"key space {key_space}, UNSORTED inputs: device sort + merge "
+                                   "(BASELINE configs[3], D2)",
+                       "tuples_per_side": n, "key_space": key_space, "n_out": self.n_out,
+                       "parallelism": f"replicas x{world}"}
+
+    def step(self):
+        self.eng.sort_tuples(self.UA, out=self.A)
+        self.eng.sort_tuples(self.UB, out=self.B)
+        self._fn(self.A, self.B, out=self.out, count=self.count, trim=False)
+
+    def cpu_baseline(self, seconds, threads):
+        return None
+
+
 class ShardFold(Workload):
     """configs[4]: R replicas sharded over the ranks; fold + all-reduce(max)."""
     name = "shard_fold"
@@ -400,6 +437,8 @@ def make_workload(name, eng, rank, world, args):
         return VClockClassify(eng, rank, world, args.pairs, 128)
     if name in ("lww_merge", "orset_merge"):
         return SetMerge(eng, rank, world, args.set_n, args.key_space, lww=(name == "lww_merge"))
+    if name in ("lww_merge_d2", "orset_merge_d2"):
+        return SetMergeUnsorted(eng, rank, world, args.set_n, args.key_space, lww=(name == "lww_merge_d2"))
     if name == "shard_fold":
         return ShardFold(eng, rank, world, args.total_rows, args.nodes)
     if name == "shard_join":
@@ -426,7 +465,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gcounter_join",
-                    choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
+                    choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge", "lww_merge_d2", "orset_merge_d2",
                              "shard_fold", "shard_join", "refmerge"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)

@@ -1,0 +1,435 @@
+// sort.hip -- device sort of SoA tuples into the set-merge input order
+// (unsorted set state; BASELINE configs[3]).
+//
+// Order: ascending (key, ts, rep, tomb) -- the merge's (key, ts, rep) order,
+// with tomb breaking exact tag ties so the result is canonical (independent
+// of the input order).
+//
+// Every field is replaced by its offset from the field's minimum and the
+// four offsets are packed into one composite integer of W = bk+bt+br+1 bits
+// (tomb lowest, key highest): comparing composites IS comparing tuples.  W is
+// usually far below 64 (the D config: 23+20+6+1 = 50 bits), so the sort is a
+// plain 64-bit LSD radix sort of the composites; wider data use 2 or 3 words
+// per composite (W <= 161).  The last pass decodes the composite straight
+// into the SoA output: the sort moves no payload and gathers nothing.
+//
+// Passes (8-bit digits, P = ceil(W / 8)):
+//   k_sort_minmax : field minima/maxima (one read of the input)
+//   k_sort_hist   : composite digit histograms of all P passes at once
+//   k_sort_buckets: per-pass exclusive scan of the 256 buckets
+//   k_sort_pass   : per tile of 4096 composites (ticketed, so tiles are
+//                   processed in order): stable in-tile ranking by wave
+//                   ballots (a few barriers per tile), per-digit decoupled
+//                   look-back (one lane per digit), LDS-staged scatter in
+//                   digit order (runs of ~16 consecutive outputs per digit).
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int SB = 256;          // threads per sort workgroup
+constexpr int SR = 16;           // composites per thread
+constexpr int ST = SB * SR;      // 4096 composites per tile
+constexpr int SWAVES = SB / 64;
+
+struct SortPlan {
+    uint64_t kmin, tmin, rmin;
+    uint32_t bk, bt, br;         // bit widths of the key / ts / rep offsets
+    uint32_t W, P, words;        // composite bits, passes, 64-bit words
+};
+
+struct SortMinMax {              // reduced with atomics (initialised by the host)
+    unsigned long long kmin, kmax, tmin, tmax, rmin, rmax;
+};
+
+__device__ __forceinline__ uint32_t bitwidth(uint64_t x) { return x ? 64u - (uint32_t)__clzll((long long)x) : 0u; }
+
+__global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, SortMinMax *mm) {
+    unsigned long long kmin = ~0ULL, kmax = 0, tmin = ~0ULL, tmax = 0, rmin = ~0ULL, rmax = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const unsigned long long k = in.key[i], t = in.ts[i], r = in.rep[i];
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+        tmin = t < tmin ? t : tmin;
+        tmax = t > tmax ? t : tmax;
+        rmin = r < rmin ? r : rmin;
+        rmax = r > rmax ? r : rmax;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, m, 64));
+        kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, m, 64));
+        tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, m, 64));
+        tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, m, 64));
+        rmin = min(rmin, (unsigned long long)__shfl_xor(rmin, m, 64));
+        rmax = max(rmax, (unsigned long long)__shfl_xor(rmax, m, 64));
+    }
+    // workgroup reduction first: one atomic per field per workgroup (six
+    // contended addresses: per-wave atomics took 9x the read time)
+    __shared__ unsigned long long sred[6][4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sred[0][w] = kmin;
+        sred[1][w] = kmax;
+        sred[2][w] = tmin;
+        sred[3][w] = tmax;
+        sred[4][w] = rmin;
+        sred[5][w] = rmax;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int f = threadIdx.x;
+        unsigned long long v = sred[f][0];
+        for (int k = 1; k < 4; ++k) v = (f & 1) ? max(v, sred[f][k]) : min(v, sred[f][k]);
+        unsigned long long *dst = &mm->kmin + f;
+        if (f & 1) atomicMax(dst, v);
+        else atomicMin(dst, v);
+    }
+}
+
+__global__ void k_sort_plan(const SortMinMax *mm, SortPlan *plan) {
+    SortPlan p;
+    p.kmin = mm->kmin;
+    p.tmin = mm->tmin;
+    p.rmin = mm->rmin;
+    p.bk = bitwidth(mm->kmax - mm->kmin);
+    p.bt = bitwidth(mm->tmax - mm->tmin);
+    p.br = bitwidth(mm->rmax - mm->rmin);
+    p.W = p.bk + p.bt + p.br + 1;
+    p.P = (p.W + 7) / 8;
+    p.words = (p.W + 63) / 64;
+    *plan = p;
+}
+
+// ---------------------------------------------------------------- composite
+template <int WORDS>
+struct CKey {
+    uint64_t w[WORDS];
+};
+
+// OR v (b bits) into c at bit offset s
+template <int WORDS>
+__device__ __forceinline__ void put_bits(CKey<WORDS> &c, uint32_t s, uint64_t v, uint32_t b) {
+    if (b == 0) return;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) {
+        const int lo = q * 64;
+        if ((int)s >= lo + 64 || (int)(s + b) <= lo) continue;
+        if ((int)s >= lo) c.w[q] |= v << (s - lo);
+        else c.w[q] |= v >> (lo - s);
+    }
+}
+template <int WORDS>
+__device__ __forceinline__ uint64_t get_bits(const CKey<WORDS> &c, uint32_t s, uint32_t b) {
+    if (b == 0) return 0;
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) {
+        const int lo = q * 64;
+        if ((int)s >= lo + 64 || (int)(s + b) <= lo) continue;
+        if ((int)s >= lo) v |= c.w[q] >> (s - lo);
+        else v |= c.w[q] << (lo - s);
+    }
+    return b == 64 ? v : (v & ((1ULL << b) - 1));
+}
+template <int WORDS>
+__device__ __forceinline__ CKey<WORDS> compose(const SortPlan &p, uint64_t k, uint64_t t, uint32_t r, uint8_t tomb) {
+    CKey<WORDS> c;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) c.w[q] = 0;
+    c.w[0] = tomb ? 1u : 0u;
+    put_bits(c, 1, (uint64_t)(r - p.rmin), p.br);
+    put_bits(c, 1 + p.br, t - p.tmin, p.bt);
+    put_bits(c, 1 + p.br + p.bt, k - p.kmin, p.bk);
+    return c;
+}
+template <int WORDS>
+__device__ __forceinline__ uint32_t digit_of(const CKey<WORDS> &c, uint32_t pass) {
+    const uint32_t s = 8 * pass;
+    uint64_t x = c.w[0];                      // select, not a runtime index: keeps c in registers
+#pragma unroll
+    for (int q = 1; q < WORDS; ++q)
+        if ((s >> 6) == (uint32_t)q) x = c.w[q];
+    return (uint32_t)(x >> (s & 63)) & 255u;
+}
+
+// ---------------------------------------------------------------- histograms
+template <int WORDS>
+__global__ __launch_bounds__(256) void k_sort_hist(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
+                                                   uint32_t *__restrict__ ghist) {
+    __shared__ uint32_t h[24 * 256];
+    const SortPlan p = *plan_;
+    for (int i = threadIdx.x; i < (int)p.P * 256; i += 256) h[i] = 0;
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const CKey<WORDS> c = compose<WORDS>(p, in.key[i], in.ts[i], in.rep[i], in.tomb[i]);
+        for (uint32_t q = 0; q < p.P; ++q) atomicAdd(&h[q * 256 + digit_of(c, q)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (int)p.P * 256; i += 256)
+        if (h[i]) atomicAdd(&ghist[i], h[i]);
+}
+
+// bucket_start[q][d] = composites of pass q with a digit below d
+__global__ __launch_bounds__(256) void k_sort_buckets(const SortPlan *__restrict__ plan_, const uint32_t *ghist,
+                                                      uint32_t *bstart) {
+    __shared__ uint32_t wsum[SWAVES];
+    const SortPlan p = *plan_;
+    const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    for (uint32_t q = 0; q < p.P; ++q) {
+        const uint32_t v = ghist[q * 256 + d];
+        uint32_t x = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        bstart[q * 256 + d] = off + x - v;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- one pass
+// status[t*256 + d] = tag | flag | count: tag = pass + 1 (bits 56..63), so a
+// word left by an earlier pass reads as "not published" and the array needs
+// one memset per sort, not per pass.
+constexpr uint64_t kSAgg = 1ULL << 54, kSInc = 2ULL << 54;
+
+template <int WORDS, bool FIRST, bool LAST>
+__global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
+                                                  const SortPlan *__restrict__ plan_, uint32_t pass,
+                                                  const uint32_t *__restrict__ bstart, uint64_t *status,
+                                                  uint32_t *ticket, uint64_t *__restrict__ dst, crdt_tuples out,
+                                                  uint32_t *err) {
+    // wc: per (round, wave, digit) counts, then their exclusive prefix;
+    // reused (after the ranks are taken) as the staging area of the tile
+    constexpr int WC_BYTES = SR * SWAVES * 256 * 2;
+    constexpr int STAGE_BYTES = ST * 8 * WORDS;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WC_BYTES > STAGE_BYTES ? WC_BYTES : STAGE_BYTES];
+    __shared__ uint32_t s_tot[256], s_lstart[256], s_excl[256];
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_wsum[SWAVES];
+    uint16_t *wc = (uint16_t *)lds;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const SortPlan p = *plan_;
+    const uint64_t tag = (uint64_t)(pass + 1) << 56;
+
+    for (int i = tid; i < SR * SWAVES * 256 / 4; i += SB) ((uint64_t *)lds)[i] = 0;
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t t = s_tile;
+    const size_t base = (size_t)t * ST;
+
+    // ---- load (and compose on the first pass) SR composites per thread, round-major
+    CKey<WORDS> c[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        const size_t e = base + (size_t)r * SB + tid;
+        if (e < n) {
+            if constexpr (FIRST) {
+                c[r] = compose<WORDS>(p, in.key[e], in.ts[e], in.rep[e], in.tomb[e]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < WORDS; ++q) c[r].w[q] = src[(size_t)q * n + e];
+            }
+        }
+    }
+
+    // ---- stable in-tile rank: wave ballots per round, then one prefix per digit
+    uint32_t rk[SR / 4];                      // rank within the wave, 8 bits each
+#pragma unroll
+    for (int r = 0; r < SR / 4; ++r) rk[r] = 0;
+    uint32_t dg[SR / 4];                      // digits, 8 bits each (256: past the end)
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        const size_t e = base + (size_t)r * SB + tid;
+        const bool valid = e < n;
+        const uint32_t d = valid ? digit_of(c[r], pass) : 0u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t m = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & ((1ULL << lane) - 1ULL));
+        if (valid && below == 0) wc[(r * SWAVES + w) * 256 + d] = (uint16_t)__popcll(peers);
+        rk[r >> 2] |= below << (8 * (r & 3));
+        if ((r & 3) == 0) dg[r >> 2] = 0;
+        dg[r >> 2] |= (valid ? d : 255u) << (8 * (r & 3));
+    }
+    __syncthreads();
+    {   // thread d: exclusive prefix of digit d over (round, wave), in tile order
+        const int d = tid;
+        uint32_t run = 0;
+        for (int i = 0; i < SR * SWAVES; ++i) {
+            const uint32_t v = wc[i * 256 + d];
+            wc[i * 256 + d] = (uint16_t)run;
+            run += v;
+        }
+        s_tot[d] = run;
+        // publish this tile's count of digit d at once (decoupled look-back)
+        __hip_atomic_store(status + (size_t)t * 256 + d, tag | (t == 0 ? kSInc : kSAgg) | run, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        // local start of digit d in the digit-sorted tile
+        uint32_t x = run;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wsum[w] = x;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int k = 0; k < w; ++k) off += s_wsum[k];
+        s_lstart[d] = off + x - run;
+    }
+    __syncthreads();                          // s_lstart of every digit
+    uint32_t pos[SR / 2];                     // local positions, 16 bits each
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        const uint32_t d = (dg[r >> 2] >> (8 * (r & 3))) & 255u;
+        const size_t e = base + (size_t)r * SB + tid;
+        uint32_t lp = 0;
+        if (e < n) lp = s_lstart[d] + wc[(r * SWAVES + w) * 256 + d] + ((rk[r >> 2] >> (8 * (r & 3))) & 255u);
+        if ((r & 1) == 0) pos[r >> 1] = 0;
+        pos[r >> 1] |= lp << (16 * (r & 1));
+    }
+    __syncthreads();                          // wc dead: the area becomes the stage
+    {
+        uint64_t *stage = (uint64_t *)lds;
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+            const size_t e = base + (size_t)r * SB + tid;
+            if (e < n) {
+                const uint32_t lp = (pos[r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
+#pragma unroll
+                for (int q = 0; q < WORDS; ++q) stage[q * ST + lp] = c[r].w[q];
+            }
+        }
+    }
+    // ---- look-back for digit d (one lane per digit), bounded
+    {
+        const int d = tid;
+        uint64_t excl = 0;
+        if (t > 0) {
+            int64_t b = (int64_t)t - 1;
+            unsigned spins = 0;
+            while (b >= 0) {
+                const uint64_t s =
+                    __hip_atomic_load(status + (size_t)b * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((s & (0xFFULL << 56)) != tag || (s & (3ULL << 54)) == 0) {
+                    if (++spins > (1u << 24)) {
+                        atomicOr(err, CRDT_DEV_LOOKBACK);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += s & 0xFFFFFFFFULL;
+                if (s & kSInc) break;
+                --b;
+            }
+            __hip_atomic_store(status + (size_t)t * 256 + d, tag | kSInc | (excl + s_tot[d]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_excl[d] = bstart[pass * 256 + d] + (uint32_t)excl;
+    }
+    __syncthreads();
+    // ---- scatter in digit order: consecutive j of one digit -> consecutive outputs
+    const size_t cnt = n - base < (size_t)ST ? n - base : (size_t)ST;
+    const uint64_t *stage = (const uint64_t *)lds;
+    for (int j = tid; j < (int)cnt; j += SB) {
+        CKey<WORDS> v;
+#pragma unroll
+        for (int q = 0; q < WORDS; ++q) v.w[q] = stage[q * ST + j];
+        const uint32_t d = digit_of(v, pass);
+        const size_t o = (size_t)s_excl[d] + (uint32_t)(j - (int)s_lstart[d]);
+        if constexpr (LAST) {
+            out.key[o] = p.kmin + get_bits(v, 1 + p.br + p.bt, p.bk);
+            out.ts[o] = p.tmin + get_bits(v, 1 + p.br, p.bt);
+            out.rep[o] = (uint32_t)(p.rmin + get_bits(v, 1, p.br));
+            out.tomb[o] = (uint8_t)(v.w[0] & 1u);
+        } else {
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) dst[(size_t)q * n + o] = v.w[q];
+        }
+    }
+}
+
+template <int WORDS>
+static void launch_pass(bool first, bool last, unsigned grid, hipStream_t s, const crdt_tuples &in,
+                        const uint64_t *src, size_t n, const SortPlan *plan, uint32_t pass, const uint32_t *bstart,
+                        uint64_t *status, uint32_t *ticket, uint64_t *dst, const crdt_tuples &out, uint32_t *err) {
+    if (first && last)
+        k_sort_pass<WORDS, true, true><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+    else if (first)
+        k_sort_pass<WORDS, true, false><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+    else if (last)
+        k_sort_pass<WORDS, false, true><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+    else
+        k_sort_pass<WORDS, false, false><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+}
+
+template <int WORDS>
+static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &out, const SortPlan *plan_d,
+                      uint32_t P, uint64_t *bufs, uint32_t *ghist, uint32_t *bstart, uint64_t *status,
+                      uint32_t *tickets) {
+    const hipStream_t s = ctx->stream;
+    const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
+    k_sort_hist<WORDS><<<grid_for(n, 256, (unsigned)ctx->num_cus * 4), 256, 0, s>>>(in, n, plan_d, ghist);
+    k_sort_buckets<<<1, 256, 0, s>>>(plan_d, ghist, bstart);
+    uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
+    for (uint32_t q = 0; q < P; ++q) {
+        launch_pass<WORDS>(q == 0, q + 1 == P, ntiles, s, in, a, n, plan_d, q, bstart, status, tickets + q, b, out,
+                           ctx->dev_status);
+        std::swap(a, b);
+    }
+    return check_launch(ctx);
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, crdt_tuples *out) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!in || !out) return CRDT_E_INVAL;
+    if (n == 0) return CRDT_OK;
+    if (!in->key || !in->ts || !in->rep || !in->tomb || !out->key || !out->ts || !out->rep || !out->tomb)
+        return CRDT_E_INVAL;
+    if (n >= (1ULL << 32)) return CRDT_E_RANGE;       // 32-bit in-tile / bucket arithmetic
+    const size_t ntiles = (n + ST - 1) / ST;
+    const size_t b_mm = Carve::round(sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
+    const size_t b_hist = Carve::round(24 * 256 * 4), b_tk = Carve::round(24 * 4);
+    const size_t b_status = Carve::round(ntiles * 256 * 8), b_bufs = Carve::round(2 * 3 * n * 8);
+    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_hist + b_tk + b_status + b_bufs + 1024);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    SortMinMax *mm = w.take<SortMinMax>(1);
+    SortPlan *plan = w.take<SortPlan>(1);
+    uint32_t *ghist = w.take<uint32_t>(24 * 256);
+    uint32_t *tickets = w.take<uint32_t>(24);
+    uint64_t *status = w.take<uint64_t>(ntiles * 256);
+    uint32_t *bstart = w.take<uint32_t>(24 * 256);
+    uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
+    const hipStream_t s = ctx->stream;
+    const SortMinMax init{~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
+    hipError_t e = hipMemcpyAsync(mm, &init, sizeof(init), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(ghist, 0, 24 * 256 * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(tickets, 0, 24 * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(status, 0, ntiles * 256 * 8, s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    k_sort_minmax<<<grid_for(n, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(*in, n, mm);
+    k_sort_plan<<<1, 1, 0, s>>>(mm, plan);
+    // the pass count and composite width decide the launches: one small read-back
+    SortPlan h;
+    e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (h.words == 1) return sort_words<1>(ctx, *in, n, *out, plan, h.P, bufs, ghist, bstart, status, tickets);
+    if (h.words == 2) return sort_words<2>(ctx, *in, n, *out, plan, h.P, bufs, ghist, bstart, status, tickets);
+    return sort_words<3>(ctx, *in, n, *out, plan, h.P, bufs, ghist, bstart, status, tickets);
+}

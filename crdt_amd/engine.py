@@ -222,6 +222,18 @@ class Engine:
         """OR-Set merge: union of tags, tombstones OR-ed."""
         return self._set_merge("crdt_orset_merge", a, b, out, count, trim)
 
+    def sort_tuples(self, t: TupleSet, out: TupleSet | None = None) -> TupleSet:
+        """Device sort into ascending (key, ts, rep, tomb) order (config D2)."""
+        n = len(t)
+        out = TupleSet.empty(n, self.device) if out is None else out
+        for s in (t, out):
+            self._check(s.key, s.ts, itemsize=8)
+            self._check(s.rep, itemsize=4)
+            self._check(s.tomb, itemsize=1)
+        ct, co = t.c(), out.c()
+        self._call("crdt_tuples_sort", C.byref(ct), n, C.byref(co))
+        return out
+
     def count_unsorted(self, t: TupleSet) -> int:
         bad = torch.empty(1, dtype=torch.int64, device=self.device)
         ct = t.c()

@@ -146,6 +146,13 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
                      size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 /* Sortedness check (host-facing validation): *bad_dev = number of adjacent
  * pairs with t[i] > t[i+1]. */
+/* Sort n SoA tuples (device) into ascending (key, ts, rep, tomb) order --
+ * the merge input order, with tomb (0/1) breaking exact tag ties so the
+ * result does not depend on the input order (config D2: unsorted state).
+ * LSD radix sort of a packed composite of the fields' offsets from their
+ * minima; synchronises the stream once (to size the passes).  in and out
+ * must not overlap.  n < 2^32. */
+int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, crdt_tuples *out);
 int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
                                uint64_t *bad_dev);
 /* Diagnostic: after crdt_set_option("sets.stamps", 1), the last set merge
