@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fold a tools/profile.sh run into committed evidence under profiles/.
 
-    python tools/pmc_summary.py <workload> <kernel-substring> [round-tag]
+    python tools/pmc_summary.py <workload> <kernel-substring> [round-tag] [launches-per-step]
 
 Reads gpurun_out/prof_<workload>/{trace,pmc_fetch,pmc_write} and
   * copies the rocprofv3 --stats kernel summary to
@@ -36,6 +36,7 @@ def per_launch(path, kernel, counter):
 def main():
     wl, kernel = sys.argv[1], sys.argv[2]
     tag = sys.argv[3] if len(sys.argv) > 3 else "r01"
+    lps = int(sys.argv[4]) if len(sys.argv) > 4 else 1     # launches of the kernel per bench step
     src = os.path.join(ROOT, "gpurun_out", f"prof_{wl}")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -48,7 +49,7 @@ def main():
     algo = bench["roofline"]["bytes_per_launch"]
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
-    hbm = 2 * fk * 1024 + wk * 1024
+    hbm = (2 * fk * 1024 + wk * 1024) * lps          # per bench step, like bytes_per_launch
     # average duration of the kernel in the --stats summary
     avg_ns = None
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
@@ -58,6 +59,7 @@ def main():
                 break
     rec = {
         "workload": wl, "kernel": kernel, "launches_fetch": len(fetch), "launches_write": len(write),
+        "launches_per_step": lps,
         "FETCH_SIZE_KiB_per_launch": fk, "WRITE_SIZE_KiB_per_launch": wk,
         "hbm_bytes_per_launch": int(round(hbm)), "bytes_per_launch_algorithmic": algo,
         "traffic_over_algorithmic": round(hbm / algo, 4),
