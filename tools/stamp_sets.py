@@ -61,8 +61,6 @@ def main():
         print(f"  {nm:12s} median {np.median(d):9.0f}  p90 {np.percentile(d, 90):9.0f}")
     tot = st[:, 5] - st[:, 0]
     print(f"  {'total':12s} median {np.median(tot):9.0f}  p90 {np.percentile(tot, 90):9.0f}")
-    span = st[:, 5].max() - st[:, 0].min()
-    print(f"  kernel span {span} cycles; sum(tile)/span = {tot.sum() / span:.1f} tiles in flight on average")
 
 
 if __name__ == "__main__":
