@@ -256,7 +256,7 @@ using namespace crdt;
 struct crdt_server { Server s; };
 
 extern "C" int crdt_server_new(crdt_ctx *ctx, int port, crdt_server **out) {
-    if (!ctx || !out) return CRDT_E_INVAL;
+    if (!out) return CRDT_E_INVAL;            // ctx NULL: a host-only server (codec, AddCommand; no merge)
     crdt_server *p = new (std::nothrow) crdt_server();
     if (!p) return CRDT_E_NOMEM;
     p->s.ctx = ctx;
@@ -311,7 +311,7 @@ extern "C" int crdt_servers_merge(crdt_server *const *srvs, size_t n) {
     if (std::adjacent_find(order.begin(), order.end()) != order.end()) return CRDT_E_INVAL;   // duplicates
     crdt_ctx *ctx = v[0]->ctx;
     for (auto *s : v)
-        if (s->ctx->device != ctx->device) return CRDT_E_INVAL;
+        if (!s->ctx || s->ctx->device != ctx->device) return CRDT_E_INVAL;   // host-only servers cannot merge
     int rc = bind(ctx);
     if (rc) return rc;
     for (auto *s : v) s->Alive = false;                         // main.go:41
@@ -433,5 +433,402 @@ extern "C" int crdt_server_state_at(crdt_server *srv, size_t i, const char **key
     *klen = s.state_view[i].first.size();
     *val = s.state_view[i].second.data();
     *vlen = s.state_view[i].second.size();
+    return CRDT_OK;
+}
+
+// ---------------------------------------------------------------- gossip wire codec
+// The reference's gossip wire format:
+//   serve : Gossip handler (main.go:153-170): 502 "Unreachable" unless Alive,
+//           else 200 + server.Diff.ToJSON() (main.go:159).  gods v1.18.1
+//           treemap ToJSON = json.Marshal(map[string]interface{}) keyed by
+//           strconv.FormatInt(ts): encoding/json writes map keys sorted as
+//           BYTE STRINGS ("-5" < "10" < "2"), values (map[string]string or
+//           *Command) as objects with sorted keys, no whitespace.
+//   pull  : main.go:245-256: json.Unmarshal into map[string]map[string]string
+//           (any error: the round is skipped, main.go:247-249), then for each
+//           key Atoi(key) -> RemoteDiff.Put(int64(atoi), value); a key that
+//           fails Atoi RETURNS from the gossip goroutine (main.go:252-253).
+// Strings follow Go 1.18 encoding/json: Marshal escapes the quote and the
+// backslash with a backslash, newline / CR / tab as \n \r \t, other bytes < 0x20
+// and the HTML-unsafe '<' '>' '&' as \u00XX (lowercase hex), U+2028 / U+2029
+// as \u2028 / \u2029, and each byte of invalid UTF-8 as \ufffd; Unmarshal
+// accepts any valid JSON and replaces invalid UTF-8 / unpaired surrogates
+// with U+FFFD.
+
+static void json_put_string(std::string &o, const std::string &s) {
+    static const char *hex = "0123456789abcdef";
+    o.push_back('"');
+    size_t i = 0;
+    const size_t n = s.size();
+    while (i < n) {
+        const unsigned char b = (unsigned char)s[i];
+        if (b < 0x80) {
+            if (b >= 0x20 && b != '"' && b != '\\' && b != '<' && b != '>' && b != '&') {
+                o.push_back((char)b);
+            } else if (b == '"' || b == '\\') {
+                o.push_back('\\');
+                o.push_back((char)b);
+            } else if (b == '\n') {
+                o += "\\n";
+            } else if (b == '\r') {
+                o += "\\r";
+            } else if (b == '\t') {
+                o += "\\t";
+            } else {
+                o += "\\u00";
+                o.push_back(hex[b >> 4]);
+                o.push_back(hex[b & 15]);
+            }
+            ++i;
+            continue;
+        }
+        // decode one UTF-8 sequence the way utf8.DecodeRuneInString does
+        uint32_t cp = 0;
+        size_t len = 0;
+        if (b >= 0xC2 && b <= 0xDF) { len = 2; cp = b & 0x1F; }
+        else if (b >= 0xE0 && b <= 0xEF) { len = 3; cp = b & 0x0F; }
+        else if (b >= 0xF0 && b <= 0xF4) { len = 4; cp = b & 0x07; }
+        bool ok = len != 0 && i + len <= n;
+        for (size_t k = 1; ok && k < len; ++k) {
+            const unsigned char c = (unsigned char)s[i + k];
+            if ((c & 0xC0) != 0x80) ok = false;
+            cp = (cp << 6) | (c & 0x3F);
+        }
+        if (ok) {   // reject overlongs, surrogates, > U+10FFFF (second-byte ranges of utf8.DecodeRune)
+            const unsigned char c1 = (unsigned char)s[i + 1];
+            if (b == 0xE0 && c1 < 0xA0) ok = false;
+            if (b == 0xED && c1 > 0x9F) ok = false;
+            if (b == 0xF0 && c1 < 0x90) ok = false;
+            if (b == 0xF4 && c1 > 0x8F) ok = false;
+        }
+        if (!ok) {
+            o += "\\ufffd";
+            ++i;
+            continue;
+        }
+        if (cp == 0x2028 || cp == 0x2029) {
+            o += cp == 0x2028 ? "\\u2028" : "\\u2029";
+        } else {
+            o.append(s, i, len);
+        }
+        i += len;
+    }
+    o.push_back('"');
+}
+
+static void json_put_value(std::string &o, const Value &v) {
+    std::vector<const std::pair<std::string, std::string> *> kv;
+    kv.reserve(v.kv.size());
+    for (auto &e : v.kv) kv.push_back(&e);
+    std::sort(kv.begin(), kv.end(), [](auto *a, auto *b) { return a->first < b->first; });
+    o.push_back('{');
+    for (size_t i = 0; i < kv.size(); ++i) {
+        if (i) o.push_back(',');
+        json_put_string(o, kv[i]->first);
+        o.push_back(':');
+        json_put_string(o, kv[i]->second);
+    }
+    o.push_back('}');
+}
+
+// *len = bytes of the response body; the body is copied to buf when cap
+// allows (else CRDT_E_RANGE with *len = the size needed).
+extern "C" int crdt_server_gossip_json(crdt_server *srv, char *buf, size_t cap, size_t *len, int *http_status) {
+    if (!srv || !len || !http_status) return CRDT_E_INVAL;
+    std::string body;
+    {
+        std::lock_guard<std::mutex> g(srv->s.Lock);                   // main.go:155-156
+        if (!srv->s.Alive) {
+            *http_status = 502;
+            body = "Unreachable";                                    // main.go:166
+        } else {
+            *http_status = 200;
+            std::vector<std::pair<std::string, const Value *>> items;
+            items.reserve(srv->s.Diff.size());
+            for (auto &e : srv->s.Diff) items.emplace_back(std::to_string((long long)e.first), e.second.get());
+            std::sort(items.begin(), items.end(), [](auto &a, auto &b) { return a.first < b.first; });
+            body.push_back('{');
+            for (size_t i = 0; i < items.size(); ++i) {
+                if (i) body.push_back(',');
+                json_put_string(body, items[i].first);
+                body.push_back(':');
+                json_put_value(body, *items[i].second);
+            }
+            body.push_back('}');
+        }
+    }
+    *len = body.size();
+    if (!buf || cap < body.size()) return CRDT_E_RANGE;
+    std::copy(body.begin(), body.end(), buf);
+    return CRDT_OK;
+}
+
+namespace {
+
+// Minimal RFC 8259 parser for exactly the shape main.go:246 decodes into:
+// an object of objects of strings (or null).  Anything else is an error,
+// which json.Unmarshal reports (a type error included) and main.go skips.
+struct JsonIn {
+    const char *p, *e;
+    bool fail = false;
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+    }
+    bool lit(const char *s) {
+        const char *q = p;
+        for (; *s; ++s, ++q)
+            if (q >= e || *q != *s) return false;
+        p = q;
+        return true;
+    }
+    static void put_utf8(std::string &o, uint32_t cp) {
+        if (cp < 0x80) o.push_back((char)cp);
+        else if (cp < 0x800) { o.push_back((char)(0xC0 | (cp >> 6))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+        else if (cp < 0x10000) {
+            o.push_back((char)(0xE0 | (cp >> 12)));
+            o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            o.push_back((char)(0x80 | (cp & 0x3F)));
+        } else {
+            o.push_back((char)(0xF0 | (cp >> 18)));
+            o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+            o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            o.push_back((char)(0x80 | (cp & 0x3F)));
+        }
+    }
+    int hex4() {
+        if (e - p < 4) return -1;
+        int v = 0;
+        for (int k = 0; k < 4; ++k) {
+            const char c = p[k];
+            int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+            if (d < 0) return -1;
+            v = v * 16 + d;
+        }
+        p += 4;
+        return v;
+    }
+    bool str(std::string &o) {
+        if (p >= e || *p != '"') return false;
+        ++p;
+        while (p < e) {
+            const unsigned char c = (unsigned char)*p;
+            if (c == '"') { ++p; return true; }
+            if (c < 0x20) return false;                 // raw control characters are invalid JSON
+            if (c == '\\') {
+                if (++p >= e) return false;
+                const char x = *p++;
+                switch (x) {
+                    case '"': o.push_back('"'); break;
+                    case '\\': o.push_back('\\'); break;
+                    case '/': o.push_back('/'); break;
+                    case 'b': o.push_back('\b'); break;
+                    case 'f': o.push_back('\f'); break;
+                    case 'n': o.push_back('\n'); break;
+                    case 'r': o.push_back('\r'); break;
+                    case 't': o.push_back('\t'); break;
+                    case 'u': {
+                        int u = hex4();
+                        if (u < 0) return false;
+                        uint32_t cp = (uint32_t)u;
+                        if (cp >= 0xD800 && cp < 0xDC00) {       // high surrogate: pair or U+FFFD
+                            if (e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+                                const char *save = p;
+                                p += 2;
+                                const int lo = hex4();
+                                if (lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (uint32_t)(lo - 0xDC00);
+                                else { p = save; cp = 0xFFFD; }
+                            } else {
+                                cp = 0xFFFD;
+                            }
+                        } else if (cp >= 0xDC00 && cp < 0xE000) {
+                            cp = 0xFFFD;
+                        }
+                        put_utf8(o, cp);
+                        break;
+                    }
+                    default: return false;
+                }
+                continue;
+            }
+            if (c < 0x80) { o.push_back((char)c); ++p; continue; }
+            // raw UTF-8: copy valid sequences, replace each invalid byte with U+FFFD
+            size_t len = c >= 0xC2 && c <= 0xDF ? 2 : c >= 0xE0 && c <= 0xEF ? 3 : c >= 0xF0 && c <= 0xF4 ? 4 : 0;
+            bool ok = len != 0 && (size_t)(e - p) >= len;
+            for (size_t k = 1; ok && k < len; ++k) ok = ((unsigned char)p[k] & 0xC0) == 0x80;
+            if (ok) {
+                const unsigned char c1 = (unsigned char)p[1];
+                if ((c == 0xE0 && c1 < 0xA0) || (c == 0xED && c1 > 0x9F) || (c == 0xF0 && c1 < 0x90) ||
+                    (c == 0xF4 && c1 > 0x8F))
+                    ok = false;
+            }
+            if (ok) { o.append(p, len); p += len; }
+            else { put_utf8(o, 0xFFFD); ++p; }
+        }
+        return false;
+    }
+    // object of strings (or null) -> kv (duplicate keys: the last wins)
+    bool inner(std::vector<std::pair<std::string, std::string>> &kv, bool *is_null) {
+        ws();
+        *is_null = false;
+        if (lit("null")) { *is_null = true; return true; }
+        if (p >= e || *p != '{') return false;
+        ++p;
+        ws();
+        std::map<std::string, std::string> m;
+        if (p < e && *p == '}') { ++p; return true; }
+        for (;;) {
+            std::string k, v;
+            ws();
+            if (!str(k)) return false;
+            ws();
+            if (p >= e || *p != ':') return false;
+            ++p;
+            ws();
+            if (lit("null")) {
+                // a null member leaves the map entry at its zero value "" (json.Unmarshal)
+                m[k] = std::string();
+            } else if (!str(v)) {
+                return false;                                // non-string member: a type error
+            } else {
+                m[k] = v;
+            }
+            ws();
+            if (p < e && *p == ',') { ++p; continue; }
+            if (p < e && *p == '}') { ++p; break; }
+            return false;
+        }
+        kv.assign(m.begin(), m.end());
+        return true;
+    }
+};
+
+bool go_atoi64(const std::string &x, long long *out) {
+    if (x.empty()) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (x[0] == '+' || x[0] == '-') {
+        neg = x[0] == '-';
+        i = 1;
+        if (x.size() == 1) return false;
+    }
+    unsigned long long acc = 0;
+    for (; i < x.size(); ++i) {
+        const unsigned d = (unsigned char)x[i] - (unsigned)'0';
+        if (d > 9 || acc > (0xFFFFFFFFFFFFFFFFULL - d) / 10) return false;
+        acc = acc * 10 + d;
+    }
+    if ((!neg && acc >= 0x8000000000000000ULL) || (neg && acc > 0x8000000000000000ULL)) return false;
+    *out = neg ? (long long)(0 - acc) : (long long)acc;
+    return true;
+}
+
+}  // namespace
+
+// *outcome: 0 = ingested into RemoteDiff (the reference then calls merge(),
+// main.go:257); 1 = not valid JSON of that shape: nothing ingested, the round
+// is skipped (main.go:247-249); 2 = a key failed Atoi: the reference's gossip
+// goroutine returns (main.go:252-253) -- nothing is ingested here (Go's
+// random map order makes "that key first" one of the legal executions).
+// Keys with equal Atoi values ("1", "01") are applied in byte order of the
+// key strings, the last one winning (one of Go's legal orders).
+extern "C" int crdt_server_ingest_json(crdt_server *srv, const char *data, size_t len, int *outcome) {
+    if (!srv || !outcome || (!data && len)) return CRDT_E_INVAL;
+    JsonIn in{data, data + len};
+    std::map<std::string, std::pair<std::vector<std::pair<std::string, std::string>>, bool>> top;
+    bool ok = true;
+    in.ws();
+    if (in.lit("null")) {
+        in.ws();
+        ok = in.p == in.e;                                   // null: the map stays nil, no error
+        *outcome = ok ? 0 : 1;
+        return CRDT_OK;
+    }
+    if (in.p >= in.e || *in.p != '{') ok = false;
+    else {
+        ++in.p;
+        in.ws();
+        if (in.p < in.e && *in.p == '}') ++in.p;
+        else {
+            for (;;) {
+                std::string k;
+                in.ws();
+                if (!in.str(k)) { ok = false; break; }
+                in.ws();
+                if (in.p >= in.e || *in.p != ':') { ok = false; break; }
+                ++in.p;
+                std::vector<std::pair<std::string, std::string>> kv;
+                bool is_null = false;
+                if (!in.inner(kv, &is_null)) { ok = false; break; }
+                top[k] = {std::move(kv), is_null};             // duplicate keys: the last wins
+                in.ws();
+                if (in.p < in.e && *in.p == ',') { ++in.p; continue; }
+                if (in.p < in.e && *in.p == '}') { ++in.p; break; }
+                ok = false;
+                break;
+            }
+        }
+        in.ws();
+        if (in.p != in.e) ok = false;                        // trailing data is a syntax error
+    }
+    if (!ok) { *outcome = 1; return CRDT_OK; }
+    std::vector<std::pair<long long, const std::vector<std::pair<std::string, std::string>> *>> puts;
+    for (auto &t : top) {
+        long long ts;
+        if (!go_atoi64(t.first, &ts)) { *outcome = 2; return CRDT_OK; }
+        puts.emplace_back(ts, &t.second.first);
+    }
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    for (auto &pv : puts) {
+        auto v = std::make_shared<Value>();
+        v->local = false;
+        v->kv = *pv.second;
+        srv->s.RemoteDiff[(int64_t)pv.first] = std::move(v);
+    }
+    *outcome = 0;
+    return CRDT_OK;
+}
+
+// AliveState handler (main.go:141-151) after strconv.ParseBool: sets Alive.
+extern "C" int crdt_server_set_alive(crdt_server *srv, int alive) {
+    if (!srv) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    srv->s.Alive = alive != 0;
+    return CRDT_OK;
+}
+
+// Ascending RemoteDiff keys (RemoteDiff.Keys()); writes min(cap, len).
+extern "C" int crdt_server_remote_keys(crdt_server *srv, int64_t *ts, size_t cap, size_t *n) {
+    if (!srv || !n) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    size_t i = 0;
+    for (auto &e : srv->s.RemoteDiff) {
+        if (i >= cap) break;
+        if (ts) ts[i] = e.first;
+        ++i;
+    }
+    *n = srv->s.RemoteDiff.size();
+    return CRDT_OK;
+}
+
+// treemap Get(ts) on Diff (remote = 0) or RemoteDiff (remote = 1):
+// CRDT_E_RANGE when ts is absent; else *npairs = the value's pair count and,
+// when i < *npairs, its i-th pair (key, value).  Values are immutable once
+// stored, so the pointers stay valid while the entry remains in the map.
+extern "C" int crdt_server_entry_at(crdt_server *srv, int remote, int64_t ts, size_t i, const char **key,
+                                    size_t *klen, const char **val, size_t *vlen, size_t *npairs) {
+    if (!srv || !npairs) return CRDT_E_INVAL;
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    auto &m = remote ? srv->s.RemoteDiff : srv->s.Diff;
+    auto it = m.find(ts);
+    if (it == m.end()) return CRDT_E_RANGE;
+    const Value &v = *it->second;
+    *npairs = v.kv.size();
+    if (i < v.kv.size()) {
+        if (!key || !klen || !val || !vlen) return CRDT_E_INVAL;
+        *key = v.kv[i].first.data();
+        *klen = v.kv[i].first.size();
+        *val = v.kv[i].second.data();
+        *vlen = v.kv[i].second.size();
+    }
     return CRDT_OK;
 }

@@ -15,7 +15,7 @@ merges many servers in one device call.  No CPU path exists.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, Iterable, List, Sequence
+from typing import Tuple, Dict, Iterable, List, Sequence
 
 from . import _lib
 from ._lib import call
@@ -27,8 +27,18 @@ def Int64Comparator(a: int, b: int) -> int:
     return _lib.lib().crdt_compare_int64(a, b)
 
 
+def _enc(x) -> bytes:
+    return x if isinstance(x, bytes) else x.encode("utf-8", "surrogatepass")
+
+
+def _dec(b: bytes) -> str:
+    # Go strings are byte strings: bytes that are not UTF-8 survive as lone
+    # surrogates (surrogateescape) so a Get round-trips what a Put stored.
+    return b.decode("utf-8", "surrogateescape")
+
+
 def _kv_arrays(d: Dict[str, str]):
-    items = [(k.encode("utf-8", "surrogatepass"), v.encode("utf-8", "surrogatepass")) for k, v in d.items()]
+    items = [(_enc(k), _enc(v)) for k, v in d.items()]
     n = len(items)
     keys = (C.c_char_p * max(n, 1))(*[k for k, _ in items])
     vals = (C.c_char_p * max(n, 1))(*[v for _, v in items])
@@ -54,8 +64,31 @@ class _TreeMap:
     def Keys(self) -> List[int]:
         return [t for t, _ in self._srv._diff_entries()] if not self._remote else self._remote_keys()
 
-    def _remote_keys(self):
-        raise NotImplementedError("RemoteDiff is write-only from the host (gossip ingest)")
+    def _remote_keys(self) -> List[int]:
+        n = C.c_size_t()
+        call("crdt_server_remote_keys", self._srv._h, None, 0, C.byref(n))
+        cap = n.value
+        ts = (C.c_int64 * max(cap, 1))()
+        call("crdt_server_remote_keys", self._srv._h, ts, cap, C.byref(n))
+        return [ts[i] for i in range(min(cap, n.value))]
+
+    def Get(self, ts: int) -> Tuple[Dict[str, str] | None, bool]:
+        """treemap Get (gods v1.18.1): (value, found); the value as a dict."""
+        k, kl, v, vl, n = C.c_void_p(), C.c_size_t(), C.c_void_p(), C.c_size_t(), C.c_size_t()
+        h, r = self._srv._h, 1 if self._remote else 0
+        rc = _lib.lib().crdt_server_entry_at(h, r, int(ts), 0, C.byref(k), C.byref(kl), C.byref(v), C.byref(vl),
+                                             C.byref(n))
+        if rc == -6:                       # CRDT_E_RANGE: absent
+            return None, False
+        if rc < 0:
+            _lib.check("crdt_server_entry_at", rc)
+        out = {}
+        for i in range(n.value):
+            call("crdt_server_entry_at", h, r, int(ts), i, C.byref(k), C.byref(kl), C.byref(v), C.byref(vl),
+                 C.byref(n))
+            out[_dec(C.string_at(k.value, kl.value) if kl.value else b"")] = \
+                _dec(C.string_at(v.value, vl.value) if vl.value else b"")
+        return out, True
 
     def Size(self) -> int:
         n = C.c_size_t()
@@ -68,9 +101,9 @@ class Server:
 
     def __init__(self, eng, port: int, initial_state: Dict[str, str] | None = None,
                  friend_list: Sequence[str] = ()):
-        self._eng = eng
+        self._eng = eng                       # None: host-only (codec, AddCommand; no merge)
         h = C.c_void_p()
-        call("crdt_server_new", eng.ctx, int(port), C.byref(h))
+        call("crdt_server_new", eng.ctx if eng is not None else None, int(port), C.byref(h))
         self._h = h
         self.Port = port
         self.InitialState = dict(initial_state or {})
@@ -95,8 +128,36 @@ class Server:
 
     def merge(self) -> None:
         """(*Server).merge() -- main.go:35-100, bit-exact, on the GPU."""
+        if self._eng is None:
+            raise _lib.CrdtLibraryError("host-only Server (no engine): merge() runs on the GPU")
         self._eng._bind()
         call("crdt_server_merge", self._h)
+
+    def Gossip(self) -> Tuple[int, bytes]:
+        """GET /gossip (main.go:153-170): (HTTP status, body) -- 200 with
+        Diff.ToJSON() (main.go:159) or 502 "Unreachable"."""
+        n, st = C.c_size_t(), C.c_int()
+        while True:
+            buf = C.create_string_buffer(max(n.value, 1))
+            rc = _lib.lib().crdt_server_gossip_json(self._h, buf, n.value, C.byref(n), C.byref(st))
+            if rc != -6:                        # CRDT_E_RANGE: *n = size needed; retry (Diff may grow)
+                break
+        if rc < 0:
+            _lib.check("crdt_server_gossip_json", rc)
+        return st.value, buf.raw[: n.value]
+
+    def SetAlive(self, alive: bool) -> None:
+        """AliveState handler (main.go:141-151) after ParseBool."""
+        call("crdt_server_set_alive", self._h, 1 if alive else 0)
+
+    def IngestGossip(self, data: bytes) -> int:
+        """The gossip pull's decode (main.go:245-256).  Returns 0 = ingested
+        into RemoteDiff (merge() next, main.go:257), 1 = bad JSON / shape, round
+        skipped (main.go:247-249), 2 = a key failed Atoi, the reference's gossip
+        goroutine returns (main.go:252-253)."""
+        out = C.c_int()
+        call("crdt_server_ingest_json", self._h, bytes(data), len(data), C.byref(out))
+        return out.value
 
     def AddCommand(self, ts_ms: int, data: Dict[str, str]) -> int:
         """POST /data after decoding (main.go:173-215); returns the HTTP status."""

@@ -212,7 +212,9 @@ int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *str_bytes_dev, const uint64_t 
  * arrays of (pointer, length) byte strings; a repeated key overwrites (Go
  * map semantics).  All functions lock the server's mutex (main.go:32). */
 typedef struct crdt_server crdt_server;
-/* NewServer(port, initialState, friendList) (main.go:102-113). */
+/* NewServer(port, initialState, friendList) (main.go:102-113).  ctx may be
+ * NULL for a host-only server (gossip codec, AddCommand): merge() then
+ * returns CRDT_E_INVAL. */
 int crdt_server_new(crdt_ctx *ctx, int port, crdt_server **out);
 int crdt_server_free(crdt_server *srv);
 int crdt_server_init_state(crdt_server *srv, const char *const *keys, const size_t *key_lens,
@@ -263,6 +265,28 @@ int crdt_synth_vclock_pairs(crdt_ctx *ctx, uint64_t seed, uint64_t *a_dev, uint6
                             size_t pairs, size_t nodes, uint64_t pair_base);
 int crdt_synth_set_tuples(crdt_ctx *ctx, uint64_t seed, uint32_t side, const crdt_tuples *out,
                           size_t n, uint64_t key_space);
+
+/* ------------------------------------------------ gossip wire codec (§8(f) row 2)
+ * Gossip handler (main.go:153-170): *http_status = 502 ("Unreachable")
+ * unless Alive, else 200 with server.Diff.ToJSON() (main.go:159): gods
+ * treemap ToJSON -> json.Marshal of {FormatInt(ts): value}, keys sorted as
+ * byte strings, Go 1.18 encoding/json escaping.  The body goes to buf when
+ * cap allows (else CRDT_E_RANGE, *len = size needed). */
+int crdt_server_gossip_json(crdt_server *srv, char *buf, size_t cap, size_t *len, int *http_status);
+/* Gossip pull decode (main.go:245-256): json.Unmarshal into
+ * map[string]map[string]string, then RemoteDiff.Put(int64(Atoi(key)), value).
+ * *outcome: 0 ingested (call merge next, main.go:257); 1 invalid JSON or shape,
+ * round skipped (main.go:247-249); 2 a key failed Atoi, the reference's
+ * gossip goroutine returns (main.go:252-253), nothing ingested. */
+int crdt_server_ingest_json(crdt_server *srv, const char *data, size_t len, int *outcome);
+/* AliveState handler (main.go:141-151), after strconv.ParseBool. */
+int crdt_server_set_alive(crdt_server *srv, int alive);
+/* Ascending RemoteDiff keys; writes min(cap, len). */
+int crdt_server_remote_keys(crdt_server *srv, int64_t *ts, size_t cap, size_t *n);
+/* treemap Get(ts) on Diff (remote = 0) / RemoteDiff (remote = 1): CRDT_E_RANGE
+ * if absent; else *npairs and, when i < *npairs, the i-th (key, value) pair. */
+int crdt_server_entry_at(crdt_server *srv, int remote, int64_t ts, size_t i, const char **key,
+                         size_t *key_len, const char **val, size_t *val_len, size_t *npairs);
 
 #ifdef __cplusplus
 }
