@@ -10,6 +10,7 @@ int g_vclock_pairs_per_wave = 4;
 int g_sets_stamps = 0;
 int g_sets_grid_per_cu = 0;
 int g_sets_diag = 0;
+int g_rm_diag = 0;
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -187,6 +188,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic: WRONG output order
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sets_diag = (int)v;
+    } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 no fold, 2 no flush, 3 no LDS, 4 no table
+        if (v < 0 || v > 4) return CRDT_E_INVAL;
+        g_rm_diag = (int)v;
     } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sets_stamps = (int)v;

@@ -15,11 +15,9 @@
 //    The sum is order-independent (mod 2^64), which is what lets the fold run
 //    as parallel atomics instead of the reference's serial descending loop.
 //
-// Kernels: atoi over the string arena; walk flags (binary search per R
-// entry); device scan of the flags; L and R scatters into the new Diff;
-// per-replica replay over the new Diff with LDS accumulators (k_replay).
-// (Workgroup-per-replica and chunk-parallel walk/scatter variants measured
-// no faster: every variant is bound by chains of dependent global loads.)
+// Kernels: atoi over the string arena; tiled merge-path walk (count pass,
+// device scan, write pass producing the new Diff and folding the replay into
+// per-slot accumulators); per-slot closed form (k_slot_final).
 #include <algorithm>
 
 #include "scan.hpp"
@@ -59,216 +57,493 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
     }
 }
 
-// Replica owning global entry g: largest p with off[p] <= g.
-__device__ __forceinline__ uint32_t owner(const uint64_t *off, uint32_t replicas, uint64_t g) {
-    uint32_t lo = 0, hi = replicas;          // off[0] <= g < off[replicas]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (off[mid] <= g) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ uint64_t lower_bound_i64(const int64_t *v, uint64_t lo, uint64_t hi, int64_t x) {
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (v[mid] < x) lo = mid + 1;        // signed order: Int64Comparator (main.go:106)
-        else hi = mid;
-    }
-    return lo;
-}
-
-__global__ void k_walk_flags(crdt_refmerge_in in, uint32_t *__restrict__ flag, uint64_t *__restrict__ rpos) {
-    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < in.n_r; g += (uint64_t)gridDim.x * 256) {
-        const uint32_t p = owner(in.r_off, in.replicas, g);
-        const uint64_t lb = in.l_off[p], le = in.l_off[p + 1];
-        const int64_t r = in.r_ts[g];
-        const uint64_t pos = lower_bound_i64(in.l_ts, lb, le, r);
-        flag[g] = (pos < le && in.l_ts[pos] != r) ? 1u : 0u;
-        rpos[g] = pos - lb;
-    }
-}
-
-__global__ void k_out_off(crdt_refmerge_in in, const uint64_t *__restrict__ ib, uint64_t *__restrict__ out_off) {
-    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p <= in.replicas; p += gridDim.x * 256)
-        out_off[p] = in.l_off[p] + ib[in.r_off[p]];
-}
-
-__global__ void k_scatter_l(crdt_refmerge_in in, const uint64_t *__restrict__ ib, crdt_refmerge_out out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < in.n_l; i += (uint64_t)gridDim.x * 256) {
-        const uint32_t p = owner(in.l_off, in.replicas, i);
-        const uint64_t rb = in.r_off[p], re = in.r_off[p + 1];
-        const uint64_t lbr = lower_bound_i64(in.r_ts, rb, re, in.l_ts[i]);
-        const uint64_t o = out.off[p] + (i - in.l_off[p]) + (ib[lbr] - ib[rb]);
-        out.ts[o] = in.l_ts[i];
-        out.origin[o] = in.l_origin[i];
-        out.src[o] = (int64_t)i;
-    }
-}
-
-__global__ void k_scatter_r(crdt_refmerge_in in, const uint32_t *__restrict__ flag,
-                            const uint64_t *__restrict__ rpos, const uint64_t *__restrict__ ib,
-                            crdt_refmerge_out out) {
-    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < in.n_r; g += (uint64_t)gridDim.x * 256) {
-        if (!flag[g]) continue;
-        const uint32_t p = owner(in.r_off, in.replicas, g);
-        const uint64_t o = out.off[p] + rpos[g] + (ib[g] - ib[in.r_off[p]]);
-        out.ts[o] = in.r_ts[g];
-        out.origin[o] = 0;
-        out.src[o] = -(int64_t)g - 1;
-    }
-}
-
-// ---------------------------------------------------------------- replay
-// One workgroup per replica, over the replica's NEW Diff (already written by
-// the scatters, ascending ts): an entry's position o in it orders the
-// entries by ts, so the base holder of a key (its max-ts entry) is the one
-// with the largest (o << 32 | string id) -- a single 64-bit max, reduced in
-// the same pass as the sums and counts.  The per-key accumulators live in an
-// LDS hash table (slots of different replicas are disjoint, so the workgroup
-// owns every slot it touches: no global atomics); a replica with more
-// distinct keys than the table holds is redone by the same workgroup through
-// its slice of slot-indexed global accumulators.  (Four contended global
-// atomics per key plus a second base pass took 4x longer; chunk-parallel
-// workgroups with a table flush were 1.4x slower than this.)
-constexpr int RT = 1024;                  // LDS table entries per workgroup
+// ---------------------------------------------------------------- walk + replay
+// Tiled merge path.  Per replica the new Diff is the merge of L and R (L
+// first on an equal ts) keeping every L entry and the R entries that are
+// "inserted" (below max(L), not equal to the L entry just before them in
+// merge order).  Each replica's merge sequence (|L|+|R| items) is cut into
+// tiles of MT items (geometry precomputed per tile); a tile's L and R ranges
+// come from a merge-path split (64-ary, one wave), are staged in LDS with
+// coalesced loads and merged by 256 threads x MI items.
+//   k_rm_count : split at the tile start (kept) + inserted-R count per tile,
+//                and the replay fold of the tile's emitted remote-origin
+//                entries (main.go:75-98) into an LDS table keyed by slot,
+//                flushed with one set of global atomics per (tile, slot);
+//   device scan of the counts -> every tile's output offset;
+//   k_rm_write : re-merge, write the tile's new-Diff slice through LDS
+//                (coalesced);
+//   k_slot_final: per-slot closed form.
+// The replay's per-key state is order-free: best = max over holders of
+// (rank in the replica's merge sequence) << 32 | string id (the max-ts
+// holder, since the merge sequence is ts-ascending), plus the wrapped sum
+// and count of the parsable values; so tiles can fold independently.  (Per-entry binary
+// searches over the logs, and a per-replica replay pass re-reading the new
+// Diff, were each bound by chains of dependent global loads.)
+constexpr int MT = 2048;                  // merge items per tile
+constexpr int MB = 256;                   // threads per tile
+constexpr int MI = MT / MB;               // items per thread
+constexpr int TT = 512;                   // LDS replay-table entries per tile
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-struct SlotAcc {                          // global fallback, indexed by slot
-    unsigned long long *best;
-    unsigned *nent;
+struct TileGeo {                          // 64 B per tile
+    uint64_t lb, nl, rb, nr, d0, d1;
+    int64_t maxl;
+    uint32_t p, first;                    // replica; first tile of the replica
+};
+
+struct SlotAcc {                          // global replay accumulators, by slot
+    unsigned long long *best;             // 0 = slot untouched
     unsigned long long *sum;
     unsigned *npar;
 };
 
-__global__ void k_slot_clear(crdt_refmerge_out out, SlotAcc acc, uint32_t n) {
-    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
-        out.st_kind[s] = 0;               // untouched slot: key absent from CurrentState
-        out.st_str[s] = 0;
-        out.st_sum[s] = 0;
-        acc.best[s] = 0;
-        acc.nent[s] = 0;
-        acc.sum[s] = 0;
-        acc.npar[s] = 0;
+__global__ void k_rm_ntiles(crdt_refmerge_in in, uint32_t *__restrict__ nt) {
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
+        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (in.r_off[p + 1] - in.r_off[p]);
+        nt[p] = (uint32_t)((n + MT - 1) / MT);
     }
 }
 
-// kv range of new-Diff entry o, clamped to the arena
-__device__ __forceinline__ void entry_kv(const crdt_refmerge_in &in, const crdt_refmerge_out &out, uint64_t o,
-                                         uint64_t *kb, uint64_t *ke) {
-    const int64_t src = out.src[o];
-    if (src >= 0) {
-        *kb = in.l_kv[src];
-        *ke = in.l_kv[src + 1];
-    } else {
-        const uint64_t g = (uint64_t)(-(src + 1));
-        *kb = in.r_kv[g];
-        *ke = in.r_kv[g + 1];
+// per-tile geometry (tbase = exclusive scan of the tile counts)
+__global__ void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, TileGeo *__restrict__ geo) {
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
+        TileGeo g;
+        g.p = p;
+        g.lb = in.l_off[p];
+        g.nl = in.l_off[p + 1] - g.lb;
+        g.rb = in.r_off[p];
+        g.nr = in.r_off[p + 1] - g.rb;
+        g.maxl = g.nl ? in.l_ts[g.lb + g.nl - 1] : 0;
+        const uint64_t t0 = tbase[p], t1 = tbase[p + 1];
+        g.first = (uint32_t)t0;
+        for (uint64_t t = t0; t < t1; ++t) {
+            g.d0 = (t - t0) * MT;
+            g.d1 = g.d0 + MT < g.nl + g.nr ? g.d0 + MT : g.nl + g.nr;
+            geo[t] = g;
+        }
     }
-    if (*ke > in.n_kv) *ke = in.n_kv;     // malformed ranges never read out of bounds
+}
+
+// Merge-path split of diagonal d (first d items of the merge): the number of
+// L items among them.  Whole wave, 64-ary: pred(a) = L[a] <= R[d-1-a] holds
+// for a < split and fails from it on.
+__device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, const int64_t *R, uint64_t nr,
+                                               uint64_t d, int lane) {
+    uint64_t lo = d > nr ? d - nr : 0, hi = d < nl ? d : nl;
+    while (lo < hi) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t a = lo + (uint64_t)lane * step;
+        const bool valid = a < hi;
+        const bool pred = valid && L[a] <= R[d - 1 - a];
+        const int c = __popcll(__ballot(pred));         // monotone: lanes 0..c-1
+        const int nv = __popcll(__ballot(valid));
+        const uint64_t nlo = c ? lo + (uint64_t)(c - 1) * step + 1 : lo;
+        const uint64_t nhi = c < nv ? lo + (uint64_t)c * step : hi;
+        lo = nlo;
+        hi = nhi;
+    }
+    return lo;
+}
+
+// sm[0] = L[a0-1] (when a0 > 0), sm[1..na] = L[a0..a1), sm[na+1..] = R[b0..b1).
+// Thread-level merge of diagonals [k0, k1) of the tile: bit i of *isl / *emit
+// = item i is an L entry / is emitted.  Returns the split (ia) at k0.
+__device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na, uint32_t nb, uint32_t k0,
+                                                 uint32_t k1, bool has_prev0, bool l_any, int64_t maxl,
+                                                 uint32_t *isl, uint32_t *emit) {
+    uint32_t lo = k0 > nb ? k0 - nb : 0, hi = k0 < na ? k0 : na;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sm[1 + mid] <= sm[1 + na + (k0 - 1 - mid)]) lo = mid + 1;
+        else hi = mid;
+    }
+    uint32_t ia = lo, ib = k0 - lo;
+    const uint32_t ia0 = ia;
+    uint32_t fl = 0, fe = 0;
+    for (uint32_t k = k0, i = 0; k < k1; ++k, ++i) {
+        const bool take_l = ia < na && (ib >= nb || sm[1 + ia] <= sm[1 + na + ib]);
+        if (take_l) {
+            fl |= 1u << i;
+            fe |= 1u << i;
+            ++ia;
+        } else {
+            const int64_t r = sm[1 + na + ib];
+            const bool has_prev = ia > 0 || has_prev0;
+            const bool dup = has_prev && sm[ia] == r;    // sm[ia] = L entry just before (global a0+ia-1)
+            if (l_any && r < maxl && !dup) fe |= 1u << i;
+            ++ib;
+        }
+    }
+    *isl = fl;
+    *emit = fe;
+    return ia0;
+}
+
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_w, uint32_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int k = 0; k < MB / 64; ++k) {
+        base += k < w ? s_w[k] : 0;
+        tot += s_w[k];
+    }
+    *total = tot;
+    return base + x - v;
+}
+
+__device__ __forceinline__ uint32_t table_find(uint32_t *t_slot, uint32_t slot) {
+    uint32_t h = (slot * 2654435761u) >> 23;             // 9-bit hash
+    for (int probe = 0; probe < 16; ++probe, h = (h + 1) & (TT - 1)) {
+        uint32_t c = t_slot[h];                          // plain read first: most pairs hit a claimed entry
+        if (c == kEmpty) c = atomicCAS(&t_slot[h], kEmpty, slot);
+        if (c == kEmpty || c == slot) return h;
+    }
+    return kEmpty;
+}
+
+// Fold one (slot, string) pair of a remote-origin entry whose rank in the
+// replica's merge sequence is `rank` (>= 1).
+__device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *t_best, unsigned long long *t_sum,
+                                          uint32_t *t_npar, const SlotAcc &acc, bool use_lds, uint32_t slot,
+                                          uint32_t v, uint64_t rank, bool okv, int64_t x) {
+    const unsigned long long best = (rank << 32) | v;
+    const uint32_t idx = use_lds ? table_find(t_slot, slot) : kEmpty;
+    if (idx != kEmpty) {
+        atomicMax(&t_best[idx], best);
+        if (okv) {
+            atomicAdd(&t_sum[idx], (unsigned long long)x);   // mod 2^64 (main.go:95)
+            atomicAdd(&t_npar[idx], 1u);
+        }
+    } else {                                             // table full: straight to the slot
+        atomicMax(&acc.best[slot], best);
+        if (okv) {
+            atomicAdd(&acc.sum[slot], (unsigned long long)x);
+            atomicAdd(&acc.npar[slot], 1u);
+        }
+    }
+}
+
+// Pass 1: split at the tile start (kept for pass 2), inserted-R count, and
+// the replay fold of the tile's emitted remote-origin entries.  An emitted
+// entry's rank in the replica's merge sequence (d0 + local diagonal + 1)
+// orders the replica's new Diff like its ts, so best = rank << 32 | string
+// picks the max-ts holder without knowing output positions.
+// Grid = an upper bound on the tile count: blocks past it zero their count.
+__global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, uint32_t replicas,
+                                                 const uint64_t *__restrict__ tbase,
+                                                 const TileGeo *__restrict__ geo, uint64_t *__restrict__ ta,
+                                                 uint32_t *__restrict__ tcnt, const uint8_t *__restrict__ ok,
+                                                 const int64_t *__restrict__ val, SlotAcc acc, int diag) {
+    __shared__ alignas(16) int64_t s_buf[MT + 1];        // merge input, then the replay table
+    __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> local diagonal + 1, 0 = dropped
+    __shared__ uint64_t s_a[2];
+    __shared__ uint32_t s_w[MB / 64];
+    const uint64_t t = blockIdx.x;
+    if (t >= tbase[replicas]) {
+        if (threadIdx.x == 0) tcnt[t] = 0;
+        return;
+    }
+    const TileGeo g = geo[t];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < 2) {
+        const uint64_t a = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, w ? g.d1 : g.d0, lane);
+        if (lane == 0) s_a[w] = a;
+    }
+    __syncthreads();
+    const uint64_t a0 = s_a[0], a1 = s_a[1];
+    if (threadIdx.x == 0) ta[t] = a0;
+    const uint32_t na = (uint32_t)(a1 - a0), nb = (uint32_t)(g.d1 - g.d0) - na;
+    const uint64_t b0 = g.d0 - a0;
+    int64_t *sm = s_buf;
+    for (uint32_t k = threadIdx.x; k < na; k += MB) sm[1 + k] = in.l_ts[g.lb + a0 + k];
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[g.rb + b0 + k];
+    if (threadIdx.x == 0 && a0 > 0) sm[0] = in.l_ts[g.lb + a0 - 1];
+    const uint32_t n = na + nb;
+    // Replay-fold operands of this thread's MI entries (e = tid + f*MB),
+    // loaded before the merge so their latency hides behind it: kv range
+    // (remote-origin entries only; *Command values are skipped, main.go:80),
+    // then the first kv of each entry.  Further kvs (rare: the reference's
+    // load generator writes one kv per entry) take a serial tail loop.
+    const bool fold = diag != 1 && in.n_slots != 0;
+    uint64_t e_kb[MI];
+    uint32_t e_cnt[MI], e_slot[MI], e_v[MI];
+#pragma unroll
+    for (int f = 0; f < MI; ++f) {
+        const uint32_t e = threadIdx.x + (uint32_t)f * MB;
+        e_kb[f] = 0;
+        e_cnt[f] = 0;
+        if (fold && e < n) {
+            const bool r = e >= na;
+            const uint32_t li = r ? e - na : e;
+            const bool remote = r || in.l_origin[g.lb + a0 + li] == 0;
+            if (remote) {
+                const uint64_t *kv = r ? in.r_kv + g.rb + b0 + li : in.l_kv + g.lb + a0 + li;
+                const uint64_t kb = kv[0], ke = kv[1] < in.n_kv ? kv[1] : in.n_kv;   // stay in bounds
+                e_kb[f] = kb;
+                e_cnt[f] = kb < ke ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < MI; ++f) {
+        e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
+        e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
+    }
+    const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
+    const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
+    uint32_t isl, emit;
+    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.nl > 0, g.maxl, &isl, &emit);
+    {
+        uint32_t ia = ia0, ib = k0 - ia0;
+        for (uint32_t i = 0; i < k1 - k0; ++i) {
+            const uint16_t dk = (emit >> i & 1u) ? (uint16_t)(k0 + i + 1) : (uint16_t)0;
+            if (isl >> i & 1u) s_dk[ia++] = dk;
+            else s_dk[na + ib++] = dk;
+        }
+    }
+    uint32_t total;
+    block_excl_sum((uint32_t)__popc(emit & ~isl), s_w, &total);   // (its barrier also retires sm)
+    if (threadIdx.x == 0) tcnt[t] = total;
+    if (!fold) return;
+    bool e_ok[MI];
+    int64_t e_x[MI];
+#pragma unroll
+    for (int f = 0; f < MI; ++f) {
+        const bool good = e_slot[f] < in.n_slots && e_v[f] < in.n_str;
+        e_ok[f] = good ? ok[e_v[f]] != 0 : false;
+        e_x[f] = good ? val[e_v[f]] : 0;                 // val[] is 0 where !ok
+    }
+    uint32_t *t_slot = reinterpret_cast<uint32_t *>(s_buf);
+    unsigned long long *t_best = reinterpret_cast<unsigned long long *>(s_buf) + TT / 2;
+    unsigned long long *t_sum = t_best + TT;
+    uint32_t *t_npar = reinterpret_cast<uint32_t *>(t_sum + TT);
+    for (int h = threadIdx.x; h < TT; h += MB) {
+        t_slot[h] = kEmpty;
+        t_best[h] = 0;
+        t_sum[h] = 0;
+        t_npar[h] = 0;
+    }
+    __syncthreads();
+    const bool use_lds = diag != 3;
+#pragma unroll
+    for (int f = 0; f < MI; ++f) {
+        const uint32_t e = threadIdx.x + (uint32_t)f * MB;
+        const uint32_t dk = e_cnt[f] ? s_dk[e] : 0u;     // 0: dropped R entry / no kv
+        if (!dk) continue;
+        const uint64_t rank = g.d0 + dk;
+        if (diag == 4) {                                 // timing diagnostic: loads only, no table
+            if (((rank << 32) ^ e_v[f] ^ (uint64_t)e_x[f]) == 0x123456789ull) acc.npar[0] = e_slot[f];
+            continue;
+        }
+        if (e_slot[f] < in.n_slots && e_v[f] < in.n_str)
+            fold_pair(t_slot, t_best, t_sum, t_npar, acc, use_lds, e_slot[f], e_v[f], rank, e_ok[f], e_x[f]);
+        for (uint64_t q = e_kb[f] + 1; q < e_kb[f] + e_cnt[f]; ++q) {
+            const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
+            if (slot >= in.n_slots || v >= in.n_str) continue;
+            const bool okv = ok[v] != 0;
+            fold_pair(t_slot, t_best, t_sum, t_npar, acc, use_lds, slot, v, rank, okv, okv ? val[v] : 0);
+        }
+    }
+    __syncthreads();
+    if (diag == 2) return;
+    for (int h = threadIdx.x; h < TT; h += MB) {
+        const uint32_t slot = t_slot[h];
+        if (slot == kEmpty) continue;
+        atomicMax(&acc.best[slot], t_best[h]);
+        if (t_npar[h]) {
+            atomicAdd(&acc.sum[slot], t_sum[h]);
+            atomicAdd(&acc.npar[slot], t_npar[h]);
+        }
+    }
+}
+
+// Pass 2: re-merge, stage the tile's new-Diff slice in LDS (over the merge
+// input once it is dead) and write it coalesced.  ic = exclusive scan of
+// tcnt: inserted R entries before tile t (all replicas), so the slice starts
+// at l_off[p] + a0 + ic[t].
+__global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, uint32_t replicas,
+                                                 const uint64_t *__restrict__ tbase,
+                                                 const TileGeo *__restrict__ geo, const uint64_t *__restrict__ ta,
+                                                 const uint64_t *__restrict__ ic, crdt_refmerge_out out) {
+    __shared__ alignas(16) int64_t s_buf[MT + 1];
+    __shared__ uint8_t so[MT];                           // origins of the tile's L entries
+    __shared__ uint16_t s_idx[MT];                       // output slot -> entry (bit 15: R)
+    __shared__ uint32_t s_w[MB / 64];
+    const uint64_t t = blockIdx.x;
+    if (t >= tbase[replicas]) return;
+    const TileGeo g = geo[t];
+    const uint64_t a0 = ta[t];
+    const uint64_t a1 = t + 1 < tbase[g.p + 1] ? ta[t + 1] : g.nl;
+    const uint64_t ict = ic[t];
+    const uint32_t na = (uint32_t)(a1 - a0), nb = (uint32_t)(g.d1 - g.d0) - na;
+    const uint64_t b0 = g.d0 - a0;
+    int64_t *sm = s_buf;
+    for (uint32_t k = threadIdx.x; k < na; k += MB) {
+        sm[1 + k] = in.l_ts[g.lb + a0 + k];
+        so[k] = in.l_origin[g.lb + a0 + k];
+    }
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[g.rb + b0 + k];
+    if (threadIdx.x == 0 && a0 > 0) sm[0] = in.l_ts[g.lb + a0 - 1];
+    __syncthreads();
+    const uint32_t n = na + nb;
+    const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
+    const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
+    uint32_t isl, emit;
+    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.nl > 0, g.maxl, &isl, &emit);
+    int64_t vts[MI];
+    uint32_t vid[MI];
+    {
+        uint32_t ia = ia0, ib = k0 - ia0;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            vts[i] = 0;
+            vid[i] = 0;
+            if ((uint32_t)i < k1 - k0) {
+                if (isl >> i & 1u) {
+                    vts[i] = sm[1 + ia];
+                    vid[i] = ia++;
+                } else {
+                    vts[i] = sm[1 + na + ib];
+                    vid[i] = 0x8000u | ib++;
+                }
+            }
+        }
+    }
+    uint32_t total;
+    uint32_t pos = block_excl_sum((uint32_t)__popc(emit), s_w, &total);   // (its barrier also retires sm)
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        if ((uint32_t)i < k1 - k0 && (emit >> i & 1u)) {
+            s_buf[pos] = vts[i];
+            s_idx[pos] = (uint16_t)vid[i];
+            ++pos;
+        }
+    }
+    __syncthreads();
+    const uint64_t ob = g.lb + a0 + ict;                 // l_off[p] == g.lb
+    for (uint32_t k = threadIdx.x; k < total; k += MB) {
+        const uint32_t id = s_idx[k], li = id & 0x7FFFu;
+        const bool r = id >> 15;
+        out.ts[ob + k] = s_buf[k];
+        out.src[ob + k] = r ? -(int64_t)(g.rb + b0 + li) - 1 : (int64_t)(g.lb + a0 + li);
+        out.origin[ob + k] = r ? 0 : so[li];
+    }
+}
+
+// ---- single-workgroup planning / scan for the common batch sizes (one
+// launch instead of the multi-kernel device scan: every launch here costs
+// ~4 us, more than the work)
+constexpr int SB = 1024;                  // threads of the single-workgroup kernels
+constexpr size_t kSmallPlan = 1u << 16;   // replicas / tiles handled by one workgroup
+
+__device__ __forceinline__ uint64_t block_excl_u64(uint64_t v, uint64_t *s_w, uint64_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint64_t base = 0, tot = 0;
+    for (int k = 0; k < SB / 64; ++k) {
+        base += k < w ? s_w[k] : 0;
+        tot += s_w[k];
+    }
+    __syncthreads();                                     // s_w reused by the next call
+    *total = tot;
+    return base + x - v;
+}
+
+// Exclusive scan of n <= kSmallPlan values by one workgroup: each thread
+// sums a contiguous chunk (independent loads), one block scan, then the
+// chunk is re-read (L2-hot) and written.  out[n] = total.
+template <typename Get>
+__device__ __forceinline__ void small_scan(Get get, uint32_t n, uint64_t *__restrict__ out, uint64_t *s_w) {
+    const uint32_t per = (n + SB - 1) / SB;
+    const uint32_t b = threadIdx.x * per < n ? threadIdx.x * per : n;
+    const uint32_t e = b + per < n ? b + per : n;
+    uint64_t sum = 0;
+    for (uint32_t i = b; i < e; ++i) sum += get(i);
+    uint64_t tot;
+    uint64_t x = block_excl_u64(sum, s_w, &tot);
+    for (uint32_t i = b; i < e; ++i) {
+        out[i] = x;
+        x += get(i);
+    }
+    if (threadIdx.x == 0) out[n] = tot;
+}
+
+// tbase = exclusive scan of the per-replica tile counts (tbase[np] = tiles)
+__global__ __launch_bounds__(SB) void k_rm_plan_small(crdt_refmerge_in in, uint64_t *__restrict__ tbase) {
+    __shared__ uint64_t s_w[SB / 64];
+    small_scan([&](uint32_t p) -> uint64_t {
+        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (in.r_off[p + 1] - in.r_off[p]);
+        return (n + MT - 1) / MT;
+    }, in.replicas, tbase, s_w);
+}
+
+// ic = exclusive scan of tcnt[0..n) (ic[n] = total), then
+// out.off[p] = l_off[p] + ic[tbase[p]]
+__global__ __launch_bounds__(SB) void k_rm_scan_small(const uint32_t *__restrict__ tcnt, uint32_t n,
+                                                      uint64_t *__restrict__ ic, crdt_refmerge_in in,
+                                                      const uint64_t *__restrict__ tbase,
+                                                      uint64_t *__restrict__ out_off) {
+    __shared__ uint64_t s_w[SB / 64];
+    small_scan([&](uint32_t i) -> uint64_t { return tcnt[i]; }, n, ic, s_w);
+    __syncthreads();                                     // ic visible to the whole workgroup
+    for (uint32_t p = threadIdx.x; p <= in.replicas; p += SB) out_off[p] = in.l_off[p] + ic[tbase[p]];
+}
+
+// Go Atoi over the string arena and the replay accumulators' reset, one launch.
+__global__ void k_rm_prep(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, uint64_t nstr,
+                          uint8_t *__restrict__ ok, int64_t *__restrict__ val, SlotAcc acc, uint32_t ns) {
+    const uint64_t n = nstr > ns ? nstr : ns;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        if (i < nstr) {
+            int64_t v = 0;
+            const bool good = go_atoi(bytes + off[i], off[i + 1] - off[i], &v);
+            ok[i] = good;
+            val[i] = good ? v : 0;
+        }
+        if (i < ns) {
+            acc.best[i] = 0;
+            acc.sum[i] = 0;
+            acc.npar[i] = 0;
+        }
+    }
+}
+
+// out.off[p] = l_off[p] + inserted R entries of replicas before p
+__global__ void k_out_off(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, const uint64_t *__restrict__ ic,
+                          uint64_t *__restrict__ out_off) {
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p <= in.replicas; p += gridDim.x * 256)
+        out_off[p] = in.l_off[p] + ic[tbase[p]];
 }
 
 // Per-key closed form (main.go:82-96): verbatim base unless the base parses
 // AND another holder's value parses; then Itoa(sum) with int64 wrap.
-__device__ __forceinline__ void slot_final(const crdt_refmerge_out &out, const uint8_t *ok, uint32_t slot,
-                                           unsigned long long best, unsigned npar, unsigned long long sum) {
-    const uint32_t str = (uint32_t)best;
-    const bool sum_form = ok[str] && npar >= 2;
-    out.st_kind[slot] = sum_form ? 2 : 1;
-    out.st_str[slot] = str;
-    out.st_sum[slot] = sum_form ? (int64_t)sum : 0;
-}
-
-__global__ __launch_bounds__(256) void k_replay(crdt_refmerge_in in, const uint8_t *__restrict__ ok,
-                                                const int64_t *__restrict__ val, crdt_refmerge_out out,
-                                                SlotAcc acc) {
-    __shared__ uint32_t t_slot[RT];
-    __shared__ unsigned long long t_best[RT];
-    __shared__ unsigned long long t_sum[RT];
-    __shared__ uint32_t t_nent[RT], t_npar[RT];
-    __shared__ int s_over;
-    const int tid = threadIdx.x;
-    for (uint32_t p = blockIdx.x; p < in.replicas; p += gridDim.x) {
-        for (int h = tid; h < RT; h += 256) {
-            t_slot[h] = kEmpty;
-            t_best[h] = 0;
-            t_sum[h] = 0;
-            t_nent[h] = 0;
-            t_npar[h] = 0;
+__global__ void k_slot_final(crdt_refmerge_out out, SlotAcc acc, const uint8_t *__restrict__ ok, uint32_t n) {
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        const unsigned long long best = acc.best[s];
+        if (!best) {                                     // no remote holder: absent from CurrentState
+            out.st_kind[s] = 0;
+            out.st_str[s] = 0;
+            out.st_sum[s] = 0;
+            continue;
         }
-        if (tid == 0) s_over = 0;
-        __syncthreads();
-        const uint64_t ob = out.off[p], oe = out.off[p + 1];
-        for (uint64_t o = ob + tid; o < oe; o += 256) {
-            if (out.origin[o]) continue;                 // *Command: skipped (main.go:80)
-            uint64_t kb, ke;
-            entry_kv(in, out, o, &kb, &ke);
-            const unsigned long long pos = (unsigned long long)(o - ob) << 32;
-            for (uint64_t q = kb; q < ke; ++q) {
-                const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
-                if (slot >= in.n_slots || v >= in.n_str) continue;
-                uint32_t h = (slot * 2654435761u) >> 22;   // 10-bit hash
-                int idx = -1;
-                for (int probe = 0; probe < 32; ++probe, h = (h + 1) & (RT - 1)) {
-                    const uint32_t c = atomicCAS(&t_slot[h], kEmpty, slot);
-                    if (c == kEmpty || c == slot) {
-                        idx = (int)h;
-                        break;
-                    }
-                }
-                if (idx < 0) {
-                    s_over = 1;
-                    continue;
-                }
-                atomicMax(&t_best[idx], pos | v);
-                atomicAdd(&t_nent[idx], 1u);
-                if (ok[v]) {
-                    atomicAdd(&t_sum[idx], (unsigned long long)val[v]);   // mod 2^64 (main.go:95)
-                    atomicAdd(&t_npar[idx], 1u);
-                }
-            }
-        }
-        __syncthreads();
-        if (!s_over) {
-            for (int h = tid; h < RT; h += 256)
-                if (t_slot[h] != kEmpty) slot_final(out, ok, t_slot[h], t_best[h], t_npar[h], t_sum[h]);
-        } else {
-            // too many distinct keys for the table: this replica again through
-            // its own (disjoint) slice of the global accumulators
-            for (uint64_t o = ob + tid; o < oe; o += 256) {
-                if (out.origin[o]) continue;
-                uint64_t kb, ke;
-                entry_kv(in, out, o, &kb, &ke);
-                const unsigned long long pos = (unsigned long long)(o - ob) << 32;
-                for (uint64_t q = kb; q < ke; ++q) {
-                    const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
-                    if (slot >= in.n_slots || v >= in.n_str) continue;
-                    atomicMax(&acc.best[slot], pos | v);
-                    atomicAdd(&acc.nent[slot], 1u);
-                    if (ok[v]) {
-                        atomicAdd(&acc.sum[slot], (unsigned long long)val[v]);
-                        atomicAdd(&acc.npar[slot], 1u);
-                    }
-                }
-            }
-            __threadfence();
-            __syncthreads();
-            for (uint64_t o = ob + tid; o < oe; o += 256) {
-                if (out.origin[o]) continue;
-                uint64_t kb, ke;
-                entry_kv(in, out, o, &kb, &ke);
-                for (uint64_t q = kb; q < ke; ++q) {
-                    const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
-                    if (slot >= in.n_slots || v >= in.n_str) continue;
-                    slot_final(out, ok, slot,
-                               __hip_atomic_load(&acc.best[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __hip_atomic_load(&acc.npar[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               __hip_atomic_load(&acc.sum[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                }
-            }
-        }
-        __syncthreads();                                 // table reused by the next replica
+        const uint32_t str = (uint32_t)best;
+        const bool sum_form = ok[str] && acc.npar[s] >= 2;
+        out.st_kind[s] = sum_form ? 2 : 1;
+        out.st_str[s] = str;
+        out.st_sum[s] = sum_form ? (int64_t)acc.sum[s] : 0;
     }
 }
 
@@ -303,40 +578,58 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
     if (in.n_str && (!in.str_bytes || !in.str_off)) return CRDT_E_INVAL;
     if (in.n_kv && !in.n_str) return CRDT_E_INVAL;
 
-    const size_t nr = in.n_r, ns = in.n_slots, nstr = in.n_str;
-    const size_t need = Carve::round((nr + 1) * 4) + Carve::round(nr * 8 + 8) + Carve::round((nr + 1) * 8) +
-                        scan_tmp_bytes(nr) + Carve::round(nstr + 1) + Carve::round(nstr * 8 + 8) +
-                        Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) * 2 + 4096;
+    const size_t nr = in.n_r, ns = in.n_slots, nstr = in.n_str, np = in.replicas;
+    const size_t tmax = (in.n_l + nr) / MT + np + 1;             // >= tiles over all replicas
+    if (tmax > 0x7fffffffULL) return CRDT_E_RANGE;
+    const size_t need = Carve::round(np * 4 + 4) + Carve::round((np + 1) * 8) + scan_tmp_bytes(std::max(np, tmax)) +
+                        Carve::round((tmax + 1) * sizeof(TileGeo)) + Carve::round(tmax * 8 + 8) * 2 +
+                        Carve::round(tmax * 4 + 4) + Carve::round(nstr + 1) + Carve::round(nstr * 8 + 8) +
+                        Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) + 4096;
     rc = ws_reserve(ctx, need);
     if (rc) return rc;
     Carve w(ctx->ws);
-    uint32_t *flag = w.take<uint32_t>(nr + 1);
-    uint64_t *rpos = w.take<uint64_t>(nr + 1);
-    uint64_t *ib = w.take<uint64_t>(nr + 1);
-    void *tmp = w.take<char>(scan_tmp_bytes(nr));
+    uint32_t *nt = w.take<uint32_t>(np + 1);
+    uint64_t *tbase = w.take<uint64_t>(np + 1);
+    void *tmp = w.take<char>(scan_tmp_bytes(std::max(np, tmax)));
+    TileGeo *geo = w.take<TileGeo>(tmax + 1);
+    uint64_t *ta = w.take<uint64_t>(tmax + 1);
+    uint64_t *ic = w.take<uint64_t>(tmax + 1);
+    uint32_t *tcnt = w.take<uint32_t>(tmax + 1);
     uint8_t *ok = w.take<uint8_t>(nstr + 1);
     int64_t *val = w.take<int64_t>(nstr + 1);
     SlotAcc acc;
     acc.best = w.take<unsigned long long>(ns + 1);
     acc.sum = w.take<unsigned long long>(ns + 1);
-    acc.nent = w.take<unsigned>(ns + 1);
     acc.npar = w.take<unsigned>(ns + 1);
 
     const hipStream_t s = ctx->stream;
     const unsigned cap = (unsigned)ctx->num_cus * 8;
-    if (nstr) k_atoi<<<grid_for(nstr, 256, cap), 256, 0, s>>>(in.str_bytes, in.str_off, nstr, ok, val);
-    if (nr) k_walk_flags<<<grid_for(nr, 256, cap), 256, 0, s>>>(in, flag, rpos);
+    const uint32_t reps = in.replicas;
+    if (nstr || ns)
+        k_rm_prep<<<grid_for(std::max(nstr, ns), 256, cap), 256, 0, s>>>(in.str_bytes, in.str_off, nstr, ok, val, acc,
+                                                                          (uint32_t)ns);
+    if (np <= kSmallPlan) {
+        k_rm_plan_small<<<1, SB, 0, s>>>(in, tbase);
+    } else {
+        k_rm_ntiles<<<grid_for(np, 256, cap), 256, 0, s>>>(in, nt);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+        rc = exclusive_scan_u32(ctx, nt, tbase, np, tmp);         // tbase[np] = tile count
+        if (rc) return rc;
+    }
+    k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, geo);
+    // grids = an upper bound on the tile count; blocks past tbase[np] exit at once
+    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, reps, tbase, geo, ta, tcnt, ok, val, acc, g_rm_diag);
     rc = check_launch(ctx);
     if (rc) return rc;
-    rc = exclusive_scan_u32(ctx, flag, ib, nr, tmp);
-    if (rc) return rc;
-    k_out_off<<<grid_for((size_t)in.replicas + 1, 256, cap), 256, 0, s>>>(in, ib, out.off);
-    if (in.n_l) k_scatter_l<<<grid_for(in.n_l, 256, cap), 256, 0, s>>>(in, ib, out);
-    if (nr) k_scatter_r<<<grid_for(nr, 256, cap), 256, 0, s>>>(in, flag, rpos, ib, out);
-    if (ns) {
-        k_slot_clear<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, (uint32_t)ns);
-        if (in.n_l + nr) k_replay<<<std::min<unsigned>(in.replicas, (unsigned)ctx->num_cus * 4), 256, 0, s>>>(
-            in, ok, val, out, acc);
+    if (tmax <= kSmallPlan) {
+        k_rm_scan_small<<<1, SB, 0, s>>>(tcnt, (uint32_t)tmax, ic, in, tbase, out.off);
+    } else {
+        rc = exclusive_scan_u32(ctx, tcnt, ic, tmax, tmp);
+        if (rc) return rc;
+        k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
+    k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, reps, tbase, geo, ta, ic, out);
+    if (ns) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, ok, (uint32_t)ns);
     return check_launch(ctx);
 }

@@ -87,6 +87,27 @@ def test_packed_batch_matches_oracle(eng):
         assert m.sum() > 0
 
 
+def test_many_replicas_multi_kernel_plan(eng):
+    """> 65536 replicas (and tiles): the planning and tile-count scan take the
+    multi-kernel device-scan path instead of the single-workgroup one.
+    Replicas sampled across the batch are checked against the oracle, and
+    the new-Diff ranges against a host recount."""
+    from refmerge_util import oracle_packed_replica
+    h = synth.refmerge_packed(23, 70_000, 12)
+    out = eng.refmerge_batch(refmerge.to_device(h, eng.device))
+    off = out["off"].cpu().numpy()
+    ts, org, src = (out[k].cpu().numpy() for k in ("ts", "origin", "src"))
+    kind = out["st_kind"].cpu().numpy()
+    assert off[0] == 0 and np.all(np.diff(off) >= np.diff(h["l_off"]))
+    for p in list(range(0, 70_000, 997)) + [69_999]:
+        o_ts, o_or, o_src, k, _, _ = oracle_packed_replica(h, p)
+        a, b = int(off[p]), int(off[p + 1])
+        np.testing.assert_array_equal(ts[a:b], o_ts)
+        np.testing.assert_array_equal(org[a:b], o_or)
+        np.testing.assert_array_equal(src[a:b], o_src)
+        np.testing.assert_array_equal(kind[p * 62:(p + 1) * 62], k)
+
+
 def test_servers_batched_equals_single(eng):
     reps = synth.refmerge_demo(5, replicas=6, entries=2000, multi_key=0.2)
     batch = [_server_from(eng, d, r, 8080 + i) for i, (d, r) in enumerate(reps)]
@@ -142,9 +163,9 @@ def test_device_atoi_matches_go(eng):
 
 
 def test_many_keys_per_replica_matches_oracle(eng):
-    """Replicas with ~2500 distinct keys overflow the replay's 1024-entry LDS
-    table and take the per-replica global-accumulator path; mixed in one
-    batch with small replicas that stay in LDS."""
+    """Replicas with ~2500 distinct keys overflow the replay fold's 512-entry
+    per-tile LDS table, so part of their pairs go straight to the global slot
+    accumulators; mixed in one batch with small replicas that stay in LDS."""
     rng = np.random.default_rng(5)
     reps = []
     for r, nkeys in enumerate((2500, 40, 3000)):
