@@ -12,7 +12,7 @@ __all__ = ["CrdtError", "CrdtLibraryError", "LIB_PATH", "lib", "Engine", "TupleS
 
 
 def __getattr__(name):  # lazy: submodules load on first use
-    if name in ("Engine", "TupleSet", "as_u64", "u64_tensor", "sort_tuples"):
+    if name in ("Engine", "TupleSet", "as_u64", "u64_tensor"):
         from . import engine
         return getattr(engine, name)
     if name in ("Server", "NewServer", "Command", "Data", "Int64Comparator"):

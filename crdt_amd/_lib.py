@@ -109,6 +109,7 @@ SIGNATURES = {
     "crdt_orset_merge": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
                               C.POINTER(crdt_tuples), _P]),
     "crdt_tuples_sort": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples)]),
+    "crdt_u64_lower_bound": (_I, [_CTX, _P, _SZ, _P, _SZ, _P]),
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),
     "crdt_debug_set_stamps": (_I, [_CTX, _P, _SZ, C.POINTER(_SZ)]),
     "crdt_debug_set_grid": (_I, [C.POINTER(_SZ), C.POINTER(C.c_int)]),

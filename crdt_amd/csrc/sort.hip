@@ -391,7 +391,34 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
 
 }  // namespace crdt
 
+namespace crdt {
+// out[i] = lower_bound(v[0..n), probes[i]) in unsigned order: one thread per probe.
+__global__ void k_lower_bound_u64(const uint64_t *__restrict__ v, uint64_t n, const uint64_t *__restrict__ probes,
+                                  uint64_t m, uint64_t *__restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t x = probes[i];
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (v[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        out[i] = lo;
+    }
+}
+}  // namespace crdt
+
 using namespace crdt;
+
+extern "C" int crdt_u64_lower_bound(crdt_ctx *ctx, const uint64_t *sorted, size_t n, const uint64_t *probes, size_t m,
+                                    uint64_t *out) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (m == 0) return CRDT_OK;
+    if (!probes || !out || (n && !sorted)) return CRDT_E_INVAL;
+    k_lower_bound_u64<<<grid_for(m, 256, (unsigned)ctx->num_cus * 4), 256, 0, ctx->stream>>>(sorted, n, probes, m, out);
+    return check_launch(ctx);
+}
 
 extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, crdt_tuples *out) {
     int rc = bind(ctx);

@@ -234,6 +234,15 @@ class Engine:
         self._call("crdt_tuples_sort", C.byref(ct), n, C.byref(co))
         return out
 
+    def lower_bound_u64(self, sorted_u64: torch.Tensor, probes: torch.Tensor) -> torch.Tensor:
+        """lower_bound of every probe in an ascending uint64 (int64-stored)
+        device array, unsigned order (crdt_u64_lower_bound)."""
+        self._check(sorted_u64, probes, itemsize=8)
+        out = torch.empty(probes.numel(), dtype=torch.int64, device=self.device)
+        self._call("crdt_u64_lower_bound", sorted_u64.data_ptr(), sorted_u64.numel(), probes.data_ptr(),
+                   probes.numel(), out.data_ptr())
+        return out
+
     def count_unsorted(self, t: TupleSet) -> int:
         bad = torch.empty(1, dtype=torch.int64, device=self.device)
         ct = t.c()
@@ -305,33 +314,6 @@ class Engine:
         t = TupleSet.empty(n, self.device)
         ct = t.c()
         self._call("crdt_synth_set_tuples", seed, side, C.byref(ct), n, key_space)
-        if sort:
-            t = sort_tuples(t)
+        if sort:                                          # D1 inputs: the device tuple sort
+            t = self.sort_tuples(t)
         return t
-
-
-def sort_tuples(t: TupleSet) -> TupleSet:
-    """Stable sort by (key, ts, rep): input preparation for the D1 config.
-
-    Input prep only (not the measured path): the synthetic fields fit one
-    int64 composite (key < 2^37, ts < 2^20, rep < 2^6).
-    """
-    if len(t) == 0:
-        return t
-    kmax = int(t.key.max().item())
-    tmax = int(t.ts.max().item())
-    rmax = int(t.rep.max().item())
-    if kmax >= (1 << 37) or tmax >= (1 << 20) or rmax >= (1 << 6) or min(
-            int(t.key.min().item()), int(t.ts.min().item()), int(t.rep.min().item())) < 0:
-        # general case: three stable passes, least significant field first;
-        # uint64 fields are sign-flipped so signed argsort gives unsigned order
-        flip = torch.iinfo(torch.int64).min
-        order = torch.argsort(t.rep.to(torch.int64) & 0xFFFFFFFF, stable=True)
-        for f in (t.ts, t.key):
-            g = f[order] ^ flip
-            order = order[torch.argsort(g, stable=True)]
-    else:
-        comp = (t.key << 26) | (t.ts << 6) | t.rep.to(torch.int64)
-        order = torch.argsort(comp, stable=True)
-    return TupleSet(t.key[order].contiguous(), t.ts[order].contiguous(), t.rep[order].contiguous(),
-                    t.tomb[order].contiguous())

@@ -19,8 +19,9 @@ The reference's analog is pull gossip of the whole log over HTTP
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Tuple
+from typing import List, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -85,3 +86,77 @@ def allgather_v(t: torch.Tensor, group=None) -> torch.Tensor:
 def key_splitters(key_space: int, world: int) -> List[int]:
     """Equal-width key ranges [s_r, s_{r+1}) for `world` ranks (uint64 keys)."""
     return [key_space * r // world for r in range(world)] + [key_space]
+
+
+# ---------------------------------------------------------------- keyed sets (§8(e) D)
+KEY_END = 2**64                   # exclusive upper end of the uint64 key space
+
+
+def sample_keys(t, per: int) -> torch.Tensor:
+    """`per` keys at evenly spaced positions of a key-sorted TupleSet."""
+    n = len(t)
+    if n == 0 or per <= 0:
+        return t.key[:0]
+    idx = torch.arange(per, dtype=torch.int64, device=t.key.device) * n // per
+    return t.key[idx]
+
+
+def splitters_from_samples(samples: np.ndarray, world: int) -> List[int]:
+    """Rank r owns keys [s[r], s[r+1]); s[0] = 0, s[world] = 2^64, the inner
+    splitters are the world-quantiles of the pooled uint64 key sample."""
+    s = np.sort(np.asarray(samples, dtype=np.uint64))
+    inner = [int(s[(r * len(s)) // world]) if len(s) else 0 for r in range(1, world)]
+    return [0] + inner + [KEY_END]
+
+
+def sample_splitters(a, b, world: int, group=None, per: int = 256) -> List[int]:
+    """Balanced key splitters for a sharded set merge: every rank samples its
+    sorted inputs, the samples are all-gathered (one small exchange) and
+    every rank derives the same splitters from the pooled sample."""
+    loc = torch.cat([sample_keys(a, per), sample_keys(b, per)])
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        loc = allgather_v(loc, group)
+    return splitters_from_samples(loc.cpu().numpy().view(np.uint64), world)
+
+
+def key_range(eng, t, lo: int, hi: int):
+    """The tuples of a key-sorted TupleSet with lo <= key < hi (a view; one
+    device lower_bound per end, crdt_u64_lower_bound)."""
+    from .engine import TupleSet
+    n = len(t)
+    i, j = 0, n
+    if n:
+        probes = [lo] + ([hi] if hi < KEY_END else [])
+        pr = torch.tensor(np.array(probes, dtype=np.uint64).view(np.int64), device=t.key.device)
+        got = eng.lower_bound_u64(t.key, pr).cpu().tolist()
+        i = got[0]
+        j = got[1] if hi < KEY_END else n
+    return TupleSet(t.key[i:j], t.ts[i:j], t.rep[i:j], t.tomb[i:j])
+
+
+def merge_key_range(eng, a, b, lo: int, hi: int, lww: bool = True):
+    """One rank's share of a key-range-sharded merge: the LWW / OR-Set merge
+    of the [lo, hi) slices of both sorted inputs (outputs for a key depend
+    only on that key's tuples, so the shards are independent)."""
+    fn = eng.lww_merge if lww else eng.orset_merge
+    return fn(key_range(eng, a, lo, hi), key_range(eng, b, lo, hi))
+
+
+def sharded_set_merge(eng, a, b, lww: bool = True, group=None, gather: bool = True,
+                      splitters: Sequence[int] | None = None):
+    """Set merge of A and B (both key-sorted, present on every rank) sharded
+    by key range over the ranks of `group`: sample splitters (unless given),
+    merge this rank's range on its GPU, then (gather=True) an all-gather-v of
+    the four SoA fields in rank order -- the globally sorted merged state.
+    One rank (or no process group): the plain device merge."""
+    from .engine import TupleSet
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return merge_key_range(eng, a, b, 0, KEY_END, lww)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    spl = list(splitters) if splitters is not None else sample_splitters(a, b, world, group)
+    m = merge_key_range(eng, a, b, spl[rank], spl[rank + 1], lww)
+    if not gather:
+        return m
+    return TupleSet(allgather_v(m.key, group), allgather_v(m.ts, group), allgather_v(m.rep, group),
+                    allgather_v(m.tomb, group))
+

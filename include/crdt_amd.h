@@ -153,6 +153,10 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
  * minima; synchronises the stream once (to size the passes).  in and out
  * must not overlap.  n < 2^32. */
 int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, crdt_tuples *out);
+/* out[i] = lower_bound(sorted[0..n), probes[i]) in unsigned order, for m
+ * probes (device arrays): key-range sharding of a sorted set (§8(e) D). */
+int crdt_u64_lower_bound(crdt_ctx *ctx, const uint64_t *sorted_dev, size_t n, const uint64_t *probes_dev,
+                         size_t m, uint64_t *out_dev);
 int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
                                uint64_t *bad_dev);
 /* Diagnostic: after crdt_set_option("sets.stamps", 1), the last set merge

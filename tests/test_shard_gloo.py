@@ -26,6 +26,14 @@ def _port():
 
 
 def _worker(rank, world, port, q):
+    try:
+        _worker_body(rank, world, port, q)
+    except Exception:                        # surface the failure instead of a queue timeout
+        import traceback
+        q.put((rank, "ERROR", traceback.format_exc()))
+
+
+def _worker_body(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,11 +54,15 @@ def _worker(rank, world, port, q):
         ks = 5000
         sa = synth.sort_tuples_np(*synth.set_tuples(8, 0, 20000, ks))
         sb = synth.sort_tuples_np(*synth.set_tuples(8, 1, 20000, ks))
-        spl = shard.key_splitters(ks, world)
+        # sampled splitters (shard.sample_splitters: one all-gather of samples)
+        from crdt_amd.engine import TupleSet
+        spl = shard.sample_splitters(TupleSet.from_numpy(*sa, "cpu"), TupleSet.from_numpy(*sb, "cpu"), world,
+                                     per=64)
         lo, hi = spl[rank], spl[rank + 1]
 
         def part(s):
-            i, j = np.searchsorted(s[0], lo), np.searchsorted(s[0], hi)
+            i = np.searchsorted(s[0], np.uint64(lo))
+            j = np.searchsorted(s[0], np.uint64(hi)) if hi < shard.KEY_END else len(s[0])
             return tuple(x[i:j] for x in s)
 
         m = oracle.lww_merge(part(sa), part(sb))
@@ -58,7 +70,7 @@ def _worker(rank, world, port, q):
         tss = shard.allgather_v(torch.from_numpy(m[1].view(np.int64).copy())).numpy().view(np.uint64)
         full_m = oracle.lww_merge(sa, sb)
         q.put((rank, np.array_equal(got_fold, exp_fold), np.array_equal(keys, full_m[0]),
-               np.array_equal(tss, full_m[1]), (b, e)))
+               np.array_equal(tss, full_m[1]), (b, e), spl))
     finally:
         dist.destroy_process_group()
 
@@ -75,8 +87,12 @@ def test_gloo_sharded_exchange(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
-    for rank, fold_ok, keys_ok, ts_ok, _ in res:
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[1] != "ERROR", r[2]
+    for rank, fold_ok, keys_ok, ts_ok, _, _ in res:
         assert fold_ok, f"rank {rank}: sharded fold != oracle fold"
         assert keys_ok and ts_ok, f"rank {rank}: gathered LWW merge != oracle"
     assert res[0][4][1] == res[1][4][0]      # contiguous shards
+    assert res[0][5] == res[1][5]            # every rank derives the same splitters
+    assert res[0][5][0] == 0 and res[0][5][-1] == shard.KEY_END and len(res[0][5]) == world + 1
