@@ -71,6 +71,10 @@ class crdt_refmerge_out(C.Structure):
     ]
 
 
+class crdt_refmerge_acc(C.Structure):
+    _fields_ = [("best", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p)]
+
+
 _P = C.c_void_p
 _SZ = C.c_size_t
 _U64 = C.c_uint64
@@ -115,6 +119,14 @@ SIGNATURES = {
     "crdt_debug_set_grid": (_I, [C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
+    "crdt_refmerge_batch_ex": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out), _P,
+                                    C.POINTER(crdt_refmerge_acc)]),
+    "crdt_refmerge_local_maxl": (_I, [_CTX, C.POINTER(crdt_refmerge_in), _P]),
+    "crdt_refmerge_acc_rank": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, C.c_uint32, _P]),
+    "crdt_refmerge_acc_owner_str": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, _P, _P, _P]),
+    "crdt_refmerge_acc_set_best": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, _P, _P]),
+    "crdt_refmerge_finalize": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, _P, _P, _U64,
+                                    C.POINTER(crdt_refmerge_out)]),
     "crdt_server_new": (_I, [_CTX, _I, C.POINTER(_P)]),
     "crdt_server_free": (_I, [_P]),
     "crdt_server_init_state": (_I, [_P, _P, _P, _P, _P, _SZ]),

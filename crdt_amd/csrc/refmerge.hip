@@ -105,7 +105,10 @@ __global__ void k_rm_ntiles(crdt_refmerge_in in, uint32_t *__restrict__ nt) {
 }
 
 // per-tile geometry (tbase = exclusive scan of the tile counts)
-__global__ void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, TileGeo *__restrict__ geo) {
+// maxl_ovr (nullable): per-replica max(L) to insert below, instead of the
+// local L's last key (the ts-range-sharded merge passes the global max).
+__global__ void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, const int64_t *__restrict__ maxl_ovr,
+                         TileGeo *__restrict__ geo) {
     for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
         TileGeo g;
         g.p = p;
@@ -113,7 +116,8 @@ __global__ void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase
         g.nl = in.l_off[p + 1] - g.lb;
         g.rb = in.r_off[p];
         g.nr = in.r_off[p + 1] - g.rb;
-        g.maxl = g.nl ? in.l_ts[g.lb + g.nl - 1] : 0;
+        // empty L: INT64_MIN, below which no remote ts is ever inserted
+        g.maxl = maxl_ovr ? maxl_ovr[p] : g.nl ? in.l_ts[g.lb + g.nl - 1] : INT64_MIN;
         const uint64_t t0 = tbase[p], t1 = tbase[p + 1];
         g.first = (uint32_t)t0;
         for (uint64_t t = t0; t < t1; ++t) {
@@ -149,7 +153,7 @@ __device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, co
 // Thread-level merge of diagonals [k0, k1) of the tile: bit i of *isl / *emit
 // = item i is an L entry / is emitted.  Returns the split (ia) at k0.
 __device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na, uint32_t nb, uint32_t k0,
-                                                 uint32_t k1, bool has_prev0, bool l_any, int64_t maxl,
+                                                 uint32_t k1, bool has_prev0, int64_t maxl,
                                                  uint32_t *isl, uint32_t *emit) {
     uint32_t lo = k0 > nb ? k0 - nb : 0, hi = k0 < na ? k0 : na;
     while (lo < hi) {
@@ -170,7 +174,7 @@ __device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na,
             const int64_t r = sm[1 + na + ib];
             const bool has_prev = ia > 0 || has_prev0;
             const bool dup = has_prev && sm[ia] == r;    // sm[ia] = L entry just before (global a0+ia-1)
-            if (l_any && r < maxl && !dup) fe |= 1u << i;
+            if (r < maxl && !dup) fe |= 1u << i;
             ++ib;
         }
     }
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, uint32_t r
     const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
     uint32_t isl, emit;
-    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.nl > 0, g.maxl, &isl, &emit);
+    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.maxl, &isl, &emit);
     {
         uint32_t ia = ia0, ib = k0 - ia0;
         for (uint32_t i = 0; i < k1 - k0; ++i) {
@@ -396,7 +400,7 @@ __global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, uint32_t r
     const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
     uint32_t isl, emit;
-    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.nl > 0, g.maxl, &isl, &emit);
+    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.maxl, &isl, &emit);
     int64_t vts[MI];
     uint32_t vid[MI];
     {
@@ -562,9 +566,15 @@ extern "C" int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *bytes, const uint64
 }
 
 extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp) {
+    return crdt_refmerge_batch_ex(ctx, inp, outp, nullptr, nullptr);
+}
+
+extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                                      const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out) {
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
+    if (acc_out && inp->n_slots && (!acc_out->best || !acc_out->sum || !acc_out->npar)) return CRDT_E_INVAL;
     const crdt_refmerge_in in = *inp;
     const crdt_refmerge_out out = *outp;
     if (in.replicas == 0) return CRDT_OK;
@@ -574,7 +584,7 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
     if (in.n_r && !in.r_ts) return CRDT_E_INVAL;
     if (in.n_kv && (!in.kv_key || !in.kv_val)) return CRDT_E_INVAL;
     if (in.n_l + in.n_r && (!out.ts || !out.origin || !out.src)) return CRDT_E_INVAL;
-    if (in.n_slots && (!out.st_kind || !out.st_str || !out.st_sum)) return CRDT_E_INVAL;
+    if (!acc_out && in.n_slots && (!out.st_kind || !out.st_str || !out.st_sum)) return CRDT_E_INVAL;
     if (in.n_str && (!in.str_bytes || !in.str_off)) return CRDT_E_INVAL;
     if (in.n_kv && !in.n_str) return CRDT_E_INVAL;
 
@@ -601,6 +611,11 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
     acc.best = w.take<unsigned long long>(ns + 1);
     acc.sum = w.take<unsigned long long>(ns + 1);
     acc.npar = w.take<unsigned>(ns + 1);
+    if (acc_out) {                                               // the caller keeps the unreduced accumulators
+        acc.best = reinterpret_cast<unsigned long long *>(acc_out->best);
+        acc.sum = reinterpret_cast<unsigned long long *>(acc_out->sum);
+        acc.npar = acc_out->npar;
+    }
 
     const hipStream_t s = ctx->stream;
     const unsigned cap = (unsigned)ctx->num_cus * 8;
@@ -617,7 +632,7 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
         rc = exclusive_scan_u32(ctx, nt, tbase, np, tmp);         // tbase[np] = tile count
         if (rc) return rc;
     }
-    k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, geo);
+    k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
     // grids = an upper bound on the tile count; blocks past tbase[np] exit at once
     k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, reps, tbase, geo, ta, tcnt, ok, val, acc, g_rm_diag);
     rc = check_launch(ctx);
@@ -630,6 +645,94 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
     k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, reps, tbase, geo, ta, ic, out);
-    if (ns) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, ok, (uint32_t)ns);
+    if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, ok, (uint32_t)ns);
     return check_launch(ctx);
 }
+
+// ---------------------------------------------------------------- ts-range-sharded merge (§8(e))
+namespace crdt {
+__global__ void k_rm_local_maxl(crdt_refmerge_in in, int64_t *__restrict__ out) {
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
+        const uint64_t b = in.l_off[p], e = in.l_off[p + 1];
+        out[p] = e > b ? in.l_ts[e - 1] : INT64_MIN;
+    }
+}
+
+// mode 0: c = best ? shard << 40 | (best >> 32) : 0   (cross-shard rank of the max-ts holder)
+// mode 1: v = (c != 0 && c == cmax) ? (uint32)best : 0  (only the owning shard contributes)
+// mode 2: best = cmax ? 1 << 32 | (uint32)v : 0          (the reduced accumulator)
+__global__ void k_rm_acc_xform(crdt_refmerge_acc acc, uint32_t n, int mode, uint32_t shard, int64_t *__restrict__ c,
+                               const int64_t *__restrict__ cmax, int64_t *__restrict__ v) {
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        const uint64_t best = acc.best[s];
+        if (mode == 0) c[s] = best ? (int64_t)(((uint64_t)shard << 40) | (best >> 32)) : 0;
+        else if (mode == 1) v[s] = (c[s] != 0 && c[s] == cmax[s]) ? (int64_t)(uint32_t)best : 0;
+        else acc.best[s] = cmax[s] ? ((1ull << 32) | (uint32_t)v[s]) : 0;
+    }
+}
+}  // namespace crdt
+
+extern "C" int crdt_refmerge_local_maxl(crdt_ctx *ctx, const crdt_refmerge_in *in, int64_t *maxl_dev) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!in || !maxl_dev) return CRDT_E_INVAL;
+    if (in->replicas == 0) return CRDT_OK;
+    if (!in->l_off || (in->n_l && !in->l_ts)) return CRDT_E_INVAL;
+    k_rm_local_maxl<<<grid_for(in->replicas, 256, (unsigned)ctx->num_cus * 4), 256, 0, ctx->stream>>>(*in, maxl_dev);
+    return check_launch(ctx);
+}
+
+static int acc_xform(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n, int mode, uint32_t shard, int64_t *c,
+                     const int64_t *cmax, int64_t *v) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (n == 0) return CRDT_OK;
+    if (!acc || !acc->best || n > 0xffffffffULL) return CRDT_E_INVAL;
+    k_rm_acc_xform<<<grid_for(n, 256, (unsigned)ctx->num_cus * 4), 256, 0, ctx->stream>>>(*acc, (uint32_t)n, mode,
+                                                                                        shard, c, cmax, v);
+    return check_launch(ctx);
+}
+
+extern "C" int crdt_refmerge_acc_rank(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, uint32_t shard,
+                                      int64_t *c_dev) {
+    if (!c_dev || shard >= (1u << 23)) return CRDT_E_INVAL;
+    return acc_xform(ctx, acc, n_slots, 0, shard, c_dev, nullptr, nullptr);
+}
+
+extern "C" int crdt_refmerge_acc_owner_str(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots,
+                                           const int64_t *c_dev, const int64_t *cmax_dev, int64_t *v_dev) {
+    if (!c_dev || !cmax_dev || !v_dev) return CRDT_E_INVAL;
+    return acc_xform(ctx, acc, n_slots, 1, 0, const_cast<int64_t *>(c_dev), cmax_dev, v_dev);
+}
+
+extern "C" int crdt_refmerge_acc_set_best(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots,
+                                          const int64_t *cmax_dev, const int64_t *v_dev) {
+    if (!cmax_dev || !v_dev) return CRDT_E_INVAL;
+    return acc_xform(ctx, acc, n_slots, 2, 0, nullptr, cmax_dev, const_cast<int64_t *>(v_dev));
+}
+
+extern "C" int crdt_refmerge_finalize(crdt_ctx *ctx, const crdt_refmerge_acc *accp, size_t n_slots,
+                                      const uint8_t *str_bytes, const uint64_t *str_off, uint64_t n_str,
+                                      const crdt_refmerge_out *outp) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (n_slots == 0) return CRDT_OK;
+    if (!accp || !outp || !accp->best || !accp->sum || !accp->npar || n_slots > 0xffffffffULL) return CRDT_E_INVAL;
+    if (!outp->st_kind || !outp->st_str || !outp->st_sum) return CRDT_E_INVAL;
+    if (n_str && (!str_bytes || !str_off)) return CRDT_E_INVAL;
+    rc = ws_reserve(ctx, Carve::round(n_str + 1) + Carve::round(n_str * 8 + 8) + 4096);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    uint8_t *ok = w.take<uint8_t>(n_str + 1);
+    int64_t *val = w.take<int64_t>(n_str + 1);
+    const unsigned cap = (unsigned)ctx->num_cus * 8;
+    if (n_str) k_atoi<<<grid_for(n_str, 256, cap), 256, 0, ctx->stream>>>(str_bytes, str_off, n_str, ok, val);
+    SlotAcc acc;
+    acc.best = reinterpret_cast<unsigned long long *>(accp->best);
+    acc.sum = reinterpret_cast<unsigned long long *>(accp->sum);
+    acc.npar = accp->npar;
+    // a best string id >= n_str cannot occur (pairs with v >= n_str are never folded)
+    k_slot_final<<<grid_for(n_slots, 256, cap), 256, 0, ctx->stream>>>(*outp, acc, ok, (uint32_t)n_slots);
+    return check_launch(ctx);
+}
+

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import call, crdt_refmerge_in, crdt_refmerge_out, crdt_tuples
+from ._lib import call, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_out, crdt_tuples
 
 VC_EQUAL, VC_BEFORE, VC_AFTER, VC_CONCURRENT = 0, 1, 2, 3
 
@@ -250,11 +250,22 @@ class Engine:
         return int(bad.item())
 
     # ------------------------------------------------------------ RefMerge (a1-a3)
-    def refmerge_batch(self, packed: dict) -> dict:
+    def _refmerge_in(self, d: dict) -> crdt_refmerge_in:
+        return crdt_refmerge_in(
+            d["replicas"], int(d["n_slots"]), d["l_ts"].numel(), d["r_ts"].numel(), d["kv_key"].numel(),
+            d["str_off"].numel() - 1,
+            _ptr(d["l_off"]), _ptr(d["l_ts"]), _ptr(d["l_origin"]), _ptr(d["l_kv"]),
+            _ptr(d["r_off"]), _ptr(d["r_ts"]), _ptr(d["r_kv"]),
+            _ptr(d["kv_key"]), _ptr(d["kv_val"]), _ptr(d["str_bytes"]), _ptr(d["str_off"]))
+
+    def refmerge_batch(self, packed: dict, maxl: torch.Tensor | None = None,
+                       acc: dict | None = None) -> dict:
         """Run the batched bit-exact reference merge on a packed batch.
 
         ``packed`` holds device tensors produced by
         :func:`crdt_amd.refmerge.pack_batch`; returns device output tensors.
+        ``maxl`` / ``acc``: the ts-range-sharded form (crdt_refmerge_batch_ex;
+        see :func:`crdt_amd.shard.sharded_refmerge`).
         """
         d = packed
         n_l, n_r = d["l_ts"].numel(), d["r_ts"].numel()
@@ -269,14 +280,58 @@ class Engine:
             "st_str": torch.empty(max(n_slots, 1), dtype=torch.int32, device=dev),
             "st_sum": torch.empty(max(n_slots, 1), dtype=torch.int64, device=dev),
         }
-        cin = crdt_refmerge_in(
-            d["replicas"], n_slots, n_l, n_r, d["kv_key"].numel(), d["str_off"].numel() - 1,
-            _ptr(d["l_off"]), _ptr(d["l_ts"]), _ptr(d["l_origin"]), _ptr(d["l_kv"]),
-            _ptr(d["r_off"]), _ptr(d["r_ts"]), _ptr(d["r_kv"]),
-            _ptr(d["kv_key"]), _ptr(d["kv_val"]), _ptr(d["str_bytes"]), _ptr(d["str_off"]))
+        cin = self._refmerge_in(d)
         cout = crdt_refmerge_out(*(out[k].data_ptr() for k in
                                    ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum")))
-        self._call("crdt_refmerge_batch", C.byref(cin), C.byref(cout))
+        if maxl is None and acc is None:
+            self._call("crdt_refmerge_batch", C.byref(cin), C.byref(cout))
+        else:
+            if maxl is not None:
+                self._check(maxl, itemsize=8)
+            cacc = self._acc(acc) if acc is not None else None
+            self._call("crdt_refmerge_batch_ex", C.byref(cin), C.byref(cout),
+                       maxl.data_ptr() if maxl is not None else None, C.byref(cacc) if cacc is not None else None)
+        return out
+
+    # -- ts-range-sharded RefMerge steps
+    def refmerge_acc_new(self, n_slots: int) -> dict:
+        n = max(n_slots, 1)
+        return {"best": torch.zeros(n, dtype=torch.int64, device=self.device),
+                "sum": torch.zeros(n, dtype=torch.int64, device=self.device),
+                "npar": torch.zeros(n, dtype=torch.int32, device=self.device)}
+
+    @staticmethod
+    def _acc(acc: dict) -> crdt_refmerge_acc:
+        return crdt_refmerge_acc(acc["best"].data_ptr(), acc["sum"].data_ptr(), acc["npar"].data_ptr())
+
+    def refmerge_local_maxl(self, packed: dict) -> torch.Tensor:
+        out = torch.empty(max(packed["replicas"], 1), dtype=torch.int64, device=self.device)
+        cin = self._refmerge_in(packed)
+        self._call("crdt_refmerge_local_maxl", C.byref(cin), out.data_ptr())
+        return out
+
+    def refmerge_acc_rank(self, acc: dict, n_slots: int, shard: int) -> torch.Tensor:
+        c = torch.empty(max(n_slots, 1), dtype=torch.int64, device=self.device)
+        ca = self._acc(acc)
+        self._call("crdt_refmerge_acc_rank", C.byref(ca), n_slots, shard, c.data_ptr())
+        return c
+
+    def refmerge_acc_owner_str(self, acc: dict, n_slots: int, c: torch.Tensor, cmax: torch.Tensor) -> torch.Tensor:
+        v = torch.empty(max(n_slots, 1), dtype=torch.int64, device=self.device)
+        ca = self._acc(acc)
+        self._call("crdt_refmerge_acc_owner_str", C.byref(ca), n_slots, c.data_ptr(), cmax.data_ptr(), v.data_ptr())
+        return v
+
+    def refmerge_acc_set_best(self, acc: dict, n_slots: int, cmax: torch.Tensor, v: torch.Tensor) -> None:
+        ca = self._acc(acc)
+        self._call("crdt_refmerge_acc_set_best", C.byref(ca), n_slots, cmax.data_ptr(), v.data_ptr())
+
+    def refmerge_finalize(self, packed: dict, acc: dict, out: dict) -> dict:
+        ca = self._acc(acc)
+        cout = crdt_refmerge_out(*(out[k].data_ptr() for k in
+                                   ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum")))
+        self._call("crdt_refmerge_finalize", C.byref(ca), int(packed["n_slots"]), _ptr(packed["str_bytes"]),
+                   _ptr(packed["str_off"]), packed["str_off"].numel() - 1, C.byref(cout))
         return out
 
     def atoi_batch(self, str_bytes: torch.Tensor, str_off: torch.Tensor):

@@ -160,3 +160,39 @@ def sharded_set_merge(eng, a, b, lww: bool = True, group=None, gather: bool = Tr
     return TupleSet(allgather_v(m.key, group), allgather_v(m.ts, group), allgather_v(m.rep, group),
                     allgather_v(m.tomb, group))
 
+
+
+# ---------------------------------------------------------------- RefMerge by ts range (§8(e))
+def sharded_refmerge(eng, packed: dict, group=None) -> dict:
+    """(*Server).merge() of one batch of replicas whose Diff/RemoteDiff logs
+    are split by ts range over the ranks of `group` (rank r holds the r-th
+    ts range of every replica, ranks in ascending ts order; `packed` is this
+    rank's slice in the crdt_refmerge_in layout).  Exchange steps:
+      1. all-reduce(MAX) of every replica's local max(L): remote ts at or
+         above the GLOBAL max(L) are dropped (main.go:49);
+      2. the local merge with that max -> this rank's slice of the new Diff
+         (slices concatenate in rank order) + unreduced replay accumulators;
+      3. all-reduce(MAX) of the cross-rank rank of each key's max-ts holder,
+         all-reduce(SUM) of the owner's string id, of the wrapped sums and of
+         the parsable counts (main.go:82-96);
+      4. CurrentState from the reduced accumulators, identical on every rank.
+    Integer reductions only: bit-exact for any world size.  Returns the
+    refmerge_batch output dict (new-Diff slice + the full state)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    n_slots = int(packed["n_slots"])
+    maxl = eng.refmerge_local_maxl(packed)
+    if world > 1:
+        dist.all_reduce(maxl, op=dist.ReduceOp.MAX, group=group)     # int64 ts: signed MAX is exact
+    acc = eng.refmerge_acc_new(n_slots)
+    out = eng.refmerge_batch(packed, maxl=maxl, acc=acc)
+    if world > 1 and n_slots:
+        c = eng.refmerge_acc_rank(acc, n_slots, rank)
+        cmax = c.clone()
+        dist.all_reduce(cmax, op=dist.ReduceOp.MAX, group=group)
+        v = eng.refmerge_acc_owner_str(acc, n_slots, c, cmax)
+        dist.all_reduce(v, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(acc["sum"], op=dist.ReduceOp.SUM, group=group)   # int64 add wraps (main.go:95)
+        dist.all_reduce(acc["npar"], op=dist.ReduceOp.SUM, group=group)
+        eng.refmerge_acc_set_best(acc, n_slots, cmax, v)
+    return eng.refmerge_finalize(packed, acc, out)

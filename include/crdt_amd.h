@@ -206,6 +206,38 @@ typedef struct crdt_refmerge_out {
 
 /* All pointers in `in` / `out` are device pointers. */
 int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out);
+/* ts-range-sharded RefMerge (§8(e)): one batch of replicas whose logs are
+ * split by ts range over G shards (one per GPU).  Steps per shard:
+ *   1. crdt_refmerge_local_maxl -> all-reduce(MAX) over shards: max(L) per replica;
+ *   2. crdt_refmerge_batch_ex(maxl = that, acc = per-slot accumulators): the
+ *      shard's slice of the new Diff (shards concatenate in ts order) and its
+ *      unreduced replay fold (state outputs untouched);
+ *   3. acc_rank -> all-reduce(MAX) = cmax; acc_owner_str -> all-reduce(SUM);
+ *      all-reduce(SUM) of acc.sum and acc.npar; acc_set_best;
+ *   4. crdt_refmerge_finalize: CurrentState (st_*) from the reduced accumulators.
+ * Integer-only reductions: bit-exact for any shard count. */
+typedef struct crdt_refmerge_acc {
+    uint64_t *best;     /* [n_slots] 0 = no remote holder; else rank << 32 | string id */
+    int64_t  *sum;      /* [n_slots] wrapped sum of the parsable values (main.go:95) */
+    uint32_t *npar;     /* [n_slots] number of parsable values */
+} crdt_refmerge_acc;
+/* maxl_dev (nullable): per-replica max(L) replacing the local L's last key
+ * (INT64_MIN: none).  acc (nullable): per-slot accumulators written there
+ * instead of finalising st_kind/st_str/st_sum. */
+int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out,
+                           const int64_t *maxl_dev, const crdt_refmerge_acc *acc);
+int crdt_refmerge_local_maxl(crdt_ctx *ctx, const crdt_refmerge_in *in, int64_t *maxl_dev);
+/* c[s] = best ? shard << 40 | rank : 0  (shards in ts order; shard < 2^23) */
+int crdt_refmerge_acc_rank(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, uint32_t shard,
+                           int64_t *c_dev);
+/* v[s] = the string id if this shard holds the global max (c == cmax), else 0 */
+int crdt_refmerge_acc_owner_str(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, const int64_t *c_dev,
+                                const int64_t *cmax_dev, int64_t *v_dev);
+/* acc.best[s] = cmax ? 1 << 32 | v : 0 (the reduced accumulator) */
+int crdt_refmerge_acc_set_best(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, const int64_t *cmax_dev,
+                               const int64_t *v_dev);
+int crdt_refmerge_finalize(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, const uint8_t *str_bytes_dev,
+                           const uint64_t *str_off_dev, uint64_t n_str, const crdt_refmerge_out *out);
 /* Go strconv.Atoi over a string arena: ok[s] = parsable, val[s] = value. */
 int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *str_bytes_dev, const uint64_t *str_off_dev,
                     uint64_t n_str, uint8_t *ok_dev, int64_t *val_dev);
