@@ -188,8 +188,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic: WRONG output order
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sets_diag = (int)v;
-    } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 no fold, 2 no flush, 3 no LDS, 4 no table
-        if (v < 0 || v > 4) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 skip the replay fold; 2 no flush, 4 no table, 5 no Atoi gather
+        if (v < 0 || v > 5) return CRDT_E_INVAL;
         g_rm_diag = (int)v;
     } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
         if (v != 0 && v != 1) return CRDT_E_INVAL;

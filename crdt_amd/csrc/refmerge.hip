@@ -62,34 +62,73 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 // first on an equal ts) keeping every L entry and the R entries that are
 // "inserted" (below max(L), not equal to the L entry just before them in
 // merge order).  Each replica's merge sequence (|L|+|R| items) is cut into
-// tiles of MT items (geometry precomputed per tile); a tile's L and R ranges
-// come from a merge-path split (64-ary, one wave), are staged in LDS with
-// coalesced loads and merged by 256 threads x MI items.
-//   k_rm_count : split at the tile start (kept) + inserted-R count per tile,
-//                and the replay fold of the tile's emitted remote-origin
-//                entries (main.go:75-98) into an LDS table keyed by slot,
-//                flushed with one set of global atomics per (tile, slot);
-//   device scan of the counts -> every tile's output offset;
+// tiles of MT items; every tile pass loads one 64-B descriptor and stages
+// its L and R ranges in LDS with coalesced loads.
+//   k_rm_plan_small / scan + k_rm_geo : tiles per replica, tile geometry;
+//   k_rm_split : one wave per tile, 64-ary merge-path splits -> descriptors;
+//   k_rm_count : merge (256 threads x MI items): inserted-R count per tile
+//                and every entry's rank in the merge order (l_dk / r_dk);
+//   scan of the counts -> each tile's output offset, out.off;
 //   k_rm_write : re-merge, write the tile's new-Diff slice through LDS
 //                (coalesced);
+//   k_rm_fold  : the replay (main.go:75-98) of the tile's emitted
+//                remote-origin entries into an LDS table keyed by slot,
+//                flushed with one set of global atomics per (tile, slot);
 //   k_slot_final: per-slot closed form.
 // The replay's per-key state is order-free: best = max over holders of
 // (rank in the replica's merge sequence) << 32 | string id (the max-ts
 // holder, since the merge sequence is ts-ascending), plus the wrapped sum
-// and count of the parsable values; so tiles can fold independently.  (Per-entry binary
-// searches over the logs, and a per-replica replay pass re-reading the new
-// Diff, were each bound by chains of dependent global loads.)
+// and count of the parsable values; so tiles fold independently.  (Per-entry
+// binary searches over the logs, and a per-replica replay pass re-reading
+// the new Diff, were each bound by chains of dependent global loads; every
+// tile pass here is still latency-bound at 2-4 TB/s, see DESIGN.md.)
 constexpr int MT = 2048;                  // merge items per tile
 constexpr int MB = 256;                   // threads per tile
 constexpr int MI = MT / MB;               // items per thread
 constexpr int TT = 512;                   // LDS replay-table entries per tile
+constexpr int FB = 512;                   // threads of the replay-fold kernel (one tile each)
+constexpr int FI = MT / FB;               // entries per fold thread
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-struct TileGeo {                          // 64 B per tile
+struct TileGeo {                          // 64 B per tile (per-replica geometry)
     uint64_t lb, nl, rb, nr, d0, d1;
     int64_t maxl;
     uint32_t p, first;                    // replica; first tile of the replica
 };
+
+struct TileDesc {                         // 64 B per tile: everything a tile pass needs, one load
+    uint64_t l0, r0;                      // global index of the tile's first L / R entry
+    uint64_t d0;                          // the tile's first diagonal in the replica's merge sequence
+    int64_t maxl;                         // insert below this (max(L) of the replica)
+    int64_t lprev;                        // L entry just before the tile (valid if has_prev)
+    uint32_t na, nb;                      // L / R entries of the tile; na + nb == 0: no tile
+    uint32_t has_prev, pad[3];
+};
+
+struct alignas(16) OkVal {                // Go Atoi of one arena string: one 16-B gather per lookup
+    int64_t val;                          // 0 where !ok
+    int64_t ok;
+};
+
+// LDS copy of n bytes from global src: aligned dword loads for the interior,
+// byte loads for the ragged ends (never reads outside [src, src + n)).
+__device__ __forceinline__ void stage_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, int tid, int nthreads) {
+    const uintptr_t a = (uintptr_t)src;
+    uint32_t head = (uint32_t)((4 - (a & 3)) & 3);
+    if (head > n) head = n;
+    const uint32_t words = (n - head) / 4;
+    const uint32_t tail0 = head + words * 4;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(src + head);
+    for (uint32_t k = tid; k < words; k += nthreads) {
+        const uint32_t x = w[k];
+        dst[head + 4 * k] = (uint8_t)x;
+        dst[head + 4 * k + 1] = (uint8_t)(x >> 8);
+        dst[head + 4 * k + 2] = (uint8_t)(x >> 16);
+        dst[head + 4 * k + 3] = (uint8_t)(x >> 24);
+    }
+    if ((uint32_t)tid < head) dst[tid] = src[tid];
+    if ((uint32_t)tid < n - tail0) dst[tail0 + tid] = src[tail0 + tid];
+}
 
 struct SlotAcc {                          // global replay accumulators, by slot
     unsigned long long *best;             // 0 = slot untouched
@@ -147,6 +186,32 @@ __device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, co
         hi = nhi;
     }
     return lo;
+}
+
+// Tile descriptors: one wave per tile computes the merge-path splits at
+// its two diagonals (64-ary) and packs the tile's ranges; slots past the
+// tile count get an empty descriptor.
+__global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t replicas,
+                                                  const uint64_t *__restrict__ tbase, const TileGeo *__restrict__ geo,
+                                                  uint64_t tmax, TileDesc *__restrict__ desc) {
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= tmax) return;
+    TileDesc d = {};
+    if (t < tbase[replicas]) {
+        const TileGeo g = geo[t];
+        const uint64_t a0 = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d0, lane);
+        const uint64_t a1 = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d1, lane);
+        d.l0 = g.lb + a0;
+        d.r0 = g.rb + (g.d0 - a0);
+        d.d0 = g.d0;
+        d.maxl = g.maxl;
+        d.na = (uint32_t)(a1 - a0);
+        d.nb = (uint32_t)((g.d1 - a1) - (g.d0 - a0));
+        d.has_prev = a0 > 0;
+        d.lprev = a0 > 0 ? in.l_ts[g.lb + a0 - 1] : 0;
+    }
+    if (lane == 0) desc[t] = d;
 }
 
 // sm[0] = L[a0-1] (when a0 > 0), sm[1..na] = L[a0..a1), sm[na+1..] = R[b0..b1).
@@ -233,77 +298,30 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
     }
 }
 
-// Pass 1: split at the tile start (kept for pass 2), inserted-R count, and
-// the replay fold of the tile's emitted remote-origin entries.  An emitted
-// entry's rank in the replica's merge sequence (d0 + local diagonal + 1)
-// orders the replica's new Diff like its ts, so best = rank << 32 | string
-// picks the max-ts holder without knowing output positions.
-// Grid = an upper bound on the tile count: blocks past it zero their count.
-__global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, uint32_t replicas,
-                                                 const uint64_t *__restrict__ tbase,
-                                                 const TileGeo *__restrict__ geo, uint64_t *__restrict__ ta,
-                                                 uint32_t *__restrict__ tcnt, const uint8_t *__restrict__ ok,
-                                                 const int64_t *__restrict__ val, SlotAcc acc, int diag) {
-    __shared__ alignas(16) int64_t s_buf[MT + 1];        // merge input, then the replay table
-    __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> local diagonal + 1, 0 = dropped
-    __shared__ uint64_t s_a[2];
+// Pass 1: inserted-R count of each tile, and every entry's rank in its
+// tile's merge order (local diagonal + 1; 0 = an R entry that is not
+// inserted) for the replay fold.  Grid = the tile-count upper bound.
+__global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                 uint32_t *__restrict__ tcnt, uint16_t *__restrict__ l_dk,
+                                                 uint16_t *__restrict__ r_dk) {
+    __shared__ int64_t sm[MT + 1];
+    __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> local diagonal + 1
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
-    if (t >= tbase[replicas]) {
-        if (threadIdx.x == 0) tcnt[t] = 0;
+    const TileDesc d = desc[t];
+    const uint32_t na = d.na, nb = d.nb, n = na + nb;
+    if (n == 0) {
+        if (threadIdx.x == 0) tcnt[t] = 0;              // the scan runs over the whole grid
         return;
     }
-    const TileGeo g = geo[t];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (w < 2) {
-        const uint64_t a = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, w ? g.d1 : g.d0, lane);
-        if (lane == 0) s_a[w] = a;
-    }
+    for (uint32_t k = threadIdx.x; k < na; k += MB) sm[1 + k] = in.l_ts[d.l0 + k];
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[d.r0 + k];
+    if (threadIdx.x == 0) sm[0] = d.lprev;
     __syncthreads();
-    const uint64_t a0 = s_a[0], a1 = s_a[1];
-    if (threadIdx.x == 0) ta[t] = a0;
-    const uint32_t na = (uint32_t)(a1 - a0), nb = (uint32_t)(g.d1 - g.d0) - na;
-    const uint64_t b0 = g.d0 - a0;
-    int64_t *sm = s_buf;
-    for (uint32_t k = threadIdx.x; k < na; k += MB) sm[1 + k] = in.l_ts[g.lb + a0 + k];
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[g.rb + b0 + k];
-    if (threadIdx.x == 0 && a0 > 0) sm[0] = in.l_ts[g.lb + a0 - 1];
-    const uint32_t n = na + nb;
-    // Replay-fold operands of this thread's MI entries (e = tid + f*MB),
-    // loaded before the merge so their latency hides behind it: kv range
-    // (remote-origin entries only; *Command values are skipped, main.go:80),
-    // then the first kv of each entry.  Further kvs (rare: the reference's
-    // load generator writes one kv per entry) take a serial tail loop.
-    const bool fold = diag != 1 && in.n_slots != 0;
-    uint64_t e_kb[MI];
-    uint32_t e_cnt[MI], e_slot[MI], e_v[MI];
-#pragma unroll
-    for (int f = 0; f < MI; ++f) {
-        const uint32_t e = threadIdx.x + (uint32_t)f * MB;
-        e_kb[f] = 0;
-        e_cnt[f] = 0;
-        if (fold && e < n) {
-            const bool r = e >= na;
-            const uint32_t li = r ? e - na : e;
-            const bool remote = r || in.l_origin[g.lb + a0 + li] == 0;
-            if (remote) {
-                const uint64_t *kv = r ? in.r_kv + g.rb + b0 + li : in.l_kv + g.lb + a0 + li;
-                const uint64_t kb = kv[0], ke = kv[1] < in.n_kv ? kv[1] : in.n_kv;   // stay in bounds
-                e_kb[f] = kb;
-                e_cnt[f] = kb < ke ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int f = 0; f < MI; ++f) {
-        e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
-        e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
-    }
     const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
     uint32_t isl, emit;
-    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.maxl, &isl, &emit);
+    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
     {
         uint32_t ia = ia0, ib = k0 - ia0;
         for (uint32_t i = 0; i < k1 - k0; ++i) {
@@ -313,51 +331,89 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, uint32_t r
         }
     }
     uint32_t total;
-    block_excl_sum((uint32_t)__popc(emit & ~isl), s_w, &total);   // (its barrier also retires sm)
+    block_excl_sum((uint32_t)__popc(emit & ~isl), s_w, &total);   // (its barrier also publishes s_dk)
     if (threadIdx.x == 0) tcnt[t] = total;
-    if (!fold) return;
-    bool e_ok[MI];
-    int64_t e_x[MI];
-#pragma unroll
-    for (int f = 0; f < MI; ++f) {
-        const bool good = e_slot[f] < in.n_slots && e_v[f] < in.n_str;
-        e_ok[f] = good ? ok[e_v[f]] != 0 : false;
-        e_x[f] = good ? val[e_v[f]] : 0;                 // val[] is 0 where !ok
-    }
-    uint32_t *t_slot = reinterpret_cast<uint32_t *>(s_buf);
-    unsigned long long *t_best = reinterpret_cast<unsigned long long *>(s_buf) + TT / 2;
-    unsigned long long *t_sum = t_best + TT;
-    uint32_t *t_npar = reinterpret_cast<uint32_t *>(t_sum + TT);
-    for (int h = threadIdx.x; h < TT; h += MB) {
+    if (!l_dk) return;
+    for (uint32_t k = threadIdx.x; k < na; k += MB) l_dk[d.l0 + k] = s_dk[k];
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) r_dk[d.r0 + k] = s_dk[na + k];
+}
+
+// Replay fold (main.go:75-98) of one tile's emitted remote-origin entries
+// into an LDS table keyed by slot, flushed with one set of global atomics
+// per (tile, slot).  An entry's rank in the replica's merge sequence
+// (d0 + dk) orders the replica's new Diff like its ts, so best = rank << 32
+// | string id picks the max-ts holder without knowing output positions.
+// FI entries per thread (e = tid + f*FB, coalesced), every load of the
+// batch issued before the first atomic; an entry's kv end is the next
+// lane's kv start (a shuffle).  Further kvs of an entry (rare: the
+// reference's load generator writes one kv per entry) take a tail loop.
+__global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
+                                                const OkVal *__restrict__ okv, SlotAcc acc, int diag) {
+    __shared__ uint32_t t_slot[TT];
+    __shared__ unsigned long long t_best[TT];
+    __shared__ unsigned long long t_sum[TT];
+    __shared__ uint32_t t_npar[TT];
+    const uint64_t t = blockIdx.x;
+    const TileDesc d = desc[t];
+    const uint32_t na = d.na, nb = d.nb, n = na + nb;
+    if (n == 0) return;
+    const int lane = threadIdx.x & 63;
+    for (int h = threadIdx.x; h < TT; h += FB) {
         t_slot[h] = kEmpty;
         t_best[h] = 0;
         t_sum[h] = 0;
         t_npar[h] = 0;
     }
-    __syncthreads();
-    const bool use_lds = diag != 3;
+    uint64_t e_kb[FI];
+    uint32_t e_dk[FI], e_cnt[FI], e_slot[FI], e_v[FI];
 #pragma unroll
-    for (int f = 0; f < MI; ++f) {
-        const uint32_t e = threadIdx.x + (uint32_t)f * MB;
-        const uint32_t dk = e_cnt[f] ? s_dk[e] : 0u;     // 0: dropped R entry / no kv
-        if (!dk) continue;
-        const uint64_t rank = g.d0 + dk;
-        if (diag == 4) {                                 // timing diagnostic: loads only, no table
-            if (((rank << 32) ^ e_v[f] ^ (uint64_t)e_x[f]) == 0x123456789ull) acc.npar[0] = e_slot[f];
-            continue;
-        }
+    for (int f = 0; f < FI; ++f) {
+        const uint32_t e = threadIdx.x + (uint32_t)f * FB;
+        const bool r = e >= na;
+        const uint64_t gi = r ? d.r0 + (e - na) : d.l0 + e;
+        const uint64_t *kv = (r ? in.r_kv : in.l_kv) + gi;
+        const bool in_tile = e < n;
+        const uint64_t kb = in_tile ? kv[0] : 0;
+        const uint64_t nxt = __shfl_down(kb, 1);
+        uint32_t dk = in_tile ? (r ? r_dk[gi] : l_dk[gi]) : 0u;
+        if (in_tile && !r && in.l_origin[gi]) dk = 0;    // *Command: skipped by the replay (main.go:80)
+        uint64_t ke = nxt;
+        if (in_tile && (lane == 63 || e + 1 == na || e + 1 >= n)) ke = kv[1];
+        ke = ke < in.n_kv ? ke : in.n_kv;                 // malformed ranges stay in bounds
+        e_kb[f] = kb;
+        e_dk[f] = dk;
+        e_cnt[f] = (dk && kb < ke) ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
+    }
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
+        e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
+    }
+    OkVal e_o[FI];
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        e_o[f] = OkVal{0, 0};
+        if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
+    }
+    __syncthreads();                                     // table initialised
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        if (!e_cnt[f]) continue;
+        const uint64_t rank = d.d0 + e_dk[f];
         if (e_slot[f] < in.n_slots && e_v[f] < in.n_str)
-            fold_pair(t_slot, t_best, t_sum, t_npar, acc, use_lds, e_slot[f], e_v[f], rank, e_ok[f], e_x[f]);
+            fold_pair(t_slot, t_best, t_sum, t_npar, acc, true, e_slot[f], e_v[f], rank, e_o[f].ok != 0,
+                      e_o[f].val);
         for (uint64_t q = e_kb[f] + 1; q < e_kb[f] + e_cnt[f]; ++q) {
             const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
             if (slot >= in.n_slots || v >= in.n_str) continue;
-            const bool okv = ok[v] != 0;
-            fold_pair(t_slot, t_best, t_sum, t_npar, acc, use_lds, slot, v, rank, okv, okv ? val[v] : 0);
+            const OkVal o = okv[v];
+            fold_pair(t_slot, t_best, t_sum, t_npar, acc, true, slot, v, rank, o.ok != 0, o.val);
         }
     }
     __syncthreads();
     if (diag == 2) return;
-    for (int h = threadIdx.x; h < TT; h += MB) {
+    for (int h = threadIdx.x; h < TT; h += FB) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;
         atomicMax(&acc.best[slot], t_best[h]);
@@ -371,36 +427,28 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, uint32_t r
 // Pass 2: re-merge, stage the tile's new-Diff slice in LDS (over the merge
 // input once it is dead) and write it coalesced.  ic = exclusive scan of
 // tcnt: inserted R entries before tile t (all replicas), so the slice starts
-// at l_off[p] + a0 + ic[t].
-__global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, uint32_t replicas,
-                                                 const uint64_t *__restrict__ tbase,
-                                                 const TileGeo *__restrict__ geo, const uint64_t *__restrict__ ta,
+// at l_off[p] + a0 + ic[t] = l0 + ic[t].
+__global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  const uint64_t *__restrict__ ic, crdt_refmerge_out out) {
     __shared__ alignas(16) int64_t s_buf[MT + 1];
     __shared__ uint8_t so[MT];                           // origins of the tile's L entries
     __shared__ uint16_t s_idx[MT];                       // output slot -> entry (bit 15: R)
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
-    if (t >= tbase[replicas]) return;
-    const TileGeo g = geo[t];
-    const uint64_t a0 = ta[t];
-    const uint64_t a1 = t + 1 < tbase[g.p + 1] ? ta[t + 1] : g.nl;
+    const TileDesc d = desc[t];
+    const uint32_t na = d.na, nb = d.nb, n = na + nb;
+    if (n == 0) return;
     const uint64_t ict = ic[t];
-    const uint32_t na = (uint32_t)(a1 - a0), nb = (uint32_t)(g.d1 - g.d0) - na;
-    const uint64_t b0 = g.d0 - a0;
     int64_t *sm = s_buf;
-    for (uint32_t k = threadIdx.x; k < na; k += MB) {
-        sm[1 + k] = in.l_ts[g.lb + a0 + k];
-        so[k] = in.l_origin[g.lb + a0 + k];
-    }
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[g.rb + b0 + k];
-    if (threadIdx.x == 0 && a0 > 0) sm[0] = in.l_ts[g.lb + a0 - 1];
+    for (uint32_t k = threadIdx.x; k < na; k += MB) sm[1 + k] = in.l_ts[d.l0 + k];
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[d.r0 + k];
+    stage_bytes(so, in.l_origin + d.l0, na, threadIdx.x, MB);
+    if (threadIdx.x == 0) sm[0] = d.lprev;
     __syncthreads();
-    const uint32_t n = na + nb;
     const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
     uint32_t isl, emit;
-    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, a0 > 0, g.maxl, &isl, &emit);
+    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
     int64_t vts[MI];
     uint32_t vid[MI];
     {
@@ -431,12 +479,12 @@ __global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, uint32_t r
         }
     }
     __syncthreads();
-    const uint64_t ob = g.lb + a0 + ict;                 // l_off[p] == g.lb
+    const uint64_t ob = d.l0 + ict;
     for (uint32_t k = threadIdx.x; k < total; k += MB) {
         const uint32_t id = s_idx[k], li = id & 0x7FFFu;
         const bool r = id >> 15;
         out.ts[ob + k] = s_buf[k];
-        out.src[ob + k] = r ? -(int64_t)(g.rb + b0 + li) - 1 : (int64_t)(g.lb + a0 + li);
+        out.src[ob + k] = r ? -(int64_t)(d.r0 + li) - 1 : (int64_t)(d.l0 + li);
         out.origin[ob + k] = r ? 0 : so[li];
     }
 }
@@ -508,14 +556,14 @@ __global__ __launch_bounds__(SB) void k_rm_scan_small(const uint32_t *__restrict
 
 // Go Atoi over the string arena and the replay accumulators' reset, one launch.
 __global__ void k_rm_prep(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, uint64_t nstr,
-                          uint8_t *__restrict__ ok, int64_t *__restrict__ val, SlotAcc acc, uint32_t ns) {
+                          OkVal *__restrict__ okv, SlotAcc acc, uint32_t ns) {
     const uint64_t n = nstr > ns ? nstr : ns;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         if (i < nstr) {
             int64_t v = 0;
             const bool good = go_atoi(bytes + off[i], off[i + 1] - off[i], &v);
-            ok[i] = good;
-            val[i] = good ? v : 0;
+            okv[i].val = good ? v : 0;
+            okv[i].ok = good;
         }
         if (i < ns) {
             acc.best[i] = 0;
@@ -534,7 +582,7 @@ __global__ void k_out_off(crdt_refmerge_in in, const uint64_t *__restrict__ tbas
 
 // Per-key closed form (main.go:82-96): verbatim base unless the base parses
 // AND another holder's value parses; then Itoa(sum) with int64 wrap.
-__global__ void k_slot_final(crdt_refmerge_out out, SlotAcc acc, const uint8_t *__restrict__ ok, uint32_t n) {
+__global__ void k_slot_final(crdt_refmerge_out out, SlotAcc acc, const OkVal *__restrict__ okv, uint32_t n) {
     for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
         const unsigned long long best = acc.best[s];
         if (!best) {                                     // no remote holder: absent from CurrentState
@@ -544,7 +592,7 @@ __global__ void k_slot_final(crdt_refmerge_out out, SlotAcc acc, const uint8_t *
             continue;
         }
         const uint32_t str = (uint32_t)best;
-        const bool sum_form = ok[str] && acc.npar[s] >= 2;
+        const bool sum_form = okv[str].ok && acc.npar[s] >= 2;
         out.st_kind[s] = sum_form ? 2 : 1;
         out.st_str[s] = str;
         out.st_sum[s] = sum_form ? (int64_t)acc.sum[s] : 0;
@@ -592,8 +640,9 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
     const size_t tmax = (in.n_l + nr) / MT + np + 1;             // >= tiles over all replicas
     if (tmax > 0x7fffffffULL) return CRDT_E_RANGE;
     const size_t need = Carve::round(np * 4 + 4) + Carve::round((np + 1) * 8) + scan_tmp_bytes(std::max(np, tmax)) +
-                        Carve::round((tmax + 1) * sizeof(TileGeo)) + Carve::round(tmax * 8 + 8) * 2 +
-                        Carve::round(tmax * 4 + 4) + Carve::round(nstr + 1) + Carve::round(nstr * 8 + 8) +
+                        Carve::round((tmax + 1) * sizeof(TileGeo)) * 2 + Carve::round(tmax * 8 + 8) +
+                        Carve::round(tmax * 4 + 4) + Carve::round((nstr + 1) * sizeof(OkVal)) +
+                        Carve::round(in.n_l * 2 + 2) + Carve::round(nr * 2 + 2) +
                         Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) + 4096;
     rc = ws_reserve(ctx, need);
     if (rc) return rc;
@@ -602,11 +651,12 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
     uint64_t *tbase = w.take<uint64_t>(np + 1);
     void *tmp = w.take<char>(scan_tmp_bytes(std::max(np, tmax)));
     TileGeo *geo = w.take<TileGeo>(tmax + 1);
-    uint64_t *ta = w.take<uint64_t>(tmax + 1);
+    TileDesc *desc = w.take<TileDesc>(tmax + 1);
     uint64_t *ic = w.take<uint64_t>(tmax + 1);
     uint32_t *tcnt = w.take<uint32_t>(tmax + 1);
-    uint8_t *ok = w.take<uint8_t>(nstr + 1);
-    int64_t *val = w.take<int64_t>(nstr + 1);
+    uint16_t *l_dk = w.take<uint16_t>(in.n_l + 1);
+    uint16_t *r_dk = w.take<uint16_t>(nr + 1);
+    OkVal *okv = w.take<OkVal>(nstr + 1);
     SlotAcc acc;
     acc.best = w.take<unsigned long long>(ns + 1);
     acc.sum = w.take<unsigned long long>(ns + 1);
@@ -621,7 +671,7 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
     const unsigned cap = (unsigned)ctx->num_cus * 8;
     const uint32_t reps = in.replicas;
     if (nstr || ns)
-        k_rm_prep<<<grid_for(std::max(nstr, ns), 256, cap), 256, 0, s>>>(in.str_bytes, in.str_off, nstr, ok, val, acc,
+        k_rm_prep<<<grid_for(std::max(nstr, ns), 256, cap), 256, 0, s>>>(in.str_bytes, in.str_off, nstr, okv, acc,
                                                                           (uint32_t)ns);
     if (np <= kSmallPlan) {
         k_rm_plan_small<<<1, SB, 0, s>>>(in, tbase);
@@ -633,8 +683,9 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
         if (rc) return rc;
     }
     k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
-    // grids = an upper bound on the tile count; blocks past tbase[np] exit at once
-    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, reps, tbase, geo, ta, tcnt, ok, val, acc, g_rm_diag);
+    k_rm_split<<<(unsigned)((tmax + 3) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
+    // tile grids = the tile-count upper bound; empty descriptors exit at once
+    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, ns ? l_dk : nullptr, r_dk);
     rc = check_launch(ctx);
     if (rc) return rc;
     if (tmax <= kSmallPlan) {
@@ -644,8 +695,10 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
         if (rc) return rc;
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
-    k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, reps, tbase, geo, ta, ic, out);
-    if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, ok, (uint32_t)ns);
+    k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, desc, ic, out);
+    if (ns && g_rm_diag != 1)                                     // (diag 1: timing without the replay fold)
+        k_rm_fold<<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag);
+    if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
     return check_launch(ctx);
 }
 
@@ -720,19 +773,18 @@ extern "C" int crdt_refmerge_finalize(crdt_ctx *ctx, const crdt_refmerge_acc *ac
     if (!accp || !outp || !accp->best || !accp->sum || !accp->npar || n_slots > 0xffffffffULL) return CRDT_E_INVAL;
     if (!outp->st_kind || !outp->st_str || !outp->st_sum) return CRDT_E_INVAL;
     if (n_str && (!str_bytes || !str_off)) return CRDT_E_INVAL;
-    rc = ws_reserve(ctx, Carve::round(n_str + 1) + Carve::round(n_str * 8 + 8) + 4096);
+    rc = ws_reserve(ctx, Carve::round((n_str + 1) * sizeof(OkVal)) + 4096);
     if (rc) return rc;
     Carve w(ctx->ws);
-    uint8_t *ok = w.take<uint8_t>(n_str + 1);
-    int64_t *val = w.take<int64_t>(n_str + 1);
+    OkVal *okv = w.take<OkVal>(n_str + 1);
     const unsigned cap = (unsigned)ctx->num_cus * 8;
-    if (n_str) k_atoi<<<grid_for(n_str, 256, cap), 256, 0, ctx->stream>>>(str_bytes, str_off, n_str, ok, val);
+    if (n_str) k_rm_prep<<<grid_for(n_str, 256, cap), 256, 0, ctx->stream>>>(str_bytes, str_off, n_str, okv, SlotAcc{}, 0);
     SlotAcc acc;
     acc.best = reinterpret_cast<unsigned long long *>(accp->best);
     acc.sum = reinterpret_cast<unsigned long long *>(accp->sum);
     acc.npar = accp->npar;
     // a best string id >= n_str cannot occur (pairs with v >= n_str are never folded)
-    k_slot_final<<<grid_for(n_slots, 256, cap), 256, 0, ctx->stream>>>(*outp, acc, ok, (uint32_t)n_slots);
+    k_slot_final<<<grid_for(n_slots, 256, cap), 256, 0, ctx->stream>>>(*outp, acc, okv, (uint32_t)n_slots);
     return check_launch(ctx);
 }
 
