@@ -362,7 +362,7 @@ class RefMergeBatch(Workload):
     name = "refmerge"
     unit = "remote-entries/s"
     dtype = "int64"
-    kernel = "refmerge (whole op: walk, scan, scatters, replay)"
+    kernel = "refmerge (whole op: k_rm_plan/geo/split/count/scan/write/fold + k_slot_final)"
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         from crdt_amd import refmerge, synth
