@@ -426,9 +426,41 @@ class RefMergeBatch(Workload):
                           f"replicas of the same batch on {threads} threads, {dt:.1f}s"}
 
 
+class RefMergeDelta(RefMergeBatch):
+    """The same batch through the incremental replay:
+    crdt_refmerge_delta folds only the inserted R entries into a carried
+    ts-keyed state.  Each step restores the state of L first (a 1.7 MB
+    device copy, inside the timed region) so every step is the same merge."""
+    name = "refmerge_delta"
+    kernel = "refmerge_delta (whole op: walk passes + k_rp_fold x2 + k_rp_final + state restore)"
+
+    def __init__(self, eng, rank, world, replicas, entries, seed=2024):
+        super().__init__(eng, rank, world, replicas, entries, seed)
+        self.st0 = eng.replay_state_init(self.dev)
+        self.st = {k: v.clone() for k, v in self.st0.items()}
+        self.config["workload"] = self.config["workload"].replace("RefMerge", "RefMerge, incremental replay,", 1)
+        h = self.host
+        self.n_rkv = int(h["r_kv"][-1] - h["r_kv"][0])
+
+    def bytes_per_launch(self):
+        # L ts + origin, R ts + kv range + its kvs, the output, the state (read + write), strings
+        return (self.n_l * 9 + self.n_r * 16 + self.n_rkv * 8 + self.n_out * 17
+                + self.host["n_slots"] * (28 * 2 + 13) + int(self.host["str_off"][-1]))
+
+    def step(self):
+        for k, v in self.st0.items():
+            self.st[k].copy_(v)
+        self.eng.refmerge_delta(self.dev, self.st)
+
+    def cpu_baseline(self, seconds, threads):
+        return None
+
+
 def make_workload(name, eng, rank, world, args):
     if name == "refmerge":
         return RefMergeBatch(eng, rank, world, args.replicas, args.entries)
+    if name == "refmerge_delta":
+        return RefMergeDelta(eng, rank, world, args.replicas, args.entries)
     if name == "gcounter_join":
         return GCounterJoin(eng, rank, world, args.rows, args.nodes)
     if name == "pncounter_join":
@@ -466,7 +498,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gcounter_join",
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge", "lww_merge_d2", "orset_merge_d2",
-                             "shard_fold", "shard_join", "refmerge"])
+                             "shard_fold", "shard_join", "refmerge", "refmerge_delta"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)

@@ -71,6 +71,11 @@ class crdt_refmerge_out(C.Structure):
     ]
 
 
+class crdt_replay_state(C.Structure):
+    _fields_ = [("best_key", C.c_void_p), ("best_str", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p),
+                ("nhold", C.c_void_p)]
+
+
 class crdt_refmerge_acc(C.Structure):
     _fields_ = [("best", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p)]
 
@@ -122,6 +127,9 @@ SIGNATURES = {
     "crdt_refmerge_batch_ex": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out), _P,
                                     C.POINTER(crdt_refmerge_acc)]),
     "crdt_refmerge_local_maxl": (_I, [_CTX, C.POINTER(crdt_refmerge_in), _P]),
+    "crdt_replay_state_init": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_replay_state)]),
+    "crdt_refmerge_delta": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out),
+                                 C.POINTER(crdt_replay_state)]),
     "crdt_refmerge_acc_rank": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, C.c_uint32, _P]),
     "crdt_refmerge_acc_owner_str": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, _P, _P, _P]),
     "crdt_refmerge_acc_set_best": (_I, [_CTX, C.POINTER(crdt_refmerge_acc), _SZ, _P, _P]),

@@ -333,9 +333,10 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
     uint32_t total;
     block_excl_sum((uint32_t)__popc(emit & ~isl), s_w, &total);   // (its barrier also publishes s_dk)
     if (threadIdx.x == 0) tcnt[t] = total;
-    if (!l_dk) return;
-    for (uint32_t k = threadIdx.x; k < na; k += MB) l_dk[d.l0 + k] = s_dk[k];
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) r_dk[d.r0 + k] = s_dk[na + k];
+    if (l_dk)
+        for (uint32_t k = threadIdx.x; k < na; k += MB) l_dk[d.l0 + k] = s_dk[k];
+    if (r_dk)
+        for (uint32_t k = threadIdx.x; k < nb; k += MB) r_dk[d.r0 + k] = s_dk[na + k];
 }
 
 // Replay fold (main.go:75-98) of one tile's emitted remote-origin entries
@@ -613,15 +614,37 @@ extern "C" int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *bytes, const uint64
     return check_launch(ctx);
 }
 
+static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                        const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta);
+
 extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp) {
-    return crdt_refmerge_batch_ex(ctx, inp, outp, nullptr, nullptr);
+    return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr);
+}
+
+namespace crdt {
+static int rp_delta_fold(crdt_ctx *ctx, const crdt_refmerge_in &in, const uint16_t *r_dk, const OkVal *okv,
+                         const crdt_replay_state &st, const crdt_refmerge_out *out);
 }
 
 extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
                                       const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out) {
+    return refmerge_run(ctx, inp, outp, maxl_dev, acc_out, nullptr);
+}
+
+extern "C" int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                                   const crdt_replay_state *st) {
+    if (!st) return CRDT_E_INVAL;
+    return refmerge_run(ctx, inp, outp, nullptr, nullptr, st);
+}
+
+static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                        const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta) {
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
+    if (delta && inp->n_slots && (!delta->best_key || !delta->best_str || !delta->sum || !delta->npar ||
+                                  !delta->nhold))
+        return CRDT_E_INVAL;
     if (acc_out && inp->n_slots && (!acc_out->best || !acc_out->sum || !acc_out->npar)) return CRDT_E_INVAL;
     const crdt_refmerge_in in = *inp;
     const crdt_refmerge_out out = *outp;
@@ -685,7 +708,7 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
     k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
     k_rm_split<<<(unsigned)((tmax + 3) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
-    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, ns ? l_dk : nullptr, r_dk);
+    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, ns && !delta ? l_dk : nullptr, ns ? r_dk : nullptr);
     rc = check_launch(ctx);
     if (rc) return rc;
     if (tmax <= kSmallPlan) {
@@ -696,6 +719,11 @@ extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
     k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, desc, ic, out);
+    if (delta) {                                                  // incremental replay: fold only the inserted R
+        rc = check_launch(ctx);
+        if (rc) return rc;
+        return ns ? rp_delta_fold(ctx, in, r_dk, okv, *delta, &out) : CRDT_OK;
+    }
     if (ns && g_rm_diag != 1)                                     // (diag 1: timing without the replay fold)
         k_rm_fold<<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag);
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
@@ -785,6 +813,196 @@ extern "C" int crdt_refmerge_finalize(crdt_ctx *ctx, const crdt_refmerge_acc *ac
     acc.npar = accp->npar;
     // a best string id >= n_str cannot occur (pairs with v >= n_str are never folded)
     k_slot_final<<<grid_for(n_slots, 256, cap), 256, 0, ctx->stream>>>(*outp, acc, okv, (uint32_t)n_slots);
+    return check_launch(ctx);
+}
+
+// ---------------------------------------------------------------- incremental replay (§8(f) row 3)
+// The reference re-folds the whole Diff on every merge (main.go:76).  A
+// merge only ever ADDS remote entries to Diff (inserted R; an equal ts keeps
+// the local entry), so the replay over Diff' = the replay over Diff plus the
+// inserted entries -- provided the per-key state is keyed by ts, not by a
+// merge-order rank: best_key = max over holders of ts ^ 2^63 (order-
+// preserving), best_str = the string of that holder (ts are unique within a
+// Diff, so exactly one holder matches), the wrapped sum and the parsable and
+// holder counts.  Two passes per fold: max/sum/counts through a per-block
+// LDS table flushed with global atomics, then the unique max holder writes
+// its string.  (A local write that overwrites a remote entry at the same ms,
+// main.go:187, removes a holder: the caller rebuilds the state then.)
+namespace crdt {
+constexpr int RPB = 256;                  // threads per block
+constexpr int RPE = 4;                    // entries per thread per round
+
+__device__ __forceinline__ uint64_t ord_ts(int64_t ts) { return (uint64_t)ts ^ 0x8000000000000000ull; }
+
+// PHASE 1: max / sum / counts; PHASE 2: the max holder writes its string.
+// RSIDE: the R entries marked inserted in r_dk (delta); else the L entries
+// of remote origin (state init).
+template <bool RSIDE, int PHASE>
+__global__ __launch_bounds__(RPB) void k_rp_fold(crdt_refmerge_in in, const uint16_t *__restrict__ r_dk,
+                                                 const OkVal *__restrict__ okv, crdt_replay_state st) {
+    __shared__ uint32_t t_slot[TT];
+    __shared__ unsigned long long t_max[TT];
+    __shared__ unsigned long long t_sum[TT];
+    __shared__ uint32_t t_npar[TT], t_nh[TT];
+    const uint64_t n = RSIDE ? in.n_r : in.n_l;
+    const uint64_t *kvo = RSIDE ? in.r_kv : in.l_kv;
+    const int64_t *tsv = RSIDE ? in.r_ts : in.l_ts;
+    for (uint64_t base = (uint64_t)blockIdx.x * RPB * RPE; base < n; base += (uint64_t)gridDim.x * RPB * RPE) {
+        if (PHASE == 1) {
+            for (int h = threadIdx.x; h < TT; h += RPB) {
+                t_slot[h] = kEmpty;
+                t_max[h] = 0;
+                t_sum[h] = 0;
+                t_npar[h] = 0;
+                t_nh[h] = 0;
+            }
+            __syncthreads();
+        }
+        // every load of the round issued before the first atomic
+        uint64_t e_kb[RPE], e_key[RPE];
+        uint32_t e_cnt[RPE], e_slot[RPE], e_v[RPE];
+#pragma unroll
+        for (int f = 0; f < RPE; ++f) {
+            const uint64_t e = base + threadIdx.x + (uint64_t)f * RPB;
+            e_cnt[f] = 0;
+            e_kb[f] = 0;
+            e_key[f] = 0;
+            if (e < n) {
+                const bool take = RSIDE ? r_dk[e] != 0 : in.l_origin[e] == 0;   // *Command skipped (main.go:80)
+                const uint64_t kb = kvo[e], ke = kvo[e + 1] < in.n_kv ? kvo[e + 1] : in.n_kv;
+                e_kb[f] = kb;
+                e_key[f] = ord_ts(tsv[e]);
+                e_cnt[f] = take && kb < ke ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < RPE; ++f) {
+            e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
+            e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
+        }
+        OkVal e_o[RPE];
+#pragma unroll
+        for (int f = 0; f < RPE; ++f) {
+            e_o[f] = OkVal{0, 0};
+            if (PHASE == 1 && e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
+        }
+#pragma unroll
+        for (int f = 0; f < RPE; ++f) {
+            for (uint32_t j = 0; j < e_cnt[f]; ++j) {
+                uint32_t slot = e_slot[f], v = e_v[f];
+                OkVal o = e_o[f];
+                if (j) {                                     // further kvs of the entry (rare)
+                    slot = in.kv_key[e_kb[f] + j];
+                    v = in.kv_val[e_kb[f] + j];
+                    if (PHASE == 1 && slot < in.n_slots && v < in.n_str) o = okv[v];
+                }
+                if (slot >= in.n_slots || v >= in.n_str) continue;
+                const uint64_t key = e_key[f];
+                if (PHASE == 2) {
+                    if (st.best_key[slot] == key) st.best_str[slot] = v;   // the unique max holder
+                    continue;
+                }
+                const uint32_t idx = table_find(t_slot, slot);
+                if (idx != kEmpty) {
+                    atomicMax(&t_max[idx], key);
+                    atomicAdd(&t_nh[idx], 1u);
+                    if (o.ok) {
+                        atomicAdd(&t_sum[idx], (unsigned long long)o.val);   // mod 2^64 (main.go:95)
+                        atomicAdd(&t_npar[idx], 1u);
+                    }
+                } else {
+                    atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), key);
+                    atomicAdd(&st.nhold[slot], 1u);
+                    if (o.ok) {
+                        atomicAdd(reinterpret_cast<unsigned long long *>(&st.sum[slot]), (unsigned long long)o.val);
+                        atomicAdd(&st.npar[slot], 1u);
+                    }
+                }
+            }
+        }
+        if (PHASE == 1) {
+            __syncthreads();
+            for (int h = threadIdx.x; h < TT; h += RPB) {
+                const uint32_t slot = t_slot[h];
+                if (slot == kEmpty) continue;
+                atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), t_max[h]);
+                atomicAdd(&st.nhold[slot], t_nh[h]);
+                if (t_npar[h]) {
+                    atomicAdd(reinterpret_cast<unsigned long long *>(&st.sum[slot]), t_sum[h]);
+                    atomicAdd(&st.npar[slot], t_npar[h]);
+                }
+            }
+            __syncthreads();                                 // table reused by the next round
+        }
+    }
+}
+
+__global__ void k_rp_clear(crdt_replay_state st, uint32_t n) {
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        st.best_key[s] = 0;
+        st.best_str[s] = 0;
+        st.sum[s] = 0;
+        st.npar[s] = 0;
+        st.nhold[s] = 0;
+    }
+}
+
+// CurrentState from the state (closed form as k_slot_final)
+__global__ void k_rp_final(crdt_refmerge_out out, crdt_replay_state st, const OkVal *__restrict__ okv, uint32_t n) {
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        if (!st.nhold[s]) {
+            out.st_kind[s] = 0;
+            out.st_str[s] = 0;
+            out.st_sum[s] = 0;
+            continue;
+        }
+        const uint32_t str = st.best_str[s];
+        const bool sum_form = okv[str].ok && st.npar[s] >= 2;
+        out.st_kind[s] = sum_form ? 2 : 1;
+        out.st_str[s] = str;
+        out.st_sum[s] = sum_form ? st.sum[s] : 0;
+    }
+}
+
+static int rp_delta_fold(crdt_ctx *ctx, const crdt_refmerge_in &in, const uint16_t *r_dk, const OkVal *okv,
+                         const crdt_replay_state &st, const crdt_refmerge_out *out) {
+    const hipStream_t s = ctx->stream;
+    const unsigned g = grid_for((in.n_r + RPE - 1) / RPE, RPB, (unsigned)ctx->num_cus * 8);
+    if (in.n_r) {
+        k_rp_fold<true, 1><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
+        k_rp_fold<true, 2><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
+    }
+    k_rp_final<<<grid_for(in.n_slots, 256, (unsigned)ctx->num_cus * 8), 256, 0, s>>>(*out, st, okv, in.n_slots);
+    return check_launch(ctx);
+}
+}  // namespace crdt
+
+// Replay state of the L logs alone (their remote-origin entries): the
+// starting point of crdt_refmerge_delta.  R is ignored.
+extern "C" int crdt_replay_state_init(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_replay_state *st) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!inp || !st) return CRDT_E_INVAL;
+    const crdt_refmerge_in in = *inp;
+    if (in.n_slots == 0) return CRDT_OK;
+    if (!st->best_key || !st->best_str || !st->sum || !st->npar || !st->nhold) return CRDT_E_INVAL;
+    if (in.n_l && (!in.l_ts || !in.l_origin || !in.l_kv)) return CRDT_E_INVAL;
+    if (in.n_kv && (!in.kv_key || !in.kv_val || !in.n_str)) return CRDT_E_INVAL;
+    if (in.n_str && (!in.str_bytes || !in.str_off)) return CRDT_E_INVAL;
+    rc = ws_reserve(ctx, Carve::round((in.n_str + 1) * sizeof(OkVal)) + 4096);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    OkVal *okv = w.take<OkVal>(in.n_str + 1);
+    const hipStream_t s = ctx->stream;
+    const unsigned cap = (unsigned)ctx->num_cus * 8;
+    if (in.n_str)
+        k_rm_prep<<<grid_for(in.n_str, 256, cap), 256, 0, s>>>(in.str_bytes, in.str_off, in.n_str, okv, SlotAcc{}, 0);
+    k_rp_clear<<<grid_for(in.n_slots, 256, cap), 256, 0, s>>>(*st, in.n_slots);
+    if (in.n_l) {
+        const unsigned g = grid_for((in.n_l + RPE - 1) / RPE, RPB, cap);
+        k_rp_fold<false, 1><<<g, RPB, 0, s>>>(in, nullptr, okv, *st);
+        k_rp_fold<false, 2><<<g, RPB, 0, s>>>(in, nullptr, okv, *st);
+    }
     return check_launch(ctx);
 }
 

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import call, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_out, crdt_tuples
+from ._lib import call, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_out, crdt_replay_state, crdt_tuples
 
 VC_EQUAL, VC_BEFORE, VC_AFTER, VC_CONCURRENT = 0, 1, 2, 3
 
@@ -259,7 +259,7 @@ class Engine:
             _ptr(d["kv_key"]), _ptr(d["kv_val"]), _ptr(d["str_bytes"]), _ptr(d["str_off"]))
 
     def refmerge_batch(self, packed: dict, maxl: torch.Tensor | None = None,
-                       acc: dict | None = None) -> dict:
+                       acc: dict | None = None, _delta: dict | None = None) -> dict:
         """Run the batched bit-exact reference merge on a packed batch.
 
         ``packed`` holds device tensors produced by
@@ -283,7 +283,10 @@ class Engine:
         cin = self._refmerge_in(d)
         cout = crdt_refmerge_out(*(out[k].data_ptr() for k in
                                    ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum")))
-        if maxl is None and acc is None:
+        if _delta is not None:
+            cs = self._rstate(_delta)
+            self._call("crdt_refmerge_delta", C.byref(cin), C.byref(cout), C.byref(cs))
+        elif maxl is None and acc is None:
             self._call("crdt_refmerge_batch", C.byref(cin), C.byref(cout))
         else:
             if maxl is not None:
@@ -291,6 +294,30 @@ class Engine:
             cacc = self._acc(acc) if acc is not None else None
             self._call("crdt_refmerge_batch_ex", C.byref(cin), C.byref(cout),
                        maxl.data_ptr() if maxl is not None else None, C.byref(cacc) if cacc is not None else None)
+        return out
+
+    # -- incremental replay
+    def replay_state_new(self, n_slots: int) -> dict:
+        n = max(n_slots, 1)
+        z = lambda dt: torch.zeros(n, dtype=dt, device=self.device)
+        return {"best_key": z(torch.int64), "best_str": z(torch.int32), "sum": z(torch.int64),
+                "npar": z(torch.int32), "nhold": z(torch.int32)}
+
+    @staticmethod
+    def _rstate(st: dict) -> crdt_replay_state:
+        return crdt_replay_state(*(st[k].data_ptr() for k in ("best_key", "best_str", "sum", "npar", "nhold")))
+
+    def replay_state_init(self, packed: dict, st: dict | None = None) -> dict:
+        """Replay state of the batch's L logs (crdt_replay_state_init)."""
+        st = self.replay_state_new(int(packed["n_slots"])) if st is None else st
+        cin, cs = self._refmerge_in(packed), self._rstate(st)
+        self._call("crdt_replay_state_init", C.byref(cin), C.byref(cs))
+        return st
+
+    def refmerge_delta(self, packed: dict, st: dict) -> dict:
+        """crdt_refmerge_batch with the replay folded incrementally into
+        ``st`` (the state of ``packed``'s L logs; updated in place)."""
+        out = self.refmerge_batch(packed, _delta=st)
         return out
 
     # -- ts-range-sharded RefMerge steps (SURVEY §8(e))

@@ -238,6 +238,28 @@ int crdt_refmerge_acc_set_best(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size
                                const int64_t *v_dev);
 int crdt_refmerge_finalize(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, const uint8_t *str_bytes_dev,
                            const uint64_t *str_off_dev, uint64_t n_str, const crdt_refmerge_out *out);
+
+/* Incremental replay (§8(f) row 3).  The reference re-folds the whole Diff
+ * on every merge (main.go:76); a merge only adds remote entries, so a
+ * per-key state keyed by ts can be carried across merges:
+ *   crdt_replay_state_init(L)     -- state of the L logs' remote entries;
+ *   crdt_refmerge_delta(L, R, st) -- the merge of crdt_refmerge_batch, but
+ *       the replay folds only the inserted R entries into st (updated in
+ *       place) and CurrentState (st_*) is finalised from st.
+ * Bit-exact with crdt_refmerge_batch as long as st describes the L passed
+ * in: after a delta merge the caller's next L is the new Diff.  A local
+ * write that replaces a remote entry at the same ms (main.go:187) removes a
+ * holder: rebuild st with crdt_replay_state_init then. */
+typedef struct crdt_replay_state {
+    uint64_t *best_key;  /* [n_slots] max over remote holders of ts ^ 2^63 (order-preserving) */
+    uint32_t *best_str;  /* [n_slots] string id of that holder */
+    int64_t  *sum;       /* [n_slots] wrapped sum of the parsable values */
+    uint32_t *npar;      /* [n_slots] parsable holders */
+    uint32_t *nhold;     /* [n_slots] remote holders (0: key absent from CurrentState) */
+} crdt_replay_state;
+int crdt_replay_state_init(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_replay_state *st);
+int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out,
+                        const crdt_replay_state *st);
 /* Go strconv.Atoi over a string arena: ok[s] = parsable, val[s] = value. */
 int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *str_bytes_dev, const uint64_t *str_off_dev,
                     uint64_t n_str, uint8_t *ok_dev, int64_t *val_dev);
