@@ -456,7 +456,59 @@ class RefMergeDelta(RefMergeBatch):
         return None
 
 
+class GossipRound(Workload):
+    """Anti-entropy round (crdt_amd.gossip): every replica
+    of a configs[0]-shaped population pulls a random peer's whole Diff
+    (entries + kv pairs re-based to its key slots), all replicas merge in one
+    batched call, and the next Diffs are materialised.  Each step restarts
+    from the same initial population (the round does not modify its input
+    tensors), with a fresh peer draw."""
+    name = "gossip_round"
+    unit = "remote-entries/s"
+    dtype = "int64"
+    kernel = "gossip round (crdt_seg_* assembly + refmerge + Diff materialisation)"
+
+    def __init__(self, eng, rank, world, replicas, entries, seed=2024):
+        from crdt_amd import gossip, synth
+        h = synth.refmerge_packed(seed + rank, replicas, entries)
+        n_l = len(h["l_ts"])
+        host = {"replicas": replicas, "l_off": h["l_off"], "l_ts": h["l_ts"], "l_origin": h["l_origin"],
+                "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
+                "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
+        self.pop = gossip.Population(eng, host, 62)
+        self.init = (self.pop.off, self.pop.ts, self.pop.origin, self.pop.kv_off, self.pop.kv_key, self.pop.kv_val)
+        self.rng = np.random.default_rng(seed)
+        self.gossip, self.P, self.n_l = gossip, replicas, n_l
+        self.peers = gossip.random_peers(self.rng, replicas, 0, replicas)
+        out = self.step()
+        torch.cuda.synchronize()
+        self.n_out = int(out["off"][-1].item())
+        self.config = {"workload": f"gossip round: {replicas} replicas x {entries} Diff entries each pull a random "
+                                   "peer's Diff and merge (BASELINE configs[0] shape at scale)",
+                       "replicas": replicas, "entries": entries, "n_new_diff": self.n_out,
+                       "parallelism": f"replicas x{world}"}
+
+    def units(self):
+        return self.n_l                      # every pulled entry (a peer's whole Diff per replica)
+
+    def bytes_per_launch(self):
+        # R assembly (read + write ts, kv range, kv pair), the merge (inputs + outputs once),
+        # the next Diff's kv gather (read + write kv pair, write kv range)
+        n_r, n_out = self.n_l, self.n_out
+        return n_r * 24 * 2 + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
+
+    def step(self):
+        p = self.pop
+        p.off, p.ts, p.origin, p.kv_off, p.kv_key, p.kv_val = self.init
+        return p.round(self.peers)
+
+    def cpu_baseline(self, seconds, threads):
+        return None
+
+
 def make_workload(name, eng, rank, world, args):
+    if name == "gossip_round":
+        return GossipRound(eng, rank, world, args.replicas, args.entries)
     if name == "refmerge":
         return RefMergeBatch(eng, rank, world, args.replicas, args.entries)
     if name == "refmerge_delta":
@@ -498,7 +550,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="gcounter_join",
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge", "lww_merge_d2", "orset_merge_d2",
-                             "shard_fold", "shard_join", "refmerge", "refmerge_delta"])
+                             "shard_fold", "shard_join", "refmerge", "refmerge_delta", "gossip_round"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)

@@ -146,6 +146,11 @@ SIGNATURES = {
     "crdt_server_diff_len": (_I, [_P, C.POINTER(_SZ)]),
     "crdt_server_remote_len": (_I, [_P, C.POINTER(_SZ)]),
     "crdt_server_diff_keys": (_I, [_P, _P, _P, _SZ, C.POINTER(_SZ)]),
+    "crdt_seg_offsets": (_I, [_CTX, _SZ, _P, _P, _P, _U64, _P]),
+    "crdt_seg_copy": (_I, [_CTX, _SZ, _P, _P, _P, _P, _SZ, _P, _P, _P, _P, _I]),
+    "crdt_seg_fill_u32": (_I, [_CTX, _SZ, _P, _P, _P]),
+    "crdt_counts_to_offsets": (_I, [_CTX, _P, _SZ, _U64, _P]),
+    "crdt_offsets_to_counts": (_I, [_CTX, _P, _SZ, _P]),
     "crdt_server_gossip_json": (_I, [_P, C.c_char_p, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_server_ingest_json": (_I, [_P, C.c_char_p, _SZ, C.POINTER(C.c_int)]),
     "crdt_server_set_alive": (_I, [_P, _I]),

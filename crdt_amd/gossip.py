@@ -1,0 +1,240 @@
+"""Anti-entropy rounds on the GPU.
+
+The reference runs one gossip goroutine per Server (main.go:226-261): every
+round it picks a random friend, GETs its /gossip (the friend's whole Diff,
+main.go:159), decodes it into RemoteDiff (every pulled entry becomes a remote
+map, main.go:245-256) and merges (main.go:257).  Here a population of
+replicas lives in HBM in the crdt_refmerge_in layout and a whole round runs
+as device passes:
+
+  1. RemoteDiff of replica p := the Diff segment of its peer q -- a segmented
+     copy of q's entries (crdt_seg_copy), then of their kv pairs with the key
+     slots re-based from q's slot range to p's (a per-entry slot delta);
+  2. the bit-exact merge of every replica at once (crdt_refmerge_batch);
+  3. the next Diff := the merge's new Diff, its kv pairs gathered by `src`
+     from the L / R arena (crdt_seg_copy with the merge's own +/- coding).
+
+Rounds are synchronous (every replica pulls the Diffs as of the round's
+start), one legal schedule of the reference's asynchronous goroutines.
+Across GPUs (one process per GPU, replicas partitioned by contiguous
+ranges) each rank all-gathers the population's Diffs once per round over
+RCCL and pulls any peer from that import block.
+
+Key slots: local replica i's key k is slot i*K + k (K keys per replica).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import shard
+from .engine import Engine
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+class Population:
+    """P replicas' Diffs (this rank's block of a population) on one GPU."""
+
+    def __init__(self, eng: Engine, host: dict, keys_per_replica: int, first: int = 0):
+        """host: numpy arrays {replicas, l_off, l_ts, l_origin, l_kv, kv_key
+        (local slot ids), kv_val, str_bytes, str_off}; `first` = global id of
+        local replica 0."""
+        self.eng, self.K, self.first = eng, int(keys_per_replica), int(first)
+        self.P = int(host["replicas"])
+        dev = eng.device
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+        self.off = t(host["l_off"], np.int64)
+        self.ts = t(host["l_ts"], np.int64)
+        self.origin = t(host["l_origin"], np.uint8)
+        self.kv_off = t(host["l_kv"], np.int64)
+        self.kv_key = t(np.asarray(host["kv_key"]).view(np.uint32).view(np.int32), np.int32)
+        self.kv_val = t(np.asarray(host["kv_val"]).view(np.uint32).view(np.int32), np.int32)
+        self.str_bytes = t(host["str_bytes"], np.uint8)
+        self.str_off = t(host["str_off"], np.int64)
+        self.state = None
+
+    # ---------------------------------------------------------------- helpers
+    def _call(self, fn, *args):
+        self.eng._call(fn, *args)
+
+    def _seg_offsets(self, codes, a_off, b_off, base=0):
+        out = torch.empty(codes.numel() + 1, dtype=torch.int64, device=self.eng.device)
+        self._call("crdt_seg_offsets", codes.numel(), _p(codes), _p(a_off), _p(b_off), int(base), _p(out))
+        return out
+
+    def _seg_copy(self, codes, a_off, b_off, dst_off, a, b, n_out, delta=None, wide=0):
+        dst = torch.empty(max(int(n_out), 1), dtype=a.dtype, device=self.eng.device)
+        self._call("crdt_seg_copy", codes.numel(), _p(codes), _p(a_off), _p(b_off), _p(dst_off), a.element_size(),
+                   _p(a), _p(b), _p(dst), _p(delta), wide)
+        return dst[: int(n_out)]
+
+    def _counts(self, off):
+        c = torch.empty(max(off.numel() - 1, 1), dtype=torch.int32, device=self.eng.device)
+        self._call("crdt_offsets_to_counts", _p(off), off.numel() - 1, _p(c))
+        return c[: off.numel() - 1]
+
+    def _offsets(self, counts, base=0):
+        o = torch.empty(counts.numel() + 1, dtype=torch.int64, device=self.eng.device)
+        self._call("crdt_counts_to_offsets", _p(counts), counts.numel(), int(base), _p(o))
+        return o
+
+    def _iota(self, n, negative=False):
+        a = torch.arange(n, dtype=torch.int64, device=self.eng.device)
+        return -(a + 1) if negative else a
+
+    # ---------------------------------------------------------------- exchange
+    def export_block(self) -> List[torch.Tensor]:
+        """This rank's Diffs as the 5 flat arrays an import block is built
+        from: entries per replica, ts, kv pairs per entry, kv keys, values."""
+        return [self._counts(self.off), self.ts, self._counts(self.kv_off), self.kv_key, self.kv_val]
+
+    def import_from_blocks(self, blocks: Sequence[List[torch.Tensor]]) -> dict:
+        """Concatenate every rank's exported block (rank order = global
+        replica order) into one import block (the 'B' source of a round)."""
+        cat = [torch.cat([b[i] for b in blocks]) for i in range(5)]
+        return self._make_import(*cat)
+
+    def gather_import(self, group=None) -> dict:
+        """All-gather the population's Diffs (one all-gather-v per array)."""
+        blk = self.export_block()
+        return self._make_import(*[shard.allgather_v(x, group) for x in blk])
+
+    def _make_import(self, ecnt, ts, kvcnt, kkey, kval) -> dict:
+        return {"off": self._offsets(ecnt.contiguous()), "ts": ts.contiguous(),
+                "kv_off": self._offsets(kvcnt.contiguous()), "kv_key": kkey.contiguous(),
+                "kv_val": kval.contiguous()}
+
+    # ---------------------------------------------------------------- rounds
+    def round(self, peers: Sequence[int], imp: dict | None = None, peer_first: Sequence[int] | None = None) -> dict:
+        """One pull round: local replica i pulls the Diff of global replica
+        peers[i] and merges.  imp = None: every peer is local (this rank);
+        else peers index the import block (global ids) and peer_first[i] is
+        the global id of the first replica on the peer's rank (for the slot
+        re-basing).  Returns the merge output (new-Diff ranges and state)."""
+        eng, dev, K = self.eng, self.eng.device, self.K
+        peers = np.asarray(peers, dtype=np.int64)
+        assert len(peers) == self.P
+        if imp is None:
+            lq = peers - self.first
+            assert np.all((lq >= 0) & (lq < self.P)), "peer not on this rank: pass an import block"
+            codes_np = lq
+            b = {"off": None, "ts": None, "kv_off": None, "kv_key": None, "kv_val": None}
+        else:
+            codes_np = -(peers + 1)
+            b = imp
+            lq = peers - np.asarray(peer_first if peer_first is not None else np.zeros_like(peers), dtype=np.int64)
+        # the slot re-basing of each pulled pair: (i - local index of q) * K, mod 2^32
+        delta_np = ((np.arange(self.P, dtype=np.int64) - lq) * K) % (1 << 32)
+        codes = torch.from_numpy(codes_np.copy()).to(dev)
+        delta = torch.from_numpy(delta_np.astype(np.uint32).view(np.int32)).to(dev)
+
+        # 1. RemoteDiff: entries, then their kv pairs behind the Diff's kv pairs in one arena
+        r_off = self._seg_offsets(codes, self.off, b["off"])
+        n_r = int(r_off[-1].item())
+        n_a = self.ts.numel()
+        n_b = b["ts"].numel() if b["ts"] is not None else 0
+        ecodes = self._seg_copy(codes, self.off, b["off"], r_off, self._iota(n_a), self._iota(max(n_b, 1), True),
+                                n_r, wide=1)
+        r_ts = self._seg_copy(codes, self.off, b["off"], r_off, self.ts, b["ts"] if n_b else self.ts, n_r, wide=1)
+        edelta = torch.empty(max(n_r, 1), dtype=torch.int32, device=dev)
+        self._call("crdt_seg_fill_u32", self.P, _p(r_off), _p(delta), _p(edelta))
+        n_lkv = self.kv_key.numel()
+        r_kv = self._seg_offsets(ecodes, self.kv_off, b["kv_off"], base=n_lkv)
+        n_rkv = int(r_kv[-1].item()) - n_lkv
+        arena_k = torch.empty(max(n_lkv + n_rkv, 1), dtype=torch.int32, device=dev)
+        arena_v = torch.empty_like(arena_k)
+        arena_k[:n_lkv].copy_(self.kv_key)
+        arena_v[:n_lkv].copy_(self.kv_val)
+        if n_r:
+            bk = b["kv_key"] if n_b else self.kv_key
+            bv = b["kv_val"] if n_b else self.kv_val
+            self._call("crdt_seg_copy", n_r, _p(ecodes), _p(self.kv_off), _p(b["kv_off"]), _p(r_kv), 4,
+                       _p(self.kv_key), _p(bk), _p(arena_k), _p(edelta), 0)
+            self._call("crdt_seg_copy", n_r, _p(ecodes), _p(self.kv_off), _p(b["kv_off"]), _p(r_kv), 4,
+                       _p(self.kv_val), _p(bv), _p(arena_v), None, 0)
+        # 2. the merge of every local replica
+        packed = {"replicas": self.P, "n_slots": self.P * K, "l_off": self.off, "l_ts": self.ts,
+                  "l_origin": self.origin, "l_kv": self.kv_off, "r_off": r_off, "r_ts": r_ts, "r_kv": r_kv,
+                  "kv_key": arena_k[: n_lkv + n_rkv], "kv_val": arena_v[: n_lkv + n_rkv],
+                  "str_bytes": self.str_bytes, "str_off": self.str_off}
+        out = eng.refmerge_batch(packed)
+        # 3. the next Diff: entries from the merge, kv pairs gathered by src
+        n_out = int(out["off"][-1].item())
+        src = out["src"][:n_out].contiguous()
+        new_kv = self._seg_offsets(src, self.kv_off, r_kv)
+        n_kv = int(new_kv[-1].item())
+        # (fresh buffers every round: the views below own no one else's data)
+        self.kv_key = self._seg_copy(src, self.kv_off, r_kv, new_kv, arena_k, arena_k, n_kv)
+        self.kv_val = self._seg_copy(src, self.kv_off, r_kv, new_kv, arena_v, arena_v, n_kv)
+        self.kv_off = new_kv
+        self.off = out["off"]
+        self.ts = out["ts"][:n_out]
+        self.origin = out["origin"][:n_out]
+        self.state = {k: out[k] for k in ("st_kind", "st_str", "st_sum")}
+        return out
+
+    def append_local(self, host_new: dict) -> None:
+        """Local writes (AddCommand's Diff.Put of a *Command, main.go:187)
+        appended after each replica's Diff: host_new = {off (P+1), ts,
+        kv_off, kv_key (local slot ids), kv_val}; every new ts must exceed
+        its replica's current last ts."""
+        dev = self.eng.device
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+        b_off, b_ts = t(host_new["off"], np.int64), t(host_new["ts"], np.int64)
+        b_kv = t(host_new["kv_off"], np.int64)
+        b_key = t(np.asarray(host_new["kv_key"]).astype(np.uint32).view(np.int32), np.int32)
+        b_val = t(np.asarray(host_new["kv_val"]).astype(np.uint32).view(np.int32), np.int32)
+        n_b = b_ts.numel()
+        codes_np = np.empty(2 * self.P, np.int64)
+        codes_np[0::2] = np.arange(self.P)
+        codes_np[1::2] = -(np.arange(self.P) + 1)
+        codes = torch.from_numpy(codes_np).to(dev)
+        d_off = self._seg_offsets(codes, self.off, b_off)
+        n = int(d_off[-1].item())
+        ecodes = self._seg_copy(codes, self.off, b_off, d_off, self._iota(self.ts.numel()),
+                                self._iota(max(n_b, 1), True), n, wide=1)
+        ts = self._seg_copy(codes, self.off, b_off, d_off, self.ts, b_ts, n, wide=1)
+        org = self._seg_copy(codes, self.off, b_off, d_off, self.origin,
+                             torch.ones(max(n_b, 1), dtype=torch.uint8, device=dev), n, wide=1)
+        kv = self._seg_offsets(ecodes, self.kv_off, b_kv)
+        m = int(kv[-1].item())
+        self.kv_key = self._seg_copy(ecodes, self.kv_off, b_kv, kv, self.kv_key, b_key, m)
+        self.kv_val = self._seg_copy(ecodes, self.kv_off, b_kv, kv, self.kv_val, b_val, m)
+        self.kv_off, self.ts, self.origin = kv, ts, org
+        self.off = d_off[0::2].contiguous()
+
+    # ---------------------------------------------------------------- readback
+    def to_host(self) -> dict:
+        g = lambda x: x.cpu().numpy()
+        return {"off": g(self.off), "ts": g(self.ts), "origin": g(self.origin), "kv_off": g(self.kv_off),
+                "kv_key": g(self.kv_key).view(np.uint32), "kv_val": g(self.kv_val).view(np.uint32)}
+
+
+def random_peers(rng: np.random.Generator, total: int, first: int, count: int) -> np.ndarray:
+    """A random friend other than itself for each of replicas [first, first+count)
+    (friendList = every other server, main.go:306-317)."""
+    r = rng.integers(0, total - 1, size=total)
+    ids = np.arange(total)
+    peers = np.where(r >= ids, r + 1, r)
+    return peers[first:first + count]
+
+
+def sharded_round(pop: Population, peers_all: np.ndarray, group=None) -> dict:
+    """One round across the ranks of `group`: every rank all-gathers the
+    population's Diffs, then pulls its replicas' peers from that block."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return pop.round(peers_all[pop.first:pop.first + pop.P])
+    P_all = len(peers_all)
+    firsts = [shard.shard_range(P_all, world, r)[0] for r in range(world)]
+    owner_first = np.array([max(f for f in firsts if f <= q) for q in range(P_all)], dtype=np.int64)
+    imp = pop.gather_import(group)
+    mine = peers_all[pop.first:pop.first + pop.P]
+    return pop.round(mine, imp=imp, peer_first=owner_first[mine])

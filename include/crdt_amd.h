@@ -324,6 +324,27 @@ int crdt_synth_vclock_pairs(crdt_ctx *ctx, uint64_t seed, uint64_t *a_dev, uint6
 int crdt_synth_set_tuples(crdt_ctx *ctx, uint64_t seed, uint32_t side, const crdt_tuples *out,
                           size_t n, uint64_t key_space);
 
+/* ------------------------------------------------ anti-entropy rounds (§8(f) row 4)
+ * Device assembly of gossip pull rounds (main.go:226-261) for a replica
+ * population held in the crdt_refmerge_in layout (crdt_amd/gossip.py).
+ * Segmented copy with two sources: segment s copies source segment code[s]
+ * (>= 0: A's segment code[s]; < 0: B's segment -code[s]-1, B may be NULL
+ * when no code is negative) of elem_size-byte elements (1, 4 or 8) to
+ * dst + dst_off[s] * elem_size; with delta (4-byte elements only) each
+ * element of segment s gets + delta[s] (mod 2^32: key-slot re-basing).
+ * wide = 1: one wave per segment (long segments), else one thread. */
+int crdt_seg_offsets(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
+                     const uint64_t *b_off_dev, uint64_t base, uint64_t *dst_off_dev);
+int crdt_seg_copy(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
+                  const uint64_t *b_off_dev, const uint64_t *dst_off_dev, size_t elem_size, const void *a_dev,
+                  const void *b_dev, void *dst_dev, const uint32_t *delta_dev, int wide);
+/* dst[dst_off[s] .. dst_off[s+1]) = val[s] */
+int crdt_seg_fill_u32(crdt_ctx *ctx, size_t n_seg, const uint64_t *dst_off_dev, const uint32_t *val_dev,
+                      uint32_t *dst_dev);
+/* off[i] = base + sum(counts[0..i)), off[n] = base + total; and back. */
+int crdt_counts_to_offsets(crdt_ctx *ctx, const uint32_t *counts_dev, size_t n, uint64_t base, uint64_t *off_dev);
+int crdt_offsets_to_counts(crdt_ctx *ctx, const uint64_t *off_dev, size_t n, uint32_t *counts_dev);
+
 /* ------------------------------------------------ gossip wire codec (§8(f) row 2)
  * Gossip handler (main.go:153-170): *http_status = 502 ("Unreachable")
  * unless Alive, else 200 with server.Diff.ToJSON() (main.go:159): gods
