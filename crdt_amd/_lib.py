@@ -153,6 +153,8 @@ SIGNATURES = {
     "crdt_offsets_to_counts": (_I, [_CTX, _P, _SZ, _P]),
     "crdt_server_gossip_json": (_I, [_P, C.c_char_p, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_server_ingest_json": (_I, [_P, C.c_char_p, _SZ, C.POINTER(C.c_int)]),
+    "crdt_server_gossip_binary": (_I, [_P, C.c_char_p, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]),
+    "crdt_server_ingest_binary": (_I, [_P, C.c_char_p, _SZ, C.POINTER(C.c_int)]),
     "crdt_server_set_alive": (_I, [_P, _I]),
     "crdt_server_remote_keys": (_I, [_P, _P, _SZ, C.POINTER(_SZ)]),
     "crdt_server_entry_at": (_I, [_P, _I, C.c_int64, _SZ, C.POINTER(C.c_void_p), C.POINTER(_SZ),

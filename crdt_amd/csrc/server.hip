@@ -16,6 +16,7 @@
 // server into one CSR batch, runs ONE device call, and rebuilds Diff and
 // CurrentState from the device result.  There is no CPU merge path.
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -830,5 +831,118 @@ extern "C" int crdt_server_entry_at(crdt_server *srv, int remote, int64_t ts, si
         *val = v.kv[i].second.data();
         *vlen = v.kv[i].second.size();
     }
+    return CRDT_OK;
+}
+
+// ---------------------------------------------------------------- binary SoA gossip codec
+// The same Diff as the JSON body (§8(f) row 2, "move to a binary SoA codec
+// and keep the JSON codec"), with no text round trip: little-endian
+//   char magic[8] = "CRDTSOA1"; u64 n_entries, n_pairs, n_bytes;
+//   i64 ts[n_entries] (ascending); u32 pairs[n_entries];
+//   u32 klen[n_pairs], vlen[n_pairs]; u8 bytes[n_bytes]
+// (each pair's key bytes then value bytes, pairs of an entry sorted by key).
+// Ingest is the decode loop of main.go:245-256 without Atoi: every entry is
+// put into RemoteDiff as a remote map; duplicate ts / keys: the last wins.
+namespace {
+constexpr char kSoaMagic[8] = {'C', 'R', 'D', 'T', 'S', 'O', 'A', '1'};
+
+template <typename T>
+void put_le(std::string &o, T v) {
+    for (size_t i = 0; i < sizeof(T); ++i) o.push_back((char)((uint64_t)v >> (8 * i) & 0xFF));
+}
+
+template <typename T>
+T get_le(const unsigned char *p) {
+    uint64_t v = 0;
+    for (size_t i = 0; i < sizeof(T); ++i) v |= (uint64_t)p[i] << (8 * i);
+    return (T)v;
+}
+}  // namespace
+
+extern "C" int crdt_server_gossip_binary(crdt_server *srv, char *buf, size_t cap, size_t *len, int *http_status) {
+    if (!srv || !len || !http_status) return CRDT_E_INVAL;
+    std::string body;
+    {
+        std::lock_guard<std::mutex> g(srv->s.Lock);
+        if (!srv->s.Alive) {
+            *http_status = 502;
+            body = "Unreachable";
+        } else {
+            *http_status = 200;
+            uint64_t np = 0, nb = 0;
+            std::vector<std::vector<const std::pair<std::string, std::string> *>> sorted;
+            sorted.reserve(srv->s.Diff.size());
+            for (auto &e : srv->s.Diff) {
+                std::vector<const std::pair<std::string, std::string> *> kv;
+                for (auto &x : e.second->kv) {
+                    kv.push_back(&x);
+                    nb += x.first.size() + x.second.size();
+                }
+                std::sort(kv.begin(), kv.end(), [](auto *a, auto *b) { return a->first < b->first; });
+                np += kv.size();
+                sorted.push_back(std::move(kv));
+            }
+            body.append(kSoaMagic, 8);
+            put_le<uint64_t>(body, srv->s.Diff.size());
+            put_le<uint64_t>(body, np);
+            put_le<uint64_t>(body, nb);
+            for (auto &e : srv->s.Diff) put_le<int64_t>(body, e.first);
+            for (auto &kv : sorted) put_le<uint32_t>(body, (uint32_t)kv.size());
+            for (auto &kv : sorted)
+                for (auto *x : kv) put_le<uint32_t>(body, (uint32_t)x->first.size());
+            for (auto &kv : sorted)
+                for (auto *x : kv) put_le<uint32_t>(body, (uint32_t)x->second.size());
+            for (auto &kv : sorted)
+                for (auto *x : kv) {
+                    body += x->first;
+                    body += x->second;
+                }
+        }
+    }
+    *len = body.size();
+    if (!buf || cap < body.size()) return CRDT_E_RANGE;
+    std::copy(body.begin(), body.end(), buf);
+    return CRDT_OK;
+}
+
+// *outcome: 0 = ingested into RemoteDiff; 1 = malformed (nothing ingested).
+extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, size_t len, int *outcome) {
+    if (!srv || !outcome || (!data && len)) return CRDT_E_INVAL;
+    *outcome = 1;
+    const unsigned char *p = reinterpret_cast<const unsigned char *>(data);
+    if (len < 32 || std::memcmp(p, kSoaMagic, 8) != 0) return CRDT_OK;
+    const uint64_t ne = get_le<uint64_t>(p + 8), np = get_le<uint64_t>(p + 16), nb = get_le<uint64_t>(p + 24);
+    // sizes in 128-bit-safe arithmetic: every count is bounded by the body length first
+    if (ne > len / 12 || np > len / 8 || nb > len) return CRDT_OK;
+    const uint64_t need = 32 + ne * 12 + np * 8 + nb;
+    if (need != len) return CRDT_OK;
+    const unsigned char *pts = p + 32, *ppairs = pts + ne * 8, *pkl = ppairs + ne * 4, *pvl = pkl + np * 4,
+                        *pb = pvl + np * 4;
+    uint64_t pairs_total = 0, bytes_total = 0;
+    for (uint64_t i = 0; i < ne; ++i) pairs_total += get_le<uint32_t>(ppairs + 4 * i);
+    if (pairs_total != np) return CRDT_OK;
+    for (uint64_t j = 0; j < np; ++j) bytes_total += (uint64_t)get_le<uint32_t>(pkl + 4 * j) + get_le<uint32_t>(pvl + 4 * j);
+    if (bytes_total != nb) return CRDT_OK;
+    std::vector<std::pair<int64_t, std::shared_ptr<Value>>> puts;
+    puts.reserve(ne);
+    uint64_t j = 0, off = 0;
+    for (uint64_t i = 0; i < ne; ++i) {
+        const uint32_t k = get_le<uint32_t>(ppairs + 4 * i);
+        std::map<std::string, std::string> m;                   // duplicate keys: the last wins
+        for (uint32_t u = 0; u < k; ++u, ++j) {
+            const uint32_t kl = get_le<uint32_t>(pkl + 4 * j), vl = get_le<uint32_t>(pvl + 4 * j);
+            std::string key(reinterpret_cast<const char *>(pb + off), kl);
+            off += kl;
+            m[key] = std::string(reinterpret_cast<const char *>(pb + off), vl);
+            off += vl;
+        }
+        auto v = std::make_shared<Value>();
+        v->local = false;
+        v->kv.assign(m.begin(), m.end());
+        puts.emplace_back(get_le<int64_t>(pts + 8 * i), std::move(v));
+    }
+    std::lock_guard<std::mutex> g(srv->s.Lock);
+    for (auto &pv : puts) srv->s.RemoteDiff[pv.first] = std::move(pv.second);
+    *outcome = 0;
     return CRDT_OK;
 }

@@ -146,6 +146,24 @@ class Server:
             _lib.check("crdt_server_gossip_json", rc)
         return st.value, buf.raw[: n.value]
 
+    def GossipBinary(self) -> Tuple[int, bytes]:
+        """The binary SoA form of the Gossip response (crdt_server_gossip_binary)."""
+        n, st = C.c_size_t(), C.c_int()
+        while True:
+            buf = C.create_string_buffer(max(n.value, 1))
+            rc = _lib.lib().crdt_server_gossip_binary(self._h, buf, n.value, C.byref(n), C.byref(st))
+            if rc != -6:
+                break
+        if rc < 0:
+            _lib.check("crdt_server_gossip_binary", rc)
+        return st.value, buf.raw[: n.value]
+
+    def IngestBinary(self, data: bytes) -> int:
+        """Binary SoA pull decode: 0 = ingested into RemoteDiff, 1 = malformed."""
+        out = C.c_int()
+        call("crdt_server_ingest_binary", self._h, bytes(data), len(data), C.byref(out))
+        return out.value
+
     def SetAlive(self, alive: bool) -> None:
         """AliveState handler (main.go:141-151) after ParseBool."""
         call("crdt_server_set_alive", self._h, 1 if alive else 0)

@@ -358,6 +358,12 @@ int crdt_server_gossip_json(crdt_server *srv, char *buf, size_t cap, size_t *len
  * round skipped (main.go:247-249); 2 a key failed Atoi, the reference's
  * gossip goroutine returns (main.go:252-253), nothing ingested. */
 int crdt_server_ingest_json(crdt_server *srv, const char *data, size_t len, int *outcome);
+/* Binary SoA form of the same Diff (§8(f) row 2: keep JSON for
+ * compatibility, add a binary codec): "CRDTSOA1", u64 n_entries, n_pairs,
+ * n_bytes, i64 ts[], u32 pairs[], u32 klen[], u32 vlen[], bytes (little
+ * endian).  Ingest: *outcome 0 = put into RemoteDiff, 1 = malformed. */
+int crdt_server_gossip_binary(crdt_server *srv, char *buf, size_t cap, size_t *len, int *http_status);
+int crdt_server_ingest_binary(crdt_server *srv, const char *data, size_t len, int *outcome);
 /* AliveState handler (main.go:141-151), after strconv.ParseBool. */
 int crdt_server_set_alive(crdt_server *srv, int alive);
 /* Ascending RemoteDiff keys; writes min(cap, len). */

@@ -166,3 +166,50 @@ def test_ingest_random_bodies_match_restatement():
         assert got == o_remote, body
         s.close()
     assert all(v > 50 for v in seen.values()), seen
+
+
+# ---------------------------------------------------------------- binary SoA codec
+def test_binary_roundtrip_equals_json_roundtrip():
+    """serve binary -> pull binary puts exactly what serve JSON -> pull JSON
+    puts (random Diffs, every byte value in keys and values)."""
+    rng = random.Random(77)
+    for _ in range(30):
+        a = _srv()
+        diff = {}
+        for _ in range(rng.randrange(0, 25)):
+            ts = rng.choice([rng.randrange(-2**63, 2**63), rng.randrange(-9, 9)])
+            kv = {_rand_str(rng, _ALPHA): _rand_str(rng, _ALPHA) for _ in range(rng.randrange(0, 4))}
+            diff[ts] = kv
+            a.Diff.Put(ts, Command(kv) if rng.random() < 0.5 else kv)
+        st, body = a.GossipBinary()
+        assert st == 200 and body[:8] == b"CRDTSOA1"
+        bj, bb = _srv(), _srv()
+        assert bj.IngestGossip(a.Gossip()[1]) == 0
+        assert bb.IngestBinary(body) == 0
+        assert bb.RemoteDiff.Keys() == bj.RemoteDiff.Keys() == sorted(diff)
+        for ts in diff:
+            assert bb.RemoteDiff.Get(ts) == bj.RemoteDiff.Get(ts) == (diff[ts], True)
+        for s in (a, bj, bb):
+            s.close()
+
+
+def test_binary_raw_bytes_survive():
+    """Unlike JSON (invalid UTF-8 -> U+FFFD), the binary codec is byte-exact."""
+    a = _srv([(3, False, {"k": "\xff\x00"})])                # latin-1 -> bytes ff 00
+    b = _srv()
+    assert b.IngestBinary(a.GossipBinary()[1]) == 0
+    got, found = b.RemoteDiff.Get(3)
+    assert found and got == {"k": _dec(b"\xff\x00")}
+
+
+def test_binary_malformed_bodies_rejected():
+    a = _srv([(1, False, {"a": "1"}), (2, True, {"b": "22", "c": "3"})])
+    body = a.GossipBinary()[1]
+    b = _srv()
+    for bad in [b"", b"CRDTSOA1", body[:-1], body + b"x", b"CRDTSOA2" + body[8:],
+                body[:8] + (2**62).to_bytes(8, "little") + body[16:],      # n_entries too large
+                body[:16] + (99).to_bytes(8, "little") + body[24:]]:        # n_pairs inconsistent
+        assert b.IngestBinary(bad) == 1
+    assert b.RemoteDiff.Size() == 0
+    a.SetAlive(False)
+    assert a.GossipBinary() == (502, b"Unreachable")
