@@ -92,3 +92,46 @@ def test_no_gpu_fails_loudly():
         Engine(0)
     ctx = C.c_void_p()
     assert _lib.lib().crdt_ctx_create(0, None, C.byref(ctx)) == -4   # CRDT_E_NODEV
+
+
+def _ctx_functions():
+    """(name, argtypes) of every declared entry point whose first parameter
+    is the context."""
+    with open(os.path.join(ROOT, "include", "crdt_amd.h")) as f:
+        src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    names = re.findall(r"^\s*int\s+(crdt_\w+)\s*\(\s*(?:const\s+)?crdt_ctx\s*\*", src, flags=re.M)
+    return [(n, _lib.SIGNATURES[n][1]) for n in sorted(set(names))]
+
+
+@pytest.mark.parametrize("name,argtypes", _ctx_functions(), ids=[n for n, _ in _ctx_functions()])
+def test_every_device_entry_point_rejects_a_null_context(name, argtypes):
+    """No entry point dereferences a NULL context: each returns a negative
+    crdt_status (CRDT_E_INVAL) instead of crashing the host process."""
+    zero = []
+    for t in argtypes[1:]:
+        zero.append(None if t in (C.c_void_p, C.c_char_p) or issubclass(t, C._Pointer) else 0)
+    rc = getattr(_lib.lib(), name)(None, *zero)
+    if name in ("crdt_ctx_destroy", "crdt_ctx_last_hip_error"):
+        assert rc == 0                               # free(NULL)-like no-op / "no HIP error"
+    else:
+        assert rc < 0, f"{name} returned {rc}"
+
+
+def _srv_functions():
+    with open(os.path.join(ROOT, "include", "crdt_amd.h")) as f:
+        src = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    names = re.findall(r"^\s*int\s+(crdt_server\w*)\s*\(\s*crdt_server\s*\*", src, flags=re.M)
+    return [(n, _lib.SIGNATURES[n][1]) for n in sorted(set(names))]
+
+
+@pytest.mark.parametrize("name,argtypes", _srv_functions(), ids=[n for n, _ in _srv_functions()])
+def test_every_server_entry_point_rejects_a_null_server(name, argtypes):
+    zero = [None if t in (C.c_void_p, C.c_char_p) or issubclass(t, C._Pointer) else 0 for t in argtypes[1:]]
+    rc = getattr(_lib.lib(), name)(None, *zero)
+    if name == "crdt_server_free":
+        assert rc == 0                               # free(NULL)-like no-op
+    elif name == "crdt_servers_merge":
+        assert rc == 0                               # an empty batch
+        assert _lib.lib().crdt_servers_merge(None, 1) == -1
+    else:
+        assert rc < 0, f"{name} returned {rc}"
