@@ -67,8 +67,12 @@ __device__ __forceinline__ bool g_le_lazy(const crdt_tuples &A, size_t i, const 
 // elements.  P(i) = A[i] <= B[d-1-i] is true for i < answer, false after.
 // (One diagonal per wave with 64 probes per round was 2x slower: four times
 // the waves, and a key tie in any lane stalls the whole wave's round.)
+// It also zeroes the merge's look-back status words and tile counter
+// (zero_words of them): one launch instead of a memset plus a launch.
 __global__ __launch_bounds__(256) void k_partition(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
-                                                   size_t tile, size_t ntiles, uint64_t *__restrict__ split) {
+                                                   size_t tile, size_t ntiles, uint64_t *__restrict__ split,
+                                                   uint64_t *__restrict__ zero, size_t zero_words) {
+    for (size_t z = (size_t)blockIdx.x * 256 + threadIdx.x; z < zero_words; z += (size_t)gridDim.x * 256) zero[z] = 0;
     const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
     const size_t t = ((((size_t)blockIdx.x * 256 + threadIdx.x) >> 6) << 2) + (size_t)grp;
     const size_t n = na + nb;
@@ -768,7 +772,7 @@ static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const 
     const crdt_tuples *sides[2] = {&A, &B};
     for (const crdt_tuples *t : sides)
         if (((uintptr_t)t->key | (uintptr_t)t->ts) & 7 || (uintptr_t)t->rep & 3) return CRDT_E_INVAL;
-    // status words + tile counter first (one memset), split after
+    // status words + tile counter first (zeroed by k_partition), split after
     const size_t b_status = Carve::round((ntiles + 4) * sizeof(uint64_t));
     const size_t b_split = Carve::round((ntiles + 1) * sizeof(uint64_t));
     const size_t b_stamps = g_sets_stamps ? Carve::round(ntiles * 16 * sizeof(uint64_t)) : 0;
@@ -783,10 +787,10 @@ static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const 
     g_last_stamps = stamps;
     g_last_stamps_n = stamps ? ntiles * 16 : 0;
     const hipStream_t s = ctx->stream;
-    hipError_t e = hipMemsetAsync(status, 0, b_status, s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
+    hipError_t e = hipSuccess;
     const size_t diags = ntiles + 1;                      // 4 diagonals per wave, 16 per block
-    k_partition<<<(unsigned)((diags + 15) / 16), 256, 0, s>>>(A, B, na, nb, TILE, ntiles, split);
+    k_partition<<<(unsigned)((diags + 15) / 16), 256, 0, s>>>(A, B, na, nb, TILE, ntiles, split, status,
+                                                              b_status / sizeof(uint64_t));
     // persistent grid: CUs x the occupancy query (tiles are claimed
     // dynamically, so a workgroup that is not resident owns nothing and any
     // grid is correct; a spilling build is refused: its scratch traffic
