@@ -96,14 +96,23 @@ struct TileGeo {                          // 64 B per tile (per-replica geometry
     uint32_t p, first;                    // replica; first tile of the replica
 };
 
-struct TileDesc {                         // 64 B per tile: everything a tile pass needs, one load
+struct TileDesc {                         // 64 B per tile; a tile pass loads its own and the next one
     uint64_t l0, r0;                      // global index of the tile's first L / R entry
     uint64_t d0;                          // the tile's first diagonal in the replica's merge sequence
     int64_t maxl;                         // insert below this (max(L) of the replica)
     int64_t lprev;                        // L entry just before the tile (valid if has_prev)
-    uint32_t na, nb;                      // L / R entries of the tile; na + nb == 0: no tile
-    uint32_t has_prev, pad[3];
+    uint64_t lend;                        // end of the replica's L (global index)
+    uint32_t n;                           // merge items of the tile; 0: no tile
+    uint32_t has_prev, pad[2];
 };
+
+// The tile's L / R entry counts: its L range ends where the next tile's
+// begins (same replica: d0 > 0) or at the replica's L end.
+__device__ __forceinline__ void tile_counts(const TileDesc &d, const TileDesc &dn, uint32_t *na, uint32_t *nb) {
+    const uint64_t l1 = (dn.n && dn.d0 > 0) ? dn.l0 : d.lend;
+    *na = (uint32_t)(l1 - d.l0);
+    *nb = d.n - *na;
+}
 
 struct alignas(16) OkVal {                // Go Atoi of one arena string: one 16-B gather per lookup
     int64_t val;                          // 0 where !ok
@@ -188,26 +197,25 @@ __device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, co
     return lo;
 }
 
-// Tile descriptors: one wave per tile computes the merge-path splits at
-// its two diagonals (64-ary) and packs the tile's ranges; slots past the
-// tile count get an empty descriptor.
+// Tile descriptors: one wave per tile computes the merge-path split at its
+// first diagonal (64-ary) and packs the tile's ranges (its end is the next
+// descriptor's start); slots past the tile count get an empty descriptor.
 __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t replicas,
                                                   const uint64_t *__restrict__ tbase, const TileGeo *__restrict__ geo,
                                                   uint64_t tmax, TileDesc *__restrict__ desc) {
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (t >= tmax) return;
+    if (t > tmax) return;                                // desc[tmax]: always an empty sentinel
     TileDesc d = {};
     if (t < tbase[replicas]) {
         const TileGeo g = geo[t];
         const uint64_t a0 = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d0, lane);
-        const uint64_t a1 = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d1, lane);
         d.l0 = g.lb + a0;
         d.r0 = g.rb + (g.d0 - a0);
         d.d0 = g.d0;
         d.maxl = g.maxl;
-        d.na = (uint32_t)(a1 - a0);
-        d.nb = (uint32_t)((g.d1 - a1) - (g.d0 - a0));
+        d.lend = g.lb + g.nl;
+        d.n = (uint32_t)(g.d1 - g.d0);
         d.has_prev = a0 > 0;
         d.lprev = a0 > 0 ? in.l_ts[g.lb + a0 - 1] : 0;
     }
@@ -308,8 +316,10 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
     __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> local diagonal + 1
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
-    const TileDesc d = desc[t];
-    const uint32_t na = d.na, nb = d.nb, n = na + nb;
+    const TileDesc d = desc[t], dn = desc[t + 1];
+    uint32_t na, nb;
+    tile_counts(d, dn, &na, &nb);
+    const uint32_t n = na + nb;
     if (n == 0) {
         if (threadIdx.x == 0) tcnt[t] = 0;              // the scan runs over the whole grid
         return;
@@ -356,8 +366,10 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     __shared__ unsigned long long t_sum[TT];
     __shared__ uint32_t t_npar[TT];
     const uint64_t t = blockIdx.x;
-    const TileDesc d = desc[t];
-    const uint32_t na = d.na, nb = d.nb, n = na + nb;
+    const TileDesc d = desc[t], dn = desc[t + 1];
+    uint32_t na, nb;
+    tile_counts(d, dn, &na, &nb);
+    const uint32_t n = na + nb;
     if (n == 0) return;
     const int lane = threadIdx.x & 63;
     for (int h = threadIdx.x; h < TT; h += FB) {
@@ -436,8 +448,10 @@ __global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, const Tile
     __shared__ uint16_t s_idx[MT];                       // output slot -> entry (bit 15: R)
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
-    const TileDesc d = desc[t];
-    const uint32_t na = d.na, nb = d.nb, n = na + nb;
+    const TileDesc d = desc[t], dn = desc[t + 1];
+    uint32_t na, nb;
+    tile_counts(d, dn, &na, &nb);
+    const uint32_t n = na + nb;
     if (n == 0) return;
     const uint64_t ict = ic[t];
     int64_t *sm = s_buf;
@@ -516,20 +530,33 @@ __device__ __forceinline__ uint64_t block_excl_u64(uint64_t v, uint64_t *s_w, ui
 }
 
 // Exclusive scan of n <= kSmallPlan values by one workgroup: each thread
-// sums a contiguous chunk (independent loads), one block scan, then the
-// chunk is re-read (L2-hot) and written.  out[n] = total.
+// holds a contiguous chunk in registers (independent loads), one block
+// scan, then the chunk's prefixes are written.  out[n] = total.
 template <typename Get>
 __device__ __forceinline__ void small_scan(Get get, uint32_t n, uint64_t *__restrict__ out, uint64_t *s_w) {
     const uint32_t per = (n + SB - 1) / SB;
     const uint32_t b = threadIdx.x * per < n ? threadIdx.x * per : n;
     const uint32_t e = b + per < n ? b + per : n;
+    // 8 loads in flight per thread per batch; the second pass re-reads (L2-hot)
     uint64_t sum = 0;
-    for (uint32_t i = b; i < e; ++i) sum += get(i);
+    for (uint32_t c = b; c < e; c += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = c + k < e ? get(c + k) : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += v[k];
+    }
     uint64_t tot;
     uint64_t x = block_excl_u64(sum, s_w, &tot);
-    for (uint32_t i = b; i < e; ++i) {
-        out[i] = x;
-        x += get(i);
+    for (uint32_t c = b; c < e; c += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = c + k < e ? get(c + k) : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (c + k < e) out[c + k] = x;
+            x += v[k];
+        }
     }
     if (threadIdx.x == 0) out[n] = tot;
 }
@@ -706,7 +733,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
     }
     k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
-    k_rm_split<<<(unsigned)((tmax + 3) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
+    k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
     k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, ns && !delta ? l_dk : nullptr, ns ? r_dk : nullptr);
     rc = check_launch(ctx);
