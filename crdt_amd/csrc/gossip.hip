@@ -13,7 +13,9 @@
 // One primitive does all of it: a segmented copy with two sources, where
 // segment s copies source segment code[s] (>= 0: source A, < 0: source B
 // segment -code[s]-1) to dst[dst_off[s]..).  Short segments (kv lists) take
-// a thread each, long ones (per-replica entry ranges) a wave each.
+// a thread each, long ones (per-replica entry ranges) a workgroup each.
+#include <algorithm>
+
 #include "scan.hpp"
 
 namespace crdt {
@@ -68,19 +70,19 @@ __global__ void k_seg_copy_thread(uint64_t n, const int64_t *__restrict__ code, 
     }
 }
 
+// long segments (per-replica entry ranges): a whole workgroup per segment
 template <typename T>
-__global__ void k_seg_copy_wave(uint64_t n, const int64_t *__restrict__ code, const uint64_t *__restrict__ a_off,
-                                const uint64_t *__restrict__ b_off, const uint64_t *__restrict__ dst_off,
-                                const T *__restrict__ a, const T *__restrict__ b, T *__restrict__ dst,
-                                const uint32_t *__restrict__ delta) {
-    const int lane = threadIdx.x & 63;
-    for (uint64_t s = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; s < n; s += ((uint64_t)gridDim.x * 256) >> 6) {
+__global__ void k_seg_copy_block(uint64_t n, const int64_t *__restrict__ code, const uint64_t *__restrict__ a_off,
+                                 const uint64_t *__restrict__ b_off, const uint64_t *__restrict__ dst_off,
+                                 const T *__restrict__ a, const T *__restrict__ b, T *__restrict__ dst,
+                                 const uint32_t *__restrict__ delta) {
+    for (uint64_t s = blockIdx.x; s < n; s += gridDim.x) {
         uint64_t sb, se;
         bool fb;
         seg_src(code[s], a_off, b_off, &sb, &se, &fb);
         const T *src = fb ? b : a;
         const uint64_t o = dst_off[s];
-        for (uint64_t i = sb + lane; i < se; i += 64) dst[o + (i - sb)] = add_delta(src[i], delta, s);
+        for (uint64_t i = sb + threadIdx.x; i < se; i += 256) dst[o + (i - sb)] = add_delta(src[i], delta, s);
     }
 }
 
@@ -99,7 +101,7 @@ static void launch_copy(crdt_ctx *ctx, uint64_t n, const int64_t *code, const ui
                         int wide) {
     const unsigned cap = (unsigned)ctx->num_cus * 8;
     if (wide)
-        k_seg_copy_wave<T><<<grid_for(n * 64, 256, cap), 256, 0, ctx->stream>>>(
+        k_seg_copy_block<T><<<(unsigned)std::min<uint64_t>(n, 65535), 256, 0, ctx->stream>>>(
             n, code, a_off, b_off, dst_off, (const T *)a, (const T *)b, (T *)dst, delta);
     else
         k_seg_copy_thread<T><<<grid_for(n, 256, cap), 256, 0, ctx->stream>>>(

@@ -332,7 +332,7 @@ int crdt_synth_set_tuples(crdt_ctx *ctx, uint64_t seed, uint32_t side, const crd
  * when no code is negative) of elem_size-byte elements (1, 4 or 8) to
  * dst + dst_off[s] * elem_size; with delta (4-byte elements only) each
  * element of segment s gets + delta[s] (mod 2^32: key-slot re-basing).
- * wide = 1: one wave per segment (long segments), else one thread. */
+ * wide = 1: one workgroup per segment (long segments), else one thread. */
 int crdt_seg_offsets(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
                      const uint64_t *b_off_dev, uint64_t base, uint64_t *dst_off_dev);
 int crdt_seg_copy(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
