@@ -11,6 +11,7 @@ int g_sets_stamps = 0;
 int g_sets_grid_per_cu = 0;
 int g_sets_diag = 0;
 int g_rm_diag = 0;
+int g_scan_items = 8;
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -191,6 +192,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 skip the replay fold; 2 no flush, 4 no table, 5 no Atoi gather
         if (v < 0 || v > 5) return CRDT_E_INVAL;
         g_rm_diag = (int)v;
+    } else if (!strcmp(name, "scan.items")) {        // items per lane of the single-pass scan
+        if (v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
+        g_scan_items = (int)v;
     } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sets_stamps = (int)v;

@@ -7,12 +7,14 @@ map, main.go:245-256) and merges (main.go:257).  Here a population of
 replicas lives in HBM in the crdt_refmerge_in layout and a whole round runs
 as device passes:
 
-  1. RemoteDiff of replica p := the Diff segment of its peer q -- a segmented
-     copy of q's entries (crdt_seg_copy), then of their kv pairs with the key
-     slots re-based from q's slot range to p's (a per-entry slot delta);
+  1. RemoteDiff of replica p := the Diff segment of its peer q -- per-replica
+     segmented copies (crdt_seg_copy2): q's ts and kv offsets (re-based by
+     one per-replica delta), then q's kv pairs with the key slots re-based
+     from q's slot range to p's;
   2. the bit-exact merge of every replica at once (crdt_refmerge_batch);
-  3. the next Diff := the merge's new Diff, its kv pairs gathered by `src`
-     from the L / R arena (crdt_seg_copy with the merge's own +/- coding).
+  3. the next Diff := the merge's new Diff, its kv offsets scanned and kv
+     pairs gathered by `src` from the L / R arena in one pass
+     (crdt_seg_gather2 with the merge's own +/- coding).
 
 Rounds are synchronous (every replica pulls the Diffs as of the round's
 start), one legal schedule of the reference's asynchronous goroutines.
@@ -135,30 +137,36 @@ class Population:
         codes = torch.from_numpy(codes_np.copy()).to(dev)
         delta = torch.from_numpy(delta_np.astype(np.uint32).view(np.int32)).to(dev)
 
-        # 1. RemoteDiff: entries, then their kv pairs behind the Diff's kv pairs in one arena
+        # 1. RemoteDiff: entries, then their kv pairs behind the Diff's kv pairs in one arena.
+        # A pulled Diff is one contiguous entry range and one contiguous kv range of its
+        # source, so every copy is per replica: R's kv offsets are the source's offsets
+        # plus a per-replica delta (no per-entry scan).
+        a_kr = self.kv_off[self.off]                       # kv range of each local replica's Diff
+        b_kr = b["kv_off"][b["off"]] if imp is not None else None
         r_off = self._seg_offsets(codes, self.off, b["off"])
-        n_r = int(r_off[-1].item())
-        n_a = self.ts.numel()
-        n_b = b["ts"].numel() if b["ts"] is not None else 0
-        ecodes = self._seg_copy(codes, self.off, b["off"], r_off, self._iota(n_a), self._iota(max(n_b, 1), True),
-                                n_r, wide=1)
-        r_ts = self._seg_copy(codes, self.off, b["off"], r_off, self.ts, b["ts"] if n_b else self.ts, n_r, wide=1)
-        edelta = torch.empty(max(n_r, 1), dtype=torch.int32, device=dev)
-        self._call("crdt_seg_fill_u32", self.P, _p(r_off), _p(delta), _p(edelta))
         n_lkv = self.kv_key.numel()
-        r_kv = self._seg_offsets(ecodes, self.kv_off, b["kv_off"], base=n_lkv)
-        n_rkv = int(r_kv[-1].item()) - n_lkv
+        r_kb = self._seg_offsets(codes, a_kr, b_kr, base=n_lkv)   # where each replica's pulled kv pairs go
+        n_r, n_kv_end = (int(x) for x in torch.stack([r_off[-1], r_kb[-1]]).cpu())
+        n_rkv = n_kv_end - n_lkv
+        n_b = b["ts"].numel() if b["ts"] is not None else 0
+        src_kr = a_kr[codes.clamp(min=0)] if imp is None else b_kr[(-codes - 1).clamp(min=0)]
+        kdelta = r_kb[:-1] - src_kr
+        r_kv = torch.empty(n_r + 1, dtype=torch.int64, device=dev)
+        r_ts = torch.empty(n_r, dtype=torch.int64, device=dev)
+        r_kv[n_r:].copy_(r_kb[-1:])
         arena_k = torch.empty(max(n_lkv + n_rkv, 1), dtype=torch.int32, device=dev)
         arena_v = torch.empty_like(arena_k)
         arena_k[:n_lkv].copy_(self.kv_key)
         arena_v[:n_lkv].copy_(self.kv_val)
         if n_r:
+            bo = b["kv_off"] if n_b else self.kv_off
+            bt = b["ts"] if n_b else self.ts
+            self._call("crdt_seg_copy2", self.P, _p(codes), _p(self.off), _p(b["off"]), _p(r_off), 8,
+                       _p(self.kv_off), _p(bo), _p(r_kv), _p(kdelta), _p(self.ts), _p(bt), _p(r_ts), 1)
             bk = b["kv_key"] if n_b else self.kv_key
             bv = b["kv_val"] if n_b else self.kv_val
-            self._call("crdt_seg_copy", n_r, _p(ecodes), _p(self.kv_off), _p(b["kv_off"]), _p(r_kv), 4,
-                       _p(self.kv_key), _p(bk), _p(arena_k), _p(edelta), 0)
-            self._call("crdt_seg_copy", n_r, _p(ecodes), _p(self.kv_off), _p(b["kv_off"]), _p(r_kv), 4,
-                       _p(self.kv_val), _p(bv), _p(arena_v), None, 0)
+            self._call("crdt_seg_copy2", self.P, _p(codes), _p(a_kr), _p(b_kr), _p(r_kb), 4,
+                       _p(self.kv_key), _p(bk), _p(arena_k), _p(delta), _p(self.kv_val), _p(bv), _p(arena_v), 1)
         # 2. the merge of every local replica
         packed = {"replicas": self.P, "n_slots": self.P * K, "l_off": self.off, "l_ts": self.ts,
                   "l_origin": self.origin, "l_kv": self.kv_off, "r_off": r_off, "r_ts": r_ts, "r_kv": r_kv,
@@ -168,11 +176,15 @@ class Population:
         # 3. the next Diff: entries from the merge, kv pairs gathered by src
         n_out = int(out["off"][-1].item())
         src = out["src"][:n_out].contiguous()
-        new_kv = self._seg_offsets(src, self.kv_off, r_kv)
-        n_kv = int(new_kv[-1].item())
+        # offsets and kv gather in one pass; the arena size bounds the new Diff's kv count
         # (fresh buffers every round: the views below own no one else's data)
-        self.kv_key = self._seg_copy(src, self.kv_off, r_kv, new_kv, arena_k, arena_k, n_kv)
-        self.kv_val = self._seg_copy(src, self.kv_off, r_kv, new_kv, arena_v, arena_v, n_kv)
+        new_kv = torch.empty(n_out + 1, dtype=torch.int64, device=dev)
+        nk = torch.empty_like(arena_k)
+        nv = torch.empty_like(arena_k)
+        self._call("crdt_seg_gather2", n_out, _p(src), _p(self.kv_off), _p(r_kv), 0, _p(new_kv), 4, _p(arena_k),
+                   _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
+        n_kv = int(new_kv[-1].item())
+        self.kv_key, self.kv_val = nk[:n_kv], nv[:n_kv]
         self.kv_off = new_kv
         self.off = out["off"]
         self.ts = out["ts"][:n_out]

@@ -338,6 +338,20 @@ int crdt_seg_offsets(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const
 int crdt_seg_copy(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
                   const uint64_t *b_off_dev, const uint64_t *dst_off_dev, size_t elem_size, const void *a_dev,
                   const void *b_dev, void *dst_dev, const uint32_t *delta_dev, int wide);
+/* Two arrays by the same segment map in one pass: segment s of a0/b0 ->
+ * dst0 with + delta0[s] (an elem_size-byte integer, mod 2^(8*elem_size);
+ * delta0 may be NULL) and, when dst1 != NULL, of a1/b1 -> dst1 verbatim. */
+int crdt_seg_copy2(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
+                   const uint64_t *b_off_dev, const uint64_t *dst_off_dev, size_t elem_size, const void *a0_dev,
+                   const void *b0_dev, void *dst0_dev, const void *delta0_dev, const void *a1_dev,
+                   const void *b1_dev, void *dst1_dev, int wide);
+/* crdt_seg_offsets and a one-thread-per-segment crdt_seg_copy2 (no delta)
+ * fused into one pass: each segment is copied as soon as its scanned offset
+ * is known (dst_off[n_seg] = base + total). */
+int crdt_seg_gather2(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const uint64_t *a_off_dev,
+                     const uint64_t *b_off_dev, uint64_t base, uint64_t *dst_off_dev, size_t elem_size,
+                     const void *a0_dev, const void *b0_dev, void *dst0_dev, const void *a1_dev,
+                     const void *b1_dev, void *dst1_dev);
 /* dst[dst_off[s] .. dst_off[s+1]) = val[s] */
 int crdt_seg_fill_u32(crdt_ctx *ctx, size_t n_seg, const uint64_t *dst_off_dev, const uint32_t *val_dev,
                       uint32_t *dst_dev);
