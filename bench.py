@@ -476,6 +476,7 @@ class GossipRound(Workload):
                 "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
                 "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
         self.pop = gossip.Population(eng, host, 62)
+        self.host = h
         self.init = (self.pop.off, self.pop.ts, self.pop.origin, self.pop.kv_off, self.pop.kv_key, self.pop.kv_val)
         self.rng = np.random.default_rng(seed)
         self.gossip, self.P, self.n_l = gossip, replicas, n_l
@@ -503,7 +504,44 @@ class GossipRound(Workload):
         return p.round(self.peers)
 
     def cpu_baseline(self, seconds, threads):
-        return None
+        """The round's merge on the host: oc_refmerge (C restatement of
+        main.go:35-100) of replica p's Diff with its peer's whole Diff as
+        remote maps (main.go:245-256), one replica per call, independent
+        replicas on `threads` host threads; units = pulled entries.  The
+        per-replica arrays (the pull, with key slots made local) are built
+        before the timed region."""
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle
+        h = self.host
+        n_l = self.n_l
+        kvk, kvv = h["kv_key"].view(np.uint32)[:n_l], h["kv_val"].view(np.uint32)[:n_l]
+        jobs = []
+        for p in range(min(self.P, 4 * threads)):
+            q = int(self.peers[p])
+            lb, le = int(h["l_off"][p]), int(h["l_off"][p + 1])
+            qb, qe = int(h["l_off"][q]), int(h["l_off"][q + 1])
+            lk0, lk1 = int(h["l_kv"][lb]), int(h["l_kv"][le])
+            qk0, qk1 = int(h["l_kv"][qb]), int(h["l_kv"][qe])
+            kv_key = np.concatenate([kvk[lk0:lk1] - np.uint32(p * 62), kvk[qk0:qk1] - np.uint32(q * 62)])
+            kv_val = np.concatenate([kvv[lk0:lk1], kvv[qk0:qk1]])
+            l_kv = (h["l_kv"][lb:le + 1] - lk0).astype(np.uint32)
+            r_kv = (h["l_kv"][qb:qe + 1] - qk0 + (lk1 - lk0)).astype(np.uint32)
+            jobs.append((h["l_ts"][lb:le].copy(), h["l_origin"][lb:le].copy(), l_kv, h["l_ts"][qb:qe].copy(),
+                         r_kv, kv_key, kv_val, qe - qb))
+
+        def run(j):
+            oracle.refmerge_packed(j[0], j[1], j[2], j[3], j[4], j[5], j[6], h["str_bytes"], h["str_off"], 62)
+            return j[7]
+
+        done, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            while time.perf_counter() - t0 < seconds:
+                done += sum(ex.map(run, jobs))
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oc_refmerge (C restatement of main.go:35-100) of a replica's Diff with its peer's "
+                          f"pulled Diff, one replica per call, {len(jobs)} replicas of the round on {threads} "
+                          f"threads, {dt:.1f}s"}
 
 
 def make_workload(name, eng, rank, world, args):

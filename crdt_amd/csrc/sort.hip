@@ -13,18 +13,25 @@
 // per composite (W <= 161).  The last pass decodes the composite straight
 // into the SoA output: the sort moves no payload and gathers nothing.
 //
-// Passes (8-bit digits, P = ceil(W / 8)):
+// Passes (8-bit digits, P = ceil(W / 8)), reduce-then-scan per pass:
 //   k_sort_minmax : field minima/maxima (one read of the input)
-//   k_sort_hist   : composite digit histograms of all P passes at once
-//   k_sort_buckets: per-pass exclusive scan of the 256 buckets
-//   k_sort_pass   : per tile of 4096 composites (ticketed, so tiles are
-//                   processed in order): stable in-tile ranking by wave
-//                   ballots (a few barriers per tile), per-digit decoupled
-//                   look-back (one lane per digit), LDS-staged scatter in
-//                   digit order (runs of ~16 consecutive outputs per digit).
+//   k_sort_up     : per tile of 4096 composites, its 256 digit counts,
+//                   stored digit-major (cnt[d * ntiles + t])
+//   k_sort_colscan: one workgroup per digit: exclusive scan of its column
+//                   of tile counts, and the digit's total
+//   k_sort_pass   : per tile: stable in-tile ranking by wave ballots (a few
+//                   barriers per tile), LDS-staged scatter in digit order
+//                   (runs of ~16 consecutive outputs per digit) from the
+//                   scanned starts (each tile scans the 256 digit totals
+//                   itself for the digit bases).
+// No tile waits on another: a onesweep-style per-digit decoupled look-back
+// (tiles ticketed in order, each digit's lane walking back over published
+// counts) was replaced because on MI355X every status word and ticket is a
+// memory-side round trip across the 8 XCDs' non-coherent L2s; the extra
+// read of the upsweep costs less than those chains.
 #include <algorithm>
 
-#include "common.hpp"
+#include "scan.hpp"
 
 namespace crdt {
 
@@ -153,81 +160,13 @@ __device__ __forceinline__ uint32_t digit_of(const CKey<WORDS> &c, uint32_t pass
     return (uint32_t)(x >> (s & 63)) & 255u;
 }
 
-// ---------------------------------------------------------------- histograms
-template <int WORDS>
-__global__ __launch_bounds__(256) void k_sort_hist(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
-                                                   uint32_t *__restrict__ ghist) {
-    __shared__ uint32_t h[24 * 256];
-    const SortPlan p = *plan_;
-    for (int i = threadIdx.x; i < (int)p.P * 256; i += 256) h[i] = 0;
-    __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        const CKey<WORDS> c = compose<WORDS>(p, in.key[i], in.ts[i], in.rep[i], in.tomb[i]);
-        for (uint32_t q = 0; q < p.P; ++q) atomicAdd(&h[q * 256 + digit_of(c, q)], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < (int)p.P * 256; i += 256)
-        if (h[i]) atomicAdd(&ghist[i], h[i]);
-}
-
-// bucket_start[q][d] = composites of pass q with a digit below d
-__global__ __launch_bounds__(256) void k_sort_buckets(const SortPlan *__restrict__ plan_, const uint32_t *ghist,
-                                                      uint32_t *bstart) {
-    __shared__ uint32_t wsum[SWAVES];
-    const SortPlan p = *plan_;
-    const int d = threadIdx.x, lane = d & 63, w = d >> 6;
-    for (uint32_t q = 0; q < p.P; ++q) {
-        const uint32_t v = ghist[q * 256 + d];
-        uint32_t x = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        uint32_t off = 0;
-        for (int k = 0; k < w; ++k) off += wsum[k];
-        bstart[q * 256 + d] = off + x - v;
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------- one pass
-// status[t*256 + d] = tag | flag | count: tag = pass + 1 (bits 56..63), so a
-// word left by an earlier pass reads as "not published" and the array needs
-// one memset per sort, not per pass.
-constexpr uint64_t kSAgg = 1ULL << 54, kSInc = 2ULL << 54;
-
-template <int WORDS, bool FIRST, bool LAST>
-__global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
-                                                  const SortPlan *__restrict__ plan_, uint32_t pass,
-                                                  const uint32_t *__restrict__ bstart, uint64_t *status,
-                                                  uint32_t *ticket, uint64_t *__restrict__ dst, crdt_tuples out,
-                                                  uint32_t *err) {
-    // wc: per (round, wave, digit) counts, then their exclusive prefix;
-    // reused (after the ranks are taken) as the staging area of the tile
-    constexpr int WC_BYTES = SR * SWAVES * 256 * 2;
-    constexpr int STAGE_BYTES = ST * 8 * WORDS;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[WC_BYTES > STAGE_BYTES ? WC_BYTES : STAGE_BYTES];
-    __shared__ uint32_t s_tot[256], s_lstart[256], s_excl[256];
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t s_wsum[SWAVES];
-    uint16_t *wc = (uint16_t *)lds;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const SortPlan p = *plan_;
-    const uint64_t tag = (uint64_t)(pass + 1) << 56;
-
-    for (int i = tid; i < SR * SWAVES * 256 / 4; i += SB) ((uint64_t *)lds)[i] = 0;
-    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t t = s_tile;
-    const size_t base = (size_t)t * ST;
-
-    // ---- load (and compose on the first pass) SR composites per thread, round-major
-    CKey<WORDS> c[SR];
+// ---------------------------------------------------------------- upsweep
+template <int WORDS, bool FIRST>
+__device__ __forceinline__ void sort_load(const crdt_tuples &in, const uint64_t *__restrict__ src, size_t n,
+                                          const SortPlan &p, size_t base, CKey<WORDS> *c) {
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
-        const size_t e = base + (size_t)r * SB + tid;
+        const size_t e = base + (size_t)r * SB + threadIdx.x;
         if (e < n) {
             if constexpr (FIRST) {
                 c[r] = compose<WORDS>(p, in.key[e], in.ts[e], in.rep[e], in.tomb[e]);
@@ -237,6 +176,87 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
             }
         }
     }
+}
+
+// cnt[d * ntiles + t] = composites of tile t with digit d in this pass
+template <int WORDS, bool FIRST>
+__global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
+                                                const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
+                                                uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t h[SWAVES * 256];          // one histogram per wave: fewer LDS atomic collisions
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
+    const SortPlan p = *plan_;
+    const size_t base = (size_t)blockIdx.x * ST;
+    CKey<WORDS> c[SR];
+    sort_load<WORDS, FIRST>(in, src, n, p, base, c);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SR; ++r)
+        if (base + (size_t)r * SB + tid < n) atomicAdd(&h[w * 256 + digit_of(c[r], pass)], 1u);
+    __syncthreads();
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < SWAVES; ++k) v += h[k * 256 + tid];
+    cnt[(size_t)tid * ntiles + blockIdx.x] = v;
+}
+
+// loc[d * ntiles + t] = tile t's start within digit d's bucket; tot[d] = bucket size
+__global__ __launch_bounds__(256) void k_sort_colscan(const uint32_t *__restrict__ cnt, uint32_t ntiles,
+                                                      uint32_t *__restrict__ loc, uint32_t *__restrict__ tot) {
+    constexpr int K = 8;
+    const uint32_t *c = cnt + (size_t)blockIdx.x * ntiles;
+    uint32_t *o = loc + (size_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += 256 * K) {
+        const uint32_t i0 = t0 + threadIdx.x * K;
+        uint32_t v[K], s = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            v[k] = i0 + k < ntiles ? c[i0 + k] : 0u;
+            s += v[k];
+        }
+        uint64_t all;
+        uint32_t run = carry + (uint32_t)block_exclusive_scan_u64(s, &all);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (i0 + k < ntiles) o[i0 + k] = run;
+            run += v[k];
+        }
+        carry += (uint32_t)all;
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+// ---------------------------------------------------------------- one pass
+// output start of tile t's digit-d composites = (sum of tot[0..d)) + loc[d * ntiles + t]
+template <int WORDS, bool FIRST, bool LAST>
+__global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
+                                                  const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
+                                                  const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
+                                                  uint64_t *__restrict__ dst, crdt_tuples out) {
+    // wc: per (round, wave, digit) counts, then their exclusive prefix;
+    // reused (after the ranks are taken) as the staging area of the tile
+    constexpr int WC_BYTES = SR * SWAVES * 256 * 2;
+    constexpr int STAGE_BYTES = ST * 8 * WORDS;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[WC_BYTES > STAGE_BYTES ? WC_BYTES : STAGE_BYTES];
+    __shared__ uint32_t s_lstart[256], s_excl[256];
+    __shared__ uint32_t s_wsum[SWAVES];
+    uint16_t *wc = (uint16_t *)lds;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const SortPlan p = *plan_;
+    const uint32_t t = blockIdx.x;
+    const size_t base = (size_t)t * ST;
+    for (int i = tid; i < SR * SWAVES * 256 / 4; i += SB) ((uint64_t *)lds)[i] = 0;
+    {
+        const uint32_t lt = loc[(size_t)tid * ntiles + t];
+        uint64_t all;
+        s_excl[tid] = (uint32_t)block_exclusive_scan_u64(tot[tid], &all) + lt;   // barriers inside
+    }
+
+    // ---- load (and compose on the first pass) SR composites per thread, round-major
+    CKey<WORDS> c[SR];
+    sort_load<WORDS, FIRST>(in, src, n, p, base, c);
 
     // ---- stable in-tile rank: wave ballots per round, then one prefix per digit
     uint32_t rk[SR / 4];                      // rank within the wave, 8 bits each
@@ -269,10 +289,6 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
             wc[i * 256 + d] = (uint16_t)run;
             run += v;
         }
-        s_tot[d] = run;
-        // publish this tile's count of digit d at once (decoupled look-back)
-        __hip_atomic_store(status + (size_t)t * 256 + d, tag | (t == 0 ? kSInc : kSAgg) | run, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
         // local start of digit d in the digit-sorted tile
         uint32_t x = run;
         for (int o = 1; o < 64; o <<= 1) {
@@ -309,33 +325,6 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
             }
         }
     }
-    // ---- look-back for digit d (one lane per digit), bounded
-    {
-        const int d = tid;
-        uint64_t excl = 0;
-        if (t > 0) {
-            int64_t b = (int64_t)t - 1;
-            unsigned spins = 0;
-            while (b >= 0) {
-                const uint64_t s =
-                    __hip_atomic_load(status + (size_t)b * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((s & (0xFFULL << 56)) != tag || (s & (3ULL << 54)) == 0) {
-                    if (++spins > (1u << 24)) {
-                        atomicOr(err, CRDT_DEV_LOOKBACK);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += s & 0xFFFFFFFFULL;
-                if (s & kSInc) break;
-                --b;
-            }
-            __hip_atomic_store(status + (size_t)t * 256 + d, tag | kSInc | (excl + s_tot[d]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_excl[d] = bstart[pass * 256 + d] + (uint32_t)excl;
-    }
     __syncthreads();
     // ---- scatter in digit order: consecutive j of one digit -> consecutive outputs
     const size_t cnt = n - base < (size_t)ST ? n - base : (size_t)ST;
@@ -359,31 +348,32 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
 }
 
 template <int WORDS>
-static void launch_pass(bool first, bool last, unsigned grid, hipStream_t s, const crdt_tuples &in,
-                        const uint64_t *src, size_t n, const SortPlan *plan, uint32_t pass, const uint32_t *bstart,
-                        uint64_t *status, uint32_t *ticket, uint64_t *dst, const crdt_tuples &out, uint32_t *err) {
+static void launch_pass(bool first, bool last, unsigned grid, hipStream_t st, const crdt_tuples &in,
+                        const uint64_t *src, size_t n, const SortPlan *plan, uint32_t pass, const uint32_t *loc,
+                        const uint32_t *tot, uint64_t *dst, const crdt_tuples &out) {
     if (first && last)
-        k_sort_pass<WORDS, true, true><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+        k_sort_pass<WORDS, true, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
     else if (first)
-        k_sort_pass<WORDS, true, false><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+        k_sort_pass<WORDS, true, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
     else if (last)
-        k_sort_pass<WORDS, false, true><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+        k_sort_pass<WORDS, false, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
     else
-        k_sort_pass<WORDS, false, false><<<grid, SB, 0, s>>>(in, src, n, plan, pass, bstart, status, ticket, dst, out, err);
+        k_sort_pass<WORDS, false, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
 }
 
 template <int WORDS>
 static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &out, const SortPlan *plan_d,
-                      uint32_t P, uint64_t *bufs, uint32_t *ghist, uint32_t *bstart, uint64_t *status,
-                      uint32_t *tickets) {
-    const hipStream_t s = ctx->stream;
+                      uint32_t P, uint64_t *bufs, uint32_t *cnt, uint32_t *loc, uint32_t *tot) {
+    const hipStream_t st = ctx->stream;
     const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
-    k_sort_hist<WORDS><<<grid_for(n, 256, (unsigned)ctx->num_cus * 4), 256, 0, s>>>(in, n, plan_d, ghist);
-    k_sort_buckets<<<1, 256, 0, s>>>(plan_d, ghist, bstart);
     uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
     for (uint32_t q = 0; q < P; ++q) {
-        launch_pass<WORDS>(q == 0, q + 1 == P, ntiles, s, in, a, n, plan_d, q, bstart, status, tickets + q, b, out,
-                           ctx->dev_status);
+        if (q == 0)
+            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt);
+        else
+            k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt);
+        k_sort_colscan<<<256, 256, 0, st>>>(cnt, ntiles, loc, tot);
+        launch_pass<WORDS>(q == 0, q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
         std::swap(a, b);
     }
     return check_launch(ctx);
@@ -428,26 +418,21 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
     if (!in->key || !in->ts || !in->rep || !in->tomb || !out->key || !out->ts || !out->rep || !out->tomb)
         return CRDT_E_INVAL;
     if (n >= (1ULL << 32)) return CRDT_E_RANGE;       // 32-bit in-tile / bucket arithmetic
-    const size_t ntiles = (n + ST - 1) / ST;
+    const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;
     const size_t b_mm = Carve::round(sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
-    const size_t b_hist = Carve::round(24 * 256 * 4), b_tk = Carve::round(24 * 4);
-    const size_t b_status = Carve::round(ntiles * 256 * 8), b_bufs = Carve::round(2 * 3 * n * 8);
-    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_hist + b_tk + b_status + b_bufs + 1024);
+    const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
+    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + 1024);
     if (rc) return rc;
     Carve w(ctx->ws);
     SortMinMax *mm = w.take<SortMinMax>(1);
     SortPlan *plan = w.take<SortPlan>(1);
-    uint32_t *ghist = w.take<uint32_t>(24 * 256);
-    uint32_t *tickets = w.take<uint32_t>(24);
-    uint64_t *status = w.take<uint64_t>(ntiles * 256);
-    uint32_t *bstart = w.take<uint32_t>(24 * 256);
+    uint32_t *cnt = w.take<uint32_t>(ncnt);
+    uint32_t *loc = w.take<uint32_t>(ncnt);
+    uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
     const hipStream_t s = ctx->stream;
     const SortMinMax init{~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
     hipError_t e = hipMemcpyAsync(mm, &init, sizeof(init), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemsetAsync(ghist, 0, 24 * 256 * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(tickets, 0, 24 * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(status, 0, ntiles * 256 * 8, s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     k_sort_minmax<<<grid_for(n, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(*in, n, mm);
     k_sort_plan<<<1, 1, 0, s>>>(mm, plan);
@@ -456,7 +441,7 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
     e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
-    if (h.words == 1) return sort_words<1>(ctx, *in, n, *out, plan, h.P, bufs, ghist, bstart, status, tickets);
-    if (h.words == 2) return sort_words<2>(ctx, *in, n, *out, plan, h.P, bufs, ghist, bstart, status, tickets);
-    return sort_words<3>(ctx, *in, n, *out, plan, h.P, bufs, ghist, bstart, status, tickets);
+    if (h.words == 1) return sort_words<1>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
+    if (h.words == 2) return sort_words<2>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
+    return sort_words<3>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
 }
