@@ -274,7 +274,29 @@ class SetMergeUnsorted(SetMerge):
         self._fn(self.A, self.B, out=self.out, count=self.count, trim=False)
 
     def cpu_baseline(self, seconds, threads):
-        return None
+        """numpy lexsort of each unsorted side (the oracle's sort order) then
+        the oracle's serial merge, one thread, on a 1M-tuple-per-side slice
+        of the same device inputs (a full-size rep would take too long)."""
+        from oracle import oracle
+        m = min(self.n, 1_000_000)
+        ua = [x[:m] for x in self.UA.to_numpy()]
+        ub = [x[:m] for x in self.UB.to_numpy()]
+        fn = oracle.lww_merge if self.lww else oracle.orset_merge
+
+        def srt(t):
+            o = np.lexsort((t[3], t[2], t[1], t[0]))
+            return tuple(np.ascontiguousarray(x[o]) for x in t)
+
+        done, t0 = 0, time.perf_counter()
+        while True:
+            fn(srt(ua), srt(ub))
+            done += 2 * m
+            if time.perf_counter() - t0 > seconds:
+                break
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": 1, "kind": "port",
+                "sample": f"numpy lexsort of both unsorted sides + oc_{self.name[:-3]} (serial merge), {m} tuples "
+                          f"per side (slice of the device inputs), {done // (2 * m)} reps"}
 
 
 class ShardFold(Workload):
