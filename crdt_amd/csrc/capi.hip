@@ -186,8 +186,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.grid_per_cu")) { // 0 = occupancy query (co-residency required)
         if (v < 0 || v > 16) return CRDT_E_INVAL;
         g_sets_grid_per_cu = (int)v;
-    } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic: WRONG output order
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic, WRONG output: 1 no look-back, 2 loader only
+        if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_sets_diag = (int)v;
     } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 skip the replay fold; 2 no flush, 4 no table, 5 no Atoi gather
         if (v < 0 || v > 5) return CRDT_E_INVAL;

@@ -418,6 +418,18 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
         uint8_t tbm[SET_ITEMS];
         const int dd = tid * SET_ITEMS < b.len ? tid * SET_ITEMS : b.len;
         const int nv = b.len - dd < SET_ITEMS ? b.len - dd : SET_ITEMS;
+        if (diag == 2) {
+            // timing diagnostic only (the loader pipeline's ceiling): the data
+            // waves release each tile unmerged and write nothing
+            data_barrier(&s_dbar, dgen);
+            if (tid == 0) {
+                st_status(status + cur, cur == 0 ? kFlagInc : kFlagAgg);
+                s_tot[k & 3] = 0;
+                lds_publish(&s_tot_tag[k & 3], k + 1);
+                lds_publish(&s_free_tag[bi], k + 1);
+            }
+            continue;
+        }
         {
             int lo = dd > b.nb_t ? dd - b.nb_t : 0, hi = dd < b.na_t ? dd : b.na_t;
             const int jb = b.na_t + dd - 1;   // B index paired with A index i: jb - i
