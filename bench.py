@@ -241,12 +241,14 @@ class SetMerge(Workload):
 
 
 class SetMergeUnsorted(SetMerge):
-    """configs[3] D2: both sides arrive UNSORTED; a step is the device sort
-    of each side (crdt_tuples_sort: LSD radix over the packed composite)
-    followed by the merge.  Algorithmic bytes are those of the merge itself
-    (inputs read once, output written once); the sort's passes are the
-    price of unsorted input, so frac reads against that."""
-    kernel = "k_sort_* (2 sides) + k_partition + k_set_merge"
+    """configs[3] D2: both sides arrive UNSORTED; a step is ONE device sort
+    of both sides together (crdt_*_merge_unsorted: LSD radix over a packed
+    (key, ts, rep, side, tomb) composite, whose order is the stable merge of
+    the sorted sides) followed by a neighbour dedup of the sorted composites.
+    Algorithmic bytes are those of the merge itself (inputs read once, output
+    written once); the sort's passes are the price of unsorted input, so frac
+    reads against that."""
+    kernel = "k_sort_* (both sides at once) + k_dd_count + k_dd_apply"
 
     def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
         self.eng, self.n, self.lww = eng, n, lww
@@ -254,24 +256,20 @@ class SetMergeUnsorted(SetMerge):
         s = seed + 7919 * rank
         self.UA = eng.synth_set_tuples(s, 0, n, key_space, sort=False)
         self.UB = eng.synth_set_tuples(s, 1, n, key_space, sort=False)
-        self.A = E.TupleSet.empty(n, eng.device)
-        self.B = E.TupleSet.empty(n, eng.device)
         self.out = E.TupleSet.empty(2 * n, eng.device)
         self.count = torch.zeros(1, dtype=torch.int64, device=eng.device)
-        self._fn = eng.lww_merge if lww else eng.orset_merge
+        self._fn = eng.lww_merge_unsorted if lww else eng.orset_merge_unsorted
         self.step()
         torch.cuda.synchronize()
         self.n_out = int(self.count.item())
         self.config = {"workload": f"{'LWW-Element-Set' if lww else 'OR-Set'} merge, {n} tuples per side, "
-                                   f"key space {key_space}, UNSORTED inputs: device sort + merge "
+                                   f"key space {key_space}, UNSORTED inputs: one device sort of both sides + dedup "
                                    "(BASELINE configs[3], D2)",
                        "tuples_per_side": n, "key_space": key_space, "n_out": self.n_out,
                        "parallelism": f"replicas x{world}"}
 
     def step(self):
-        self.eng.sort_tuples(self.UA, out=self.A)
-        self.eng.sort_tuples(self.UB, out=self.B)
-        self._fn(self.A, self.B, out=self.out, count=self.count, trim=False)
+        self._fn(self.UA, self.UB, out=self.out, count=self.count, trim=False)
 
     def cpu_baseline(self, seconds, threads):
         """numpy lexsort of each unsorted side (the oracle's sort order) then

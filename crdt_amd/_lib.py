@@ -117,6 +117,10 @@ SIGNATURES = {
                             C.POINTER(crdt_tuples), _P]),
     "crdt_orset_merge": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
                               C.POINTER(crdt_tuples), _P]),
+    "crdt_lww_merge_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                                     C.POINTER(crdt_tuples), _P]),
+    "crdt_orset_merge_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                                       C.POINTER(crdt_tuples), _P]),
     "crdt_tuples_sort": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples)]),
     "crdt_u64_lower_bound": (_I, [_CTX, _P, _SZ, _P, _SZ, _P]),
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),

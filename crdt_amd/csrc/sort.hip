@@ -44,6 +44,9 @@ struct SortPlan {
     uint64_t kmin, tmin, rmin;
     uint32_t bk, bt, br;         // bit widths of the key / ts / rep offsets
     uint32_t W, P, words;        // composite bits, passes, 64-bit words
+    uint32_t b0;                 // bit offset of the rep field: 1 (tomb) + side bits (0 or 1)
+    uint64_t n1;                 // composites [0, n1) come from in (side 0), [n1, n) from in2 (side 1)
+    crdt_tuples in2;
 };
 
 struct SortMinMax {              // reduced with atomics (initialised by the host)
@@ -94,15 +97,18 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, S
     }
 }
 
-__global__ void k_sort_plan(const SortMinMax *mm, SortPlan *plan) {
+__global__ void k_sort_plan(const SortMinMax *mm, SortPlan *plan, uint32_t side_bits, crdt_tuples in2, uint64_t n1) {
     SortPlan p;
+    p.b0 = 1 + side_bits;
+    p.n1 = n1;
+    p.in2 = in2;
     p.kmin = mm->kmin;
     p.tmin = mm->tmin;
     p.rmin = mm->rmin;
     p.bk = bitwidth(mm->kmax - mm->kmin);
     p.bt = bitwidth(mm->tmax - mm->tmin);
     p.br = bitwidth(mm->rmax - mm->rmin);
-    p.W = p.bk + p.bt + p.br + 1;
+    p.W = p.bk + p.bt + p.br + p.b0;
     p.P = (p.W + 7) / 8;
     p.words = (p.W + 63) / 64;
     *plan = p;
@@ -139,15 +145,18 @@ __device__ __forceinline__ uint64_t get_bits(const CKey<WORDS> &c, uint32_t s, u
     }
     return b == 64 ? v : (v & ((1ULL << b) - 1));
 }
+// (key, ts, rep[, side], tomb) from the highest bits down; the side bit (the
+// fused two-input sort) puts A's copy of an equal tag before B's
 template <int WORDS>
-__device__ __forceinline__ CKey<WORDS> compose(const SortPlan &p, uint64_t k, uint64_t t, uint32_t r, uint8_t tomb) {
+__device__ __forceinline__ CKey<WORDS> compose(const SortPlan &p, uint64_t k, uint64_t t, uint32_t r, uint8_t tomb,
+                                               uint32_t side) {
     CKey<WORDS> c;
 #pragma unroll
     for (int q = 0; q < WORDS; ++q) c.w[q] = 0;
-    c.w[0] = tomb ? 1u : 0u;
-    put_bits(c, 1, (uint64_t)(r - p.rmin), p.br);
-    put_bits(c, 1 + p.br, t - p.tmin, p.bt);
-    put_bits(c, 1 + p.br + p.bt, k - p.kmin, p.bk);
+    c.w[0] = (tomb ? 1u : 0u) | ((uint64_t)side << 1);
+    put_bits(c, p.b0, (uint64_t)(r - p.rmin), p.br);
+    put_bits(c, p.b0 + p.br, t - p.tmin, p.bt);
+    put_bits(c, p.b0 + p.br + p.bt, k - p.kmin, p.bk);
     return c;
 }
 template <int WORDS>
@@ -169,7 +178,12 @@ __device__ __forceinline__ void sort_load(const crdt_tuples &in, const uint64_t 
         const size_t e = base + (size_t)r * SB + threadIdx.x;
         if (e < n) {
             if constexpr (FIRST) {
-                c[r] = compose<WORDS>(p, in.key[e], in.ts[e], in.rep[e], in.tomb[e]);
+                if (e < p.n1) {
+                    c[r] = compose<WORDS>(p, in.key[e], in.ts[e], in.rep[e], in.tomb[e], 0);
+                } else {
+                    const size_t f = e - p.n1;
+                    c[r] = compose<WORDS>(p, p.in2.key[f], p.in2.ts[f], p.in2.rep[f], p.in2.tomb[f], 1);
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < WORDS; ++q) c[r].w[q] = src[(size_t)q * n + e];
@@ -336,9 +350,9 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
         const uint32_t d = digit_of(v, pass);
         const size_t o = (size_t)s_excl[d] + (uint32_t)(j - (int)s_lstart[d]);
         if constexpr (LAST) {
-            out.key[o] = p.kmin + get_bits(v, 1 + p.br + p.bt, p.bk);
-            out.ts[o] = p.tmin + get_bits(v, 1 + p.br, p.bt);
-            out.rep[o] = (uint32_t)(p.rmin + get_bits(v, 1, p.br));
+            out.key[o] = p.kmin + get_bits(v, p.b0 + p.br + p.bt, p.bk);
+            out.ts[o] = p.tmin + get_bits(v, p.b0 + p.br, p.bt);
+            out.rep[o] = (uint32_t)(p.rmin + get_bits(v, p.b0, p.br));
             out.tomb[o] = (uint8_t)(v.w[0] & 1u);
         } else {
 #pragma unroll
@@ -361,9 +375,12 @@ static void launch_pass(bool first, bool last, unsigned grid, hipStream_t st, co
         k_sort_pass<WORDS, false, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
 }
 
+// P passes; the last decodes into `out`, or (decode = false) leaves the
+// sorted composites in *result (word-major planes of n)
 template <int WORDS>
 static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &out, const SortPlan *plan_d,
-                      uint32_t P, uint64_t *bufs, uint32_t *cnt, uint32_t *loc, uint32_t *tot) {
+                      uint32_t P, uint64_t *bufs, uint32_t *cnt, uint32_t *loc, uint32_t *tot, bool decode = true,
+                      uint64_t **result = nullptr) {
     const hipStream_t st = ctx->stream;
     const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
     uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
@@ -373,9 +390,10 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
         else
             k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt);
         k_sort_colscan<<<256, 256, 0, st>>>(cnt, ntiles, loc, tot);
-        launch_pass<WORDS>(q == 0, q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
+        launch_pass<WORDS>(q == 0, decode && q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
         std::swap(a, b);
     }
+    if (result) *result = a;
     return check_launch(ctx);
 }
 
@@ -395,6 +413,204 @@ __global__ void k_lower_bound_u64(const uint64_t *__restrict__ v, uint64_t n, co
         }
         out[i] = lo;
     }
+}
+}  // namespace crdt
+
+namespace crdt {
+// ---------------------------------------------------------------- fused D2 merge
+// Unsorted set merge as ONE sort: both sides' tuples go through the radix
+// sort together with a side bit between rep and tomb, composite order
+// (key, ts, rep, side, tomb).  That order IS the stable merge of the two
+// sorted sides (A's copies of an equal tag first, each side's copies by
+// tomb), so the LWW / OR-Set merge reduces to a dedup over neighbours of the
+// sorted composites: no decode pass, no second sort, no merge path.
+//   LWW: emit the last composite of each key run (the key's maximal tag);
+//        its tomb is that of the FIRST composite of its tag run
+//   OR : emit the first composite of each tag run; tomb = OR over the run
+// Count pass (per 2048-composite tile) -> scan of the tile counts -> apply
+// pass (ballot ranks, compacted stores straight to the SoA output).
+enum { DD_LWW = 0, DD_OR = 1 };
+constexpr int DB = 256;              // threads per dedup workgroup
+constexpr int DI = 8;                // composites per thread (round-major)
+constexpr int DT = DB * DI;          // 2048 composites per tile
+
+template <int WORDS>
+__device__ __forceinline__ CKey<WORDS> ck_load(const uint64_t *__restrict__ c, size_t n, size_t e) {
+    CKey<WORDS> v;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) v.w[q] = c[(size_t)q * n + e];
+    return v;
+}
+// bits [s, 64*WORDS) of x and y equal
+template <int WORDS>
+__device__ __forceinline__ bool eq_from(const CKey<WORDS> &x, const CKey<WORDS> &y, uint32_t s) {
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) {
+        const uint32_t lo = 64u * q;
+        if (s >= lo + 64) continue;
+        const uint64_t m = s > lo ? ~0ULL << (s - lo) : ~0ULL;
+        eq = eq && ((x.w[q] ^ y.w[q]) & m) == 0;
+    }
+    return eq;
+}
+template <int MODE, int WORDS>
+__device__ __forceinline__ bool dd_emit(const uint64_t *__restrict__ c, size_t n, size_t e, const CKey<WORDS> &v,
+                                        const SortPlan &p) {
+    if constexpr (MODE == DD_LWW) {
+        if (e + 1 == n) return true;
+        return !eq_from(v, ck_load<WORDS>(c, n, e + 1), p.b0 + p.br + p.bt);
+    } else {
+        if (e == 0) return true;
+        return !eq_from(v, ck_load<WORDS>(c, n, e - 1), p.b0);
+    }
+}
+
+template <int MODE, int WORDS>
+__global__ __launch_bounds__(DB) void k_dd_count(const uint64_t *__restrict__ c, size_t n,
+                                                 const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t s_w[DB / 64];
+    const SortPlan p = *plan_;
+    const size_t base = (size_t)blockIdx.x * DT;
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < DI; ++r) {
+        const size_t e = base + (size_t)r * DB + threadIdx.x;
+        if (e < n) m += dd_emit<MODE, WORDS>(c, n, e, ck_load<WORDS>(c, n, e), p) ? 1u : 0u;
+    }
+    for (int o = 32; o >= 1; o >>= 1) m += __shfl_xor(m, o, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < DB / 64; ++w) t += s_w[w];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+template <int MODE, int WORDS>
+__global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c, size_t n,
+                                                 const SortPlan *__restrict__ plan_, const uint32_t *__restrict__ loc,
+                                                 const uint32_t *__restrict__ tot, crdt_tuples out,
+                                                 uint64_t *__restrict__ out_count) {
+    __shared__ uint32_t s_c[DI * (DB / 64)];      // emits per (round, wave), then their exclusive prefix
+    const SortPlan p = *plan_;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const size_t base = (size_t)blockIdx.x * DT;
+    if (blockIdx.x == 0 && tid == 0) *out_count = tot[0];
+    uint64_t em[DI];
+    CKey<WORDS> v[DI];
+#pragma unroll
+    for (int r = 0; r < DI; ++r) {
+        const size_t e = base + (size_t)r * DB + tid;
+        bool f = false;
+        if (e < n) {
+            v[r] = ck_load<WORDS>(c, n, e);
+            f = dd_emit<MODE, WORDS>(c, n, e, v[r], p);
+        }
+        em[r] = __ballot(f);
+        if (lane == 0) s_c[r * (DB / 64) + w] = (uint32_t)__popcll(em[r]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int i = 0; i < DI * (DB / 64); ++i) {
+            const uint32_t x = s_c[i];
+            s_c[i] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    const size_t t0 = loc[blockIdx.x];
+    const uint32_t sk = p.b0 + p.br + p.bt;
+#pragma unroll
+    for (int r = 0; r < DI; ++r) {
+        if (!((em[r] >> lane) & 1)) continue;
+        const size_t e = base + (size_t)r * DB + tid;
+        const size_t o = t0 + s_c[r * (DB / 64) + w] + (uint32_t)__popcll(em[r] & ((1ULL << lane) - 1ULL));
+        uint8_t tomb;
+        if constexpr (MODE == DD_LWW) {           // tomb of the first copy of this tag
+            size_t j = e;
+            while (j > 0 && eq_from(ck_load<WORDS>(c, n, j - 1), v[r], p.b0)) --j;
+            tomb = (uint8_t)(ck_load<WORDS>(c, n, j).w[0] & 1u);
+        } else {                                  // OR over the tag's copies
+            tomb = (uint8_t)(v[r].w[0] & 1u);
+            for (size_t j = e + 1; j < n; ++j) {
+                const CKey<WORDS> x = ck_load<WORDS>(c, n, j);
+                if (!eq_from(x, v[r], p.b0)) break;
+                tomb |= (uint8_t)(x.w[0] & 1u);
+            }
+        }
+        out.key[o] = p.kmin + get_bits(v[r], sk, p.bk);
+        out.ts[o] = p.tmin + get_bits(v[r], p.b0 + p.br, p.bt);
+        out.rep[o] = (uint32_t)(p.rmin + get_bits(v[r], p.b0, p.br));
+        out.tomb[o] = tomb;
+    }
+}
+
+template <int MODE, int WORDS>
+static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPlan *plan, uint32_t *cnt,
+                       uint32_t *loc, uint32_t *tot, const crdt_tuples &out, uint64_t *out_count) {
+    const hipStream_t st = ctx->stream;
+    const unsigned nt = (unsigned)((n + DT - 1) / DT);
+    k_dd_count<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, cnt);
+    k_sort_colscan<<<1, 256, 0, st>>>(cnt, nt, loc, tot);
+    k_dd_apply<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, loc, tot, out, out_count);
+    return check_launch(ctx);
+}
+
+static bool tuples_full(const crdt_tuples *t) { return t && t->key && t->ts && t->rep && t->tomb; }
+
+template <int MODE>
+static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
+                              crdt_tuples *out, uint64_t *out_count) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!out_count || !tuples_full(out)) return CRDT_E_INVAL;
+    if ((na && !tuples_full(a)) || (nb && !tuples_full(b))) return CRDT_E_INVAL;
+    const size_t n = na + nb;
+    const hipStream_t s = ctx->stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(out_count, 0, sizeof(uint64_t), s);
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    }
+    if (n >= (1ULL << 32)) return CRDT_E_RANGE;       // 32-bit in-tile / bucket arithmetic
+    const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
+    const crdt_tuples A = na ? *a : none, B = nb ? *b : none;
+    const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
+    const size_t b_mm = Carve::round(sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
+    const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
+    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + 1024);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    SortMinMax *mm = w.take<SortMinMax>(1);
+    SortPlan *plan = w.take<SortPlan>(1);
+    uint32_t *cnt = w.take<uint32_t>(ncnt);
+    uint32_t *loc = w.take<uint32_t>(ncnt);
+    uint32_t *tot = w.take<uint32_t>(256);
+    uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
+    const SortMinMax init{~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
+    hipError_t e = hipMemcpyAsync(mm, &init, sizeof(init), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (na) k_sort_minmax<<<grid_for(na, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(A, na, mm);
+    if (nb) k_sort_minmax<<<grid_for(nb, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(B, nb, mm);
+    k_sort_plan<<<1, 1, 0, s>>>(mm, plan, 1, B, na);
+    SortPlan h;
+    e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    uint64_t *sorted = nullptr;
+    if (h.words == 1) {
+        rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
+        return rc ? rc : dedup_words<MODE, 1>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
+    }
+    if (h.words == 2) {
+        rc = sort_words<2>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
+        return rc ? rc : dedup_words<MODE, 2>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
+    }
+    rc = sort_words<3>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
+    return rc ? rc : dedup_words<MODE, 3>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
 }
 }  // namespace crdt
 
@@ -435,7 +651,7 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
     hipError_t e = hipMemcpyAsync(mm, &init, sizeof(init), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     k_sort_minmax<<<grid_for(n, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(*in, n, mm);
-    k_sort_plan<<<1, 1, 0, s>>>(mm, plan);
+    k_sort_plan<<<1, 1, 0, s>>>(mm, plan, 0, crdt_tuples{nullptr, nullptr, nullptr, nullptr}, n);
     // the pass count and composite width decide the launches: one small read-back
     SortPlan h;
     e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
@@ -444,4 +660,14 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
     if (h.words == 1) return sort_words<1>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
     if (h.words == 2) return sort_words<2>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
     return sort_words<3>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
+}
+
+extern "C" int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                                       size_t nb, crdt_tuples *out, uint64_t *out_count_dev) {
+    return set_merge_unsorted<DD_LWW>(ctx, a, na, b, nb, out, out_count_dev);
+}
+
+extern "C" int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                                         size_t nb, crdt_tuples *out, uint64_t *out_count_dev) {
+    return set_merge_unsorted<DD_OR>(ctx, a, na, b, nb, out, out_count_dev);
 }

@@ -222,6 +222,17 @@ class Engine:
         """OR-Set merge: union of tags, tombstones OR-ed."""
         return self._set_merge("crdt_orset_merge", a, b, out, count, trim)
 
+    def lww_merge_unsorted(self, a: TupleSet, b: TupleSet, out: TupleSet | None = None,
+                           count: torch.Tensor | None = None, trim: bool = True):
+        """LWW merge of UNSORTED sides (D2): one fused device sort + dedup;
+        equal to sort_tuples of each side followed by lww_merge."""
+        return self._set_merge("crdt_lww_merge_unsorted", a, b, out, count, trim)
+
+    def orset_merge_unsorted(self, a: TupleSet, b: TupleSet, out: TupleSet | None = None,
+                             count: torch.Tensor | None = None, trim: bool = True):
+        """OR-Set merge of UNSORTED sides (D2): one fused device sort + dedup."""
+        return self._set_merge("crdt_orset_merge_unsorted", a, b, out, count, trim)
+
     def sort_tuples(self, t: TupleSet, out: TupleSet | None = None) -> TupleSet:
         """Device sort into ascending (key, ts, rep, tomb) order (config D2)."""
         n = len(t)

@@ -144,6 +144,17 @@ int crdt_lww_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tu
 /* OR-Set: union of unique tags (key, ts, rep); tomb OR-ed over equal tags. */
 int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                      size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
+/* The same two merges on UNSORTED inputs (config D2), as one device sort of
+ * both sides together with a side bit between rep and tomb -- composite
+ * order (key, ts, rep, side, tomb) is the stable merge of the two sorted
+ * sides -- followed by a neighbour dedup of the sorted composites.  Output
+ * identical to crdt_tuples_sort of each side then crdt_lww_merge /
+ * crdt_orset_merge.  Synchronises the stream once (to size the passes).
+ * na + nb < 2^32; out capacity >= na + nb. */
+int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                            size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
+int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                              size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 /* Sortedness check (host-facing validation): *bad_dev = number of adjacent
  * pairs with t[i] > t[i+1]. */
 /* Sort n SoA tuples (device) into ascending (key, ts, rep, tomb) order --

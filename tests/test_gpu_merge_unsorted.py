@@ -1,0 +1,105 @@
+"""Fused D2 merge (crdt_lww_merge_unsorted / crdt_orset_merge_unsorted): one
+device sort of both unsorted sides with a side bit, then a neighbour dedup.
+Bit-exact against the oracle's merge of the numpy-lexsorted sides -- the same
+expectation as the two-sort path (test_gpu_sort.py) -- across composite widths
+of 1, 2 and 3 words, dedup tile edges, empty sides, cross-side duplicate tags
+with differing tombs, and a full config-D pair checked by the two-sort path."""
+import numpy as np
+import pytest
+
+from crdt_amd import synth
+from crdt_amd.engine import TupleSet
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+MODES = [("lww", oracle.lww_merge), ("orset", oracle.orset_merge)]
+
+
+def _np_sorted(t):
+    o = np.lexsort((t[3], t[2], t[1], t[0]))
+    return tuple(np.ascontiguousarray(x[o]) for x in t)
+
+
+def _empty():
+    return (np.zeros(0, np.uint64), np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+
+
+def _check(eng, ua, ub):
+    A = TupleSet.from_numpy(*ua, eng.device)
+    B = TupleSet.from_numpy(*ub, eng.device)
+    sa, sb = _np_sorted(ua), _np_sorted(ub)
+    for name, ref in MODES:
+        fn = getattr(eng, f"{name}_merge_unsorted")
+        got = fn(A, B).to_numpy()
+        exp = ref(sa, sb)
+        for g, e, f in zip(got, exp, ("key", "ts", "rep", "tomb")):
+            np.testing.assert_array_equal(g, e, err_msg=f"{name} {f}")
+    assert eng.device_status() == 0
+
+
+@pytest.mark.parametrize("na,nb", [(1, 0), (0, 1), (1, 1), (2047, 1), (1024, 1024), (1025, 1024),
+                                   (4096, 4097), (30_000, 7), (100_000, 120_000)])
+def test_unsorted_config_d_shape(eng, na, nb):
+    ks = max(1, (na + nb) // 3)
+    _check(eng, synth.set_tuples(5 + na, 0, na, ks), synth.set_tuples(5 + na, 1, nb, ks))
+
+
+def test_unsorted_empty_both(eng):
+    A = TupleSet.from_numpy(*_empty(), eng.device)
+    for name, _ in MODES:
+        out = getattr(eng, f"{name}_merge_unsorted")(A, A)
+        assert len(out) == 0
+
+
+def test_unsorted_cross_side_duplicates(eng):
+    """Identical tags on both sides and within a side, tombs differing: the
+    LWW winner's tomb comes from A's lowest-tomb copy; OR ORs every copy."""
+    rng = np.random.default_rng(9)
+    n = 20_000
+    key = rng.integers(0, 300, n, dtype=np.uint64)
+    ts = rng.integers(0, 4, n, dtype=np.uint64)
+    rep = rng.integers(0, 3, n, dtype=np.uint64).astype(np.uint32)
+    ta = rng.integers(0, 2, n, dtype=np.uint8)
+    tb = rng.integers(0, 2, n, dtype=np.uint8)
+    perm = rng.permutation(n)
+    _check(eng, (key, ts, rep, ta), (key[perm], ts[perm], rep[perm], tb[perm]))
+
+
+def test_unsorted_two_and_three_words(eng):
+    rng = np.random.default_rng(10)
+    n = 40_000
+    for kbits, tbits, rbits in ((40, 30, 10), (64, 64, 32)):
+        def side(m):
+            key = rng.integers(0, 2**kbits, m, dtype=np.uint64)
+            key[: m // 10] = key[m // 10: 2 * (m // 10)]          # key ties
+            ts = rng.integers(0, 2**tbits, m, dtype=np.uint64)
+            rep = rng.integers(0, 2**rbits, m, dtype=np.uint64).astype(np.uint32)
+            return key, ts, rep, rng.integers(0, 2, m, dtype=np.uint8)
+        a = side(n)
+        b = side(n - 3)
+        b[0][:500] = a[0][:500]                                    # cross-side equal tags
+        b[1][:500] = a[1][:500]
+        b[2][:500] = a[2][:500]
+        _check(eng, a, b)
+
+
+def test_unsorted_extremes(eng):
+    key = np.array([0, 2**64 - 1, 2**63, 0, 2**64 - 1], np.uint64)
+    ts = np.array([2**64 - 1, 0, 5, 2**64 - 1, 1], np.uint64)
+    rep = np.array([2**32 - 1, 0, 1, 2**32 - 1, 0], np.uint32)
+    tomb = np.array([1, 0, 1, 0, 1], np.uint8)
+    _check(eng, (key, ts, rep, tomb), (key[::-1].copy(), ts[::-1].copy(), rep[::-1].copy(), tomb))
+
+
+def test_unsorted_full_config_d_equals_two_sort_path(eng):
+    n, ks = 10_000_000, 8_000_000
+    UA = eng.synth_set_tuples(2024, 0, n, ks, sort=False)
+    UB = eng.synth_set_tuples(2024, 1, n, ks, sort=False)
+    A, B = eng.sort_tuples(UA), eng.sort_tuples(UB)
+    for name in ("lww", "orset"):
+        ref = getattr(eng, f"{name}_merge")(A, B)
+        got = getattr(eng, f"{name}_merge_unsorted")(UA, UB)
+        assert len(got) == len(ref)
+        for g, e in zip((got.key, got.ts, got.rep, got.tomb), (ref.key, ref.ts, ref.rep, ref.tomb)):
+            assert bool((g == e).all())
