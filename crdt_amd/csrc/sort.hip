@@ -49,23 +49,43 @@ struct SortPlan {
     crdt_tuples in2;
 };
 
-struct SortMinMax {              // reduced with atomics (initialised by the host)
+struct SortMinMax {              // one per minmax workgroup, reduced by k_sort_plan
     unsigned long long kmin, kmax, tmin, tmax, rmin, rmax;
 };
 
 __device__ __forceinline__ uint32_t bitwidth(uint64_t x) { return x ? 64u - (uint32_t)__clzll((long long)x) : 0u; }
 
+// VEC: key / ts / rep 16-byte aligned -- four tuples per lane per step in
+// 16-byte loads (five in flight per lane instead of three 8/4-byte ones)
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, SortMinMax *mm) {
     unsigned long long kmin = ~0ULL, kmax = 0, tmin = ~0ULL, tmax = 0, rmin = ~0ULL, rmax = 0;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        const unsigned long long k = in.key[i], t = in.ts[i], r = in.rep[i];
+    auto acc = [&](unsigned long long k, unsigned long long t, unsigned long long r) {
         kmin = k < kmin ? k : kmin;
         kmax = k > kmax ? k : kmax;
         tmin = t < tmin ? t : tmin;
         tmax = t > tmax ? t : tmax;
         rmin = r < rmin ? r : rmin;
         rmax = r > rmax ? r : rmax;
+    };
+    size_t i0 = 0;
+    if constexpr (VEC) {
+        const size_t n4 = n / 4;
+        const ulonglong2 *K = (const ulonglong2 *)in.key, *T = (const ulonglong2 *)in.ts;
+        const uint4 *R = (const uint4 *)in.rep;
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+            const ulonglong2 k0 = K[2 * i], k1 = K[2 * i + 1];
+            const ulonglong2 t0 = T[2 * i], t1 = T[2 * i + 1];
+            const uint4 r = R[i];
+            acc(k0.x, t0.x, r.x);
+            acc(k0.y, t0.y, r.y);
+            acc(k1.x, t1.x, r.z);
+            acc(k1.y, t1.y, r.w);
+        }
+        i0 = n4 * 4;
     }
+    for (size_t i = i0 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        acc(in.key[i], in.ts[i], in.rep[i]);
     for (int m = 32; m >= 1; m >>= 1) {
         kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, m, 64));
         kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, m, 64));
@@ -74,8 +94,8 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, S
         rmin = min(rmin, (unsigned long long)__shfl_xor(rmin, m, 64));
         rmax = max(rmax, (unsigned long long)__shfl_xor(rmax, m, 64));
     }
-    // workgroup reduction first: one atomic per field per workgroup (six
-    // contended addresses: per-wave atomics took 9x the read time)
+    // workgroup partials, reduced by k_sort_plan (atomics on six shared
+    // addresses serialised: they took as long as the whole read)
     __shared__ unsigned long long sred[6][4];
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -91,13 +111,50 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, S
         const int f = threadIdx.x;
         unsigned long long v = sred[f][0];
         for (int k = 1; k < 4; ++k) v = (f & 1) ? max(v, sred[f][k]) : min(v, sred[f][k]);
-        unsigned long long *dst = &mm->kmin + f;
-        if (f & 1) atomicMax(dst, v);
-        else atomicMin(dst, v);
+        (&mm[blockIdx.x].kmin)[f] = v;
     }
 }
 
-__global__ void k_sort_plan(const SortMinMax *mm, SortPlan *plan, uint32_t side_bits, crdt_tuples in2, uint64_t n1) {
+constexpr unsigned MM_BLOCKS = 1024;   // minmax partials per input (at most)
+
+// returns the number of partials written to mm[0, g)
+static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, SortMinMax *mm) {
+    const bool vec = (((uintptr_t)in.key | (uintptr_t)in.ts | (uintptr_t)in.rep) & 15) == 0;
+    const unsigned g = std::min(MM_BLOCKS, grid_for(vec ? n / 4 + 1 : n, 256, (unsigned)ctx->num_cus * 4));
+    if (vec) k_sort_minmax<true><<<g, 256, 0, ctx->stream>>>(in, n, mm);
+    else k_sort_minmax<false><<<g, 256, 0, ctx->stream>>>(in, n, mm);
+    return g;
+}
+
+// reduces the nmm minmax partials, then thread 0 sizes the composite
+__global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32_t nmm, SortPlan *plan,
+                                                   uint32_t side_bits, crdt_tuples in2, uint64_t n1) {
+    __shared__ unsigned long long sr[6][256];
+    const int tid = threadIdx.x;
+    unsigned long long v[6] = {~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
+    for (uint32_t i = tid; i < nmm; i += 256)
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+            const unsigned long long x = (&mms[i].kmin)[f];
+            v[f] = (f & 1) ? (x > v[f] ? x : v[f]) : (x < v[f] ? x : v[f]);
+        }
+#pragma unroll
+    for (int f = 0; f < 6; ++f) sr[f][tid] = v[f];
+    for (int h = 128; h >= 1; h >>= 1) {      // tree over the 256 thread partials
+        __syncthreads();
+        if (tid < h)
+#pragma unroll
+            for (int f = 0; f < 6; ++f) {
+                const unsigned long long x = sr[f][tid + h], y = sr[f][tid];
+                sr[f][tid] = (f & 1) ? (x > y ? x : y) : (x < y ? x : y);
+            }
+    }
+    __syncthreads();
+    if (tid >= 6) return;
+    const unsigned long long r = sr[tid][0];
+    const SortMinMax m{__shfl(r, 0), __shfl(r, 1), __shfl(r, 2), __shfl(r, 3), __shfl(r, 4), __shfl(r, 5)};
+    if (tid != 0) return;
+    const SortMinMax *mm = &m;
     SortPlan p;
     p.b0 = 1 + side_bits;
     p.n1 = n1;
@@ -196,7 +253,7 @@ __device__ __forceinline__ void sort_load(const crdt_tuples &in, const uint64_t 
 template <int WORDS, bool FIRST>
 __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
                                                 const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
-                                                uint32_t *__restrict__ cnt) {
+                                                uint32_t *__restrict__ cnt, uint64_t *__restrict__ comp) {
     __shared__ uint32_t h[SWAVES * 256];          // one histogram per wave: fewer LDS atomic collisions
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
@@ -204,6 +261,15 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
     const size_t base = (size_t)blockIdx.x * ST;
     CKey<WORDS> c[SR];
     sort_load<WORDS, FIRST>(in, src, n, p, base, c);
+    if constexpr (FIRST) {                        // the composites, so pass 0 reads 8 B instead of a tuple
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+            const size_t e = base + (size_t)r * SB + tid;
+            if (e < n)
+#pragma unroll
+                for (int q = 0; q < WORDS; ++q) comp[(size_t)q * n + e] = c[r].w[q];
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < SR; ++r)
@@ -385,12 +451,13 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
     const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
     uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
     for (uint32_t q = 0; q < P; ++q) {
+        // pass 0's upsweep composes from the tuples and stores the composites
         if (q == 0)
-            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt);
+            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a);
         else
-            k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt);
+            k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr);
         k_sort_colscan<<<256, 256, 0, st>>>(cnt, ntiles, loc, tot);
-        launch_pass<WORDS>(q == 0, decode && q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
+        launch_pass<WORDS>(false, decode && q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
         std::swap(a, b);
     }
     if (result) *result = a;
@@ -579,25 +646,22 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples A = na ? *a : none, B = nb ? *b : none;
     const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
-    const size_t b_mm = Carve::round(sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
+    const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
     rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + 1024);
     if (rc) return rc;
     Carve w(ctx->ws);
-    SortMinMax *mm = w.take<SortMinMax>(1);
+    SortMinMax *mm = w.take<SortMinMax>(2 * MM_BLOCKS);
     SortPlan *plan = w.take<SortPlan>(1);
     uint32_t *cnt = w.take<uint32_t>(ncnt);
     uint32_t *loc = w.take<uint32_t>(ncnt);
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
-    const SortMinMax init{~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
-    hipError_t e = hipMemcpyAsync(mm, &init, sizeof(init), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    if (na) k_sort_minmax<<<grid_for(na, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(A, na, mm);
-    if (nb) k_sort_minmax<<<grid_for(nb, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(B, nb, mm);
-    k_sort_plan<<<1, 1, 0, s>>>(mm, plan, 1, B, na);
+    unsigned nmm = na ? launch_minmax(ctx, A, na, mm) : 0;
+    if (nb) nmm += launch_minmax(ctx, B, nb, mm + nmm);
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na);
     SortPlan h;
-    e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
+    hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     uint64_t *sorted = nullptr;
@@ -635,26 +699,23 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
         return CRDT_E_INVAL;
     if (n >= (1ULL << 32)) return CRDT_E_RANGE;       // 32-bit in-tile / bucket arithmetic
     const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;
-    const size_t b_mm = Carve::round(sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
+    const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
     rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + 1024);
     if (rc) return rc;
     Carve w(ctx->ws);
-    SortMinMax *mm = w.take<SortMinMax>(1);
+    SortMinMax *mm = w.take<SortMinMax>(2 * MM_BLOCKS);
     SortPlan *plan = w.take<SortPlan>(1);
     uint32_t *cnt = w.take<uint32_t>(ncnt);
     uint32_t *loc = w.take<uint32_t>(ncnt);
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
     const hipStream_t s = ctx->stream;
-    const SortMinMax init{~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
-    hipError_t e = hipMemcpyAsync(mm, &init, sizeof(init), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    k_sort_minmax<<<grid_for(n, 256, (unsigned)ctx->num_cus * 2), 256, 0, s>>>(*in, n, mm);
-    k_sort_plan<<<1, 1, 0, s>>>(mm, plan, 0, crdt_tuples{nullptr, nullptr, nullptr, nullptr}, n);
+    const unsigned nmm = launch_minmax(ctx, *in, n, mm);
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 0, crdt_tuples{nullptr, nullptr, nullptr, nullptr}, n);
     // the pass count and composite width decide the launches: one small read-back
     SortPlan h;
-    e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
+    hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     if (h.words == 1) return sort_words<1>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
