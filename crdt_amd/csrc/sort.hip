@@ -522,28 +522,37 @@ __device__ __forceinline__ bool eq_from(const CKey<WORDS> &x, const CKey<WORDS> 
     return eq;
 }
 template <int MODE, int WORDS>
-__device__ __forceinline__ bool dd_emit(const uint64_t *__restrict__ c, size_t n, size_t e, const CKey<WORDS> &v,
-                                        const SortPlan &p) {
-    if constexpr (MODE == DD_LWW) {
-        if (e + 1 == n) return true;
-        return !eq_from(v, ck_load<WORDS>(c, n, e + 1), p.b0 + p.br + p.bt);
-    } else {
-        if (e == 0) return true;
-        return !eq_from(v, ck_load<WORDS>(c, n, e - 1), p.b0);
-    }
-}
-
-template <int MODE, int WORDS>
 __global__ __launch_bounds__(DB) void k_dd_count(const uint64_t *__restrict__ c, size_t n,
                                                  const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt) {
     __shared__ uint32_t s_w[DB / 64];
     const SortPlan p = *plan_;
     const size_t base = (size_t)blockIdx.x * DT;
+    const int lane = threadIdx.x & 63;
     uint32_t m = 0;
+    CKey<WORDS> v[DI];
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
         const size_t e = base + (size_t)r * DB + threadIdx.x;
-        if (e < n) m += dd_emit<MODE, WORDS>(c, n, e, ck_load<WORDS>(c, n, e), p) ? 1u : 0u;
+        if (e < n) v[r] = ck_load<WORDS>(c, n, e);
+        else
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) v[r].w[q] = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < DI; ++r) {                // neighbour from the adjacent lane; edge lanes load it
+        const size_t e = base + (size_t)r * DB + threadIdx.x;
+        CKey<WORDS> nb;
+        if constexpr (MODE == DD_LWW) {
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) nb.w[q] = (uint64_t)__shfl_down((unsigned long long)v[r].w[q], 1, 64);
+            if (lane == 63 && e + 1 < n) nb = ck_load<WORDS>(c, n, e + 1);
+            m += (e < n && (e + 1 == n || !eq_from(v[r], nb, p.b0 + p.br + p.bt))) ? 1u : 0u;
+        } else {
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) nb.w[q] = (uint64_t)__shfl_up((unsigned long long)v[r].w[q], 1, 64);
+            if (lane == 0 && e > 0 && e < n) nb = ck_load<WORDS>(c, n, e - 1);
+            m += (e < n && (e == 0 || !eq_from(v[r], nb, p.b0))) ? 1u : 0u;
+        }
     }
     for (int o = 32; o >= 1; o >>= 1) m += __shfl_xor(m, o, 64);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = m;
@@ -566,15 +575,40 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const size_t base = (size_t)blockIdx.x * DT;
     if (blockIdx.x == 0 && tid == 0) *out_count = tot[0];
+    // the neighbours in sorted order come from the adjacent lanes (shuffles);
+    // only a wave's edge lanes load them
     uint64_t em[DI];
     CKey<WORDS> v[DI];
+    uint8_t tb[DI];                               // output tomb; bit 1: the tag run continues (rare walk)
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
         const size_t e = base + (size_t)r * DB + tid;
-        bool f = false;
-        if (e < n) {
-            v[r] = ck_load<WORDS>(c, n, e);
-            f = dd_emit<MODE, WORDS>(c, n, e, v[r], p);
+        if (e < n) v[r] = ck_load<WORDS>(c, n, e);
+        else
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) v[r].w[q] = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < DI; ++r) {
+        const size_t e = base + (size_t)r * DB + tid;
+        CKey<WORDS> nx, pv;
+#pragma unroll
+        for (int q = 0; q < WORDS; ++q) {
+            nx.w[q] = (uint64_t)__shfl_down((unsigned long long)v[r].w[q], 1, 64);
+            pv.w[q] = (uint64_t)__shfl_up((unsigned long long)v[r].w[q], 1, 64);
+        }
+        const bool valid = e < n, has_next = e + 1 < n, has_prev = e > 0;
+        if (lane == 63 && has_next) nx = ck_load<WORDS>(c, n, e + 1);
+        if (lane == 0 && has_prev && valid) pv = ck_load<WORDS>(c, n, e - 1);
+        const bool same_prev = has_prev && eq_from(pv, v[r], p.b0);     // previous copy of the same tag
+        const bool same_next = has_next && eq_from(nx, v[r], p.b0);
+        bool f;
+        if constexpr (MODE == DD_LWW) {
+            f = valid && (!has_next || !eq_from(v[r], nx, p.b0 + p.br + p.bt));
+            tb[r] = (uint8_t)((v[r].w[0] & 1u) | (same_prev ? 2u : 0u));
+        } else {
+            f = valid && !same_prev;
+            tb[r] = (uint8_t)((v[r].w[0] & 1u) | (same_next ? 2u : 0u));
         }
         em[r] = __ballot(f);
         if (lane == 0) s_c[r * (DB / 64) + w] = (uint32_t)__popcll(em[r]);
@@ -596,17 +630,18 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         if (!((em[r] >> lane) & 1)) continue;
         const size_t e = base + (size_t)r * DB + tid;
         const size_t o = t0 + s_c[r * (DB / 64) + w] + (uint32_t)__popcll(em[r] & ((1ULL << lane) - 1ULL));
-        uint8_t tomb;
-        if constexpr (MODE == DD_LWW) {           // tomb of the first copy of this tag
-            size_t j = e;
-            while (j > 0 && eq_from(ck_load<WORDS>(c, n, j - 1), v[r], p.b0)) --j;
-            tomb = (uint8_t)(ck_load<WORDS>(c, n, j).w[0] & 1u);
-        } else {                                  // OR over the tag's copies
-            tomb = (uint8_t)(v[r].w[0] & 1u);
-            for (size_t j = e + 1; j < n; ++j) {
-                const CKey<WORDS> x = ck_load<WORDS>(c, n, j);
-                if (!eq_from(x, v[r], p.b0)) break;
-                tomb |= (uint8_t)(x.w[0] & 1u);
+        uint8_t tomb = tb[r] & 1u;
+        if (tb[r] & 2u) {
+            if constexpr (MODE == DD_LWW) {       // tomb of the first copy of this tag
+                size_t j = e - 1;
+                while (j > 0 && eq_from(ck_load<WORDS>(c, n, j - 1), v[r], p.b0)) --j;
+                tomb = (uint8_t)(ck_load<WORDS>(c, n, j).w[0] & 1u);
+            } else {                              // OR over the tag's copies
+                for (size_t j = e + 1; j < n; ++j) {
+                    const CKey<WORDS> x = ck_load<WORDS>(c, n, j);
+                    if (!eq_from(x, v[r], p.b0)) break;
+                    tomb |= (uint8_t)(x.w[0] & 1u);
+                }
             }
         }
         out.key[o] = p.kmin + get_bits(v[r], sk, p.bk);
