@@ -10,6 +10,7 @@ int g_vclock_pairs_per_wave = 4;
 int g_sets_stamps = 0;
 int g_sets_grid_per_cu = 0;
 int g_sets_diag = 0;
+int g_sets_knobs = 1;
 int g_rm_diag = 0;
 int g_scan_items = 8;
 
@@ -186,6 +187,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.grid_per_cu")) { // 0 = occupancy query (co-residency required)
         if (v < 0 || v > 16) return CRDT_E_INVAL;
         g_sets_grid_per_cu = (int)v;
+    } else if (!strcmp(name, "sets.knobs")) {        // bit 0: control-wave priority; bit 1: spinning data barrier
+        if (v < 0 || v > 3) return CRDT_E_INVAL;
+        g_sets_knobs = (int)v;
     } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic, WRONG output: 1 no look-back, 2 loader only
         if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_sets_diag = (int)v;

@@ -39,6 +39,7 @@ extern JoinTuning g_join;
 extern int g_vclock_pairs_per_wave;
 extern int g_sets_grid_per_cu; // persistent set-merge workgroups per CU (0 = occupancy query)
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
+extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at s_setprio 2, bit 1 spinning data barrier
 extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
 extern int g_sets_stamps;   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
 

@@ -178,11 +178,15 @@ __device__ __forceinline__ void lds_wait(const uint32_t *tag, uint32_t v) {
 
 // Barrier among the ND data waves only (the loader and look-back waves run
 // on): an LDS arrival counter; gen advances by ND per use.
-__device__ __forceinline__ void data_barrier(uint32_t *cnt, uint32_t &gen) {
+__device__ __forceinline__ void data_barrier(uint32_t *cnt, uint32_t &gen, int spin = 0) {
     gen += ND;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // this wave's LDS accesses are done
     if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+    if (spin) {
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) {}
+    } else {
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+    }
     asm volatile("" ::: "memory");
 }
 
@@ -234,7 +238,7 @@ template <int MODE>
 __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
     crdt_tuples A, crdt_tuples B, size_t na, size_t nb, const uint64_t *__restrict__ split, uint64_t *status,
     uint32_t *tile_ctr, uint32_t *err, uint32_t ntiles, crdt_tuples out, uint64_t *__restrict__ out_count,
-    uint64_t *stamps, int diag) {
+    uint64_t *stamps, int diag, int knobs) {
     __shared__ TileBuf buf[2];
     __shared__ uint16_t smi[TILE];
     __shared__ uint32_t s_wsum[ND];
@@ -272,6 +276,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
     if (tid == 0) s_dbar = 0;
     __syncthreads();                          // the only workgroup-wide barrier
 
+    if (role >= ND && (knobs & 1)) __builtin_amdgcn_s_setprio(2);   // control waves issue first
     if (role == ND) {
         // ============================================================ loader wave
         for (uint32_t k = 0;; ++k) {
@@ -421,7 +426,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
         if (diag == 2) {
             // timing diagnostic only (the loader pipeline's ceiling): the data
             // waves release each tile unmerged and write nothing
-            data_barrier(&s_dbar, dgen);
+            data_barrier(&s_dbar, dgen, knobs & 2);
             if (tid == 0) {
                 st_status(status + cur, cur == 0 ? kFlagInc : kFlagAgg);
                 s_tot[k & 3] = 0;
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
             s_wl_t[w] = it[SET_ITEMS - 1].t;
             s_wl_r[w] = it[SET_ITEMS - 1].r;
         }
-        data_barrier(&s_dbar, dgen);                                       // smi, wave edges
+        data_barrier(&s_dbar, dgen, knobs & 2);                                       // smi, wave edges
         STAMP(cur, 1);
 
         // ---- merged neighbours of this lane's run (lane +-1 by shuffles),
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
             woff = x - (uint32_t)__popc(emask);
             if (lane == 63) s_wsum[w] = x;
         }
-        data_barrier(&s_dbar, dgen);                                       // wave sums
+        data_barrier(&s_dbar, dgen, knobs & 2);                                       // wave sums
         STAMP(cur, 2);
         uint32_t total = 0, local_off = woff;
 #pragma unroll
@@ -632,7 +637,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
 #undef LTAG_A
 #undef LTAG_B
 #undef LTOMB
-        data_barrier(&s_dbar, dgen);                                       // inputs dead
+        data_barrier(&s_dbar, dgen, knobs & 2);                                       // inputs dead
 
         // ---- stage t_k's output in this buffer at its local offsets
         {
@@ -648,7 +653,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
                 }
             }
         }
-        data_barrier(&s_dbar, dgen);                                       // staged
+        data_barrier(&s_dbar, dgen, knobs & 2);                                       // staged
         STAMP(cur, 4);
         // ---- hold it in registers in copy-out order (written out next iteration)
 #pragma unroll
@@ -667,7 +672,7 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
         }
         held2 = held1;
         held1 = total;
-        data_barrier(&s_dbar, dgen);                                       // staged copy read
+        data_barrier(&s_dbar, dgen, knobs & 2);                                       // staged copy read
         if (tid == 0) lds_publish(&s_free_tag[bi], k + 1);                 // the loader may refill it
         STAMP(cur, 5);
     }
@@ -766,7 +771,7 @@ static int set_merge_impl(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const 
     g_last_grid = grid;
     g_last_occ = occ;
     k_set_merge<MODE><<<(unsigned)grid, SET_BLOCK, 0, s>>>(A, B, na, nb, split, status, ctr, err, (uint32_t)ntiles,
-                                                           O, out_count, stamps, g_sets_diag);
+                                                           O, out_count, stamps, g_sets_diag, g_sets_knobs);
     return check_launch(ctx);
 }
 
