@@ -497,7 +497,7 @@ class GossipRound(Workload):
                 "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
         self.pop = gossip.Population(eng, host, 62)
         self.host = h
-        self.init = (self.pop.off, self.pop.ts, self.pop.origin, self.pop.kv_off, self.pop.kv_key, self.pop.kv_val)
+        self.init = self.pop.snapshot()
         self.rng = np.random.default_rng(seed)
         self.gossip, self.P, self.n_l = gossip, replicas, n_l
         self.peers = gossip.random_peers(self.rng, replicas, 0, replicas)
@@ -519,9 +519,8 @@ class GossipRound(Workload):
         return n_r * 24 * 2 + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
 
     def step(self):
-        p = self.pop
-        p.off, p.ts, p.origin, p.kv_off, p.kv_key, p.kv_val = self.init
-        return p.round(self.peers)
+        self.pop.restore(self.init)           # every step is the same round from the same Diffs
+        return self.pop.round(self.peers)
 
     def cpu_baseline(self, seconds, threads):
         """The round's merge on the host: oc_refmerge (C restatement of

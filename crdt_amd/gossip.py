@@ -56,11 +56,29 @@ class Population:
         self.ts = t(host["l_ts"], np.int64)
         self.origin = t(host["l_origin"], np.uint8)
         self.kv_off = t(host["l_kv"], np.int64)
-        self.kv_key = t(np.asarray(host["kv_key"]).view(np.uint32).view(np.int32), np.int32)
-        self.kv_val = t(np.asarray(host["kv_val"]).view(np.uint32).view(np.int32), np.int32)
+        kk = np.asarray(host["kv_key"]).view(np.uint32).view(np.int32)
+        kvv = np.asarray(host["kv_val"]).view(np.uint32).view(np.int32)
+        # the kv pairs live at the front of an arena with room for a round's pulled pairs
+        cap = 2 * max(len(kk), 1)
+        ak = torch.empty(cap, dtype=torch.int32, device=dev)
+        av = torch.empty(cap, dtype=torch.int32, device=dev)
+        ak[: len(kk)].copy_(t(kk, np.int32))
+        av[: len(kvv)].copy_(t(kvv, np.int32))
+        self.kv_key, self.kv_val = ak[: len(kk)], av[: len(kvv)]
         self.str_bytes = t(host["str_bytes"], np.uint8)
         self.str_off = t(host["str_off"], np.int64)
         self.state = None
+        # kv arena of the next round: the current Diff's kv pairs are its
+        # prefix (written there by the last round's gather), spare capacity
+        # behind them takes the pulled pairs -- no copy of the Diff's pairs
+        self._arena = (ak, av)
+
+    def snapshot(self) -> tuple:
+        """The population's Diffs (device views; a round never writes them)."""
+        return (self.off, self.ts, self.origin, self.kv_off, self.kv_key, self.kv_val, self._arena)
+
+    def restore(self, snap: tuple) -> None:
+        (self.off, self.ts, self.origin, self.kv_off, self.kv_key, self.kv_val, self._arena) = snap
 
     # ---------------------------------------------------------------- helpers
     def _call(self, fn, *args):
@@ -154,10 +172,15 @@ class Population:
         r_kv = torch.empty(n_r + 1, dtype=torch.int64, device=dev)
         r_ts = torch.empty(n_r, dtype=torch.int64, device=dev)
         r_kv[n_r:].copy_(r_kb[-1:])
-        arena_k = torch.empty(max(n_lkv + n_rkv, 1), dtype=torch.int32, device=dev)
-        arena_v = torch.empty_like(arena_k)
-        arena_k[:n_lkv].copy_(self.kv_key)
-        arena_v[:n_lkv].copy_(self.kv_val)
+        ar = self._arena
+        if (ar is not None and ar[0].numel() >= n_lkv + n_rkv and n_lkv > 0
+                and ar[0].data_ptr() == self.kv_key.data_ptr() and ar[1].data_ptr() == self.kv_val.data_ptr()):
+            arena_k, arena_v = ar                             # the Diff's pairs are already its prefix
+        else:
+            arena_k = torch.empty(max(n_lkv + n_rkv, 1), dtype=torch.int32, device=dev)
+            arena_v = torch.empty_like(arena_k)
+            arena_k[:n_lkv].copy_(self.kv_key)
+            arena_v[:n_lkv].copy_(self.kv_val)
         if n_r:
             bo = b["kv_off"] if n_b else self.kv_off
             bt = b["ts"] if n_b else self.ts
@@ -177,14 +200,18 @@ class Population:
         n_out = int(out["off"][-1].item())
         src = out["src"][:n_out].contiguous()
         # offsets and kv gather in one pass; the arena size bounds the new Diff's kv count
-        # (fresh buffers every round: the views below own no one else's data)
+        # into fresh buffers with room behind the pairs for the next round's pulled pairs
+        # (a pull round moves about one population's worth of pairs; short capacity
+        # falls back to a copy into a new arena)
         new_kv = torch.empty(n_out + 1, dtype=torch.int64, device=dev)
-        nk = torch.empty_like(arena_k)
-        nv = torch.empty_like(arena_k)
+        cap = 2 * max(n_lkv + n_rkv, 1)
+        nk = torch.empty(cap, dtype=torch.int32, device=dev)
+        nv = torch.empty(cap, dtype=torch.int32, device=dev)
         self._call("crdt_seg_gather2", n_out, _p(src), _p(self.kv_off), _p(r_kv), 0, _p(new_kv), 4, _p(arena_k),
                    _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
         n_kv = int(new_kv[-1].item())
         self.kv_key, self.kv_val = nk[:n_kv], nv[:n_kv]
+        self._arena = (nk, nv)
         self.kv_off = new_kv
         self.off = out["off"]
         self.ts = out["ts"][:n_out]
