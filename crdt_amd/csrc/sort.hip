@@ -281,29 +281,51 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
     cnt[(size_t)tid * ntiles + blockIdx.x] = v;
 }
 
-// loc[d * ntiles + t] = tile t's start within digit d's bucket; tot[d] = bucket size
-__global__ __launch_bounds__(256) void k_sort_colscan(const uint32_t *__restrict__ cnt, uint32_t ntiles,
+// loc[d * ntiles + t] = tile t's start within digit d's bucket; tot[d] = bucket size.
+// One 1024-thread workgroup per column: 8192 tile counts per block-scan round
+// (one round up to 33M composites; a 256-thread, 2048-per-round form spent
+// most of its 9.6 us in three serial rounds of barriers).
+constexpr int CSB = 1024;
+__global__ __launch_bounds__(CSB) void k_sort_colscan(const uint32_t *__restrict__ cnt, uint32_t ntiles,
                                                       uint32_t *__restrict__ loc, uint32_t *__restrict__ tot) {
     constexpr int K = 8;
+    constexpr int NW = CSB / 64;
+    __shared__ uint32_t s_w[NW];
     const uint32_t *c = cnt + (size_t)blockIdx.x * ntiles;
     uint32_t *o = loc + (size_t)blockIdx.x * ntiles;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < ntiles; t0 += 256 * K) {
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += CSB * K) {
         const uint32_t i0 = t0 + threadIdx.x * K;
-        uint32_t v[K], s = 0;
+        uint32_t v[K], sum = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             v[k] = i0 + k < ntiles ? c[i0 + k] : 0u;
-            s += v[k];
+            sum += v[k];
         }
-        uint64_t all;
-        uint32_t run = carry + (uint32_t)block_exclusive_scan_u64(s, &all);
+        uint32_t x = sum;                       // wave inclusive scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t off = 0, all = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const uint32_t ws = s_w[k];
+            off += k < w ? ws : 0u;
+            all += ws;
+        }
+        __syncthreads();                        // s_w is rewritten next round
+        uint32_t run = carry + off + x - sum;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             if (i0 + k < ntiles) o[i0 + k] = run;
             run += v[k];
         }
-        carry += (uint32_t)all;
+        carry += all;
     }
     if (threadIdx.x == 0) tot[blockIdx.x] = carry;
 }
@@ -456,7 +478,7 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
             k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a);
         else
             k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr);
-        k_sort_colscan<<<256, 256, 0, st>>>(cnt, ntiles, loc, tot);
+        k_sort_colscan<<<256, CSB, 0, st>>>(cnt, ntiles, loc, tot);
         launch_pass<WORDS>(false, decode && q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
         std::swap(a, b);
     }
@@ -657,7 +679,7 @@ static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPla
     const hipStream_t st = ctx->stream;
     const unsigned nt = (unsigned)((n + DT - 1) / DT);
     k_dd_count<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, cnt);
-    k_sort_colscan<<<1, 256, 0, st>>>(cnt, nt, loc, tot);
+    k_sort_colscan<<<1, CSB, 0, st>>>(cnt, nt, loc, tot);
     k_dd_apply<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, loc, tot, out, out_count);
     return check_launch(ctx);
 }
