@@ -67,10 +67,10 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 //   k_rm_plan_small / scan + k_rm_geo : tiles per replica, tile geometry;
 //   k_rm_split : one wave per tile, 64-ary merge-path splits -> descriptors;
 //   k_rm_count : merge (256 threads x MI items): inserted-R count per tile
-//                and every entry's rank in the merge order (l_dk / r_dk);
+//                and every entry's rank among the tile's emitted entries;
 //   scan of the counts -> each tile's output offset, out.off;
-//   k_rm_write : re-merge, write the tile's new-Diff slice through LDS
-//                (coalesced);
+//   k_rm_write : the tile's new-Diff slice staged in LDS by rank, written
+//                coalesced;
 //   k_rm_fold  : the replay (main.go:75-98) of the tile's emitted
 //                remote-origin entries into an LDS table keyed by slot,
 //                flushed with one set of global atomics per (tile, slot);
@@ -118,26 +118,6 @@ struct alignas(16) OkVal {                // Go Atoi of one arena string: one 16
     int64_t val;                          // 0 where !ok
     int64_t ok;
 };
-
-// LDS copy of n bytes from global src: aligned dword loads for the interior,
-// byte loads for the ragged ends (never reads outside [src, src + n)).
-__device__ __forceinline__ void stage_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, int tid, int nthreads) {
-    const uintptr_t a = (uintptr_t)src;
-    uint32_t head = (uint32_t)((4 - (a & 3)) & 3);
-    if (head > n) head = n;
-    const uint32_t words = (n - head) / 4;
-    const uint32_t tail0 = head + words * 4;
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(src + head);
-    for (uint32_t k = tid; k < words; k += nthreads) {
-        const uint32_t x = w[k];
-        dst[head + 4 * k] = (uint8_t)x;
-        dst[head + 4 * k + 1] = (uint8_t)(x >> 8);
-        dst[head + 4 * k + 2] = (uint8_t)(x >> 16);
-        dst[head + 4 * k + 3] = (uint8_t)(x >> 24);
-    }
-    if ((uint32_t)tid < head) dst[tid] = src[tid];
-    if ((uint32_t)tid < n - tail0) dst[tail0 + tid] = src[tail0 + tid];
-}
 
 struct SlotAcc {                          // global replay accumulators, by slot
     unsigned long long *best;             // 0 = slot untouched
@@ -306,14 +286,17 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
     }
 }
 
-// Pass 1: inserted-R count of each tile, and every entry's rank in its
-// tile's merge order (local diagonal + 1; 0 = an R entry that is not
-// inserted) for the replay fold.  Grid = the tile-count upper bound.
+// Pass 1: inserted-R count of each tile, and every entry's rank among the
+// tile's emitted entries (1-based; 0 = an R entry that is not inserted).
+// The rank is the entry's offset in the tile's new-Diff slice (the write
+// pass scatters by it without re-merging) and, offset by the tile's first
+// diagonal, orders the replica's new Diff like its ts for the replay fold.
+// Grid = the tile-count upper bound.
 __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint16_t *__restrict__ l_dk,
                                                  uint16_t *__restrict__ r_dk) {
     __shared__ int64_t sm[MT + 1];
-    __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> local diagonal + 1
+    __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> emitted rank + 1
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
     const TileDesc d = desc[t], dn = desc[t + 1];
@@ -332,21 +315,22 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
     uint32_t isl, emit;
     const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
+    // one block scan of (emitted, inserted R) packed in 16-bit halves (<= MT each)
+    uint32_t total;
+    uint32_t pos = block_excl_sum((uint32_t)__popc(emit) | (uint32_t)__popc(emit & ~isl) << 16, s_w, &total) & 0xFFFFu;
     {
         uint32_t ia = ia0, ib = k0 - ia0;
         for (uint32_t i = 0; i < k1 - k0; ++i) {
-            const uint16_t dk = (emit >> i & 1u) ? (uint16_t)(k0 + i + 1) : (uint16_t)0;
+            const uint16_t dk = (emit >> i & 1u) ? (uint16_t)(++pos) : (uint16_t)0;
             if (isl >> i & 1u) s_dk[ia++] = dk;
             else s_dk[na + ib++] = dk;
         }
     }
-    uint32_t total;
-    block_excl_sum((uint32_t)__popc(emit & ~isl), s_w, &total);   // (its barrier also publishes s_dk)
-    if (threadIdx.x == 0) tcnt[t] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) tcnt[t] = total >> 16;
     if (l_dk)
         for (uint32_t k = threadIdx.x; k < na; k += MB) l_dk[d.l0 + k] = s_dk[k];
-    if (r_dk)
-        for (uint32_t k = threadIdx.x; k < nb; k += MB) r_dk[d.r0 + k] = s_dk[na + k];
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) r_dk[d.r0 + k] = s_dk[na + k];
 }
 
 // Replay fold (main.go:75-98) of one tile's emitted remote-origin entries
@@ -358,19 +342,33 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
 // batch issued before the first atomic; an entry's kv end is the next
 // lane's kv start (a shuffle).  Further kvs of an entry (rare: the
 // reference's load generator writes one kv per entry) take a tail loop.
+// WRITE: the same pass also writes the tile's new-Diff slice (k_rm_write's
+// work: the entries it already reads are staged in LDS by their rank).
+template <bool WRITE>
 __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                 const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
-                                                const OkVal *__restrict__ okv, SlotAcc acc, int diag) {
+                                                const OkVal *__restrict__ okv, SlotAcc acc, int diag,
+                                                const uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ ic,
+                                                crdt_refmerge_out out) {
     __shared__ uint32_t t_slot[TT];
     __shared__ unsigned long long t_best[TT];
     __shared__ unsigned long long t_sum[TT];
     __shared__ uint32_t t_npar[TT];
+    __shared__ int64_t s_ts[WRITE ? MT : 1];
+    __shared__ uint16_t s_idx[WRITE ? MT : 1];
+    __shared__ uint8_t s_org[WRITE ? MT : 1];
     const uint64_t t = blockIdx.x;
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
     tile_counts(d, dn, &na, &nb);
     const uint32_t n = na + nb;
     if (n == 0) return;
+    uint32_t total = 0;
+    uint64_t ob = 0;
+    if (WRITE) {
+        total = na + tcnt[t];
+        ob = d.l0 + ic[t];
+    }
     const int lane = threadIdx.x & 63;
     for (int h = threadIdx.x; h < TT; h += FB) {
         t_slot[h] = kEmpty;
@@ -390,7 +388,16 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         const uint64_t kb = in_tile ? kv[0] : 0;
         const uint64_t nxt = __shfl_down(kb, 1);
         uint32_t dk = in_tile ? (r ? r_dk[gi] : l_dk[gi]) : 0u;
-        if (in_tile && !r && in.l_origin[gi]) dk = 0;    // *Command: skipped by the replay (main.go:80)
+        const uint8_t org = (in_tile && !r) ? in.l_origin[gi] : 0;
+        if (WRITE && dk) {
+            const uint32_t p = dk - 1u;
+            if (p < MT) {
+                s_ts[p] = r ? in.r_ts[gi] : in.l_ts[gi];
+                s_idx[p] = (uint16_t)(r ? 0x8000u | (e - na) : e);
+                s_org[p] = org;
+            }
+        }
+        if (org) dk = 0;                                 // *Command: skipped by the replay (main.go:80)
         uint64_t ke = nxt;
         if (in_tile && (lane == 63 || e + 1 == na || e + 1 >= n)) ke = kv[1];
         ke = ke < in.n_kv ? ke : in.n_kv;                 // malformed ranges stay in bounds
@@ -409,7 +416,15 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         e_o[f] = OkVal{0, 0};
         if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
     }
-    __syncthreads();                                     // table initialised
+    __syncthreads();                                     // table initialised (and the slice staged)
+    if (WRITE)
+        for (uint32_t k = threadIdx.x; k < total; k += FB) {
+            const uint32_t id = s_idx[k], li = id & 0x7FFFu;
+            const bool r = id >> 15;
+            out.ts[ob + k] = s_ts[k];
+            out.src[ob + k] = r ? -(int64_t)(d.r0 + li) - 1 : (int64_t)(d.l0 + li);
+            out.origin[ob + k] = s_org[k];
+        }
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
         if (!e_cnt[f]) continue;
@@ -437,70 +452,48 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     }
 }
 
-// Pass 2: re-merge, stage the tile's new-Diff slice in LDS (over the merge
-// input once it is dead) and write it coalesced.  ic = exclusive scan of
-// tcnt: inserted R entries before tile t (all replicas), so the slice starts
-// at l_off[p] + a0 + ic[t] = l0 + ic[t].
+// Pass 2: the tile's new-Diff slice.  Every L entry is emitted and the
+// count pass ranked each emitted entry within the tile, so the slice is
+// staged in LDS by rank (no re-merge) and written coalesced.  ic = exclusive
+// scan of tcnt: inserted R entries before tile t (all replicas), so the
+// slice starts at l_off[p] + a0 + ic[t] = l0 + ic[t].
 __global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
-                                                 const uint64_t *__restrict__ ic, crdt_refmerge_out out) {
-    __shared__ alignas(16) int64_t s_buf[MT + 1];
-    __shared__ uint8_t so[MT];                           // origins of the tile's L entries
+                                                 const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
+                                                 const uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ ic,
+                                                 crdt_refmerge_out out) {
+    __shared__ int64_t s_ts[MT];
     __shared__ uint16_t s_idx[MT];                       // output slot -> entry (bit 15: R)
-    __shared__ uint32_t s_w[MB / 64];
+    __shared__ uint8_t s_org[MT];
     const uint64_t t = blockIdx.x;
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
     tile_counts(d, dn, &na, &nb);
-    const uint32_t n = na + nb;
-    if (n == 0) return;
-    const uint64_t ict = ic[t];
-    int64_t *sm = s_buf;
-    for (uint32_t k = threadIdx.x; k < na; k += MB) sm[1 + k] = in.l_ts[d.l0 + k];
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[d.r0 + k];
-    stage_bytes(so, in.l_origin + d.l0, na, threadIdx.x, MB);
-    if (threadIdx.x == 0) sm[0] = d.lprev;
-    __syncthreads();
-    const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
-    const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
-    uint32_t isl, emit;
-    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
-    int64_t vts[MI];
-    uint32_t vid[MI];
-    {
-        uint32_t ia = ia0, ib = k0 - ia0;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-            vts[i] = 0;
-            vid[i] = 0;
-            if ((uint32_t)i < k1 - k0) {
-                if (isl >> i & 1u) {
-                    vts[i] = sm[1 + ia];
-                    vid[i] = ia++;
-                } else {
-                    vts[i] = sm[1 + na + ib];
-                    vid[i] = 0x8000u | ib++;
-                }
-            }
+    if (na + nb == 0) return;
+    const uint32_t total = na + tcnt[t];
+    const uint64_t ob = d.l0 + ic[t];
+    for (uint32_t k = threadIdx.x; k < na; k += MB) {
+        const uint32_t p = (uint32_t)l_dk[d.l0 + k] - 1u;   // >= 0: every L entry is emitted
+        if (p < MT) {
+            s_ts[p] = in.l_ts[d.l0 + k];
+            s_idx[p] = (uint16_t)k;
+            s_org[p] = in.l_origin[d.l0 + k];
         }
     }
-    uint32_t total;
-    uint32_t pos = block_excl_sum((uint32_t)__popc(emit), s_w, &total);   // (its barrier also retires sm)
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-        if ((uint32_t)i < k1 - k0 && (emit >> i & 1u)) {
-            s_buf[pos] = vts[i];
-            s_idx[pos] = (uint16_t)vid[i];
-            ++pos;
+    for (uint32_t k = threadIdx.x; k < nb; k += MB) {
+        const uint32_t p = (uint32_t)r_dk[d.r0 + k] - 1u;
+        if (p < MT) {
+            s_ts[p] = in.r_ts[d.r0 + k];
+            s_idx[p] = (uint16_t)(0x8000u | k);
+            s_org[p] = 0;
         }
     }
     __syncthreads();
-    const uint64_t ob = d.l0 + ict;
     for (uint32_t k = threadIdx.x; k < total; k += MB) {
         const uint32_t id = s_idx[k], li = id & 0x7FFFu;
         const bool r = id >> 15;
-        out.ts[ob + k] = s_buf[k];
+        out.ts[ob + k] = s_ts[k];
         out.src[ob + k] = r ? -(int64_t)(d.r0 + li) - 1 : (int64_t)(d.l0 + li);
-        out.origin[ob + k] = r ? 0 : so[li];
+        out.origin[ob + k] = s_org[k];
     }
 }
 
@@ -735,7 +728,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
-    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, ns && !delta ? l_dk : nullptr, ns ? r_dk : nullptr);
+    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk);
     rc = check_launch(ctx);
     if (rc) return rc;
     if (tmax <= kSmallPlan) {
@@ -745,14 +738,20 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
-    k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, desc, ic, out);
+    const bool fused = ns && !delta && g_rm_diag == 0;            // the replay fold also writes the slice
+    if (!fused) k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, desc, l_dk, r_dk, tcnt, ic, out);
     if (delta) {                                                  // incremental replay: fold only the inserted R
         rc = check_launch(ctx);
         if (rc) return rc;
         return ns ? rp_delta_fold(ctx, in, r_dk, okv, *delta, &out) : CRDT_OK;
     }
     if (ns && g_rm_diag != 1)                                     // (diag 1: timing without the replay fold)
-        k_rm_fold<<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag);
+    {
+        if (fused)
+            k_rm_fold<true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out);
+        else
+            k_rm_fold<false><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag, tcnt, ic, out);
+    }
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
     return check_launch(ctx);
 }
