@@ -132,14 +132,16 @@ __global__ void k_rm_ntiles(crdt_refmerge_in in, uint32_t *__restrict__ nt) {
     }
 }
 
-// per-tile geometry (tbase = exclusive scan of the tile counts)
+// per-tile geometry (tbase = exclusive scan of the tile counts): one wave
+// per replica, its lanes write the replica's tiles.
 // maxl_ovr (nullable): per-replica max(L) to insert below, instead of the
 // local L's last key (the ts-range-sharded merge passes the global max).
-__global__ void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, const int64_t *__restrict__ maxl_ovr,
-                         TileGeo *__restrict__ geo) {
-    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
+__global__ __launch_bounds__(256) void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase,
+                                                const int64_t *__restrict__ maxl_ovr, TileGeo *__restrict__ geo) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < in.replicas; p += (uint64_t)gridDim.x * 4) {
         TileGeo g;
-        g.p = p;
+        g.p = (uint32_t)p;
         g.lb = in.l_off[p];
         g.nl = in.l_off[p + 1] - g.lb;
         g.rb = in.r_off[p];
@@ -148,7 +150,7 @@ __global__ void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase
         g.maxl = maxl_ovr ? maxl_ovr[p] : g.nl ? in.l_ts[g.lb + g.nl - 1] : INT64_MIN;
         const uint64_t t0 = tbase[p], t1 = tbase[p + 1];
         g.first = (uint32_t)t0;
-        for (uint64_t t = t0; t < t1; ++t) {
+        for (uint64_t t = t0 + lane; t < t1; t += 64) {
             g.d0 = (t - t0) * MT;
             g.d1 = g.d0 + MT < g.nl + g.nr ? g.d0 + MT : g.nl + g.nr;
             geo[t] = g;
@@ -530,6 +532,22 @@ __device__ __forceinline__ void small_scan(Get get, uint32_t n, uint64_t *__rest
     const uint32_t per = (n + SB - 1) / SB;
     const uint32_t b = threadIdx.x * per < n ? threadIdx.x * per : n;
     const uint32_t e = b + per < n ? b + per : n;
+    if (per <= 16) {                                     // n <= 16k: one read, the chunk stays in registers
+        uint64_t v[16], sum = 0, tot;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            v[k] = b + k < e ? get(b + k) : 0;
+            sum += v[k];
+        }
+        uint64_t x = block_excl_u64(sum, s_w, &tot);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (b + k < e) out[b + k] = x;
+            x += v[k];
+        }
+        if (threadIdx.x == 0) out[n] = tot;
+        return;
+    }
     // 8 loads in flight per thread per batch; the second pass re-reads (L2-hot)
     uint64_t sum = 0;
     for (uint32_t c = b; c < e; c += 8) {
@@ -725,7 +743,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         rc = exclusive_scan_u32(ctx, nt, tbase, np, tmp);         // tbase[np] = tile count
         if (rc) return rc;
     }
-    k_rm_geo<<<grid_for(np, 256, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
+    k_rm_geo<<<grid_for((np + 3) / 4, 1, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
     k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk);
