@@ -204,6 +204,26 @@ __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t 
     if (lane == 0) desc[t] = d;
 }
 
+// Stage the tile's merge items in LDS: every thread issues its MI loads
+// before the first store (a load / store per item in turn left the pass
+// waiting on MI serial HBM round trips).
+__device__ __forceinline__ void load_tile_ts(const crdt_refmerge_in &in, const TileDesc &d, uint32_t na, uint32_t n,
+                                             int64_t *sm) {
+    int64_t v[MI];
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+        const uint32_t k = threadIdx.x + (uint32_t)j * MB;
+        v[j] = k < na ? in.l_ts[d.l0 + k] : k < n ? in.r_ts[d.r0 + (k - na)] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+        const uint32_t k = threadIdx.x + (uint32_t)j * MB;
+        if (k < n) sm[1 + k] = v[j];
+    }
+    if (threadIdx.x == 0) sm[0] = d.lprev;
+    __syncthreads();
+}
+
 // sm[0] = L[a0-1] (when a0 > 0), sm[1..na] = L[a0..a1), sm[na+1..] = R[b0..b1).
 // Thread-level merge of diagonals [k0, k1) of the tile: bit i of *isl / *emit
 // = item i is an L entry / is emitted.  Returns the split (ia) at k0.
@@ -309,10 +329,7 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
         if (threadIdx.x == 0) tcnt[t] = 0;              // the scan runs over the whole grid
         return;
     }
-    for (uint32_t k = threadIdx.x; k < na; k += MB) sm[1 + k] = in.l_ts[d.l0 + k];
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) sm[1 + na + k] = in.r_ts[d.r0 + k];
-    if (threadIdx.x == 0) sm[0] = d.lprev;
-    __syncthreads();
+    load_tile_ts(in, d, na, n, sm);
     const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
     uint32_t isl, emit;
@@ -391,10 +408,11 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         const uint64_t nxt = __shfl_down(kb, 1);
         uint32_t dk = in_tile ? (r ? r_dk[gi] : l_dk[gi]) : 0u;
         const uint8_t org = (in_tile && !r) ? in.l_origin[gi] : 0;
+        const int64_t ts = (WRITE && in_tile) ? (r ? in.r_ts[gi] : in.l_ts[gi]) : 0;   // issued beside dk
         if (WRITE && dk) {
             const uint32_t p = dk - 1u;
             if (p < MT) {
-                s_ts[p] = r ? in.r_ts[gi] : in.l_ts[gi];
+                s_ts[p] = ts;
                 s_idx[p] = (uint16_t)(r ? 0x8000u | (e - na) : e);
                 s_org[p] = org;
             }
@@ -471,22 +489,27 @@ __global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, const Tile
     uint32_t na, nb;
     tile_counts(d, dn, &na, &nb);
     if (na + nb == 0) return;
-    const uint32_t total = na + tcnt[t];
+    const uint32_t n = na + nb, total = na + tcnt[t];
     const uint64_t ob = d.l0 + ic[t];
-    for (uint32_t k = threadIdx.x; k < na; k += MB) {
-        const uint32_t p = (uint32_t)l_dk[d.l0 + k] - 1u;   // >= 0: every L entry is emitted
-        if (p < MT) {
-            s_ts[p] = in.l_ts[d.l0 + k];
-            s_idx[p] = (uint16_t)k;
-            s_org[p] = in.l_origin[d.l0 + k];
-        }
+    uint32_t dk[MI];
+    int64_t ts[MI];
+    uint8_t org[MI];
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {                       // every load issued before the first LDS store
+        const uint32_t k = threadIdx.x + (uint32_t)j * MB;
+        const bool r = k >= na;
+        const uint64_t gi = r ? d.r0 + (k - na) : d.l0 + k;
+        dk[j] = k < n ? (r ? r_dk[gi] : l_dk[gi]) : 0u;   // every L entry is emitted (dk >= 1)
+        ts[j] = k < n ? (r ? in.r_ts[gi] : in.l_ts[gi]) : 0;
+        org[j] = k < na ? in.l_origin[gi] : 0;
     }
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) {
-        const uint32_t p = (uint32_t)r_dk[d.r0 + k] - 1u;
-        if (p < MT) {
-            s_ts[p] = in.r_ts[d.r0 + k];
-            s_idx[p] = (uint16_t)(0x8000u | k);
-            s_org[p] = 0;
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+        const uint32_t k = threadIdx.x + (uint32_t)j * MB, p = dk[j] - 1u;
+        if (dk[j] && p < MT) {
+            s_ts[p] = ts[j];
+            s_idx[p] = (uint16_t)(k < na ? k : 0x8000u | (k - na));
+            s_org[p] = org[j];
         }
     }
     __syncthreads();
