@@ -88,6 +88,7 @@ constexpr int MI = MT / MB;               // items per thread
 constexpr int TT = 512;                   // LDS replay-table entries per tile
 constexpr int FB = 512;                   // threads of the replay-fold kernel (one tile each)
 constexpr int FI = MT / FB;               // entries per fold thread
+constexpr uint32_t OKC = 256;             // string tables up to this size are staged in the fold's LDS
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct TileGeo {                          // 64 B per tile (per-replica geometry)
@@ -376,6 +377,8 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     __shared__ int64_t s_ts[WRITE ? MT : 1];
     __shared__ uint16_t s_idx[WRITE ? MT : 1];
     __shared__ uint8_t s_org[WRITE ? MT : 1];
+    __shared__ int64_t s_okval[OKC];
+    __shared__ uint8_t s_okok[OKC];
     const uint64_t t = blockIdx.x;
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
@@ -395,33 +398,52 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         t_sum[h] = 0;
         t_npar[h] = 0;
     }
-    uint64_t e_kb[FI];
+    // a small string table (the reference's load generator writes ten
+    // values, main.go:282) is staged in LDS: the Atoi lookup leaves the
+    // chain of dependent global loads (kv range -> kv pair -> Atoi record)
+    const bool okc = in.n_str <= OKC;
+    if (okc && threadIdx.x < in.n_str) {
+        const OkVal o = okv[threadIdx.x];
+        s_okval[threadIdx.x] = o.val;
+        s_okok[threadIdx.x] = (uint8_t)(o.ok != 0);
+    }
+    uint64_t e_kb[FI], e_k1[FI];
     uint32_t e_dk[FI], e_cnt[FI], e_slot[FI], e_v[FI];
+    uint8_t e_org[FI];
+    int64_t e_ts[FI];
 #pragma unroll
-    for (int f = 0; f < FI; ++f) {
+    for (int f = 0; f < FI; ++f) {                       // every entry load issued before the first use
         const uint32_t e = threadIdx.x + (uint32_t)f * FB;
         const bool r = e >= na;
         const uint64_t gi = r ? d.r0 + (e - na) : d.l0 + e;
         const uint64_t *kv = (r ? in.r_kv : in.l_kv) + gi;
         const bool in_tile = e < n;
-        const uint64_t kb = in_tile ? kv[0] : 0;
+        const bool edge = lane == 63 || e + 1 == na || e + 1 >= n;   // kv end not in the next lane
+        e_kb[f] = in_tile ? kv[0] : 0;
+        e_k1[f] = (in_tile && edge) ? kv[1] : 0;
+        e_dk[f] = in_tile ? (r ? r_dk[gi] : l_dk[gi]) : 0u;
+        e_org[f] = (in_tile && !r) ? in.l_origin[gi] : 0;
+        e_ts[f] = (WRITE && in_tile) ? (r ? in.r_ts[gi] : in.l_ts[gi]) : 0;
+    }
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        const uint32_t e = threadIdx.x + (uint32_t)f * FB;
+        const bool r = e >= na;
+        const bool edge = lane == 63 || e + 1 == na || e + 1 >= n;
+        const uint64_t kb = e_kb[f];
         const uint64_t nxt = __shfl_down(kb, 1);
-        uint32_t dk = in_tile ? (r ? r_dk[gi] : l_dk[gi]) : 0u;
-        const uint8_t org = (in_tile && !r) ? in.l_origin[gi] : 0;
-        const int64_t ts = (WRITE && in_tile) ? (r ? in.r_ts[gi] : in.l_ts[gi]) : 0;   // issued beside dk
+        uint32_t dk = e_dk[f];
         if (WRITE && dk) {
             const uint32_t p = dk - 1u;
             if (p < MT) {
-                s_ts[p] = ts;
+                s_ts[p] = e_ts[f];
                 s_idx[p] = (uint16_t)(r ? 0x8000u | (e - na) : e);
-                s_org[p] = org;
+                s_org[p] = e_org[f];
             }
         }
-        if (org) dk = 0;                                 // *Command: skipped by the replay (main.go:80)
-        uint64_t ke = nxt;
-        if (in_tile && (lane == 63 || e + 1 == na || e + 1 >= n)) ke = kv[1];
+        if (e_org[f]) dk = 0;                            // *Command: skipped by the replay (main.go:80)
+        uint64_t ke = edge ? e_k1[f] : nxt;
         ke = ke < in.n_kv ? ke : in.n_kv;                 // malformed ranges stay in bounds
-        e_kb[f] = kb;
         e_dk[f] = dk;
         e_cnt[f] = (dk && kb < ke) ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
     }
@@ -431,12 +453,19 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
     }
     OkVal e_o[FI];
+    if (!okc)
 #pragma unroll
-    for (int f = 0; f < FI; ++f) {
-        e_o[f] = OkVal{0, 0};
-        if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
-    }
+        for (int f = 0; f < FI; ++f) {
+            e_o[f] = OkVal{0, 0};
+            if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
+        }
     __syncthreads();                                     // table initialised (and the slice staged)
+    if (okc)
+#pragma unroll
+        for (int f = 0; f < FI; ++f) {
+            e_o[f] = OkVal{0, 0};
+            if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = OkVal{s_okval[e_v[f]], s_okok[e_v[f]]};
+        }
     if (WRITE)
         for (uint32_t k = threadIdx.x; k < total; k += FB) {
             const uint32_t id = s_idx[k], li = id & 0x7FFFu;

@@ -65,10 +65,31 @@ def test_large_batch_matches_oracle(eng):
         assert s_gpu == s_or
 
 
-def test_packed_batch_matches_oracle(eng):
-    """The bench's packed config-A-at-scale batch: every replica checked."""
+def _big_string_table(h, n_str, seed):
+    """Re-point every kv value at one of n_str strings (numbers, Atoi edge
+    cases and words): the fold stages tables of <= 256 strings in LDS, larger
+    ones take the global Atoi lookup."""
+    rng = np.random.default_rng(seed)
+    base = ["-9223372036854775808", "9223372036854775807", "9223372036854775808", "+7", "007", "-0", "x1", ""]
+    strs = base + [str(int(v)) if i % 5 else f"w{i}" for i, v in
+                   enumerate(rng.integers(-2**62, 2**62, size=n_str - len(base)))]
+    blob = "".join(strs).encode()
+    so = np.zeros(len(strs) + 1, np.int64)
+    so[1:] = np.cumsum([len(x.encode()) for x in strs])
+    h = dict(h)
+    h["kv_val"] = rng.integers(0, n_str, size=len(h["kv_val"])).astype(np.uint32).view(np.int32)
+    h["str_bytes"], h["str_off"] = np.frombuffer(blob, np.uint8).copy(), so
+    return h
+
+
+@pytest.mark.parametrize("n_str", [0, 256, 257, 5000])
+def test_packed_batch_matches_oracle(eng, n_str):
+    """The bench's packed config-A-at-scale batch: every replica checked
+    (n_str 0: the generator's own ten values plus odd strings)."""
     from refmerge_util import oracle_packed_replica
     h = synth.refmerge_packed(11, 48, 5000)
+    if n_str:
+        h = _big_string_table(h, n_str, n_str)
     out = eng.refmerge_batch(refmerge.to_device(h, eng.device))
     off = out["off"].cpu().numpy()
     ts, org, src = (out[k].cpu().numpy() for k in ("ts", "origin", "src"))
