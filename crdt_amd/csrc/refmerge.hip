@@ -364,13 +364,18 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
 // reference's load generator writes one kv per entry) take a tail loop.
 // WRITE: the same pass also writes the tile's new-Diff slice (k_rm_write's
 // work: the entries it already reads are staged in LDS by their rank).
-template <bool WRITE>
+// DELTA (with WRITE): the incremental replay's first phase instead -- only
+// the inserted R entries are folded, keyed by ts ^ 2^63, into the carried
+// state st (max, holder count, wrapped sum, parsable count).
+template <bool WRITE, bool DELTA = false>
 __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                 const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
                                                 const OkVal *__restrict__ okv, SlotAcc acc, int diag,
                                                 const uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ ic,
-                                                crdt_refmerge_out out) {
+                                                crdt_refmerge_out out, crdt_replay_state st) {
+    static_assert(WRITE || !DELTA, "the delta fold runs inside the write pass");
     __shared__ uint32_t t_slot[TT];
+    __shared__ uint32_t t_nh[DELTA ? TT : 1];
     __shared__ unsigned long long t_best[TT];
     __shared__ unsigned long long t_sum[TT];
     __shared__ uint32_t t_npar[TT];
@@ -397,6 +402,7 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         t_best[h] = 0;
         t_sum[h] = 0;
         t_npar[h] = 0;
+        if (DELTA) t_nh[h] = 0;
     }
     // a small string table (the reference's load generator writes ten
     // values, main.go:282) is staged in LDS: the Atoi lookup leaves the
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
                 s_org[p] = e_org[f];
             }
         }
-        if (e_org[f]) dk = 0;                            // *Command: skipped by the replay (main.go:80)
+        if (e_org[f] || (DELTA && !r)) dk = 0;           // *Command: skipped by the replay (main.go:80)
         uint64_t ke = edge ? e_k1[f] : nxt;
         ke = ke < in.n_kv ? ke : in.n_kv;                 // malformed ranges stay in bounds
         e_dk[f] = dk;
@@ -477,15 +483,36 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
         if (!e_cnt[f]) continue;
-        const uint64_t rank = d.d0 + e_dk[f];
-        if (e_slot[f] < in.n_slots && e_v[f] < in.n_str)
-            fold_pair(t_slot, t_best, t_sum, t_npar, acc, true, e_slot[f], e_v[f], rank, e_o[f].ok != 0,
-                      e_o[f].val);
-        for (uint64_t q = e_kb[f] + 1; q < e_kb[f] + e_cnt[f]; ++q) {
-            const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
+        const uint64_t rank = DELTA ? (uint64_t)e_ts[f] ^ 0x8000000000000000ull : d.d0 + e_dk[f];
+        for (uint32_t j = 0; j < e_cnt[f]; ++j) {
+            uint32_t slot = e_slot[f], v = e_v[f];
+            OkVal o = e_o[f];
+            if (j) {                                     // further kvs of the entry (rare)
+                slot = in.kv_key[e_kb[f] + j];
+                v = in.kv_val[e_kb[f] + j];
+                if (slot < in.n_slots && v < in.n_str) o = okv[v];
+            }
             if (slot >= in.n_slots || v >= in.n_str) continue;
-            const OkVal o = okv[v];
-            fold_pair(t_slot, t_best, t_sum, t_npar, acc, true, slot, v, rank, o.ok != 0, o.val);
+            if (!DELTA) {
+                fold_pair(t_slot, t_best, t_sum, t_npar, acc, true, slot, v, rank, o.ok != 0, o.val);
+                continue;
+            }
+            const uint32_t idx = table_find(t_slot, slot);
+            if (idx != kEmpty) {
+                atomicMax(&t_best[idx], (unsigned long long)rank);
+                atomicAdd(&t_nh[idx], 1u);
+                if (o.ok) {
+                    atomicAdd(&t_sum[idx], (unsigned long long)o.val);   // mod 2^64 (main.go:95)
+                    atomicAdd(&t_npar[idx], 1u);
+                }
+            } else {                                     // table full: straight to the state
+                atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), (unsigned long long)rank);
+                atomicAdd(&st.nhold[slot], 1u);
+                if (o.ok) {
+                    atomicAdd(reinterpret_cast<unsigned long long *>(&st.sum[slot]), (unsigned long long)o.val);
+                    atomicAdd(&st.npar[slot], 1u);
+                }
+            }
         }
     }
     __syncthreads();
@@ -493,6 +520,15 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     for (int h = threadIdx.x; h < TT; h += FB) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;
+        if (DELTA) {
+            atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), t_best[h]);
+            atomicAdd(&st.nhold[slot], t_nh[h]);
+            if (t_npar[h]) {
+                atomicAdd(reinterpret_cast<unsigned long long *>(&st.sum[slot]), t_sum[h]);
+                atomicAdd(&st.npar[slot], t_npar[h]);
+            }
+            continue;
+        }
         atomicMax(&acc.best[slot], t_best[h]);
         if (t_npar[h]) {
             atomicAdd(&acc.sum[slot], t_sum[h]);
@@ -713,7 +749,7 @@ extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
 
 namespace crdt {
 static int rp_delta_fold(crdt_ctx *ctx, const crdt_refmerge_in &in, const uint16_t *r_dk, const OkVal *okv,
-                         const crdt_replay_state &st, const crdt_refmerge_out *out);
+                         const crdt_replay_state &st, const crdt_refmerge_out *out, bool phase1_done);
 }
 
 extern "C" int crdt_refmerge_batch_ex(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
@@ -808,19 +844,23 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
-    const bool fused = ns && !delta && g_rm_diag == 0;            // the replay fold also writes the slice
+    const bool fused = ns && g_rm_diag == 0;                      // the replay fold also writes the slice
     if (!fused) k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, desc, l_dk, r_dk, tcnt, ic, out);
     if (delta) {                                                  // incremental replay: fold only the inserted R
+        if (fused)                                                // (its first phase, with the slice write)
+            k_rm_fold<true, true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out,
+                                                                 *delta);
         rc = check_launch(ctx);
         if (rc) return rc;
-        return ns ? rp_delta_fold(ctx, in, r_dk, okv, *delta, &out) : CRDT_OK;
+        return ns ? rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, fused) : CRDT_OK;
     }
-    if (ns && g_rm_diag != 1)                                     // (diag 1: timing without the replay fold)
-    {
+    if (ns && g_rm_diag != 1) {                                   // (diag 1: timing without the replay fold)
         if (fused)
-            k_rm_fold<true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out);
+            k_rm_fold<true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out,
+                                                           crdt_replay_state{});
         else
-            k_rm_fold<false><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag, tcnt, ic, out);
+            k_rm_fold<false><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag, tcnt, ic, out,
+                                                            crdt_replay_state{});
     }
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
     return check_launch(ctx);
@@ -940,9 +980,19 @@ __global__ __launch_bounds__(RPB) void k_rp_fold(crdt_refmerge_in in, const uint
     __shared__ unsigned long long t_max[TT];
     __shared__ unsigned long long t_sum[TT];
     __shared__ uint32_t t_npar[TT], t_nh[TT];
+    __shared__ int64_t s_okval[OKC];
+    __shared__ uint8_t s_okok[OKC];
     const uint64_t n = RSIDE ? in.n_r : in.n_l;
     const uint64_t *kvo = RSIDE ? in.r_kv : in.l_kv;
     const int64_t *tsv = RSIDE ? in.r_ts : in.l_ts;
+    const bool okc = PHASE == 1 && in.n_str <= OKC;      // small string table: Atoi records in LDS
+    if (okc)
+        for (uint32_t i = threadIdx.x; i < in.n_str; i += RPB) {
+            const OkVal o = okv[i];
+            s_okval[i] = o.val;
+            s_okok[i] = (uint8_t)(o.ok != 0);
+        }
+    // (the first round's table-init barrier publishes the staged records)
     for (uint64_t base = (uint64_t)blockIdx.x * RPB * RPE; base < n; base += (uint64_t)gridDim.x * RPB * RPE) {
         if (PHASE == 1) {
             for (int h = threadIdx.x; h < TT; h += RPB) {
@@ -980,7 +1030,8 @@ __global__ __launch_bounds__(RPB) void k_rp_fold(crdt_refmerge_in in, const uint
 #pragma unroll
         for (int f = 0; f < RPE; ++f) {
             e_o[f] = OkVal{0, 0};
-            if (PHASE == 1 && e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
+            if (PHASE == 1 && e_slot[f] < in.n_slots && e_v[f] < in.n_str)
+                e_o[f] = okc ? OkVal{s_okval[e_v[f]], s_okok[e_v[f]]} : okv[e_v[f]];
         }
 #pragma unroll
         for (int f = 0; f < RPE; ++f) {
@@ -1061,11 +1112,11 @@ __global__ void k_rp_final(crdt_refmerge_out out, crdt_replay_state st, const Ok
 }
 
 static int rp_delta_fold(crdt_ctx *ctx, const crdt_refmerge_in &in, const uint16_t *r_dk, const OkVal *okv,
-                         const crdt_replay_state &st, const crdt_refmerge_out *out) {
+                         const crdt_replay_state &st, const crdt_refmerge_out *out, bool phase1_done) {
     const hipStream_t s = ctx->stream;
     const unsigned g = grid_for((in.n_r + RPE - 1) / RPE, RPB, (unsigned)ctx->num_cus * 8);
     if (in.n_r) {
-        k_rp_fold<true, 1><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
+        if (!phase1_done) k_rp_fold<true, 1><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
         k_rp_fold<true, 2><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
     }
     k_rp_final<<<grid_for(in.n_slots, 256, (unsigned)ctx->num_cus * 8), 256, 0, s>>>(*out, st, okv, in.n_slots);
