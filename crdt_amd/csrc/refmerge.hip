@@ -162,21 +162,30 @@ __global__ __launch_bounds__(256) void k_rm_geo(crdt_refmerge_in in, const uint6
 // Merge-path split of diagonal d (first d items of the merge): the number of
 // L items among them.  Whole wave, 64-ary: pred(a) = L[a] <= R[d-1-a] holds
 // for a < split and fails from it on.
+// *lprev = L[split - 1] when split > 0: a raise of lo always comes from a
+// lane that probed L[new lo - 1], so it is shuffled out of the search and
+// only a split that never moved off its lower bound loads it.
 __device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, const int64_t *R, uint64_t nr,
-                                               uint64_t d, int lane) {
+                                               uint64_t d, int lane, int64_t *lprev) {
     uint64_t lo = d > nr ? d - nr : 0, hi = d < nl ? d : nl;
+    const uint64_t lo0 = lo;
+    int64_t lp = 0;
     while (lo < hi) {
         const uint64_t step = (hi - lo + 63) / 64;
         const uint64_t a = lo + (uint64_t)lane * step;
         const bool valid = a < hi;
-        const bool pred = valid && L[a] <= R[d - 1 - a];
+        const int64_t lv = valid ? L[a] : 0;
+        const bool pred = valid && lv <= R[d - 1 - a];
         const int c = __popcll(__ballot(pred));         // monotone: lanes 0..c-1
         const int nv = __popcll(__ballot(valid));
+        const int64_t lc = __shfl(lv, c ? c - 1 : 0);
+        if (c) lp = lc;                                  // L[nlo - 1]
         const uint64_t nlo = c ? lo + (uint64_t)(c - 1) * step + 1 : lo;
         const uint64_t nhi = c < nv ? lo + (uint64_t)c * step : hi;
         lo = nlo;
         hi = nhi;
     }
+    *lprev = lo > lo0 ? lp : lo > 0 ? L[lo - 1] : 0;
     return lo;
 }
 
@@ -192,7 +201,8 @@ __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t 
     TileDesc d = {};
     if (t < tbase[replicas]) {
         const TileGeo g = geo[t];
-        const uint64_t a0 = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d0, lane);
+        int64_t lprev;
+        const uint64_t a0 = wave_split(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d0, lane, &lprev);
         d.l0 = g.lb + a0;
         d.r0 = g.rb + (g.d0 - a0);
         d.d0 = g.d0;
@@ -200,7 +210,7 @@ __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t 
         d.lend = g.lb + g.nl;
         d.n = (uint32_t)(g.d1 - g.d0);
         d.has_prev = a0 > 0;
-        d.lprev = a0 > 0 ? in.l_ts[g.lb + a0 - 1] : 0;
+        d.lprev = lprev;
     }
     if (lane == 0) desc[t] = d;
 }
