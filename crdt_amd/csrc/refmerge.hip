@@ -120,6 +120,11 @@ struct alignas(16) OkVal {                // Go Atoi of one arena string: one 16
     int64_t ok;
 };
 
+struct RpCand {                           // delta replay: a tile's max holder of one slot
+    uint64_t key;                         // ts ^ 2^63
+    uint32_t slot, str;
+};
+
 struct SlotAcc {                          // global replay accumulators, by slot
     unsigned long long *best;             // 0 = slot untouched
     unsigned long long *sum;
@@ -327,11 +332,12 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
 // Grid = the tile-count upper bound.
 __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint16_t *__restrict__ l_dk,
-                                                 uint16_t *__restrict__ r_dk) {
+                                                 uint16_t *__restrict__ r_dk, uint32_t *__restrict__ zero) {
     __shared__ int64_t sm[MT + 1];
     __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> emitted rank + 1
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
+    if (zero && t == 0 && threadIdx.x == 0) *zero = 0;   // (the delta fold's overflow flag)
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
     tile_counts(d, dn, &na, &nb);
@@ -382,10 +388,13 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
                                                 const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
                                                 const OkVal *__restrict__ okv, SlotAcc acc, int diag,
                                                 const uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ ic,
-                                                crdt_refmerge_out out, crdt_replay_state st) {
+                                                crdt_refmerge_out out, crdt_replay_state st,
+                                                RpCand *__restrict__ cand, uint32_t *__restrict__ cand_n,
+                                                uint32_t *__restrict__ ovf) {
     static_assert(WRITE || !DELTA, "the delta fold runs inside the write pass");
     __shared__ uint32_t t_slot[TT];
     __shared__ uint32_t t_nh[DELTA ? TT : 1];
+    __shared__ uint32_t s_nc, s_ovf;
     __shared__ unsigned long long t_best[TT];
     __shared__ unsigned long long t_sum[TT];
     __shared__ uint32_t t_npar[TT];
@@ -394,12 +403,21 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     __shared__ uint8_t s_org[WRITE ? MT : 1];
     __shared__ int64_t s_okval[OKC];
     __shared__ uint8_t s_okok[OKC];
+    // DELTA: string of the tile's max holder of each table entry, over the
+    // Atoi records (read for the last time before the fold's closing barrier;
+    // keeps four workgroups' LDS within a CU)
+    static_assert(OKC * sizeof(int64_t) >= TT * sizeof(uint32_t), "t_str alias");
+    uint32_t *t_str = reinterpret_cast<uint32_t *>(s_okval);
     const uint64_t t = blockIdx.x;
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
     tile_counts(d, dn, &na, &nb);
     const uint32_t n = na + nb;
-    if (n == 0) return;
+    if (n == 0) {
+        if (DELTA && threadIdx.x == 0) cand_n[t] = 0;
+        return;
+    }
+    if (DELTA && threadIdx.x == 0) s_nc = s_ovf = 0;
     uint32_t total = 0;
     uint64_t ob = 0;
     if (WRITE) {
@@ -516,6 +534,7 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
                     atomicAdd(&t_npar[idx], 1u);
                 }
             } else {                                     // table full: straight to the state
+                s_ovf = 1;                               // (the holder pass then walks the entries)
                 atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), (unsigned long long)rank);
                 atomicAdd(&st.nhold[slot], 1u);
                 if (o.ok) {
@@ -527,10 +546,27 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     }
     __syncthreads();
     if (diag == 2) return;
+    if (DELTA) {                                         // each slot's tile-local max holder -> t_str
+#pragma unroll
+        for (int f = 0; f < FI; ++f) {
+            if (!e_cnt[f]) continue;
+            const uint64_t key = (uint64_t)e_ts[f] ^ 0x8000000000000000ull;
+            for (uint32_t j = 0; j < e_cnt[f]; ++j) {
+                const uint32_t slot = j ? in.kv_key[e_kb[f] + j] : e_slot[f];
+                const uint32_t v = j ? in.kv_val[e_kb[f] + j] : e_v[f];
+                if (slot >= in.n_slots || v >= in.n_str) continue;
+                const uint32_t idx = table_find(t_slot, slot);   // present, or the window was full
+                if (idx != kEmpty && t_best[idx] == key) t_str[idx] = v;   // ts unique: one holder
+            }
+        }
+        __syncthreads();
+    }
     for (int h = threadIdx.x; h < TT; h += FB) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;
         if (DELTA) {
+            const uint32_t c = atomicAdd(&s_nc, 1u);
+            cand[(uint64_t)t * TT + c] = RpCand{t_best[h], slot, t_str[h]};
             atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), t_best[h]);
             atomicAdd(&st.nhold[slot], t_nh[h]);
             if (t_npar[h]) {
@@ -543,6 +579,45 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         if (t_npar[h]) {
             atomicAdd(&acc.sum[slot], t_sum[h]);
             atomicAdd(&acc.npar[slot], t_npar[h]);
+        }
+    }
+    if (DELTA) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            cand_n[t] = s_nc;
+            if (s_ovf) *ovf = 1;
+        }
+    }
+}
+
+// Delta replay, second phase: the global max holder of each slot writes its
+// string.  Every tile left one candidate (its max holder) per slot it
+// touched, so only those are checked -- unless some tile's LDS table
+// overflowed (its pairs went straight to the state without a candidate):
+// then every inserted R entry is checked.  ts are unique, so exactly one
+// holder matches the max.
+__global__ __launch_bounds__(64) void k_rp_holder(crdt_refmerge_in in, const uint16_t *__restrict__ r_dk,
+                                                  crdt_replay_state st, const RpCand *__restrict__ cand,
+                                                  const uint32_t *__restrict__ cand_n,
+                                                  const uint32_t *__restrict__ ovf, uint64_t tmax) {
+    if (*ovf) {
+        for (uint64_t e = (uint64_t)blockIdx.x * 64 + threadIdx.x; e < in.n_r; e += (uint64_t)gridDim.x * 64) {
+            if (!r_dk[e]) continue;
+            const uint64_t kb = in.r_kv[e], ke = in.r_kv[e + 1] < in.n_kv ? in.r_kv[e + 1] : in.n_kv;
+            const uint64_t key = (uint64_t)in.r_ts[e] ^ 0x8000000000000000ull;
+            for (uint64_t q = kb; q < ke; ++q) {
+                const uint32_t slot = in.kv_key[q], v = in.kv_val[q];
+                if (slot >= in.n_slots || v >= in.n_str) continue;
+                if (st.best_key[slot] == key) st.best_str[slot] = v;
+            }
+        }
+        return;
+    }
+    for (uint64_t t = blockIdx.x; t < tmax; t += gridDim.x) {
+        const uint32_t n = cand_n[t];
+        for (uint32_t h = threadIdx.x; h < n; h += 64) {
+            const RpCand c = cand[t * TT + h];
+            if (st.best_key[c.slot] == c.key) st.best_str[c.slot] = c.str;
         }
     }
 }
@@ -802,7 +877,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
                         Carve::round((tmax + 1) * sizeof(TileGeo)) * 2 + Carve::round(tmax * 8 + 8) +
                         Carve::round(tmax * 4 + 4) + Carve::round((nstr + 1) * sizeof(OkVal)) +
                         Carve::round(in.n_l * 2 + 2) + Carve::round(nr * 2 + 2) +
-                        Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) + 4096;
+                        Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) + 4096 +
+                        (delta ? Carve::round(tmax * TT * sizeof(RpCand)) + Carve::round(tmax * 4 + 4) + 256 : 0);
     rc = ws_reserve(ctx, need);
     if (rc) return rc;
     Carve w(ctx->ws);
@@ -815,6 +891,9 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     uint32_t *tcnt = w.take<uint32_t>(tmax + 1);
     uint16_t *l_dk = w.take<uint16_t>(in.n_l + 1);
     uint16_t *r_dk = w.take<uint16_t>(nr + 1);
+    RpCand *cand = delta ? w.take<RpCand>(tmax * TT) : nullptr;   // delta: per-tile max-holder candidates
+    uint32_t *cand_n = delta ? w.take<uint32_t>(tmax + 1) : nullptr;
+    uint32_t *ovf = delta ? w.take<uint32_t>(4) : nullptr;        // a tile's LDS table overflowed
     OkVal *okv = w.take<OkVal>(nstr + 1);
     SlotAcc acc;
     acc.best = w.take<unsigned long long>(ns + 1);
@@ -844,7 +923,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     k_rm_geo<<<grid_for((np + 3) / 4, 1, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
-    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk);
+    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk, ovf);
     rc = check_launch(ctx);
     if (rc) return rc;
     if (tmax <= kSmallPlan) {
@@ -859,18 +938,24 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     if (delta) {                                                  // incremental replay: fold only the inserted R
         if (fused)                                                // (its first phase, with the slice write)
             k_rm_fold<true, true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out,
-                                                                 *delta);
+                                                                 *delta, cand, cand_n, ovf);
         rc = check_launch(ctx);
         if (rc) return rc;
-        return ns ? rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, fused) : CRDT_OK;
+        if (!ns) return CRDT_OK;
+        if (fused) {                                              // second phase: the candidates' holders
+            k_rp_holder<<<(unsigned)tmax, 64, 0, s>>>(in, r_dk, *delta, cand, cand_n, ovf, tmax);
+            rc = check_launch(ctx);
+            if (rc) return rc;
+        }
+        return rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, fused);
     }
     if (ns && g_rm_diag != 1) {                                   // (diag 1: timing without the replay fold)
         if (fused)
             k_rm_fold<true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out,
-                                                           crdt_replay_state{});
+                                                           crdt_replay_state{}, nullptr, nullptr, nullptr);
         else
             k_rm_fold<false><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag, tcnt, ic, out,
-                                                            crdt_replay_state{});
+                                                            crdt_replay_state{}, nullptr, nullptr, nullptr);
     }
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
     return check_launch(ctx);
@@ -1126,8 +1211,10 @@ static int rp_delta_fold(crdt_ctx *ctx, const crdt_refmerge_in &in, const uint16
     const hipStream_t s = ctx->stream;
     const unsigned g = grid_for((in.n_r + RPE - 1) / RPE, RPB, (unsigned)ctx->num_cus * 8);
     if (in.n_r) {
-        if (!phase1_done) k_rp_fold<true, 1><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
-        k_rp_fold<true, 2><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
+        if (!phase1_done) {
+            k_rp_fold<true, 1><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
+            k_rp_fold<true, 2><<<g, RPB, 0, s>>>(in, r_dk, okv, st);
+        }
     }
     k_rp_final<<<grid_for(in.n_slots, 256, (unsigned)ctx->num_cus * 8), 256, 0, s>>>(*out, st, okv, in.n_slots);
     return check_launch(ctx);

@@ -123,3 +123,43 @@ def test_delta_on_kats(eng):
     full = eng.refmerge_batch(d)
     st = eng.replay_state_init(d)
     _same_merge(full, eng.refmerge_delta(d, st))
+
+
+def test_delta_table_overflow(eng):
+    """Replicas with thousands of distinct keys overflow the delta fold's
+    512-entry per-tile LDS table (pairs go straight to the carried state and
+    the holder pass walks every inserted entry); mixed with a small replica."""
+    from crdt_amd.server import Command
+    rng = np.random.default_rng(6)
+    pk = refmerge.Packer()
+    for nkeys in (2500, 40, 3000):
+        diff, remote, ts = {}, {}, 0
+        for _ in range(4000):
+            ts += int(rng.integers(1, 4))
+            m = {}
+            for _ in range(int(rng.integers(1, 4))):
+                v = int(rng.integers(-50, 50))
+                m[f"key{int(rng.integers(0, nkeys))}"] = str(v) if rng.random() > 0.05 else f"x{v}"
+            if rng.random() < 0.5:
+                diff[ts] = Command(m) if rng.random() < 0.3 else m
+            else:
+                remote[ts] = m
+        pk.add_replica(diff, remote)
+    d = refmerge.to_device(pk.arrays(), eng.device)
+    full = eng.refmerge_batch(d)
+    st = eng.replay_state_init(d)
+    _same_merge(full, eng.refmerge_delta(d, st))
+
+
+def test_delta_large_batch_then_overflow(eng):
+    """A candidate-path delta merge followed by an overflow-path one on the
+    same engine: the overflow flag is reset per merge."""
+    h = synth.refmerge_packed(8, 16, 3000)
+    d = refmerge.to_device(h, eng.device)
+    st = eng.replay_state_init(d)
+    _same_merge(eng.refmerge_batch(d), eng.refmerge_delta(d, st))
+    test_delta_table_overflow(eng)
+    h = synth.refmerge_packed(9, 16, 3000)
+    d = refmerge.to_device(h, eng.device)
+    st = eng.replay_state_init(d)
+    _same_merge(eng.refmerge_batch(d), eng.refmerge_delta(d, st))
