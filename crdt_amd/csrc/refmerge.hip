@@ -89,7 +89,7 @@ constexpr int TT = 512;                   // LDS replay-table entries per tile
 constexpr int FB = 512;                   // threads of the replay-fold kernel (one tile each)
 constexpr int FI = MT / FB;               // entries per fold thread
 #ifndef RM_SPLIT_PW
-#define RM_SPLIT_PW 32                    // merge-path search width (probing lanes)
+#define RM_SPLIT_PW 16                    // merge-path search width (probing lanes)
 #endif
 constexpr uint32_t OKC = 256;             // string tables up to this size are staged in the fold's LDS
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
@@ -170,7 +170,8 @@ __global__ __launch_bounds__(256) void k_rm_geo(crdt_refmerge_in in, const uint6
 // Merge-path split of diagonal d (first d items of the merge): the number of
 // L items among them.  One wave, PW-ary (lanes 0..PW-1 probe): the pass is
 // bound by the scattered probe loads, not by the rounds -- 256-ary (4 probes
-// per lane) took 53 us against 64-ary's 23 us for 10.6k tiles.
+// per lane) took 53 us, 64-ary 23 us, 32-ary 18.6 us, 16-ary 15.2 us for
+// 10.6k tiles of 10k-entry logs.
 // pred(a) = L[a] <= R[d-1-a] holds for a < split and fails from it on.
 // *lprev = L[split - 1] when split > 0: a raise of lo always comes from a
 // probe of L[new lo - 1], so it is shuffled out of the search and only a
