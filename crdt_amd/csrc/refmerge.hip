@@ -141,12 +141,36 @@ __global__ void k_rm_ntiles(crdt_refmerge_in in, uint32_t *__restrict__ nt) {
     }
 }
 
+// Go Atoi of strings i (okv) and the reset of replay accumulator i, for
+// i = i0, i0 + stride, ...
+__device__ __forceinline__ void prep_items(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off,
+                                           uint64_t nstr, OkVal *__restrict__ okv, SlotAcc acc, uint32_t ns,
+                                           uint64_t i0, uint64_t stride) {
+    const uint64_t n = nstr > ns ? nstr : ns;
+    for (uint64_t i = i0; i < n; i += stride) {
+        if (i < nstr) {
+            int64_t v = 0;
+            const bool good = go_atoi(bytes + off[i], off[i + 1] - off[i], &v);
+            okv[i].val = good ? v : 0;
+            okv[i].ok = good;
+        }
+        if (i < ns) {
+            acc.best[i] = 0;
+            acc.sum[i] = 0;
+            acc.npar[i] = 0;
+        }
+    }
+}
+
 // per-tile geometry (tbase = exclusive scan of the tile counts): one wave
 // per replica, its lanes write the replica's tiles.
 // maxl_ovr (nullable): per-replica max(L) to insert below, instead of the
 // local L's last key (the ts-range-sharded merge passes the global max).
+// The same launch runs the Atoi / accumulator-reset prep (independent work,
+// one launch fewer in front of the tile passes).
 __global__ __launch_bounds__(256) void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase,
-                                                const int64_t *__restrict__ maxl_ovr, TileGeo *__restrict__ geo) {
+                                                const int64_t *__restrict__ maxl_ovr, TileGeo *__restrict__ geo,
+                                                OkVal *__restrict__ okv, SlotAcc acc, uint32_t ns) {
     const int lane = threadIdx.x & 63;
     for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < in.replicas; p += (uint64_t)gridDim.x * 4) {
         TileGeo g;
@@ -165,6 +189,8 @@ __global__ __launch_bounds__(256) void k_rm_geo(crdt_refmerge_in in, const uint6
             geo[t] = g;
         }
     }
+    prep_items(in.str_bytes, in.str_off, in.n_str, okv, acc, ns, (uint64_t)blockIdx.x * 256 + threadIdx.x,
+               (uint64_t)gridDim.x * 256);
 }
 
 // Merge-path split of diagonal d (first d items of the merge): the number of
@@ -790,20 +816,7 @@ __global__ __launch_bounds__(SB) void k_rm_scan_small(const uint32_t *__restrict
 // Go Atoi over the string arena and the replay accumulators' reset, one launch.
 __global__ void k_rm_prep(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off, uint64_t nstr,
                           OkVal *__restrict__ okv, SlotAcc acc, uint32_t ns) {
-    const uint64_t n = nstr > ns ? nstr : ns;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        if (i < nstr) {
-            int64_t v = 0;
-            const bool good = go_atoi(bytes + off[i], off[i + 1] - off[i], &v);
-            okv[i].val = good ? v : 0;
-            okv[i].ok = good;
-        }
-        if (i < ns) {
-            acc.best[i] = 0;
-            acc.sum[i] = 0;
-            acc.npar[i] = 0;
-        }
-    }
+    prep_items(bytes, off, nstr, okv, acc, ns, (uint64_t)blockIdx.x * 256 + threadIdx.x, (uint64_t)gridDim.x * 256);
 }
 
 // out.off[p] = l_off[p] + inserted R entries of replicas before p
@@ -929,9 +942,6 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     const hipStream_t s = ctx->stream;
     const unsigned cap = (unsigned)ctx->num_cus * 8;
     const uint32_t reps = in.replicas;
-    if (nstr || ns)
-        k_rm_prep<<<grid_for(std::max(nstr, ns), 256, cap), 256, 0, s>>>(in.str_bytes, in.str_off, nstr, okv, acc,
-                                                                          (uint32_t)ns);
     if (np <= kSmallPlan) {
         k_rm_plan_small<<<1, SB, 0, s>>>(in, tbase);
     } else {
@@ -941,7 +951,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         rc = exclusive_scan_u32(ctx, nt, tbase, np, tmp);         // tbase[np] = tile count
         if (rc) return rc;
     }
-    k_rm_geo<<<grid_for((np + 3) / 4, 1, cap), 256, 0, s>>>(in, tbase, maxl_dev, geo);
+    k_rm_geo<<<std::max(grid_for((np + 3) / 4, 1, cap), grid_for(std::max(nstr, ns), 256, cap)), 256, 0, s>>>(
+        in, tbase, maxl_dev, geo, okv, acc, (uint32_t)ns);
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
     k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk, ovf);
