@@ -84,9 +84,29 @@ __global__ void k_seg_copy_block(uint64_t n, const int64_t *__restrict__ code, c
         const T *s1 = fb ? p.b1 : p.a1;
         const T dl = p.delta ? p.delta[s] : (T)0;
         const uint64_t o = dst_off[s] - sb;
-        for (uint64_t i = sb + part * 256 + threadIdx.x; i < se; i += (uint64_t)parts * 256) {
-            p.d0[o + i] = (T)(s0[i] + dl);
-            if constexpr (kTwo) p.d1[o + i] = s1[i];
+        T *__restrict__ d0 = p.d0;
+        T *__restrict__ d1 = p.d1;
+        const uint64_t st = (uint64_t)parts * 256;
+        uint64_t i = sb + part * 256 + threadIdx.x;
+        // U elements per thread in flight before the first store (a load /
+        // store per element in turn waited on one HBM round trip each)
+        constexpr int U = 4;
+        for (; i + (U - 1) * st < se; i += U * st) {
+            T x[U], y[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                x[k] = s0[i + k * st];
+                if constexpr (kTwo) y[k] = s1[i + k * st];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                d0[o + i + k * st] = (T)(x[k] + dl);
+                if constexpr (kTwo) d1[o + i + k * st] = y[k];
+            }
+        }
+        for (; i < se; i += st) {
+            d0[o + i] = (T)(s0[i] + dl);
+            if constexpr (kTwo) d1[o + i] = s1[i];
         }
     }
 }
