@@ -207,3 +207,15 @@ def test_many_keys_per_replica_matches_oracle(eng):
         d_or, s_or = oracle_merge(diff, remote)
         assert list(d_gpu) == list(d_or)
         assert s_gpu == s_or
+
+
+def test_slice_write_without_slots(eng):
+    """n_slots = 0 (no replay): the new Diff comes from the standalone slice
+    write (k_rm_write) instead of the fused fold pass -- same slices."""
+    h = synth.refmerge_packed(12, 40, 4000)
+    full = eng.refmerge_batch(refmerge.to_device(h, eng.device))
+    bare = eng.refmerge_batch(refmerge.to_device(dict(h, n_slots=0), eng.device))
+    n = int(full["off"][-1])
+    np.testing.assert_array_equal(bare["off"].cpu().numpy(), full["off"].cpu().numpy())
+    for k in ("ts", "origin", "src"):
+        np.testing.assert_array_equal(bare[k][:n].cpu().numpy(), full[k][:n].cpu().numpy())
