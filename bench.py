@@ -3,14 +3,18 @@
 
     python bench.py --gpus N --steps K --warmup W [--workload NAME]
 
-Default workload = BASELINE.json configs[1]: G-Counter join of 1M replicas x
-64 nodes uint64 per GPU (out = max(A, B) elementwise).  One "step" = one
-pass of the hot path over one batch; inputs are generated in HBM before the
-timed region.  N>1: one process per GPU (torchrun), each rank joins its own
-replica shard (weak scaling, no data-path collective: pairwise joins of
-independent replicas have no exchange step).  The sharded whole-population
-join with its real exchange step (fold + RCCL all-reduce(max)) is
---workload shard_fold (configs[4]).
+Default workload = BASELINE.json configs[4] (the north_star's scaling
+config): a 100M-replica x 64-node uint64 G-Counter population sharded by
+contiguous rows over the N GPUs; one step = every rank folds its shard
+(crdt_gcounter_fold) and ONE RCCL ncclAllReduce(ncclUint64, ncclMax) of the
+512-B fold joins the shards (crdt_shard_fold_max_u64, the library's own
+communicator).  At N=1 the whole 51.2-GB population is on one GPU.  Total
+work is fixed as N grows ("strong").  configs[1] (pairwise join of 1M x 64)
+is --workload gcounter_join.
+
+N>1: one process per GPU.  Under torchrun the ranks come from the env; a
+plain `python bench.py --gpus N` spawns its own N rank processes before the
+parent touches the GPU and exits with their status.
 
 Prints ONE JSON line (rank 0) with value = whole-job units/s, a roofline
 object for the dominant kernel (HIP-event-timed on the launch stream) and a
@@ -55,6 +59,49 @@ def dist_init():
         else:
             dist.init_process_group(backend)
     return world, rank, dev
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their env) and return the first
+    failing exit status (0 if all succeed).  Runs before this process makes
+    any GPU call; if a rank fails the others are stopped (a peer blocked in a
+    collective would never return)."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in procs:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def cpu_share() -> tuple[int, int]:
+    """(threads for the CPU baseline, CPUs in this process's affinity mask).
+    The box grants each GPU a CPU share that OMP_NUM_THREADS states while the
+    affinity mask may show the whole machine: use the smaller of the two."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(env) if env.isdigit() and int(env) > 0 else aff
+    return max(1, min(aff, share)), aff
 
 
 def barrier(world):
@@ -225,19 +272,42 @@ class SetMerge(Workload):
         self._fn(self.A, self.B, out=self.out, count=self.count, trim=False)
 
     def cpu_baseline(self, seconds, threads):
+        """The oracle's serial merge run on `threads` host threads, each over
+        one key range of both sorted inputs (a key's output depends only on
+        its own tuples, so key-range pieces concatenate to the whole merge --
+        the same split the multi-GPU path uses)."""
+        from concurrent.futures import ThreadPoolExecutor
         from oracle import oracle
         a = self.A.to_numpy()
         b = self.B.to_numpy()
         fn = oracle.lww_merge if self.lww else oracle.orset_merge
-        done, t0 = 0, time.perf_counter()
-        while True:
-            fn(a, b)
-            done += 2 * self.n
-            if time.perf_counter() - t0 > seconds:
-                break
-        dt = time.perf_counter() - t0
-        return {"value": done / dt, "unit": self.unit, "cores": 1, "kind": "port",
-                "sample": f"oc_{self.name} (serial merge), {self.n} tuples per side, {done // (2 * self.n)} reps"}
+        pieces = _key_range_pieces(a, b, threads)
+        with ThreadPoolExecutor(threads) as ex:
+            got = list(ex.map(lambda ab: fn(*ab), pieces))
+            n_cpu = sum(len(g[0]) for g in got)
+            assert n_cpu == self.n_out, f"cpu merge length {n_cpu} != device {self.n_out}"
+            done, t0 = 0, time.perf_counter()
+            while True:
+                list(ex.map(lambda ab: fn(*ab), pieces))
+                done += 2 * self.n
+                if time.perf_counter() - t0 > seconds:
+                    break
+            dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oc_{self.name} (C restatement) on {threads} threads, one key range of both sorted "
+                          f"sides each, {self.n} tuples per side, {done // (2 * self.n)} reps in {dt:.1f}s"}
+
+
+def _key_range_pieces(a, b, parts):
+    """Split two key-sorted SoA tuple sets into `parts` aligned key ranges."""
+    keys = np.concatenate([a[0], b[0]])
+    if len(keys) == 0:
+        return [(a, b)]
+    qs = np.unique(np.quantile(keys, np.linspace(0, 1, parts + 1)[1:-1], method="nearest").astype(np.uint64))
+    ia = [0] + list(np.searchsorted(a[0], qs)) + [len(a[0])]
+    ib = [0] + list(np.searchsorted(b[0], qs)) + [len(b[0])]
+    return [(tuple(x[ia[i]:ia[i + 1]] for x in a), tuple(x[ib[i]:ib[i + 1]] for x in b))
+            for i in range(len(ia) - 1)]
 
 
 class SetMergeUnsorted(SetMerge):
@@ -285,38 +355,58 @@ class SetMergeUnsorted(SetMerge):
             o = np.lexsort((t[3], t[2], t[1], t[0]))
             return tuple(np.ascontiguousarray(x[o]) for x in t)
 
+        from concurrent.futures import ThreadPoolExecutor
         done, t0 = 0, time.perf_counter()
-        while True:
-            fn(srt(ua), srt(ub))
-            done += 2 * m
-            if time.perf_counter() - t0 > seconds:
-                break
+        with ThreadPoolExecutor(threads) as ex:
+            while True:
+                sa, sb = ex.map(srt, (ua, ub))
+                list(ex.map(lambda ab: fn(*ab), _key_range_pieces(sa, sb, threads)))
+                done += 2 * m
+                if time.perf_counter() - t0 > seconds:
+                    break
         dt = time.perf_counter() - t0
-        return {"value": done / dt, "unit": self.unit, "cores": 1, "kind": "port",
-                "sample": f"numpy lexsort of both unsorted sides + oc_{self.name[:-3]} (serial merge), {m} tuples "
-                          f"per side (slice of the device inputs), {done // (2 * m)} reps"}
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"numpy lexsort of both unsorted sides (one thread each) + oc_{self.name[:-3]} on {threads} "
+                          f"threads over key ranges, {m} tuples per side (slice of the device inputs), "
+                          f"{done // (2 * m)} reps"}
+
+
+def native_comm(eng, world):
+    """The library's own RCCL communicator (crdt_shard_comm_init_rank), one
+    rank per process; None in the gloo rehearsal (ranks sharing one GPU,
+    which RCCL refuses): the exchange then goes through torch.distributed."""
+    if os.environ.get("CRDT_BENCH_BACKEND", "nccl") != "nccl":
+        return None
+    from crdt_amd import shard
+    return shard.Comm.init_rank(eng)
 
 
 class ShardFold(Workload):
-    """configs[4]: R replicas sharded over the ranks; fold + all-reduce(max)."""
+    """configs[4] E1: `total_rows` replicas sharded by contiguous rows over
+    the ranks; a step = each rank folds its [rows, 64] shard on its GPU, then
+    ONE ncclAllReduce(ncclUint64, ncclMax) of the 512-B folds
+    (crdt_shard_fold_max_u64).  Rows processed per step summed over ranks =
+    total_rows (strong scaling)."""
     name = "shard_fold"
     unit = "replica-merges/s"
     kernel = "k_fold_pow2"
+    scaling = "strong"
 
     def __init__(self, eng, rank, world, total_rows, nodes, seed=2024):
-        import ctypes as C
-        from crdt_amd import _lib
+        from crdt_amd import shard
         self.eng, self.world, self.nodes, self.total = eng, world, nodes, total_rows
-        b, e = C.c_uint64(), C.c_uint64()
-        _lib.call("crdt_shard_range", total_rows, world, rank, C.byref(b), C.byref(e))
-        self.rows = e.value - b.value
-        self.a = eng.synth_counters(seed, 1, self.rows, nodes, row_base=b.value)
+        b, e = shard.shard_range(total_rows, world, rank)
+        self.row0, self.rows = b, e - b
+        self.a = eng.synth_counters(seed, 1, self.rows, nodes, row_base=b)
         self.fold = torch.empty(nodes, dtype=torch.int64, device=eng.device)
-        self.ordered = torch.empty(nodes, dtype=torch.int64, device=eng.device)
-        self.config = {"workload": f"sharded fold, {total_rows} replicas x {nodes} nodes total, "
-                                   f"fold + all-reduce(max) (BASELINE configs[4])",
+        self.comm = native_comm(eng, world)
+        xchg = "RCCL ncclAllReduce(ncclUint64, ncclMax) via crdt_shard_fold_max_u64" if self.comm else \
+            "gloo all-reduce(max) rehearsal (ranks share one GPU)"
+        self.config = {"workload": f"sharded fold, {total_rows} replicas x {nodes} nodes uint64 total "
+                                   f"({total_rows * nodes * 8 / 1e9:.1f} GB), per-GPU fold + all-reduce(max) "
+                                   "(BASELINE configs[4], E1)",
                        "total_rows": total_rows, "rows_per_gpu": self.rows, "nodes": nodes,
-                       "parallelism": f"row-shard x{world} + RCCL all-reduce(max)"}
+                       "parallelism": f"row-shard x{world} + {xchg}"}
 
     def units(self):
         return self.rows
@@ -325,28 +415,57 @@ class ShardFold(Workload):
         return self.rows * self.nodes * 8
 
     def step(self):
-        from crdt_amd import shard
-        self.eng.gcounter_fold(self.a, out=self.fold)
-        if self.world > 1:
-            shard.allreduce_max_u64(self.fold, self.eng)     # RCCL all-reduce(max), 512 B
+        if self.comm is not None:
+            self.comm.fold_max([self.a], [self.fold])
+        else:
+            from crdt_amd import shard
+            self.eng.gcounter_fold(self.a, out=self.fold)
+            if self.world > 1:
+                shard.allreduce_max_u64(self.fold, self.eng)
 
     def cpu_baseline(self, seconds, threads):
-        return None
+        """oc_gcounter_fold over `threads` row ranges of a 2M-row (1 GB)
+        slice of the same device population, max-combined (the same
+        associative join), repeated for ~`seconds`."""
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle
+        rows = min(self.rows, 2_000_000)
+        a = E.as_u64(self.a[:rows]).reshape(rows, self.nodes)
+        parts = [a[i * rows // threads:(i + 1) * rows // threads] for i in range(threads)]
+
+        def fold(ex):
+            return np.maximum.reduce(list(ex.map(oracle.gcounter_fold, parts)))
+
+        with ThreadPoolExecutor(threads) as ex:
+            got = fold(ex)
+            assert np.array_equal(got, E.as_u64(self.eng.gcounter_fold(self.a[:rows]))), "fold parity"
+            done, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < seconds:
+                fold(ex)
+                done += rows
+            dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": threads, "kind": "port",
+                "sample": f"oracle/crdt_oracle.c oc_gcounter_fold (C restatement; no Go toolchain) over {threads} "
+                          f"row ranges of {rows} replicas x {self.nodes} nodes copied from the device population, "
+                          f"max-combined, {done // rows} reps in {dt:.1f}s"}
 
 
 class ShardJoin(Workload):
     """configs[4] E2: every rank holds a DIVERGENT full copy of the
-    [rows, nodes] counter state; the join is one RCCL all-reduce(MAX) over
-    xGMI (uint64 through the order-preserving map x ^ 2^63, crdt_amd.shard).
-    The bound is xGMI, reported as bus bandwidth 2(G-1)/G * S / t."""
+    [rows, nodes] counter state; the join is one in-place
+    ncclAllReduce(ncclUint64, ncclMax) over xGMI
+    (crdt_shard_allreduce_max_u64).  The bound is xGMI, reported as bus
+    bandwidth 2(G-1)/G * S / t."""
     name = "shard_join"
     unit = "replica-merges/s"
-    kernel = "RCCL all-reduce(max) + 2 order-map passes"
+    kernel = "RCCL ncclAllReduce(ncclUint64, ncclMax)"
 
     def __init__(self, eng, rank, world, rows, nodes, seed=2024):
         self.eng, self.world, self.rows, self.nodes = eng, world, rows, nodes
         self.state = eng.synth_counters(seed, 100 + rank, rows, nodes)    # divergent per rank
-        self.buf = torch.empty_like(self.state)
+        self.comm = native_comm(eng, world)
+        if self.comm is None:
+            self.buf = torch.empty_like(self.state)
         self.config = {"workload": f"divergent full-state join, {rows} replicas x {nodes} nodes uint64 "
                                    f"({rows * nodes * 8 / 1e9:.3f} GB) per rank, all-reduce(max) "
                                    "(BASELINE configs[4], E2)" + ("" if world > 1 else "; single rank: no exchange"),
@@ -356,9 +475,12 @@ class ShardJoin(Workload):
         return self.rows            # each rank's copy of every replica row merged once per step
 
     def bytes_per_launch(self):
-        return 4 * self.rows * self.nodes * 8   # the two order-map passes (read + write each)
+        return self.rows * self.nodes * 8 * 2     # each rank reads its copy and writes the joined state
 
     def step(self):
+        if self.comm is not None:
+            self.comm.allreduce_max_u64([self.state])
+            return
         self.eng.u64_to_ordered_i64(self.state, out=self.buf)
         if self.world > 1:
             import torch.distributed as dist
@@ -563,9 +685,102 @@ class GossipRound(Workload):
                           f"threads, {dt:.1f}s"}
 
 
+class ServerMerge(Workload):
+    """The path a Go caller of merge() actually hits (main.go:245-257):
+    configs[0]'s 5 replicas x 10k Diff entries (main.go:319-321), each
+    pulling a peer's Diff.  A step = for every Server, the gossip pull decode
+    of the peer's body into RemoteDiff (crdt_server_ingest_binary,
+    main.go:245-256) and then ONE crdt_servers_merge of all five: the host
+    pack of Diff + RemoteDiff, H2D, the RefMerge kernels, D2H and the
+    rebuild of Diff / CurrentState (server.hip).  Re-merging the same pull is
+    a no-op on the state (KAT-5), so every step does the same work.  Host-
+    and PCIe-bound by construction; the roofline object is not meaningful
+    here (reported against the device bytes for completeness)."""
+    name = "server_merge"
+    unit = "remote-entries/s"
+    dtype = "int64"
+    kernel = "crdt_servers_merge end to end (host pack + H2D + refmerge kernels + D2H + unpack)"
+
+    def __init__(self, eng, rank, world, replicas, entries, seed=2024):
+        from crdt_amd import refmerge, server, synth
+        self.eng, self.server = eng, server
+        demo = synth.refmerge_demo(seed + rank, replicas, entries)
+        self.demo = demo
+        self.srv = []
+        for p, (diff, _) in enumerate(demo):
+            s = server.Server(eng, 8080 + p)
+            for ts, v in diff.items():
+                s.Diff.Put(ts, v)
+            self.srv.append(s)
+        # each replica's pull: the RemoteDiff of the demo, served as a binary
+        # gossip body by a host-only peer (its Diff = those remote maps)
+        self.bodies = []
+        for p, (_, remote) in enumerate(demo):
+            peer = server.Server(None, 9000 + p)
+            for ts, v in remote.items():
+                peer.Diff.Put(ts, dict(v))
+            st, body = peer.GossipBinary()
+            assert st == 200
+            self.bodies.append(body)
+            peer.close()
+        self.n_r = sum(len(r) for _, r in demo)
+        self.step()
+        self.n_diff = sum(len(s.DiffSignature) for s in self.srv)
+        self.config = {"workload": f"Server.merge() end to end: {replicas} replicas x {entries} Diff entries, "
+                                   f"each ingests a peer's pulled Diff (binary gossip body) and all merge in one "
+                                   "crdt_servers_merge (BASELINE configs[0], main.go:245-257, :319-321)",
+                       "replicas": replicas, "entries": entries, "n_remote": self.n_r, "n_diff": self.n_diff,
+                       "parallelism": f"replicas x{world}"}
+
+    def units(self):
+        return self.n_r
+
+    def bytes_per_launch(self):
+        return self.n_diff * 17 + self.n_r * 16
+
+    def step(self):
+        for s, body in zip(self.srv, self.bodies):
+            assert s.IngestBinary(body) == 0
+        self.server.merge_servers(self.srv)
+
+    def cpu_baseline(self, seconds, threads):
+        """oc_refmerge of each replica's (Diff, pulled RemoteDiff), one replica
+        per call on min(replicas, threads) threads -- the reference merges each
+        Server under its own mutex in its own goroutine (main.go:43-44, :321).
+        Ingest is not timed on this side (the packed arrays are prepared
+        first), so the ratio favours the CPU."""
+        from concurrent.futures import ThreadPoolExecutor
+        from crdt_amd import refmerge
+        from oracle import oracle
+        jobs = []
+        for diff, remote in self.demo:
+            pk = refmerge.Packer()
+            pk.add_replica(diff, remote)
+            h = pk.arrays()
+            jobs.append((h["l_ts"], h["l_origin"], h["l_kv"].astype(np.uint32), h["r_ts"], h["r_kv"].astype(np.uint32),
+                         h["kv_key"].view(np.uint32), h["kv_val"].view(np.uint32), h["str_bytes"], h["str_off"],
+                         int(h["n_slots"]), len(h["r_ts"])))
+
+        def run(j):
+            oracle.refmerge_packed(*j[:10])
+            return j[10]
+
+        nt = min(len(jobs), threads)
+        done, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(nt) as ex:
+            while time.perf_counter() - t0 < seconds:
+                done += sum(ex.map(run, jobs))
+        dt = time.perf_counter() - t0
+        return {"value": done / dt, "unit": self.unit, "cores": nt, "kind": "port",
+                "sample": f"oc_refmerge (C restatement of main.go:35-100) of the same {len(jobs)} replicas' Diff + "
+                          f"pulled RemoteDiff, one replica per call on {nt} threads, {dt:.1f}s"}
+
+
 def make_workload(name, eng, rank, world, args):
     if name == "gossip_round":
         return GossipRound(eng, rank, world, args.replicas, args.entries)
+    if name == "server_merge":
+        return ServerMerge(eng, rank, world, args.demo_replicas, args.demo_entries)
     if name == "refmerge":
         return RefMergeBatch(eng, rank, world, args.replicas, args.entries)
     if name == "refmerge_delta":
@@ -605,9 +820,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="gcounter_join",
-                    choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge", "lww_merge_d2", "orset_merge_d2",
-                             "shard_fold", "shard_join", "refmerge", "refmerge_delta", "gossip_round"])
+    ap.add_argument("--workload", default="shard_fold",
+                    choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
+                             "lww_merge_d2", "orset_merge_d2", "shard_fold", "shard_join", "refmerge",
+                             "refmerge_delta", "gossip_round", "server_merge"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)
@@ -616,14 +832,18 @@ def main():
     ap.add_argument("--total-rows", type=int, default=100_000_000)
     ap.add_argument("--replicas", type=int, default=1000)
     ap.add_argument("--entries", type=int, default=10_000)
+    ap.add_argument("--demo-replicas", type=int, default=5)      # main.go:319-321
+    ap.add_argument("--demo-entries", type=int, default=10_000)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--option", action="append", default=[], help="name=value kernel knob (crdt_set_option)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))          # before any GPU call in this process
     world, rank, local = dist_init()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a mismatched n_gpus")
     for o in args.option:
         k, v = o.split("=")
         from crdt_amd import _lib
@@ -651,6 +871,12 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
 
+    # kernels cannot return errors: a raised device flag (e.g. a set merge's
+    # bounded look-back timing out) means the timed outputs are invalid
+    flags = eng.device_status(clear=True)
+    if flags:
+        raise SystemExit(f"rank {rank}: device-side failure flags 0x{flags:x} during the timed loop: "
+                         "outputs invalid, no line reported")
     step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
     gpu_s = sum(step_ms) / 1e3
     elapsed = max_over_ranks(wall, world, dev)
@@ -670,16 +896,19 @@ def main():
                 "timing": "HIP events on the launch stream, per step"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and hasattr(wl, "cpu_baseline"):
-            threads = min(16, os.cpu_count() or 1)
+            threads, aff = cpu_share()
             cpu = wl.cpu_baseline(args.cpu_seconds, threads)
             if cpu is not None:
                 cpu["value"] = round(cpu["value"], 1)
                 cpu["host_cpu"] = _cpu_model()
                 cpu["nproc"] = os.cpu_count()
+                cpu["affinity_cpus"] = aff
+                cpu["cpu_share"] = ("threads = min(affinity mask, OMP_NUM_THREADS = "
+                                    f"{os.environ.get('OMP_NUM_THREADS', 'unset')}): the GPU's host CPU share")
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": wl.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-            "higher_is_better": True, "scaling": "weak" if wl.name != "shard_fold" else "strong",
+            "higher_is_better": True, "scaling": getattr(wl, "scaling", "weak"),
             "vs_baseline": None, "dtype": wl.dtype,
             "data": "synthetic (SplitMix64-seeded, generated in HBM)",
             "config": wl.config, "roofline": roof, "cpu_baseline": cpu,

@@ -29,6 +29,8 @@ STATUS_NAMES = {
     -4: "CRDT_E_NODEV",
     -5: "CRDT_E_UNSORTED",
     -6: "CRDT_E_RANGE",
+    -7: "CRDT_E_COMM",
+    -8: "CRDT_E_DEVICE",
 }
 
 
@@ -171,6 +173,23 @@ SIGNATURES = {
     "crdt_shard_range": (_I, [_U64, _I, _I, C.POINTER(_U64), C.POINTER(_U64)]),
     "crdt_u64_to_ordered_i64": (_I, [_CTX, _P, _P, _SZ]),
     "crdt_ordered_i64_to_u64": (_I, [_CTX, _P, _P, _SZ]),
+    "crdt_shard_unique_id": (_I, [_P, _SZ]),
+    "crdt_shard_comm_create": (_I, [C.POINTER(_I), _I, C.POINTER(_P)]),
+    "crdt_shard_comm_init_rank": (_I, [_CTX, _P, _I, _I, C.POINTER(_P)]),
+    "crdt_shard_comm_destroy": (_I, [_P]),
+    "crdt_shard_comm_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
+    "crdt_shard_member_ctx": (_I, [_P, _I, C.POINTER(_P)]),
+    "crdt_shard_comm_last_error": (_I, [_P]),
+    "crdt_shard_sync": (_I, [_P]),
+    "crdt_shard_fold_max_u64": (_I, [_P, C.POINTER(_P), C.POINTER(_SZ), _SZ, C.POINTER(_P)]),
+    "crdt_shard_allreduce_max_u64": (_I, [_P, C.POINTER(_P), _SZ]),
+    "crdt_shard_allreduce": (_I, [_P, C.POINTER(_P), _SZ, _I, _I]),
+    "crdt_shard_set_allgather_v": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ,
+                                        C.POINTER(_SZ)]),
+    "crdt_shard_lww_merge": (_I, [_P, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                                  C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ)]),
+    "crdt_shard_orset_merge": (_I, [_P, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                                    C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ)]),
     "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
     "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),
     "crdt_synth_set_tuples": (_I, [_CTX, _U64, C.c_uint32, C.POINTER(crdt_tuples), _SZ, _U64]),

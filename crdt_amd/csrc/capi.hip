@@ -2,6 +2,8 @@
 // entry points of the C-ABI (include/crdt_amd.h).
 #include <string.h>
 
+#include <atomic>
+
 #include "common.hpp"
 
 namespace crdt {
@@ -13,6 +15,7 @@ int g_sets_diag = 0;
 int g_sets_knobs = 1;
 int g_rm_diag = 0;
 int g_scan_items = 8;
+std::atomic<int> g_fail_refmerge{0};
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -50,6 +53,8 @@ extern "C" const char *crdt_status_str(int s) {
         case CRDT_E_NODEV: return "no gfx950 device";
         case CRDT_E_UNSORTED: return "input not sorted";
         case CRDT_E_RANGE: return "size exceeds kernel index range";
+        case CRDT_E_COMM: return "RCCL error";
+        case CRDT_E_DEVICE: return "device-side failure flag raised (output invalid)";
         default: return "unknown status";
     }
 }
@@ -132,13 +137,26 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
 }
 
 extern "C" int crdt_ctx_set_stream(crdt_ctx *ctx, void *stream) {
-    if (!ctx) return CRDT_E_INVAL;
+    int rc = bind(ctx);
+    if (rc) return rc;
+    hipStream_t ns = (hipStream_t)stream;
+    if (ns == ctx->stream) return CRDT_OK;
+    // The workspace, staging buffer and status word are shared by every call
+    // of the context: work still queued on the old stream must finish before
+    // the new stream reuses (or ws_reserve frees) them.  The new stream waits
+    // on an event recorded behind the old stream's work (no host sync).
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ns, ev, 0);
+    if (ev) (void)hipEventDestroy(ev);
+    if (e != hipSuccess) return hip_fail(ctx, e);
     if (ctx->own_stream) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipStreamDestroy(ctx->stream);
         ctx->own_stream = false;
     }
-    ctx->stream = (hipStream_t)stream;
+    ctx->stream = ns;
     return CRDT_OK;
 }
 
@@ -199,6 +217,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "scan.items")) {        // items per lane of the single-pass scan
         if (v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
         g_scan_items = (int)v;
+    } else if (!strcmp(name, "fail.refmerge")) {     // fault injection: the next v RefMerge calls fail (CRDT_E_NOMEM)
+        if (v < 0 || v > 1000) return CRDT_E_INVAL;
+        g_fail_refmerge = (int)v;
     } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sets_stamps = (int)v;

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -41,7 +43,8 @@ extern int g_sets_grid_per_cu; // persistent set-merge workgroups per CU (0 = oc
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
 extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at s_setprio 2, bit 1 spinning data barrier
 extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
-extern int g_sets_stamps;   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
+extern int g_sets_stamps;
+extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

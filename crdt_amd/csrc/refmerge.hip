@@ -887,6 +887,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
+    for (int f = g_fail_refmerge.load(); f > 0;)                  // injected failure (error-path tests)
+        if (g_fail_refmerge.compare_exchange_weak(f, f - 1)) return CRDT_E_NOMEM;
     if (delta && inp->n_slots && (!delta->best_key || !delta->best_str || !delta->sum || !delta->npar ||
                                   !delta->nhold))
         return CRDT_E_INVAL;
@@ -905,6 +907,12 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     if (in.n_kv && !in.n_str) return CRDT_E_INVAL;
 
     const size_t nr = in.n_r, ns = in.n_slots, nstr = in.n_str, np = in.replicas;
+    // The replay keys a holder as best = rank << 32 | string id, rank = its
+    // 1-based position in the replica's merge sequence (<= |L_p| + |R_p|), and
+    // the ts-range-sharded form re-packs it as shard << 40 | rank: every
+    // replica's sequence must stay below 2^32 entries and string ids must fit
+    // 32 bits.  n_l + n_r bounds every replica's sequence.
+    if (in.n_l + nr >= 0xffffffffULL || nstr > 0xffffffffULL) return CRDT_E_RANGE;
     const size_t tmax = (in.n_l + nr) / MT + np + 1;             // >= tiles over all replicas
     if (tmax > 0x7fffffffULL) return CRDT_E_RANGE;
     const size_t need = Carve::round(np * 4 + 4) + Carve::round((np + 1) * 8) + scan_tmp_bytes(std::max(np, tmax)) +
@@ -1039,7 +1047,8 @@ static int acc_xform(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n, int 
 
 extern "C" int crdt_refmerge_acc_rank(crdt_ctx *ctx, const crdt_refmerge_acc *acc, size_t n_slots, uint32_t shard,
                                       int64_t *c_dev) {
-    if (!c_dev || shard >= (1u << 23)) return CRDT_E_INVAL;
+    if (!c_dev) return CRDT_E_INVAL;
+    if (shard >= (1u << 23)) return CRDT_E_RANGE;      // shard << 40 | rank must stay a positive int64
     return acc_xform(ctx, acc, n_slots, 0, shard, c_dev, nullptr, nullptr);
 }
 

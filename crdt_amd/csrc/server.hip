@@ -31,6 +31,7 @@ namespace crdt {
 
 struct Value {                       // map[string]string or *Command
     bool local = false;              // true: *Command (main.go:187), skipped by the replay
+    bool nil = false;                // a nil map: pulled as JSON null (main.go:246), re-served as null
     std::vector<std::pair<std::string, std::string>> kv;   // unique keys
 };
 
@@ -518,6 +519,10 @@ static void json_put_string(std::string &o, const std::string &s) {
 }
 
 static void json_put_value(std::string &o, const Value &v) {
+    if (v.nil) {                     // json.Marshal of a nil map[string]string (main.go:159)
+        o += "null";
+        return;
+    }
     std::vector<const std::pair<std::string, std::string> *> kv;
     kv.reserve(v.kv.size());
     for (auto &e : v.kv) kv.push_back(&e);
@@ -772,17 +777,18 @@ extern "C" int crdt_server_ingest_json(crdt_server *srv, const char *data, size_
         if (in.p != in.e) ok = false;                        // trailing data is a syntax error
     }
     if (!ok) { *outcome = 1; return CRDT_OK; }
-    std::vector<std::pair<long long, const std::vector<std::pair<std::string, std::string>> *>> puts;
+    std::vector<std::pair<long long, const std::pair<std::vector<std::pair<std::string, std::string>>, bool> *>> puts;
     for (auto &t : top) {
         long long ts;
         if (!go_atoi64(t.first, &ts)) { *outcome = 2; return CRDT_OK; }
-        puts.emplace_back(ts, &t.second.first);
+        puts.emplace_back(ts, &t.second);
     }
     std::lock_guard<std::mutex> g(srv->s.Lock);
     for (auto &pv : puts) {
         auto v = std::make_shared<Value>();
         v->local = false;
-        v->kv = *pv.second;
+        v->kv = pv.second->first;
+        v->nil = pv.second->second;
         srv->s.RemoteDiff[(int64_t)pv.first] = std::move(v);
     }
     *outcome = 0;
@@ -838,13 +844,14 @@ extern "C" int crdt_server_entry_at(crdt_server *srv, int remote, int64_t ts, si
 // The same Diff as the JSON body (§8(f) row 2, "move to a binary SoA codec
 // and keep the JSON codec"), with no text round trip: little-endian
 //   char magic[8] = "CRDTSOA1"; u64 n_entries, n_pairs, n_bytes;
-//   i64 ts[n_entries] (ascending); u32 pairs[n_entries];
+//   i64 ts[n_entries] (ascending); u32 pairs[n_entries] (0xFFFFFFFF: a nil map, no pairs);
 //   u32 klen[n_pairs], vlen[n_pairs]; u8 bytes[n_bytes]
 // (each pair's key bytes then value bytes, pairs of an entry sorted by key).
 // Ingest is the decode loop of main.go:245-256 without Atoi: every entry is
 // put into RemoteDiff as a remote map; duplicate ts / keys: the last wins.
 namespace {
 constexpr char kSoaMagic[8] = {'C', 'R', 'D', 'T', 'S', 'O', 'A', '1'};
+constexpr uint32_t kNilPairs = 0xFFFFFFFFu;        // pairs[i] of a nil map (JSON null): no pairs follow
 
 template <typename T>
 void put_le(std::string &o, T v) {
@@ -887,7 +894,13 @@ extern "C" int crdt_server_gossip_binary(crdt_server *srv, char *buf, size_t cap
             put_le<uint64_t>(body, np);
             put_le<uint64_t>(body, nb);
             for (auto &e : srv->s.Diff) put_le<int64_t>(body, e.first);
-            for (auto &kv : sorted) put_le<uint32_t>(body, (uint32_t)kv.size());
+            {
+                size_t i = 0;
+                for (auto &e : srv->s.Diff) {
+                    const uint32_t c = (uint32_t)sorted[i++].size();
+                    put_le<uint32_t>(body, e.second->nil ? kNilPairs : c);
+                }
+            }
             for (auto &kv : sorted)
                 for (auto *x : kv) put_le<uint32_t>(body, (uint32_t)x->first.size());
             for (auto &kv : sorted)
@@ -919,7 +932,10 @@ extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, siz
     const unsigned char *pts = p + 32, *ppairs = pts + ne * 8, *pkl = ppairs + ne * 4, *pvl = pkl + np * 4,
                         *pb = pvl + np * 4;
     uint64_t pairs_total = 0, bytes_total = 0;
-    for (uint64_t i = 0; i < ne; ++i) pairs_total += get_le<uint32_t>(ppairs + 4 * i);
+    for (uint64_t i = 0; i < ne; ++i) {
+        const uint32_t k = get_le<uint32_t>(ppairs + 4 * i);
+        pairs_total += k == kNilPairs ? 0 : k;
+    }
     if (pairs_total != np) return CRDT_OK;
     for (uint64_t j = 0; j < np; ++j) bytes_total += (uint64_t)get_le<uint32_t>(pkl + 4 * j) + get_le<uint32_t>(pvl + 4 * j);
     if (bytes_total != nb) return CRDT_OK;
@@ -927,7 +943,7 @@ extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, siz
     puts.reserve(ne);
     uint64_t j = 0, off = 0;
     for (uint64_t i = 0; i < ne; ++i) {
-        const uint32_t k = get_le<uint32_t>(ppairs + 4 * i);
+        const uint32_t k0 = get_le<uint32_t>(ppairs + 4 * i), k = k0 == kNilPairs ? 0 : k0;
         std::map<std::string, std::string> m;                   // duplicate keys: the last wins
         for (uint32_t u = 0; u < k; ++u, ++j) {
             const uint32_t kl = get_le<uint32_t>(pkl + 4 * j), vl = get_le<uint32_t>(pvl + 4 * j);
@@ -938,6 +954,7 @@ extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, siz
         }
         auto v = std::make_shared<Value>();
         v->local = false;
+        v->nil = k0 == kNilPairs;
         v->kv.assign(m.begin(), m.end());
         puts.emplace_back(get_le<int64_t>(pts + 8 * i), std::move(v));
     }

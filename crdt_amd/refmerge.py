@@ -145,15 +145,9 @@ def to_device(arrs: dict, device) -> dict:
     return out
 
 
-def merge_batch(eng, replicas: Sequence[Tuple[dict, dict]]):
-    """Bit-exact (*Server).merge() of every (Diff, RemoteDiff) pair in ONE
-    device call.  Returns [(new_diff, current_state), ...]."""
-    pk = Packer()
-    for diff, remote in replicas:
-        pk.add_replica(diff, remote)
-    arrs = pk.arrays()
-    dev = to_device(arrs, eng.device)
-    out = eng.refmerge_batch(dev)
+def unpack_batch(pk: Packer, arrs: dict, out: dict):
+    """Device outputs of a packed batch -> [(new_diff, current_state), ...]
+    with the Diff values being the Packer's own value objects."""
     off = out["off"].cpu().numpy()
     n_out = int(off[-1])
     ts = out["ts"][:n_out].cpu().numpy()
@@ -177,3 +171,14 @@ def merge_batch(eng, replicas: Sequence[Tuple[dict, dict]]):
                 state[pk.slot_names[slot]] = str(int(ssum[slot]))        # strconv.Itoa (main.go:96)
         results.append((new_diff, state))
     return results
+
+
+def merge_batch(eng, replicas: Sequence[Tuple[dict, dict]]):
+    """Bit-exact (*Server).merge() of every (Diff, RemoteDiff) pair in ONE
+    device call.  Returns [(new_diff, current_state), ...]."""
+    pk = Packer()
+    for diff, remote in replicas:
+        pk.add_replica(diff, remote)
+    arrs = pk.arrays()
+    out = eng.refmerge_batch(to_device(arrs, eng.device))
+    return unpack_batch(pk, arrs, out)

@@ -196,3 +196,129 @@ def sharded_refmerge(eng, packed: dict, group=None) -> dict:
         dist.all_reduce(acc["npar"], op=dist.ReduceOp.SUM, group=group)
         eng.refmerge_acc_set_best(acc, n_slots, cmax, v)
     return eng.refmerge_finalize(packed, acc, out)
+
+
+# ---------------------------------------------------------------- native RCCL communicator
+class Comm:
+    """The C-ABI's own RCCL communicator (crdt_shard_*, csrc/shard.hip).
+
+    * ``Comm.create(devices)``: one process drives every listed GPU
+      (ncclCommInitAll); per-member inputs are lists indexed by member, each
+      tensor on that member's GPU.  Member contexts run on streams the
+      library owns: inputs must be ready (torch.cuda.synchronize) before a
+      call, and :meth:`sync` before outputs are read.
+    * ``Comm.init_rank(eng, group)``: one member per process (one process per
+      GPU, as torchrun launches the bench); rank 0's RCCL unique id travels
+      over the torch.distributed group once, after that every data-path
+      collective is the library's own ncclAllReduce / ncclBroadcast on the
+      engine's stream.
+
+    uint64 state travels as ncclUint64 with ncclMax: RCCL's unsigned max is
+    exactly the G-Counter / vector-clock join.
+    """
+
+    def __init__(self, handle: C.c_void_p, devices: Sequence[torch.device], owner=None):
+        self._h = handle
+        self.devices = list(devices)
+        self._owner = owner                 # keeps a borrowed Engine alive
+        m, n, r0 = C.c_int(), C.c_int(), C.c_int()
+        _lib.call("crdt_shard_comm_info", handle, C.byref(m), C.byref(n), C.byref(r0))
+        self.members, self.nranks, self.rank0 = m.value, n.value, r0.value
+
+    @classmethod
+    def create(cls, devices: Sequence[int]) -> "Comm":
+        arr = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        _lib.call("crdt_shard_comm_create", arr, len(devices), C.byref(h))
+        return cls(h, [torch.device("cuda", d) for d in devices])
+
+    @classmethod
+    def init_rank(cls, eng, group=None) -> "Comm":
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            _lib.call("crdt_shard_unique_id", uid, 128)
+        if world > 1:
+            obj = [uid.raw if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            uid = C.create_string_buffer(obj[0], 128)
+        eng._bind()
+        h = C.c_void_p()
+        _lib.call("crdt_shard_comm_init_rank", eng.ctx, uid, world, rank, C.byref(h), ctx=eng.ctx)
+        return cls(h, [eng.device], owner=eng)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().crdt_shard_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _call(self, fn: str, *args) -> None:
+        if self._owner is not None:
+            self._owner._bind()
+        st = getattr(_lib.lib(), fn)(self._h, *args)
+        if st < 0:
+            raise _lib.CrdtError(fn, st, _lib.lib().crdt_shard_comm_last_error(self._h))
+
+    def _ptrs(self, ts) -> C.Array:
+        if len(ts) != self.members:
+            raise ValueError(f"expected one tensor per member ({self.members})")
+        for t, d in zip(ts, self.devices):
+            if t.device != d or not t.is_contiguous():
+                raise ValueError(f"member tensor must be contiguous on {d}")
+        return (C.c_void_p * self.members)(*[t.data_ptr() for t in ts])
+
+    def sync(self) -> None:
+        self._call("crdt_shard_sync")
+
+    def fold_max(self, shards: Sequence[torch.Tensor], outs: Sequence[torch.Tensor] | None = None):
+        """Config E1: per-member fold of its [rows, nodes] shard, then
+        ncclAllReduce(ncclUint64, ncclMax): every member's out = the global fold."""
+        nodes = shards[0].shape[1]
+        if outs is None:
+            outs = [torch.empty(nodes, dtype=torch.int64, device=d) for d in self.devices]
+        rows = (C.c_size_t * self.members)(*[s.shape[0] for s in shards])
+        self._call("crdt_shard_fold_max_u64", self._ptrs(shards), rows, nodes, self._ptrs(outs))
+        return outs
+
+    def allreduce_max_u64(self, bufs: Sequence[torch.Tensor]):
+        """Config E2: in-place ncclAllReduce(ncclUint64, ncclMax)."""
+        self._call("crdt_shard_allreduce_max_u64", self._ptrs(bufs), bufs[0].numel())
+        return bufs
+
+    def allreduce(self, bufs: Sequence[torch.Tensor], op: str = "sum"):
+        """In-place all-reduce of int64 / int32 tensors (signed), op 'sum' | 'max'."""
+        t = {torch.int64: 0, torch.int32: 3}[bufs[0].dtype]
+        self._call("crdt_shard_allreduce", self._ptrs(bufs), bufs[0].numel(), t, {"sum": 0, "max": 1}[op])
+        return bufs
+
+    @staticmethod
+    def _tuples(sets) -> C.Array:
+        from ._lib import crdt_tuples
+        return (crdt_tuples * len(sets))(*[s.c() for s in sets])
+
+    def set_allgather_v(self, locals_, outs, cap: int) -> int:
+        """Every member's out <- all ranks' local tuples in rank order; returns the length."""
+        n = (C.c_size_t * self.members)(*[len(s) for s in locals_])
+        tot = C.c_size_t()
+        self._call("crdt_shard_set_allgather_v", self._tuples(locals_), n, self._tuples(outs), cap, C.byref(tot))
+        return tot.value
+
+    def set_merge(self, a, b, lww: bool = True, outs=None):
+        """Key-range-sharded LWW / OR-Set merge of inputs every member holds
+        in full; returns per-member TupleSets (the whole merged state)."""
+        from .engine import TupleSet
+        na, nb = len(a[0]), len(b[0])
+        cap = max(na + nb, 1)
+        outs = [TupleSet.empty(cap, d) for d in self.devices] if outs is None else outs
+        n = C.c_size_t()
+        self._call("crdt_shard_lww_merge" if lww else "crdt_shard_orset_merge", self._tuples(a), na,
+                   self._tuples(b), nb, self._tuples(outs), cap, C.byref(n))
+        return [o.slice(n.value) for o in outs]

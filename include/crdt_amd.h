@@ -38,7 +38,9 @@ typedef enum crdt_status {
     CRDT_E_NOMEM = -3,      /* device allocation failed */
     CRDT_E_NODEV = -4,      /* no usable gfx950 device */
     CRDT_E_UNSORTED = -5,   /* input violates the documented sort order */
-    CRDT_E_RANGE = -6       /* an index/size does not fit the kernel's integer width */
+    CRDT_E_RANGE = -6,      /* an index/size does not fit the kernel's integer width */
+    CRDT_E_COMM = -7,       /* RCCL error; see crdt_shard_comm_last_error() */
+    CRDT_E_DEVICE = -8      /* a kernel raised a device-side failure flag (CRDT_DEV_*): output invalid */
 } crdt_status;
 
 typedef struct crdt_ctx crdt_ctx;
@@ -74,7 +76,9 @@ int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
 /* Kernel tuning knobs (process-wide), for A/B runs: "join.unroll" (1,2,4,8),
  * "join.nontemporal" (0/1), "join.blocks_per_cu" (1..64),
  * "vclock.pairs_per_wave" (1,2,4,8), "sets.grid_per_cu" (0 = occupancy query);
- * diagnostics: "sets.stamps" (0/1), "sets.diag_no_lookback" (0/1, WRONG output).
+ * diagnostics: "sets.stamps" (0/1), "sets.diag_no_lookback" (0/1, WRONG output);
+ * fault injection: "fail.refmerge" (n: the next n RefMerge calls return
+ * CRDT_E_NOMEM before touching the device -- error-path tests).
  * Returns CRDT_E_INVAL for an unknown name or value. */
 int crdt_set_option(const char *name, int64_t value);
 
@@ -324,6 +328,56 @@ int crdt_shard_range(uint64_t rows, int world, int rank, uint64_t *begin, uint64
  * int64 MAX all-reduce (RCCL/gloo) compute the unsigned max exactly. */
 int crdt_u64_to_ordered_i64(crdt_ctx *ctx, const uint64_t *in_dev, int64_t *out_dev, size_t n);
 int crdt_ordered_i64_to_u64(crdt_ctx *ctx, const int64_t *in_dev, uint64_t *out_dev, size_t n);
+
+/* Multi-GPU joins over RCCL (xGMI).  The reference's analog is pull gossip of
+ * whole logs over HTTP (main.go:226-258); there is no reference collective.
+ * A communicator has one or more LOCAL members (a GPU, its crdt_ctx and its
+ * RCCL rank):
+ *   crdt_shard_comm_create    -- ONE process drives every listed GPU
+ *                                (ncclCommInitAll; calls are RCCL groups);
+ *   crdt_shard_comm_init_rank -- one member per process (one process per GPU,
+ *                                ncclCommInitRank); `id` is rank 0's
+ *                                crdt_shard_unique_id, shipped to every rank
+ *                                by the host (any channel).
+ * Per-member arguments are arrays indexed by member; pointers in them are
+ * device pointers on that member's GPU.  Work is enqueued on each member's
+ * context stream (crdt_shard_member_ctx) unless a call says it synchronises. */
+typedef struct crdt_comm crdt_comm;
+#define CRDT_SHARD_ID_BYTES 128
+int crdt_shard_unique_id(void *id, size_t cap);
+int crdt_shard_comm_create(const int *devices, int n, crdt_comm **out);
+int crdt_shard_comm_init_rank(crdt_ctx *ctx, const void *id, int nranks, int rank, crdt_comm **out);
+int crdt_shard_comm_destroy(crdt_comm *comm);
+int crdt_shard_comm_info(const crdt_comm *comm, int *members, int *nranks, int *rank0);
+int crdt_shard_member_ctx(crdt_comm *comm, int member, crdt_ctx **ctx);
+int crdt_shard_comm_last_error(const crdt_comm *comm);     /* last ncclResult_t */
+int crdt_shard_sync(crdt_comm *comm);
+/* Config E1: member i folds its [rows[i] x nodes] row shard (crdt_gcounter_fold),
+ * then ncclAllReduce(ncclUint64, ncclMax) of the nodes-long folds: every
+ * member's out[i] holds the global join of the whole population. */
+int crdt_shard_fold_max_u64(crdt_comm *comm, const uint64_t *const *shard_dev, const size_t *rows, size_t nodes,
+                            uint64_t *const *out_dev);
+/* Config E2: divergent full-state copies joined in place,
+ * ncclAllReduce(ncclUint64, ncclMax). */
+int crdt_shard_allreduce_max_u64(crdt_comm *comm, uint64_t *const *buf_dev, size_t n);
+/* Generic in-place all-reduce for the sharded RefMerge accumulators. */
+enum { CRDT_SHARD_I64 = 0, CRDT_SHARD_U64 = 1, CRDT_SHARD_U32 = 2, CRDT_SHARD_I32 = 3 };
+enum { CRDT_SHARD_SUM = 0, CRDT_SHARD_MAX = 1 };
+int crdt_shard_allreduce(crdt_comm *comm, void *const *buf_dev, size_t n, int type, int op);
+/* Keyed sets: member i contributes local[i] (n_local[i] tuples); every
+ * member's out[i] (capacity cap) receives all ranks' tuples concatenated in
+ * rank order; *n_total = that length (CRDT_E_RANGE if > cap).  Synchronises. */
+int crdt_shard_set_allgather_v(crdt_comm *comm, const crdt_tuples *local, const size_t *n_local,
+                               const crdt_tuples *out, size_t cap, size_t *n_total);
+/* Key-range-sharded LWW / OR-Set merge of sorted inputs that EVERY member
+ * holds in full (a[i], b[i]): splitters = rank quantiles of a sample of both
+ * key arrays (identical data, so no exchange), each member merges its range,
+ * then crdt_shard_set_allgather_v.  out[i] == crdt_lww_merge / crdt_orset_merge
+ * of the whole inputs on every member.  Synchronises. */
+int crdt_shard_lww_merge(crdt_comm *comm, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
+                         const crdt_tuples *out, size_t cap, size_t *n_out);
+int crdt_shard_orset_merge(crdt_comm *comm, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
+                           const crdt_tuples *out, size_t cap, size_t *n_out);
 
 /* ------------------------------------------------ synthetic state (bench/tests)
  * SplitMix64-seeded generators; identical to the numpy

@@ -60,3 +60,67 @@ def oracle_merge(diff, remote):
         elif kind[slot] == 2:
             state[pk.slot_names[slot]] = str(int(ssum[slot]))
     return new_diff, state
+
+
+def assert_batch_matches_oracle(h, out, slots_per_replica=62, replicas=None):
+    """Every replica (or the listed ones) of a packed batch's device output
+    == oracle_packed_replica: new Diff ts / origin / src and CurrentState."""
+    off = out["off"].cpu().numpy()
+    ts, org, src = (out[k].cpu().numpy() for k in ("ts", "origin", "src"))
+    kind, sstr, ssum = (out[k].cpu().numpy() for k in ("st_kind", "st_str", "st_sum"))
+    for p in (range(h["replicas"]) if replicas is None else replicas):
+        o_ts, o_or, o_src, k, s, v = oracle_packed_replica(h, p, slots_per_replica)
+        a, b = int(off[p]), int(off[p + 1])
+        np.testing.assert_array_equal(ts[a:b], o_ts)
+        np.testing.assert_array_equal(org[a:b], o_or)
+        np.testing.assert_array_equal(src[a:b], o_src)
+        sl = slice(p * slots_per_replica, (p + 1) * slots_per_replica)
+        np.testing.assert_array_equal(kind[sl], k)
+        np.testing.assert_array_equal(sstr[sl].view(np.uint32)[k == 1], s[k == 1])
+        np.testing.assert_array_equal(ssum[sl][k == 2], v[k == 2])
+
+
+def split_ts_range(h, lo, hi):
+    """The [lo, hi) ts slice of every replica of a host packed batch (kv pairs
+    carried along), plus the global L / R index of each kept entry
+    (`l_sel` / `r_sel`): one rank's share of a ts-range-sharded batch."""
+    P = h["replicas"]
+    kvk, kvv = h["kv_key"], h["kv_val"]
+    out = {"replicas": P, "n_slots": h["n_slots"], "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
+    keys, vals = [], []
+    nkv = 0
+    for side in ("l", "r"):
+        off, ts, kv = h[f"{side}_off"], h[f"{side}_ts"], h[f"{side}_kv"]
+        sel = []
+        noff = [0]
+        for p in range(P):
+            b, e = int(off[p]), int(off[p + 1])
+            i = b + int(np.searchsorted(ts[b:e], lo, side="left"))
+            j = b + int(np.searchsorted(ts[b:e], hi, side="left"))
+            sel.append(np.arange(i, j))
+            noff.append(noff[-1] + (j - i))
+        sel = np.concatenate(sel).astype(np.int64) if sel else np.zeros(0, np.int64)
+        cnt = (kv[sel + 1] - kv[sel]).astype(np.int64)
+        nkvo = np.zeros(len(sel) + 1, np.int64)
+        nkvo[1:] = np.cumsum(cnt)
+        idx = np.concatenate([np.arange(kv[s], kv[s + 1]) for s in sel]).astype(np.int64) if len(sel) else \
+            np.zeros(0, np.int64)
+        keys.append(kvk[idx])
+        vals.append(kvv[idx])
+        out[f"{side}_off"] = np.array(noff, np.int64)
+        out[f"{side}_ts"] = ts[sel].copy()
+        out[f"{side}_kv"] = nkvo + nkv
+        out[f"{side}_sel"] = sel
+        if side == "l":
+            out["l_origin"] = h["l_origin"][sel].copy()
+        nkv += int(nkvo[-1])
+    out["kv_key"] = np.concatenate(keys)
+    out["kv_val"] = np.concatenate(vals)
+    return out
+
+
+def ts_splitters(h, world):
+    """world + 1 ts splitters: quantiles of every L and R ts, open ends."""
+    allts = np.sort(np.concatenate([h["l_ts"], h["r_ts"]]))
+    return [int(np.iinfo(np.int64).min)] + [int(allts[(r * len(allts)) // world]) for r in range(1, world)] + \
+        [int(np.iinfo(np.int64).max)]

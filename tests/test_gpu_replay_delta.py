@@ -163,3 +163,38 @@ def test_delta_large_batch_then_overflow(eng):
     d = refmerge.to_device(h, eng.device)
     st = eng.replay_state_init(d)
     _same_merge(eng.refmerge_batch(d), eng.refmerge_delta(d, st))
+
+
+# ---- pinned to the oracle / the hand-derived KATs directly (not only to the full GPU refold)
+def test_delta_kats_match_expected(eng):
+    """Every KAT through crdt_replay_state_init + crdt_refmerge_delta: the new
+    Diff and CurrentState equal the hand-derived expectations."""
+    from refmerge_util import diff_signature
+    kats = load_kats()
+    pk = refmerge.Packer()
+    for k in kats:
+        pk.add_replica(*kat_inputs(k))
+    arrs = pk.arrays()
+    d = refmerge.to_device(arrs, eng.device)
+    st = eng.replay_state_init(d)
+    res = refmerge.unpack_batch(pk, arrs, eng.refmerge_delta(d, st))
+    for k, (diff, state) in zip(kats, res):
+        assert diff_signature(diff) == k["diff"], k["name"]
+        assert state == k["state"], k["name"]
+
+
+def test_delta_chained_merges_match_oracle(eng):
+    """Three chained delta merges (the carried state is never rebuilt): every
+    replica's new Diff and CurrentState == oc_refmerge of that merge's
+    (L, R), main.go:35-100."""
+    from refmerge_util import assert_batch_matches_oracle
+    rng = np.random.default_rng(19)
+    h = synth.refmerge_packed(14, 24, 2500)
+    d = refmerge.to_device(h, eng.device)
+    st = eng.replay_state_init(d)
+    for _ in range(3):
+        out = eng.refmerge_delta(d, st)
+        assert_batch_matches_oracle(h, out)
+        h = _next_round({**h, "kv_key": h["kv_key"].view(np.uint32), "kv_val": h["kv_val"].view(np.uint32)},
+                        out, rng)
+        d = refmerge.to_device(h, eng.device)

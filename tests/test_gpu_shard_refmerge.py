@@ -12,46 +12,9 @@ import pytest
 import torch
 
 from crdt_amd import refmerge, synth
+from refmerge_util import split_ts_range as _split, ts_splitters
 
 pytestmark = pytest.mark.gpu
-
-
-def _split(h, lo, hi):
-    """The [lo, hi) ts slice of every replica of a host packed batch, plus the
-    global L / R index of each kept entry."""
-    P = h["replicas"]
-    kvk, kvv = h["kv_key"], h["kv_val"]
-    out = {"replicas": P, "n_slots": h["n_slots"], "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
-    keys, vals = [], []
-    nkv = 0
-    for side in ("l", "r"):
-        off, ts, kv = h[f"{side}_off"], h[f"{side}_ts"], h[f"{side}_kv"]
-        sel = []
-        noff = [0]
-        for p in range(P):
-            b, e = int(off[p]), int(off[p + 1])
-            i = b + int(np.searchsorted(ts[b:e], lo, side="left"))
-            j = b + int(np.searchsorted(ts[b:e], hi, side="left"))
-            sel.append(np.arange(i, j))
-            noff.append(noff[-1] + (j - i))
-        sel = np.concatenate(sel).astype(np.int64) if sel else np.zeros(0, np.int64)
-        cnt = (kv[sel + 1] - kv[sel]).astype(np.int64)
-        nkvo = np.zeros(len(sel) + 1, np.int64)
-        nkvo[1:] = np.cumsum(cnt)
-        idx = np.concatenate([np.arange(kv[s], kv[s + 1]) for s in sel]).astype(np.int64) if len(sel) else \
-            np.zeros(0, np.int64)
-        keys.append(kvk[idx])
-        vals.append(kvv[idx])
-        out[f"{side}_off"] = np.array(noff, np.int64)
-        out[f"{side}_ts"] = ts[sel].copy()
-        out[f"{side}_kv"] = nkvo + nkv
-        out[f"{side}_sel"] = sel
-        if side == "l":
-            out["l_origin"] = h["l_origin"][sel].copy()
-        nkv += int(nkvo[-1])
-    out["kv_key"] = np.concatenate(keys)
-    out["kv_val"] = np.concatenate(vals)
-    return out
 
 
 def _run_sharded(eng, shards):
@@ -75,9 +38,7 @@ def _run_sharded(eng, shards):
 def test_ts_range_sharded_refmerge_equals_unsharded(eng, world):
     h = synth.refmerge_packed(41, 64, 3000)
     full = eng.refmerge_batch(refmerge.to_device(h, eng.device))
-    allts = np.sort(np.concatenate([h["l_ts"], h["r_ts"]]))
-    spl = [int(np.iinfo(np.int64).min)] + [int(allts[(r * len(allts)) // world]) for r in range(1, world)] + \
-        [int(np.iinfo(np.int64).max)]
+    spl = ts_splitters(h, world)
     shards = [_split(h, spl[r], spl[r + 1]) for r in range(world)]
     # the top shard's exclusive end must not lose ts == INT64_MAX (none in this data)
     assert sum(len(s["l_ts"]) for s in shards) == len(h["l_ts"])
