@@ -917,6 +917,8 @@ def main():
         if hasattr(wl, "extra"):
             out.update(wl.extra(avg_ms))
         print(json.dumps(out), flush=True)
+    if getattr(wl, "comm", None) is not None:
+        wl.comm.close()                               # before the engine whose context it borrows
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -78,6 +78,31 @@ class crdt_replay_state(C.Structure):
                 ("nhold", C.c_void_p)]
 
 
+class crdt_local_in(C.Structure):
+    _fields_ = [
+        ("replicas", C.c_uint32), ("n_slots", C.c_uint32),
+        ("n_l", C.c_uint64), ("n_c", C.c_uint64), ("n_kv", C.c_uint64), ("n_str", C.c_uint64),
+        ("l_off", C.c_void_p), ("l_ts", C.c_void_p), ("l_origin", C.c_void_p),
+        ("c_off", C.c_void_p), ("c_ts", C.c_void_p), ("c_kv", C.c_void_p),
+        ("kv_key", C.c_void_p), ("kv_val", C.c_void_p), ("str_bytes", C.c_void_p), ("str_off", C.c_void_p),
+    ]
+
+
+class crdt_local_out(C.Structure):
+    _fields_ = [("off", C.c_void_p), ("ts", C.c_void_p), ("origin", C.c_void_p), ("src", C.c_void_p),
+                ("status", C.c_void_p), ("st_kind", C.c_void_p), ("st_str", C.c_void_p), ("st_sum", C.c_void_p)]
+
+
+class crdt_gossip_bodies(C.Structure):
+    _fields_ = [("n_bodies", C.c_uint32), ("key_cap", C.c_uint32), ("kv_base", C.c_uint64), ("data", C.c_void_p),
+                ("body_off", C.c_void_p), ("slot_base", C.c_void_p)]
+
+
+class crdt_gossip_decoded(C.Structure):
+    _fields_ = [("r_off", C.c_void_p), ("r_ts", C.c_void_p), ("r_kv", C.c_void_p), ("kv_key", C.c_void_p),
+                ("kv_val", C.c_void_p)]
+
+
 class crdt_refmerge_acc(C.Structure):
     _fields_ = [("best", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p)]
 
@@ -130,6 +155,7 @@ SIGNATURES = {
     "crdt_debug_set_grid": (_I, [C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
+    "crdt_local_apply": (_I, [_CTX, C.POINTER(crdt_local_in), C.POINTER(crdt_local_out)]),
     "crdt_refmerge_batch_ex": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out), _P,
                                     C.POINTER(crdt_refmerge_acc)]),
     "crdt_refmerge_local_maxl": (_I, [_CTX, C.POINTER(crdt_refmerge_in), _P]),
@@ -164,6 +190,13 @@ SIGNATURES = {
     "crdt_server_gossip_binary": (_I, [_P, C.c_char_p, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_server_ingest_binary": (_I, [_P, C.c_char_p, _SZ, C.POINTER(C.c_int)]),
     "crdt_server_set_alive": (_I, [_P, _I]),
+    "crdt_strtab_create": (_I, [_CTX, _SZ, _SZ, C.POINTER(_P)]),
+    "crdt_strtab_destroy": (_I, [_P]),
+    "crdt_strtab_info": (_I, [_P, C.POINTER(_U64), C.POINTER(_U64), C.POINTER(_P), C.POINTER(_P)]),
+    "crdt_strtab_get": (_I, [_P, _U64, C.POINTER(_P), C.POINTER(_SZ)]),
+    "crdt_strtab_intern": (_I, [_CTX, _P, _P, _P, _SZ, _P]),
+    "crdt_gossip_decode": (_I, [_CTX, C.POINTER(crdt_gossip_bodies), _P, _P, C.POINTER(crdt_gossip_decoded),
+                                C.POINTER(C.c_uint32)]),
     "crdt_server_remote_keys": (_I, [_P, _P, _SZ, C.POINTER(_SZ)]),
     "crdt_server_entry_at": (_I, [_P, _I, C.c_int64, _SZ, C.POINTER(C.c_void_p), C.POINTER(_SZ),
                                  C.POINTER(C.c_void_p), C.POINTER(_SZ), C.POINTER(_SZ)]),

@@ -8,7 +8,9 @@
 
 namespace crdt {
 JoinTuning g_join;
-int g_vclock_pairs_per_wave = 4;
+FoldTuning g_fold;
+int g_vclock_pairs_per_wave = 8;   // tools/tune_vclock.py at 10M x 128: 8 x 1 block/CU 6.50 TB/s
+int g_vclock_blocks_per_cu = 1;    //   against 6.19 TB/s for 4 x 8
 int g_sets_stamps = 0;
 int g_sets_grid_per_cu = 0;
 int g_sets_diag = 0;
@@ -199,9 +201,21 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "join.blocks_per_cu")) {
         if (v < 1 || v > 64) return CRDT_E_INVAL;
         g_join.blocks_per_cu = (int)v;
+    } else if (!strcmp(name, "fold.unroll")) {
+        if (v != 1 && v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
+        g_fold.unroll = (int)v;
+    } else if (!strcmp(name, "fold.nontemporal")) {
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_fold.nontemporal = (int)v;
+    } else if (!strcmp(name, "fold.blocks_per_cu")) {
+        if (v < 1 || v > 64) return CRDT_E_INVAL;
+        g_fold.blocks_per_cu = (int)v;
     } else if (!strcmp(name, "vclock.pairs_per_wave")) {
         if (v != 1 && v != 2 && v != 4 && v != 8) return CRDT_E_INVAL;
         g_vclock_pairs_per_wave = (int)v;
+    } else if (!strcmp(name, "vclock.blocks_per_cu")) {
+        if (v < 1 || v > 64) return CRDT_E_INVAL;
+        g_vclock_blocks_per_cu = (int)v;
     } else if (!strcmp(name, "sets.grid_per_cu")) { // 0 = occupancy query (co-residency required)
         if (v < 0 || v > 16) return CRDT_E_INVAL;
         g_sets_grid_per_cu = (int)v;

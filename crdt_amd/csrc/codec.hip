@@ -1,0 +1,698 @@
+// codec.hip -- the gossip pull decoded on the device.
+//
+// The reference's pull (main.go:245-256) decodes the peer's whole Diff
+// (Diff.ToJSON, main.go:159) into RemoteDiff and merges (main.go:257).  The
+// build's binary SoA form of that body (crdt_server_gossip_binary:
+// "CRDTSOA1", u64 n_entries, n_pairs, n_bytes, i64 ts[], u32 pairs[],
+// u32 klen[], u32 vlen[], bytes) lands here in HBM as raw bytes and is turned
+// straight into the crdt_refmerge_in R arrays:
+//   r_ts[e]            = ts[i]
+//   r_kv[e]            = kv_base + exclusive scan of pairs[]
+//   kv_key[kv_base+j]  = slot_base(body) + id of key j in a KEY table
+//   kv_val[kv_base+j]  = id of value j in a VALUE table (the merge's string arena)
+// Strings are interned into device string tables (crdt_strtab): open
+// addressing over 64-bit entries {hash32, id | pending-pair}, ids dense in
+// first-seen order, bytes in an append-only arena with str_off offsets.
+// Interning is three passes with no intra-kernel publication beyond the
+// claim CAS itself: (A) every pair finds its string or CLAIMS an empty entry
+// tagged with its own pair index (equal strings compare bytes against the
+// claimer's bytes, which are in the immutable body); (B) claimers get dense
+// ids by a scan, copy their bytes into the arena and turn the entry into the
+// id; (C) every pair reads its entry's id.  Bodies the device path does not
+// take (a nil map, ts not ascending, keys of an entry not strictly ascending,
+// a key beyond the caller's slot range, a full table) are flagged per body:
+// the host decodes those (crdt_server_ingest_binary), as the reference would.
+#include <string.h>
+
+#include <vector>
+
+#include "scan.hpp"
+
+struct crdt_strtab {
+    int device = 0;
+    uint64_t *tab = nullptr;      // [H] entries, kEmpty or hash32 << 32 | tag << 31 | payload
+    uint64_t H = 0;               // power of two
+    uint8_t *bytes = nullptr;
+    uint64_t cap_bytes = 0;
+    uint64_t *off = nullptr;      // [cap_n + 1]: off[id], off[n] = bytes used
+    uint64_t cap_n = 0;
+    uint64_t n = 0, nbytes = 0;   // host-known (after each synchronising call)
+    std::vector<uint8_t> h_bytes; // host mirror of the arena (append-only)
+    std::vector<uint64_t> h_off{0};
+};
+
+namespace crdt {
+namespace {
+
+constexpr uint64_t kEmptyE = ~0ull;
+constexpr uint32_t kPend = 0x80000000u;
+constexpr uint32_t kIdMask = 0x7FFFFFFFu;
+constexpr uint32_t kNilPairs = 0xFFFFFFFFu;
+
+enum : uint32_t {
+    kBodyMalformed = 1u,          // sizes / counts inconsistent: nothing of the body is usable
+    kBodyHost = 2u,               // valid, but the device path does not take it (host decode)
+    kBodyFull = 4u,               // a string table was full (grow and retry, or host decode)
+};
+
+__device__ __forceinline__ uint32_t hash32(const uint8_t *p, uint32_t n) {
+    uint32_t h = 2166136261u;                          // FNV-1a
+    for (uint32_t i = 0; i < n; ++i) h = (h ^ p[i]) * 16777619u;
+    return h;
+}
+
+__device__ __forceinline__ uint32_t le32(const uint8_t *p) {
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+__device__ __forceinline__ uint64_t le64(const uint8_t *p) { return (uint64_t)le32(p) | (uint64_t)le32(p + 4) << 32; }
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// strictly ascending as byte strings (Go string order)
+__device__ __forceinline__ bool bytes_lt(const uint8_t *a, uint32_t na, const uint8_t *b, uint32_t nb) {
+    const uint32_t n = na < nb ? na : nb;
+    for (uint32_t i = 0; i < n; ++i)
+        if (a[i] != b[i]) return a[i] < b[i];
+    return na < nb;
+}
+
+struct TabView {
+    uint64_t *tab;
+    uint64_t mask;
+    const uint8_t *bytes;
+    const uint64_t *off;
+};
+
+// Pass A: find the string or claim an empty entry for pending reference
+// `self`.  get(ref, &p, &len) returns the bytes of a pending reference.
+// Returns the entry index (kEmptyE as uint64 on a full table); *rep = claimed.
+template <class Get>
+__device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, uint32_t len, uint32_t self,
+                              const Get &get, bool *rep) {
+    *rep = false;
+    uint64_t i = h & t.mask;
+    for (uint64_t probe = 0; probe <= t.mask; ++probe, i = (i + 1) & t.mask) {
+        uint64_t e = __hip_atomic_load(&t.tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == kEmptyE) {
+            const uint64_t want = (uint64_t)h << 32 | kPend | self;
+            const uint64_t old = atomicCAS((unsigned long long *)&t.tab[i], (unsigned long long)kEmptyE,
+                                           (unsigned long long)want);
+            if (old == kEmptyE) {
+                *rep = true;
+                return i;
+            }
+            e = old;
+        }
+        if ((uint32_t)(e >> 32) != h) continue;
+        const uint32_t pay = (uint32_t)e;
+        const uint8_t *q;
+        uint32_t qn;
+        if (pay & kPend) {
+            get(pay & kIdMask, &q, &qn);
+        } else {
+            const uint32_t id = pay & kIdMask;
+            q = t.bytes + t.off[id];
+            qn = (uint32_t)(t.off[id + 1] - t.off[id]);
+        }
+        if (qn == len && bytes_eq(q, s, len)) return i;
+    }
+    return kEmptyE;
+}
+
+// ---------------------------------------------------------------- bodies
+struct BodyDesc {                  // one pulled body, concatenated in one device buffer
+    uint64_t data;                 // byte offset of the body
+    uint64_t e0, q0;               // first global entry / pair of the body
+    uint64_t ne, np, nb;
+    uint32_t slot_base;
+    uint32_t pad;
+};
+
+__device__ __forceinline__ uint32_t find_body(const BodyDesc *b, uint32_t nbody, uint64_t x, bool pairs) {
+    uint32_t lo = 0, hi = nbody;                     // last body whose first item <= x
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((pairs ? b[mid].q0 : b[mid].e0) <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct DecodeCtx {
+    const uint8_t *data;
+    const BodyDesc *bd;
+    uint32_t nbody;
+    uint32_t *flag;                // [nbody]
+    const uint64_t *boff;          // [n_pairs + 1] scan of (klen + vlen) over all pairs
+    const uint32_t *klen;          // [n_pairs]
+    uint64_t n_pairs;
+    // pair j: key bytes and value bytes, clamped to the body's byte region
+    // (lengths that overrun it mark the body malformed: never read past it)
+    __device__ void pair_bytes(uint64_t j, const uint8_t **kp, uint32_t *kn, const uint8_t **vp, uint32_t *vn) const {
+        const uint32_t b = find_body(bd, nbody, j, true);
+        const BodyDesc d = bd[b];
+        const uint8_t *region = data + d.data + 32 + 12 * d.ne + 8 * d.np;
+        const uint64_t o = boff[j] - boff[d.q0];
+        const uint64_t k = klen[j], v = boff[j + 1] - boff[j] - k;
+        if (o > d.nb || k > d.nb - o || v > d.nb - o - k) {
+            atomicOr(&flag[b], kBodyMalformed);
+            *kp = *vp = region;
+            *kn = *vn = 0;
+            return;
+        }
+        *kp = region + o;
+        *kn = (uint32_t)k;
+        *vp = region + o + k;
+        *vn = (uint32_t)v;
+    }
+};
+
+// per entry: ts, pair count; ts must ascend strictly within a body, no nil map
+__global__ void k_dec_entries(DecodeCtx c, uint64_t n_e, int64_t *__restrict__ r_ts, uint32_t *__restrict__ cnt) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n_e; e += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = find_body(c.bd, c.nbody, e, false);
+        const BodyDesc d = c.bd[b];
+        const uint64_t i = e - d.e0;
+        const uint8_t *base = c.data + d.data + 32;
+        const int64_t ts = (int64_t)le64(base + 8 * i);
+        uint32_t k = le32(base + 8 * d.ne + 4 * i);
+        if (k == kNilPairs) {                             // a nil map: the host path keeps its flag
+            atomicOr(&c.flag[b], kBodyHost);
+            k = 0;
+        }
+        if (i && (int64_t)le64(base + 8 * (i - 1)) >= ts) atomicOr(&c.flag[b], kBodyHost);
+        r_ts[e] = ts;
+        cnt[e] = k;
+    }
+}
+
+struct PairLenSrc {                // scan source: klen + vlen of pair j (also records klen)
+    DecodeCtx c;
+    uint32_t *klen_out;
+    struct Item {
+        uint64_t len = 0;
+    };
+    __device__ Item load(uint64_t j) const {
+        const uint32_t b = find_body(c.bd, c.nbody, j, true);
+        const BodyDesc d = c.bd[b];
+        const uint64_t q = j - d.q0;
+        const uint8_t *base = c.data + d.data + 32 + 12 * d.ne;
+        const uint32_t kl = le32(base + 4 * q), vl = le32(base + 4 * d.np + 4 * q);
+        klen_out[j] = kl;
+        return Item{(uint64_t)kl + vl};
+    }
+};
+
+struct CountSrc32 {
+    const uint32_t *in;
+    struct Item {
+        uint64_t len = 0;
+    };
+    __device__ Item load(uint64_t i) const { return Item{in[i]}; }
+};
+
+// per body: counts consistent with the header (pairs and bytes)
+__global__ void k_dec_bodies(DecodeCtx c, const uint64_t *__restrict__ pre) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= c.nbody) return;
+    const BodyDesc d = c.bd[b];
+    if (pre[d.e0 + d.ne] - pre[d.e0] != d.np) atomicOr(&c.flag[b], kBodyMalformed);
+    if (c.boff[d.q0 + d.np] - c.boff[d.q0] != d.nb) atomicOr(&c.flag[b], kBodyMalformed);
+}
+
+// r_kv = kv_base + pre; mark the first pair of each entry
+// (a malformed body's pair counts may run past n_p: its marks are dropped,
+// the body is flagged by k_dec_bodies)
+__global__ void k_dec_kv(const uint64_t *__restrict__ pre, uint64_t n_e, uint64_t n_p, uint64_t kv_base,
+                         uint64_t *__restrict__ r_kv, uint8_t *__restrict__ first) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= n_e; e += (uint64_t)gridDim.x * 256) {
+        const uint64_t p = pre[e];
+        r_kv[e] = kv_base + p;
+        if (e < n_e && pre[e + 1] > p && p < n_p) first[p] = 1;
+    }
+}
+
+struct PendGet {                   // bytes of pending reference j (key or value part of pair j)
+    DecodeCtx c;
+    bool value;
+    __device__ void operator()(uint32_t j, const uint8_t **p, uint32_t *n) const {
+        const uint8_t *kp, *vp;
+        uint32_t kn, vn;
+        c.pair_bytes(j, &kp, &kn, &vp, &vn);
+        *p = value ? vp : kp;
+        *n = value ? vn : kn;
+    }
+};
+
+// pass A over both tables; key order check within an entry
+__global__ void k_dec_claim(DecodeCtx c, TabView kt, TabView vt, const uint8_t *__restrict__ first,
+                            uint64_t *__restrict__ kslot, uint64_t *__restrict__ vslot, uint32_t *__restrict__ krep,
+                            uint32_t *__restrict__ vrep, uint32_t *__restrict__ kh, uint32_t *__restrict__ vh) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < c.n_pairs; j += (uint64_t)gridDim.x * 256) {
+        const uint8_t *kp, *vp;
+        uint32_t kn, vn;
+        c.pair_bytes(j, &kp, &kn, &vp, &vn);
+        const uint32_t b = find_body(c.bd, c.nbody, j, true);
+        if (j && !first[j] && j > c.bd[b].q0) {
+            const uint8_t *pkp, *pvp;
+            uint32_t pkn, pvn;
+            c.pair_bytes(j - 1, &pkp, &pkn, &pvp, &pvn);
+            if (!bytes_lt(pkp, pkn, kp, kn)) atomicOr(&c.flag[b], kBodyHost);   // served bodies sort keys
+        }
+        bool r;
+        const uint32_t h1 = hash32(kp, kn), h2 = hash32(vp, vn);
+        const uint64_t si = tab_claim(kt, h1, kp, kn, (uint32_t)j, PendGet{c, false}, &r);
+        krep[j] = r ? 1u : 0u;
+        const uint64_t sv = tab_claim(vt, h2, vp, vn, (uint32_t)j, PendGet{c, true}, &r);
+        vrep[j] = r ? 1u : 0u;
+        if (si == kEmptyE || sv == kEmptyE) atomicOr(&c.flag[b], kBodyFull);
+        kslot[j] = si;
+        vslot[j] = sv;
+        kh[j] = h1;
+        vh[j] = h2;
+    }
+}
+
+struct RepLenSrc {                 // scan source: bytes of the claimers' strings
+    DecodeCtx c;
+    const uint32_t *rep;
+    bool value;
+    struct Item {
+        uint64_t len = 0;
+    };
+    __device__ Item load(uint64_t j) const {
+        if (!rep[j]) return Item{0};
+        const uint8_t *kp, *vp;
+        uint32_t kn, vn;
+        c.pair_bytes(j, &kp, &kn, &vp, &vn);
+        return Item{value ? vn : kn};
+    }
+};
+
+// pass B: claimers -> dense ids, bytes into the arena, entry -> id
+__global__ void k_dec_assign(DecodeCtx c, TabView t, bool value, const uint32_t *__restrict__ rep,
+                             const uint64_t *__restrict__ rank, const uint64_t *__restrict__ rboff,
+                             const uint64_t *__restrict__ slot, const uint32_t *__restrict__ hsh, uint64_t n_old,
+                             uint64_t bytes_old, uint8_t *__restrict__ arena, uint64_t *__restrict__ off) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < c.n_pairs; j += (uint64_t)gridDim.x * 256) {
+        if (!rep[j] || slot[j] == kEmptyE) continue;
+        const uint8_t *kp, *vp;
+        uint32_t kn, vn;
+        c.pair_bytes(j, &kp, &kn, &vp, &vn);
+        const uint8_t *p = value ? vp : kp;
+        const uint32_t n = value ? vn : kn;
+        const uint64_t id = n_old + rank[j];
+        const uint64_t o = bytes_old + rboff[j];
+        for (uint32_t i = 0; i < n; ++i) arena[o + i] = p[i];
+        off[id] = o;
+        t.tab[slot[j]] = (uint64_t)hsh[j] << 32 | (uint32_t)id;
+    }
+}
+
+__global__ void k_off_end(uint64_t *__restrict__ off, const uint64_t *__restrict__ n_new_dev,
+                          const uint64_t *__restrict__ bytes_new_dev, uint64_t n_old, uint64_t bytes_old) {
+    off[n_old + *n_new_dev] = bytes_old + *bytes_new_dev;
+}
+
+// pass C: ids into the kv arrays (key ids re-based to the body's slot range)
+__global__ void k_dec_ids(DecodeCtx c, const uint64_t *__restrict__ kslot, const uint64_t *__restrict__ vslot,
+                          const uint64_t *__restrict__ ktab, const uint64_t *__restrict__ vtab, uint32_t key_cap,
+                          uint64_t kv_base, uint32_t *__restrict__ kv_key, uint32_t *__restrict__ kv_val) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < c.n_pairs; j += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = find_body(c.bd, c.nbody, j, true);
+        if (kslot[j] == kEmptyE || vslot[j] == kEmptyE) continue;
+        const uint32_t kid = (uint32_t)ktab[kslot[j]] & kIdMask;
+        const uint32_t vid = (uint32_t)vtab[vslot[j]] & kIdMask;
+        if (kid >= key_cap) atomicOr(&c.flag[b], kBodyHost);   // key beyond the replica's slot range
+        kv_key[kv_base + j] = c.bd[b].slot_base + kid;
+        kv_val[kv_base + j] = vid;
+    }
+}
+
+// rehash: every id re-inserted (ids are unique: no byte compare needed)
+__global__ void k_rehash(uint64_t *__restrict__ tab, uint64_t mask, const uint8_t *__restrict__ bytes,
+                         const uint64_t *__restrict__ off, uint64_t n) {
+    for (uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (uint64_t)gridDim.x * 256) {
+        const uint32_t h = hash32(bytes + off[id], (uint32_t)(off[id + 1] - off[id]));
+        uint64_t i = h & mask;
+        for (;;) {
+            const uint64_t old = atomicCAS((unsigned long long *)&tab[i], (unsigned long long)kEmptyE,
+                                           (unsigned long long)((uint64_t)h << 32 | (uint32_t)id));
+            if (old == kEmptyE) break;
+            i = (i + 1) & mask;
+        }
+    }
+}
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1024;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int dev_grow(crdt_ctx *ctx, void **p, uint64_t old_bytes, uint64_t new_bytes) {
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, new_bytes);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (*p && old_bytes) {
+        e = hipMemcpyAsync(q, *p, old_bytes, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(q);
+            return hip_fail(ctx, e);
+        }
+        (void)hipFree(*p);
+    }
+    *p = q;
+    return CRDT_OK;
+}
+
+// Room for `more` strings of `more_bytes` bytes: grow the arena / offsets
+// (copy) and the hash table (rehash at load <= 1/2).
+int tab_reserve(crdt_ctx *ctx, crdt_strtab *t, uint64_t more, uint64_t more_bytes) {
+    int rc;
+    if (t->nbytes + more_bytes > t->cap_bytes) {
+        const uint64_t cap = std::max<uint64_t>(2 * t->cap_bytes, t->nbytes + more_bytes + 4096);
+        rc = dev_grow(ctx, (void **)&t->bytes, t->nbytes, cap);
+        if (rc) return rc;
+        t->cap_bytes = cap;
+    }
+    if (t->n + more > t->cap_n) {
+        const uint64_t cap = std::max<uint64_t>(2 * t->cap_n, t->n + more + 256);
+        rc = dev_grow(ctx, (void **)&t->off, (t->n + 1) * 8, (cap + 1) * 8);
+        if (rc) return rc;
+        t->cap_n = cap;
+    }
+    if (2 * (t->n + more) > t->H) {
+        const uint64_t H = pow2_at_least(4 * (t->n + more));
+        uint64_t *nt = nullptr;
+        hipError_t e = hipMalloc(&nt, H * 8);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        e = hipMemsetAsync(nt, 0xFF, H * 8, ctx->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(nt);
+            return hip_fail(ctx, e);
+        }
+        if (t->n) k_rehash<<<grid_for(t->n, 256, (unsigned)ctx->num_cus * 4), 256, 0, ctx->stream>>>(
+            nt, H - 1, t->bytes, t->off, t->n);
+        e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(nt);
+            return hip_fail(ctx, e);
+        }
+        if (t->tab) (void)hipFree(t->tab);
+        t->tab = nt;
+        t->H = H;
+    }
+    return CRDT_OK;
+}
+
+// host mirror: pull the strings added since the last sync
+int tab_pull_new(crdt_ctx *ctx, crdt_strtab *t, uint64_t n_new, uint64_t bytes_new) {
+    const uint64_t n0 = t->h_off.size() - 1, b0 = t->h_bytes.size();
+    t->h_off.resize(n_new + 1);
+    t->h_bytes.resize(bytes_new);
+    hipError_t e = hipSuccess;
+    if (n_new > n0)
+        e = hipMemcpyAsync(t->h_off.data() + n0 + 1, t->off + n0 + 1, (n_new - n0) * 8, hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess && bytes_new > b0)
+        e = hipMemcpyAsync(t->h_bytes.data() + b0, t->bytes + b0, bytes_new - b0, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    t->n = n_new;
+    t->nbytes = bytes_new;
+    return CRDT_OK;
+}
+
+}  // namespace
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_strtab_create(crdt_ctx *ctx, size_t cap_strings, size_t cap_bytes, crdt_strtab **out) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!out) return CRDT_E_INVAL;
+    *out = nullptr;
+    crdt_strtab *t = new (std::nothrow) crdt_strtab();
+    if (!t) return CRDT_E_NOMEM;
+    t->device = ctx->device;
+    rc = tab_reserve(ctx, t, std::max<size_t>(cap_strings, 16), std::max<size_t>(cap_bytes, 256));
+    if (!rc) {
+        hipError_t e = hipMemsetAsync(t->off, 0, 8, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = hip_fail(ctx, e);
+    }
+    if (rc) {
+        (void)crdt_strtab_destroy(t);
+        return rc;
+    }
+    *out = t;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_strtab_destroy(crdt_strtab *t) {
+    if (!t) return CRDT_OK;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != t->device) (void)hipSetDevice(t->device);
+    if (t->tab) (void)hipFree(t->tab);
+    if (t->bytes) (void)hipFree(t->bytes);
+    if (t->off) (void)hipFree(t->off);
+    delete t;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_strtab_info(const crdt_strtab *t, uint64_t *n_str, uint64_t *n_bytes, const uint8_t **bytes_dev,
+                                const uint64_t **off_dev) {
+    if (!t || !n_str || !n_bytes) return CRDT_E_INVAL;
+    *n_str = t->n;
+    *n_bytes = t->nbytes;
+    if (bytes_dev) *bytes_dev = t->bytes;
+    if (off_dev) *off_dev = t->off;
+    return CRDT_OK;
+}
+
+// i-th string of the table's host mirror (valid until the next call that adds strings)
+extern "C" int crdt_strtab_get(const crdt_strtab *t, uint64_t id, const char **p, size_t *len) {
+    if (!t || !p || !len) return CRDT_E_INVAL;
+    if (id >= t->n) return CRDT_E_RANGE;
+    *p = (const char *)t->h_bytes.data() + t->h_off[id];
+    *len = t->h_off[id + 1] - t->h_off[id];
+    return CRDT_OK;
+}
+
+extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, crdt_strtab *keys,
+                                  crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!in || !keys || !vals || !out || !body_status) return CRDT_E_INVAL;
+    if (keys->device != ctx->device || vals->device != ctx->device) return CRDT_E_INVAL;
+    const uint32_t nb = in->n_bodies;
+    if (nb == 0) return CRDT_OK;
+    if (!in->data || !in->body_off || !in->slot_base || !out->r_off) return CRDT_E_INVAL;
+    const hipStream_t s = ctx->stream;
+    // headers (32 B per body) to the host: the sizes the decode is planned with
+    std::vector<uint8_t> hdr(32 * (size_t)nb, 0);
+    hipError_t e = hipSuccess;
+    for (uint32_t b = 0; b < nb && e == hipSuccess; ++b) {
+        const uint64_t len = in->body_off[b + 1] - in->body_off[b];
+        if (in->body_off[b + 1] < in->body_off[b]) return CRDT_E_INVAL;
+        if (len >= 32) e = hipMemcpyAsync(&hdr[32 * b], in->data + in->body_off[b], 32, hipMemcpyDeviceToHost, s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    std::vector<BodyDesc> bd(nb);
+    std::vector<uint64_t> r_off(nb + 1, 0);
+    uint64_t n_e = 0, n_p = 0, n_b = 0;
+    static const char magic[8] = {'C', 'R', 'D', 'T', 'S', 'O', 'A', '1'};
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t len = in->body_off[b + 1] - in->body_off[b];
+        const uint8_t *h = &hdr[32 * b];
+        uint64_t ne = 0, np = 0, nby = 0;
+        body_status[b] = 0;
+        if (len < 32 || memcmp(h, magic, 8) != 0) {
+            body_status[b] = kBodyMalformed;
+        } else {
+            memcpy(&ne, h + 8, 8);
+            memcpy(&np, h + 16, 8);
+            memcpy(&nby, h + 24, 8);
+            if (ne > len / 12 || np > len / 8 || nby > len || 32 + ne * 12 + np * 8 + nby != len || np >= kPend)
+                body_status[b] = kBodyMalformed;
+        }
+        if (body_status[b]) ne = np = nby = 0;           // contributes nothing
+        bd[b] = BodyDesc{in->body_off[b], n_e, n_p, ne, np, nby, in->slot_base[b], 0};
+        n_e += ne;
+        n_p += np;
+        n_b += nby;
+        r_off[b + 1] = n_e;
+    }
+    if (n_p >= kPend || n_e >= 0xFFFFFFFFull) return CRDT_E_RANGE;
+    if ((n_e && (!out->r_ts || !out->r_kv)) || (n_p && (!out->kv_key || !out->kv_val))) return CRDT_E_INVAL;
+    rc = tab_reserve(ctx, keys, n_p, n_b);
+    if (!rc) rc = tab_reserve(ctx, vals, n_p, n_b);
+    if (rc) return rc;
+    // workspace
+    const size_t need = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 4) + Carve::round((n_e + 1) * 4) +
+                        Carve::round((n_e + 1) * 8) + Carve::round(n_p * 4 + 4) + Carve::round((n_p + 1) * 8) * 7 +
+                        Carve::round(n_p + 1) + Carve::round(n_p * 4 + 4) * 4 + 4 * scan_lb_tmp_bytes(n_p + n_e) +
+                        Carve::round(64) + 4096;
+    rc = ws_reserve(ctx, need);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    BodyDesc *d_bd = w.take<BodyDesc>(nb);
+    uint32_t *d_flag = w.take<uint32_t>(nb);
+    uint32_t *cnt = w.take<uint32_t>(n_e + 1);
+    uint64_t *pre = w.take<uint64_t>(n_e + 1);
+    uint32_t *klen = w.take<uint32_t>(n_p + 1);
+    uint64_t *boff = w.take<uint64_t>(n_p + 1);
+    uint64_t *kslot = w.take<uint64_t>(n_p + 1);
+    uint64_t *vslot = w.take<uint64_t>(n_p + 1);
+    uint64_t *krank = w.take<uint64_t>(n_p + 1);
+    uint64_t *vrank = w.take<uint64_t>(n_p + 1);
+    uint64_t *kboff = w.take<uint64_t>(n_p + 1);
+    uint64_t *vboff = w.take<uint64_t>(n_p + 1);
+    uint8_t *first = w.take<uint8_t>(n_p + 1);
+    uint32_t *krep = w.take<uint32_t>(n_p + 1);
+    uint32_t *vrep = w.take<uint32_t>(n_p + 1);
+    uint32_t *kh = w.take<uint32_t>(n_p + 1);
+    uint32_t *vh = w.take<uint32_t>(n_p + 1);
+    void *tmp = w.take<char>(scan_lb_tmp_bytes(n_p + n_e));
+    e = hipMemcpyAsync(d_bd, bd.data(), nb * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, nb * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(first, 0, n_p + 1, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(out->r_off, r_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    DecodeCtx c{in->data, d_bd, nb, d_flag, boff, klen, n_p};
+    const unsigned cap = (unsigned)ctx->num_cus * 8;
+    if (n_e) {
+        k_dec_entries<<<grid_for(n_e, 256, cap), 256, 0, s>>>(c, n_e, out->r_ts, cnt);
+        rc = check_launch(ctx);
+        if (!rc) rc = scan_lb(ctx, CountSrc32{cnt}, NoAct(), n_e, 0, pre, tmp);
+        if (rc) return rc;
+    } else {
+        e = hipMemsetAsync(pre, 0, 8, s);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
+    rc = scan_lb(ctx, PairLenSrc{c, klen}, NoAct(), n_p, 0, boff, tmp);
+    if (rc) return rc;
+    k_dec_bodies<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(c, pre);
+    k_dec_kv<<<grid_for(n_e + 1, 256, cap), 256, 0, s>>>(pre, n_e, n_p, in->kv_base, out->r_kv, first);
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    const uint64_t kn0 = keys->n, kb0 = keys->nbytes, vn0 = vals->n, vb0 = vals->nbytes;
+    // counters: [0] new keys, [1] new key bytes, [2] new values, [3] new value bytes
+    uint64_t *ctr = w.take<uint64_t>(8);
+    if (n_p) {
+        TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
+        TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
+        k_dec_claim<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kt, vt, first, kslot, vslot, krep, vrep, kh, vh);
+        rc = check_launch(ctx);
+        if (!rc) rc = scan_lb(ctx, CountSrc32{krep}, NoAct(), n_p, 0, krank, tmp);
+        if (!rc) rc = scan_lb(ctx, CountSrc32{vrep}, NoAct(), n_p, 0, vrank, tmp);
+        if (!rc) rc = scan_lb(ctx, RepLenSrc{c, krep, false}, NoAct(), n_p, 0, kboff, tmp);
+        if (!rc) rc = scan_lb(ctx, RepLenSrc{c, vrep, true}, NoAct(), n_p, 0, vboff, tmp);
+        if (rc) return rc;
+        k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kt, false, krep, krank, kboff, kslot, kh, kn0, kb0,
+                                                            keys->bytes, keys->off);
+        k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, vt, true, vrep, vrank, vboff, vslot, vh, vn0, vb0,
+                                                            vals->bytes, vals->off);
+        k_off_end<<<1, 1, 0, s>>>(keys->off, krank + n_p, kboff + n_p, kn0, kb0);
+        k_off_end<<<1, 1, 0, s>>>(vals->off, vrank + n_p, vboff + n_p, vn0, vb0);
+        k_dec_ids<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kslot, vslot, keys->tab, vals->tab, in->key_cap,
+                                                         in->kv_base, out->kv_key, out->kv_val);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+        e = hipMemcpyAsync(ctr + 0, krank + n_p, 8, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(ctr + 1, kboff + n_p, 8, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(ctr + 2, vrank + n_p, 8, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(ctr + 3, vboff + n_p, 8, hipMemcpyDeviceToDevice, s);
+    } else {
+        e = hipMemsetAsync(ctr, 0, 32, s);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    uint64_t h_ctr[4];
+    std::vector<uint32_t> flags(nb);
+    e = hipMemcpyAsync(h_ctr, ctr, 32, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    for (uint32_t b = 0; b < nb; ++b) {
+        body_status[b] |= flags[b];
+        if (body_status[b] & kBodyMalformed) body_status[b] = kBodyMalformed;   // nothing else applies then
+    }
+    rc = tab_pull_new(ctx, keys, kn0 + h_ctr[0], kb0 + h_ctr[1]);
+    if (!rc) rc = tab_pull_new(ctx, vals, vn0 + h_ctr[2], vb0 + h_ctr[3]);
+    return rc;
+}
+
+// Intern n strings [off[i], off[i+1]) of a device arena (host callers seeding
+// a table): ids_dev[i] = the string's id.  Runs as a decode of one synthetic
+// body would, via the same three passes.  Synchronises.
+extern "C" int crdt_strtab_intern(crdt_ctx *ctx, crdt_strtab *t, const uint8_t *bytes_dev, const uint64_t *off_host,
+                                  size_t n, uint32_t *ids_dev) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!t || (n && (!bytes_dev || !off_host || !ids_dev))) return CRDT_E_INVAL;
+    if (n == 0) return CRDT_OK;
+    if (n >= kPend) return CRDT_E_RANGE;
+    // a synthetic body: n entries of one pair each, key = the string, value = ""
+    const uint64_t nbytes = off_host[n] - off_host[0];
+    std::vector<uint8_t> body(32 + 12 * n + 8 * n);
+    memcpy(body.data(), "CRDTSOA1", 8);
+    const uint64_t hdr[3] = {n, n, nbytes};
+    memcpy(body.data() + 8, hdr, 24);
+    for (size_t i = 0; i < n; ++i) {
+        const int64_t ts = (int64_t)i;
+        const uint32_t one = 1, kl = (uint32_t)(off_host[i + 1] - off_host[i]), vl = 0;
+        memcpy(body.data() + 32 + 8 * i, &ts, 8);
+        memcpy(body.data() + 32 + 8 * n + 4 * i, &one, 4);
+        memcpy(body.data() + 32 + 12 * n + 4 * i, &kl, 4);
+        memcpy(body.data() + 32 + 16 * n + 4 * i, &vl, 4);
+    }
+    uint8_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, body.size() + nbytes);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    e = hipMemcpyAsync(d, body.data(), body.size(), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && nbytes)
+        e = hipMemcpyAsync(d + body.size(), bytes_dev + off_host[0], nbytes, hipMemcpyDeviceToDevice, ctx->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return hip_fail(ctx, e);
+    }
+    crdt_strtab *scratch = nullptr;                     // the synthetic values ("") go to a throwaway table
+    rc = crdt_strtab_create(ctx, 16, 256, &scratch);
+    if (rc) {
+        (void)hipFree(d);
+        return rc;
+    }
+    int64_t *r_ts = nullptr;
+    uint64_t *r_kv = nullptr, *r_off = nullptr;
+    uint32_t *vv = nullptr;
+    e = hipMalloc(&r_ts, n * 8);
+    if (e == hipSuccess) e = hipMalloc(&r_kv, (n + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&r_off, 16);
+    if (e == hipSuccess) e = hipMalloc(&vv, n * 4);
+    if (e == hipSuccess) {
+        const uint64_t boff[2] = {0, body.size() + nbytes};
+        const uint32_t sb = 0;
+        crdt_gossip_bodies gb{1, 0xFFFFFFFFu, 0, d, boff, &sb};
+        crdt_gossip_decoded go{r_off, r_ts, r_kv, ids_dev, vv};
+        uint32_t st = 0;
+        rc = crdt_gossip_decode(ctx, &gb, t, scratch, &go, &st);
+        if (!rc && (st & ~kBodyHost)) rc = (st & kBodyFull) ? CRDT_E_NOMEM : CRDT_E_INVAL;   // (order flags do not apply)
+    } else {
+        rc = hip_fail(ctx, e);
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+    for (void *p : {(void *)d, (void *)r_ts, (void *)r_kv, (void *)r_off, (void *)vv})
+        if (p) (void)hipFree(p);
+    (void)crdt_strtab_destroy(scratch);
+    return rc;
+}

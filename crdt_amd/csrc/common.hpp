@@ -38,7 +38,14 @@ struct JoinTuning {
     int blocks_per_cu = 2;  // grid = CUs * blocks_per_cu (grid-stride beyond); ~16 KiB in flight per CU
 };
 extern JoinTuning g_join;
+struct FoldTuning {
+    int unroll = 8;         // 16-B vectors in flight per lane (tools/tune_fold.py: 8 x 1 block/CU
+    int nontemporal = 1;    //   = 32 KiB in flight per CU, 7.06 TB/s at 100M x 64, against
+    int blocks_per_cu = 1;  //   6.18 TB/s for 4 x 4)
+};
+extern FoldTuning g_fold;
 extern int g_vclock_pairs_per_wave;
+extern int g_vclock_blocks_per_cu;
 extern int g_sets_grid_per_cu; // persistent set-merge workgroups per CU (0 = occupancy query)
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
 extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at s_setprio 2, bit 1 spinning data barrier

@@ -53,7 +53,7 @@ __global__ void k_join_tail(const uint64_t *a, const uint64_t *b, uint64_t *o, s
 // Column max over rows.  Fast path: nodes a power of two in [2, 512], so a
 // 256-lane block covers 512 uint64 = 512/nodes whole rows per load and every
 // lane keeps the same column pair for the whole grid-stride loop.
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_fold_pow2(const u64x2 *__restrict__ a, size_t n2,
                                                    int nodes, uint64_t *__restrict__ partial) {
     const size_t stride = (size_t)gridDim.x * 256;
@@ -62,11 +62,11 @@ __global__ __launch_bounds__(256) void k_fold_pow2(const u64x2 *__restrict__ a, 
     for (; i + (size_t)(U - 1) * stride < n2; i += (size_t)U * stride) {
         u64x2 x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = ld<true>(a + i + (size_t)u * stride);
+        for (int u = 0; u < U; ++u) x[u] = ld<NT>(a + i + (size_t)u * stride);
 #pragma unroll
         for (int u = 0; u < U; ++u) m = vmax(m, x[u]);
     }
-    for (; i < n2; i += stride) m = vmax(m, ld<true>(a + i));
+    for (; i < n2; i += stride) m = vmax(m, ld<NT>(a + i));
     __shared__ u64x2 red[256];
     red[threadIdx.x] = m;
     __syncthreads();
@@ -240,14 +240,31 @@ extern "C" int crdt_gcounter_fold(crdt_ctx *ctx, const uint64_t *a, size_t rows,
     if (!a) return CRDT_E_INVAL;
     const bool pow2 = nodes >= 2 && nodes <= 512 && (nodes & (nodes - 1)) == 0 && aligned16(a);
     unsigned grid;
-    if (pow2) grid = grid_for(rows * nodes / 2, 256 * 4, (unsigned)(ctx->num_cus * 4));
+    const unsigned bpc = (unsigned)g_fold.blocks_per_cu;
+    if (pow2) grid = grid_for(rows * nodes / 2, 256 * (unsigned)g_fold.unroll, (unsigned)ctx->num_cus * bpc);
     else grid = grid_for(rows, 1, (unsigned)(ctx->num_cus * 4));
     const size_t part_bytes = (size_t)grid * nodes * sizeof(uint64_t);
     rc = ws_reserve(ctx, part_bytes);
     if (rc) return rc;
     uint64_t *partial = (uint64_t *)ctx->ws;
-    if (pow2) k_fold_pow2<4><<<grid, 256, 0, ctx->stream>>>((const u64x2 *)a, rows * nodes / 2, (int)nodes, partial);
-    else k_fold_generic<<<grid, 256, 0, ctx->stream>>>(a, rows, nodes, partial);
+    if (pow2) {
+        const u64x2 *va = (const u64x2 *)a;
+        const size_t n2 = rows * nodes / 2;
+        const hipStream_t s = ctx->stream;
+        const bool nt = g_fold.nontemporal != 0;
+#define FOLD(U) (nt ? k_fold_pow2<U, true><<<grid, 256, 0, s>>>(va, n2, (int)nodes, partial) \
+                    : k_fold_pow2<U, false><<<grid, 256, 0, s>>>(va, n2, (int)nodes, partial))
+        switch (g_fold.unroll) {
+            case 1: FOLD(1); break;
+            case 2: FOLD(2); break;
+            case 8: FOLD(8); break;
+            case 16: FOLD(16); break;
+            default: FOLD(4); break;
+        }
+#undef FOLD
+    } else {
+        k_fold_generic<<<grid, 256, 0, ctx->stream>>>(a, rows, nodes, partial);
+    }
     rc = check_launch(ctx);
     if (rc) return rc;
     const unsigned g2 = grid < 32 ? grid : 32;

@@ -101,7 +101,7 @@ extern "C" int crdt_vclock_classify(crdt_ctx *ctx, const uint64_t *a, const uint
     if (!a || !b || !cls) return CRDT_E_INVAL;
     const bool vec = (((uintptr_t)a | (uintptr_t)b) & 15) == 0;
     const hipStream_t s = ctx->stream;
-    const unsigned grid = grid_for(pairs * 64, 256, (unsigned)(ctx->num_cus * 8));
+    const unsigned grid = grid_for(pairs * 64, 256, (unsigned)(ctx->num_cus * g_vclock_blocks_per_cu));
     const u64x2 *va = (const u64x2 *)a, *vb = (const u64x2 *)b;
     const int ppw = g_vclock_pairs_per_wave;
     if (vec && nodes == 128) launch_vc<128>(ppw, grid, s, va, vb, cls, pairs);

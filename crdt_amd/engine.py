@@ -14,7 +14,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import call, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_out, crdt_replay_state, crdt_tuples
+from ._lib import (call, crdt_local_in, crdt_local_out, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_out,
+                   crdt_replay_state, crdt_tuples)
 
 VC_EQUAL, VC_BEFORE, VC_AFTER, VC_CONCURRENT = 0, 1, 2, 3
 
@@ -85,8 +86,18 @@ class Engine:
         call("crdt_ctx_create", self.device.index, self._stream, C.byref(ctx))
         self.ctx = ctx
         self._lib = lib
+        self._dependents = []              # weakrefs to objects borrowing ctx (shard.Comm)
+
+    def _depend(self, obj) -> None:
+        import weakref
+        self._dependents.append(weakref.ref(obj))
 
     def close(self) -> None:
+        for r in getattr(self, "_dependents", []):   # borrowers first: they use ctx in their teardown
+            o = r()
+            if o is not None:
+                o.close()
+        self._dependents = []
         if getattr(self, "ctx", None):
             self._lib.crdt_ctx_destroy(self.ctx)
             self.ctx = None
@@ -370,6 +381,32 @@ class Engine:
                                    ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum")))
         self._call("crdt_refmerge_finalize", C.byref(ca), int(packed["n_slots"]), _ptr(packed["str_bytes"]),
                    _ptr(packed["str_off"]), packed["str_off"].numel() - 1, C.byref(cout))
+        return out
+
+    # -- batched local apply
+    def local_apply(self, diff: dict, cmds: dict, state: dict, str_bytes: torch.Tensor,
+                    str_off: torch.Tensor, n_slots: int) -> dict:
+        """AddCommand (main.go:173-215) for every replica at once
+        (crdt_local_apply).  diff = {off, ts, origin} (device), cmds = {off,
+        ts, kv_off, kv_key, kv_val} (device; arrival order per replica),
+        state = {st_kind, st_str, st_sum} updated in place.  Returns the new
+        Diff {off, ts, origin, src} (src < 0: command -(src+1)) and the
+        per-command HTTP status."""
+        dev = self.device
+        n_l, n_c = diff["ts"].numel(), cmds["ts"].numel()
+        P = diff["off"].numel() - 1
+        out = {"off": torch.empty(P + 1, dtype=torch.int64, device=dev),
+               "ts": torch.empty(max(n_l + n_c, 1), dtype=torch.int64, device=dev),
+               "origin": torch.empty(max(n_l + n_c, 1), dtype=torch.uint8, device=dev),
+               "src": torch.empty(max(n_l + n_c, 1), dtype=torch.int64, device=dev),
+               "status": torch.empty(max(n_c, 1), dtype=torch.int16, device=dev)}
+        cin = crdt_local_in(P, n_slots, n_l, n_c, cmds["kv_key"].numel(), str_off.numel() - 1,
+                            _ptr(diff["off"]), _ptr(diff["ts"]), _ptr(diff["origin"]),
+                            _ptr(cmds["off"]), _ptr(cmds["ts"]), _ptr(cmds["kv_off"]),
+                            _ptr(cmds["kv_key"]), _ptr(cmds["kv_val"]), _ptr(str_bytes), _ptr(str_off))
+        cout = crdt_local_out(*(out[k].data_ptr() for k in ("off", "ts", "origin", "src", "status")),
+                              *(state[k].data_ptr() for k in ("st_kind", "st_str", "st_sum")))
+        self._call("crdt_local_apply", C.byref(cin), C.byref(cout))
         return out
 
     def atoi_batch(self, str_bytes: torch.Tensor, str_off: torch.Tensor):

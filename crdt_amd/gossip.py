@@ -172,15 +172,7 @@ class Population:
         r_kv = torch.empty(n_r + 1, dtype=torch.int64, device=dev)
         r_ts = torch.empty(n_r, dtype=torch.int64, device=dev)
         r_kv[n_r:].copy_(r_kb[-1:])
-        ar = self._arena
-        if (ar is not None and ar[0].numel() >= n_lkv + n_rkv and n_lkv > 0
-                and ar[0].data_ptr() == self.kv_key.data_ptr() and ar[1].data_ptr() == self.kv_val.data_ptr()):
-            arena_k, arena_v = ar                             # the Diff's pairs are already its prefix
-        else:
-            arena_k = torch.empty(max(n_lkv + n_rkv, 1), dtype=torch.int32, device=dev)
-            arena_v = torch.empty_like(arena_k)
-            arena_k[:n_lkv].copy_(self.kv_key)
-            arena_v[:n_lkv].copy_(self.kv_val)
+        arena_k, arena_v = self._kv_arena(n_lkv, n_rkv)   # the Diff's pairs are already its prefix
         if n_r:
             bo = b["kv_off"] if n_b else self.kv_off
             bt = b["ts"] if n_b else self.ts
@@ -190,6 +182,44 @@ class Population:
             bv = b["kv_val"] if n_b else self.kv_val
             self._call("crdt_seg_copy2", self.P, _p(codes), _p(a_kr), _p(b_kr), _p(r_kb), 4,
                        _p(self.kv_key), _p(bk), _p(arena_k), _p(delta), _p(self.kv_val), _p(bv), _p(arena_v), 1)
+        return self._merge_round(r_off, r_ts, r_kv, arena_k, arena_v, n_lkv, n_rkv)
+
+    def _kv_arena(self, n_lkv: int, n_more: int):
+        """A kv arena whose prefix is the Diff's pairs, with room for n_more."""
+        ar = self._arena
+        if (ar is not None and ar[0].numel() >= n_lkv + n_more and n_lkv > 0
+                and ar[0].data_ptr() == self.kv_key.data_ptr() and ar[1].data_ptr() == self.kv_val.data_ptr()):
+            return ar
+        dev = self.eng.device
+        arena_k = torch.empty(max(n_lkv + n_more, 1), dtype=torch.int32, device=dev)
+        arena_v = torch.empty_like(arena_k)
+        arena_k[:n_lkv].copy_(self.kv_key)
+        arena_v[:n_lkv].copy_(self.kv_val)
+        return arena_k, arena_v
+
+    def round_wire(self, data: torch.Tensor, body_off: Sequence[int], keys, vals, n_entries: int,
+                   n_pairs: int) -> dict:
+        """One pull round whose pulls arrive on the wire: body i (bytes
+        data[body_off[i]:body_off[i+1]] in HBM, the binary form of a peer's
+        Diff.ToJSON, main.go:159) is replica i's RemoteDiff.  The device
+        decode (crdt_gossip_decode, main.go:245-256) interns keys into `keys`
+        (key id k -> slot i*K + k) and values into `vals`, whose arena becomes
+        the population's string arena; then the batched merge and the next
+        Diffs as in round().  n_entries / n_pairs: totals of the bodies'
+        headers (codec.body_counts)."""
+        from . import codec
+        n_lkv = self.kv_key.numel()
+        arena_k, arena_v = self._kv_arena(n_lkv, n_pairs)
+        dec, st = codec.decode(self.eng, data, body_off, [i * self.K for i in range(self.P)], self.K, keys, vals,
+                               n_lkv, arena_k, arena_v, n_entries)
+        if st.any():
+            raise ValueError(f"bodies not taken by the device decode (status {st[st != 0][:8].tolist()}): "
+                             "decode those on the host")
+        self.str_bytes, self.str_off = vals.arena()
+        return self._merge_round(dec["r_off"], dec["r_ts"], dec["r_kv"], arena_k, arena_v, n_lkv, n_pairs)
+
+    def _merge_round(self, r_off, r_ts, r_kv, arena_k, arena_v, n_lkv: int, n_rkv: int) -> dict:
+        eng, dev, K = self.eng, self.eng.device, self.K
         # 2. the merge of every local replica
         packed = {"replicas": self.P, "n_slots": self.P * K, "l_off": self.off, "l_ts": self.ts,
                   "l_origin": self.origin, "l_kv": self.kv_off, "r_off": r_off, "r_ts": r_ts, "r_kv": r_kv,
@@ -248,6 +278,51 @@ class Population:
         self.kv_val = self._seg_copy(ecodes, self.kv_off, b_kv, kv, self.kv_val, b_val, m)
         self.kv_off, self.ts, self.origin = kv, ts, org
         self.off = d_off[0::2].contiguous()
+
+    def empty_state(self) -> dict:
+        """CurrentState with every key slot absent (NewServer with an empty
+        initialState, main.go:102-105)."""
+        n = max(self.P * self.K, 1)
+        dev = self.eng.device
+        return {"st_kind": torch.zeros(n, dtype=torch.uint8, device=dev),
+                "st_str": torch.zeros(n, dtype=torch.int32, device=dev),
+                "st_sum": torch.zeros(n, dtype=torch.int64, device=dev)}
+
+    def apply_local(self, host_cmds: dict) -> np.ndarray:
+        """POST /data on every replica at once (AddCommand, main.go:173-215;
+        crdt_local_apply): host_cmds = {off (P+1), ts, kv_off, kv_key (local
+        slot ids), kv_val}, commands in arrival order per replica, pairs in
+        apply order.  The Diffs get the *Command entries (a same-ms write
+        replaces, main.go:187), CurrentState the local apply; returns the
+        HTTP status of each command (200 / 500)."""
+        dev = self.eng.device
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+        cmds = {"off": t(host_cmds["off"], np.int64), "ts": t(host_cmds["ts"], np.int64),
+                "kv_off": t(host_cmds["kv_off"], np.int64),
+                "kv_key": t(np.asarray(host_cmds["kv_key"]).astype(np.uint32).view(np.int32), np.int32),
+                "kv_val": t(np.asarray(host_cmds["kv_val"]).astype(np.uint32).view(np.int32), np.int32)}
+        if self.state is None:
+            self.state = self.empty_state()
+        out = self.eng.local_apply({"off": self.off, "ts": self.ts, "origin": self.origin}, cmds, self.state,
+                                   self.str_bytes, self.str_off, self.P * self.K)
+        n_out = int(out["off"][-1].item())
+        src = out["src"][:n_out].contiguous()
+        new_kv = torch.empty(n_out + 1, dtype=torch.int64, device=dev)
+        cap = 2 * max(self.kv_key.numel() + cmds["kv_key"].numel(), 1)
+        nk = torch.empty(cap, dtype=torch.int32, device=dev)
+        nv = torch.empty(cap, dtype=torch.int32, device=dev)
+        # the Diff's kv pairs: from the old Diff (src >= 0) or the command (src < 0); command
+        # slots are local slot ids re-based to the replica's range by the caller's layout
+        self._call("crdt_seg_gather2", n_out, _p(src), _p(self.kv_off), _p(cmds["kv_off"]), 0, _p(new_kv), 4,
+                   _p(self.kv_key), _p(cmds["kv_key"]), _p(nk), _p(self.kv_val), _p(cmds["kv_val"]), _p(nv))
+        n_kv = int(new_kv[-1].item())
+        self.kv_key, self.kv_val = nk[:n_kv], nv[:n_kv]
+        self._arena = (nk, nv)
+        self.kv_off = new_kv
+        self.off = out["off"]
+        self.ts = out["ts"][:n_out]
+        self.origin = out["origin"][:n_out]
+        return out["status"][: cmds["ts"].numel()].cpu().numpy().astype(np.int64)
 
     # ---------------------------------------------------------------- readback
     def to_host(self) -> dict:

@@ -247,10 +247,14 @@ class Comm:
         eng._bind()
         h = C.c_void_p()
         _lib.call("crdt_shard_comm_init_rank", eng.ctx, uid, world, rank, C.byref(h), ctx=eng.ctx)
-        return cls(h, [eng.device], owner=eng)
+        c = cls(h, [eng.device], owner=eng)
+        eng._depend(c)                      # eng.close() destroys the communicator first
+        return c
 
     def close(self) -> None:
         if getattr(self, "_h", None):
+            if self._owner is not None and not getattr(self._owner, "ctx", None):
+                raise RuntimeError("engine closed before its communicator")   # never reached via Engine.close
             _lib.lib().crdt_shard_comm_destroy(self._h)
             self._h = None
 

@@ -68,6 +68,7 @@ int crdt_ctx_sync(crdt_ctx *ctx);
  * decoupled look-back exceeded its bounded wait (a scheduling fault, never
  * expected) raises CRDT_DEV_LOOKBACK and its output is invalid. */
 #define CRDT_DEV_LOOKBACK 1u
+#define CRDT_DEV_RANGE 2u          /* a batch exceeded a per-replica kernel limit (its output is invalid) */
 int crdt_ctx_device_status(crdt_ctx *ctx, uint32_t *flags, int clear);
 int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 /* Pre-size the context's device workspace so that later calls never
@@ -275,6 +276,46 @@ typedef struct crdt_replay_state {
 int crdt_replay_state_init(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_replay_state *st);
 int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out,
                         const crdt_replay_state *st);
+/* Batched local apply (§8(f) row 1): AddCommand (main.go:173-215) for many
+ * replicas in one call.  Replica p's commands are c_off[p] .. c_off[p+1] in
+ * ARRIVAL order, command j = (c_ts[j], pairs [c_kv[j], c_kv[j+1]) of the
+ * kv_key / kv_val arena, applied in the order given).  Per command, as the
+ * handler does: Diff.Put(ts, &data) (main.go:187: an equal ts is REPLACED, so
+ * of several same-ms commands the last stays), then the CurrentState apply
+ * (main.go:188-207): an absent key is set verbatim and the command stops
+ * (status 200); else Atoi(current) + Atoi(value) -> Itoa (int64 wrap), an
+ * Atoi failure stops it with status 500.  The new Diff is written like a
+ * RefMerge output (src >= 0: Diff index, < 0: command j as -(j+1)); the
+ * state (kind/str/sum per key slot, as crdt_refmerge_out) is updated in
+ * place.  At most 4096 commands per replica per call (CRDT_DEV_RANGE
+ * otherwise); the Alive check (502) is the host's. */
+typedef struct crdt_local_in {
+    uint32_t replicas;
+    uint32_t n_slots;
+    uint64_t n_l, n_c, n_kv, n_str;
+    const uint64_t *l_off;      /* [replicas+1] the Diffs (ascending unique ts per replica) */
+    const int64_t  *l_ts;
+    const uint8_t  *l_origin;
+    const uint64_t *c_off;      /* [replicas+1] commands per replica */
+    const int64_t  *c_ts;       /* [n_c] */
+    const uint64_t *c_kv;       /* [n_c+1] pair ranges */
+    const uint32_t *kv_key;     /* [n_kv] key slot */
+    const uint32_t *kv_val;     /* [n_kv] value string id */
+    const uint8_t  *str_bytes;
+    const uint64_t *str_off;    /* [n_str+1] */
+} crdt_local_in;
+typedef struct crdt_local_out {
+    uint64_t *off;              /* [replicas+1] */
+    int64_t  *ts;               /* capacity n_l + n_c */
+    uint8_t  *origin;
+    int64_t  *src;
+    uint16_t *status;           /* [n_c] HTTP status of each command: 200 / 500 */
+    uint8_t  *st_kind;          /* [n_slots] CurrentState, in / out */
+    uint32_t *st_str;
+    int64_t  *st_sum;
+} crdt_local_out;
+int crdt_local_apply(crdt_ctx *ctx, const crdt_local_in *in, const crdt_local_out *out);
+
 /* Go strconv.Atoi over a string arena: ok[s] = parsable, val[s] = value. */
 int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *str_bytes_dev, const uint64_t *str_off_dev,
                     uint64_t n_str, uint8_t *ok_dev, int64_t *val_dev);
@@ -443,6 +484,54 @@ int crdt_server_ingest_json(crdt_server *srv, const char *data, size_t len, int 
  * endian).  Ingest: *outcome 0 = put into RemoteDiff, 1 = malformed. */
 int crdt_server_gossip_binary(crdt_server *srv, char *buf, size_t cap, size_t *len, int *http_status);
 int crdt_server_ingest_binary(crdt_server *srv, const char *data, size_t len, int *outcome);
+/* Device string tables (string -> dense id in first-seen order, bytes in an
+ * append-only arena; str_off[n] = bytes used): the key dictionary and the
+ * value arena the device gossip decode interns into.  A table belongs to one
+ * device; calls that add strings synchronise and refresh a host mirror
+ * (crdt_strtab_get). */
+typedef struct crdt_strtab crdt_strtab;
+int crdt_strtab_create(crdt_ctx *ctx, size_t cap_strings, size_t cap_bytes, crdt_strtab **out);
+int crdt_strtab_destroy(crdt_strtab *tab);
+/* counts and the device arena (bytes_dev / off_dev nullable): off_dev[0..n_str]
+ * is the crdt_refmerge_in str_off of the table's strings. */
+int crdt_strtab_info(const crdt_strtab *tab, uint64_t *n_str, uint64_t *n_bytes, const uint8_t **bytes_dev,
+                     const uint64_t **off_dev);
+int crdt_strtab_get(const crdt_strtab *tab, uint64_t id, const char **p, size_t *len);
+/* Intern the n strings [off_host[i], off_host[i+1]) of a device byte arena:
+ * ids_dev[i] = the string's id (new strings appended).  Synchronises. */
+int crdt_strtab_intern(crdt_ctx *ctx, crdt_strtab *tab, const uint8_t *bytes_dev, const uint64_t *off_host, size_t n,
+                       uint32_t *ids_dev);
+
+/* Gossip pull decoded on the device (§8(f) row 2; main.go:245-256): binary SoA
+ * bodies (crdt_server_gossip_binary) concatenated in HBM become the
+ * crdt_refmerge_in R arrays of one replica each: r_off (0-based entry ranges
+ * per body), r_ts, r_kv (= kv_base + pair offsets), and at
+ * [kv_base, kv_base + pairs) the kv arena's key slots (slot_base[b] + the
+ * key's id in `keys`) and value string ids (ids in `vals`: the merge's string
+ * arena is that table's).  body_status[b] (host): 0 decoded; 1 malformed
+ * (nothing of it is usable, as crdt_server_ingest_binary's outcome 1); 2 valid
+ * but not taken by the device path (a nil map, ts not strictly ascending,
+ * keys of an entry not strictly ascending, a key id >= key_cap): decode that
+ * body on the host; 4 a table was full.  The decoded arrays of a non-zero
+ * body are not valid.  Synchronises (once for the headers, once at the end). */
+typedef struct crdt_gossip_bodies {
+    uint32_t n_bodies;
+    uint32_t key_cap;           /* key ids >= key_cap: status 2 (the replica's slot range is full) */
+    uint64_t kv_base;           /* first kv-arena index of the decoded pairs */
+    const uint8_t *data;        /* device: the bodies, concatenated */
+    const uint64_t *body_off;   /* host [n_bodies+1]: byte ranges of the bodies in data */
+    const uint32_t *slot_base;  /* host [n_bodies]: key slot of key id 0, per body */
+} crdt_gossip_bodies;
+typedef struct crdt_gossip_decoded {
+    uint64_t *r_off;            /* device [n_bodies+1] */
+    int64_t  *r_ts;             /* device [entries] */
+    uint64_t *r_kv;             /* device [entries+1] */
+    uint32_t *kv_key;           /* device, written at [kv_base, kv_base + pairs) */
+    uint32_t *kv_val;
+} crdt_gossip_decoded;
+int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, crdt_strtab *keys, crdt_strtab *vals,
+                       const crdt_gossip_decoded *out, uint32_t *body_status);
+
 /* AliveState handler (main.go:141-151), after strconv.ParseBool. */
 int crdt_server_set_alive(crdt_server *srv, int alive);
 /* Ascending RemoteDiff keys; writes min(cap, len). */

@@ -77,3 +77,27 @@ def merge(diff: dict, remote: dict):
                 continue
             state[key] = str(_wrap64(curr + change))         # main.go:95-96 (Itoa)
     return diff, state
+
+
+def add_command(diff: dict, state: dict, ts: int, data: dict, alive: bool = True) -> int:
+    """AddCommand (main.go:173-215) after the request body's JSON decode:
+    Diff.Put(ts, &data) (main.go:187; a same-ms write replaces the entry),
+    then the local apply to CurrentState (main.go:188-207), keys in sorted
+    order (Go's map order is random: sorted order is one legal execution).
+    Mutates diff and state; returns the HTTP status (200 / 500 / 502)."""
+    if not alive:                                            # main.go:209-212
+        return 502
+    diff[ts] = Command(data)                                 # main.go:187
+    for key in sorted(data):                                 # main.go:188
+        value = data[key]
+        if key not in state:                                 # main.go:189-193: insert, RETURN
+            state[key] = value
+            return 200
+        ok, curr = go_atoi(state[key])                       # main.go:195-199
+        if not ok:
+            return 500
+        ok, change = go_atoi(value)                          # main.go:200-204
+        if not ok:
+            return 500
+        state[key] = str(_wrap64(curr + change))             # main.go:205-206 (Itoa)
+    return 200                                               # main.go:207-208

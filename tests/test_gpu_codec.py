@@ -1,0 +1,153 @@
+"""GPU: the gossip pull decoded on the device (SURVEY §8(f) row 2,
+crdt_gossip_decode) -- binary SoA bodies served by the host mirror
+(crdt_server_gossip_binary, the wire form of Diff.ToJSON, main.go:159) are
+decoded in HBM into RemoteDiff arrays (main.go:245-256).  Checked against
+the host ingest of the same bodies (crdt_server_ingest_binary, itself pinned
+to the JSON codec and its Go encoding/json KATs by tests/test_gossip_json.py)
+and, through whole pull rounds, against the pyref simulation of the
+reference's rounds."""
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+from crdt_amd import codec, gossip
+from crdt_amd.refmerge import Command
+from crdt_amd.server import Server
+from gossip_util import K, KEYS, STRS, _host_round, _pack, _rand_diff, _same_diffs, _state, _unpack
+
+pytestmark = pytest.mark.gpu
+
+
+def _serve(diff) -> bytes:
+    """The binary gossip body of a Diff (host-only Server: main.go:153-170)."""
+    s = Server(None, 8080)
+    for ts, v in diff.items():
+        s.Diff.Put(ts, v)
+    st, body = s.GossipBinary()
+    s.close()
+    assert st == 200
+    return body
+
+
+def _raw_body(entries):
+    """Hand-built binary body: entries = [(ts, [(k, v), ...] or None)] in the
+    given order (None: a nil map)."""
+    ts, pairs, kl, vl, by = [], [], [], [], b""
+    for t, kv in entries:
+        ts.append(t)
+        pairs.append(0xFFFFFFFF if kv is None else len(kv))
+        for k, v in kv or []:
+            kl.append(len(k))
+            vl.append(len(v))
+            by += k + v
+    n = len(kl)
+    return (b"CRDTSOA1" + struct.pack("<QQQ", len(ts), n, len(by)) + struct.pack(f"<{len(ts)}q", *ts) +
+            struct.pack(f"<{len(ts)}I", *pairs) + struct.pack(f"<{n}I", *kl) + struct.pack(f"<{n}I", *vl) + by)
+
+
+def _upload(eng, bodies):
+    off = np.zeros(len(bodies) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in bodies])
+    blob = b"".join(bodies) or b"\0"
+    return torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(eng.device), off.tolist()
+
+
+def _decode(eng, bodies, keys, vals, key_cap=1 << 20, kv_base=3):
+    data, off = _upload(eng, bodies)
+    ne = sum(codec.body_counts(b)[0] for b in bodies)
+    npairs = sum(codec.body_counts(b)[1] for b in bodies)
+    kk = torch.full((kv_base + npairs + 1,), -1, dtype=torch.int32, device=eng.device)
+    kv = torch.full_like(kk, -1)
+    dec, st = codec.decode(eng, data, off, [1000 * i for i in range(len(bodies))], key_cap, keys, vals, kv_base,
+                           kk, kv, ne)
+    return dec, st, kk.cpu().numpy(), kv.cpu().numpy()
+
+
+_ODD = ["", "x", "\xff\x00", "é", "007", "-0", "\n\t\"<>&", "9223372036854775808"]
+
+
+def test_decode_matches_host_ingest(eng):
+    rng = np.random.default_rng(4)
+    diffs = []
+    for b in range(11):
+        d, t = {}, int(rng.integers(-50, 50))
+        for _ in range(int(rng.integers(0, 60))):
+            t += int(rng.integers(1, 9))
+            kv = {f"k{int(q)}".encode() if q % 3 else _ODD[int(q) % len(_ODD)].encode("latin-1"):
+                  (str(int(rng.integers(-30, 30))) if rng.random() < 0.8 else _ODD[int(rng.integers(0, len(_ODD)))])
+                  .encode("latin-1") for q in rng.choice(20, int(rng.integers(0, 5)), replace=False)}
+            d[t] = Command(kv) if rng.random() < 0.5 else kv
+        diffs.append(d)
+    bodies = [_serve(d) for d in diffs]
+    keys, vals = codec.StrTab(eng, 4, 64), codec.StrTab(eng, 4, 64)       # tiny: forces growth + rehash
+    dec, st, kk, kv = _decode(eng, bodies, keys, vals)
+    assert not st.any(), st
+    r_off, r_ts, r_kv = (dec[x].cpu().numpy() for x in ("r_off", "r_ts", "r_kv"))
+    ks, vs = keys.strings(), vals.strings()
+    assert len(set(ks)) == len(ks) and len(set(vs)) == len(vs)          # interned: each string once
+    for b, body in enumerate(bodies):
+        host = Server(None, 9000)
+        assert host.IngestBinary(body) == 0
+        exp_ts = host.RemoteDiff.Keys()
+        got_ts = r_ts[r_off[b]:r_off[b + 1]].tolist()
+        assert got_ts == exp_ts
+        for e, t in zip(range(r_off[b], r_off[b + 1]), exp_ts):
+            got = {}
+            for q in range(r_kv[e], r_kv[e + 1]):
+                got[ks[kk[q] - 1000 * b].decode("utf-8", "surrogateescape")] = \
+                    vs[kv[q]].decode("utf-8", "surrogateescape")
+            assert got == host.RemoteDiff.Get(t)[0]
+        host.close()
+    # a second decode re-uses the interned strings (no new ids for seen strings)
+    n_k, n_v = len(keys), len(vals)
+    _, st2, _, _ = _decode(eng, bodies[:3], keys, vals)
+    assert not st2.any() and (len(keys), len(vals)) == (n_k, n_v)
+
+
+def test_decode_flags(eng):
+    keys, vals = codec.StrTab(eng), codec.StrTab(eng)
+    good = _raw_body([(1, [(b"a", b"1")]), (2, [(b"a", b"2"), (b"b", b"3")])])
+    bodies = [
+        good,
+        good[:-1],                                                   # truncated: malformed (header sizes)
+        _raw_body([(1, [(b"a", b"1")]), (5, None)]),                 # nil map: host path (keeps the nil flag)
+        _raw_body([(3, [(b"a", b"1")]), (2, [(b"a", b"1")])]),       # ts not ascending: host path
+        _raw_body([(1, [(b"b", b"1"), (b"a", b"2")])]),              # keys not ascending: host path
+        _raw_body([(1, [(b"a", b"1"), (b"a", b"2")])]),              # duplicate key: host path
+    ]
+    bad_count = bytearray(good)
+    struct.pack_into("<I", bad_count, 32 + 16, 5)                    # pairs[0] = 5 != header n_pairs
+    bodies.append(bytes(bad_count))
+    _, st, _, _ = _decode(eng, bodies, keys, vals)
+    assert st.tolist() == [0, 1, 2, 2, 2, 2, 1], st
+    # a key id past the replica's slot range takes the host path
+    k2, v2 = codec.StrTab(eng), codec.StrTab(eng)
+    _, st, _, _ = _decode(eng, [_raw_body([(1, [(b"a", b"1"), (b"b", b"1"), (b"c", b"1")])])], k2, v2, key_cap=2)
+    assert st.tolist() == [2]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_wire_rounds_match_reference_simulation(eng, seed):
+    """Pull rounds whose pulls arrive as binary bodies (decoded on the device,
+    Population.round_wire) == the pyref simulation of the reference's
+    rounds (main.go:226-258)."""
+    rng = np.random.default_rng(seed)
+    P = 7
+    diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 40))) for i in range(P)]
+    pop = gossip.Population(eng, _pack(diffs), K)
+    keys, vals = codec.StrTab(eng), codec.StrTab(eng)
+    assert keys.intern(KEYS).tolist() == list(range(K))                  # key id = KEYS index
+    assert vals.intern(STRS).tolist() == list(range(len(STRS)))          # string id = STRS index
+    for rnd in range(5):
+        peers = gossip.random_peers(rng, P, 0, P)
+        bodies = [_serve(diffs[q]) for q in peers]
+        data, off = _upload(eng, bodies)
+        ne = sum(codec.body_counts(b)[0] for b in bodies)
+        npairs = sum(codec.body_counts(b)[1] for b in bodies)
+        pop.round_wire(data, off, keys, vals, ne, npairs)
+        diffs, states = _host_round(diffs, peers)
+        _same_diffs(_unpack(pop), diffs)
+        assert _state(pop) == states, f"round {rnd}"
+    assert len(keys) == K and len(vals) == len(STRS)                     # nothing new was interned
