@@ -685,6 +685,68 @@ class GossipRound(Workload):
                           f"threads, {dt:.1f}s"}
 
 
+class GossipRoundWire(GossipRound):
+    """The anti-entropy round with its pulls ON THE WIRE (SURVEY §8(f) rows 2
+    and 4): every replica's pull arrives as the binary gossip body of a
+    random peer's Diff (crdt_server_gossip_binary's format, the wire form of
+    Diff.ToJSON, main.go:159), already in HBM; a step decodes all bodies on
+    the device (crdt_gossip_decode: keys and values interned into device
+    string tables, main.go:245-256), merges every replica in one batched call
+    and materialises the next Diffs.  Each step restarts from the same
+    population and the same bodies."""
+    name = "gossip_round_wire"
+    kernel = "gossip round from wire bodies (crdt_gossip_decode + refmerge + Diff materialisation)"
+
+    def __init__(self, eng, rank, world, replicas, entries, seed=2024):
+        from crdt_amd import codec, gossip, synth
+        h = synth.refmerge_packed(seed + rank, replicas, entries)
+        n_l = len(h["l_ts"])
+        host = {"replicas": replicas, "l_off": h["l_off"], "l_ts": h["l_ts"], "l_origin": h["l_origin"],
+                "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
+                "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
+        self.pop = gossip.Population(eng, host, 62)
+        self.host, self.P, self.n_l, self.gossip = h, replicas, n_l, gossip
+        names = [c.encode() for c in synth.ALPHABET]
+        self.keys, self.vals = codec.StrTab(eng), codec.StrTab(eng)
+        self.keys.intern(names)                                   # key id = alphabet index (slot p*62 + k)
+        strs = [bytes(h["str_bytes"][h["str_off"][i]:h["str_off"][i + 1]]) for i in range(len(h["str_off"]) - 1)]
+        self.vals.intern(strs)                                    # string ids = the packed batch's
+        blob, boff = codec.encode_packed_diffs(host, names, 62)
+        self.rng = np.random.default_rng(seed)
+        self.peers = gossip.random_peers(self.rng, replicas, 0, replicas)
+        bodies = [blob[boff[q]:boff[q + 1]] for q in self.peers]       # replica i pulls peers[i]
+        self.body_off = np.zeros(replicas + 1, np.int64)
+        self.body_off[1:] = np.cumsum([len(b) for b in bodies])
+        self.body_bytes = int(self.body_off[-1])
+        self.data = torch.frombuffer(bytearray(b"".join(bodies)), dtype=torch.uint8).to(eng.device)
+        self.n_e = sum(codec.body_counts(b)[0] for b in bodies)
+        self.n_p = sum(codec.body_counts(b)[1] for b in bodies)
+        self.init = self.pop.snapshot()
+        self.str0 = (self.pop.str_bytes, self.pop.str_off)
+        out = self.step()
+        torch.cuda.synchronize()
+        self.n_out = int(out["off"][-1].item())
+        self.config = {"workload": f"gossip round from the wire: {replicas} replicas x {entries} Diff entries each "
+                                   "pull a random peer's Diff as a binary gossip body in HBM, device decode + "
+                                   "batched merge (BASELINE configs[0] shape at scale)",
+                       "replicas": replicas, "entries": entries, "body_bytes": self.body_bytes,
+                       "n_new_diff": self.n_out, "parallelism": f"replicas x{world}"}
+
+    def units(self):
+        return self.n_e                      # every pulled entry
+
+    def bytes_per_launch(self):
+        # the bodies read once, R written (ts, kv range, kv pair), the merge
+        # (inputs + outputs once), the next Diff's kv gather
+        n_r, n_out = self.n_e, self.n_out
+        return self.body_bytes + n_r * 24 + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
+
+    def step(self):
+        self.pop.restore(self.init)
+        self.pop.str_bytes, self.pop.str_off = self.str0
+        return self.pop.round_wire(self.data, self.body_off.tolist(), self.keys, self.vals, self.n_e, self.n_p)
+
+
 class ServerMerge(Workload):
     """The path a Go caller of merge() actually hits (main.go:245-257):
     configs[0]'s 5 replicas x 10k Diff entries (main.go:319-321), each
@@ -779,6 +841,8 @@ class ServerMerge(Workload):
 def make_workload(name, eng, rank, world, args):
     if name == "gossip_round":
         return GossipRound(eng, rank, world, args.replicas, args.entries)
+    if name == "gossip_round_wire":
+        return GossipRoundWire(eng, rank, world, args.replicas, args.entries)
     if name == "server_merge":
         return ServerMerge(eng, rank, world, args.demo_replicas, args.demo_entries)
     if name == "refmerge":
@@ -823,7 +887,7 @@ def main():
     ap.add_argument("--workload", default="shard_fold",
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
                              "lww_merge_d2", "orset_merge_d2", "shard_fold", "shard_join", "refmerge",
-                             "refmerge_delta", "gossip_round", "server_merge"])
+                             "refmerge_delta", "gossip_round", "gossip_round_wire", "server_merge"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)

@@ -123,3 +123,47 @@ def decode(eng, data: torch.Tensor, body_off: Sequence[int], slot_base: Sequence
     call("crdt_gossip_decode", eng.ctx, C.byref(gb), keys._h, vals._h, C.byref(go), st, ctx=eng.ctx)
     out["r_ts"] = out["r_ts"][:n_entries]
     return out, np.array(st[:nb], dtype=np.uint32)
+
+
+def encode_packed_diffs(h: dict, key_names: Sequence[bytes], slots_per_replica: int):
+    """Binary gossip bodies (crdt_server_gossip_binary's format) of every
+    replica's Diff in a packed batch (crdt_amd.synth.refmerge_packed layout:
+    one kv per entry, key slot p * slots_per_replica + k -> key_names[k]),
+    vectorised.  Returns (blob, offsets) with body p = blob[off[p]:off[p+1]]."""
+    P = h["replicas"]
+    l_off = np.asarray(h["l_off"], np.int64)
+    ts = np.asarray(h["l_ts"], np.int64)
+    kv_key = np.asarray(h["kv_key"]).view(np.uint32).astype(np.int64)[: len(ts)]
+    kv_val = np.asarray(h["kv_val"]).view(np.uint32).astype(np.int64)[: len(ts)]
+    if not np.array_equal(np.asarray(h["l_kv"], np.int64), np.arange(len(ts) + 1)):
+        raise ValueError("one kv per entry expected")
+    sb = np.asarray(h["str_bytes"], np.uint8)
+    so = np.asarray(h["str_off"], np.int64)
+    names = [bytes(k) for k in key_names]
+    if any(len(k) != 1 for k in names):
+        raise ValueError("single-byte key names expected (the reference's alphabet, main.go:274)")
+    kbyte = np.frombuffer(b"".join(names), np.uint8)
+    rep = np.repeat(np.arange(P, dtype=np.int64), np.diff(l_off))
+    kidx = kv_key - rep * slots_per_replica
+    vlen = (so[kv_val + 1] - so[kv_val]).astype(np.int64)
+    rec = 1 + vlen                                        # key byte + value bytes per entry
+    rec_off = np.zeros(len(ts) + 1, np.int64)
+    rec_off[1:] = np.cumsum(rec)
+    data = np.empty(int(rec_off[-1]), np.uint8)
+    data[rec_off[:-1]] = kbyte[kidx]
+    # value bytes: for byte t of entry e, source so[v_e] + t, destination rec_off[e] + 1 + t
+    e_of = np.repeat(np.arange(len(ts)), vlen)
+    within = np.arange(int(vlen.sum())) - np.repeat(np.cumsum(vlen) - vlen, vlen)
+    data[rec_off[e_of] + 1 + within] = sb[so[kv_val[e_of]] + within]
+    bodies = []
+    for p in range(P):
+        a, b = int(l_off[p]), int(l_off[p + 1])
+        ne = b - a
+        nby = int(rec_off[b] - rec_off[a])
+        hdr = MAGIC + struct.pack("<QQQ", ne, ne, nby)
+        bodies.append(hdr + ts[a:b].astype("<i8").tobytes() + np.ones(ne, "<u4").tobytes() +
+                      np.ones(ne, "<u4").tobytes() + vlen[a:b].astype("<u4").tobytes() +
+                      data[rec_off[a]:rec_off[b]].tobytes())
+    off = np.zeros(P + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in bodies])
+    return b"".join(bodies), off

@@ -48,6 +48,8 @@ constexpr uint64_t kEmptyE = ~0ull;
 constexpr uint32_t kPend = 0x80000000u;
 constexpr uint32_t kIdMask = 0x7FFFFFFFu;
 constexpr uint32_t kNilPairs = 0xFFFFFFFFu;
+constexpr uint32_t kEmptyE32 = 0xFFFFFFFFu;  // a pair's slot record: resolved in pass A
+constexpr uint32_t kRepBit = 0x80000000u;    // the pair claimed the entry (tables < 2^31 entries)
 
 enum : uint32_t {
     kBodyMalformed = 1u,          // sizes / counts inconsistent: nothing of the body is usable
@@ -92,17 +94,21 @@ struct TabView {
 // Returns the entry index (kEmptyE as uint64 on a full table); *rep = claimed.
 template <class Get>
 __device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, uint32_t len, uint32_t self,
-                              const Get &get, bool *rep) {
+                              const Get &get, bool *rep, uint64_t *ent) {
     *rep = false;
     uint64_t i = h & t.mask;
     for (uint64_t probe = 0; probe <= t.mask; ++probe, i = (i + 1) & t.mask) {
-        uint64_t e = __hip_atomic_load(&t.tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a plain load first: ids from earlier calls never change inside a
+        // pass; an entry it shows empty may have been claimed meanwhile (the
+        // CAS then returns the claim)
+        uint64_t e = t.tab[i];
         if (e == kEmptyE) {
             const uint64_t want = (uint64_t)h << 32 | kPend | self;
             const uint64_t old = atomicCAS((unsigned long long *)&t.tab[i], (unsigned long long)kEmptyE,
                                            (unsigned long long)want);
             if (old == kEmptyE) {
                 *rep = true;
+                *ent = want;
                 return i;
             }
             e = old;
@@ -118,7 +124,10 @@ __device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, ui
             q = t.bytes + t.off[id];
             qn = (uint32_t)(t.off[id + 1] - t.off[id]);
         }
-        if (qn == len && bytes_eq(q, s, len)) return i;
+        if (qn == len && bytes_eq(q, s, len)) {
+            *ent = e;
+            return i;
+        }
     }
     return kEmptyE;
 }
@@ -171,41 +180,46 @@ struct DecodeCtx {
     }
 };
 
+constexpr uint32_t kChunk = 1024;  // items per workgroup of the body-major grids (grid.y = body)
+
 // per entry: ts, pair count; ts must ascend strictly within a body, no nil map
-__global__ void k_dec_entries(DecodeCtx c, uint64_t n_e, int64_t *__restrict__ r_ts, uint32_t *__restrict__ cnt) {
-    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n_e; e += (uint64_t)gridDim.x * 256) {
-        const uint32_t b = find_body(c.bd, c.nbody, e, false);
-        const BodyDesc d = c.bd[b];
-        const uint64_t i = e - d.e0;
-        const uint8_t *base = c.data + d.data + 32;
+__global__ __launch_bounds__(256) void k_dec_entries(DecodeCtx c, int64_t *__restrict__ r_ts,
+                                                     uint32_t *__restrict__ cnt) {
+    const uint32_t b = blockIdx.y;
+    const BodyDesc d = c.bd[b];
+    const uint8_t *base = c.data + d.data + 32;
+    bool host = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * kChunk + threadIdx.x; i < d.ne && i < (uint64_t)(blockIdx.x + 1) * kChunk;
+         i += 256) {
         const int64_t ts = (int64_t)le64(base + 8 * i);
         uint32_t k = le32(base + 8 * d.ne + 4 * i);
         if (k == kNilPairs) {                             // a nil map: the host path keeps its flag
-            atomicOr(&c.flag[b], kBodyHost);
+            host = true;
             k = 0;
         }
-        if (i && (int64_t)le64(base + 8 * (i - 1)) >= ts) atomicOr(&c.flag[b], kBodyHost);
-        r_ts[e] = ts;
-        cnt[e] = k;
+        if (i && (int64_t)le64(base + 8 * (i - 1)) >= ts) host = true;
+        r_ts[d.e0 + i] = ts;
+        cnt[d.e0 + i] = k;
     }
+    if (__any(host) && (threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(host)) - 1)
+        atomicOr(&c.flag[b], kBodyHost);
 }
 
-struct PairLenSrc {                // scan source: klen + vlen of pair j (also records klen)
-    DecodeCtx c;
-    uint32_t *klen_out;
-    struct Item {
-        uint64_t len = 0;
-    };
-    __device__ Item load(uint64_t j) const {
-        const uint32_t b = find_body(c.bd, c.nbody, j, true);
-        const BodyDesc d = c.bd[b];
-        const uint64_t q = j - d.q0;
-        const uint8_t *base = c.data + d.data + 32 + 12 * d.ne;
+// per pair: klen and klen + vlen (u32; an overflow marks the body malformed)
+__global__ __launch_bounds__(256) void k_dec_pairs(DecodeCtx c, uint32_t *__restrict__ klen,
+                                                   uint32_t *__restrict__ plen) {
+    const uint32_t b = blockIdx.y;
+    const BodyDesc d = c.bd[b];
+    const uint8_t *base = c.data + d.data + 32 + 12 * d.ne;
+    for (uint64_t q = (uint64_t)blockIdx.x * kChunk + threadIdx.x; q < d.np && q < (uint64_t)(blockIdx.x + 1) * kChunk;
+         q += 256) {
         const uint32_t kl = le32(base + 4 * q), vl = le32(base + 4 * d.np + 4 * q);
-        klen_out[j] = kl;
-        return Item{(uint64_t)kl + vl};
+        const uint64_t t = (uint64_t)kl + vl;
+        if (t > 0xFFFFFFFFull) atomicOr(&c.flag[b], kBodyMalformed);
+        klen[d.q0 + q] = kl;
+        plen[d.q0 + q] = t > 0xFFFFFFFFull ? 0u : (uint32_t)t;
     }
-};
+}
 
 struct CountSrc32 {
     const uint32_t *in;
@@ -248,44 +262,97 @@ struct PendGet {                   // bytes of pending reference j (key or value
     }
 };
 
-// pass A over both tables; key order check within an entry
-__global__ void k_dec_claim(DecodeCtx c, TabView kt, TabView vt, const uint8_t *__restrict__ first,
-                            uint64_t *__restrict__ kslot, uint64_t *__restrict__ vslot, uint32_t *__restrict__ krep,
-                            uint32_t *__restrict__ vrep, uint32_t *__restrict__ kh, uint32_t *__restrict__ vh) {
-    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < c.n_pairs; j += (uint64_t)gridDim.x * 256) {
-        const uint8_t *kp, *vp;
-        uint32_t kn, vn;
-        c.pair_bytes(j, &kp, &kn, &vp, &vn);
-        const uint32_t b = find_body(c.bd, c.nbody, j, true);
-        if (j && !first[j] && j > c.bd[b].q0) {
-            const uint8_t *pkp, *pvp;
-            uint32_t pkn, pvn;
-            c.pair_bytes(j - 1, &pkp, &pkn, &pvp, &pvn);
-            if (!bytes_lt(pkp, pkn, kp, kn)) atomicOr(&c.flag[b], kBodyHost);   // served bodies sort keys
+// pass A over both tables, body-major.  A pair whose string is already in a
+// table (an id from an earlier call) gets its ids written at once; the
+// others record their entry (bit 31: this pair claimed it) for passes B / C
+// and count the claims (ctr[0] keys, ctr[1] values).  kEmptyE slots: done.
+__global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
+                                                   const uint8_t *__restrict__ first, uint32_t key_cap,
+                                                   uint64_t kv_base, uint32_t *__restrict__ kslot,
+                                                   uint32_t *__restrict__ vslot, uint32_t *__restrict__ kv_key,
+                                                   uint32_t *__restrict__ kv_val, unsigned long long *__restrict__ ctr) {
+    const uint32_t b = blockIdx.y;
+    const BodyDesc d = c.bd[b];
+    const uint8_t *region = c.data + d.data + 32 + 12 * d.ne + 8 * d.np;
+    const uint64_t o0 = c.boff[d.q0];
+    bool host = false, bad = false, full = false;
+    uint32_t nk = 0, nv = 0;
+    for (uint64_t q = (uint64_t)blockIdx.x * kChunk + threadIdx.x; q < d.np && q < (uint64_t)(blockIdx.x + 1) * kChunk;
+         q += 256) {
+        const uint64_t j = d.q0 + q;
+        const uint64_t o = c.boff[j] - o0, k = c.klen[j], v = c.boff[j + 1] - c.boff[j] - k;
+        uint32_t ks = kEmptyE32, vs = kEmptyE32;
+        if (o > d.nb || k > d.nb - o || v > d.nb - o - k) {
+            bad = true;
+        } else {
+            const uint8_t *kp = region + o, *vp = region + o + k;
+            if (q && !first[j]) {                            // keys of an entry strictly ascending
+                const uint64_t po = c.boff[j - 1] - o0, pk = c.klen[j - 1];
+                if (po + pk <= o && !bytes_lt(region + po, (uint32_t)pk, kp, (uint32_t)k)) host = true;
+            }
+            bool r;
+            uint64_t e;
+            const uint64_t si = tab_claim(kt, hash32(kp, (uint32_t)k), kp, (uint32_t)k, (uint32_t)j,
+                                          PendGet{c, false}, &r, &e);
+            if (si == kEmptyE) {
+                full = true;
+            } else {
+                if (!r && !((uint32_t)e & kPend)) {          // an existing id
+                    const uint32_t kid = (uint32_t)e & kIdMask;
+                    if (kid >= key_cap) host = true;
+                    kv_key[kv_base + j] = d.slot_base + kid;
+                } else {
+                    ks = (uint32_t)si | (r ? kRepBit : 0u);
+                    nk += r;
+                }
+            }
+            const uint64_t sv = tab_claim(vt, hash32(vp, (uint32_t)v), vp, (uint32_t)v, (uint32_t)j,
+                                          PendGet{c, true}, &r, &e);
+            if (sv == kEmptyE) {
+                full = true;
+            } else {
+                if (!r && !((uint32_t)e & kPend)) {
+                    kv_val[kv_base + j] = (uint32_t)e & kIdMask;
+                } else {
+                    vs = (uint32_t)sv | (r ? kRepBit : 0u);
+                    nv += r;
+                }
+            }
         }
-        bool r;
-        const uint32_t h1 = hash32(kp, kn), h2 = hash32(vp, vn);
-        const uint64_t si = tab_claim(kt, h1, kp, kn, (uint32_t)j, PendGet{c, false}, &r);
-        krep[j] = r ? 1u : 0u;
-        const uint64_t sv = tab_claim(vt, h2, vp, vn, (uint32_t)j, PendGet{c, true}, &r);
-        vrep[j] = r ? 1u : 0u;
-        if (si == kEmptyE || sv == kEmptyE) atomicOr(&c.flag[b], kBodyFull);
-        kslot[j] = si;
-        vslot[j] = sv;
-        kh[j] = h1;
-        vh[j] = h2;
+        kslot[j] = ks;
+        vslot[j] = vs;
+    }
+    const uint32_t fl = (bad ? kBodyMalformed : 0u) | (host ? kBodyHost : 0u) | (full ? kBodyFull : 0u);
+    for (int m = 32; m >= 1; m >>= 1) {
+        nk += __shfl_xor(nk, m, 64);
+        nv += __shfl_xor(nv, m, 64);
+    }
+    uint32_t wfl = fl;
+    for (int m = 32; m >= 1; m >>= 1) wfl |= __shfl_xor(wfl, m, 64);
+    if ((threadIdx.x & 63) == 0) {
+        if (wfl) atomicOr(&c.flag[b], wfl);
+        if (nk) atomicAdd(&ctr[0], (unsigned long long)nk);
+        if (nv) atomicAdd(&ctr[1], (unsigned long long)nv);
     }
 }
 
+struct RepCntSrc {                 // scan source: 1 for a claimer
+    const uint32_t *slot;
+    struct Item {
+        uint64_t len = 0;
+    };
+    __device__ Item load(uint64_t j) const { return Item{(slot[j] != kEmptyE32 && (slot[j] & kRepBit)) ? 1u : 0u}; }
+};
+
 struct RepLenSrc {                 // scan source: bytes of the claimers' strings
     DecodeCtx c;
-    const uint32_t *rep;
+    const uint32_t *slot;
     bool value;
     struct Item {
         uint64_t len = 0;
     };
     __device__ Item load(uint64_t j) const {
-        if (!rep[j]) return Item{0};
+        if (slot[j] == kEmptyE32 || !(slot[j] & kRepBit)) return Item{0};
         const uint8_t *kp, *vp;
         uint32_t kn, vn;
         c.pair_bytes(j, &kp, &kn, &vp, &vn);
@@ -294,12 +361,12 @@ struct RepLenSrc {                 // scan source: bytes of the claimers' string
 };
 
 // pass B: claimers -> dense ids, bytes into the arena, entry -> id
-__global__ void k_dec_assign(DecodeCtx c, TabView t, bool value, const uint32_t *__restrict__ rep,
-                             const uint64_t *__restrict__ rank, const uint64_t *__restrict__ rboff,
-                             const uint64_t *__restrict__ slot, const uint32_t *__restrict__ hsh, uint64_t n_old,
+__global__ void k_dec_assign(DecodeCtx c, TabView t, bool value, const uint32_t *__restrict__ slot,
+                             const uint64_t *__restrict__ rank, const uint64_t *__restrict__ rboff, uint64_t n_old,
                              uint64_t bytes_old, uint8_t *__restrict__ arena, uint64_t *__restrict__ off) {
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < c.n_pairs; j += (uint64_t)gridDim.x * 256) {
-        if (!rep[j] || slot[j] == kEmptyE) continue;
+        const uint32_t sl = slot[j];
+        if (sl == kEmptyE32 || !(sl & kRepBit)) continue;
         const uint8_t *kp, *vp;
         uint32_t kn, vn;
         c.pair_bytes(j, &kp, &kn, &vp, &vn);
@@ -309,7 +376,8 @@ __global__ void k_dec_assign(DecodeCtx c, TabView t, bool value, const uint32_t 
         const uint64_t o = bytes_old + rboff[j];
         for (uint32_t i = 0; i < n; ++i) arena[o + i] = p[i];
         off[id] = o;
-        t.tab[slot[j]] = (uint64_t)hsh[j] << 32 | (uint32_t)id;
+        const uint64_t si = sl & ~kRepBit;
+        t.tab[si] = (t.tab[si] & 0xFFFFFFFF00000000ull) | (uint32_t)id;   // keep the hash, drop the pending tag
     }
 }
 
@@ -318,18 +386,19 @@ __global__ void k_off_end(uint64_t *__restrict__ off, const uint64_t *__restrict
     off[n_old + *n_new_dev] = bytes_old + *bytes_new_dev;
 }
 
-// pass C: ids into the kv arrays (key ids re-based to the body's slot range)
-__global__ void k_dec_ids(DecodeCtx c, const uint64_t *__restrict__ kslot, const uint64_t *__restrict__ vslot,
+// pass C: ids of the pairs whose string was new in this call
+__global__ void k_dec_ids(DecodeCtx c, const uint32_t *__restrict__ kslot, const uint32_t *__restrict__ vslot,
                           const uint64_t *__restrict__ ktab, const uint64_t *__restrict__ vtab, uint32_t key_cap,
                           uint64_t kv_base, uint32_t *__restrict__ kv_key, uint32_t *__restrict__ kv_val) {
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < c.n_pairs; j += (uint64_t)gridDim.x * 256) {
-        const uint32_t b = find_body(c.bd, c.nbody, j, true);
-        if (kslot[j] == kEmptyE || vslot[j] == kEmptyE) continue;
-        const uint32_t kid = (uint32_t)ktab[kslot[j]] & kIdMask;
-        const uint32_t vid = (uint32_t)vtab[vslot[j]] & kIdMask;
-        if (kid >= key_cap) atomicOr(&c.flag[b], kBodyHost);   // key beyond the replica's slot range
-        kv_key[kv_base + j] = c.bd[b].slot_base + kid;
-        kv_val[kv_base + j] = vid;
+        const uint32_t ks = kslot[j], vs = vslot[j];
+        if (ks != kEmptyE32) {
+            const uint32_t b = find_body(c.bd, c.nbody, j, true);
+            const uint32_t kid = (uint32_t)ktab[ks & ~kRepBit] & kIdMask;
+            if (kid >= key_cap) atomicOr(&c.flag[b], kBodyHost);   // key beyond the replica's slot range
+            kv_key[kv_base + j] = c.bd[b].slot_base + kid;
+        }
+        if (vs != kEmptyE32) kv_val[kv_base + j] = (uint32_t)vtab[vs & ~kRepBit] & kIdMask;
     }
 }
 
@@ -346,6 +415,15 @@ __global__ void k_rehash(uint64_t *__restrict__ tab, uint64_t mask, const uint8_
             i = (i + 1) & mask;
         }
     }
+}
+
+// hdr[32 b ..] = the first 32 bytes of body b (zeros if shorter)
+__global__ void k_gather_headers(const uint8_t *__restrict__ data, const uint64_t *__restrict__ off, uint32_t nb,
+                                 uint8_t *__restrict__ hdr) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= nb) return;
+    const bool ok = off[b + 1] - off[b] >= 32;
+    for (int i = 0; i < 32; ++i) hdr[32 * (size_t)b + i] = ok ? data[off[b] + i] : 0;
 }
 
 uint64_t pow2_at_least(uint64_t x) {
@@ -497,16 +575,27 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     if (nb == 0) return CRDT_OK;
     if (!in->data || !in->body_off || !in->slot_base || !out->r_off) return CRDT_E_INVAL;
     const hipStream_t s = ctx->stream;
-    // headers (32 B per body) to the host: the sizes the decode is planned with
-    std::vector<uint8_t> hdr(32 * (size_t)nb, 0);
-    hipError_t e = hipSuccess;
-    for (uint32_t b = 0; b < nb && e == hipSuccess; ++b) {
-        const uint64_t len = in->body_off[b + 1] - in->body_off[b];
+    // headers (32 B per body) to the host in one gather + one copy: the sizes
+    // the decode is planned with
+    for (uint32_t b = 0; b < nb; ++b)
         if (in->body_off[b + 1] < in->body_off[b]) return CRDT_E_INVAL;
-        if (len >= 32) e = hipMemcpyAsync(&hdr[32 * b], in->data + in->body_off[b], 32, hipMemcpyDeviceToHost, s);
+    std::vector<uint8_t> hdr(32 * (size_t)nb, 0);
+    rc = ws_reserve(ctx, Carve::round((nb + 1) * 8) + Carve::round(32 * (size_t)nb) + 512);
+    if (rc) return rc;
+    hipError_t e;
+    {
+        Carve w0(ctx->ws);
+        uint64_t *d_off = w0.take<uint64_t>(nb + 1);
+        uint8_t *d_hdr = w0.take<uint8_t>(32 * (size_t)nb);
+        e = hipMemcpyAsync(d_off, in->body_off, (nb + 1) * 8, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        k_gather_headers<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(in->data, d_off, nb, d_hdr);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+        e = hipMemcpyAsync(hdr.data(), d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(ctx, e);
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
     std::vector<BodyDesc> bd(nb);
     std::vector<uint64_t> r_off(nb + 1, 0);
     uint64_t n_e = 0, n_p = 0, n_b = 0;
@@ -539,9 +628,8 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     if (rc) return rc;
     // workspace
     const size_t need = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 4) + Carve::round((n_e + 1) * 4) +
-                        Carve::round((n_e + 1) * 8) + Carve::round(n_p * 4 + 4) + Carve::round((n_p + 1) * 8) * 7 +
-                        Carve::round(n_p + 1) + Carve::round(n_p * 4 + 4) * 4 + 4 * scan_lb_tmp_bytes(n_p + n_e) +
-                        Carve::round(64) + 4096;
+                        Carve::round((n_e + 1) * 8) + Carve::round(n_p * 4 + 4) * 4 + Carve::round((n_p + 1) * 8) * 5 +
+                        Carve::round(n_p + 1) + scan_lb_tmp_bytes(std::max(n_p, n_e)) + Carve::round(64) + 4096;
     rc = ws_reserve(ctx, need);
     if (rc) return rc;
     Carve w(ctx->ws);
@@ -550,29 +638,34 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     uint32_t *cnt = w.take<uint32_t>(n_e + 1);
     uint64_t *pre = w.take<uint64_t>(n_e + 1);
     uint32_t *klen = w.take<uint32_t>(n_p + 1);
+    uint32_t *plen = w.take<uint32_t>(n_p + 1);
+    uint32_t *kslot = w.take<uint32_t>(n_p + 1);
+    uint32_t *vslot = w.take<uint32_t>(n_p + 1);
     uint64_t *boff = w.take<uint64_t>(n_p + 1);
-    uint64_t *kslot = w.take<uint64_t>(n_p + 1);
-    uint64_t *vslot = w.take<uint64_t>(n_p + 1);
     uint64_t *krank = w.take<uint64_t>(n_p + 1);
     uint64_t *vrank = w.take<uint64_t>(n_p + 1);
     uint64_t *kboff = w.take<uint64_t>(n_p + 1);
     uint64_t *vboff = w.take<uint64_t>(n_p + 1);
     uint8_t *first = w.take<uint8_t>(n_p + 1);
-    uint32_t *krep = w.take<uint32_t>(n_p + 1);
-    uint32_t *vrep = w.take<uint32_t>(n_p + 1);
-    uint32_t *kh = w.take<uint32_t>(n_p + 1);
-    uint32_t *vh = w.take<uint32_t>(n_p + 1);
-    void *tmp = w.take<char>(scan_lb_tmp_bytes(n_p + n_e));
+    unsigned long long *ctr = w.take<unsigned long long>(8);
+    void *tmp = w.take<char>(scan_lb_tmp_bytes(std::max(n_p, n_e)));
     e = hipMemcpyAsync(d_bd, bd.data(), nb * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, nb * 4, s);
     if (e == hipSuccess) e = hipMemsetAsync(first, 0, n_p + 1, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(out->r_off, r_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, 64, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out->r_off, r_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     DecodeCtx c{in->data, d_bd, nb, d_flag, boff, klen, n_p};
+    uint64_t max_ne = 0, max_np = 0;
+    for (auto &x : bd) {
+        max_ne = std::max(max_ne, x.ne);
+        max_np = std::max(max_np, x.np);
+    }
+    const dim3 ge((unsigned)std::max<uint64_t>((max_ne + kChunk - 1) / kChunk, 1), nb);
+    const dim3 gp((unsigned)std::max<uint64_t>((max_np + kChunk - 1) / kChunk, 1), nb);
     const unsigned cap = (unsigned)ctx->num_cus * 8;
     if (n_e) {
-        k_dec_entries<<<grid_for(n_e, 256, cap), 256, 0, s>>>(c, n_e, out->r_ts, cnt);
+        k_dec_entries<<<ge, 256, 0, s>>>(c, out->r_ts, cnt);
         rc = check_launch(ctx);
         if (!rc) rc = scan_lb(ctx, CountSrc32{cnt}, NoAct(), n_e, 0, pre, tmp);
         if (rc) return rc;
@@ -580,55 +673,77 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
         e = hipMemsetAsync(pre, 0, 8, s);
         if (e != hipSuccess) return hip_fail(ctx, e);
     }
-    rc = scan_lb(ctx, PairLenSrc{c, klen}, NoAct(), n_p, 0, boff, tmp);
+    if (n_p) {
+        k_dec_pairs<<<gp, 256, 0, s>>>(c, klen, plen);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+    }
+    rc = scan_lb(ctx, CountSrc32{plen}, NoAct(), n_p, 0, boff, tmp);
     if (rc) return rc;
     k_dec_bodies<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(c, pre);
     k_dec_kv<<<grid_for(n_e + 1, 256, cap), 256, 0, s>>>(pre, n_e, n_p, in->kv_base, out->r_kv, first);
     rc = check_launch(ctx);
     if (rc) return rc;
     const uint64_t kn0 = keys->n, kb0 = keys->nbytes, vn0 = vals->n, vb0 = vals->nbytes;
-    // counters: [0] new keys, [1] new key bytes, [2] new values, [3] new value bytes
-    uint64_t *ctr = w.take<uint64_t>(8);
+    TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
+    TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
-        TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
-        TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
-        k_dec_claim<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kt, vt, first, kslot, vslot, krep, vrep, kh, vh);
+        k_dec_claim<<<gp, 256, 0, s>>>(c, kt, vt, first, in->key_cap, in->kv_base, kslot, vslot, out->kv_key,
+                                       out->kv_val, ctr);
         rc = check_launch(ctx);
-        if (!rc) rc = scan_lb(ctx, CountSrc32{krep}, NoAct(), n_p, 0, krank, tmp);
-        if (!rc) rc = scan_lb(ctx, CountSrc32{vrep}, NoAct(), n_p, 0, vrank, tmp);
-        if (!rc) rc = scan_lb(ctx, RepLenSrc{c, krep, false}, NoAct(), n_p, 0, kboff, tmp);
-        if (!rc) rc = scan_lb(ctx, RepLenSrc{c, vrep, true}, NoAct(), n_p, 0, vboff, tmp);
         if (rc) return rc;
-        k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kt, false, krep, krank, kboff, kslot, kh, kn0, kb0,
-                                                            keys->bytes, keys->off);
-        k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, vt, true, vrep, vrank, vboff, vslot, vh, vn0, vb0,
-                                                            vals->bytes, vals->off);
-        k_off_end<<<1, 1, 0, s>>>(keys->off, krank + n_p, kboff + n_p, kn0, kb0);
-        k_off_end<<<1, 1, 0, s>>>(vals->off, vrank + n_p, vboff + n_p, vn0, vb0);
+    }
+    // claims and flags to the host: the id passes run only when new strings arrived
+    uint64_t h_ctr[8];
+    std::vector<uint32_t> flags(nb);
+    e = hipMemcpyAsync(h_ctr, ctr, 64, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    uint64_t new_k = 0, new_kb = 0, new_v = 0, new_vb = 0;
+    if (h_ctr[0] || h_ctr[1]) {
+        if (h_ctr[0]) {
+            rc = scan_lb(ctx, RepCntSrc{kslot}, NoAct(), n_p, 0, krank, tmp);
+            if (!rc) rc = scan_lb(ctx, RepLenSrc{c, kslot, false}, NoAct(), n_p, 0, kboff, tmp);
+            if (rc) return rc;
+            k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kt, false, kslot, krank, kboff, kn0, kb0,
+                                                                keys->bytes, keys->off);
+            k_off_end<<<1, 1, 0, s>>>(keys->off, krank + n_p, kboff + n_p, kn0, kb0);
+        }
+        if (h_ctr[1]) {
+            rc = scan_lb(ctx, RepCntSrc{vslot}, NoAct(), n_p, 0, vrank, tmp);
+            if (!rc) rc = scan_lb(ctx, RepLenSrc{c, vslot, true}, NoAct(), n_p, 0, vboff, tmp);
+            if (rc) return rc;
+            k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, vt, true, vslot, vrank, vboff, vn0, vb0,
+                                                                vals->bytes, vals->off);
+            k_off_end<<<1, 1, 0, s>>>(vals->off, vrank + n_p, vboff + n_p, vn0, vb0);
+        }
         k_dec_ids<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kslot, vslot, keys->tab, vals->tab, in->key_cap,
                                                          in->kv_base, out->kv_key, out->kv_val);
         rc = check_launch(ctx);
         if (rc) return rc;
-        e = hipMemcpyAsync(ctr + 0, krank + n_p, 8, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(ctr + 1, kboff + n_p, 8, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(ctr + 2, vrank + n_p, 8, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(ctr + 3, vboff + n_p, 8, hipMemcpyDeviceToDevice, s);
-    } else {
-        e = hipMemsetAsync(ctr, 0, 32, s);
+        uint64_t sizes[4] = {0, 0, 0, 0};
+        if (h_ctr[0]) {
+            e = hipMemcpyAsync(&sizes[0], krank + n_p, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(&sizes[1], kboff + n_p, 8, hipMemcpyDeviceToHost, s);
+        }
+        if (e == hipSuccess && h_ctr[1]) {
+            e = hipMemcpyAsync(&sizes[2], vrank + n_p, 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(&sizes[3], vboff + n_p, 8, hipMemcpyDeviceToHost, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        new_k = sizes[0], new_kb = sizes[1], new_v = sizes[2], new_vb = sizes[3];
     }
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    uint64_t h_ctr[4];
-    std::vector<uint32_t> flags(nb);
-    e = hipMemcpyAsync(h_ctr, ctr, 32, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
+    e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     for (uint32_t b = 0; b < nb; ++b) {
         body_status[b] |= flags[b];
         if (body_status[b] & kBodyMalformed) body_status[b] = kBodyMalformed;   // nothing else applies then
     }
-    rc = tab_pull_new(ctx, keys, kn0 + h_ctr[0], kb0 + h_ctr[1]);
-    if (!rc) rc = tab_pull_new(ctx, vals, vn0 + h_ctr[2], vb0 + h_ctr[3]);
+    rc = CRDT_OK;
+    if (new_k) rc = tab_pull_new(ctx, keys, kn0 + new_k, kb0 + new_kb);
+    if (!rc && new_v) rc = tab_pull_new(ctx, vals, vn0 + new_v, vb0 + new_vb);
     return rc;
 }
 
