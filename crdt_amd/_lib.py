@@ -95,7 +95,7 @@ class crdt_local_out(C.Structure):
 
 class crdt_gossip_bodies(C.Structure):
     _fields_ = [("n_bodies", C.c_uint32), ("key_cap", C.c_uint32), ("kv_base", C.c_uint64), ("data", C.c_void_p),
-                ("body_off", C.c_void_p), ("slot_base", C.c_void_p)]
+                ("body_off", C.c_void_p), ("slot_base", C.c_void_p), ("host_hdr", C.c_void_p)]
 
 
 class crdt_gossip_decoded(C.Structure):

@@ -95,6 +95,10 @@ extern "C" int crdt_ctx_create(int device, void *stream, crdt_ctx **out) {
     if (e == hipSuccess) e = hipMemset(ctx->dev_status, 0, 256);
     if (e != hipSuccess) {
         if (ctx->dev_status) (void)hipFree(ctx->dev_status);
+    server_ctx_release(ctx);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    (void)crdt_strtab_destroy(ctx->keys);
+    (void)crdt_strtab_destroy(ctx->vals);
         delete ctx;
         return e == hipErrorOutOfMemory ? CRDT_E_NOMEM : CRDT_E_HIP;
     }
@@ -133,6 +137,10 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->io) (void)hipFree(ctx->io);
     if (ctx->dev_status) (void)hipFree(ctx->dev_status);
+    server_ctx_release(ctx);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    (void)crdt_strtab_destroy(ctx->keys);
+    (void)crdt_strtab_destroy(ctx->vals);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return CRDT_OK;

@@ -579,11 +579,13 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     // the decode is planned with
     for (uint32_t b = 0; b < nb; ++b)
         if (in->body_off[b + 1] < in->body_off[b]) return CRDT_E_INVAL;
-    std::vector<uint8_t> hdr(32 * (size_t)nb, 0);
-    rc = ws_reserve(ctx, Carve::round((nb + 1) * 8) + Carve::round(32 * (size_t)nb) + 512);
-    if (rc) return rc;
+    std::vector<uint8_t> hdr_buf;
+    const uint8_t *hdr = in->host_hdr;
     hipError_t e;
-    {
+    if (!hdr) {
+        hdr_buf.assign(32 * (size_t)nb, 0);
+        rc = ws_reserve(ctx, Carve::round((nb + 1) * 8) + Carve::round(32 * (size_t)nb) + 512);
+        if (rc) return rc;
         Carve w0(ctx->ws);
         uint64_t *d_off = w0.take<uint64_t>(nb + 1);
         uint8_t *d_hdr = w0.take<uint8_t>(32 * (size_t)nb);
@@ -592,9 +594,10 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
         k_gather_headers<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(in->data, d_off, nb, d_hdr);
         rc = check_launch(ctx);
         if (rc) return rc;
-        e = hipMemcpyAsync(hdr.data(), d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
+        e = hipMemcpyAsync(hdr_buf.data(), d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(ctx, e);
+        hdr = hdr_buf.data();
     }
     std::vector<BodyDesc> bd(nb);
     std::vector<uint64_t> r_off(nb + 1, 0);
@@ -697,6 +700,7 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     uint64_t h_ctr[8];
     std::vector<uint32_t> flags(nb);
     e = hipMemcpyAsync(h_ctr, ctr, 64, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     uint64_t new_k = 0, new_kb = 0, new_v = 0, new_vb = 0;
@@ -730,13 +734,11 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
             e = hipMemcpyAsync(&sizes[2], vrank + n_p, 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipMemcpyAsync(&sizes[3], vboff + n_p, 8, hipMemcpyDeviceToHost, s);
         }
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);          // the id pass may flag a body too
         if (e != hipSuccess) return hip_fail(ctx, e);
         new_k = sizes[0], new_kb = sizes[1], new_v = sizes[2], new_vb = sizes[3];
     }
-    e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
     for (uint32_t b = 0; b < nb; ++b) {
         body_status[b] |= flags[b];
         if (body_status[b] & kBodyMalformed) body_status[b] = kBodyMalformed;   // nothing else applies then
@@ -797,7 +799,7 @@ extern "C" int crdt_strtab_intern(crdt_ctx *ctx, crdt_strtab *t, const uint8_t *
     if (e == hipSuccess) {
         const uint64_t boff[2] = {0, body.size() + nbytes};
         const uint32_t sb = 0;
-        crdt_gossip_bodies gb{1, 0xFFFFFFFFu, 0, d, boff, &sb};
+        crdt_gossip_bodies gb{1, 0xFFFFFFFFu, 0, d, boff, &sb, body.data()};
         crdt_gossip_decoded go{r_off, r_ts, r_kv, ids_dev, vv};
         uint32_t st = 0;
         rc = crdt_gossip_decode(ctx, &gb, t, scratch, &go, &st);

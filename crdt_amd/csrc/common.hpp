@@ -20,6 +20,11 @@ struct crdt_ctx {
     void *io = nullptr;      // device staging for host-facing calls (crdt_server_*)
     size_t io_bytes = 0;
     uint32_t *dev_status = nullptr;   // device-side failure flags (CRDT_DEV_*), read by crdt_ctx_device_status
+    crdt_strtab *keys = nullptr;      // device string tables of the context's Servers (key ids, value ids)
+    crdt_strtab *vals = nullptr;
+    void *srv_batch = nullptr;        // batched Server merge scratch (server.hip)
+    void *pinned = nullptr;           // pinned host staging (pulled bodies on their way to HBM)
+    size_t pinned_bytes = 0;
 };
 
 namespace crdt {
@@ -52,6 +57,8 @@ extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at
 extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
 extern int g_sets_stamps;
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
+
+void server_ctx_release(crdt_ctx *ctx);   // server.hip: the context's Server-merge scratch
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

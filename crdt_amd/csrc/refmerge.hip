@@ -64,8 +64,9 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 // merge order).  Each replica's merge sequence (|L|+|R| items) is cut into
 // tiles of MT items; every tile pass loads one 64-B descriptor and stages
 // its L and R ranges in LDS with coalesced loads.
-//   k_rm_plan_small / scan + k_rm_geo : tiles per replica, tile geometry;
-//   k_rm_split : one wave per tile, 64-ary merge-path splits -> descriptors;
+//   k_rm_plan_small / scan : tiles per replica;
+//   k_rm_split : one wave per tile: its geometry and 16-ary merge-path split
+//                -> descriptors (plus the Atoi / accumulator-reset prep);
 //   k_rm_count : merge (256 threads x MI items): inserted-R count per tile
 //                and every entry's rank among the tile's emitted entries;
 //   scan of the counts -> each tile's output offset, out.off;
@@ -162,37 +163,6 @@ __device__ __forceinline__ void prep_items(const uint8_t *__restrict__ bytes, co
     }
 }
 
-// per-tile geometry (tbase = exclusive scan of the tile counts): one wave
-// per replica, its lanes write the replica's tiles.
-// maxl_ovr (nullable): per-replica max(L) to insert below, instead of the
-// local L's last key (the ts-range-sharded merge passes the global max).
-// The same launch runs the Atoi / accumulator-reset prep (independent work,
-// one launch fewer in front of the tile passes).
-__global__ __launch_bounds__(256) void k_rm_geo(crdt_refmerge_in in, const uint64_t *__restrict__ tbase,
-                                                const int64_t *__restrict__ maxl_ovr, TileGeo *__restrict__ geo,
-                                                OkVal *__restrict__ okv, SlotAcc acc, uint32_t ns) {
-    const int lane = threadIdx.x & 63;
-    for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < in.replicas; p += (uint64_t)gridDim.x * 4) {
-        TileGeo g;
-        g.p = (uint32_t)p;
-        g.lb = in.l_off[p];
-        g.nl = in.l_off[p + 1] - g.lb;
-        g.rb = in.r_off[p];
-        g.nr = in.r_off[p + 1] - g.rb;
-        // empty L: INT64_MIN, below which no remote ts is ever inserted
-        g.maxl = maxl_ovr ? maxl_ovr[p] : g.nl ? in.l_ts[g.lb + g.nl - 1] : INT64_MIN;
-        const uint64_t t0 = tbase[p], t1 = tbase[p + 1];
-        g.first = (uint32_t)t0;
-        for (uint64_t t = t0 + lane; t < t1; t += 64) {
-            g.d0 = (t - t0) * MT;
-            g.d1 = g.d0 + MT < g.nl + g.nr ? g.d0 + MT : g.nl + g.nr;
-            geo[t] = g;
-        }
-    }
-    prep_items(in.str_bytes, in.str_off, in.n_str, okv, acc, ns, (uint64_t)blockIdx.x * 256 + threadIdx.x,
-               (uint64_t)gridDim.x * 256);
-}
-
 // Merge-path split of diagonal d (first d items of the merge): the number of
 // L items among them.  One wave, PW-ary (lanes 0..PW-1 probe): the pass is
 // bound by the scattered probe loads, not by the rounds -- 256-ary (4 probes
@@ -241,18 +211,50 @@ __device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, co
     return lo;
 }
 
-// Tile descriptors: one wave per tile computes the merge-path split at its
-// first diagonal (64-ary) and packs the tile's ranges (its end is the next
-// descriptor's start); slots past the tile count get an empty descriptor.
+// The geometry of tile t from tbase (exclusive scan of the tiles per
+// replica): its replica is the last p with tbase[p] <= t (replicas with no
+// tile share their successor's tbase and are skipped by the search).
+// maxl_ovr (nullable): per-replica max(L) to insert below, instead of the
+// local L's last key (the ts-range-sharded merge passes the global max).
+__device__ __forceinline__ TileGeo tile_geo(const crdt_refmerge_in &in, const uint64_t *__restrict__ tbase,
+                                            const int64_t *__restrict__ maxl_ovr, uint64_t t) {
+    uint32_t lo = 0, hi = in.replicas;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tbase[mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    TileGeo g;
+    g.p = lo;
+    g.lb = in.l_off[lo];
+    g.nl = in.l_off[lo + 1] - g.lb;
+    g.rb = in.r_off[lo];
+    g.nr = in.r_off[lo + 1] - g.rb;
+    g.maxl = maxl_ovr ? maxl_ovr[lo] : g.nl ? in.l_ts[g.lb + g.nl - 1] : INT64_MIN;   // empty L: nothing inserted
+    g.first = (uint32_t)tbase[lo];
+    g.d0 = (t - tbase[lo]) * MT;
+    g.d1 = g.d0 + MT < g.nl + g.nr ? g.d0 + MT : g.nl + g.nr;
+    return g;
+}
+
+// Tile descriptors: one wave per tile computes the tile's geometry and the
+// merge-path split at its first diagonal and packs the tile's ranges (its
+// end is the next descriptor's start); slots past the tile count get an
+// empty descriptor.  The same launch runs the Atoi / accumulator-reset prep
+// (independent work).
 __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t replicas,
-                                                  const uint64_t *__restrict__ tbase, const TileGeo *__restrict__ geo,
-                                                  uint64_t tmax, TileDesc *__restrict__ desc) {
+                                                  const uint64_t *__restrict__ tbase,
+                                                  const int64_t *__restrict__ maxl_ovr, uint64_t tmax,
+                                                  TileDesc *__restrict__ desc, OkVal *__restrict__ okv, SlotAcc acc,
+                                                  uint32_t ns) {
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    prep_items(in.str_bytes, in.str_off, in.n_str, okv, acc, ns, (uint64_t)blockIdx.x * 256 + threadIdx.x,
+               (uint64_t)gridDim.x * 256);
     if (t > tmax) return;                                // desc[tmax]: always an empty sentinel
     TileDesc d = {};
     if (t < tbase[replicas]) {
-        const TileGeo g = geo[t];
+        const TileGeo g = tile_geo(in, tbase, maxl_ovr, t);
         int64_t lprev;
         const uint64_t a0 = wave_split<RM_SPLIT_PW>(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d0, lane, &lprev);
         d.l0 = g.lb + a0;
@@ -927,7 +929,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     uint32_t *nt = w.take<uint32_t>(np + 1);
     uint64_t *tbase = w.take<uint64_t>(np + 1);
     void *tmp = w.take<char>(scan_tmp_bytes(std::max(np, tmax)));
-    TileGeo *geo = w.take<TileGeo>(tmax + 1);
+
     TileDesc *desc = w.take<TileDesc>(tmax + 1);
     uint64_t *ic = w.take<uint64_t>(tmax + 1);
     uint32_t *tcnt = w.take<uint32_t>(tmax + 1);
@@ -959,13 +961,15 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         rc = exclusive_scan_u32(ctx, nt, tbase, np, tmp);         // tbase[np] = tile count
         if (rc) return rc;
     }
-    k_rm_geo<<<std::max(grid_for((np + 3) / 4, 1, cap), grid_for(std::max(nstr, ns), 256, cap)), 256, 0, s>>>(
-        in, tbase, maxl_dev, geo, okv, acc, (uint32_t)ns);
-    k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, geo, tmax, desc);
+    k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, maxl_dev, tmax, desc, okv, acc,
+                                                           (uint32_t)ns);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
     k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk, ovf);
     rc = check_launch(ctx);
     if (rc) return rc;
+    // (a completion ticket letting the count pass's last block do this scan
+    // measured 95 us against 56 + 11.5: same-address arrivals serialise at
+    // ~11 ns each and the tail runs alone after the grid)
     if (tmax <= kSmallPlan) {
         k_rm_scan_small<<<1, SB, 0, s>>>(tcnt, (uint32_t)tmax, ic, in, tbase, out.off);
     } else {

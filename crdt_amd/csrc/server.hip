@@ -17,6 +17,7 @@
 // CurrentState from the device result.  There is no CPU merge path.
 #include <algorithm>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -35,6 +36,21 @@ struct Value {                       // map[string]string or *Command
     std::vector<std::pair<std::string, std::string>> kv;   // unique keys
 };
 
+// A grow-only device buffer.
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    template <class T> T *as() const { return (T *)p; }
+};
+
+// The Diff resident in HBM (SoA, the crdt_refmerge_in L layout of one
+// replica): kv_key = key ids of the context's key table, kv_val = value
+// string ids of its value table (also the merge's string arena).
+struct DevDiff {
+    DBuf ts, origin, kv_off, kv_key, kv_val;      // [n], [n], [n+1], [n_kv], [n_kv]
+    uint64_t n = 0, n_kv = 0;
+};
+
 struct Server {
     crdt_ctx *ctx = nullptr;
     std::map<std::string, std::string> InitialState;        // main.go:24
@@ -47,6 +63,21 @@ struct Server {
     bool Alive = true;                                      // main.go:31
     std::mutex Lock;                                        // main.go:32
     std::vector<std::pair<std::string, std::string>> state_view;   // CurrentState snapshot for iteration
+    // Device residency (servers with a context): the Diff lives in HBM
+    // between merges; the host map above is a lazily rebuilt view.
+    //   host_valid : Diff (the std::map) is current;
+    //   dev_valid  : dd is current up to pend_cmds (local writes queued for
+    //                the device, applied by crdt_local_apply at the next merge);
+    //   pend       : one pulled binary body not yet parsed into RemoteDiff
+    //                (the device decodes it straight into the merge's R).
+    bool host_valid = true, dev_valid = false;
+    DevDiff dd, dd2;                                        // current + next (swapped per merge)
+    std::vector<std::pair<int64_t, std::shared_ptr<const Value>>> pend_cmds;
+    char *pend_body = nullptr;         // pinned host copy of the parked pull (a full-rate H2D at the merge)
+    size_t pend_len = 0, pend_cap = 0;
+    bool pend = false;
+    DBuf body, r_ts, r_kv, r_off, l_off, o_off, o_src, st_kind, st_str, st_sum, c_ts, c_kv, c_key, c_val, c_off,
+        c_status;
 };
 
 static int io_reserve(crdt_ctx *ctx, size_t bytes) {
@@ -251,6 +282,727 @@ static std::shared_ptr<const Value> make_value(bool local, const char *const *ke
     return v;
 }
 
+// ---------------------------------------------------------------- device residency
+// The binary SoA body of a treemap (crdt_server_gossip_binary's format):
+// entries ascending, pairs of an entry sorted by key, nil maps as 0xFFFFFFFF.
+constexpr uint32_t kNilPairsH = 0xFFFFFFFFu;
+
+static void put_u32(std::string &o, uint32_t v) { o.append((const char *)&v, 4); }
+static void put_u64(std::string &o, uint64_t v) { o.append((const char *)&v, 8); }
+
+static void encode_soa(const std::map<int64_t, std::shared_ptr<const Value>> &m, std::string &body) {
+    uint64_t np = 0, nb = 0;
+    for (auto &e : m) {
+        np += e.second->kv.size();
+        for (auto &x : e.second->kv) nb += x.first.size() + x.second.size();
+    }
+    body.clear();
+    body.reserve(32 + 12 * m.size() + 8 * np + nb);
+    body.append("CRDTSOA1", 8);
+    put_u64(body, m.size());
+    put_u64(body, np);
+    put_u64(body, nb);
+    for (auto &e : m) put_u64(body, (uint64_t)e.first);
+    for (auto &e : m) put_u32(body, e.second->nil ? kNilPairsH : (uint32_t)e.second->kv.size());
+    for (auto &e : m)                                  // Value::kv is key-sorted (make_value / ingest)
+        for (auto &x : e.second->kv) put_u32(body, (uint32_t)x.first.size());
+    for (auto &e : m)
+        for (auto &x : e.second->kv) put_u32(body, (uint32_t)x.second.size());
+    for (auto &e : m)
+        for (auto &x : e.second->kv) {
+            body += x.first;
+            body += x.second;
+        }
+}
+
+static bool has_nil(const std::map<int64_t, std::shared_ptr<const Value>> &m) {
+    for (auto &e : m)
+        if (e.second->nil) return true;
+    return false;
+}
+
+static int dbuf(crdt_ctx *ctx, DBuf &b, size_t bytes, size_t keep = 0) {
+    if (bytes <= b.cap) return CRDT_OK;
+    const size_t want = std::max<size_t>(bytes + bytes / 2, 4096);
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, want);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (b.p) {
+        if (keep) e = hipMemcpyAsync(q, b.p, std::min(keep, b.cap), hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        (void)hipFree(b.p);
+        if (e != hipSuccess) {
+            (void)hipFree(q);
+            b.p = nullptr;
+            b.cap = 0;
+            return hip_fail(ctx, e);
+        }
+    }
+    b.p = q;
+    b.cap = want;
+    return CRDT_OK;
+}
+
+static void dbuf_free(DBuf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+}
+
+// Pinned host staging of the context (grow-only; the stream is drained first).
+static int pinned_reserve(crdt_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->pinned_bytes) return CRDT_OK;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_bytes = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 2, 1 << 20);
+    e = hipHostMalloc(&ctx->pinned, want, 0);
+    if (e != hipSuccess) {
+        ctx->pinned = nullptr;
+        return hip_fail(ctx, e);
+    }
+    ctx->pinned_bytes = want;
+    return CRDT_OK;
+}
+
+static int ctx_tables(crdt_ctx *ctx) {
+    int rc = CRDT_OK;
+    if (!ctx->keys) rc = crdt_strtab_create(ctx, 1024, 1 << 14, &ctx->keys);
+    if (!rc && !ctx->vals) rc = crdt_strtab_create(ctx, 1024, 1 << 16, &ctx->vals);
+    return rc;
+}
+
+static std::string tab_str(const crdt_strtab *t, uint64_t id) {
+    const char *p = nullptr;
+    size_t n = 0;
+    if (crdt_strtab_get(t, id, &p, &n) != CRDT_OK) return std::string();
+    return std::string(p, n);
+}
+
+// H2D a body and decode it with the context's tables: entries -> r_ts /
+// r_kv (+ kv_base), pairs -> kv_key / kv_val at kv_base.  *status = the
+// body's decode status (0: taken).
+static int dev_decode(crdt_ctx *ctx, DBuf &body_dev, const char *body, size_t len, bool pinned, uint64_t kv_base,
+                      int64_t *r_ts, uint64_t *r_kv, uint64_t *r_off, uint32_t *kv_key, uint32_t *kv_val,
+                      uint32_t *status) {
+    int rc = dbuf(ctx, body_dev, len);
+    if (!rc && !pinned) rc = pinned_reserve(ctx, len);
+    if (rc) return rc;
+    if (!pinned) memcpy(ctx->pinned, body, len);
+    hipError_t e = hipMemcpyAsync(body_dev.p, pinned ? body : ctx->pinned, len, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const uint64_t boff[2] = {0, len};
+    const uint32_t sb = 0;
+    crdt_gossip_bodies gb{1, 0xFFFFFFFFu, kv_base, body_dev.as<uint8_t>(), boff, &sb,
+                          len >= 32 ? (const uint8_t *)body : nullptr};
+    crdt_gossip_decoded go{r_off, r_ts, r_kv, kv_key, kv_val};
+    return crdt_gossip_decode(ctx, &gb, ctx->keys, ctx->vals, &go, status);
+}
+
+static uint64_t body_u64(const std::string &b, size_t at) {
+    uint64_t v = 0;
+    memcpy(&v, b.data() + at, 8);
+    return v;
+}
+
+// Upload the host Diff (nil-free) into dd: decode its body; origin from the host.
+static int dev_upload(crdt_ctx *ctx, Server &s) {
+    std::string body;
+    encode_soa(s.Diff, body);
+    const uint64_t ne = s.Diff.size(), np = body_u64(body, 16);
+    int rc = dbuf(ctx, s.dd.ts, ne * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.dd.origin, ne + 1);
+    if (!rc) rc = dbuf(ctx, s.dd.kv_off, (ne + 1) * 8);
+    if (!rc) rc = dbuf(ctx, s.dd.kv_key, np * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.dd.kv_val, np * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.r_off, 16);
+    if (rc) return rc;
+    uint32_t st = 0;
+    rc = dev_decode(ctx, s.body, body.data(), body.size(), false, 0, s.dd.ts.as<int64_t>(), s.dd.kv_off.as<uint64_t>(),
+                    s.r_off.as<uint64_t>(), s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), &st);
+    if (rc) return rc;
+    if (st) return CRDT_E_UNSORTED;                   // (never: a treemap's body is ascending and nil-free)
+    std::vector<uint8_t> org;
+    org.reserve(ne);
+    for (auto &e : s.Diff) org.push_back(e.second->local ? 1 : 0);
+    if (ne) {
+        hipError_t e = hipMemcpyAsync(s.dd.origin.p, org.data(), ne, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);   // org is a local
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
+    s.dd.n = ne;
+    s.dd.n_kv = np;
+    s.dev_valid = true;
+    s.pend_cmds.clear();
+    return CRDT_OK;
+}
+
+// Rebuild the host Diff from dd (then the queued local writes on top).
+static int make_host(Server &s) {
+    if (s.host_valid) return CRDT_OK;
+    crdt_ctx *ctx = s.ctx;
+    const uint64_t n = s.dd.n, nk = s.dd.n_kv;
+    std::vector<int64_t> ts(n);
+    std::vector<uint8_t> org(n);
+    std::vector<uint64_t> ko(n + 1);
+    std::vector<uint32_t> kk(nk), kv(nk);
+    hipError_t e = hipSuccess;
+    if (n) e = hipMemcpyAsync(ts.data(), s.dd.ts.p, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(org.data(), s.dd.origin.p, n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(ko.data(), s.dd.kv_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nk) e = hipMemcpyAsync(kk.data(), s.dd.kv_key.p, nk * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nk) e = hipMemcpyAsync(kv.data(), s.dd.kv_val.p, nk * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    std::vector<std::string> kname, vname;             // the tables' strings, by id
+    uint64_t nks = 0, nvs = 0, b0 = 0;
+    (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);
+    (void)crdt_strtab_info(ctx->vals, &nvs, &b0, nullptr, nullptr);
+    kname.reserve(nks);
+    for (uint64_t i = 0; i < nks; ++i) kname.push_back(tab_str(ctx->keys, i));
+    vname.reserve(nvs);
+    for (uint64_t i = 0; i < nvs; ++i) vname.push_back(tab_str(ctx->vals, i));
+    std::map<int64_t, std::shared_ptr<const Value>> m;
+    for (uint64_t i = 0; i < n; ++i) {
+        auto v = std::make_shared<Value>();
+        v->local = org[i] != 0;
+        for (uint64_t q = ko[i] - ko[0]; q < ko[i + 1] - ko[0]; ++q)
+            v->kv.emplace_back(kk[q] < nks ? kname[kk[q]] : std::string(), kv[q] < nvs ? vname[kv[q]] : std::string());
+        m.emplace_hint(m.end(), ts[i], std::move(v));
+    }
+    for (auto &c : s.pend_cmds) m[c.first] = c.second;   // queued local writes (same-ms: the later one)
+    s.Diff.swap(m);
+    s.host_valid = true;
+    return CRDT_OK;
+}
+
+// The pulled binary body parked for the device becomes RemoteDiff entries
+// (a reader of RemoteDiff, or a second pull before the merge).
+static void parse_soa_into(Server &s, const char *data, size_t len);
+static void absorb_pending(Server &s) {
+    if (!s.pend) return;
+    s.pend = false;
+    parse_soa_into(s, s.pend_body, s.pend_len);
+}
+
+// Apply the queued local writes to dd (crdt_local_apply, Diff only: the
+// CurrentState apply already ran on the host when each write arrived).
+static int dev_flush_cmds(crdt_ctx *ctx, Server &s) {
+    if (s.pend_cmds.empty()) return CRDT_OK;
+    std::map<int64_t, std::shared_ptr<const Value>> cm;   // Put replaces: the last same-ms write stays
+    for (auto &c : s.pend_cmds) cm[c.first] = c.second;
+    std::string body;
+    encode_soa(cm, body);
+    const uint64_t nc = cm.size(), np = body_u64(body, 16);
+    int rc = dbuf(ctx, s.c_ts, nc * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.c_kv, (nc + 1) * 8);
+    if (!rc) rc = dbuf(ctx, s.c_key, np * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.c_val, np * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.c_off, 16);
+    if (!rc) rc = dbuf(ctx, s.l_off, 16);
+    if (!rc) rc = dbuf(ctx, s.o_off, 16);
+    if (!rc) rc = dbuf(ctx, s.o_src, (s.dd.n + nc) * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.c_status, nc * 2 + 2);
+    if (!rc) rc = dbuf(ctx, s.dd2.ts, (s.dd.n + nc) * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.dd2.origin, s.dd.n + nc + 1);
+    if (!rc) rc = dbuf(ctx, s.dd2.kv_off, (s.dd.n + nc + 1) * 8);
+    if (!rc) rc = dbuf(ctx, s.dd2.kv_key, (s.dd.n_kv + np) * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.dd2.kv_val, (s.dd.n_kv + np) * 4 + 4);
+    if (rc) return rc;
+    uint32_t st = 0;
+    rc = dev_decode(ctx, s.body, body.data(), body.size(), false, 0, s.c_ts.as<int64_t>(), s.c_kv.as<uint64_t>(),
+                    s.c_off.as<uint64_t>(), s.c_key.as<uint32_t>(), s.c_val.as<uint32_t>(), &st);
+    if (rc) return rc;
+    if (st) return CRDT_E_UNSORTED;
+    const uint64_t loff[2] = {0, s.dd.n};
+    hipError_t e = hipMemcpyAsync(s.l_off.p, loff, 16, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    uint64_t nstr = 0, b0 = 0;
+    const uint8_t *sb = nullptr;
+    const uint64_t *so = nullptr;
+    (void)crdt_strtab_info(ctx->vals, &nstr, &b0, &sb, &so);
+    crdt_local_in li{1, 0, s.dd.n, nc, np, nstr, s.l_off.as<uint64_t>(), s.dd.ts.as<int64_t>(),
+                     s.dd.origin.as<uint8_t>(), s.c_off.as<uint64_t>(), s.c_ts.as<int64_t>(), s.c_kv.as<uint64_t>(),
+                     s.c_key.as<uint32_t>(), s.c_val.as<uint32_t>(), sb, so};
+    crdt_local_out lo{s.o_off.as<uint64_t>(), s.dd2.ts.as<int64_t>(), s.dd2.origin.as<uint8_t>(),
+                      s.o_src.as<int64_t>(), s.c_status.as<uint16_t>(), nullptr, nullptr, nullptr};
+    rc = crdt_local_apply(ctx, &li, &lo);
+    if (rc) return rc;
+    uint64_t oo[2] = {0, 0};
+    e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const uint64_t n_out = oo[1];
+    rc = crdt_seg_gather2(ctx, n_out, s.o_src.as<int64_t>(), s.dd.kv_off.as<uint64_t>(), s.c_kv.as<uint64_t>(), 0,
+                          s.dd2.kv_off.as<uint64_t>(), 4, s.dd.kv_key.p, s.c_key.p, s.dd2.kv_key.p, s.dd.kv_val.p,
+                          s.c_val.p, s.dd2.kv_val.p);
+    if (rc) return rc;
+    uint64_t nkv = 0;
+    e = hipMemcpyAsync(&nkv, s.dd2.kv_off.as<uint64_t>() + n_out, 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    std::swap(s.dd, s.dd2);
+    s.dd.n = n_out;
+    s.dd.n_kv = nkv;
+    s.pend_cmds.clear();
+    return CRDT_OK;
+}
+
+// merge() (main.go:35-100) of one device-resident server: the pull decoded
+// on the device into R, the batched RefMerge with this Diff as L, the next
+// Diff gathered in HBM; only CurrentState (one word per key slot) comes back.
+static int dev_merge_one(crdt_ctx *ctx, Server &s) {
+    int rc;
+    if (!s.dev_valid) {
+        rc = dev_upload(ctx, s);
+        if (rc) return rc;
+    }
+    rc = dev_flush_cmds(ctx, s);
+    if (rc) return rc;
+    std::string rbody;
+    if (!s.pend) encode_soa(s.RemoteDiff, rbody);
+    const char *rp = s.pend ? s.pend_body : rbody.data();
+    const size_t rlen = s.pend ? s.pend_len : rbody.size();
+    uint64_t ne, np;
+    memcpy(&ne, rp + 8, 8);
+    memcpy(&np, rp + 16, 8);
+    const uint64_t nl = s.dd.n, nkv = s.dd.n_kv;
+    rc = dbuf(ctx, s.dd.kv_key, (nkv + np) * 4 + 4, nkv * 4);     // R's pairs go behind L's
+    if (!rc) rc = dbuf(ctx, s.dd.kv_val, (nkv + np) * 4 + 4, nkv * 4);
+    if (!rc) rc = dbuf(ctx, s.r_ts, ne * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.r_kv, (ne + 1) * 8);
+    if (!rc) rc = dbuf(ctx, s.r_off, 16);
+    if (!rc) rc = dbuf(ctx, s.l_off, 16);
+    if (!rc) rc = dbuf(ctx, s.o_off, 16);
+    if (!rc) rc = dbuf(ctx, s.o_src, (nl + ne) * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.dd2.ts, (nl + ne) * 8 + 8);
+    if (!rc) rc = dbuf(ctx, s.dd2.origin, nl + ne + 1);
+    if (!rc) rc = dbuf(ctx, s.dd2.kv_off, (nl + ne + 1) * 8);
+    if (!rc) rc = dbuf(ctx, s.dd2.kv_key, (nkv + np) * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.dd2.kv_val, (nkv + np) * 4 + 4);
+    if (rc) return rc;
+    uint32_t st = 0;
+    rc = dev_decode(ctx, s.body, rp, rlen, s.pend, nkv, s.r_ts.as<int64_t>(), s.r_kv.as<uint64_t>(),
+                    s.r_off.as<uint64_t>(), s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), &st);
+    if (rc) return rc;
+    if (st) return CRDT_E_UNSORTED;                   // (callers route such pulls to the host path first)
+    uint64_t nks = 0, nstr = 0, b0 = 0;
+    const uint8_t *sb = nullptr;
+    const uint64_t *so = nullptr;
+    (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);
+    (void)crdt_strtab_info(ctx->vals, &nstr, &b0, &sb, &so);
+    if (nks >= 0xFFFFFFFFull) return CRDT_E_RANGE;
+    rc = dbuf(ctx, s.st_kind, nks + 1);
+    if (!rc) rc = dbuf(ctx, s.st_str, nks * 4 + 4);
+    if (!rc) rc = dbuf(ctx, s.st_sum, nks * 8 + 8);
+    if (rc) return rc;
+    const uint64_t loff[2] = {0, nl};
+    hipError_t e = hipMemcpyAsync(s.l_off.p, loff, 16, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    crdt_refmerge_in ri;
+    ri.replicas = 1;
+    ri.n_slots = (uint32_t)nks;                       // slot = key id (one replica)
+    ri.n_l = nl;
+    ri.n_r = ne;
+    ri.n_kv = nkv + np;
+    ri.n_str = nstr;
+    ri.l_off = s.l_off.as<uint64_t>();
+    ri.l_ts = s.dd.ts.as<int64_t>();
+    ri.l_origin = s.dd.origin.as<uint8_t>();
+    ri.l_kv = s.dd.kv_off.as<uint64_t>();
+    ri.r_off = s.r_off.as<uint64_t>();
+    ri.r_ts = s.r_ts.as<int64_t>();
+    ri.r_kv = s.r_kv.as<uint64_t>();
+    ri.kv_key = s.dd.kv_key.as<uint32_t>();
+    ri.kv_val = s.dd.kv_val.as<uint32_t>();
+    ri.str_bytes = sb;
+    ri.str_off = so;
+    crdt_refmerge_out ro{s.o_off.as<uint64_t>(), s.dd2.ts.as<int64_t>(), s.dd2.origin.as<uint8_t>(),
+                         s.o_src.as<int64_t>(), s.st_kind.as<uint8_t>(), s.st_str.as<uint32_t>(),
+                         s.st_sum.as<int64_t>()};
+    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    if (rc) return rc;
+    uint64_t oo[2] = {0, 0};
+    e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const uint64_t n_out = oo[1];
+    rc = crdt_seg_gather2(ctx, n_out, s.o_src.as<int64_t>(), s.dd.kv_off.as<uint64_t>(), s.r_kv.as<uint64_t>(), 0,
+                          s.dd2.kv_off.as<uint64_t>(), 4, s.dd.kv_key.p, s.dd.kv_key.p, s.dd2.kv_key.p, s.dd.kv_val.p,
+                          s.dd.kv_val.p, s.dd2.kv_val.p);
+    if (rc) return rc;
+    // CurrentState (main.go:76-96: rebuilt from empty) and the new pair count
+    std::vector<uint8_t> kind(nks);
+    std::vector<uint32_t> sstr(nks);
+    std::vector<int64_t> ssum(nks);
+    uint64_t new_nkv = 0;
+    e = hipMemcpyAsync(&new_nkv, s.dd2.kv_off.as<uint64_t>() + n_out, 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nks) e = hipMemcpyAsync(kind.data(), s.st_kind.p, nks, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nks) e = hipMemcpyAsync(sstr.data(), s.st_str.p, nks * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nks) e = hipMemcpyAsync(ssum.data(), s.st_sum.p, nks * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    std::map<std::string, std::string> state;
+    for (uint64_t k = 0; k < nks; ++k) {
+        if (kind[k] == 1) state.emplace(tab_str(ctx->keys, k), tab_str(ctx->vals, sstr[k]));
+        else if (kind[k] == 2) state.emplace(tab_str(ctx->keys, k), std::to_string((long long)ssum[k]));   // Itoa
+    }
+    std::swap(s.dd, s.dd2);
+    s.dd.n = n_out;
+    s.dd.n_kv = new_nkv;
+    s.CurrentState.swap(state);
+    s.state_view.clear();
+    s.RemoteDiff.clear();                             // main.go:75
+    s.pend = false;
+    s.pend_len = 0;
+    s.host_valid = false;
+    return CRDT_OK;
+}
+
+// ---- batched device merge of several servers (crdt_servers_merge)
+struct SegPtrs {                       // one server's device Diff, for the concat / split kernels
+    const int64_t *ts;
+    const uint8_t *origin;
+    const uint64_t *kv_off;
+    const uint32_t *kv_key, *kv_val;
+    int64_t *dts;                      // split destinations (the server's next Diff)
+    uint8_t *dorigin;
+    uint64_t *dkv_off;
+    uint32_t *dkv_key, *dkv_val;
+    uint64_t e0, n, q0, nq;            // entry / pair range in the batch
+    uint32_t slot_base, pad;
+};
+
+// L of the batch: every server's Diff behind the previous one; kv ranges
+// re-based into the shared arena, key ids into the server's slot range.
+__global__ void k_srv_concat(const SegPtrs *__restrict__ sp, int64_t *__restrict__ l_ts, uint8_t *__restrict__ l_org,
+                             uint64_t *__restrict__ l_kv, uint32_t *__restrict__ kv_key, uint32_t *__restrict__ kv_val) {
+    const SegPtrs p = sp[blockIdx.y];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * 256) {
+        l_ts[p.e0 + i] = p.ts[i];
+        l_org[p.e0 + i] = p.origin[i];
+        l_kv[p.e0 + i] = p.q0 + p.kv_off[i];
+    }
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < p.nq; q += (uint64_t)gridDim.x * 256) {
+        kv_key[p.q0 + q] = p.kv_key[q] + p.slot_base;
+        kv_val[p.q0 + q] = p.kv_val[q];
+    }
+}
+
+// The batch's new Diffs back into each server's next buffers.
+__global__ void k_srv_split(const SegPtrs *__restrict__ sp, const int64_t *__restrict__ o_ts,
+                            const uint8_t *__restrict__ o_org, const uint64_t *__restrict__ o_kv,
+                            const uint32_t *__restrict__ kv_key, const uint32_t *__restrict__ kv_val) {
+    const SegPtrs p = sp[blockIdx.y];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i <= p.n; i += (uint64_t)gridDim.x * 256) {
+        p.dkv_off[i] = o_kv[p.e0 + i] - p.q0;
+        if (i < p.n) {
+            p.dts[i] = o_ts[p.e0 + i];
+            p.dorigin[i] = o_org[p.e0 + i];
+        }
+    }
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < p.nq; q += (uint64_t)gridDim.x * 256) {
+        p.dkv_key[q] = kv_key[p.q0 + q] - p.slot_base;
+        p.dkv_val[q] = kv_val[p.q0 + q];
+    }
+}
+
+// out[i] = v[idx[i]]
+__global__ void k_gather_at(const uint64_t *__restrict__ v, const uint64_t *__restrict__ idx, size_t n,
+                            uint64_t *__restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = v[idx[i]];
+}
+
+struct BatchBufs {                     // per-context scratch of the batched server merge
+    DBuf kb, sp, body, l_ts, l_org, l_kv, l_off, kv_key, kv_val, r_off, r_ts, r_kv, o_off, o_ts, o_org, o_src, n_kv,
+        n_key, n_val, st_kind, st_str, st_sum;
+};
+
+// merge() of several device-resident servers in ONE decode, ONE RefMerge and
+// ONE gather.  Key slots: server s owns [s*kcap, (s+1)*kcap); a pull that
+// brings more new keys than the slack is reported (*retry) and the caller
+// merges one server at a time instead.
+// CRDT_SRV_PROF=1: per-phase host wall time of each batched merge on stderr
+// (a development aid; every phase ends where the host next waits anyway).
+struct PhaseClock {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    char buf[512];
+    int n = 0;
+    PhaseClock() : on(getenv("CRDT_SRV_PROF") != nullptr), t(std::chrono::steady_clock::now()) { buf[0] = 0; }
+    void mark(const char *name) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        const double us = std::chrono::duration<double, std::micro>(now - t).count();
+        t = now;
+        if (n < (int)sizeof(buf) - 64) n += snprintf(buf + n, sizeof(buf) - n, " %s=%.1f", name, us);
+    }
+    ~PhaseClock() {
+        if (on) fprintf(stderr, "[srv_merge]%s\n", buf);
+    }
+};
+
+static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *retry) {
+    *retry = false;
+    PhaseClock pc;
+    if (!ctx->srv_batch) ctx->srv_batch = new (std::nothrow) BatchBufs();
+    if (!ctx->srv_batch) return CRDT_E_NOMEM;
+    BatchBufs &bb = *(BatchBufs *)ctx->srv_batch;      // the context's scratch (a context is single-threaded)
+    int rc;
+    for (size_t i = 0; i < S; ++i) {
+        Server &s = *srv[i];
+        if (!s.dev_valid) rc = dev_upload(ctx, s);
+        else rc = CRDT_OK;
+        if (!rc) rc = dev_flush_cmds(ctx, s);
+        if (rc) return rc;
+    }
+    uint64_t nks0 = 0, b0 = 0;
+    (void)crdt_strtab_info(ctx->keys, &nks0, &b0, nullptr, nullptr);
+    uint64_t kcap = 64;
+    while (kcap < nks0 + 256) kcap <<= 1;
+    if (kcap * S >= 0xFFFFFFFFull) return CRDT_E_RANGE;
+    // the pulls, one body per server, staged in pinned host memory (one
+    // full-rate H2D instead of a pageable copy)
+    std::vector<std::string> enc(S);
+    std::vector<uint64_t> boff(S + 1, 0), e0(S + 1, 0), q0(S + 1, 0), re(S + 1, 0), rq(S + 1, 0), pin_at(S, 0);
+    std::vector<uint32_t> sbase(S);
+    std::vector<uint8_t> hdr(32 * S);
+    uint64_t pin_used = 0;
+    for (size_t i = 0; i < S; ++i) {
+        Server &s = *srv[i];
+        if (!s.pend) {
+            encode_soa(s.RemoteDiff, enc[i]);
+            pin_at[i] = pin_used;
+            pin_used += enc[i].size();
+        }
+        const char *b = s.pend ? s.pend_body : enc[i].data();
+        memcpy(&hdr[32 * i], b, 32);                    // (every body here is >= 32 bytes)
+        boff[i + 1] = boff[i] + (s.pend ? s.pend_len : enc[i].size());
+        uint64_t ne, np;
+        memcpy(&ne, b + 8, 8);
+        memcpy(&np, b + 16, 8);
+        re[i + 1] = re[i] + ne;
+        rq[i + 1] = rq[i] + np;
+        e0[i + 1] = e0[i] + s.dd.n;
+        q0[i + 1] = q0[i] + s.dd.n_kv;
+        sbase[i] = (uint32_t)(i * kcap);
+    }
+    rc = pinned_reserve(ctx, pin_used);               // bodies encoded here; parked pulls are pinned already
+    if (rc) return rc;
+    for (size_t i = 0; i < S; ++i)
+        if (!srv[i]->pend) memcpy((char *)ctx->pinned + pin_at[i], enc[i].data(), enc[i].size());
+    pc.mark("upload+encode");
+    const uint64_t nl = e0[S], nkl = q0[S], nr = re[S], nkr = rq[S], nslots = kcap * S;
+    rc = dbuf(ctx, bb.sp, S * sizeof(SegPtrs));
+    if (!rc) rc = dbuf(ctx, bb.body, boff[S] + 1);
+    if (!rc) rc = dbuf(ctx, bb.kb, (S + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.l_ts, nl * 8 + 8);
+    if (!rc) rc = dbuf(ctx, bb.l_org, nl + 1);
+    if (!rc) rc = dbuf(ctx, bb.l_kv, (nl + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.l_off, (S + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.kv_key, (nkl + nkr) * 4 + 4);
+    if (!rc) rc = dbuf(ctx, bb.kv_val, (nkl + nkr) * 4 + 4);
+    if (!rc) rc = dbuf(ctx, bb.r_off, (S + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.r_ts, nr * 8 + 8);
+    if (!rc) rc = dbuf(ctx, bb.r_kv, (nr + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.o_off, (S + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.o_ts, (nl + nr) * 8 + 8);
+    if (!rc) rc = dbuf(ctx, bb.o_org, nl + nr + 1);
+    if (!rc) rc = dbuf(ctx, bb.o_src, (nl + nr) * 8 + 8);
+    if (!rc) rc = dbuf(ctx, bb.n_kv, (nl + nr + 1) * 8);
+    if (!rc) rc = dbuf(ctx, bb.n_key, (nkl + nkr) * 4 + 4);
+    if (!rc) rc = dbuf(ctx, bb.n_val, (nkl + nkr) * 4 + 4);
+    if (!rc) rc = dbuf(ctx, bb.st_kind, nslots + 1);
+    if (!rc) rc = dbuf(ctx, bb.st_str, nslots * 4 + 4);
+    if (!rc) rc = dbuf(ctx, bb.st_sum, nslots * 8 + 8);
+    if (rc) return rc;
+    const hipStream_t st = ctx->stream;
+    // L: concat
+    std::vector<SegPtrs> sp(S);
+    uint64_t maxn = 1;
+    for (size_t i = 0; i < S; ++i) {
+        Server &s = *srv[i];
+        sp[i] = SegPtrs{s.dd.ts.as<int64_t>(), s.dd.origin.as<uint8_t>(), s.dd.kv_off.as<uint64_t>(),
+                        s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
+                        nullptr, e0[i], s.dd.n, q0[i], s.dd.n_kv, sbase[i], 0};
+        maxn = std::max<uint64_t>(maxn, std::max(s.dd.n, s.dd.n_kv));
+    }
+    hipError_t e = hipMemcpyAsync(bb.sp.p, sp.data(), S * sizeof(SegPtrs), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(bb.l_off.p, e0.data(), (S + 1) * 8, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const dim3 grid(grid_for(maxn, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
+    k_srv_concat<<<grid, 256, 0, st>>>(bb.sp.as<SegPtrs>(), bb.l_ts.as<int64_t>(), bb.l_org.as<uint8_t>(),
+                                        bb.l_kv.as<uint64_t>(), bb.kv_key.as<uint32_t>(), bb.kv_val.as<uint32_t>());
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    e = hipMemcpyAsync(bb.l_kv.as<uint64_t>() + nl, &nkl, 8, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    // R: every pull decoded at once, pairs behind L's in the arena
+    for (size_t i = 0; i < S && e == hipSuccess; ++i) {
+        const Server &s = *srv[i];
+        e = hipMemcpyAsync(bb.body.as<char>() + boff[i], s.pend ? s.pend_body : (char *)ctx->pinned + pin_at[i],
+                           boff[i + 1] - boff[i], hipMemcpyHostToDevice, st);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    std::vector<uint32_t> bst(S, 0);
+    crdt_gossip_bodies gb{(uint32_t)S, (uint32_t)kcap, nkl, bb.body.as<uint8_t>(), boff.data(), sbase.data(),
+                          hdr.data()};
+    crdt_gossip_decoded go{bb.r_off.as<uint64_t>(), bb.r_ts.as<int64_t>(), bb.r_kv.as<uint64_t>(),
+                           bb.kv_key.as<uint32_t>(), bb.kv_val.as<uint32_t>()};
+    pc.mark("alloc+concat");
+    rc = crdt_gossip_decode(ctx, &gb, ctx->keys, ctx->vals, &go, bst.data());
+    if (rc) return rc;
+    pc.mark("decode");
+    for (auto x : bst)
+        if (x) {                                       // a key past the slot slack (or a malformed pull)
+            *retry = true;
+            return CRDT_OK;
+        }
+    uint64_t nstr = 0;
+    const uint8_t *sb = nullptr;
+    const uint64_t *so = nullptr;
+    (void)crdt_strtab_info(ctx->vals, &nstr, &b0, &sb, &so);
+    crdt_refmerge_in ri;
+    ri.replicas = (uint32_t)S;
+    ri.n_slots = (uint32_t)nslots;
+    ri.n_l = nl;
+    ri.n_r = nr;
+    ri.n_kv = nkl + nkr;
+    ri.n_str = nstr;
+    ri.l_off = bb.l_off.as<uint64_t>();
+    ri.l_ts = bb.l_ts.as<int64_t>();
+    ri.l_origin = bb.l_org.as<uint8_t>();
+    ri.l_kv = bb.l_kv.as<uint64_t>();
+    ri.r_off = bb.r_off.as<uint64_t>();
+    ri.r_ts = bb.r_ts.as<int64_t>();
+    ri.r_kv = bb.r_kv.as<uint64_t>();
+    ri.kv_key = bb.kv_key.as<uint32_t>();
+    ri.kv_val = bb.kv_val.as<uint32_t>();
+    ri.str_bytes = sb;
+    ri.str_off = so;
+    crdt_refmerge_out ro{bb.o_off.as<uint64_t>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
+                         bb.o_src.as<int64_t>(), bb.st_kind.as<uint8_t>(), bb.st_str.as<uint32_t>(),
+                         bb.st_sum.as<int64_t>()};
+    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    if (rc) return rc;
+    pc.mark("refmerge_launch");
+    std::vector<uint64_t> oo(S + 1);
+    e = hipMemcpyAsync(oo.data(), bb.o_off.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    pc.mark("refmerge_wait");
+    const uint64_t n_out = oo[S];
+    rc = crdt_seg_gather2(ctx, n_out, bb.o_src.as<int64_t>(), bb.l_kv.as<uint64_t>(), bb.r_kv.as<uint64_t>(), 0,
+                          bb.n_kv.as<uint64_t>(), 4, bb.kv_key.p, bb.kv_key.p, bb.n_key.p, bb.kv_val.p, bb.kv_val.p,
+                          bb.n_val.p);
+    if (rc) return rc;
+    // pair ranges of each server's next Diff (gathered on the device), and CurrentState
+    std::vector<uint64_t> kb(S + 1);
+    k_gather_at<<<grid_for(S + 1, 256, 1u << 20), 256, 0, st>>>(bb.n_kv.as<uint64_t>(), bb.o_off.as<uint64_t>(),
+                                                                 S + 1, bb.kb.as<uint64_t>());
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    e = hipMemcpyAsync(kb.data(), bb.kb.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
+    std::vector<uint8_t> kind(nslots);
+    std::vector<uint32_t> sstr(nslots);
+    std::vector<int64_t> ssum(nslots);
+    if (e == hipSuccess) e = hipMemcpyAsync(kind.data(), bb.st_kind.p, nslots, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(sstr.data(), bb.st_str.p, nslots * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(ssum.data(), bb.st_sum.p, nslots * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    pc.mark("gather+state_d2h");
+    // split back into each server's next buffers
+    maxn = 1;
+    for (size_t i = 0; i < S; ++i) {
+        Server &s = *srv[i];
+        const uint64_t n = oo[i + 1] - oo[i], nq = kb[i + 1] - kb[i];
+        rc = dbuf(ctx, s.dd2.ts, n * 8 + 8);
+        if (!rc) rc = dbuf(ctx, s.dd2.origin, n + 1);
+        if (!rc) rc = dbuf(ctx, s.dd2.kv_off, (n + 1) * 8);
+        if (!rc) rc = dbuf(ctx, s.dd2.kv_key, nq * 4 + 4);
+        if (!rc) rc = dbuf(ctx, s.dd2.kv_val, nq * 4 + 4);
+        if (rc) return rc;
+        sp[i] = SegPtrs{nullptr, nullptr, nullptr, nullptr, nullptr, s.dd2.ts.as<int64_t>(),
+                        s.dd2.origin.as<uint8_t>(), s.dd2.kv_off.as<uint64_t>(), s.dd2.kv_key.as<uint32_t>(),
+                        s.dd2.kv_val.as<uint32_t>(), oo[i], n, kb[i], nq, sbase[i], 0};
+        maxn = std::max<uint64_t>(maxn, std::max(n + 1, nq));
+    }
+    e = hipMemcpyAsync(bb.sp.p, sp.data(), S * sizeof(SegPtrs), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const dim3 g2(grid_for(maxn, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
+    k_srv_split<<<g2, 256, 0, st>>>(bb.sp.as<SegPtrs>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
+                                     bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>());
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    e = hipStreamSynchronize(st);                      // sp (host vector) and the next buffers settled
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    pc.mark("split");
+    uint64_t nks = 0;
+    (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);
+    std::vector<std::string> kname(nks);
+    for (uint64_t k = 0; k < nks; ++k) kname[k] = tab_str(ctx->keys, k);
+    for (size_t i = 0; i < S; ++i) {
+        Server &s = *srv[i];
+        std::map<std::string, std::string> state;       // main.go:76: rebuilt from empty
+        for (uint64_t k = 0; k < nks && k < kcap; ++k) {
+            const uint64_t sl = i * kcap + k;
+            if (kind[sl] == 1) state.emplace(kname[k], tab_str(ctx->vals, sstr[sl]));
+            else if (kind[sl] == 2) state.emplace(kname[k], std::to_string((long long)ssum[sl]));   // Itoa
+        }
+        std::swap(s.dd, s.dd2);
+        s.dd.n = oo[i + 1] - oo[i];
+        s.dd.n_kv = kb[i + 1] - kb[i];
+        s.CurrentState.swap(state);
+        s.state_view.clear();
+        s.RemoteDiff.clear();                          // main.go:75
+        s.pend = false;
+        s.pend_len = 0;
+        s.host_valid = false;
+    }
+    pc.mark("state_rebuild");
+    return CRDT_OK;
+}
+
+// Frees the context's batch scratch (crdt_ctx_destroy).
+void server_ctx_release(crdt_ctx *ctx) {
+    if (!ctx->srv_batch) return;
+    BatchBufs *bb = (BatchBufs *)ctx->srv_batch;
+    for (DBuf *b : {&bb->kb, &bb->sp, &bb->body, &bb->l_ts, &bb->l_org, &bb->l_kv, &bb->l_off, &bb->kv_key, &bb->kv_val,
+                    &bb->r_off, &bb->r_ts, &bb->r_kv, &bb->o_off, &bb->o_ts, &bb->o_org, &bb->o_src, &bb->n_kv,
+                    &bb->n_key, &bb->n_val, &bb->st_kind, &bb->st_str, &bb->st_sum})
+        dbuf_free(*b);
+    delete bb;
+    ctx->srv_batch = nullptr;
+}
+
+// Can this merge run on the device?  Not with a nil map (JSON null) in the
+// Diff or the pull: the device layout has no nil flag.
+static bool dev_ok(const Server &s) {
+    if (!s.ctx) return false;
+    if (!s.dev_valid && has_nil(s.Diff)) return false;
+    if (!s.pend && has_nil(s.RemoteDiff)) return false;
+    return true;
+}
+
+static void dev_free(Server &s) {
+    if (s.ctx) {
+        (void)bind(s.ctx);
+        (void)hipStreamSynchronize(s.ctx->stream);
+    }
+    for (DBuf *b : {&s.dd.ts, &s.dd.origin, &s.dd.kv_off, &s.dd.kv_key, &s.dd.kv_val, &s.dd2.ts, &s.dd2.origin,
+                    &s.dd2.kv_off, &s.dd2.kv_key, &s.dd2.kv_val, &s.body, &s.r_ts, &s.r_kv, &s.r_off, &s.l_off,
+                    &s.o_off, &s.o_src, &s.st_kind, &s.st_str, &s.st_sum, &s.c_ts, &s.c_kv, &s.c_key, &s.c_val,
+                    &s.c_off, &s.c_status})
+        dbuf_free(*b);
+    if (s.pend_body) (void)hipHostFree(s.pend_body);
+    s.pend_body = nullptr;
+    s.pend_cap = s.pend_len = 0;
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -268,6 +1020,7 @@ extern "C" int crdt_server_new(crdt_ctx *ctx, int port, crdt_server **out) {
 }
 
 extern "C" int crdt_server_free(crdt_server *srv) {
+    if (srv) dev_free(srv->s);
     delete srv;
     return CRDT_OK;
 }
@@ -285,7 +1038,11 @@ extern "C" int crdt_server_diff_put(crdt_server *srv, int64_t ts, int local, con
                                     const size_t *klen, const char *const *vals, const size_t *vlen, size_t n) {
     if (!srv || !kv_args_ok(keys, klen, vals, vlen, n)) return CRDT_E_INVAL;
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    int rc = make_host(srv->s);
+    if (rc) return rc;
     srv->s.Diff[ts] = make_value(local != 0, keys, klen, vals, vlen, n);   // treemap Put replaces
+    srv->s.dev_valid = false;                                    // re-uploaded at the next merge
+    srv->s.pend_cmds.clear();
     return CRDT_OK;
 }
 
@@ -295,6 +1052,7 @@ extern "C" int crdt_server_remote_put(crdt_server *srv, int64_t ts, const char *
     // main.go:255 writes RemoteDiff from the gossip goroutine without the lock;
     // here the lock is taken so concurrent callers stay safe.
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    absorb_pending(srv->s);
     srv->s.RemoteDiff[ts] = make_value(false, keys, klen, vals, vlen, n);
     return CRDT_OK;
 }
@@ -318,7 +1076,32 @@ extern "C" int crdt_servers_merge(crdt_server *const *srvs, size_t n) {
     if (rc) return rc;
     for (auto *s : v) s->Alive = false;                         // main.go:41
     for (auto *s : order) s->Lock.lock();                       // main.go:43 (address order: no deadlock)
-    rc = merge_locked(ctx, v.data(), v.size());
+    // Device-resident path: every server's Diff stays in HBM, its pull is
+    // decoded on the device; the host path (pack, H2D, merge, D2H, rebuild)
+    // takes batches holding a nil map (no device representation).
+    bool dev = g_fail_refmerge.load() == 0;                     // (fault injection exercises the host path)
+    for (auto *s : v) dev = dev && dev_ok(*s) && s->ctx == ctx;
+    if (dev) rc = ctx_tables(ctx);
+    if (dev && !rc) {
+        bool retry = true;                                      // (one server: the exact-slot path)
+        if (v.size() > 1) rc = dev_merge_batch(ctx, v.data(), v.size(), &retry);
+        if (!rc && retry)                                       // one at a time (exact key slots)
+            for (auto *s : v) {
+                rc = dev_merge_one(ctx, *s);
+                if (rc) break;
+            }
+    } else if (!rc) {
+        for (auto *s : v) {
+            absorb_pending(*s);
+            if (!rc) rc = make_host(*s);
+        }
+        if (!rc) rc = merge_locked(ctx, v.data(), v.size());
+        if (!rc)
+            for (auto *s : v) {                                   // the host map is now the Diff
+                s->dev_valid = false;
+                s->pend_cmds.clear();
+            }
+    }
     for (auto *s : v) s->Alive = true;
     for (auto it = order.rbegin(); it != order.rend(); ++it) (*it)->Lock.unlock();
     return rc;
@@ -354,7 +1137,8 @@ extern "C" int crdt_server_add_command(crdt_server *srv, int64_t ts_ms, const ch
     std::lock_guard<std::mutex> g(s.Lock);
     if (!s.Alive) { *http_status = 502; return CRDT_OK; }
     auto v = make_value(true, keys, klen, vals, vlen, n);
-    s.Diff[ts_ms] = v;                                     // same-ms writes overwrite
+    if (s.host_valid) s.Diff[ts_ms] = v;                   // same-ms writes overwrite
+    if (s.dev_valid) s.pend_cmds.emplace_back(ts_ms, v);   // applied to the device Diff at the next merge
     s.state_view.clear();
     *http_status = 200;
     for (auto &kv : v->kv) {
@@ -388,6 +1172,12 @@ extern "C" int crdt_server_add_command(crdt_server *srv, int64_t ts_ms, const ch
 extern "C" int crdt_server_diff_len(crdt_server *srv, size_t *n) {
     if (!srv || !n) return CRDT_E_INVAL;
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    if (!srv->s.host_valid && srv->s.pend_cmds.empty()) {       // no need to rebuild the host view
+        *n = srv->s.dd.n;
+        return CRDT_OK;
+    }
+    int rc = make_host(srv->s);
+    if (rc) return rc;
     *n = srv->s.Diff.size();
     return CRDT_OK;
 }
@@ -395,6 +1185,7 @@ extern "C" int crdt_server_diff_len(crdt_server *srv, size_t *n) {
 extern "C" int crdt_server_remote_len(crdt_server *srv, size_t *n) {
     if (!srv || !n) return CRDT_E_INVAL;
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    absorb_pending(srv->s);
     *n = srv->s.RemoteDiff.size();
     return CRDT_OK;
 }
@@ -404,6 +1195,8 @@ extern "C" int crdt_server_remote_len(crdt_server *srv, size_t *n) {
 extern "C" int crdt_server_diff_keys(crdt_server *srv, int64_t *ts, uint8_t *local, size_t cap, size_t *n) {
     if (!srv || !n) return CRDT_E_INVAL;
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    int rc = make_host(srv->s);
+    if (rc) return rc;
     size_t i = 0;
     for (auto &e : srv->s.Diff) {
         if (i >= cap) break;
@@ -544,6 +1337,8 @@ extern "C" int crdt_server_gossip_json(crdt_server *srv, char *buf, size_t cap, 
     std::string body;
     {
         std::lock_guard<std::mutex> g(srv->s.Lock);                   // main.go:155-156
+        int rc = make_host(srv->s);
+        if (rc) return rc;
         if (!srv->s.Alive) {
             *http_status = 502;
             body = "Unreachable";                                    // main.go:166
@@ -784,6 +1579,7 @@ extern "C" int crdt_server_ingest_json(crdt_server *srv, const char *data, size_
         puts.emplace_back(ts, &t.second);
     }
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    absorb_pending(srv->s);
     for (auto &pv : puts) {
         auto v = std::make_shared<Value>();
         v->local = false;
@@ -807,6 +1603,7 @@ extern "C" int crdt_server_set_alive(crdt_server *srv, int alive) {
 extern "C" int crdt_server_remote_keys(crdt_server *srv, int64_t *ts, size_t cap, size_t *n) {
     if (!srv || !n) return CRDT_E_INVAL;
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    absorb_pending(srv->s);
     size_t i = 0;
     for (auto &e : srv->s.RemoteDiff) {
         if (i >= cap) break;
@@ -825,6 +1622,12 @@ extern "C" int crdt_server_entry_at(crdt_server *srv, int remote, int64_t ts, si
                                     size_t *klen, const char **val, size_t *vlen, size_t *npairs) {
     if (!srv || !npairs) return CRDT_E_INVAL;
     std::lock_guard<std::mutex> g(srv->s.Lock);
+    if (remote) {
+        absorb_pending(srv->s);
+    } else {
+        int rc = make_host(srv->s);
+        if (rc) return rc;
+    }
     auto &m = remote ? srv->s.RemoteDiff : srv->s.Diff;
     auto it = m.find(ts);
     if (it == m.end()) return CRDT_E_RANGE;
@@ -871,6 +1674,8 @@ extern "C" int crdt_server_gossip_binary(crdt_server *srv, char *buf, size_t cap
     std::string body;
     {
         std::lock_guard<std::mutex> g(srv->s.Lock);
+        int rc = make_host(srv->s);
+        if (rc) return rc;
         if (!srv->s.Alive) {
             *http_status = 502;
             body = "Unreachable";
@@ -918,29 +1723,14 @@ extern "C" int crdt_server_gossip_binary(crdt_server *srv, char *buf, size_t cap
     return CRDT_OK;
 }
 
-// *outcome: 0 = ingested into RemoteDiff; 1 = malformed (nothing ingested).
-extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, size_t len, int *outcome) {
-    if (!srv || !outcome || (!data && len)) return CRDT_E_INVAL;
-    *outcome = 1;
+namespace crdt {
+// RemoteDiff.Put of every entry of a validated binary body (duplicate ts /
+// keys: the last wins).
+static void parse_soa_into(Server &s, const char *data, size_t) {
     const unsigned char *p = reinterpret_cast<const unsigned char *>(data);
-    if (len < 32 || std::memcmp(p, kSoaMagic, 8) != 0) return CRDT_OK;
-    const uint64_t ne = get_le<uint64_t>(p + 8), np = get_le<uint64_t>(p + 16), nb = get_le<uint64_t>(p + 24);
-    // sizes in 128-bit-safe arithmetic: every count is bounded by the body length first
-    if (ne > len / 12 || np > len / 8 || nb > len) return CRDT_OK;
-    const uint64_t need = 32 + ne * 12 + np * 8 + nb;
-    if (need != len) return CRDT_OK;
+    const uint64_t ne = get_le<uint64_t>(p + 8), np = get_le<uint64_t>(p + 16);
     const unsigned char *pts = p + 32, *ppairs = pts + ne * 8, *pkl = ppairs + ne * 4, *pvl = pkl + np * 4,
                         *pb = pvl + np * 4;
-    uint64_t pairs_total = 0, bytes_total = 0;
-    for (uint64_t i = 0; i < ne; ++i) {
-        const uint32_t k = get_le<uint32_t>(ppairs + 4 * i);
-        pairs_total += k == kNilPairs ? 0 : k;
-    }
-    if (pairs_total != np) return CRDT_OK;
-    for (uint64_t j = 0; j < np; ++j) bytes_total += (uint64_t)get_le<uint32_t>(pkl + 4 * j) + get_le<uint32_t>(pvl + 4 * j);
-    if (bytes_total != nb) return CRDT_OK;
-    std::vector<std::pair<int64_t, std::shared_ptr<Value>>> puts;
-    puts.reserve(ne);
     uint64_t j = 0, off = 0;
     for (uint64_t i = 0; i < ne; ++i) {
         const uint32_t k0 = get_le<uint32_t>(ppairs + 4 * i), k = k0 == kNilPairs ? 0 : k0;
@@ -956,10 +1746,73 @@ extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, siz
         v->local = false;
         v->nil = k0 == kNilPairs;
         v->kv.assign(m.begin(), m.end());
-        puts.emplace_back(get_le<int64_t>(pts + 8 * i), std::move(v));
+        s.RemoteDiff[get_le<int64_t>(pts + 8 * i)] = std::move(v);
     }
+}
+}  // namespace crdt
+
+// *outcome: 0 = ingested into RemoteDiff; 1 = malformed (nothing ingested).
+extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, size_t len, int *outcome) {
+    if (!srv || !outcome || (!data && len)) return CRDT_E_INVAL;
+    *outcome = 1;
+    const unsigned char *p = reinterpret_cast<const unsigned char *>(data);
+    if (len < 32 || std::memcmp(p, kSoaMagic, 8) != 0) return CRDT_OK;
+    const uint64_t ne = get_le<uint64_t>(p + 8), np = get_le<uint64_t>(p + 16), nb = get_le<uint64_t>(p + 24);
+    // sizes in 128-bit-safe arithmetic: every count is bounded by the body length first
+    if (ne > len / 12 || np > len / 8 || nb > len) return CRDT_OK;
+    const uint64_t need = 32 + ne * 12 + np * 8 + nb;
+    if (need != len) return CRDT_OK;
+    const unsigned char *pts = p + 32, *ppairs = pts + ne * 8, *pkl = ppairs + ne * 4, *pvl = pkl + np * 4,
+                        *pb = pvl + np * 4;
+    // One pass: the pair and byte totals must match the header, and the
+    // device takes the body as it is (decoded in HBM at the merge) when it is
+    // the only pull: ts strictly ascending, keys of every entry strictly
+    // ascending, no nil map -- what every served body is.  Else the host parse.
+    uint64_t j = 0, off = 0;
+    bool device_form = true;
+    for (uint64_t i = 0; i < ne; ++i) {
+        const uint32_t k0 = get_le<uint32_t>(ppairs + 4 * i);
+        if (k0 == kNilPairs) {
+            device_form = false;
+            continue;
+        }
+        if (k0 > np - j) return CRDT_OK;                       // more pairs than the header holds
+        if (i && get_le<int64_t>(pts + 8 * i) <= get_le<int64_t>(pts + 8 * (i - 1))) device_form = false;
+        const unsigned char *prev = nullptr;
+        uint32_t prev_len = 0;
+        for (uint32_t u = 0; u < k0; ++u, ++j) {
+            const uint32_t kl = get_le<uint32_t>(pkl + 4 * j), vl = get_le<uint32_t>(pvl + 4 * j);
+            if ((uint64_t)kl + vl > nb - off) return CRDT_OK;    // more bytes than the header holds
+            const unsigned char *key = pb + off;
+            if (device_form && prev) {
+                const int c = std::memcmp(prev, key, std::min(prev_len, kl));
+                if (c > 0 || (c == 0 && prev_len >= kl)) device_form = false;
+            }
+            prev = key;
+            prev_len = kl;
+            off += (uint64_t)kl + vl;
+        }
+    }
+    if (j != np || off != nb) return CRDT_OK;
     std::lock_guard<std::mutex> g(srv->s.Lock);
-    for (auto &pv : puts) srv->s.RemoteDiff[pv.first] = std::move(pv.second);
+    Server &s = srv->s;
+    if (device_form && s.ctx && !s.pend && s.RemoteDiff.empty()) {
+        if (len > s.pend_cap) {                                 // (the previous pull's H2D completed: merges sync)
+            if (s.pend_body) (void)hipHostFree(s.pend_body);
+            s.pend_body = nullptr;
+            s.pend_cap = 0;
+            void *q = nullptr;
+            if (hipHostMalloc(&q, len + len / 2, 0) != hipSuccess) return CRDT_E_NOMEM;
+            s.pend_body = (char *)q;
+            s.pend_cap = len + len / 2;
+        }
+        memcpy(s.pend_body, data, len);
+        s.pend_len = len;
+        s.pend = true;
+    } else {
+        absorb_pending(s);
+        parse_soa_into(s, data, len);
+    }
     *outcome = 0;
     return CRDT_OK;
 }

@@ -105,6 +105,8 @@ class Server:
         h = C.c_void_p()
         call("crdt_server_new", eng.ctx if eng is not None else None, int(port), C.byref(h))
         self._h = h
+        if eng is not None:
+            eng._depend(self)                 # freed before the context its device Diff lives on
         self.Port = port
         self.InitialState = dict(initial_state or {})
         self.FriendList = list(friend_list)

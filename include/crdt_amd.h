@@ -513,7 +513,8 @@ int crdt_strtab_intern(crdt_ctx *ctx, crdt_strtab *tab, const uint8_t *bytes_dev
  * but not taken by the device path (a nil map, ts not strictly ascending,
  * keys of an entry not strictly ascending, a key id >= key_cap): decode that
  * body on the host; 4 a table was full.  The decoded arrays of a non-zero
- * body are not valid.  Synchronises (once for the headers, once at the end). */
+ * body are not valid.  Synchronises once (once more for the headers when
+ * host_hdr is NULL, and once more when new strings were interned). */
 typedef struct crdt_gossip_bodies {
     uint32_t n_bodies;
     uint32_t key_cap;           /* key ids >= key_cap: status 2 (the replica's slot range is full) */
@@ -521,6 +522,8 @@ typedef struct crdt_gossip_bodies {
     const uint8_t *data;        /* device: the bodies, concatenated */
     const uint64_t *body_off;   /* host [n_bodies+1]: byte ranges of the bodies in data */
     const uint32_t *slot_base;  /* host [n_bodies]: key slot of key id 0, per body */
+    const uint8_t *host_hdr;    /* host [32*n_bodies] or NULL: each body's first 32 bytes, when the caller
+                                   already holds them (skips the header gather and its wait) */
 } crdt_gossip_bodies;
 typedef struct crdt_gossip_decoded {
     uint64_t *r_off;            /* device [n_bodies+1] */
