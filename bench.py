@@ -750,18 +750,21 @@ class GossipRoundWire(GossipRound):
 class ServerMerge(Workload):
     """The path a Go caller of merge() actually hits (main.go:245-257):
     configs[0]'s 5 replicas x 10k Diff entries (main.go:319-321), each
-    pulling a peer's Diff.  A step = for every Server, the gossip pull decode
-    of the peer's body into RemoteDiff (crdt_server_ingest_binary,
-    main.go:245-256) and then ONE crdt_servers_merge of all five: the host
-    pack of Diff + RemoteDiff, H2D, the RefMerge kernels, D2H and the
-    rebuild of Diff / CurrentState (server.hip).  Re-merging the same pull is
-    a no-op on the state (KAT-5), so every step does the same work.  Host-
-    and PCIe-bound by construction; the roofline object is not meaningful
-    here (reported against the device bytes for completeness)."""
+    pulling a peer's Diff.  A step = for every Server, the ingest of the
+    peer's binary gossip body (crdt_server_ingest_binary, main.go:245-256:
+    host validation, the body parked in pinned memory) and then ONE
+    crdt_servers_merge of all five: H2D of the parked bodies, device decode
+    against the context's string tables, the RefMerge kernels over the
+    HBM-resident Diffs, the device split back into each server's next Diff,
+    and the CurrentState rebuild on the host (server.hip).  Re-merging the
+    same pull is a no-op on the state (KAT-5), so every step does the same
+    work.  Latency-bound by construction (a few hundred microseconds of
+    kernels, host waits between them); the roofline object is reported
+    against the device bytes for completeness."""
     name = "server_merge"
     unit = "remote-entries/s"
     dtype = "int64"
-    kernel = "crdt_servers_merge end to end (host pack + H2D + refmerge kernels + D2H + unpack)"
+    kernel = "crdt_servers_merge end to end (ingest + H2D + device decode + refmerge kernels + split + state)"
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         from crdt_amd import refmerge, server, synth

@@ -332,8 +332,16 @@ class Population:
 
 
 def random_peers(rng: np.random.Generator, total: int, first: int, count: int) -> np.ndarray:
-    """A random friend other than itself for each of replicas [first, first+count)
-    (friendList = every other server, main.go:306-317)."""
+    """A random peer other than itself for each of replicas [first, first+count).
+
+    The reference draws uniformly from friendList (main.go:230), which is
+    ports 8080..8089 (main.go:219-222): that list holds the server itself
+    and ports no server listens on, so some of its rounds pull its own Diff
+    (a no-op merge: equal keys keep the local entry, main.go:54-65) or fail
+    the request and skip (main.go:235-237).  This schedule keeps only the
+    rounds that move data: a uniform draw over the OTHER live replicas.  A
+    self-pull or a skipped round changes no state, so the reachable states
+    are the reference's; only the per-round pull rate differs."""
     r = rng.integers(0, total - 1, size=total)
     ids = np.arange(total)
     peers = np.where(r >= ids, r + 1, r)
