@@ -67,14 +67,14 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 //   k_rm_plan_small / scan : tiles per replica;
 //   k_rm_split : one wave per tile: its geometry and 16-ary merge-path split
 //                -> descriptors (plus the Atoi / accumulator-reset prep);
-//   k_rm_count : merge (256 threads x MI items): inserted-R count per tile
-//                and every entry's rank among the tile's emitted entries;
+//   k_rm_count : merge (256 threads x MI items): inserted-R count per tile;
 //   scan of the counts -> each tile's output offset, out.off;
-//   k_rm_write : the tile's new-Diff slice staged in LDS by rank, written
-//                coalesced;
-//   k_rm_fold  : the replay (main.go:75-98) of the tile's emitted
-//                remote-origin entries into an LDS table keyed by slot,
-//                flushed with one set of global atomics per (tile, slot);
+//   k_rm_tile  : re-merge (512 threads x FI items), each entry's rank among
+//                the tile's emitted entries; the tile's new-Diff slice
+//                staged in LDS by rank and written coalesced; the replay
+//                (main.go:75-98) of the tile's emitted remote-origin entries
+//                into an LDS table keyed by slot, flushed with one set of
+//                global atomics per (tile, slot);
 //   k_slot_final: per-slot closed form.
 // The replay's per-key state is order-free: best = max over holders of
 // (rank in the replica's merge sequence) << 32 | string id (the max-ts
@@ -83,11 +83,12 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 // binary searches over the logs, and a per-replica replay pass re-reading
 // the new Diff, were each bound by chains of dependent global loads; every
 // tile pass here is still latency-bound at 2-4 TB/s, see DESIGN.md.)
-constexpr int MT = 2048;                  // merge items per tile
-constexpr int MB = 256;                   // threads per tile
+constexpr int MT = 4096;                  // merge items per tile
+constexpr int MB = 512;                   // threads per tile (count pass)
 constexpr int MI = MT / MB;               // items per thread
 constexpr int TT = 512;                   // LDS replay-table entries per tile
-constexpr int FB = 512;                   // threads of the replay-fold kernel (one tile each)
+constexpr int FB = 1024;                  // threads of the tile pass (one tile each)
+constexpr int NW = MT / 64;               // 64-bit words per merge bitmap of a tile
 constexpr int FI = MT / FB;               // entries per fold thread
 #ifndef RM_SPLIT_PW
 #define RM_SPLIT_PW 16                    // merge-path search width (probing lanes)
@@ -304,18 +305,24 @@ __device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na,
     uint32_t ia = lo, ib = k0 - lo;
     const uint32_t ia0 = ia;
     uint32_t fl = 0, fe = 0;
+    // the two heads and the L entry before the L head stay in registers: one
+    // LDS read (the new head) per step
+    int64_t ha = ia < na ? sm[1 + ia] : 0, hb = ib < nb ? sm[1 + na + ib] : 0;
+    int64_t pl = sm[ia];                                 // L entry just before (global a0+ia-1)
+    bool hp = ia > 0 || has_prev0;
     for (uint32_t k = k0, i = 0; k < k1; ++k, ++i) {
-        const bool take_l = ia < na && (ib >= nb || sm[1 + ia] <= sm[1 + na + ib]);
+        const bool take_l = ia < na && (ib >= nb || ha <= hb);
         if (take_l) {
             fl |= 1u << i;
             fe |= 1u << i;
+            pl = ha;
+            hp = true;
             ++ia;
+            if (ia < na) ha = sm[1 + ia];
         } else {
-            const int64_t r = sm[1 + na + ib];
-            const bool has_prev = ia > 0 || has_prev0;
-            const bool dup = has_prev && sm[ia] == r;    // sm[ia] = L entry just before (global a0+ia-1)
-            if (r < maxl && !dup) fe |= 1u << i;
+            if (hb < maxl && !(hp && pl == hb)) fe |= 1u << i;
             ++ib;
+            if (ib < nb) hb = sm[1 + na + ib];
         }
     }
     *isl = fl;
@@ -323,6 +330,7 @@ __device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na,
     return ia0;
 }
 
+template <int NT>
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_w, uint32_t *total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t x = v;
@@ -333,7 +341,8 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_w, ui
     if (lane == 63) s_w[w] = x;
     __syncthreads();
     uint32_t base = 0, tot = 0;
-    for (int k = 0; k < MB / 64; ++k) {
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
         base += k < w ? s_w[k] : 0;
         tot += s_w[k];
     }
@@ -373,17 +382,19 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
     }
 }
 
-// Pass 1: inserted-R count of each tile, and every entry's rank among the
-// tile's emitted entries (1-based; 0 = an R entry that is not inserted).
-// The rank is the entry's offset in the tile's new-Diff slice (the write
-// pass scatters by it without re-merging) and, offset by the tile's first
-// diagonal, orders the replica's new Diff like its ts for the replay fold.
-// Grid = the tile-count upper bound.
+// Pass 1: the merge of each tile's ts in LDS (one merge per tile, the only
+// one): its inserted-R count, and the merge written out as two bitmaps in
+// merge order -- bit k of isl = merge item k is an L entry, bit k of emit =
+// it is emitted (every L entry; the inserted R entries) -- 512 B per tile,
+// bits[t * 64 + w] (w < 32: isl words, w >= 32: emit words).  The tile pass
+// reads every entry's position from them instead of merging again (a
+// second merge in the tile pass, or a 2-byte rank per entry written and
+// read back, each cost more).  Grid = the tile-count upper bound.
 __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
-                                                 uint32_t *__restrict__ tcnt, uint16_t *__restrict__ l_dk,
-                                                 uint16_t *__restrict__ r_dk, uint32_t *__restrict__ zero) {
+                                                 uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
+                                                 uint32_t *__restrict__ zero) {
+    static_assert(MI == 8, "one byte of each bitmap per thread");
     __shared__ int64_t sm[MT + 1];
-    __shared__ uint16_t s_dk[MT];                        // entry (L: li, R: na + li) -> emitted rank + 1
     __shared__ uint32_t s_w[MB / 64];
     const uint64_t t = blockIdx.x;
     if (zero && t == 0 && threadIdx.x == 0) *zero = 0;   // (the delta fold's overflow flag)
@@ -398,65 +409,79 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
     load_tile_ts(in, d, na, n, sm);
     const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
     const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
-    uint32_t isl, emit;
-    const uint32_t ia0 = thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
-    // one block scan of (emitted, inserted R) packed in 16-bit halves (<= MT each)
-    uint32_t total;
-    uint32_t pos = block_excl_sum((uint32_t)__popc(emit) | (uint32_t)__popc(emit & ~isl) << 16, s_w, &total) & 0xFFFFu;
-    {
-        uint32_t ia = ia0, ib = k0 - ia0;
-        for (uint32_t i = 0; i < k1 - k0; ++i) {
-            const uint16_t dk = (emit >> i & 1u) ? (uint16_t)(++pos) : (uint16_t)0;
-            if (isl >> i & 1u) s_dk[ia++] = dk;
-            else s_dk[na + ib++] = dk;
-        }
+    uint32_t isl = 0, emit = 0;
+    if (k0 < k1) (void)thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
+    // 8 lanes' bytes -> one 64-bit word of each bitmap
+    const int lane = threadIdx.x & 63, sh = (lane & 7) * 8;
+    uint64_t wl = (uint64_t)isl << sh, we = (uint64_t)emit << sh;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        wl |= (uint64_t)__shfl_xor((unsigned long long)wl, o);
+        we |= (uint64_t)__shfl_xor((unsigned long long)we, o);
     }
+    if ((lane & 7) == 0) {
+        const uint32_t w = threadIdx.x >> 3;
+        bits[t * 2 * NW + w] = wl;
+        bits[t * 2 * NW + NW + w] = we;
+    }
+    uint32_t x = (uint32_t)__popc(emit & ~isl);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) s_w[threadIdx.x >> 6] = x;
     __syncthreads();
-    if (threadIdx.x == 0) tcnt[t] = total >> 16;
-    if (l_dk)
-        for (uint32_t k = threadIdx.x; k < na; k += MB) l_dk[d.l0 + k] = s_dk[k];
-    for (uint32_t k = threadIdx.x; k < nb; k += MB) r_dk[d.r0 + k] = s_dk[na + k];
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < MB / 64; ++k) tot += s_w[k];
+        tcnt[t] = tot;
+    }
 }
 
-// Replay fold (main.go:75-98) of one tile's emitted remote-origin entries
+enum { RM_FOLD_NONE = 0, RM_FOLD_FULL = 1, RM_FOLD_DELTA = 2 };
+
+// Pass 2, one workgroup per tile, in merge order: wave w's lanes take merge
+// items k = 64 (w + NWV i) + lane (i < FI), so each load instruction covers 64
+// consecutive merge items -- two contiguous runs, one of L and one of R.  An
+// item's L / R index and its rank among the tile's emitted entries are
+// prefix counts of the count pass's bitmaps (one word per wave and item
+// slot: the word prefix by shuffles over the tile's 64 words, the bit
+// prefix by mbcnt), so no merge, LDS staging or barrier stands before the
+// entry loads.  Emitted entries are stored straight from registers at
+// their rank in the tile's slice (consecutive across the emitting lanes).
+// The replay fold (main.go:75-98) of the emitted remote-origin entries runs
 // into an LDS table keyed by slot, flushed with one set of global atomics
-// per (tile, slot).  An entry's rank in the replica's merge sequence
-// (d0 + dk) orders the replica's new Diff like its ts, so best = rank << 32
-// | string id picks the max-ts holder without knowing output positions.
-// FI entries per thread (e = tid + f*FB, coalesced), every load of the
-// batch issued before the first atomic; an entry's kv end is the next
-// lane's kv start (a shuffle).  Further kvs of an entry (rare: the
-// reference's load generator writes one kv per entry) take a tail loop.
-// WRITE: the same pass also writes the tile's new-Diff slice (k_rm_write's
-// work: the entries it already reads are staged in LDS by their rank).
-// DELTA (with WRITE): the incremental replay's first phase instead -- only
-// the inserted R entries are folded, keyed by ts ^ 2^63, into the carried
-// state st (max, holder count, wrapped sum, parsable count).
-template <bool WRITE, bool DELTA = false>
-__global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
-                                                const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
+// per (tile, slot).  An entry's rank in the replica's merge sequence (d0 +
+// its 1-based rank in the tile) orders the replica's new Diff like its ts,
+// so best = rank << 32 | string id picks the max-ts holder without knowing
+// output positions.  Further kvs of an entry (rare: the reference's load
+// generator writes one kv per entry) take a tail loop.
+//   FOLD == RM_FOLD_NONE : slice write only (no slots, or the timing diag)
+//   FOLD == RM_FOLD_FULL : + the replay fold into acc
+//   FOLD == RM_FOLD_DELTA: + the incremental replay's first phase -- only
+//        the inserted R entries, keyed by ts ^ 2^63, into the carried state st
+//        (max, holder count, wrapped sum, parsable count); each R entry's
+//        rank (0: not inserted) goes to r_dk for the holder pass's
+//        overflow walk.
+template <int FOLD>
+__global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                const uint64_t *__restrict__ bits, uint16_t *__restrict__ r_dk,
                                                 const OkVal *__restrict__ okv, SlotAcc acc, int diag,
-                                                const uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ ic,
-                                                crdt_refmerge_out out, crdt_replay_state st,
-                                                RpCand *__restrict__ cand, uint32_t *__restrict__ cand_n,
-                                                uint32_t *__restrict__ ovf) {
-    static_assert(WRITE || !DELTA, "the delta fold runs inside the write pass");
-    __shared__ uint32_t t_slot[TT];
+                                                const uint64_t *__restrict__ ic, crdt_refmerge_out out,
+                                                crdt_replay_state st, RpCand *__restrict__ cand,
+                                                uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf) {
+    constexpr int NWV = FB / 64;                         // waves
+    static_assert(FI * NWV == NW, "each wave takes FI words of 64 items");
+    constexpr bool DELTA = FOLD == RM_FOLD_DELTA, FOLDS = FOLD != RM_FOLD_NONE;
+    constexpr int TN = FOLDS ? TT : 1;
+    __shared__ uint32_t t_slot[TN];
     __shared__ uint32_t t_nh[DELTA ? TT : 1];
+    __shared__ unsigned long long t_key[DELTA ? TT : 1];   // DELTA: max ts ^ 2^63 of each entry
     __shared__ uint32_t s_nc, s_ovf;
-    __shared__ unsigned long long t_best[TT];
-    __shared__ unsigned long long t_sum[TT];
-    __shared__ uint32_t t_npar[TT];
-    __shared__ int64_t s_ts[WRITE ? MT : 1];
-    __shared__ uint16_t s_idx[WRITE ? MT : 1];
-    __shared__ uint8_t s_org[WRITE ? MT : 1];
-    __shared__ int64_t s_okval[OKC];
-    __shared__ uint8_t s_okok[OKC];
-    // DELTA: string of the tile's max holder of each table entry, over the
-    // Atoi records (read for the last time before the fold's closing barrier;
-    // keeps four workgroups' LDS within a CU)
-    static_assert(OKC * sizeof(int64_t) >= TT * sizeof(uint32_t), "t_str alias");
-    uint32_t *t_str = reinterpret_cast<uint32_t *>(s_okval);
+    __shared__ unsigned long long t_best[TN];
+    __shared__ unsigned long long t_sum[TN];
+    __shared__ uint32_t t_npar[TN];
+    __shared__ int64_t s_okval[FOLDS ? OKC : 1];
+    __shared__ uint8_t s_okok[FOLDS ? OKC : 1];
     const uint64_t t = blockIdx.x;
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
@@ -466,75 +491,116 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
         if (DELTA && threadIdx.x == 0) cand_n[t] = 0;
         return;
     }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the tile's bitmap words, one of each bitmap per lane, and their
+    // exclusive prefix popcounts
+    static_assert(NW == 64, "one word of each bitmap per lane");
+    const uint64_t word_l = bits[t * 2 * NW + lane], word_e = bits[t * 2 * NW + NW + lane];
+    uint32_t pre_l = (uint32_t)__popcll(word_l), pre_e = (uint32_t)__popcll(word_e);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yl = __shfl_up(pre_l, o), ye = __shfl_up(pre_e, o);
+        if (lane >= o) {
+            pre_l += yl;
+            pre_e += ye;
+        }
+    }
+    pre_l -= (uint32_t)__popcll(word_l);
+    pre_e -= (uint32_t)__popcll(word_e);
+    const uint64_t ob = d.l0 + ic[t];
     if (DELTA && threadIdx.x == 0) s_nc = s_ovf = 0;
-    uint32_t total = 0;
-    uint64_t ob = 0;
-    if (WRITE) {
-        total = na + tcnt[t];
-        ob = d.l0 + ic[t];
-    }
-    const int lane = threadIdx.x & 63;
-    for (int h = threadIdx.x; h < TT; h += FB) {
-        t_slot[h] = kEmpty;
-        t_best[h] = 0;
-        t_sum[h] = 0;
-        t_npar[h] = 0;
-        if (DELTA) t_nh[h] = 0;
-    }
+    if (FOLDS)
+        for (int h = threadIdx.x; h < TT; h += FB) {
+            t_slot[h] = kEmpty;
+            t_best[h] = 0;
+            t_sum[h] = 0;
+            t_npar[h] = 0;
+            if (DELTA) {
+                t_nh[h] = 0;
+                t_key[h] = 0;
+            }
+        }
     // a small string table (the reference's load generator writes ten
     // values, main.go:282) is staged in LDS: the Atoi lookup leaves the
     // chain of dependent global loads (kv range -> kv pair -> Atoi record)
-    const bool okc = in.n_str <= OKC;
+    const bool okc = FOLDS && in.n_str <= OKC;
     if (okc && threadIdx.x < in.n_str) {
         const OkVal o = okv[threadIdx.x];
         s_okval[threadIdx.x] = o.val;
         s_okok[threadIdx.x] = (uint8_t)(o.ok != 0);
     }
-    uint64_t e_kb[FI], e_k1[FI];
-    uint32_t e_dk[FI], e_cnt[FI], e_slot[FI], e_v[FI];
-    uint8_t e_org[FI];
+    // per item slot f: merge item k = 64 * (wv + NWV f) + lane.  The words
+    // and their prefixes are wave-uniform (scalar registers); an item's
+    // flags, L / R index and rank are recomputed from them where used.
+    uint64_t s_wl[FI], s_we[FI];
+    uint32_t s_pl[FI], s_pe[FI];
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        const int w = wvu + NWV * f;
+        // (readlane returns int: widen through uint32_t, never sign-extend)
+        s_wl[f] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_l >> 32), w) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_l, w);
+        s_we[f] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_e >> 32), w) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_e, w);
+        s_pl[f] = (uint32_t)__builtin_amdgcn_readlane(pre_l, w);
+        s_pe[f] = (uint32_t)__builtin_amdgcn_readlane(pre_e, w);
+    }
+    auto below = [&](uint64_t m) -> uint32_t {          // set bits of m below this lane
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
+    auto it_in = [&](int f) { return 64u * (uint32_t)(wvu + NWV * f) + (uint32_t)lane < n; };
+    auto it_l = [&](int f) { return (bool)((s_wl[f] >> lane) & 1); };
+    auto it_em = [&](int f) { return (bool)((s_we[f] >> lane) & 1); };
+    auto it_rk = [&](int f) { return s_pe[f] + below(s_we[f]); };        // rank among the emitted (0-based)
+    auto it_gi = [&](int f) -> uint64_t {                                // global L / R index
+        const uint32_t li = s_pl[f] + below(s_wl[f]);
+        return it_l(f) ? d.l0 + li : d.r0 + (64u * (uint32_t)(wvu + NWV * f) + (uint32_t)lane - li);
+    };
+    uint64_t e_kb[FI], e_ke[FI];
     int64_t e_ts[FI];
+    uint32_t e_cnt[FI], e_slot[FI], e_v[FI];
+    uint8_t e_org[FI];
 #pragma unroll
     for (int f = 0; f < FI; ++f) {                       // every entry load issued before the first use
-        const uint32_t e = threadIdx.x + (uint32_t)f * FB;
-        const bool r = e >= na;
-        const uint64_t gi = r ? d.r0 + (e - na) : d.l0 + e;
-        const uint64_t *kv = (r ? in.r_kv : in.l_kv) + gi;
-        const bool in_tile = e < n;
-        const bool edge = lane == 63 || e + 1 == na || e + 1 >= n;   // kv end not in the next lane
-        e_kb[f] = in_tile ? kv[0] : 0;
-        e_k1[f] = (in_tile && edge) ? kv[1] : 0;
-        e_dk[f] = in_tile ? (r ? r_dk[gi] : l_dk[gi]) : 0u;
-        e_org[f] = (in_tile && !r) ? in.l_origin[gi] : 0;
-        e_ts[f] = (WRITE && in_tile) ? (r ? in.r_ts[gi] : in.l_ts[gi]) : 0;
+        const bool in_tile = it_in(f), il = it_l(f);
+        const uint64_t gi = it_gi(f);
+        const uint64_t *kv = (il ? in.l_kv : in.r_kv) + gi;
+        e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
+        e_org[f] = (in_tile && il) ? in.l_origin[gi] : 0;
+        e_kb[f] = (FOLDS && in_tile) ? kv[0] : 0;
+        e_ke[f] = (FOLDS && in_tile) ? kv[1] : 0;
     }
+    if (FOLDS) {
 #pragma unroll
-    for (int f = 0; f < FI; ++f) {
-        const uint32_t e = threadIdx.x + (uint32_t)f * FB;
-        const bool r = e >= na;
-        const bool edge = lane == 63 || e + 1 == na || e + 1 >= n;
-        const uint64_t kb = e_kb[f];
-        const uint64_t nxt = __shfl_down(kb, 1);
-        uint32_t dk = e_dk[f];
-        if (WRITE && dk) {
-            const uint32_t p = dk - 1u;
-            if (p < MT) {
-                s_ts[p] = e_ts[f];
-                s_idx[p] = (uint16_t)(r ? 0x8000u | (e - na) : e);
-                s_org[p] = e_org[f];
-            }
+        for (int f = 0; f < FI; ++f) {
+            // *Command values are skipped by the replay (main.go:80); the
+            // delta folds only the inserted R entries
+            const bool cand_e = it_em(f) && !e_org[f] && !(DELTA && it_l(f));
+            const uint64_t kb = e_kb[f], ke = e_ke[f] < in.n_kv ? e_ke[f] : in.n_kv;   // malformed ranges stay in bounds
+            e_cnt[f] = (cand_e && kb < ke) ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
         }
-        if (e_org[f] || (DELTA && !r)) dk = 0;           // *Command: skipped by the replay (main.go:80)
-        uint64_t ke = edge ? e_k1[f] : nxt;
-        ke = ke < in.n_kv ? ke : in.n_kv;                 // malformed ranges stay in bounds
-        e_dk[f] = dk;
-        e_cnt[f] = (dk && kb < ke) ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
+#pragma unroll
+        for (int f = 0; f < FI; ++f) {
+            e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
+            e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
+        }
     }
+    // the slice, straight from registers (every L entry of the tile and its
+    // inserted R entries, at their rank)
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
-        e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
-        e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
+        const bool il = it_l(f), em = it_em(f);
+        const uint64_t gi = it_gi(f);
+        if (em) {
+            const uint64_t o = ob + it_rk(f);
+            out.ts[o] = e_ts[f];
+            out.src[o] = il ? (int64_t)gi : -(int64_t)gi - 1;
+            out.origin[o] = e_org[f];
+        }
+        if (DELTA && it_in(f) && !il) r_dk[gi] = em ? (uint16_t)(it_rk(f) + 1) : (uint16_t)0;
     }
+    if (!FOLDS) return;
     OkVal e_o[FI];
     if (!okc)
 #pragma unroll
@@ -542,25 +608,18 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
             e_o[f] = OkVal{0, 0};
             if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
         }
-    __syncthreads();                                     // table initialised (and the slice staged)
+    __syncthreads();                                     // table initialised, Atoi records staged
     if (okc)
 #pragma unroll
         for (int f = 0; f < FI; ++f) {
             e_o[f] = OkVal{0, 0};
             if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = OkVal{s_okval[e_v[f]], s_okok[e_v[f]]};
         }
-    if (WRITE)
-        for (uint32_t k = threadIdx.x; k < total; k += FB) {
-            const uint32_t id = s_idx[k], li = id & 0x7FFFu;
-            const bool r = id >> 15;
-            out.ts[ob + k] = s_ts[k];
-            out.src[ob + k] = r ? -(int64_t)(d.r0 + li) - 1 : (int64_t)(d.l0 + li);
-            out.origin[ob + k] = s_org[k];
-        }
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
         if (!e_cnt[f]) continue;
-        const uint64_t rank = DELTA ? (uint64_t)e_ts[f] ^ 0x8000000000000000ull : d.d0 + e_dk[f];
+        const uint64_t rank = d.d0 + it_rk(f) + 1;
+        const uint64_t key = (uint64_t)e_ts[f] ^ 0x8000000000000000ull;   // DELTA: the ts-keyed max
         for (uint32_t j = 0; j < e_cnt[f]; ++j) {
             uint32_t slot = e_slot[f], v = e_v[f];
             OkVal o = e_o[f];
@@ -574,9 +633,12 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
                 fold_pair(t_slot, t_best, t_sum, t_npar, acc, true, slot, v, rank, o.ok != 0, o.val);
                 continue;
             }
+            // within a tile the merge rank orders entries like their ts: the
+            // max-rank holder (rank << 32 | string) is the max-ts holder
             const uint32_t idx = table_find(t_slot, slot);
             if (idx != kEmpty) {
-                atomicMax(&t_best[idx], (unsigned long long)rank);
+                atomicMax(&t_best[idx], (unsigned long long)(rank << 32 | v));
+                atomicMax(&t_key[idx], (unsigned long long)key);
                 atomicAdd(&t_nh[idx], 1u);
                 if (o.ok) {
                     atomicAdd(&t_sum[idx], (unsigned long long)o.val);   // mod 2^64 (main.go:95)
@@ -584,7 +646,7 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
                 }
             } else {                                     // table full: straight to the state
                 s_ovf = 1;                               // (the holder pass then walks the entries)
-                atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), (unsigned long long)rank);
+                atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), (unsigned long long)key);
                 atomicAdd(&st.nhold[slot], 1u);
                 if (o.ok) {
                     atomicAdd(reinterpret_cast<unsigned long long *>(&st.sum[slot]), (unsigned long long)o.val);
@@ -595,28 +657,13 @@ __global__ __launch_bounds__(FB) void k_rm_fold(crdt_refmerge_in in, const TileD
     }
     __syncthreads();
     if (diag == 2) return;
-    if (DELTA) {                                         // each slot's tile-local max holder -> t_str
-#pragma unroll
-        for (int f = 0; f < FI; ++f) {
-            if (!e_cnt[f]) continue;
-            const uint64_t key = (uint64_t)e_ts[f] ^ 0x8000000000000000ull;
-            for (uint32_t j = 0; j < e_cnt[f]; ++j) {
-                const uint32_t slot = j ? in.kv_key[e_kb[f] + j] : e_slot[f];
-                const uint32_t v = j ? in.kv_val[e_kb[f] + j] : e_v[f];
-                if (slot >= in.n_slots || v >= in.n_str) continue;
-                const uint32_t idx = table_find(t_slot, slot);   // present, or the window was full
-                if (idx != kEmpty && t_best[idx] == key) t_str[idx] = v;   // ts unique: one holder
-            }
-        }
-        __syncthreads();
-    }
     for (int h = threadIdx.x; h < TT; h += FB) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;
         if (DELTA) {
             const uint32_t c = atomicAdd(&s_nc, 1u);
-            cand[(uint64_t)t * TT + c] = RpCand{t_best[h], slot, t_str[h]};
-            atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), t_best[h]);
+            cand[t * TT + c] = RpCand{t_key[h], slot, (uint32_t)t_best[h]};
+            atomicMax(reinterpret_cast<unsigned long long *>(&st.best_key[slot]), t_key[h]);
             atomicAdd(&st.nhold[slot], t_nh[h]);
             if (t_npar[h]) {
                 atomicAdd(reinterpret_cast<unsigned long long *>(&st.sum[slot]), t_sum[h]);
@@ -668,56 +715,6 @@ __global__ __launch_bounds__(64) void k_rp_holder(crdt_refmerge_in in, const uin
             const RpCand c = cand[t * TT + h];
             if (st.best_key[c.slot] == c.key) st.best_str[c.slot] = c.str;
         }
-    }
-}
-
-// Pass 2: the tile's new-Diff slice.  Every L entry is emitted and the
-// count pass ranked each emitted entry within the tile, so the slice is
-// staged in LDS by rank (no re-merge) and written coalesced.  ic = exclusive
-// scan of tcnt: inserted R entries before tile t (all replicas), so the
-// slice starts at l_off[p] + a0 + ic[t] = l0 + ic[t].
-__global__ __launch_bounds__(MB) void k_rm_write(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
-                                                 const uint16_t *__restrict__ l_dk, const uint16_t *__restrict__ r_dk,
-                                                 const uint32_t *__restrict__ tcnt, const uint64_t *__restrict__ ic,
-                                                 crdt_refmerge_out out) {
-    __shared__ int64_t s_ts[MT];
-    __shared__ uint16_t s_idx[MT];                       // output slot -> entry (bit 15: R)
-    __shared__ uint8_t s_org[MT];
-    const uint64_t t = blockIdx.x;
-    const TileDesc d = desc[t], dn = desc[t + 1];
-    uint32_t na, nb;
-    tile_counts(d, dn, &na, &nb);
-    if (na + nb == 0) return;
-    const uint32_t n = na + nb, total = na + tcnt[t];
-    const uint64_t ob = d.l0 + ic[t];
-    uint32_t dk[MI];
-    int64_t ts[MI];
-    uint8_t org[MI];
-#pragma unroll
-    for (int j = 0; j < MI; ++j) {                       // every load issued before the first LDS store
-        const uint32_t k = threadIdx.x + (uint32_t)j * MB;
-        const bool r = k >= na;
-        const uint64_t gi = r ? d.r0 + (k - na) : d.l0 + k;
-        dk[j] = k < n ? (r ? r_dk[gi] : l_dk[gi]) : 0u;   // every L entry is emitted (dk >= 1)
-        ts[j] = k < n ? (r ? in.r_ts[gi] : in.l_ts[gi]) : 0;
-        org[j] = k < na ? in.l_origin[gi] : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < MI; ++j) {
-        const uint32_t k = threadIdx.x + (uint32_t)j * MB, p = dk[j] - 1u;
-        if (dk[j] && p < MT) {
-            s_ts[p] = ts[j];
-            s_idx[p] = (uint16_t)(k < na ? k : 0x8000u | (k - na));
-            s_org[p] = org[j];
-        }
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < total; k += MB) {
-        const uint32_t id = s_idx[k], li = id & 0x7FFFu;
-        const bool r = id >> 15;
-        out.ts[ob + k] = s_ts[k];
-        out.src[ob + k] = r ? -(int64_t)(d.r0 + li) - 1 : (int64_t)(d.l0 + li);
-        out.origin[ob + k] = s_org[k];
     }
 }
 
@@ -918,9 +915,9 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     const size_t tmax = (in.n_l + nr) / MT + np + 1;             // >= tiles over all replicas
     if (tmax > 0x7fffffffULL) return CRDT_E_RANGE;
     const size_t need = Carve::round(np * 4 + 4) + Carve::round((np + 1) * 8) + scan_tmp_bytes(std::max(np, tmax)) +
-                        Carve::round((tmax + 1) * sizeof(TileGeo)) * 2 + Carve::round(tmax * 8 + 8) +
-                        Carve::round(tmax * 4 + 4) + Carve::round((nstr + 1) * sizeof(OkVal)) +
-                        Carve::round(in.n_l * 2 + 2) + Carve::round(nr * 2 + 2) +
+                        Carve::round((tmax + 1) * sizeof(TileDesc)) + Carve::round(tmax * 8 + 8) +
+                        Carve::round(tmax * 4 + 4) + Carve::round(tmax * 2 * NW * 8) + Carve::round((nstr + 1) * sizeof(OkVal)) +
+                        (delta ? Carve::round(nr * 2 + 2) : 0) +
                         Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) + 4096 +
                         (delta ? Carve::round(tmax * TT * sizeof(RpCand)) + Carve::round(tmax * 4 + 4) + 256 : 0);
     rc = ws_reserve(ctx, need);
@@ -933,8 +930,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     TileDesc *desc = w.take<TileDesc>(tmax + 1);
     uint64_t *ic = w.take<uint64_t>(tmax + 1);
     uint32_t *tcnt = w.take<uint32_t>(tmax + 1);
-    uint16_t *l_dk = w.take<uint16_t>(in.n_l + 1);
-    uint16_t *r_dk = w.take<uint16_t>(nr + 1);
+    uint64_t *bits = w.take<uint64_t>(tmax * 2 * NW);             // per tile: merge-order isl / emit bitmaps
+    uint16_t *r_dk = delta ? w.take<uint16_t>(nr + 1) : nullptr; // delta: inserted R ranks (holder overflow walk)
     RpCand *cand = delta ? w.take<RpCand>(tmax * TT) : nullptr;   // delta: per-tile max-holder candidates
     uint32_t *cand_n = delta ? w.take<uint32_t>(tmax + 1) : nullptr;
     uint32_t *ovf = delta ? w.take<uint32_t>(4) : nullptr;        // a tile's LDS table overflowed
@@ -964,7 +961,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, maxl_dev, tmax, desc, okv, acc,
                                                            (uint32_t)ns);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
-    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, l_dk, r_dk, ovf);
+    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf);
     rc = check_launch(ctx);
     if (rc) return rc;
     // (a completion ticket letting the count pass's last block do this scan
@@ -977,29 +974,25 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
-    const bool fused = ns && g_rm_diag == 0;                      // the replay fold also writes the slice
-    if (!fused) k_rm_write<<<(unsigned)tmax, MB, 0, s>>>(in, desc, l_dk, r_dk, tcnt, ic, out);
-    if (delta) {                                                  // incremental replay: fold only the inserted R
-        if (fused)                                                // (its first phase, with the slice write)
-            k_rm_fold<true, true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out,
-                                                                 *delta, cand, cand_n, ovf);
+    // the tile pass: slice write and (with slots) the replay fold
+    const unsigned tg = (unsigned)tmax;
+    if (delta && ns) {                                            // incremental replay: fold only the inserted R
+        k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, 0, ic, out, *delta, cand, cand_n,
+                                                   ovf);
         rc = check_launch(ctx);
         if (rc) return rc;
-        if (!ns) return CRDT_OK;
-        if (fused) {                                              // second phase: the candidates' holders
-            k_rp_holder<<<(unsigned)tmax, 64, 0, s>>>(in, r_dk, *delta, cand, cand_n, ovf, tmax);
-            rc = check_launch(ctx);
-            if (rc) return rc;
-        }
-        return rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, fused);
+        k_rp_holder<<<tg, 64, 0, s>>>(in, r_dk, *delta, cand, cand_n, ovf, tmax);   // the candidates' holders
+        rc = check_launch(ctx);
+        if (rc) return rc;
+        return rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, true);
     }
-    if (ns && g_rm_diag != 1) {                                   // (diag 1: timing without the replay fold)
-        if (fused)
-            k_rm_fold<true><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, 0, tcnt, ic, out,
-                                                           crdt_replay_state{}, nullptr, nullptr, nullptr);
-        else
-            k_rm_fold<false><<<(unsigned)tmax, FB, 0, s>>>(in, desc, l_dk, r_dk, okv, acc, g_rm_diag, tcnt, ic, out,
-                                                            crdt_replay_state{}, nullptr, nullptr, nullptr);
+    if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
+        k_rm_tile<RM_FOLD_NONE><<<tg, FB, 0, s>>>(in, desc, bits, nullptr, okv, acc, 0, ic, out, crdt_replay_state{},
+                                                  nullptr, nullptr, nullptr);
+        if (!ns || delta) return check_launch(ctx);
+    } else {
+        k_rm_tile<RM_FOLD_FULL><<<tg, FB, 0, s>>>(in, desc, bits, nullptr, okv, acc, g_rm_diag, ic, out,
+                                                  crdt_replay_state{}, nullptr, nullptr, nullptr);
     }
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
     return check_launch(ctx);

@@ -1,5 +1,6 @@
 """GPU: RefMerge on adversarial batch shapes -- replica logs sized around the
-2048-item tile (2047 / 2048 / 2049 / many tiles / one side empty / both
+tile (4096 merge items; 2048 before) and its bitmap words (64 items):
+n-1 / n / n+1 / many tiles / one side empty / both
 empty), ts at the int64 extremes and negative, heavy L/R collisions at tile
 edges, 1-2 kv pairs per entry -- replica by replica against the C oracle,
 through the full re-fold and through the incremental replay."""
@@ -15,7 +16,8 @@ K = 16
 I64 = np.iinfo(np.int64)
 STRS = [str(v) for v in range(-5, 6)] + ["x", "007", "+3", "9223372036854775807", "-9223372036854775808", ""]
 SHAPES = [(0, 0), (0, 5), (5, 0), (2047, 1), (1, 2047), (2048, 2048), (2049, 0), (0, 2049), (3000, 3000),
-          (1, 1), (6000, 10), (10, 6000), (4095, 4097), (0, 0), (700, 700)]
+          (1, 1), (6000, 10), (10, 6000), (4095, 4097), (0, 0), (700, 700),
+          (4095, 1), (1, 4095), (4096, 1), (4097, 0), (0, 4097), (8193, 3), (63, 1), (64, 64), (65, 0)]
 
 
 def _batch(seed):
