@@ -908,6 +908,12 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))          # before any GPU call in this process
+    # The result line is the only thing this process writes to stdout: native
+    # libraries (RCCL's version banner at communicator init) print to fd 1,
+    # so fd 1 is pointed at stderr and the line goes to the saved stdout.
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     world, rank, local = dist_init()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a mismatched n_gpus")
@@ -983,7 +989,8 @@ def main():
         }
         if hasattr(wl, "extra"):
             out.update(wl.extra(avg_ms))
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(result_fd, (json.dumps(out) + "\n").encode())
     if getattr(wl, "comm", None) is not None:
         wl.comm.close()                               # before the engine whose context it borrows
     if world > 1:

@@ -1,7 +1,13 @@
 #!/usr/bin/env python3
 """Fold a tools/profile.sh run into committed evidence under profiles/.
 
-    python tools/pmc_summary.py <workload> <kernel-substring> [round-tag] [launches-per-step]
+    python tools/pmc_summary.py <workload> <kernel-substrings> [round-tag] [launches-per-step]
+
+<kernel-substrings>: one substring, or several separated by commas for a
+multi-kernel step (the first names the anchor kernel: its launch count is
+the number of steps profiled; the counters of every matching kernel are
+summed and divided by it, so the traffic covers the whole step like the
+bench's whole-op bytes_per_launch).
 
 Reads gpurun_out/prof_<workload>/{trace,pmc_fetch,pmc_write} and
   * copies the rocprofv3 --stats kernel summary to
@@ -33,6 +39,17 @@ def per_launch(path, kernel, counter):
     return vals
 
 
+def per_step(path, kernels, counter):
+    """(sum over every kernel matching one of `kernels`) / launches of kernels[0]."""
+    anchor = per_launch(path, kernels[0], counter)
+    tot = 0.0
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter and any(k in row["Kernel_Name"] for k in kernels):
+                tot += float(row["Counter_Value"])
+    return [tot / len(anchor)] * len(anchor) if anchor else []
+
+
 def main():
     wl, kernel = sys.argv[1], sys.argv[2]
     tag = sys.argv[3] if len(sys.argv) > 3 else "r01"
@@ -42,8 +59,9 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{tag}_{wl}_kernel_stats.csv"))
-    fetch = per_launch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kernel, "FETCH_SIZE")
-    write = per_launch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kernel, "WRITE_SIZE")
+    kernels = kernel.split(",")
+    fetch = per_step(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), kernels, "FETCH_SIZE")
+    write = per_step(os.path.join(src, "pmc_write", "run_counter_collection.csv"), kernels, "WRITE_SIZE")
     with open(os.path.join(src, "bench_trace.json")) as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
     algo = bench["roofline"]["bytes_per_launch"]
@@ -54,7 +72,7 @@ def main():
     avg_ns = None
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Name"]:
+            if kernels[0] in row["Name"]:
                 avg_ns = float(row["AverageNs"])
                 break
     rec = {
