@@ -461,6 +461,10 @@ class ShardJoin(Workload):
     kernel = "RCCL ncclAllReduce(ncclUint64, ncclMax)"
 
     def __init__(self, eng, rank, world, rows, nodes, seed=2024):
+        if world < 2:
+            # one rank's in-place all-reduce moves nothing: a line would
+            # report bytes that were never touched
+            raise SystemExit("shard_join is the cross-GPU exchange of configs[4] E2: run it with --gpus >= 2")
         self.eng, self.world, self.rows, self.nodes = eng, world, rows, nodes
         self.state = eng.synth_counters(seed, 100 + rank, rows, nodes)    # divergent per rank
         self.comm = native_comm(eng, world)
@@ -468,7 +472,7 @@ class ShardJoin(Workload):
             self.buf = torch.empty_like(self.state)
         self.config = {"workload": f"divergent full-state join, {rows} replicas x {nodes} nodes uint64 "
                                    f"({rows * nodes * 8 / 1e9:.3f} GB) per rank, all-reduce(max) "
-                                   "(BASELINE configs[4], E2)" + ("" if world > 1 else "; single rank: no exchange"),
+                                   "(BASELINE configs[4], E2)",
                        "rows": rows, "nodes": nodes, "parallelism": f"state-replica x{world} + RCCL all-reduce(max)"}
 
     def units(self):
