@@ -67,7 +67,8 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 //   k_rm_plan_small / scan : tiles per replica;
 //   k_rm_split : one wave per tile: its geometry and 16-ary merge-path split
 //                -> descriptors (plus the Atoi / accumulator-reset prep);
-//   k_rm_count : merge (256 threads x MI items): inserted-R count per tile;
+//   k_rm_count : merge (512 threads x 8 items): inserted-R count per tile and
+//                the merge-order bitmaps;
 //   scan of the counts -> each tile's output offset, out.off;
 //   k_rm_tile  : re-merge (512 threads x FI items), each entry's rank among
 //                the tile's emitted entries; the tile's new-Diff slice
@@ -85,7 +86,6 @@ __global__ void k_atoi(const uint8_t *__restrict__ bytes, const uint64_t *__rest
 // tile pass here is still latency-bound at 2-4 TB/s, see DESIGN.md.)
 constexpr int MT = 4096;                  // merge items per tile
 constexpr int MB = 512;                   // threads per tile (count pass)
-constexpr int MI = MT / MB;               // items per thread
 constexpr int TT = 512;                   // LDS replay-table entries per tile
 constexpr int FB = 1024;                  // threads of the tile pass (one tile each)
 constexpr int NW = MT / 64;               // 64-bit words per merge bitmap of a tile
@@ -274,20 +274,22 @@ __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t 
 // 32-byte stride of a wave's merge-path probes, measured slower: count
 // 45.9 -> 48.7 us.)
 
-// Stage the tile's merge items in LDS: every thread issues its MI loads
+// Stage the tile's merge items in LDS: every thread issues its NT loads
 // before the first store (a load / store per item in turn left the pass
-// waiting on MI serial HBM round trips).
+// waiting on its serial HBM round trips).
+template <int NT>
 __device__ __forceinline__ void load_tile_ts(const crdt_refmerge_in &in, const TileDesc &d, uint32_t na, uint32_t n,
                                              int64_t *sm) {
-    int64_t v[MI];
+    constexpr int NI = MT / NT;
+    int64_t v[NI];
 #pragma unroll
-    for (int j = 0; j < MI; ++j) {
-        const uint32_t k = threadIdx.x + (uint32_t)j * MB;
+    for (int j = 0; j < NI; ++j) {
+        const uint32_t k = threadIdx.x + (uint32_t)j * NT;
         v[j] = k < na ? in.l_ts[d.l0 + k] : k < n ? in.r_ts[d.r0 + (k - na)] : 0;
     }
 #pragma unroll
-    for (int j = 0; j < MI; ++j) {
-        const uint32_t k = threadIdx.x + (uint32_t)j * MB;
+    for (int j = 0; j < NI; ++j) {
+        const uint32_t k = threadIdx.x + (uint32_t)j * NT;
         if (k < n) sm[1 + k] = v[j];
     }
     if (threadIdx.x == 0) sm[0] = d.lprev;
@@ -394,12 +396,14 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
 // reads every entry's position from them instead of merging again (a
 // second merge in the tile pass, or a 2-byte rank per entry written and
 // read back, each cost more).  Grid = the tile-count upper bound.
-__global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
                                                  uint32_t *__restrict__ zero) {
-    static_assert(MI == 8, "one byte of each bitmap per thread");
+    constexpr int NI = MT / NT, LPW = 64 / NI;           // items per thread, lanes per bitmap word
+    static_assert(NI * LPW == 64, "a bitmap word is LPW lanes' items");
     __shared__ int64_t sm[MT + 1];
-    __shared__ uint32_t s_w[MB / 64];
+    __shared__ uint32_t s_w[NT / 64];
     const uint64_t t = blockIdx.x;
     if (zero && t == 0 && threadIdx.x == 0) *zero = 0;   // (the delta fold's overflow flag)
     const TileDesc d = desc[t], dn = desc[t + 1];
@@ -410,21 +414,21 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
         if (threadIdx.x == 0) tcnt[t] = 0;              // the scan runs over the whole grid
         return;
     }
-    load_tile_ts(in, d, na, n, sm);
-    const uint32_t k0 = threadIdx.x * MI < n ? threadIdx.x * MI : n;
-    const uint32_t k1 = k0 + MI < n ? k0 + MI : n;
+    load_tile_ts<NT>(in, d, na, n, sm);
+    const uint32_t k0 = threadIdx.x * NI < n ? threadIdx.x * NI : n;
+    const uint32_t k1 = k0 + NI < n ? k0 + NI : n;
     uint32_t isl = 0, emit = 0;
     if (k0 < k1) (void)thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
-    // 8 lanes' bytes -> one 64-bit word of each bitmap
-    const int lane = threadIdx.x & 63, sh = (lane & 7) * 8;
+    // LPW lanes' item bits -> one 64-bit word of each bitmap
+    const int lane = threadIdx.x & 63, sh = (lane % LPW) * NI;
     uint64_t wl = (uint64_t)isl << sh, we = (uint64_t)emit << sh;
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) {
+    for (int o = 1; o < LPW; o <<= 1) {
         wl |= (uint64_t)__shfl_xor((unsigned long long)wl, o);
         we |= (uint64_t)__shfl_xor((unsigned long long)we, o);
     }
-    if ((lane & 7) == 0) {
-        const uint32_t w = threadIdx.x >> 3;
+    if (lane % LPW == 0) {
+        const uint32_t w = threadIdx.x / LPW;
         bits[t * 2 * NW + w] = wl;
         bits[t * 2 * NW + NW + w] = we;
     }
@@ -436,7 +440,7 @@ __global__ __launch_bounds__(MB) void k_rm_count(crdt_refmerge_in in, const Tile
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
 #pragma unroll
-        for (int k = 0; k < MB / 64; ++k) tot += s_w[k];
+        for (int k = 0; k < NT / 64; ++k) tot += s_w[k];
         tcnt[t] = tot;
     }
 }
@@ -965,7 +969,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, maxl_dev, tmax, desc, okv, acc,
                                                            (uint32_t)ns);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
-    k_rm_count<<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf);
+    // (count-pass shapes at 4096-item tiles: 256 x 16 51 us, 512 x 8 45 us, 1024 x 4 67 us)
+    k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf);
     rc = check_launch(ctx);
     if (rc) return rc;
     // (a completion ticket letting the count pass's last block do this scan
