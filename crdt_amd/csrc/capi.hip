@@ -227,8 +227,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.grid_per_cu")) { // 0 = occupancy query (co-residency required)
         if (v < 0 || v > 16) return CRDT_E_INVAL;
         g_sets_grid_per_cu = (int)v;
-    } else if (!strcmp(name, "sets.knobs")) {        // bit 0: control-wave priority; bit 1: spinning data barrier
-        if (v < 0 || v > 3) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "sets.knobs")) {        // bit 0: control-wave priority; bit 1: spinning data barrier;
+        if (v < 0 || v > 7) return CRDT_E_INVAL;     //   bit 2: LWW through the persistent tag-merge kernel
         g_sets_knobs = (int)v;
     } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic, WRONG output: 1 no look-back, 2 loader only
         if (v < 0 || v > 2) return CRDT_E_INVAL;

@@ -709,6 +709,407 @@ __global__ __launch_bounds__(SET_BLOCK, 2 * SET_BLOCK / 256) void k_set_merge(
 #undef WSTAMP
 }
 
+// ---------------------------------------------------------------- LWW by key runs
+// LWW needs no tag-ordered merge: its output is one tuple per distinct key,
+// in key order, and a key's winner depends only on the END of the key's run
+// on each side -- A's run ends at its max (ts, rep) tag, B's likewise; the
+// larger tag wins, A on an equal tag (left / local wins, main.go:54-65), and
+// the winner's tomb is that of the FIRST copy of its tag on its side (the
+// first element in the stable merged order carrying the key's max tag).  So
+// the merge runs over KEYS only (A first on an equal key), and only the run
+// ends' ts / rep / tomb are ever read:
+//   k_lww_split : merge-path splits of 4096-item tiles over the keys
+//                 (16-lane 16-ary searches, four diagonals per wave);
+//   k_lww_count : per tile, the keys merged in LDS (512 threads x 8 items):
+//                 bitmap `isa` (merge item is an A element) and `emit` (its
+//                 key differs from the next merged key: the last element of
+//                 the key's merged run -- B's run end when B holds the key,
+//                 else A's), 512 B per tile, and the tile's emit count;
+//   scan of the counts -> each tile's output offset, *out_count;
+//   k_lww_write : per tile, 1024 threads in merge order (wave w: items
+//                 64 (w + 16 f) + lane); an item's A / B index and output
+//                 rank are prefix popcounts of the bitmaps (mbcnt over
+//                 wave-uniform words); each emitting lane loads its run end
+//                 and -- for a B run end -- A's element just before it in
+//                 merged order (A's run end when it holds the same key),
+//                 picks the winner, steps back over equal-tag copies for the
+//                 first one's tomb, and stores at its rank (consecutive
+//                 across the emitting lanes).
+// No cross-workgroup waiting; the key reads are the only full pass.
+constexpr int LT = 4096;                 // merge items per LWW tile
+constexpr int LCB = 512;                 // count pass threads (8 items each)
+constexpr int LNW = LT / 64;             // bitmap words per tile and bitmap
+
+__global__ __launch_bounds__(256) void k_lww_split(const uint64_t *__restrict__ ka, const uint64_t *__restrict__ kb,
+                                                   size_t na, size_t nb, size_t ntiles, uint64_t *__restrict__ split) {
+    const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+    const size_t t = ((((size_t)blockIdx.x * 256 + threadIdx.x) >> 6) << 2) + (size_t)grp;
+    const size_t n = na + nb;
+    const size_t d = t * LT < n ? t * LT : n;
+    size_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    bool done = t > ntiles || hi <= lo;
+    // P(i) = A.key[i] <= B.key[d-1-i]: true below the split, false from it
+    while (__ballot(!done)) {
+        const size_t span = hi - lo;
+        const bool small = span <= 16;
+        const size_t c = small ? lo + (size_t)gl : lo + ((size_t)gl * span) / 16;
+        const bool valid = !done && (small ? (size_t)gl < span : true);
+        const bool p = valid && ka[c] <= kb[d - 1 - c];
+        const unsigned m = (unsigned)((__ballot(p) >> (grp * 16)) & 0xFFFF);
+        const unsigned cnt = (unsigned)__popc(m);
+        if (!done) {
+            if (small) {
+                lo += cnt;
+                done = true;
+            } else {
+                const size_t nlo = cnt > 0 ? lo + (((size_t)(cnt - 1)) * span) / 16 + 1 : lo;
+                const size_t nhi = cnt < 16 ? lo + ((size_t)cnt * span) / 16 : hi;
+                lo = nlo;
+                hi = nhi;
+                done = hi <= lo;
+            }
+        }
+    }
+    if (gl == 0 && t <= ntiles) split[t] = lo;
+}
+
+struct LwwTile {
+    size_t i0, i1, j0, j1;
+    uint32_t na, nb, n;
+};
+__device__ __forceinline__ LwwTile lww_tile(const uint64_t *__restrict__ split, uint64_t t, size_t n) {
+    LwwTile b;
+    const size_t d0 = (size_t)t * LT, d1 = d0 + LT < n ? d0 + LT : n;
+    b.i0 = split[t];
+    b.i1 = split[t + 1];
+    b.j0 = d0 - b.i0;
+    b.j1 = d1 - b.i1;
+    b.na = (uint32_t)(b.i1 - b.i0);
+    b.nb = (uint32_t)(b.j1 - b.j0);
+    b.n = b.na + b.nb;
+    return b;
+}
+
+__global__ __launch_bounds__(LCB) void k_lww_count(const uint64_t *__restrict__ ka, const uint64_t *__restrict__ kb,
+                                                   size_t na, size_t nb, const uint64_t *__restrict__ split,
+                                                   uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits) {
+    constexpr int NI = LT / LCB, LPW = 64 / NI;
+    __shared__ uint64_t sk[LT];                          // A part, then B part
+    __shared__ uint32_t s_w[LCB / 64];
+    const uint64_t t = blockIdx.x;
+    const LwwTile b = lww_tile(split, t, na + nb);
+    uint64_t v[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {                       // every load issued before the first store
+        const uint32_t k = threadIdx.x + (uint32_t)j * LCB;
+        v[j] = k < b.na ? ka[b.i0 + k] : k < b.n ? kb[b.j0 + (k - b.na)] : 0;
+    }
+    // the keys after the tile: the next merged key past its last item
+    const bool ha_next = b.i1 < na, hb_next = b.j1 < nb;
+    const uint64_t ka_next = ha_next ? ka[b.i1] : 0, kb_next = hb_next ? kb[b.j1] : 0;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const uint32_t k = threadIdx.x + (uint32_t)j * LCB;
+        if (k < b.n) sk[k] = v[j];
+    }
+    __syncthreads();
+    const uint64_t *SA = sk, *SB = sk + b.na;
+    const uint32_t k0 = threadIdx.x * NI < b.n ? threadIdx.x * NI : b.n;
+    const uint32_t k1 = k0 + NI < b.n ? k0 + NI : b.n;
+    uint32_t isa = 0, emit = 0;
+    if (k0 < k1) {
+        uint32_t lo = k0 > b.nb ? k0 - b.nb : 0, hi = k0 < b.na ? k0 : b.na;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (SA[mid] <= SB[k0 - 1 - mid]) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t ia = lo, ib = k0 - lo;
+        uint64_t ha = ia < b.na ? SA[ia] : 0, hb = ib < b.nb ? SB[ib] : 0;
+        uint64_t prev = 0;
+        for (uint32_t i = 0; i < k1 - k0; ++i) {
+            const bool take_a = ia < b.na && (ib >= b.nb || ha <= hb);
+            const uint64_t key = take_a ? ha : hb;
+            if (i > 0 && key != prev) emit |= 1u << (i - 1);
+            prev = key;
+            if (take_a) {
+                isa |= 1u << i;
+                ++ia;
+                if (ia < b.na) ha = SA[ia];
+            } else {
+                ++ib;
+                if (ib < b.nb) hb = SB[ib];
+            }
+        }
+        // the item after the thread's last one: the merge's next head, or
+        // past the tile the first of A[i1] / B[j1] (A first on an equal key)
+        bool has_next;
+        uint64_t nk;
+        if (ia < b.na || ib < b.nb) {
+            has_next = true;
+            nk = (ia < b.na && (ib >= b.nb || ha <= hb)) ? ha : hb;
+        } else {
+            has_next = ha_next || hb_next;
+            nk = (ha_next && (!hb_next || ka_next <= kb_next)) ? ka_next : kb_next;
+        }
+        if (!has_next || nk != prev) emit |= 1u << (k1 - k0 - 1);
+    }
+    const int lane = threadIdx.x & 63, sh = (lane % LPW) * NI;
+    uint64_t wl = (uint64_t)isa << sh, we = (uint64_t)emit << sh;
+#pragma unroll
+    for (int o = 1; o < LPW; o <<= 1) {
+        wl |= (uint64_t)__shfl_xor((unsigned long long)wl, o);
+        we |= (uint64_t)__shfl_xor((unsigned long long)we, o);
+    }
+    if (lane % LPW == 0) {
+        const uint32_t w = threadIdx.x / LPW;
+        bits[t * 2 * LNW + w] = wl;
+        bits[t * 2 * LNW + LNW + w] = we;
+    }
+    uint32_t x = (uint32_t)__popc(emit);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < LCB / 64; ++k) tot += s_w[k];
+        tcnt[t] = tot;
+    }
+}
+
+// exclusive scan of n <= 64k tile counts by one workgroup; out[n] = total,
+// also written to *count
+__global__ __launch_bounds__(1024) void k_lww_scan(const uint32_t *__restrict__ tcnt, uint32_t n,
+                                                   uint64_t *__restrict__ out, uint64_t *__restrict__ count) {
+    __shared__ uint64_t s_w[16];
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t b = threadIdx.x * per < n ? threadIdx.x * per : n;
+    const uint32_t e = b + per < n ? b + per : n;
+    uint64_t sum = 0;
+    for (uint32_t i = b; i < e; ++i) sum += tcnt[i];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint64_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        base += k < w ? s_w[k] : 0;
+        tot += s_w[k];
+    }
+    uint64_t run = base + x - sum;
+    for (uint32_t i = b; i < e; ++i) {
+        out[i] = run;
+        run += tcnt[i];
+    }
+    if (threadIdx.x == 0) {
+        out[n] = tot;
+        *count = tot;
+    }
+}
+
+__global__ void k_lww_total(const uint64_t *__restrict__ ic, uint64_t n, uint64_t *__restrict__ count) { *count = ic[n]; }
+
+// the first element of a side's run of equal tags ending at index w
+__device__ __forceinline__ size_t first_copy(const uint64_t *sk, const uint64_t *st, const uint32_t *sr, size_t w,
+                                             uint64_t k, uint64_t ts, uint32_t r) {
+    while (w > 0 && sk[w - 1] == k && st[w - 1] == ts && sr[w - 1] == r) --w;
+    return w;
+}
+
+// k_lww_write: one workgroup per HALF tile (2048 merge items, words
+// 32 h .. 32 h + 31 of the tile's bitmaps).  The half's A run and B run
+// (plus the two A elements and the one B element before them) are staged in
+// LDS with coalesced loads -- every field of every input element is read
+// once, in order; per-lane gathers of the run ends kept the vector-memory
+// address pipe saturated (185 µs, 52 % of wave time in issue stalls; a
+// shuffle-window variant 216-224 µs).  Then, per emitting item, X / Y / their
+// predecessors come from LDS.
+constexpr int LWH = 2048;                // merge items per write workgroup
+constexpr int LWT = 512;                 // its threads (4 items each)
+
+__global__ __launch_bounds__(LWT) void k_lww_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                                   const uint64_t *__restrict__ split,
+                                                   const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
+                                                   crdt_tuples out) {
+    constexpr int NWV = LWT / 64, FI = (LWH / 64) / NWV, CAP = LWH + 3;
+    static_assert(LNW == 64 && LWH * 2 == LT && FI * NWV * 64 == LWH, "shape");
+    __shared__ uint64_t s_key[CAP], s_ts[CAP];
+    __shared__ uint32_t s_rep[CAP];
+    __shared__ uint8_t s_tomb[CAP];
+    const uint64_t t = blockIdx.x >> 1;
+    const uint32_t h = blockIdx.x & 1;
+    const LwwTile b = lww_tile(split, t, na + nb);
+    const int lane = threadIdx.x & 63;
+    const uint64_t word_a = bits[t * 2 * LNW + lane], word_e = bits[t * 2 * LNW + LNW + lane];
+    uint32_t pre_a = (uint32_t)__popcll(word_a), pre_e = (uint32_t)__popcll(word_e);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ya = __shfl_up(pre_a, o), ye = __shfl_up(pre_e, o);
+        if (lane >= o) {
+            pre_a += ya;
+            pre_e += ye;
+        }
+    }
+    pre_a -= (uint32_t)__popcll(word_a);
+    pre_e -= (uint32_t)__popcll(word_e);
+    // the half's runs: A [ra, ra + ca), B [rb, rb + cb); staged from ra - 2 / rb - 1
+    const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane(pre_a, 32 * h);        // A items before the half
+    const uint32_t ha1 = h ? b.na : (uint32_t)__builtin_amdgcn_readlane(pre_a, 32);  // ... before its end
+    const uint32_t d0 = LWH * h;
+    const uint32_t hn = b.n > d0 ? (b.n - d0 < (uint32_t)LWH ? b.n - d0 : (uint32_t)LWH) : 0;   // items in the half
+    if (hn == 0) return;
+    const size_t ra = b.i0 + ha, rb = b.j0 + (d0 - ha);
+    const uint32_t ca = ha1 - ha, cb = hn - ca;
+    const uint32_t na2 = ca + 2;                         // staged A: ra-2 .. ra+ca-1 (slots 0 .. ca+1)
+    const uint32_t nst = na2 + cb + 1;                   // then B: rb-1 .. rb+cb-1
+    {
+        uint64_t k[5], ts[5];
+        uint32_t r[5];
+        uint8_t m[5];
+        bool v[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {                    // every staging load issued before the first store
+            const uint32_t x = threadIdx.x + (uint32_t)j * LWT;
+            const bool on_a = x < na2;
+            const size_t g = on_a ? ra - 2 + x : rb - 1 + (x - na2);
+            v[j] = x < nst && (on_a ? (ra + x >= 2 && g < na) : (rb + (x - na2) >= 1 && g < nb));
+            k[j] = v[j] ? (on_a ? A.key : B.key)[g] : 0;
+            ts[j] = v[j] ? (on_a ? A.ts : B.ts)[g] : 0;
+            r[j] = v[j] ? (on_a ? A.rep : B.rep)[g] : 0;
+            m[j] = v[j] ? (on_a ? A.tomb : B.tomb)[g] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint32_t x = threadIdx.x + (uint32_t)j * LWT;
+            if (x < nst) {
+                s_key[x] = k[j];
+                s_ts[x] = ts[j];
+                s_rep[x] = r[j];
+                s_tomb[x] = m[j];
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t ob = ic[t];
+    const int wvu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto below = [&](uint64_t msk) -> uint32_t {        // set bits of msk below this lane
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+    };
+    // staged tag equality with a given global element
+    auto tag_at = [&](uint32_t sl, uint64_t &k, uint64_t &ts, uint32_t &r) {
+        k = s_key[sl];
+        ts = s_ts[sl];
+        r = s_rep[sl];
+    };
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        const int w = 32 * (int)h + wvu + NWV * f;       // the tile's word
+        const uint64_t wa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_a >> 32), w) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_a, w);
+        const uint64_t we = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_e >> 32), w) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_e, w);
+        if (!((we >> lane) & 1)) continue;
+        const uint32_t pa = (uint32_t)__builtin_amdgcn_readlane(pre_a, w) + below(wa);   // A items before (tile)
+        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane(pre_e, w) + below(we);   // output rank
+        const uint32_t k = 64u * (uint32_t)w + (uint32_t)lane;                          // tile merge item
+        const uint32_t la = pa - ha, lb = (k - d0) - la; // A / B items of the half before this one
+        const bool is_a = (wa >> lane) & 1;
+        const size_t ai = ra + la;                       // A elements merged before this item
+        uint64_t key, ts;
+        uint32_t rep, xs;                                // the winner's staging slot
+        bool on_a;
+        size_t wi;
+        if (is_a) {                                      // an A run end whose key B does not hold
+            xs = la + 2;
+            tag_at(xs, key, ts, rep);
+            on_a = true;
+            wi = ai;
+        } else {                                         // B's run end; A's run end of the key just before it
+            const uint32_t bs = na2 + 1 + lb;
+            uint64_t kb_, tb, ka_ = 0, ta = 0;
+            uint32_t rb_, ra_ = 0;
+            tag_at(bs, kb_, tb, rb_);
+            const bool a_has = ai > 0 && (tag_at(la + 1, ka_, ta, ra_), ka_ == kb_);
+            const bool ya = a_has && (ta > tb || (ta == tb && ra_ >= rb_));   // A wins an equal tag
+            key = kb_;
+            on_a = ya;
+            xs = ya ? la + 1 : bs;
+            ts = ya ? ta : tb;
+            rep = ya ? ra_ : rb_;
+            wi = ya ? ai - 1 : rb + lb;
+        }
+        // the first copy of the winner's tag on its side: its staged
+        // predecessor, then (rare) global memory before the staging
+        uint8_t tomb = s_tomb[xs];
+        const uint32_t lo = on_a ? 0u : na2;             // first staged slot of the side
+        bool more = wi > 0;
+        uint32_t sl = xs;
+        while (more && sl > lo) {
+            uint64_t pk, pt;
+            uint32_t pr;
+            tag_at(sl - 1, pk, pt, pr);
+            if (pk != key || pt != ts || pr != rep) {
+                more = false;
+                break;
+            }
+            --sl;
+            --wi;
+            tomb = s_tomb[sl];
+            more = wi > 0;
+        }
+        if (more && sl == lo) {                          // the run of copies reaches past the staging
+            const size_t fc = first_copy(on_a ? A.key : B.key, on_a ? A.ts : B.ts, on_a ? A.rep : B.rep, wi, key, ts,
+                                         rep);
+            tomb = (on_a ? A.tomb : B.tomb)[fc];
+        }
+        const uint64_t o = ob + rk;
+        out.key[o] = key;
+        out.ts[o] = ts;
+        out.rep[o] = rep;
+        out.tomb[o] = tomb;
+    }
+}
+
+static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
+                             const crdt_tuples &O, uint64_t *out_count) {
+    const size_t n = na + nb;
+    const size_t ntiles = (n + LT - 1) / LT;
+    if (ntiles >= 0x7fffffffULL || n >= (1ULL << 62)) return CRDT_E_RANGE;
+    const size_t need = Carve::round((ntiles + 1) * 8) + Carve::round(ntiles * 4 + 4) + Carve::round((ntiles + 1) * 8) +
+                        Carve::round(ntiles * 2 * LNW * 8) + scan_tmp_bytes(ntiles) + 1024;
+    int rc = ws_reserve(ctx, need);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    uint64_t *split = w.take<uint64_t>(ntiles + 1);
+    uint32_t *tcnt = w.take<uint32_t>(ntiles + 1);
+    uint64_t *ic = w.take<uint64_t>(ntiles + 1);
+    uint64_t *bits = w.take<uint64_t>(ntiles * 2 * LNW);
+    void *tmp = w.take<char>(scan_tmp_bytes(ntiles));
+    const hipStream_t s = ctx->stream;
+    const uint64_t *ka = A.key, *kb = B.key;             // (nullptr for an empty side: never dereferenced)
+    k_lww_split<<<(unsigned)((ntiles + 1 + 15) / 16), 256, 0, s>>>(ka, kb, na, nb, ntiles, split);
+    k_lww_count<<<(unsigned)ntiles, LCB, 0, s>>>(ka, kb, na, nb, split, tcnt, bits);
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    if (ntiles <= 65536) {
+        k_lww_scan<<<1, 1024, 0, s>>>(tcnt, (uint32_t)ntiles, ic, out_count);
+    } else {
+        rc = exclusive_scan_u32(ctx, tcnt, ic, ntiles, tmp);
+        if (rc) return rc;
+        k_lww_total<<<1, 1, 0, s>>>(ic, ntiles, out_count);
+    }
+    k_lww_write<<<(unsigned)(2 * ntiles), LWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
+    return check_launch(ctx);
+}
+
 size_t g_last_grid = 0;              // diagnostic: persistent grid of the last set merge
 int g_last_occ = 0;
 uint64_t *g_last_stamps = nullptr;   // diagnostic: stamps of the last set merge (16 per tile)
@@ -791,6 +1192,8 @@ static int set_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
     crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples &A = na ? *a : empty;
     const crdt_tuples &B = nb ? *b : empty;
+    // LWW by key runs (sets.knobs bit 2: the persistent tag-merge kernel instead)
+    if (MODE == SET_LWW && !(g_sets_knobs & 4)) return lww_merge_keyruns(ctx, A, na, B, nb, *out, out_count);
     return set_merge_impl<MODE>(ctx, A, na, B, nb, *out, out_count);
 }
 
