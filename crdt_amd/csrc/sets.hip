@@ -879,8 +879,10 @@ __global__ __launch_bounds__(LCB) void k_lww_count(const uint64_t *__restrict__ 
     }
 }
 
-// exclusive scan of n <= 64k tile counts by one workgroup; out[n] = total,
-// also written to *count
+// exclusive scan of n <= 16k tile counts by one workgroup (a contiguous
+// chunk per thread); out[n] = total, also written to *count.  (Chunks held
+// in registers: 6.9 / 11.5 µs at 4.9k / 9.8k tiles; 16 coalesced rows per
+// wave: 11.9 / 12.0; this loop 5.5 / 11.9.)
 __global__ __launch_bounds__(1024) void k_lww_scan(const uint32_t *__restrict__ tcnt, uint32_t n,
                                                    uint64_t *__restrict__ out, uint64_t *__restrict__ count) {
     __shared__ uint64_t s_w[16];
@@ -1099,7 +1101,7 @@ static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, con
     k_lww_count<<<(unsigned)ntiles, LCB, 0, s>>>(ka, kb, na, nb, split, tcnt, bits);
     rc = check_launch(ctx);
     if (rc) return rc;
-    if (ntiles <= 65536) {
+    if (ntiles <= 16384) {
         k_lww_scan<<<1, 1024, 0, s>>>(tcnt, (uint32_t)ntiles, ic, out_count);
     } else {
         rc = exclusive_scan_u32(ctx, tcnt, ic, ntiles, tmp);
@@ -1107,6 +1109,309 @@ static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, con
         k_lww_total<<<1, 1, 0, s>>>(ic, ntiles, out_count);
     }
     k_lww_write<<<(unsigned)(2 * ntiles), LWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
+    return check_launch(ctx);
+}
+
+// ---------------------------------------------------------------- OR-Set, two passes
+// The same structure for the OR-Set, over TAGS: one output per distinct tag
+// (key, ts, rep) in tag order, its tomb the OR over every copy; in the
+// stable merge (A first on an equal tag) a tag's copies are consecutive --
+// A's, then B's -- so the first copy emits:
+//   k_or_split : merge-path splits of 2048-item tiles over the tags;
+//   k_or_count : per tile the tags merged in LDS (512 threads x 4 items):
+//                bitmaps `isa` and `emit` (the item's tag differs from the
+//                previous merged tag), 512 B per tile, the emit count;
+//   scan;
+//   k_or_write : per tile (512 threads, wave w: items 64 (w + 8 f) + lane),
+//                the tile's A and B runs staged in LDS (coalesced, every
+//                field once); an emitting item ORs the tombs of its tag's
+//                copies -- forward over A's, then B's from the B position
+//                of the item -- and stores at its rank.
+constexpr int OT = 2048;                 // merge items per OR tile
+constexpr int OCB = 512;                 // count pass threads (4 items each; 256 x 8: 120 us against 111)
+constexpr int OWT = 512;                 // write pass threads (4 items each)
+constexpr int ONW = OT / 64;             // bitmap words per tile and bitmap
+
+__global__ __launch_bounds__(256) void k_or_split(crdt_tuples A, crdt_tuples B, size_t na, size_t nb, size_t ntiles,
+                                                  uint64_t *__restrict__ split) {
+    const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+    const size_t t = ((((size_t)blockIdx.x * 256 + threadIdx.x) >> 6) << 2) + (size_t)grp;
+    const size_t n = na + nb;
+    const size_t d = t * OT < n ? t * OT : n;
+    size_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    bool done = t > ntiles || hi <= lo;
+    while (__ballot(!done)) {
+        const size_t span = hi - lo;
+        const bool small = span <= 16;
+        const size_t c = small ? lo + (size_t)gl : lo + ((size_t)gl * span) / 16;
+        const bool valid = !done && (small ? (size_t)gl < span : true);
+        const bool p = valid && g_le_lazy(A, c, B, d - 1 - c);
+        const unsigned m = (unsigned)((__ballot(p) >> (grp * 16)) & 0xFFFF);
+        const unsigned cnt = (unsigned)__popc(m);
+        if (!done) {
+            if (small) {
+                lo += cnt;
+                done = true;
+            } else {
+                const size_t nlo = cnt > 0 ? lo + (((size_t)(cnt - 1)) * span) / 16 + 1 : lo;
+                const size_t nhi = cnt < 16 ? lo + ((size_t)cnt * span) / 16 : hi;
+                lo = nlo;
+                hi = nhi;
+                done = hi <= lo;
+            }
+        }
+    }
+    if (gl == 0 && t <= ntiles) split[t] = lo;
+}
+
+__device__ __forceinline__ LwwTile or_tile(const uint64_t *__restrict__ split, uint64_t t, size_t n) {
+    LwwTile b;
+    const size_t d0 = (size_t)t * OT, d1 = d0 + OT < n ? d0 + OT : n;
+    b.i0 = split[t];
+    b.i1 = split[t + 1];
+    b.j0 = d0 - b.i0;
+    b.j1 = d1 - b.i1;
+    b.na = (uint32_t)(b.i1 - b.i0);
+    b.nb = (uint32_t)(b.j1 - b.j0);
+    b.n = b.na + b.nb;
+    return b;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_or_count(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                                 const uint64_t *__restrict__ split, uint32_t *__restrict__ tcnt,
+                                                 uint64_t *__restrict__ bits) {
+    constexpr int NI = OT / NT, LPW = 64 / NI, CAP = OT + 2;
+    // staged: A[i0-1], A part, B[j0-1], B part (slot 0 of each side: the
+    // element before the tile, the first item's merged predecessor candidate)
+    __shared__ uint64_t sk[CAP], st[CAP];
+    __shared__ uint32_t sr[CAP];
+    __shared__ uint32_t s_w[NT / 64];
+    const uint64_t t = blockIdx.x;
+    const LwwTile b = or_tile(split, t, na + nb);
+    const uint32_t nsa = b.na + 1, nst = nsa + b.nb + 1;
+    {
+        uint64_t k[NI + 1], ts[NI + 1];
+        uint32_t r[NI + 1];
+#pragma unroll
+        for (int j = 0; j <= NI; ++j) {                  // every staging load issued before the first store
+            const uint32_t x = threadIdx.x + (uint32_t)j * NT;
+            const bool on_a = x < nsa;
+            const size_t g = on_a ? b.i0 - 1 + x : b.j0 - 1 + (x - nsa);
+            const bool v = x < nst && (on_a ? b.i0 + x >= 1 : b.j0 + (x - nsa) >= 1);
+            k[j] = v ? (on_a ? A.key : B.key)[g] : 0;
+            ts[j] = v ? (on_a ? A.ts : B.ts)[g] : 0;
+            r[j] = v ? (on_a ? A.rep : B.rep)[g] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j <= NI; ++j) {
+            const uint32_t x = threadIdx.x + (uint32_t)j * NT;
+            if (x < nst) {
+                sk[x] = k[j];
+                st[x] = ts[j];
+                sr[x] = r[j];
+            }
+        }
+    }
+    __syncthreads();
+    // side views: A element a of the tile at slot 1 + a, B element j at nsa + 1 + j
+#define OA(x) Tag{sk[1 + (x)], st[1 + (x)], sr[1 + (x)]}
+#define OB(x) Tag{sk[nsa + 1 + (x)], st[nsa + 1 + (x)], sr[nsa + 1 + (x)]}
+    const uint32_t k0 = threadIdx.x * NI < b.n ? threadIdx.x * NI : b.n;
+    const uint32_t k1 = k0 + NI < b.n ? k0 + NI : b.n;
+    uint32_t isa = 0, emit = 0;
+    if (k0 < k1) {
+        uint32_t lo = k0 > b.nb ? k0 - b.nb : 0, hi = k0 < b.na ? k0 : b.na;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint64_t ka = sk[1 + mid], kb = sk[nsa + 1 + (k0 - 1 - mid)];
+            const bool le = ka != kb ? ka < kb : tag_le(OA(mid), OB(k0 - 1 - mid));
+            if (le) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t ia = lo, ib = k0 - lo;
+        // the merged predecessor of item k0: the later of A[ia-1], B[ib-1]
+        // (A first on an equal tag), each possibly the element before the tile
+        const bool hpa = b.i0 + ia > 0, hpb = b.j0 + ib > 0;
+        const Tag pa{sk[ia], st[ia], sr[ia]}, pb{sk[nsa + ib], st[nsa + ib], sr[nsa + ib]};
+        bool has_prev = hpa || hpb;
+        Tag prev = tag_sel(hpa && hpb ? tag_le(pa, pb) : !hpa, pb, pa);
+        Tag ha = ia < b.na ? OA(ia) : Tag{0, 0, 0}, hb = ib < b.nb ? OB(ib) : Tag{0, 0, 0};
+        for (uint32_t i = 0; i < k1 - k0; ++i) {
+            const bool take_a = ia < b.na && (ib >= b.nb || tag_le(ha, hb));
+            const Tag cur = tag_sel(take_a, ha, hb);
+            if (!has_prev || !tag_eq(prev, cur)) emit |= 1u << i;
+            prev = cur;
+            has_prev = true;
+            if (take_a) {
+                isa |= 1u << i;
+                ++ia;
+                if (ia < b.na) ha = OA(ia);
+            } else {
+                ++ib;
+                if (ib < b.nb) hb = OB(ib);
+            }
+        }
+    }
+#undef OA
+#undef OB
+    const int lane = threadIdx.x & 63, sh = (lane % LPW) * NI;
+    uint64_t wl = (uint64_t)isa << sh, we = (uint64_t)emit << sh;
+#pragma unroll
+    for (int o = 1; o < LPW; o <<= 1) {
+        wl |= (uint64_t)__shfl_xor((unsigned long long)wl, o);
+        we |= (uint64_t)__shfl_xor((unsigned long long)we, o);
+    }
+    if (lane % LPW == 0) {
+        const uint32_t w = threadIdx.x / LPW;
+        bits[t * 2 * ONW + w] = wl;
+        bits[t * 2 * ONW + ONW + w] = we;
+    }
+    uint32_t x = (uint32_t)__popc(emit);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < NT / 64; ++k) tot += s_w[k];
+        tcnt[t] = tot;
+    }
+}
+
+__global__ __launch_bounds__(OWT) void k_or_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                                  const uint64_t *__restrict__ split,
+                                                  const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
+                                                  crdt_tuples out) {
+    constexpr int NWV = OWT / 64, FI = ONW / NWV, CAP = OT + 2;
+    static_assert(FI * NWV == ONW && ONW <= 64, "shape");
+    __shared__ uint64_t s_key[CAP], s_ts[CAP];
+    __shared__ uint32_t s_rep[CAP];
+    __shared__ uint8_t s_tomb[CAP];
+    const uint64_t t = blockIdx.x;
+    const LwwTile b = or_tile(split, t, na + nb);
+    if (b.n == 0) return;
+    const int lane = threadIdx.x & 63;
+    const bool wl_ok = lane < ONW;
+    const uint64_t word_a = wl_ok ? bits[t * 2 * ONW + lane] : 0, word_e = wl_ok ? bits[t * 2 * ONW + ONW + lane] : 0;
+    uint32_t pre_a = (uint32_t)__popcll(word_a), pre_e = (uint32_t)__popcll(word_e);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ya = __shfl_up(pre_a, o), ye = __shfl_up(pre_e, o);
+        if (lane >= o) {
+            pre_a += ya;
+            pre_e += ye;
+        }
+    }
+    pre_a -= (uint32_t)__popcll(word_a);
+    pre_e -= (uint32_t)__popcll(word_e);
+    // staged: A part (slots 0 .. na-1), then B part (slots na ..): every field once
+    const uint32_t nst = b.n;
+    {
+        constexpr int NJ = (OT + OWT - 1) / OWT;
+        uint64_t k[NJ], ts[NJ];
+        uint32_t r[NJ];
+        uint8_t m[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {                   // every staging load issued before the first store
+            const uint32_t x = threadIdx.x + (uint32_t)j * OWT;
+            const bool on_a = x < b.na;
+            const size_t g = on_a ? b.i0 + x : b.j0 + (x - b.na);
+            const bool v = x < nst;
+            k[j] = v ? (on_a ? A.key : B.key)[g] : 0;
+            ts[j] = v ? (on_a ? A.ts : B.ts)[g] : 0;
+            r[j] = v ? (on_a ? A.rep : B.rep)[g] : 0;
+            m[j] = v ? (on_a ? A.tomb : B.tomb)[g] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const uint32_t x = threadIdx.x + (uint32_t)j * OWT;
+            if (x < nst) {
+                s_key[x] = k[j];
+                s_ts[x] = ts[j];
+                s_rep[x] = r[j];
+                s_tomb[x] = m[j];
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t ob = ic[t];
+    const int wvu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto below = [&](uint64_t msk) -> uint32_t {        // set bits of msk below this lane
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+    };
+#pragma unroll
+    for (int f = 0; f < FI; ++f) {
+        const int w = wvu + NWV * f;                     // the tile's word
+        // (readlane returns int: widen through uint32_t, never sign-extend)
+        const uint64_t wa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_a >> 32), w) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_a, w);
+        const uint64_t we = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_e >> 32), w) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_e, w);
+        if (!((we >> lane) & 1)) continue;
+        const uint32_t la = (uint32_t)__builtin_amdgcn_readlane(pre_a, w) + below(wa);   // A items before (tile)
+        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane(pre_e, w) + below(we);   // output rank
+        const uint32_t k = 64u * (uint32_t)w + (uint32_t)lane;
+        const uint32_t lb = k - la;                      // B items before
+        const bool is_a = (wa >> lane) & 1;
+        const uint32_t xs = is_a ? la : b.na + lb;       // the first copy's slot
+        const uint64_t key = s_key[xs], ts = s_ts[xs];
+        const uint32_t rep = s_rep[xs];
+        uint32_t tomb = 0;
+        // A's copies (an A first copy only), then B's from position lb:
+        // in the staging, then past the tile in global memory (rare)
+        if (is_a) {
+            uint32_t s = la;
+            while (s < b.na && s_key[s] == key && s_ts[s] == ts && s_rep[s] == rep) tomb |= s_tomb[s++];
+            if (s == b.na)
+                for (size_t g = b.i1; g < na && A.key[g] == key && A.ts[g] == ts && A.rep[g] == rep; ++g)
+                    tomb |= A.tomb[g];
+        }
+        {
+            uint32_t s = lb;
+            while (s < b.nb && s_key[b.na + s] == key && s_ts[b.na + s] == ts && s_rep[b.na + s] == rep)
+                tomb |= s_tomb[b.na + s++];
+            if (s == b.nb)
+                for (size_t g = b.j1; g < nb && B.key[g] == key && B.ts[g] == ts && B.rep[g] == rep; ++g)
+                    tomb |= B.tomb[g];
+        }
+        const uint64_t o = ob + rk;
+        out.key[o] = key;
+        out.ts[o] = ts;
+        out.rep[o] = rep;
+        out.tomb[o] = (uint8_t)tomb;
+    }
+}
+
+static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
+                               const crdt_tuples &O, uint64_t *out_count) {
+    const size_t n = na + nb;
+    const size_t ntiles = (n + OT - 1) / OT;
+    if (ntiles >= 0x7fffffffULL || n >= (1ULL << 62)) return CRDT_E_RANGE;
+    const size_t need = Carve::round((ntiles + 1) * 8) + Carve::round(ntiles * 4 + 4) + Carve::round((ntiles + 1) * 8) +
+                        Carve::round(ntiles * 2 * ONW * 8) + scan_tmp_bytes(ntiles) + 1024;
+    int rc = ws_reserve(ctx, need);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    uint64_t *split = w.take<uint64_t>(ntiles + 1);
+    uint32_t *tcnt = w.take<uint32_t>(ntiles + 1);
+    uint64_t *ic = w.take<uint64_t>(ntiles + 1);
+    uint64_t *bits = w.take<uint64_t>(ntiles * 2 * ONW);
+    void *tmp = w.take<char>(scan_tmp_bytes(ntiles));
+    const hipStream_t s = ctx->stream;
+    k_or_split<<<(unsigned)((ntiles + 1 + 15) / 16), 256, 0, s>>>(A, B, na, nb, ntiles, split);
+    k_or_count<OCB><<<(unsigned)ntiles, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits);
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    if (ntiles <= 16384) {
+        k_lww_scan<<<1, 1024, 0, s>>>(tcnt, (uint32_t)ntiles, ic, out_count);
+    } else {
+        rc = exclusive_scan_u32(ctx, tcnt, ic, ntiles, tmp);
+        if (rc) return rc;
+        k_lww_total<<<1, 1, 0, s>>>(ic, ntiles, out_count);
+    }
+    k_or_write<<<(unsigned)ntiles, OWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
     return check_launch(ctx);
 }
 
@@ -1192,8 +1497,10 @@ static int set_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
     crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples &A = na ? *a : empty;
     const crdt_tuples &B = nb ? *b : empty;
-    // LWW by key runs (sets.knobs bit 2: the persistent tag-merge kernel instead)
-    if (MODE == SET_LWW && !(g_sets_knobs & 4)) return lww_merge_keyruns(ctx, A, na, B, nb, *out, out_count);
+    // two-pass merges (sets.knobs bit 2: the persistent tag-merge kernel instead)
+    if (!(g_sets_knobs & 4))
+        return MODE == SET_LWW ? lww_merge_keyruns(ctx, A, na, B, nb, *out, out_count)
+                               : orset_merge_twopass(ctx, A, na, B, nb, *out, out_count);
     return set_merge_impl<MODE>(ctx, A, na, B, nb, *out, out_count);
 }
 
