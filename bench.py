@@ -242,7 +242,7 @@ class VClockClassify(Workload):
 
 class SetMerge(Workload):
     unit = "input-tuples/s"
-    kernel = "k_partition+k_set_merge"
+    kernel = "whole op: k_{lww,or}_split + k_{lww,or}_count + k_lww_scan + k_{lww,or}_write"
 
     def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
         self.eng, self.n, self.lww = eng, n, lww
