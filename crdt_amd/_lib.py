@@ -18,7 +18,9 @@ import threading
 
 import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcrdt_amd.so")
+# CRDT_AMD_LIB: another build of the same library (A/B timing of two builds
+# in one GPU call, tools/ab2.sh); never set for tests, smoke or bench lines.
+LIB_PATH = os.environ.get("CRDT_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcrdt_amd.so")
 
 CRDT_OK = 0
 STATUS_NAMES = {

@@ -228,7 +228,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v < 0 || v > 16) return CRDT_E_INVAL;
         g_sets_grid_per_cu = (int)v;
     } else if (!strcmp(name, "sets.knobs")) {        // bit 0: control-wave priority; bit 1: spinning data barrier;
-        if (v < 0 || v > 7) return CRDT_E_INVAL;     //   bit 2: the persistent tag-merge kernel (LWW, OR-Set)
+        if (v < 0 || v > 15) return CRDT_E_INVAL;    //   bit 2: the persistent tag-merge kernel (LWW, OR-Set);
+                                                     //   bit 3: register (not LDS-DMA) staging in the two-pass write passes
         g_sets_knobs = (int)v;
     } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic, WRONG output: 1 no look-back, 2 loader only
         if (v < 0 || v > 2) return CRDT_E_INVAL;

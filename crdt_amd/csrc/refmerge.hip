@@ -491,7 +491,17 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     __shared__ int64_t s_okval[FOLDS ? OKC : 1];
     __shared__ uint8_t s_okok[FOLDS ? OKC : 1];
     const uint64_t t = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the descriptors, the tile's bitmap words (one of each bitmap per lane),
+    // its offset and the staged Atoi records are independent loads: all issued
+    // before the first use (the empty-tile exit would otherwise order them)
+    static_assert(NW == 64, "one word of each bitmap per lane");
     const TileDesc d = desc[t], dn = desc[t + 1];
+    const uint64_t word_l = bits[t * 2 * NW + lane], word_e = bits[t * 2 * NW + NW + lane];
+    const uint64_t ict = ic[t];
+    const bool okc = FOLDS && in.n_str <= OKC;
+    OkVal ok0 = OkVal{0, 0};
+    if (okc && threadIdx.x < in.n_str) ok0 = okv[threadIdx.x];
     uint32_t na, nb;
     tile_counts(d, dn, &na, &nb);
     const uint32_t n = na + nb;
@@ -499,11 +509,6 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
         if (DELTA && threadIdx.x == 0) cand_n[t] = 0;
         return;
     }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // the tile's bitmap words, one of each bitmap per lane, and their
-    // exclusive prefix popcounts
-    static_assert(NW == 64, "one word of each bitmap per lane");
-    const uint64_t word_l = bits[t * 2 * NW + lane], word_e = bits[t * 2 * NW + NW + lane];
     uint32_t pre_l = (uint32_t)__popcll(word_l), pre_e = (uint32_t)__popcll(word_e);
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -515,7 +520,7 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     }
     pre_l -= (uint32_t)__popcll(word_l);
     pre_e -= (uint32_t)__popcll(word_e);
-    const uint64_t ob = d.l0 + ic[t];
+    const uint64_t ob = d.l0 + ict;
     if (DELTA && threadIdx.x == 0) s_nc = s_ovf = 0;
     if (FOLDS)
         for (int h = threadIdx.x; h < TT; h += FB) {
@@ -531,11 +536,9 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     // a small string table (the reference's load generator writes ten
     // values, main.go:282) is staged in LDS: the Atoi lookup leaves the
     // chain of dependent global loads (kv range -> kv pair -> Atoi record)
-    const bool okc = FOLDS && in.n_str <= OKC;
     if (okc && threadIdx.x < in.n_str) {
-        const OkVal o = okv[threadIdx.x];
-        s_okval[threadIdx.x] = o.val;
-        s_okok[threadIdx.x] = (uint8_t)(o.ok != 0);
+        s_okval[threadIdx.x] = ok0.val;
+        s_okok[threadIdx.x] = (uint8_t)(ok0.ok != 0);
     }
     // per item slot f: merge item k = 64 * (wv + NWV f) + lane.  The words
     // and their prefixes are wave-uniform (scalar registers); an item's

@@ -150,3 +150,21 @@ def test_sets_unaligned_views(eng, off_a, off_b):
         exp = ref(ha, hb)
         for g, e, f in zip(got, exp, ("key", "ts", "rep", "tomb")):
             np.testing.assert_array_equal(g, e, err_msg=f"{fn.__name__}.{f}")
+
+
+@pytest.mark.parametrize("knobs", [9, 5])
+def test_sets_alternative_kernels(eng, knobs):
+    """The non-default set-merge forms (sets.knobs): 9 = the two-pass write
+    passes with register staging instead of LDS-DMA, 5 = round 1's persistent
+    look-back kernel; same outputs as the oracle on long runs, tile edges and
+    views off a 16-byte boundary."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"sets.knobs", knobs)
+    try:
+        _check(eng, *_sets(77, 100_000, 100_000, 50_000))
+        _check(eng, *_sets(78, 4097, 4095, 1000))
+        test_sets_long_runs_cross_tiles(eng)
+        test_sets_unaligned_views(eng, 3, 5)
+        assert eng.device_status(clear=True) == 0
+    finally:
+        _lib.call("crdt_set_option", b"sets.knobs", 1)
