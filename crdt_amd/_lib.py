@@ -139,6 +139,8 @@ SIGNATURES = {
     "crdt_gcounter_join": (_I, [_CTX, _P, _P, _P, _SZ, _SZ]),
     "crdt_gcounter_fold": (_I, [_CTX, _P, _SZ, _SZ, _P]),
     "crdt_gcounter_value": (_I, [_CTX, _P, _SZ, _SZ, _P]),
+    "crdt_stream_copy": (_I, [_CTX, _P, _P, _SZ, _I, _I]),
+    "crdt_stream_read": (_I, [_CTX, _P, _SZ, _P, _SZ, _I, _I]),
     "crdt_pncounter_join": (_I, [_CTX, _P, _P, _P, _P, _P, _P, _SZ, _SZ]),
     "crdt_pncounter_value": (_I, [_CTX, _P, _P, _P, _SZ, _SZ]),
     "crdt_vclock_classify": (_I, [_CTX, _P, _P, _P, _SZ, _SZ]),

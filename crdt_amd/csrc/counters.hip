@@ -193,11 +193,98 @@ static int join_impl(crdt_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64
     return check_launch(ctx);
 }
 
+// ---------------------------------------------------------------- streaming peaks
+// the bench reports each kernel's fraction of a SELF-MEASURED
+// copy-kernel peak beside the 8 TB/s spec.  A plain copy (16-B loads and
+// stores, U vectors in flight per lane) and a read-only sweep (xor-reduced
+// over the workgroup, one store per workgroup) of the same form as the join / fold loops.
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_copy(const u64x2 *__restrict__ a, u64x2 *__restrict__ o, size_t n2) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (size_t)(U - 1) * stride < n2; i += (size_t)U * stride) {
+        u64x2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld<true>(a + i + (size_t)u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<true>(o + i + (size_t)u * stride, x[u]);
+    }
+    for (; i < n2; i += stride) st<true>(o + i, ld<true>(a + i));
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_read(const u64x2 *__restrict__ a, size_t n2,
+                                                     uint64_t *__restrict__ sink) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    u64x2 m = {0, 0};
+    for (; i + (size_t)(U - 1) * stride < n2; i += (size_t)U * stride) {
+        u64x2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld<true>(a + i + (size_t)u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) m ^= x[u];
+    }
+    for (; i < n2; i += stride) m ^= ld<true>(a + i);
+    // xor over the workgroup (every lane's loads feed the stored word)
+    uint64_t v = m.x ^ m.y;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+    __shared__ uint64_t red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) sink[blockIdx.x] = red[0] ^ red[1] ^ red[2] ^ red[3];
+}
+
 }  // namespace crdt
 
 using namespace crdt;
 
 static bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int crdt_stream_copy(crdt_ctx *ctx, const void *src, void *dst, size_t bytes, int unroll,
+                                int blocks_per_cu) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!src || !dst || !aligned16(src) || !aligned16(dst) || (bytes & 15)) return CRDT_E_INVAL;
+    if (blocks_per_cu < 1 || blocks_per_cu > 64) return CRDT_E_INVAL;
+    const size_t n2 = bytes / 16;
+    if (n2 == 0) return CRDT_OK;
+    const unsigned grid = grid_for(n2, 256, (unsigned)(ctx->num_cus * blocks_per_cu));
+    const u64x2 *a = (const u64x2 *)src;
+    u64x2 *o = (u64x2 *)dst;
+    const hipStream_t s = ctx->stream;
+    switch (unroll) {
+        case 1: k_stream_copy<1><<<grid, 256, 0, s>>>(a, o, n2); break;
+        case 2: k_stream_copy<2><<<grid, 256, 0, s>>>(a, o, n2); break;
+        case 4: k_stream_copy<4><<<grid, 256, 0, s>>>(a, o, n2); break;
+        case 8: k_stream_copy<8><<<grid, 256, 0, s>>>(a, o, n2); break;
+        default: return CRDT_E_INVAL;
+    }
+    return check_launch(ctx);
+}
+
+extern "C" int crdt_stream_read(crdt_ctx *ctx, const void *src, size_t bytes, uint64_t *sink_dev, size_t sink_words,
+                                int unroll, int blocks_per_cu) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!src || !sink_dev || !aligned16(src) || (bytes & 15)) return CRDT_E_INVAL;
+    if (blocks_per_cu < 1 || blocks_per_cu > 64) return CRDT_E_INVAL;
+    const size_t n2 = bytes / 16;
+    if (n2 == 0) return CRDT_OK;
+    const unsigned grid = grid_for(n2, 256, (unsigned)(ctx->num_cus * blocks_per_cu));
+    if (sink_words < grid) return CRDT_E_INVAL;         // one word per workgroup
+    const u64x2 *a = (const u64x2 *)src;
+    const hipStream_t s = ctx->stream;
+    switch (unroll) {
+        case 1: k_stream_read<1><<<grid, 256, 0, s>>>(a, n2, sink_dev); break;
+        case 2: k_stream_read<2><<<grid, 256, 0, s>>>(a, n2, sink_dev); break;
+        case 4: k_stream_read<4><<<grid, 256, 0, s>>>(a, n2, sink_dev); break;
+        case 8: k_stream_read<8><<<grid, 256, 0, s>>>(a, n2, sink_dev); break;
+        default: return CRDT_E_INVAL;
+    }
+    return check_launch(ctx);
+}
 
 extern "C" int crdt_gcounter_join(crdt_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out,
                                   size_t rows, size_t nodes) {

@@ -167,6 +167,19 @@ class Engine:
         self._call("crdt_gcounter_fold", a.data_ptr(), rows, nodes, out.data_ptr())
         return out
 
+    def stream_copy(self, src: torch.Tensor, dst: torch.Tensor, unroll: int = 4, blocks_per_cu: int = 2) -> None:
+        """dst = src with the library's streaming copy kernel (peak measurement)."""
+        self._check(src, dst)
+        n = min(src.numel() * src.element_size(), dst.numel() * dst.element_size())
+        self._call("crdt_stream_copy", src.data_ptr(), dst.data_ptr(), n & ~15, unroll, blocks_per_cu)
+
+    def stream_read(self, src: torch.Tensor, sink: torch.Tensor, unroll: int = 4, blocks_per_cu: int = 2) -> None:
+        """Read all of src (one word per workgroup to sink): read-only streaming peak."""
+        self._check(src)
+        self._check(sink, itemsize=8)
+        n = src.numel() * src.element_size()
+        self._call("crdt_stream_read", src.data_ptr(), n & ~15, sink.data_ptr(), sink.numel(), unroll, blocks_per_cu)
+
     def gcounter_value(self, a: torch.Tensor) -> torch.Tensor:
         rows, nodes = a.shape
         out = torch.empty(rows, dtype=torch.int64, device=self.device)

@@ -115,6 +115,19 @@ int crdt_pncounter_join(crdt_ctx *ctx, const uint64_t *pa_dev, const uint64_t *n
 int crdt_pncounter_value(crdt_ctx *ctx, const uint64_t *p_dev, const uint64_t *n_dev,
                          int64_t *out_dev, size_t rows, size_t nodes);
 
+/* ------------------------------------------- streaming peaks
+ * Measurement utilities, no reference counterpart: the bench reports every
+ * kernel's fraction of a self-measured copy-kernel peak beside the spec peak.
+ * crdt_stream_copy: dst = src, `bytes` (multiple of 16, 16-B aligned), 16-B
+ * nontemporal loads / stores, `unroll` in {1,2,4,8} vectors in flight per
+ * lane, grid = CUs x blocks_per_cu workgroups of 256.
+ * crdt_stream_read: reads `bytes` of src, writes one word per workgroup to
+ * sink_dev (sink_words >= CUs x blocks_per_cu). */
+int crdt_stream_copy(crdt_ctx *ctx, const void *src_dev, void *dst_dev, size_t bytes, int unroll,
+                     int blocks_per_cu);
+int crdt_stream_read(crdt_ctx *ctx, const void *src_dev, size_t bytes, uint64_t *sink_dev, size_t sink_words,
+                     int unroll, int blocks_per_cu);
+
 /* ------------------------------------------------------ vector clocks (a7) */
 typedef enum crdt_vc_class {
     CRDT_VC_EQUAL = 0,      /* a == b                  */

@@ -110,3 +110,19 @@ def test_ordered_i64_roundtrip(eng):
     # signed order of the mapped values == unsigned order of the originals
     assert (np.argsort(o.cpu().numpy(), kind="stable") == np.argsort(x, kind="stable")).all()
     np.testing.assert_array_equal(as_u64(eng.ordered_i64_to_u64(o)), x)
+
+
+def test_stream_peak_kernels(eng):
+    """The bench's self-measured peak kernels: the copy
+    reproduces its input, the read sweep touches every word (xor of the
+    per-workgroup sinks = xor of the input)."""
+    n = (1 << 20) + 6                                   # not a multiple of the grid stride
+    src = torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device=eng.device)
+    for unroll in (1, 2, 4, 8):
+        dst = torch.zeros_like(src)
+        eng.stream_copy(src, dst, unroll, 2)
+        assert torch.equal(dst, src)
+        sink = torch.zeros(1 << 16, dtype=torch.int64, device=eng.device)
+        eng.stream_read(src, sink, unroll, 1)
+        x = np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint64))
+        assert x == np.bitwise_xor.reduce(src.cpu().numpy().view(np.uint64))
