@@ -59,6 +59,11 @@ extern int g_sets_stamps;
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
 
 void server_ctx_release(crdt_ctx *ctx);   // server.hip: the context's Server-merge scratch
+// gossip.hip: crdt_seg_gather2 (4-byte elements, base 0) over n_max segments
+// of which the first *n_dev are real (a count still on the device)
+int seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,
+                          const uint64_t *a_off, const uint64_t *b_off, uint64_t *dst_off, const uint32_t *a0,
+                          const uint32_t *b0, uint32_t *dst0, const uint32_t *a1, const uint32_t *b1, uint32_t *dst1);
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

@@ -161,11 +161,13 @@ static int seg_copy_any(crdt_ctx *ctx, size_t n_seg, const int64_t *code, const 
 struct SegSrc {
     const int64_t *code;
     const uint64_t *a_off, *b_off;
+    const uint64_t *n_dev = nullptr;      // (optional) segments >= *n_dev are empty: a device-side count
     struct Item {
         uint64_t len = 0, sb = 0;
         bool fb = false;
     };
     __device__ Item load(uint64_t s) const {
+        if (n_dev && s >= *n_dev) return Item{};
         uint64_t b, e;
         bool fb;
         seg_src(code[s], a_off, b_off, &b, &e, &fb);
@@ -245,9 +247,9 @@ extern "C" int crdt_seg_offsets(crdt_ctx *ctx, size_t n_seg, const int64_t *code
 template <typename T>
 static int seg_gather(crdt_ctx *ctx, size_t n_seg, const int64_t *code, const uint64_t *a_off, const uint64_t *b_off,
                       uint64_t base, uint64_t *dst_off, const void *a0, const void *b0, void *d0, const void *a1,
-                      const void *b1, void *d1) {
+                      const void *b1, void *d1, const uint64_t *n_dev = nullptr) {
     const SegArrays<T> p{(const T *)a0, (const T *)b0, (T *)d0, nullptr, (const T *)a1, (const T *)b1, (T *)d1};
-    const SegSrc src{code, a_off, b_off};
+    const SegSrc src{code, a_off, b_off, n_dev};
     if (d1) return scan_lb(ctx, src, SegCopyAct<T, true>{p}, n_seg, base, dst_off, ctx->ws);
     return scan_lb(ctx, src, SegCopyAct<T, false>{p}, n_seg, base, dst_off, ctx->ws);
 }
@@ -267,6 +269,22 @@ extern "C" int crdt_seg_gather2(crdt_ctx *ctx, size_t n_seg, const int64_t *code
         case 8: return seg_gather<uint64_t>(ctx, n_seg, code, a_off, b_off, base, dst_off, a0, b0, dst0, a1, b1, dst1);
         default: return CRDT_E_INVAL;
     }
+}
+
+// crdt_seg_gather2 over n_max segments of which only the first *n_dev (a
+// count still on the device, <= n_max) are real: the rest scan as empty, so
+// dst_off[i] = base + total for every i in [*n_dev, n_max].  Lets a caller
+// launch the gather behind the kernel that produces the count, without a
+// host round trip for it (the batched Server.merge()).
+int crdt::seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,
+                                 const uint64_t *a_off, const uint64_t *b_off, uint64_t *dst_off, const uint32_t *a0,
+                          const uint32_t *b0, uint32_t *dst0, const uint32_t *a1, const uint32_t *b1, uint32_t *dst1) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!dst_off || !n_dev || (n_max && (!code || !a_off || !a0 || !dst0 || (dst1 && !a1)))) return CRDT_E_INVAL;
+    rc = ws_reserve(ctx, scan_lb_tmp_bytes(n_max) + 4096);
+    if (rc) return rc;
+    return seg_gather<uint32_t>(ctx, n_max, code, a_off, b_off, 0, dst_off, a0, b0, dst0, a1, b1, dst1, n_dev);
 }
 
 extern "C" int crdt_seg_copy(crdt_ctx *ctx, size_t n_seg, const int64_t *code, const uint64_t *a_off,

@@ -624,21 +624,22 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
                          s.st_sum.as<int64_t>()};
     rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
-    uint64_t oo[2] = {0, 0};
-    e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    const uint64_t n_out = oo[1];
-    rc = crdt_seg_gather2(ctx, n_out, s.o_src.as<int64_t>(), s.dd.kv_off.as<uint64_t>(), s.r_kv.as<uint64_t>(), 0,
-                          s.dd2.kv_off.as<uint64_t>(), 4, s.dd.kv_key.p, s.dd.kv_key.p, s.dd2.kv_key.p, s.dd.kv_val.p,
-                          s.dd.kv_val.p, s.dd2.kv_val.p);
+    // the new Diff's kv pairs behind the merge, its entry count still on the
+    // device (dd2 is sized for |L| + |R|): one host synchronisation per merge
+    rc = seg_gather2_dev_count(ctx, nl + ne, s.o_off.as<uint64_t>() + 1, s.o_src.as<int64_t>(),
+                               s.dd.kv_off.as<uint64_t>(), s.r_kv.as<uint64_t>(), s.dd2.kv_off.as<uint64_t>(),
+                               s.dd.kv_key.as<uint32_t>(), s.dd.kv_key.as<uint32_t>(), s.dd2.kv_key.as<uint32_t>(),
+                               s.dd.kv_val.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), s.dd2.kv_val.as<uint32_t>());
     if (rc) return rc;
-    // CurrentState (main.go:76-96: rebuilt from empty) and the new pair count
+    // CurrentState (main.go:76-96: rebuilt from empty), the entry count and
+    // the new pair count (every dst offset from the entry count on = the total)
     std::vector<uint8_t> kind(nks);
     std::vector<uint32_t> sstr(nks);
     std::vector<int64_t> ssum(nks);
-    uint64_t new_nkv = 0;
-    e = hipMemcpyAsync(&new_nkv, s.dd2.kv_off.as<uint64_t>() + n_out, 8, hipMemcpyDeviceToHost, ctx->stream);
+    uint64_t oo[2] = {0, 0}, new_nkv = 0;
+    e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(&new_nkv, s.dd2.kv_off.as<uint64_t>() + nl + ne, 8, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(kind.data(), s.st_kind.p, nks, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(sstr.data(), s.st_str.p, nks * 4, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(ssum.data(), s.st_sum.p, nks * 8, hipMemcpyDeviceToHost, ctx->stream);
@@ -650,7 +651,7 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
         else if (kind[k] == 2) state.emplace(tab_str(ctx->keys, k), std::to_string((long long)ssum[k]));   // Itoa
     }
     std::swap(s.dd, s.dd2);
-    s.dd.n = n_out;
+    s.dd.n = oo[1];
     s.dd.n_kv = new_nkv;
     s.CurrentState.swap(state);
     s.state_view.clear();
@@ -692,10 +693,18 @@ __global__ void k_srv_concat(const SegPtrs *__restrict__ sp, int64_t *__restrict
 }
 
 // The batch's new Diffs back into each server's next buffers.
+// Server y's entry range is o_off[y, y+1) of the batch's new Diff and its
+// pair range kb[y, y+1): both read on the device (the destinations are sized
+// for the upper bound), so the split needs no host round trip.
 __global__ void k_srv_split(const SegPtrs *__restrict__ sp, const int64_t *__restrict__ o_ts,
                             const uint8_t *__restrict__ o_org, const uint64_t *__restrict__ o_kv,
-                            const uint32_t *__restrict__ kv_key, const uint32_t *__restrict__ kv_val) {
-    const SegPtrs p = sp[blockIdx.y];
+                            const uint32_t *__restrict__ kv_key, const uint32_t *__restrict__ kv_val,
+                            const uint64_t *__restrict__ o_off, const uint64_t *__restrict__ kb) {
+    SegPtrs p = sp[blockIdx.y];
+    p.e0 = o_off[blockIdx.y];
+    p.n = o_off[blockIdx.y + 1] - p.e0;
+    p.q0 = kb[blockIdx.y];
+    p.nq = kb[blockIdx.y + 1] - p.q0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i <= p.n; i += (uint64_t)gridDim.x * 256) {
         p.dkv_off[i] = o_kv[p.e0 + i] - p.q0;
         if (i < p.n) {
@@ -886,61 +895,59 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     crdt_refmerge_out ro{bb.o_off.as<uint64_t>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
                          bb.o_src.as<int64_t>(), bb.st_kind.as<uint8_t>(), bb.st_str.as<uint32_t>(),
                          bb.st_sum.as<int64_t>()};
+    // each server's next Diff buffers at their upper bound (its L + its pull),
+    // so the gather and the split run behind the merge with no host round
+    // trip for the output sizes: one synchronisation per call, for CurrentState
+    uint64_t maxs = 1;
+    std::vector<SegPtrs> sq(S);
+    for (size_t i = 0; i < S && !rc; ++i) {
+        Server &s = *srv[i];
+        const uint64_t nu = s.dd.n + (re[i + 1] - re[i]), qu = s.dd.n_kv + (rq[i + 1] - rq[i]);
+        rc = dbuf(ctx, s.dd2.ts, nu * 8 + 8);
+        if (!rc) rc = dbuf(ctx, s.dd2.origin, nu + 1);
+        if (!rc) rc = dbuf(ctx, s.dd2.kv_off, (nu + 1) * 8);
+        if (!rc) rc = dbuf(ctx, s.dd2.kv_key, qu * 4 + 4);
+        if (!rc) rc = dbuf(ctx, s.dd2.kv_val, qu * 4 + 4);
+        sq[i] = SegPtrs{nullptr, nullptr, nullptr, nullptr, nullptr, s.dd2.ts.as<int64_t>(),
+                        s.dd2.origin.as<uint8_t>(), s.dd2.kv_off.as<uint64_t>(), s.dd2.kv_key.as<uint32_t>(),
+                        s.dd2.kv_val.as<uint32_t>(), 0, 0, 0, 0, sbase[i], 0};
+        maxs = std::max<uint64_t>(maxs, std::max(nu + 1, qu));
+    }
+    if (rc) return rc;
     rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
     pc.mark("refmerge_launch");
-    std::vector<uint64_t> oo(S + 1);
-    e = hipMemcpyAsync(oo.data(), bb.o_off.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    pc.mark("refmerge_wait");
-    const uint64_t n_out = oo[S];
-    rc = crdt_seg_gather2(ctx, n_out, bb.o_src.as<int64_t>(), bb.l_kv.as<uint64_t>(), bb.r_kv.as<uint64_t>(), 0,
-                          bb.n_kv.as<uint64_t>(), 4, bb.kv_key.p, bb.kv_key.p, bb.n_key.p, bb.kv_val.p, bb.kv_val.p,
-                          bb.n_val.p);
+    // the new Diff's kv pairs (the entry count stays on the device), each
+    // server's pair range, the split into its next buffers, then CurrentState
+    rc = seg_gather2_dev_count(ctx, nl + nr, bb.o_off.as<uint64_t>() + S, bb.o_src.as<int64_t>(),
+                               bb.l_kv.as<uint64_t>(), bb.r_kv.as<uint64_t>(), bb.n_kv.as<uint64_t>(),
+                               bb.kv_key.as<uint32_t>(), bb.kv_key.as<uint32_t>(), bb.n_key.as<uint32_t>(),
+                               bb.kv_val.as<uint32_t>(), bb.kv_val.as<uint32_t>(), bb.n_val.as<uint32_t>());
     if (rc) return rc;
-    // pair ranges of each server's next Diff (gathered on the device), and CurrentState
-    std::vector<uint64_t> kb(S + 1);
     k_gather_at<<<grid_for(S + 1, 256, 1u << 20), 256, 0, st>>>(bb.n_kv.as<uint64_t>(), bb.o_off.as<uint64_t>(),
                                                                  S + 1, bb.kb.as<uint64_t>());
     rc = check_launch(ctx);
     if (rc) return rc;
-    e = hipMemcpyAsync(kb.data(), bb.kb.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
+    e = hipMemcpyAsync(bb.sp.p, sq.data(), S * sizeof(SegPtrs), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const dim3 g2(grid_for(maxs, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
+    k_srv_split<<<g2, 256, 0, st>>>(bb.sp.as<SegPtrs>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
+                                     bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>(),
+                                     bb.o_off.as<uint64_t>(), bb.kb.as<uint64_t>());
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    std::vector<uint64_t> oo(S + 1), kb(S + 1);
     std::vector<uint8_t> kind(nslots);
     std::vector<uint32_t> sstr(nslots);
     std::vector<int64_t> ssum(nslots);
+    e = hipMemcpyAsync(oo.data(), bb.o_off.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(kb.data(), bb.kb.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(kind.data(), bb.st_kind.p, nslots, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(sstr.data(), bb.st_str.p, nslots * 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ssum.data(), bb.st_sum.p, nslots * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);   // (also settles sp / sq, host vectors)
     if (e != hipSuccess) return hip_fail(ctx, e);
-    pc.mark("gather+state_d2h");
-    // split back into each server's next buffers
-    maxn = 1;
-    for (size_t i = 0; i < S; ++i) {
-        Server &s = *srv[i];
-        const uint64_t n = oo[i + 1] - oo[i], nq = kb[i + 1] - kb[i];
-        rc = dbuf(ctx, s.dd2.ts, n * 8 + 8);
-        if (!rc) rc = dbuf(ctx, s.dd2.origin, n + 1);
-        if (!rc) rc = dbuf(ctx, s.dd2.kv_off, (n + 1) * 8);
-        if (!rc) rc = dbuf(ctx, s.dd2.kv_key, nq * 4 + 4);
-        if (!rc) rc = dbuf(ctx, s.dd2.kv_val, nq * 4 + 4);
-        if (rc) return rc;
-        sp[i] = SegPtrs{nullptr, nullptr, nullptr, nullptr, nullptr, s.dd2.ts.as<int64_t>(),
-                        s.dd2.origin.as<uint8_t>(), s.dd2.kv_off.as<uint64_t>(), s.dd2.kv_key.as<uint32_t>(),
-                        s.dd2.kv_val.as<uint32_t>(), oo[i], n, kb[i], nq, sbase[i], 0};
-        maxn = std::max<uint64_t>(maxn, std::max(n + 1, nq));
-    }
-    e = hipMemcpyAsync(bb.sp.p, sp.data(), S * sizeof(SegPtrs), hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    const dim3 g2(grid_for(maxn, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
-    k_srv_split<<<g2, 256, 0, st>>>(bb.sp.as<SegPtrs>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
-                                     bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>());
-    rc = check_launch(ctx);
-    if (rc) return rc;
-    e = hipStreamSynchronize(st);                      // sp (host vector) and the next buffers settled
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    pc.mark("split");
+    pc.mark("gather+split+state_d2h");
     uint64_t nks = 0;
     (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);
     std::vector<std::string> kname(nks);
