@@ -94,6 +94,46 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
+E2E_MAX_BYTES = 4 << 30      # bounded: larger populations (vclock, configs[4]) are not staged through pinned memory
+
+
+def measure_e2e(wl, reps=3):
+    """SURVEY §8(d) "also report end-to-end time including H2D/D2H": the
+    step's inputs copied from pinned host memory into its device buffers
+    (same contents, so the outputs are unchanged), the step, and its outputs
+    copied back to pinned host memory, serialised on the launch stream and
+    timed by HIP events; median of `reps`.  Never the reported `value`."""
+    if not hasattr(wl, "io"):
+        return None
+    ins, outs = wl.io()
+    nbytes = lambda ts: sum(t.numel() * t.element_size() for t in ts)
+    n_in, n_out = nbytes(ins), nbytes(outs)
+    if n_in + n_out > E2E_MAX_BYTES:
+        return {"skipped": f"{(n_in + n_out) / 1e9:.1f} GB of inputs + outputs exceed the {E2E_MAX_BYTES >> 30} GiB "
+                           "pinned-staging bound of this measurement"}
+    stream = torch.cuda.current_stream()
+    h_in = [t.cpu().pin_memory() for t in ins]
+    h_out = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in outs]
+    ms = []
+    for r in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for d, h in zip(ins, h_in):
+            d.copy_(h, non_blocking=True)
+        wl.step()
+        for h, d in zip(h_out, wl.io()[1]):
+            h.copy_(d, non_blocking=True)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if r:
+            ms.append(e0.elapsed_time(e1))
+    med = float(np.median(ms))
+    return {"ms": round(med, 4), "value": round(wl.units() / (med / 1e3), 1), "unit": wl.unit,
+            "h2d_bytes": n_in, "d2h_bytes": n_out,
+            "timing": f"H2D of the step's inputs (pinned) + step + D2H of its outputs (pinned), one stream, "
+                      f"HIP events, median of {reps}"}
+
+
 def cpu_share() -> tuple[int, int]:
     """(threads for the CPU baseline, CPUs in this process's affinity mask).
     The box grants each GPU a CPU share that OMP_NUM_THREADS states while the
@@ -204,6 +244,9 @@ class GCounterJoin(Workload):
     def step(self):
         self.eng.gcounter_join(self.a, self.b, out=self.out)
 
+    def io(self):
+        return [self.a, self.b], [self.out]
+
     def cpu_baseline(self, seconds, threads):
         from oracle import oracle
         rows = min(self.rows, 250_000)
@@ -240,6 +283,9 @@ class PNCounterJoin(GCounterJoin):
     def step(self):
         self.eng.pncounter_join(self.a, self.na, self.b, self.nb, self.out, self.nout)
 
+    def io(self):
+        return [self.a, self.na, self.b, self.nb], [self.out, self.nout]
+
     def cpu_baseline(self, seconds, threads):
         return None
 
@@ -264,6 +310,9 @@ class VClockClassify(Workload):
 
     def step(self):
         self.eng.vclock_classify(self.a, self.b, out=self.cls)
+
+    def io(self):
+        return [self.a, self.b], [self.cls]
 
     def cpu_baseline(self, seconds, threads):
         from oracle import oracle
@@ -309,6 +358,14 @@ class SetMerge(Workload):
 
     def step(self):
         self._fn(self.A, self.B, out=self.out, count=self.count, trim=False)
+
+    def _sides(self):
+        return self.A, self.B
+
+    def io(self):
+        o = self.out.slice(self.n_out)
+        ins = [t for side in self._sides() for t in (side.key, side.ts, side.rep, side.tomb)]
+        return ins, [o.key, o.ts, o.rep, o.tomb, self.count]
 
     def cpu_baseline(self, seconds, threads):
         """The oracle's serial merge run on `threads` host threads, each over
@@ -379,6 +436,9 @@ class SetMergeUnsorted(SetMerge):
 
     def step(self):
         self._fn(self.UA, self.UB, out=self.out, count=self.count, trim=False)
+
+    def _sides(self):
+        return self.UA, self.UB
 
     def cpu_baseline(self, seconds, threads):
         """numpy lexsort of each unsorted side (the oracle's sort order) then
@@ -573,7 +633,13 @@ class RefMergeBatch(Workload):
                 + self.host["n_slots"] * 13 + int(self.host["str_off"][-1]))
 
     def step(self):
-        self.eng.refmerge_batch(self.dev)
+        self.last = self.eng.refmerge_batch(self.dev)
+
+    def io(self):
+        o, n, ns = self.last, self.n_out, int(self.host["n_slots"])
+        ins = [v for v in self.dev.values() if torch.is_tensor(v)]
+        return ins, [o["off"], o["ts"][:n], o["origin"][:n], o["src"][:n], o["st_kind"][:ns], o["st_str"][:ns],
+                     o["st_sum"][:ns]]
 
     def cpu_baseline(self, seconds, threads):
         """oc_refmerge, one replica per call (the reference merges under one
@@ -1012,6 +1078,7 @@ def main():
                 "kernel": wl.kernel, "bytes_per_launch": wl.bytes_per_launch(),
                 "avg_launch_us": round(avg_ms * 1e3, 2), "median_launch_us": round(med_ms * 1e3, 2),
                 "timing": "HIP events on the launch stream, per step"}
+        e2e = measure_e2e(wl) if world == 1 else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline and hasattr(wl, "cpu_baseline"):
             threads, aff = cpu_share()
@@ -1029,7 +1096,7 @@ def main():
             "higher_is_better": True, "scaling": getattr(wl, "scaling", "weak"),
             "vs_baseline": None, "dtype": wl.dtype,
             "data": "synthetic (SplitMix64-seeded, generated in HBM)",
-            "config": wl.config, "roofline": roof, "cpu_baseline": cpu,
+            "config": wl.config, "roofline": roof, "cpu_baseline": cpu, "e2e_pcie": e2e,
             "gpu_time_s": round(gpu_s, 6),
         }
         if hasattr(wl, "extra"):
