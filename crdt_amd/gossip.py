@@ -336,12 +336,17 @@ def random_peers(rng: np.random.Generator, total: int, first: int, count: int) -
 
     The reference draws uniformly from friendList (main.go:230), which is
     ports 8080..8089 (main.go:219-222): that list holds the server itself
-    and ports no server listens on, so some of its rounds pull its own Diff
-    (a no-op merge: equal keys keep the local entry, main.go:54-65) or fail
-    the request and skip (main.go:235-237).  This schedule keeps only the
-    rounds that move data: a uniform draw over the OTHER live replicas.  A
-    self-pull or a skipped round changes no state, so the reachable states
-    are the reference's; only the per-round pull rate differs."""
+    and ports no server listens on (the demo starts 8080..8084,
+    main.go:319-321), so some of its rounds fail the request and skip
+    (main.go:234-237: no merge) and some pull its own Diff.  A self-pull
+    inserts nothing (every key equal, the local entry kept, main.go:54-65)
+    but merge() still runs (main.go:257) and rebuilds CurrentState from the
+    remote-origin entries (main.go:76), dropping what local writes applied
+    to it directly (main.go:188-207) -- the same rebuild every merge ends
+    with.  This schedule draws uniformly over the OTHER live replicas only:
+    the Diffs it reaches are the reference's, and its CurrentState is the
+    rebuild after each round's merge; it never produces the reference's
+    merge-without-new-data rounds, so per-round pull rates differ."""
     r = rng.integers(0, total - 1, size=total)
     ids = np.arange(total)
     peers = np.where(r >= ids, r + 1, r)
