@@ -54,6 +54,8 @@ extern int g_vclock_blocks_per_cu;
 extern int g_sets_grid_per_cu; // persistent set-merge workgroups per CU (0 = occupancy query)
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
 extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at s_setprio 2, bit 1 spinning data barrier
+extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
+extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
 extern int g_sets_stamps;
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)

@@ -967,21 +967,22 @@ static inline bool dma_aligned(const crdt_tuples &t) {
     return !((((uintptr_t)t.key | (uintptr_t)t.ts) & 7) | ((uintptr_t)t.rep & 3));
 }
 
-template <bool DMA>
-__global__ __launch_bounds__(LWT) void k_lww_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
-                                                   const uint64_t *__restrict__ split,
-                                                   const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
-                                                   crdt_tuples out) {
-    constexpr int NWV = LWT / 64, FI = (LWH / 64) / NWV, CAP = LWH + 3;
-    static_assert(LNW == 64 && LWH * 2 == LT && FI * NWV * 64 == LWH, "shape");
+// WH merge items per workgroup (a 1/P of a tile, P = LT / WH), WT threads
+template <bool DMA, int WH = LWH, int WT = LWT>
+__global__ __launch_bounds__(WT) void k_lww_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                                  const uint64_t *__restrict__ split,
+                                                  const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
+                                                  crdt_tuples out) {
+    constexpr int NWV = WT / 64, FI = (WH / 64) / NWV, CAP = WH + 3, P = LT / WH, WPP = LNW / P;
+    static_assert(LNW == 64 && WH * P == LT && FI * NWV * 64 == WH && WH == 4 * WT, "shape");
     // (DMA: each field holds A's run then B's, each from its 16-byte aligned-down
     // start: up to 64 bytes more than the elements)
     __shared__ alignas(16) uint64_t s_key[CAP + 8];
     __shared__ alignas(16) uint64_t s_ts[CAP + 8];
     __shared__ alignas(16) uint32_t s_rep[CAP + 16];
     __shared__ alignas(16) uint8_t s_tomb[CAP + 64];
-    const uint64_t t = blockIdx.x >> 1;
-    const uint32_t h = blockIdx.x & 1;
+    const uint64_t t = blockIdx.x / P;
+    const uint32_t h = blockIdx.x % P;
     const LwwTile b = lww_tile(split, t, na + nb);
     const int lane = threadIdx.x & 63;
     const uint64_t word_a = bits[t * 2 * LNW + lane], word_e = bits[t * 2 * LNW + LNW + lane];
@@ -998,10 +999,10 @@ __global__ __launch_bounds__(LWT) void k_lww_write(crdt_tuples A, crdt_tuples B,
     pre_a -= (uint32_t)__popcll(word_a);
     pre_e -= (uint32_t)__popcll(word_e);
     // the half's runs: A [ra, ra + ca), B [rb, rb + cb); staged from ra - 2 / rb - 1
-    const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane(pre_a, 32 * h);        // A items before the half
-    const uint32_t ha1 = h ? b.na : (uint32_t)__builtin_amdgcn_readlane(pre_a, 32);  // ... before its end
-    const uint32_t d0 = LWH * h;
-    const uint32_t hn = b.n > d0 ? (b.n - d0 < (uint32_t)LWH ? b.n - d0 : (uint32_t)LWH) : 0;   // items in the half
+    const uint32_t ha = (uint32_t)__builtin_amdgcn_readlane(pre_a, WPP * h);       // A items before the part
+    const uint32_t ha1 = h + 1 == P ? b.na : (uint32_t)__builtin_amdgcn_readlane(pre_a, WPP * (h + 1));  // ... before its end
+    const uint32_t d0 = WH * h;
+    const uint32_t hn = b.n > d0 ? (b.n - d0 < (uint32_t)WH ? b.n - d0 : (uint32_t)WH) : 0;   // items in the part
     if (hn == 0) return;
     const size_t ra = b.i0 + ha, rb = b.j0 + (d0 - ha);
     const uint32_t ca = ha1 - ha, cb = hn - ca;
@@ -1034,7 +1035,7 @@ __global__ __launch_bounds__(LWT) void k_lww_write(crdt_tuples A, crdt_tuples B,
         bool v[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {                    // every staging load issued before the first store
-            const uint32_t x = threadIdx.x + (uint32_t)j * LWT;
+            const uint32_t x = threadIdx.x + (uint32_t)j * WT;
             const bool on_a = x < na2;
             const size_t g = on_a ? ra - 2 + x : rb - 1 + (x - na2);
             v[j] = x < nst && (on_a ? (ra + x >= 2 && g < na) : (rb + (x - na2) >= 1 && g < nb));
@@ -1045,7 +1046,7 @@ __global__ __launch_bounds__(LWT) void k_lww_write(crdt_tuples A, crdt_tuples B,
         }
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-            const uint32_t x = threadIdx.x + (uint32_t)j * LWT;
+            const uint32_t x = threadIdx.x + (uint32_t)j * WT;
             if (x < nst) {
                 s_key[x] = k[j];
                 s_ts[x] = ts[j];
@@ -1069,7 +1070,7 @@ __global__ __launch_bounds__(LWT) void k_lww_write(crdt_tuples A, crdt_tuples B,
     auto tomb_at = [&](uint32_t sl) -> uint8_t { return s_tomb[(int)sl + (sl < na2 ? oa_m : ob_m)]; };
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
-        const int w = 32 * (int)h + wvu + NWV * f;       // the tile's word
+        const int w = WPP * (int)h + wvu + NWV * f;      // the tile's word
         const uint64_t wa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_a >> 32), w) << 32) |
                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_a, w);
         const uint64_t we = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_e >> 32), w) << 32) |
@@ -1164,10 +1165,17 @@ static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, con
         if (rc) return rc;
         k_lww_total<<<1, 1, 0, s>>>(ic, ntiles, out_count);
     }
-    if (!(g_sets_knobs & 8) && dma_aligned(A) && dma_aligned(B))   // LDS-DMA staging (LWW 181 -> 178 us)
-        k_lww_write<true><<<(unsigned)(2 * ntiles), LWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
-    else
-        k_lww_write<false><<<(unsigned)(2 * ntiles), LWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
+    const bool dma = !(g_sets_knobs & 8) && dma_aligned(A) && dma_aligned(B);   // LDS-DMA staging (LWW 181 -> 178 us)
+    // workgroups per tile (sets.lww_parts): 1/P of a tile's items, 4 per thread
+    const unsigned P = (unsigned)g_lww_parts, g = (unsigned)(P * ntiles);
+#define LWW_WRITE(WH)                                                                                  \
+    (dma ? k_lww_write<true, WH, WH / 4><<<g, WH / 4, 0, s>>>(A, B, na, nb, split, bits, ic, O)        \
+         : k_lww_write<false, WH, WH / 4><<<g, WH / 4, 0, s>>>(A, B, na, nb, split, bits, ic, O))
+    if (P == 2) LWW_WRITE(2048);
+    else if (P == 8) LWW_WRITE(512);
+    else if (P == 16) LWW_WRITE(256);
+    else LWW_WRITE(1024);
+#undef LWW_WRITE
     return check_launch(ctx);
 }
 
@@ -1339,25 +1347,26 @@ __global__ __launch_bounds__(NT) void k_or_count(crdt_tuples A, crdt_tuples B, s
     }
 }
 
-template <bool DMA>
-__global__ __launch_bounds__(OWT) void k_or_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
-                                                  const uint64_t *__restrict__ split,
-                                                  const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
-                                                  crdt_tuples out) {
-    constexpr int NWV = OWT / 64, FI = ONW / NWV, CAP = OT + 2;
-    static_assert(FI * NWV == ONW && ONW <= 64, "shape");
+// WH merge items per workgroup (a 1/P of a tile, P = OT / WH), WT threads
+template <bool DMA, int WH = OT, int WT = OWT>
+__global__ __launch_bounds__(WT) void k_or_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                                 const uint64_t *__restrict__ split,
+                                                 const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
+                                                 crdt_tuples out) {
+    constexpr int NWV = WT / 64, P = OT / WH, WPP = ONW / P, FI = WPP / NWV, CAP = WH + 2;
+    static_assert(FI * NWV == WPP && WH * P == OT && ONW <= 64 && WH == 4 * WT, "shape");
     __shared__ alignas(16) uint64_t s_key[CAP + 8];
     __shared__ alignas(16) uint64_t s_ts[CAP + 8];
     __shared__ alignas(16) uint32_t s_rep[CAP + 16];
     __shared__ alignas(16) uint8_t s_tomb[CAP + 64];
-    const uint64_t t = blockIdx.x;
+    const uint64_t t = blockIdx.x / P;
+    const uint32_t h = blockIdx.x % P;
     const LwwTile b = or_tile(split, t, na + nb);
     const int lane = threadIdx.x & 63;
     const bool wl_ok = lane < ONW;
     // split, bitmap words and offset loads issued together (none after the barrier)
     const uint64_t word_a = wl_ok ? bits[t * 2 * ONW + lane] : 0, word_e = wl_ok ? bits[t * 2 * ONW + ONW + lane] : 0;
     const uint64_t ob = ic[t];
-    if (b.n == 0) return;
     uint32_t pre_a = (uint32_t)__popcll(word_a), pre_e = (uint32_t)__popcll(word_e);
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1369,37 +1378,44 @@ __global__ __launch_bounds__(OWT) void k_or_write(crdt_tuples A, crdt_tuples B, 
     }
     pre_a -= (uint32_t)__popcll(word_a);
     pre_e -= (uint32_t)__popcll(word_e);
-    // staged: A part (slots 0 .. na-1), then B part (slots na ..): every field once
-    // (DMA: slot x of field f at LDS element x + (x < na ? oa[f] : ob[f]))
-    const uint32_t nst = b.n;
+    // the part's runs: A [pa0, pa0 + ca), B [pb0, pb0 + cb) (tile-relative)
+    const uint32_t d0 = WH * h;
+    const uint32_t hn = b.n > d0 ? (b.n - d0 < (uint32_t)WH ? b.n - d0 : (uint32_t)WH) : 0;   // items in the part
+    if (hn == 0) return;
+    const uint32_t pa0 = P == 1 ? 0u : (uint32_t)__builtin_amdgcn_readlane(pre_a, WPP * h);
+    const uint32_t pa1 = h + 1 == P ? b.na : (uint32_t)__builtin_amdgcn_readlane(pre_a, WPP * (h + 1));
+    const uint32_t ca = pa1 - pa0, cb = hn - ca, pb0 = d0 - pa0;
+    const size_t ga = b.i0 + pa0, gb = b.j0 + pb0;       // global index of each run's first element
+    // staged: A run (slots 0 .. ca-1), then B run (slots ca ..): every field once
+    // (DMA: slot x of field f at LDS element x + (x < ca ? oa[f] : ob[f]))
     int oa_k = 0, ob_k = 0, oa_t = 0, ob_t = 0, oa_r = 0, ob_r = 0, oa_m = 0, ob_m = 0;
     if (DMA) {
         const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const int sb = (int)b.na;
+        const int sb = (int)ca;
         uint32_t at = 0;
-        oa_k = dma_run<uint64_t, NWV>(A.key, b.i0, b.na, s_key, &at, wv, lane);
-        ob_k = dma_run<uint64_t, NWV>(B.key, b.j0, b.nb, s_key, &at, wv, lane) - sb;
+        oa_k = dma_run<uint64_t, NWV>(A.key, ga, ca, s_key, &at, wv, lane);
+        ob_k = dma_run<uint64_t, NWV>(B.key, gb, cb, s_key, &at, wv, lane) - sb;
         at = 0;
-        oa_t = dma_run<uint64_t, NWV>(A.ts, b.i0, b.na, s_ts, &at, wv, lane);
-        ob_t = dma_run<uint64_t, NWV>(B.ts, b.j0, b.nb, s_ts, &at, wv, lane) - sb;
+        oa_t = dma_run<uint64_t, NWV>(A.ts, ga, ca, s_ts, &at, wv, lane);
+        ob_t = dma_run<uint64_t, NWV>(B.ts, gb, cb, s_ts, &at, wv, lane) - sb;
         at = 0;
-        oa_r = dma_run<uint32_t, NWV>(A.rep, b.i0, b.na, s_rep, &at, wv, lane);
-        ob_r = dma_run<uint32_t, NWV>(B.rep, b.j0, b.nb, s_rep, &at, wv, lane) - sb;
+        oa_r = dma_run<uint32_t, NWV>(A.rep, ga, ca, s_rep, &at, wv, lane);
+        ob_r = dma_run<uint32_t, NWV>(B.rep, gb, cb, s_rep, &at, wv, lane) - sb;
         at = 0;
-        oa_m = dma_run<uint8_t, NWV>(A.tomb, b.i0, b.na, s_tomb, &at, wv, lane);
-        ob_m = dma_run<uint8_t, NWV>(B.tomb, b.j0, b.nb, s_tomb, &at, wv, lane) - sb;
+        oa_m = dma_run<uint8_t, NWV>(A.tomb, ga, ca, s_tomb, &at, wv, lane);
+        ob_m = dma_run<uint8_t, NWV>(B.tomb, gb, cb, s_tomb, &at, wv, lane) - sb;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
     } else {
-        constexpr int NJ = (OT + OWT - 1) / OWT;
+        constexpr int NJ = (WH + WT - 1) / WT;
         uint64_t k[NJ], ts[NJ];
         uint32_t r[NJ];
         uint8_t m[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {                   // every staging load issued before the first store
-            const uint32_t x = threadIdx.x + (uint32_t)j * OWT;
-            const bool on_a = x < b.na;
-            const size_t g = on_a ? b.i0 + x : b.j0 + (x - b.na);
-            const bool v = x < nst;
+            const uint32_t x = threadIdx.x + (uint32_t)j * WT;
+            const bool on_a = x < ca;
+            const size_t g = on_a ? ga + x : gb + (x - ca);
+            const bool v = x < hn;
             k[j] = v ? (on_a ? A.key : B.key)[g] : 0;
             ts[j] = v ? (on_a ? A.ts : B.ts)[g] : 0;
             r[j] = v ? (on_a ? A.rep : B.rep)[g] : 0;
@@ -1407,8 +1423,8 @@ __global__ __launch_bounds__(OWT) void k_or_write(crdt_tuples A, crdt_tuples B, 
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const uint32_t x = threadIdx.x + (uint32_t)j * OWT;
-            if (x < nst) {
+            const uint32_t x = threadIdx.x + (uint32_t)j * WT;
+            if (x < hn) {
                 s_key[x] = k[j];
                 s_ts[x] = ts[j];
                 s_rep[x] = r[j];
@@ -1423,40 +1439,40 @@ __global__ __launch_bounds__(OWT) void k_or_write(crdt_tuples A, crdt_tuples B, 
     };
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
-        const int w = wvu + NWV * f;                     // the tile's word
+        const int w = WPP * (int)h + wvu + NWV * f;      // the tile's word
         // (readlane returns int: widen through uint32_t, never sign-extend)
         const uint64_t wa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_a >> 32), w) << 32) |
                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_a, w);
         const uint64_t we = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_e >> 32), w) << 32) |
                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_e, w);
         if (!((we >> lane) & 1)) continue;
-        const uint32_t la = (uint32_t)__builtin_amdgcn_readlane(pre_a, w) + below(wa);   // A items before (tile)
-        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane(pre_e, w) + below(we);   // output rank
-        const uint32_t k = 64u * (uint32_t)w + (uint32_t)lane;
-        const uint32_t lb = k - la;                      // B items before
+        const uint32_t la = (uint32_t)__builtin_amdgcn_readlane(pre_a, w) + below(wa) - pa0;   // A items before (part)
+        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane(pre_e, w) + below(we);         // output rank (tile)
+        const uint32_t k = 64u * (uint32_t)w + (uint32_t)lane - d0;
+        const uint32_t lb = k - la;                      // B items before (part)
         const bool is_a = (wa >> lane) & 1;
-        const uint32_t xs = is_a ? la : b.na + lb;       // the first copy's slot
+        const uint32_t xs = is_a ? la : ca + lb;         // the first copy's slot
         const int xo = is_a ? 0 : 1;
         const uint64_t key = s_key[(int)xs + (xo ? ob_k : oa_k)], ts = s_ts[(int)xs + (xo ? ob_t : oa_t)];
         const uint32_t rep = s_rep[(int)xs + (xo ? ob_r : oa_r)];
         uint32_t tomb = 0;
         // A's copies (an A first copy only), then B's from position lb:
-        // in the staging, then past the tile in global memory (rare)
+        // in the staging, then past the part in global memory (rare)
         if (is_a) {
             uint32_t s = la;
-            while (s < b.na && s_key[(int)s + oa_k] == key && s_ts[(int)s + oa_t] == ts && s_rep[(int)s + oa_r] == rep)
+            while (s < ca && s_key[(int)s + oa_k] == key && s_ts[(int)s + oa_t] == ts && s_rep[(int)s + oa_r] == rep)
                 tomb |= s_tomb[(int)(s++) + oa_m];
-            if (s == b.na)
-                for (size_t g = b.i1; g < na && A.key[g] == key && A.ts[g] == ts && A.rep[g] == rep; ++g)
+            if (s == ca)
+                for (size_t g = ga + ca; g < na && A.key[g] == key && A.ts[g] == ts && A.rep[g] == rep; ++g)
                     tomb |= A.tomb[g];
         }
         {
             uint32_t s = lb;
-            while (s < b.nb && s_key[(int)(b.na + s) + ob_k] == key && s_ts[(int)(b.na + s) + ob_t] == ts &&
-                   s_rep[(int)(b.na + s) + ob_r] == rep)
-                tomb |= s_tomb[(int)(b.na + s++) + ob_m];
-            if (s == b.nb)
-                for (size_t g = b.j1; g < nb && B.key[g] == key && B.ts[g] == ts && B.rep[g] == rep; ++g)
+            while (s < cb && s_key[(int)(ca + s) + ob_k] == key && s_ts[(int)(ca + s) + ob_t] == ts &&
+                   s_rep[(int)(ca + s) + ob_r] == rep)
+                tomb |= s_tomb[(int)(ca + s++) + ob_m];
+            if (s == cb)
+                for (size_t g = gb + cb; g < nb && B.key[g] == key && B.ts[g] == ts && B.rep[g] == rep; ++g)
                     tomb |= B.tomb[g];
         }
         const uint64_t o = ob + rk;
@@ -1494,10 +1510,16 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
         if (rc) return rc;
         k_lww_total<<<1, 1, 0, s>>>(ic, ntiles, out_count);
     }
-    if (!(g_sets_knobs & 8) && dma_aligned(A) && dma_aligned(B))   // LDS-DMA staging (LWW 181 -> 178 us)
-        k_or_write<true><<<(unsigned)ntiles, OWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
-    else
-        k_or_write<false><<<(unsigned)ntiles, OWT, 0, s>>>(A, B, na, nb, split, bits, ic, O);
+    const bool dma = !(g_sets_knobs & 8) && dma_aligned(A) && dma_aligned(B);   // LDS-DMA staging
+    // workgroups per tile (sets.or_parts): 1/P of a tile's items, 4 per thread
+    const unsigned P = (unsigned)g_or_parts, g = (unsigned)(P * ntiles);
+#define OR_WRITE(WH)                                                                                   \
+    (dma ? k_or_write<true, WH, WH / 4><<<g, WH / 4, 0, s>>>(A, B, na, nb, split, bits, ic, O)         \
+         : k_or_write<false, WH, WH / 4><<<g, WH / 4, 0, s>>>(A, B, na, nb, split, bits, ic, O))
+    if (P == 2) OR_WRITE(1024);
+    else if (P == 4) OR_WRITE(512);
+    else OR_WRITE(2048);
+#undef OR_WRITE
     return check_launch(ctx);
 }
 

@@ -168,3 +168,39 @@ def test_sets_alternative_kernels(eng, knobs):
         assert eng.device_status(clear=True) == 0
     finally:
         _lib.call("crdt_set_option", b"sets.knobs", 1)
+
+
+@pytest.mark.parametrize("parts", [2, 8, 16])
+def test_lww_write_parts(eng, parts):
+    """The LWW write pass at every workgroup shape (sets.lww_parts: 1/parts of
+    a 4096-item tile per workgroup; default 4): tile and part edges, long key
+    runs across parts, unaligned views (register staging)."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"sets.lww_parts", parts)
+    try:
+        _check(eng, *_sets(91, 100_000, 90_000, 40_000))
+        for na, nb in ((4095, 1), (4096, 4096), (1023, 1025), (255, 257), (0, 5000)):
+            _check(eng, *_sets(92 + na, na, nb, max(1, (na + nb) // 3)))
+        test_sets_long_runs_cross_tiles(eng)
+        test_sets_unaligned_views(eng, 3, 5)
+    finally:
+        _lib.call("crdt_set_option", b"sets.lww_parts", 4)
+
+
+@pytest.mark.parametrize("parts", [1, 2, 4])
+def test_orset_write_parts(eng, parts):
+    """The OR-Set write pass at every workgroup shape (sets.or_parts: 1/parts
+    of a 2048-item tile per workgroup): tile and part edges, tag copies that
+    run past a part (the global-memory walk), unaligned views."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"sets.or_parts", parts)
+    try:
+        _check(eng, *_sets(93, 100_000, 90_000, 40_000))
+        for na, nb in ((2047, 1), (2048, 2048), (511, 513), (1023, 1025), (0, 3000)):
+            _check(eng, *_sets(94 + na, na, nb, max(1, (na + nb) // 3)))
+        test_sets_long_runs_cross_tiles(eng)
+        test_sets_identical_inputs_idempotent(eng)
+        test_sets_unaligned_views(eng, 3, 5)
+        test_sets_unaligned_views(eng, 13, 11)
+    finally:
+        _lib.call("crdt_set_option", b"sets.or_parts", 1)
