@@ -56,6 +56,7 @@ extern int g_rm_diag;           // timing diagnostic: refmerge replay fold varia
 extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at s_setprio 2, bit 1 spinning data barrier
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
+extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
 extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
 extern int g_sets_stamps;
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)

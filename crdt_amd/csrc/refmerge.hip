@@ -470,16 +470,20 @@ enum { RM_FOLD_NONE = 0, RM_FOLD_FULL = 1, RM_FOLD_DELTA = 2 };
 //        (max, holder count, wrapped sum, parsable count); each R entry's
 //        rank (0: not inserted) goes to r_dk for the holder pass's
 //        overflow walk.
-template <int FOLD>
-__global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+template <int FOLD, int PARTS = 1>
+__global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                 const uint64_t *__restrict__ bits, uint16_t *__restrict__ r_dk,
                                                 const OkVal *__restrict__ okv, SlotAcc acc, int diag,
                                                 const uint64_t *__restrict__ ic, crdt_refmerge_out out,
                                                 crdt_replay_state st, RpCand *__restrict__ cand,
                                                 uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf) {
-    constexpr int NWV = FB / 64;                         // waves
-    static_assert(FI * NWV == NW, "each wave takes FI words of 64 items");
+    // PARTS > 1: each workgroup takes 1/PARTS of the tile's items (words
+    // WPP h .. WPP h + WPP - 1) with FB / PARTS threads and its own slot table
+    constexpr int WT = FB / PARTS, NWV = WT / 64, WPP = NW / PARTS;   // threads, waves, words per workgroup
+    static_assert(FI * NWV == WPP, "each wave takes FI words of 64 items");
     constexpr bool DELTA = FOLD == RM_FOLD_DELTA, FOLDS = FOLD != RM_FOLD_NONE;
+    static_assert(!DELTA || PARTS == 1, "the delta fold keeps one candidate list per tile");
+    static_assert(WT >= (int)OKC, "one thread per staged Atoi record");
     constexpr int TN = FOLDS ? TT : 1;
     __shared__ uint32_t t_slot[TN];
     __shared__ uint32_t t_nh[DELTA ? TT : 1];
@@ -490,7 +494,8 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     __shared__ uint32_t t_npar[TN];
     __shared__ int64_t s_okval[FOLDS ? OKC : 1];
     __shared__ uint8_t s_okok[FOLDS ? OKC : 1];
-    const uint64_t t = blockIdx.x;
+    const uint64_t t = blockIdx.x / PARTS;
+    const int part = (int)(blockIdx.x % PARTS);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     // the descriptors, the tile's bitmap words (one of each bitmap per lane),
     // its offset and the staged Atoi records are independent loads: all issued
@@ -523,7 +528,7 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     const uint64_t ob = d.l0 + ict;
     if (DELTA && threadIdx.x == 0) s_nc = s_ovf = 0;
     if (FOLDS)
-        for (int h = threadIdx.x; h < TT; h += FB) {
+        for (int h = threadIdx.x; h < TT; h += WT) {
             t_slot[h] = kEmpty;
             t_best[h] = 0;
             t_sum[h] = 0;
@@ -545,7 +550,7 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     // flags, L / R index and rank are recomputed from them where used.
     uint64_t s_wl[FI], s_we[FI];
     uint32_t s_pl[FI], s_pe[FI];
-    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    const int wvu = __builtin_amdgcn_readfirstlane(wv) + WPP * part;   // this wave's first word
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
         const int w = wvu + NWV * f;
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(FB, 8) void k_rm_tile(crdt_refmerge_in in, const Ti
     }
     __syncthreads();
     if (diag == 2) return;
-    for (int h = threadIdx.x; h < TT; h += FB) {
+    for (int h = threadIdx.x; h < TT; h += WT) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;
         if (DELTA) {
@@ -998,14 +1003,21 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
         return rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, true);
     }
+    // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
+#define RM_TILE(F, P, DIAG)                                                                                   \
+    k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out, crdt_replay_state{}, \
+                                              nullptr, nullptr, nullptr)
     if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
-        k_rm_tile<RM_FOLD_NONE><<<tg, FB, 0, s>>>(in, desc, bits, nullptr, okv, acc, 0, ic, out, crdt_replay_state{},
-                                                  nullptr, nullptr, nullptr);
+        if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, 0);
+        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, 0);
+        else RM_TILE(RM_FOLD_NONE, 1, 0);
         if (!ns || delta) return check_launch(ctx);
     } else {
-        k_rm_tile<RM_FOLD_FULL><<<tg, FB, 0, s>>>(in, desc, bits, nullptr, okv, acc, g_rm_diag, ic, out,
-                                                  crdt_replay_state{}, nullptr, nullptr, nullptr);
+        if (g_rm_parts == 2) RM_TILE(RM_FOLD_FULL, 2, g_rm_diag);
+        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_FULL, 4, g_rm_diag);
+        else RM_TILE(RM_FOLD_FULL, 1, g_rm_diag);
     }
+#undef RM_TILE
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
     return check_launch(ctx);
 }

@@ -219,3 +219,21 @@ def test_slice_write_without_slots(eng):
     np.testing.assert_array_equal(bare["off"].cpu().numpy(), full["off"].cpu().numpy())
     for k in ("ts", "origin", "src"):
         np.testing.assert_array_equal(bare[k][:n].cpu().numpy(), full[k][:n].cpu().numpy())
+
+
+@pytest.mark.parametrize("parts", [2, 4])
+def test_tile_parts_match_oracle(eng, parts):
+    """The tile pass at every workgroup shape (refmerge.tile_parts: 1/parts of
+    a 4096-item tile per workgroup, each with its own slot table): the packed
+    batch with LDS-staged and global Atoi tables, the KATs and multi-key
+    config-A replicas, every replica against the oracle."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"refmerge.tile_parts", parts)
+    try:
+        for n_str in (0, 257):
+            test_packed_batch_matches_oracle(eng, n_str)
+        test_all_kats_in_one_batch(eng)
+        test_config_a_demo_matches_oracle(eng, 1)
+        test_large_batch_matches_oracle(eng)
+    finally:
+        _lib.call("crdt_set_option", b"refmerge.tile_parts", 1)

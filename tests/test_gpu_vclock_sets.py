@@ -203,4 +203,4 @@ def test_orset_write_parts(eng, parts):
         test_sets_unaligned_views(eng, 3, 5)
         test_sets_unaligned_views(eng, 13, 11)
     finally:
-        _lib.call("crdt_set_option", b"sets.or_parts", 1)
+        _lib.call("crdt_set_option", b"sets.or_parts", 2)
