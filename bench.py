@@ -1014,6 +1014,7 @@ def main():
     ap.add_argument("--demo-entries", type=int, default=10_000)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive e2e_pcie measurement")
     ap.add_argument("--option", action="append", default=[], help="name=value kernel knob (crdt_set_option)")
     args = ap.parse_args()
 
@@ -1080,7 +1081,7 @@ def main():
                 "kernel": wl.kernel, "bytes_per_launch": wl.bytes_per_launch(),
                 "avg_launch_us": round(avg_ms * 1e3, 2), "median_launch_us": round(med_ms * 1e3, 2),
                 "timing": "HIP events on the launch stream, per step"}
-        e2e = measure_e2e(wl) if world == 1 else None
+        e2e = measure_e2e(wl) if world == 1 and not args.no_e2e else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline and hasattr(wl, "cpu_baseline"):
             threads, aff = cpu_share()
