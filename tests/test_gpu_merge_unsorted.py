@@ -103,3 +103,16 @@ def test_unsorted_full_config_d_equals_two_sort_path(eng):
         assert len(got) == len(ref)
         for g, e in zip((got.key, got.ts, got.rep, got.tomb), (ref.key, ref.ts, ref.rep, ref.tomb)):
             assert bool((g == e).all())
+
+
+@pytest.mark.parametrize("n", [1, 5000])
+def test_unsorted_single_tag(eng, n):
+    """Every tuple the same tag (only side and tomb differ): no tag bit to sort
+    on, one composing pass; LWW takes A's least tomb, OR-Set ORs them all."""
+    rng = np.random.default_rng(n)
+    k = np.full(n, 7, np.uint64)
+    t = np.full(n, 2**40, np.uint64)
+    r = np.full(n, 3, np.uint32)
+    _check(eng, (k, t, r, rng.integers(0, 2, n, dtype=np.uint8)), (k.copy(), t.copy(), r.copy(),
+                                                                  rng.integers(0, 2, n, dtype=np.uint8)))
+    _check(eng, (k[:0], t[:0], r[:0], np.zeros(0, np.uint8)), (k, t, r, np.ones(n, np.uint8)))
