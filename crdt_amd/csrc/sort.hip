@@ -45,6 +45,7 @@ struct SortPlan {
     uint32_t bk, bt, br;         // bit widths of the key / ts / rep offsets
     uint32_t W, P, words;        // composite bits, passes, 64-bit words
     uint32_t b0;                 // bit offset of the rep field: 1 (tomb) + side bits (0 or 1)
+    uint32_t s0;                 // bit of the first digit (0: the whole composite is sorted)
     uint64_t n1;                 // composites [0, n1) come from in (side 0), [n1, n) from in2 (side 1)
     crdt_tuples in2;
 };
@@ -128,7 +129,8 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, So
 
 // reduces the nmm minmax partials, then thread 0 sizes the composite
 __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32_t nmm, SortPlan *plan,
-                                                   uint32_t side_bits, crdt_tuples in2, uint64_t n1) {
+                                                   uint32_t side_bits, crdt_tuples in2, uint64_t n1,
+                                                   uint32_t key_only = 0) {
     __shared__ unsigned long long sr[6][256];
     const int tid = threadIdx.x;
     unsigned long long v[6] = {~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
@@ -166,8 +168,14 @@ __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32
     p.bt = bitwidth(mm->tmax - mm->tmin);
     p.br = bitwidth(mm->rmax - mm->rmin);
     p.W = p.bk + p.bt + p.br + p.b0;
-    p.P = (p.W + 7) / 8;
     p.words = (p.W + 63) / 64;
+    // key_only (the fused LWW merge): sort on the key's bits alone -- the
+    // passes are stable, so each key's tuples stay in input order (A's, then
+    // B's) and the dedup finds the winning tag within the key's run.  Config
+    // D: 23 key bits, 3 passes instead of 7.  Single-word composites (a
+    // shifted digit never straddles a word there).
+    p.s0 = (key_only && p.words == 1) ? p.W - p.bk : 0;
+    p.P = p.W - p.s0 ? (p.W - p.s0 + 7) / 8 : 1;        // >= 1: the first pass composes
     *plan = p;
 }
 
@@ -217,8 +225,8 @@ __device__ __forceinline__ CKey<WORDS> compose(const SortPlan &p, uint64_t k, ui
     return c;
 }
 template <int WORDS>
-__device__ __forceinline__ uint32_t digit_of(const CKey<WORDS> &c, uint32_t pass) {
-    const uint32_t s = 8 * pass;
+__device__ __forceinline__ uint32_t digit_of(const CKey<WORDS> &c, uint32_t pass, uint32_t s0) {
+    const uint32_t s = 8 * pass + s0;
     uint64_t x = c.w[0];                      // select, not a runtime index: keeps c in registers
 #pragma unroll
     for (int q = 1; q < WORDS; ++q)
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < SR; ++r)
-        if (base + (size_t)r * SB + tid < n) atomicAdd(&h[w * 256 + digit_of(c[r], pass)], 1u);
+        if (base + (size_t)r * SB + tid < n) atomicAdd(&h[w * 256 + digit_of(c[r], pass, p.s0)], 1u);
     __syncthreads();
     uint32_t v = 0;
 #pragma unroll
@@ -369,7 +377,7 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
     for (int r = 0; r < SR; ++r) {
         const size_t e = base + (size_t)r * SB + tid;
         const bool valid = e < n;
-        const uint32_t d = valid ? digit_of(c[r], pass) : 0u;
+        const uint32_t d = valid ? digit_of(c[r], pass, p.s0) : 0u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -435,7 +443,7 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
         CKey<WORDS> v;
 #pragma unroll
         for (int q = 0; q < WORDS; ++q) v.w[q] = stage[q * ST + j];
-        const uint32_t d = digit_of(v, pass);
+        const uint32_t d = digit_of(v, pass, p.s0);
         const size_t o = (size_t)s_excl[d] + (uint32_t)(j - (int)s_lstart[d]);
         if constexpr (LAST) {
             out.key[o] = p.kmin + get_bits(v, p.b0 + p.br + p.bt, p.bk);
@@ -543,6 +551,57 @@ __device__ __forceinline__ bool eq_from(const CKey<WORDS> &x, const CKey<WORDS> 
     }
     return eq;
 }
+// bits [s, 64*WORDS) of x against y's: -1 / 0 / +1
+template <int WORDS>
+__device__ __forceinline__ int cmp_from(const CKey<WORDS> &x, const CKey<WORDS> &y, uint32_t s) {
+    int r = 0;
+#pragma unroll
+    for (int q = WORDS - 1; q >= 0; --q) {
+        const uint32_t lo = 64u * q;
+        if (s >= lo + 64) continue;
+        const uint64_t m = s > lo ? ~0ULL << (s - lo) : ~0ULL;
+        const uint64_t a = x.w[q] & m, b = y.w[q] & m;
+        if (r == 0 && a != b) r = a > b ? 1 : -1;
+    }
+    return r;
+}
+// LWW winner of a key's run, whatever the run's order (a key-only sort
+// leaves it in input order): the max (ts, rep) tag; its tomb that of the
+// tag's first copy in (key, ts, rep, side, tomb) order -- the least tomb of
+// A's copies, else of B's (side = bit 1 when b0 > 1)
+template <int WORDS>
+struct LwwWin {                                          // (scalars, not side-indexed arrays: no scratch)
+    CKey<WORDS> win;
+    uint32_t ta, tb, ha, hb;                             // least tomb and "holds the tag", side A / side B
+    __device__ __forceinline__ void reset(const CKey<WORDS> &x, uint32_t b0) {
+        const bool sb = b0 > 1 && ((x.w[0] >> 1) & 1u);
+        const uint32_t xt = (uint32_t)x.w[0] & 1u;
+        ta = sb ? 1u : xt;
+        tb = sb ? xt : 1u;
+        ha = sb ? 0u : 1u;
+        hb = sb ? 1u : 0u;
+    }
+    __device__ __forceinline__ LwwWin(const CKey<WORDS> &x, uint32_t b0) : win(x) { reset(x, b0); }
+    __device__ __forceinline__ void consider(const CKey<WORDS> &x, uint32_t b0) {
+        const int o = cmp_from(x, win, b0);
+        if (o > 0) {                                    // a larger tag
+            win = x;
+            reset(x, b0);
+        } else if (o == 0) {
+            const bool sb = b0 > 1 && ((x.w[0] >> 1) & 1u);
+            const uint32_t xt = (uint32_t)x.w[0] & 1u;
+            if (sb) {
+                tb &= xt;
+                hb = 1u;
+            } else {
+                ta &= xt;
+                ha = 1u;
+            }
+        }
+    }
+    __device__ __forceinline__ uint32_t tomb() const { return ha ? ta : tb; }
+};
+
 template <int MODE, int WORDS>
 __global__ __launch_bounds__(DB) void k_dd_count(const uint64_t *__restrict__ c, size_t n,
                                                  const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt) {
@@ -593,6 +652,7 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
                                                  const uint32_t *__restrict__ tot, crdt_tuples out,
                                                  uint64_t *__restrict__ out_count) {
     __shared__ uint32_t s_c[DI * (DB / 64)];      // emits per (round, wave), then their exclusive prefix
+    __shared__ uint64_t s_v[MODE == DD_LWW ? DT * WORDS : 1];   // LWW: the tile's composites (run walks)
     const SortPlan p = *plan_;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const size_t base = (size_t)blockIdx.x * DT;
@@ -609,6 +669,9 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         else
 #pragma unroll
             for (int q = 0; q < WORDS; ++q) v[r].w[q] = 0;
+        if constexpr (MODE == DD_LWW)
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) s_v[q * DT + r * DB + tid] = v[r].w[q];
     }
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
@@ -622,14 +685,17 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         const bool valid = e < n, has_next = e + 1 < n, has_prev = e > 0;
         if (lane == 63 && has_next) nx = ck_load<WORDS>(c, n, e + 1);
         if (lane == 0 && has_prev && valid) pv = ck_load<WORDS>(c, n, e - 1);
-        const bool same_prev = has_prev && eq_from(pv, v[r], p.b0);     // previous copy of the same tag
         const bool same_next = has_next && eq_from(nx, v[r], p.b0);
         bool f;
         if constexpr (MODE == DD_LWW) {
-            f = valid && (!has_next || !eq_from(v[r], nx, p.b0 + p.br + p.bt));
-            tb[r] = (uint8_t)((v[r].w[0] & 1u) | (same_prev ? 2u : 0u));
+            // the last tuple of a key run emits; with a previous tuple of the
+            // same key the run is walked for its winning tag (bit 1)
+            const uint32_t kb = p.b0 + p.br + p.bt;
+            f = valid && (!has_next || !eq_from(v[r], nx, kb));
+            // bit 1: an earlier tuple of the same key -- the emit walks the run
+            tb[r] = (uint8_t)((v[r].w[0] & 1u) | (valid && has_prev && eq_from(pv, v[r], kb) ? 2u : 0u));
         } else {
-            f = valid && !same_prev;
+            f = valid && !(has_prev && eq_from(pv, v[r], p.b0));     // the first copy of its tag
             tb[r] = (uint8_t)((v[r].w[0] & 1u) | (same_next ? 2u : 0u));
         }
         em[r] = __ballot(f);
@@ -653,11 +719,27 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         const size_t e = base + (size_t)r * DB + tid;
         const size_t o = t0 + s_c[r * (DB / 64) + w] + (uint32_t)__popcll(em[r] & ((1ULL << lane) - 1ULL));
         uint8_t tomb = tb[r] & 1u;
+        CKey<WORDS> win = v[r];
         if (tb[r] & 2u) {
-            if constexpr (MODE == DD_LWW) {       // tomb of the first copy of this tag
-                size_t j = e - 1;
-                while (j > 0 && eq_from(ck_load<WORDS>(c, n, j - 1), v[r], p.b0)) --j;
-                tomb = (uint8_t)(ck_load<WORDS>(c, n, j).w[0] & 1u);
+            if constexpr (MODE == DD_LWW) {
+                // the key's run backwards: the tile's part from LDS, the rest
+                // (a run reaching back past the tile) from global memory
+                const uint32_t kb = p.b0 + p.br + p.bt;
+                LwwWin<WORDS> lw(win, p.b0);
+                for (size_t j = e; j > 0;) {
+                    --j;
+                    CKey<WORDS> x;
+                    if (j >= base) {
+#pragma unroll
+                        for (int q = 0; q < WORDS; ++q) x.w[q] = s_v[q * DT + (j - base)];
+                    } else {
+                        x = ck_load<WORDS>(c, n, j);
+                    }
+                    if (!eq_from(x, v[r], kb)) break;
+                    lw.consider(x, p.b0);
+                }
+                win = lw.win;
+                tomb = lw.tomb();
             } else {                              // OR over the tag's copies
                 for (size_t j = e + 1; j < n; ++j) {
                     const CKey<WORDS> x = ck_load<WORDS>(c, n, j);
@@ -666,9 +748,9 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
                 }
             }
         }
-        out.key[o] = p.kmin + get_bits(v[r], sk, p.bk);
-        out.ts[o] = p.tmin + get_bits(v[r], p.b0 + p.br, p.bt);
-        out.rep[o] = (uint32_t)(p.rmin + get_bits(v[r], p.b0, p.br));
+        out.key[o] = p.kmin + get_bits(win, sk, p.bk);
+        out.ts[o] = p.tmin + get_bits(win, p.b0 + p.br, p.bt);
+        out.rep[o] = (uint32_t)(p.rmin + get_bits(win, p.b0, p.br));
         out.tomb[o] = tomb;
     }
 }
@@ -716,7 +798,7 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
     unsigned nmm = na ? launch_minmax(ctx, A, na, mm) : 0;
     if (nb) nmm += launch_minmax(ctx, B, nb, mm + nmm);
-    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na);
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, MODE == DD_LWW ? 1u : 0u);
     SortPlan h;
     hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
