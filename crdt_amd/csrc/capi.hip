@@ -232,7 +232,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         g_sets_grid_per_cu = (int)v;
     } else if (!strcmp(name, "sets.knobs")) {        // bit 0: control-wave priority; bit 1: spinning data barrier;
         if (v < 0 || v > 15) return CRDT_E_INVAL;    //   bit 2: the persistent tag-merge kernel (LWW, OR-Set);
-                                                     //   bit 3: register (not LDS-DMA) staging in the two-pass write passes
+                                                     //   bit 3: register (not LDS-DMA) staging in the two-pass
+                                                     //   write passes and the LWW count pass
         g_sets_knobs = (int)v;
     } else if (!strcmp(name, "sets.lww_parts")) {    // LWW write-pass workgroups per 4096-item tile
         if (v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;

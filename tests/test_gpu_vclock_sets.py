@@ -155,7 +155,7 @@ def test_sets_unaligned_views(eng, off_a, off_b):
 @pytest.mark.parametrize("knobs", [9, 5])
 def test_sets_alternative_kernels(eng, knobs):
     """The non-default set-merge forms (sets.knobs): 9 = the two-pass write
-    passes with register staging instead of LDS-DMA, 5 = round 1's persistent
+    passes and the LWW count pass with register staging instead of LDS-DMA, 5 = round 1's persistent
     look-back kernel; same outputs as the oracle on long runs, tile edges and
     views off a 16-byte boundary."""
     from crdt_amd import _lib
