@@ -17,6 +17,7 @@ int g_sets_diag = 0;
 int g_sets_knobs = 1;
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
+int g_rm_count_dma = 1;
 int g_lww_parts = 4;     // LWW write pass: quarter tiles (half tiles 112 -> 105 us)
 int g_rm_diag = 0;
 int g_scan_items = 8;
@@ -241,6 +242,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.or_parts")) {     // OR-Set write-pass workgroups per 2048-item tile
         if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
         g_or_parts = (int)v;
+    } else if (!strcmp(name, "refmerge.count_dma")) {   // RefMerge count pass: ts runs staged by LDS-DMA
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_rm_count_dma = (int)v;
     } else if (!strcmp(name, "refmerge.tile_parts")) {   // RefMerge tile-pass workgroups per 4096-item tile
         if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
         g_rm_parts = (int)v;

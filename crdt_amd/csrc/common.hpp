@@ -57,6 +57,7 @@ extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
+extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmerge.count_dma)
 extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
 extern int g_sets_stamps;
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
@@ -133,6 +134,32 @@ __host__ __device__ inline uint64_t stream_key(uint64_t seed, uint64_t stream) {
 // i-th output of a SplitMix64 sequence started at state k.
 __host__ __device__ inline uint64_t rnd(uint64_t k, uint64_t i) {
     return splitmix64(k + i * 0x9E3779B97F4A7C15ULL);
+}
+
+
+// LDS-DMA staging of one side's run of one field: elements [g0, g0 + cnt) of
+// src into the byte array dst from byte *at (16-byte aligned), in 16-byte
+// chunks from src + g0's aligned-down address (global_load_lds_dwordx4: 1 KB
+// per wave instruction, no VGPRs), the workgroup's waves taking chunks in
+// turn.  Returns the element index in dst of element g0; *at advances past
+// the chunks.  (Reads at most 15 bytes before / past the run, inside its
+// first / last 16-byte block.)
+template <typename E, int NWV>
+__device__ __forceinline__ int dma_run(const E *src, size_t g0, uint32_t cnt, void *dst, uint32_t *at, int wv,
+                                       int lane) {
+    const char *p = (const char *)(src + g0);
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 15);
+    const int idx = (int)((*at + sh) / sizeof(E));
+    if (cnt == 0) return idx;
+    const uint32_t bytes = (sh + cnt * (uint32_t)sizeof(E) + 15) & ~15u;
+    const char *g = p - sh;
+    char *d = (char *)dst + *at;
+    for (uint32_t off = (uint32_t)wv * 1024u; off < bytes; off += NWV * 1024u)
+        if (off + 16u * (uint32_t)lane < bytes)
+            __builtin_amdgcn_global_load_lds((const void *)(g + off + 16 * lane),
+                                             (__attribute__((address_space(3))) void *)(d + off), 16, 0, 0);
+    *at += bytes;
+    return idx;
 }
 
 }  // namespace crdt

@@ -296,16 +296,16 @@ __device__ __forceinline__ void load_tile_ts(const crdt_refmerge_in &in, const T
     __syncthreads();
 }
 
-// sm[0] = L[a0-1] (when a0 > 0), sm[1..na] = L[a0..a1), sm[na+1..] = R[b0..b1).
+// SA[0..na) = L[a0..a1), SB[0..nb) = R[b0..b1) (LDS), lprev = L[a0-1] (when a0 > 0).
 // Thread-level merge of diagonals [k0, k1) of the tile: bit i of *isl / *emit
 // = item i is an L entry / is emitted.  Returns the split (ia) at k0.
-__device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na, uint32_t nb, uint32_t k0,
-                                                 uint32_t k1, bool has_prev0, int64_t maxl,
+__device__ __forceinline__ uint32_t thread_merge(const int64_t *SA, const int64_t *SB, int64_t lprev, uint32_t na,
+                                                 uint32_t nb, uint32_t k0, uint32_t k1, bool has_prev0, int64_t maxl,
                                                  uint32_t *isl, uint32_t *emit) {
     uint32_t lo = k0 > nb ? k0 - nb : 0, hi = k0 < na ? k0 : na;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (sm[1 + mid] <= sm[1 + na + (k0 - 1 - mid)]) lo = mid + 1;
+        if (SA[mid] <= SB[k0 - 1 - mid]) lo = mid + 1;
         else hi = mid;
     }
     uint32_t ia = lo, ib = k0 - lo;
@@ -313,8 +313,8 @@ __device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na,
     uint32_t fl = 0, fe = 0;
     // the two heads and the L entry before the L head stay in registers: one
     // LDS read (the new head) per step
-    int64_t ha = ia < na ? sm[1 + ia] : 0, hb = ib < nb ? sm[1 + na + ib] : 0;
-    int64_t pl = sm[ia];                                 // L entry just before (global a0+ia-1)
+    int64_t ha = ia < na ? SA[ia] : 0, hb = ib < nb ? SB[ib] : 0;
+    int64_t pl = ia ? SA[ia - 1] : lprev;                // L entry just before (global a0+ia-1)
     bool hp = ia > 0 || has_prev0;
     for (uint32_t k = k0, i = 0; k < k1; ++k, ++i) {
         const bool take_l = ia < na && (ib >= nb || ha <= hb);
@@ -324,11 +324,11 @@ __device__ __forceinline__ uint32_t thread_merge(const int64_t *sm, uint32_t na,
             pl = ha;
             hp = true;
             ++ia;
-            if (ia < na) ha = sm[1 + ia];
+            if (ia < na) ha = SA[ia];
         } else {
             if (hb < maxl && !(hp && pl == hb)) fe |= 1u << i;
             ++ib;
-            if (ib < nb) hb = sm[1 + na + ib];
+            if (ib < nb) hb = SB[ib];
         }
     }
     *isl = fl;
@@ -399,10 +399,10 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
-                                                 uint32_t *__restrict__ zero) {
+                                                 uint32_t *__restrict__ zero, int dma) {
     constexpr int NI = MT / NT, LPW = 64 / NI;           // items per thread, lanes per bitmap word
     static_assert(NI * LPW == 64, "a bitmap word is LPW lanes' items");
-    __shared__ int64_t sm[MT + 1];
+    __shared__ alignas(16) int64_t sm[MT + 8];           // (DMA: each run from its 16-byte aligned-down start)
     __shared__ uint32_t s_w[NT / 64];
     const uint64_t t = blockIdx.x;
     if (zero && t == 0 && threadIdx.x == 0) *zero = 0;   // (the delta fold's overflow flag)
@@ -414,11 +414,25 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
         if (threadIdx.x == 0) tcnt[t] = 0;              // the scan runs over the whole grid
         return;
     }
-    load_tile_ts<NT>(in, d, na, n, sm);
+    const int64_t *SA, *SB;
+    if (dma) {                                           // LDS-DMA staging (no VGPR round trip)
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+        uint32_t at = 0;
+        const int oa = dma_run<int64_t, NT / 64>(in.l_ts, d.l0, na, sm, &at, wv, ln);
+        const int ob = dma_run<int64_t, NT / 64>(in.r_ts, d.r0, nb, sm, &at, wv, ln);
+        SA = sm + oa;
+        SB = sm + ob;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
+        __syncthreads();
+    } else {
+        load_tile_ts<NT>(in, d, na, n, sm);
+        SA = sm + 1;
+        SB = sm + 1 + na;
+    }
     const uint32_t k0 = threadIdx.x * NI < n ? threadIdx.x * NI : n;
     const uint32_t k1 = k0 + NI < n ? k0 + NI : n;
     uint32_t isl = 0, emit = 0;
-    if (k0 < k1) (void)thread_merge(sm, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
+    if (k0 < k1) (void)thread_merge(SA, SB, d.lprev, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
     // LPW lanes' item bits -> one 64-bit word of each bitmap
     const int lane = threadIdx.x & 63, sh = (lane % LPW) * NI;
     uint64_t wl = (uint64_t)isl << sh, we = (uint64_t)emit << sh;
@@ -978,7 +992,9 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
                                                            (uint32_t)ns);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
     // (count-pass shapes at 4096-item tiles: 256 x 16 51 us, 512 x 8 45 us, 1024 x 4 67 us)
-    k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf);
+    // LDS-DMA staging of the ts runs when both logs are 8-byte aligned (refmerge.count_dma)
+    const int cdma = g_rm_count_dma && !((((uintptr_t)in.l_ts) | ((uintptr_t)in.r_ts)) & 7);
+    k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma);
     rc = check_launch(ctx);
     if (rc) return rc;
     // (a completion ticket letting the count pass's last block do this scan

@@ -937,31 +937,6 @@ __device__ __forceinline__ size_t first_copy(const uint64_t *sk, const uint64_t 
 constexpr int LWH = 2048;                // merge items per write workgroup
 constexpr int LWT = 512;                 // its threads (4 items each)
 
-// LDS-DMA staging of one side's run of one field: elements [g0, g0 + cnt) of
-// src into the byte array dst from byte *at (16-byte aligned), in 16-byte
-// chunks from src + g0's aligned-down address (global_load_lds_dwordx4: 1 KB
-// per wave instruction, no VGPRs), the workgroup's waves taking chunks in
-// turn.  Returns the element index in dst of element g0; *at advances past
-// the chunks.  (Reads at most 15 bytes before / past the run, inside its
-// first / last 16-byte block.)
-template <typename E, int NWV>
-__device__ __forceinline__ int dma_run(const E *src, size_t g0, uint32_t cnt, void *dst, uint32_t *at, int wv,
-                                       int lane) {
-    const char *p = (const char *)(src + g0);
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 15);
-    const int idx = (int)((*at + sh) / sizeof(E));
-    if (cnt == 0) return idx;
-    const uint32_t bytes = (sh + cnt * (uint32_t)sizeof(E) + 15) & ~15u;
-    const char *g = p - sh;
-    char *d = (char *)dst + *at;
-    for (uint32_t off = (uint32_t)wv * 1024u; off < bytes; off += NWV * 1024u)
-        if (off + 16u * (uint32_t)lane < bytes)
-            __builtin_amdgcn_global_load_lds((const void *)(g + off + 16 * lane),
-                                             (__attribute__((address_space(3))) void *)(d + off), 16, 0, 0);
-    *at += bytes;
-    return idx;
-}
-
 // The DMA staging indexes elements from a byte offset: fields naturally aligned.
 static inline bool dma_aligned(const crdt_tuples &t) {
     return !((((uintptr_t)t.key | (uintptr_t)t.ts) & 7) | ((uintptr_t)t.rep & 3));

@@ -237,3 +237,16 @@ def test_tile_parts_match_oracle(eng, parts):
         test_large_batch_matches_oracle(eng)
     finally:
         _lib.call("crdt_set_option", b"refmerge.tile_parts", 1)
+
+
+def test_count_pass_register_staging(eng):
+    """refmerge.count_dma=0: the count pass stages the tile's ts through
+    registers instead of LDS-DMA (also the path for logs that are not 8-byte
+    aligned); same outputs on the packed batch and the KATs."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"refmerge.count_dma", 0)
+    try:
+        test_packed_batch_matches_oracle(eng, 0)
+        test_all_kats_in_one_batch(eng)
+    finally:
+        _lib.call("crdt_set_option", b"refmerge.count_dma", 1)
