@@ -549,6 +549,48 @@ class ShardFold(Workload):
                           f"max-combined, {done // rows} reps in {dt:.1f}s"}
 
 
+class ShardSetMerge(SetMerge):
+    """configs[3] as a DISTRIBUTED population (north_star (3): "all-gather
+    and final merge for keyed sets"): every rank holds only its own sorted
+    10M + 10M tuples (A and B); a step = crdt_shard_{lww,orset}_merge_local
+    -- sampled splitters (one all-gather), every rank's tuples sent to their
+    key-range owner (all-to-all-v over xGMI), the owner's merge of the
+    received runs, then the all-gather-v of the merged state to every rank.
+    Units = input tuples of all ranks; per-GPU work fixed (weak scaling).  At
+    N=1 the library skips the exchange (one rank owns every key): the line is
+    the D1 merge's, through this entry point."""
+    kernel = "whole op: crdt_shard_*_merge_local (N=1: the D1 merge passes)"
+
+    def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
+        super().__init__(eng, rank, world, n, key_space, lww, seed)
+        self.name = "shard_set_merge" if lww else "shard_orset_merge"
+        self.world = world
+        self.comm = native_comm(eng, world)
+        if self.comm is None:
+            raise SystemExit("shard_set_merge needs the native RCCL communicator (CRDT_BENCH_BACKEND=nccl)")
+        self.cap = 2 * n * world
+        self.gout = E.TupleSet.empty(self.cap, eng.device)
+        self.step()
+        torch.cuda.synchronize()
+        self.n_total = len(self.last)
+        self.config = dict(self.config, workload=(
+            f"{'LWW-Element-Set' if lww else 'OR-Set'} merge of a distributed population: {n} tuples per side "
+            f"per GPU (sorted), key space {key_space}, key-range all-to-all + local merge + all-gather-v "
+            "(BASELINE configs[3] sharded, north_star (3))"),
+            n_out_total=self.n_total, parallelism=f"key-range shard x{world} (RCCL all-to-all-v + all-gather-v)")
+
+    io = None                                   # (outputs are whole-population: no PCIe staging line)
+
+    def step(self):
+        self.last = self.comm.set_merge_local([self.A], [self.B], lww=self.lww, gather=True, cap=self.cap,
+                                              outs=[self.gout])[0]
+
+    def extra(self, avg_ms):
+        return {"exchange": {"n_out_total": self.n_total, "ranks": self.world,
+                             "note": "N>1: each rank sends every tuple to its key-range owner and receives the "
+                                     "whole merged state; roofline.bytes_per_launch counts this rank's merge only"}}
+
+
 class ShardJoin(Workload):
     """configs[4] E2: every rank holds a DIVERGENT full copy of the
     [rows, nodes] counter state; the join is one in-place
@@ -977,6 +1019,8 @@ def make_workload(name, eng, rank, world, args):
         return ShardFold(eng, rank, world, args.total_rows, args.nodes)
     if name == "shard_join":
         return ShardJoin(eng, rank, world, args.rows, args.nodes)
+    if name in ("shard_set_merge", "shard_orset_merge"):
+        return ShardSetMerge(eng, rank, world, args.set_n, args.key_space, lww=(name == "shard_set_merge"))
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -1001,7 +1045,8 @@ def main():
     ap.add_argument("--workload", default="shard_fold",
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
                              "lww_merge_d2", "orset_merge_d2", "shard_fold", "shard_join", "refmerge",
-                             "refmerge_delta", "gossip_round", "gossip_round_wire", "server_merge"])
+                             "refmerge_delta", "gossip_round", "gossip_round_wire", "server_merge",
+                             "shard_set_merge", "shard_orset_merge"])
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)

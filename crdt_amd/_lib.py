@@ -155,8 +155,6 @@ SIGNATURES = {
     "crdt_tuples_sort": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples)]),
     "crdt_u64_lower_bound": (_I, [_CTX, _P, _SZ, _P, _SZ, _P]),
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),
-    "crdt_debug_set_stamps": (_I, [_CTX, _P, _SZ, C.POINTER(_SZ)]),
-    "crdt_debug_set_grid": (_I, [C.POINTER(_SZ), C.POINTER(C.c_int)]),
     "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
     "crdt_local_apply": (_I, [_CTX, C.POINTER(crdt_local_in), C.POINTER(crdt_local_out)]),
@@ -227,6 +225,12 @@ SIGNATURES = {
                                   C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ)]),
     "crdt_shard_orset_merge": (_I, [_P, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
                                     C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ)]),
+    "crdt_shard_alltoallv": (_I, [_P, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_P), C.POINTER(_SZ), _SZ]),
+    "crdt_shard_lww_merge_local": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples),
+                                        C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ), _I]),
+    "crdt_shard_orset_merge_local": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples),
+                                          C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ), _I]),
+    "crdt_shard_refmerge": (_I, [_P, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
     "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),
     "crdt_synth_set_tuples": (_I, [_CTX, _U64, C.c_uint32, C.POINTER(crdt_tuples), _SZ, _U64]),

@@ -2,7 +2,9 @@
 // entry points of the C-ABI (include/crdt_amd.h).
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
+#include <new>
 
 #include "common.hpp"
 
@@ -11,10 +13,10 @@ JoinTuning g_join;
 FoldTuning g_fold;
 int g_vclock_pairs_per_wave = 8;   // tools/tune_vclock.py at 10M x 128: 8 x 1 block/CU 6.50 TB/s
 int g_vclock_blocks_per_cu = 1;    //   against 6.19 TB/s for 4 x 8
-int g_sets_stamps = 0;
-int g_sets_grid_per_cu = 0;
-int g_sets_diag = 0;
-int g_sets_knobs = 1;
+int g_lww_chunk = 0;      // LWW tiles per chunk, 0 = one chunk (chunked schedules measured slower: DESIGN.md §5.4)
+int g_or_chunk = 0;       // OR-Set tiles per chunk (likewise)
+int g_set_streams = 1;
+int g_shard_exchange_always = 0;
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
@@ -22,6 +24,13 @@ int g_lww_parts = 4;     // LWW write pass: quarter tiles (half tiles 112 -> 105
 int g_rm_diag = 0;
 int g_scan_items = 8;
 std::atomic<int> g_fail_refmerge{0};
+std::atomic<int> g_fail_zero_bits{0};
+
+bool take_fail_zero_bits() {
+    for (int f = g_fail_zero_bits.load(); f > 0;)
+        if (g_fail_zero_bits.compare_exchange_weak(f, f - 1)) return true;
+    return false;
+}
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -42,6 +51,36 @@ int ws_reserve(crdt_ctx *ctx, size_t bytes) {
         return hip_fail(ctx, e);
     }
     ctx->ws_bytes = want;
+    return CRDT_OK;
+}
+
+int ctx_aux(crdt_ctx *ctx) {
+    if (ctx->aux) return CRDT_OK;
+    hipError_t e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        ctx->aux = nullptr;
+        return hip_fail(ctx, e);
+    }
+    return CRDT_OK;
+}
+
+int ctx_events(crdt_ctx *ctx, size_t n) {
+    if (n <= ctx->n_ev) return CRDT_OK;
+    const size_t want = std::max<size_t>(n, 2 * ctx->n_ev);
+    hipEvent_t *ev = new (std::nothrow) hipEvent_t[want];
+    if (!ev) return CRDT_E_NOMEM;
+    for (size_t i = 0; i < ctx->n_ev; ++i) ev[i] = ctx->ev[i];
+    for (size_t i = ctx->n_ev; i < want; ++i) {
+        hipError_t e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            for (size_t j = ctx->n_ev; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return hip_fail(ctx, e);
+        }
+    }
+    delete[] ctx->ev;                    // (events already handed to pending waits stay alive)
+    ctx->ev = ev;
+    ctx->n_ev = want;
     return CRDT_OK;
 }
 }  // namespace crdt
@@ -146,6 +185,12 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
     (void)crdt_strtab_destroy(ctx->keys);
     (void)crdt_strtab_destroy(ctx->vals);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->aux) {
+        (void)hipStreamSynchronize(ctx->aux);
+        (void)hipStreamDestroy(ctx->aux);
+    }
+    for (size_t i = 0; i < ctx->n_ev; ++i) (void)hipEventDestroy(ctx->ev[i]);
+    delete[] ctx->ev;
     delete ctx;
     return CRDT_OK;
 }
@@ -228,14 +273,18 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "vclock.blocks_per_cu")) {
         if (v < 1 || v > 64) return CRDT_E_INVAL;
         g_vclock_blocks_per_cu = (int)v;
-    } else if (!strcmp(name, "sets.grid_per_cu")) { // 0 = occupancy query (co-residency required)
-        if (v < 0 || v > 16) return CRDT_E_INVAL;
-        g_sets_grid_per_cu = (int)v;
-    } else if (!strcmp(name, "sets.knobs")) {        // bit 0: control-wave priority; bit 1: spinning data barrier;
-        if (v < 0 || v > 15) return CRDT_E_INVAL;    //   bit 2: the persistent tag-merge kernel (LWW, OR-Set);
-                                                     //   bit 3: register (not LDS-DMA) staging in the two-pass
-                                                     //   write passes and the LWW count pass
-        g_sets_knobs = (int)v;
+    } else if (!strcmp(name, "sets.lww_chunk")) {    // LWW tiles per count / write chunk (0: one chunk)
+        if (v < 0 || v > 16384) return CRDT_E_INVAL;
+        g_lww_chunk = (int)v;
+    } else if (!strcmp(name, "sets.or_chunk")) {     // OR-Set tiles per count / write chunk (0: one chunk)
+        if (v < 0 || v > 16384) return CRDT_E_INVAL;
+        g_or_chunk = (int)v;
+    } else if (!strcmp(name, "sets.streams")) {      // 1: one stream; 2: chunk c+1's count beside chunk c's write
+        if (v != 1 && v != 2) return CRDT_E_INVAL;
+        g_set_streams = (int)v;
+    } else if (!strcmp(name, "shard.exchange_always")) {   // tests: the keyed-set exchange protocol even on 1 rank
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_shard_exchange_always = (int)v;
     } else if (!strcmp(name, "sets.lww_parts")) {    // LWW write-pass workgroups per 4096-item tile
         if (v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
         g_lww_parts = (int)v;
@@ -248,9 +297,6 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "refmerge.tile_parts")) {   // RefMerge tile-pass workgroups per 4096-item tile
         if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
         g_rm_parts = (int)v;
-    } else if (!strcmp(name, "sets.diag_no_lookback")) {   // timing diagnostic, WRONG output: 1 no look-back, 2 loader only
-        if (v < 0 || v > 2) return CRDT_E_INVAL;
-        g_sets_diag = (int)v;
     } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 skip the replay fold; 2 no flush, 4 no table, 5 no Atoi gather
         if (v < 0 || v > 5) return CRDT_E_INVAL;
         g_rm_diag = (int)v;
@@ -260,9 +306,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "fail.refmerge")) {     // fault injection: the next v RefMerge calls fail (CRDT_E_NOMEM)
         if (v < 0 || v > 1000) return CRDT_E_INVAL;
         g_fail_refmerge = (int)v;
-    } else if (!strcmp(name, "sets.stamps")) {      // diagnostic: per-tile phase stamps
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_sets_stamps = (int)v;
+    } else if (!strcmp(name, "fail.zero_bits")) {    // fault injection: the next v two-pass merges zero their
+        if (v < 0 || v > 1000) return CRDT_E_INVAL;    //   merge bitmaps between the passes (CRDT_DEV_RANGE)
+        g_fail_zero_bits = (int)v;
     } else {
         return CRDT_E_INVAL;
     }

@@ -238,15 +238,21 @@ __global__ void k_dec_bodies(DecodeCtx c, const uint64_t *__restrict__ pre) {
     if (c.boff[d.q0 + d.np] - c.boff[d.q0] != d.nb) atomicOr(&c.flag[b], kBodyMalformed);
 }
 
-// r_kv = kv_base + pre; mark the first pair of each entry
-// (a malformed body's pair counts may run past n_p: its marks are dropped,
-// the body is flagged by k_dec_bodies)
-__global__ void k_dec_kv(const uint64_t *__restrict__ pre, uint64_t n_e, uint64_t n_p, uint64_t kv_base,
-                         uint64_t *__restrict__ r_kv, uint8_t *__restrict__ first) {
+// r_kv = kv_base + the body's first pair + pre rebased to the body's first
+// entry, so a body whose pair counts disagree with its header (flagged by
+// k_dec_bodies) cannot shift the ranges of the bodies after it; mark the
+// first pair of each entry within its own body's pair range.
+__global__ void k_dec_kv(DecodeCtx c, const uint64_t *__restrict__ pre, uint64_t n_e, uint64_t n_p,
+                         uint64_t kv_base, uint64_t *__restrict__ r_kv, uint8_t *__restrict__ first) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= n_e; e += (uint64_t)gridDim.x * 256) {
-        const uint64_t p = pre[e];
-        r_kv[e] = kv_base + p;
-        if (e < n_e && pre[e + 1] > p && p < n_p) first[p] = 1;
+        if (e == n_e) {
+            r_kv[e] = kv_base + n_p;
+            continue;
+        }
+        const BodyDesc d = c.bd[find_body(c.bd, c.nbody, e, false)];
+        const uint64_t p = pre[e] - pre[d.e0];
+        r_kv[e] = kv_base + d.q0 + p;
+        if (pre[e + 1] > pre[e] && p < d.np) first[d.q0 + p] = 1;
     }
 }
 
@@ -267,7 +273,8 @@ struct PendGet {                   // bytes of pending reference j (key or value
 // others record their entry (bit 31: this pair claimed it) for passes B / C
 // and count the claims (ctr[0] keys, ctr[1] values).  kEmptyE slots: done.
 __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
-                                                   const uint8_t *__restrict__ first, uint32_t key_cap,
+                                                   const uint8_t *__restrict__ first, const uint32_t *__restrict__ flag0,
+                                                   uint32_t key_cap,
                                                    uint64_t kv_base, uint32_t *__restrict__ kslot,
                                                    uint32_t *__restrict__ vslot, uint32_t *__restrict__ kv_key,
                                                    uint32_t *__restrict__ kv_val, unsigned long long *__restrict__ ctr) {
@@ -275,11 +282,19 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
     const BodyDesc d = c.bd[b];
     const uint8_t *region = c.data + d.data + 32 + 12 * d.ne + 8 * d.np;
     const uint64_t o0 = c.boff[d.q0];
+    // a body the earlier passes already rejected (flag0: the flags as they
+    // stood before this pass) claims no table entries: its strings never
+    // enter the persistent tables (the host decodes it)
+    const bool rejected = flag0[b] != 0;
     bool host = false, bad = false, full = false;
     uint32_t nk = 0, nv = 0;
     for (uint64_t q = (uint64_t)blockIdx.x * kChunk + threadIdx.x; q < d.np && q < (uint64_t)(blockIdx.x + 1) * kChunk;
          q += 256) {
         const uint64_t j = d.q0 + q;
+        if (rejected) {
+            kslot[j] = vslot[j] = kEmptyE32;
+            continue;
+        }
         const uint64_t o = c.boff[j] - o0, k = c.klen[j], v = c.boff[j + 1] - c.boff[j] - k;
         uint32_t ks = kEmptyE32, vs = kEmptyE32;
         if (o > d.nb || k > d.nb - o || v > d.nb - o - k) {
@@ -630,7 +645,7 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     if (!rc) rc = tab_reserve(ctx, vals, n_p, n_b);
     if (rc) return rc;
     // workspace
-    const size_t need = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 4) + Carve::round((n_e + 1) * 4) +
+    const size_t need = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 4) * 2 + Carve::round((n_e + 1) * 4) +
                         Carve::round((n_e + 1) * 8) + Carve::round(n_p * 4 + 4) * 4 + Carve::round((n_p + 1) * 8) * 5 +
                         Carve::round(n_p + 1) + scan_lb_tmp_bytes(std::max(n_p, n_e)) + Carve::round(64) + 4096;
     rc = ws_reserve(ctx, need);
@@ -638,6 +653,7 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     Carve w(ctx->ws);
     BodyDesc *d_bd = w.take<BodyDesc>(nb);
     uint32_t *d_flag = w.take<uint32_t>(nb);
+    uint32_t *d_flag0 = w.take<uint32_t>(nb);
     uint32_t *cnt = w.take<uint32_t>(n_e + 1);
     uint64_t *pre = w.take<uint64_t>(n_e + 1);
     uint32_t *klen = w.take<uint32_t>(n_p + 1);
@@ -684,15 +700,17 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     rc = scan_lb(ctx, CountSrc32{plen}, NoAct(), n_p, 0, boff, tmp);
     if (rc) return rc;
     k_dec_bodies<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(c, pre);
-    k_dec_kv<<<grid_for(n_e + 1, 256, cap), 256, 0, s>>>(pre, n_e, n_p, in->kv_base, out->r_kv, first);
+    k_dec_kv<<<grid_for(n_e + 1, 256, cap), 256, 0, s>>>(c, pre, n_e, n_p, in->kv_base, out->r_kv, first);
     rc = check_launch(ctx);
     if (rc) return rc;
     const uint64_t kn0 = keys->n, kb0 = keys->nbytes, vn0 = vals->n, vb0 = vals->nbytes;
     TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
     TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
-        k_dec_claim<<<gp, 256, 0, s>>>(c, kt, vt, first, in->key_cap, in->kv_base, kslot, vslot, out->kv_key,
-                                       out->kv_val, ctr);
+        e = hipMemcpyAsync(d_flag0, d_flag, nb * 4, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        k_dec_claim<<<gp, 256, 0, s>>>(c, kt, vt, first, d_flag0, in->key_cap, in->kv_base, kslot, vslot,
+                                       out->kv_key, out->kv_val, ctr);
         rc = check_launch(ctx);
         if (rc) return rc;
     }

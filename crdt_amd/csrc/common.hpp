@@ -25,6 +25,12 @@ struct crdt_ctx {
     void *srv_batch = nullptr;        // batched Server merge scratch (server.hip)
     void *pinned = nullptr;           // pinned host staging (pulled bodies on their way to HBM)
     size_t pinned_bytes = 0;
+    // A second (non-blocking) stream for pipelined passes, created on first
+    // use; every call that uses it joins it back into `stream` by an event
+    // before returning, so callers only ever order against `stream`.
+    hipStream_t aux = nullptr;
+    hipEvent_t *ev = nullptr;         // event pool of the pipelined passes (timing disabled)
+    size_t n_ev = 0;
 };
 
 namespace crdt {
@@ -51,16 +57,22 @@ struct FoldTuning {
 extern FoldTuning g_fold;
 extern int g_vclock_pairs_per_wave;
 extern int g_vclock_blocks_per_cu;
-extern int g_sets_grid_per_cu; // persistent set-merge workgroups per CU (0 = occupancy query)
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
-extern int g_sets_knobs;        // set merge experiments: bit 0 control waves at s_setprio 2, bit 1 spinning data barrier
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
 extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmerge.count_dma)
-extern int g_sets_diag;         // timing diagnostic: set merge skips the look-back (wrong output)
-extern int g_sets_stamps;
-extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests   // diagnostic only: per-tile phase stamps (crdt_debug_set_stamps)
+extern int g_lww_chunk;         // set merges: tiles per count / write chunk (sets.lww_chunk, sets.or_chunk;
+extern int g_or_chunk;          //   0 = one chunk), DESIGN.md §5.4
+extern int g_shard_exchange_always;   // keyed-set shard merges run the exchange protocol on 1 rank too (tests)
+extern int g_set_streams;       // set merges: 1 = one stream, 2 = counts beside writes (sets.streams)
+extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests
+extern std::atomic<int> g_fail_zero_bits;  // fault injection ("fail.zero_bits"): bitmaps zeroed between passes
+bool take_fail_zero_bits();                // consumes one "fail.zero_bits" count
+
+// The context's aux stream / an event pool of at least n events (capi.hip).
+int ctx_aux(crdt_ctx *ctx);
+int ctx_events(crdt_ctx *ctx, size_t n);
 
 void server_ctx_release(crdt_ctx *ctx);   // server.hip: the context's Server-merge scratch
 // gossip.hip: crdt_seg_gather2 (4-byte elements, base 0) over n_max segments

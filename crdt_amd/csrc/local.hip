@@ -35,6 +35,7 @@ namespace {
 
 constexpr int LB = 256;                 // threads per replica workgroup
 constexpr uint32_t kMaxCmd = 4096;      // commands per replica per call (LDS sort)
+constexpr uint32_t kSkip = 0xFFFFFFFFu; // kcnt sentinel: the replica exceeded a limit, nothing of it is applied
 
 struct alignas(16) LaOk {               // Go Atoi of one arena string
     int64_t val;
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(LB) void k_la_plan(crdt_local_in in, uint32_t *__re
         if (threadIdx.x == 0) {
             atomicOr(err, CRDT_DEV_RANGE);
             cnt[p] = 0;
-            kcnt[p] = 0;
+            kcnt[p] = kSkip;                             // k_la_write / k_la_state leave this replica alone
         }
         return;
     }
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(LB) void k_la_write(crdt_local_in in, const uint32_
     const uint64_t lb0 = in.l_off[p], nl = in.l_off[p + 1] - lb0;
     const uint64_t c0 = in.c_off[p];
     const uint32_t k = kcnt[p];
-    if (k > kMaxCmd) return;
+    if (k > kMaxCmd) return;                             // kSkip: an empty range, nothing may land in it
     const uint64_t ob = out.off[p];
     uint32_t base = 0;
     for (uint32_t i0 = 0; i0 < k; i0 += LB) {            // (k <= kMaxCmd)
@@ -237,9 +238,14 @@ __global__ __launch_bounds__(LB) void k_la_write(crdt_local_in in, const uint32_
 }
 
 // CurrentState apply (main.go:188-207), sequential per replica.
-__global__ void k_la_state(crdt_local_in in, const LaOk *__restrict__ okv, crdt_local_out out) {
+__global__ void k_la_state(crdt_local_in in, const LaOk *__restrict__ okv, const uint32_t *__restrict__ kcnt,
+                           crdt_local_out out) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= in.replicas) return;
+    if (kcnt[p] == kSkip) {                              // over the limit: the state is left as it was, so a
+        for (uint64_t j = in.c_off[p]; j < in.c_off[p + 1]; ++j) out.status[j] = 0;   // split retry applies once
+        return;
+    }
     for (uint64_t j = in.c_off[p]; j < in.c_off[p + 1]; ++j) {
         uint16_t status = 200;
         for (uint64_t q = in.c_kv[j]; q < in.c_kv[j + 1]; ++q) {
@@ -311,6 +317,6 @@ extern "C" int crdt_local_apply(crdt_ctx *ctx, const crdt_local_in *inp, const c
     rc = exclusive_scan_u32(ctx, cnt, out.off, np, tmp);     // out.off[np] = new Diff total
     if (rc) return rc;
     k_la_write<<<(unsigned)np, LB, 0, s>>>(in, k_lb, k_j, k_eq, kcnt, out);
-    if (nc) k_la_state<<<grid_for(np, 256, 1u << 30), 256, 0, s>>>(in, okv, out);
+    if (nc) k_la_state<<<grid_for(np, 256, 1u << 30), 256, 0, s>>>(in, okv, kcnt, out);
     return check_launch(ctx);
 }

@@ -490,7 +490,8 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
                                                 const OkVal *__restrict__ okv, SlotAcc acc, int diag,
                                                 const uint64_t *__restrict__ ic, crdt_refmerge_out out,
                                                 crdt_replay_state st, RpCand *__restrict__ cand,
-                                                uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf) {
+                                                uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf,
+                                                uint32_t *__restrict__ err) {
     // PARTS > 1: each workgroup takes 1/PARTS of the tile's items (words
     // WPP h .. WPP h + WPP - 1) with FB / PARTS threads and its own slot table
     constexpr int WT = FB / PARTS, NWV = WT / 64, WPP = NW / PARTS;   // threads, waves, words per workgroup
@@ -539,6 +540,20 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
     }
     pre_l -= (uint32_t)__popcll(word_l);
     pre_e -= (uint32_t)__popcll(word_e);
+    // every L / R index and output rank below derives from the bitmaps: a
+    // tile whose bitmaps set a bit past its n items or do not hold exactly
+    // its na L entries raises CRDT_DEV_RANGE instead of reading out of range
+    {
+        const uint32_t lo = 64u * (uint32_t)lane;
+        const uint64_t valid = lo >= n ? 0ull : (n - lo >= 64u ? ~0ull : (1ull << (n - lo)) - 1);
+        const bool bad = ((word_l | word_e) & ~valid) != 0;
+        const uint32_t tot_l = (uint32_t)__shfl((int)(pre_l + (uint32_t)__popcll(word_l)), 63);
+        if (__any(bad) || tot_l != na) {
+            if (threadIdx.x == 0 && part == 0) atomicOr(err, CRDT_DEV_RANGE);
+            if (DELTA && threadIdx.x == 0) cand_n[t] = 0;
+            return;
+        }
+    }
     const uint64_t ob = d.l0 + ict;
     if (DELTA && threadIdx.x == 0) s_nc = s_ovf = 0;
     if (FOLDS)
@@ -624,6 +639,10 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
         const uint64_t gi = it_gi(f);
         if (em) {
             const uint64_t o = ob + it_rk(f);
+            if (o >= in.n_l + in.n_r) {                  // (consistent bitmaps never get here)
+                atomicOr(err, CRDT_DEV_RANGE);
+                continue;
+            }
             out.ts[o] = e_ts[f];                         // (nontemporal stores: no change, 153 us)
             out.src[o] = il ? (int64_t)gi : -(int64_t)gi - 1;
             out.origin[o] = e_org[f];
@@ -1007,11 +1026,15 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
     }
+    if (take_fail_zero_bits()) {                                  // failpoint: the tile pass must flag, not fault
+        hipError_t e = hipMemsetAsync(bits, 0, tmax * 2 * NW * 8, s);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
     // the tile pass: slice write and (with slots) the replay fold
     const unsigned tg = (unsigned)tmax;
     if (delta && ns) {                                            // incremental replay: fold only the inserted R
         k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, 0, ic, out, *delta, cand, cand_n,
-                                                   ovf);
+                                                   ovf, ctx->dev_status);
         rc = check_launch(ctx);
         if (rc) return rc;
         k_rp_holder<<<tg, 64, 0, s>>>(in, r_dk, *delta, cand, cand_n, ovf, tmax);   // the candidates' holders
@@ -1022,7 +1045,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
 #define RM_TILE(F, P, DIAG)                                                                                   \
     k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out, crdt_replay_state{}, \
-                                              nullptr, nullptr, nullptr)
+                                              nullptr, nullptr, nullptr, ctx->dev_status)
     if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
         if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, 0);
         else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, 0);

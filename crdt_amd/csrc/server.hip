@@ -168,6 +168,25 @@ struct Batch {
 template <class T> static size_t vbytes(const std::vector<T> &v) { return v.size() * sizeof(T); }
 
 // merge() for a set of servers whose locks the caller holds.
+// Device failure flags raised by the passes of one merge: before the passes
+// the status word moves to word 1 and word 0 starts clear (stream-ordered, no
+// host wait); at the merge's host synchronisation word 0 holds exactly this
+// merge's flags, and the earlier ones are put back beside them, so flags
+// raised by earlier calls stay for crdt_ctx_device_status.
+static int status_mark(crdt_ctx *ctx) {
+    hipError_t e = hipMemcpyAsync(ctx->dev_status + 1, ctx->dev_status, 4, hipMemcpyDeviceToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->dev_status, 0, 4, ctx->stream);
+    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+}
+static hipError_t status_fetch(crdt_ctx *ctx, uint32_t *two) {
+    return hipMemcpyAsync(two, ctx->dev_status, 8, hipMemcpyDeviceToHost, ctx->stream);
+}
+// (after the synchronisation) true when this merge raised a flag
+static bool status_raised(crdt_ctx *ctx, const uint32_t *two) {
+    if (two[1]) (void)hipMemsetD32Async((hipDeviceptr_t)ctx->dev_status, (int)(two[0] | two[1]), 1, ctx->stream);
+    return two[0] != 0;
+}
+
 static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
     Batch b;
     for (size_t i = 0; i < n; ++i) b.add(*srv[i]);
@@ -227,7 +246,8 @@ static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
     ro.st_kind = (uint8_t *)(d + o_kind);
     ro.st_str = (uint32_t *)(d + o_str);
     ro.st_sum = (int64_t *)(d + o_sum);
-    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    rc = status_mark(ctx);
+    if (!rc) rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
 
     std::vector<uint64_t> h_off(n + 1);
@@ -244,8 +264,11 @@ static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
             hipError_t e = hipMemcpyAsync(x.dst, d + x.src, x.bytes, hipMemcpyDeviceToHost, ctx->stream);
             if (e != hipSuccess) return hip_fail(ctx, e);
         }
-    hipError_t e = hipStreamSynchronize(ctx->stream);
+    uint32_t fl[2] = {0, 0};
+    hipError_t e = status_fetch(ctx, fl);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
+    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;           // nothing below ran: the servers are untouched
 
     for (size_t p = 0; p < n; ++p) {
         Server &s = *srv[p];
@@ -286,6 +309,7 @@ static std::shared_ptr<const Value> make_value(bool local, const char *const *ke
 // The binary SoA body of a treemap (crdt_server_gossip_binary's format):
 // entries ascending, pairs of an entry sorted by key, nil maps as 0xFFFFFFFF.
 constexpr uint32_t kNilPairsH = 0xFFFFFFFFu;
+constexpr size_t kLocalMaxCmd = 4096;         // crdt_local_apply: commands per replica per call
 
 static void put_u32(std::string &o, uint32_t v) { o.append((const char *)&v, 4); }
 static void put_u64(std::string &o, uint64_t v) { o.append((const char *)&v, 8); }
@@ -487,12 +511,9 @@ static void absorb_pending(Server &s) {
     parse_soa_into(s, s.pend_body, s.pend_len);
 }
 
-// Apply the queued local writes to dd (crdt_local_apply, Diff only: the
-// CurrentState apply already ran on the host when each write arrived).
-static int dev_flush_cmds(crdt_ctx *ctx, Server &s) {
-    if (s.pend_cmds.empty()) return CRDT_OK;
-    std::map<int64_t, std::shared_ptr<const Value>> cm;   // Put replaces: the last same-ms write stays
-    for (auto &c : s.pend_cmds) cm[c.first] = c.second;
+// Apply one chunk of the queued local writes (distinct ts, at most
+// kLocalMaxCmd: crdt_local_apply's per-replica limit) to dd.
+static int dev_flush_chunk(crdt_ctx *ctx, Server &s, const std::map<int64_t, std::shared_ptr<const Value>> &cm) {
     std::string body;
     encode_soa(cm, body);
     const uint64_t nc = cm.size(), np = body_u64(body, 16);
@@ -528,12 +549,16 @@ static int dev_flush_cmds(crdt_ctx *ctx, Server &s) {
                      s.c_key.as<uint32_t>(), s.c_val.as<uint32_t>(), sb, so};
     crdt_local_out lo{s.o_off.as<uint64_t>(), s.dd2.ts.as<int64_t>(), s.dd2.origin.as<uint8_t>(),
                       s.o_src.as<int64_t>(), s.c_status.as<uint16_t>(), nullptr, nullptr, nullptr};
-    rc = crdt_local_apply(ctx, &li, &lo);
+    rc = status_mark(ctx);
+    if (!rc) rc = crdt_local_apply(ctx, &li, &lo);
     if (rc) return rc;
     uint64_t oo[2] = {0, 0};
+    uint32_t fl[2] = {0, 0};
     e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = status_fetch(ctx, fl);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
+    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;       // dd untouched (the swap below never ran)
     const uint64_t n_out = oo[1];
     rc = crdt_seg_gather2(ctx, n_out, s.o_src.as<int64_t>(), s.dd.kv_off.as<uint64_t>(), s.c_kv.as<uint64_t>(), 0,
                           s.dd2.kv_off.as<uint64_t>(), 4, s.dd.kv_key.p, s.c_key.p, s.dd2.kv_key.p, s.dd.kv_val.p,
@@ -546,6 +571,25 @@ static int dev_flush_cmds(crdt_ctx *ctx, Server &s) {
     std::swap(s.dd, s.dd2);
     s.dd.n = n_out;
     s.dd.n_kv = nkv;
+    return CRDT_OK;
+}
+
+// Apply the queued local writes to dd (crdt_local_apply, Diff only: the
+// CurrentState apply already ran on the host when each write arrived), in
+// chunks of at most kLocalMaxCmd distinct timestamps.  A chunk that fails
+// leaves dd as the previous chunks made it and pend_cmds whole: re-applying
+// an applied chunk is a no-op (Put of the same value at the same ts).
+static int dev_flush_cmds(crdt_ctx *ctx, Server &s) {
+    if (s.pend_cmds.empty()) return CRDT_OK;
+    std::map<int64_t, std::shared_ptr<const Value>> all;  // Put replaces: the last same-ms write stays
+    for (auto &c : s.pend_cmds) all[c.first] = c.second;
+    auto it = all.begin();
+    while (it != all.end()) {
+        std::map<int64_t, std::shared_ptr<const Value>> cm;
+        for (size_t k = 0; k < kLocalMaxCmd && it != all.end(); ++k, ++it) cm.emplace_hint(cm.end(), *it);
+        const int rc = dev_flush_chunk(ctx, s, cm);
+        if (rc) return rc;
+    }
     s.pend_cmds.clear();
     return CRDT_OK;
 }
@@ -622,7 +666,8 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     crdt_refmerge_out ro{s.o_off.as<uint64_t>(), s.dd2.ts.as<int64_t>(), s.dd2.origin.as<uint8_t>(),
                          s.o_src.as<int64_t>(), s.st_kind.as<uint8_t>(), s.st_str.as<uint32_t>(),
                          s.st_sum.as<int64_t>()};
-    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    rc = status_mark(ctx);
+    if (!rc) rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
     // the new Diff's kv pairs behind the merge, its entry count still on the
     // device (dd2 is sized for |L| + |R|): one host synchronisation per merge
@@ -643,8 +688,11 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     if (e == hipSuccess && nks) e = hipMemcpyAsync(kind.data(), s.st_kind.p, nks, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(sstr.data(), s.st_str.p, nks * 4, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(ssum.data(), s.st_sum.p, nks * 8, hipMemcpyDeviceToHost, ctx->stream);
+    uint32_t fl[2] = {0, 0};
+    if (e == hipSuccess) e = status_fetch(ctx, fl);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
+    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;       // dd / RemoteDiff untouched (the swap below never ran)
     std::map<std::string, std::string> state;
     for (uint64_t k = 0; k < nks; ++k) {
         if (kind[k] == 1) state.emplace(tab_str(ctx->keys, k), tab_str(ctx->vals, sstr[k]));
@@ -914,7 +962,8 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
         maxs = std::max<uint64_t>(maxs, std::max(nu + 1, qu));
     }
     if (rc) return rc;
-    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    rc = status_mark(ctx);
+    if (!rc) rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
     pc.mark("refmerge_launch");
     // the new Diff's kv pairs (the entry count stays on the device), each
@@ -945,8 +994,11 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     if (e == hipSuccess) e = hipMemcpyAsync(kind.data(), bb.st_kind.p, nslots, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(sstr.data(), bb.st_str.p, nslots * 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ssum.data(), bb.st_sum.p, nslots * 8, hipMemcpyDeviceToHost, st);
+    uint32_t fl[2] = {0, 0};
+    if (e == hipSuccess) e = status_fetch(ctx, fl);
     if (e == hipSuccess) e = hipStreamSynchronize(st);   // (also settles sp / sq, host vectors)
     if (e != hipSuccess) return hip_fail(ctx, e);
+    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;       // no server swapped in anything
     pc.mark("gather+split+state_d2h");
     uint64_t nks = 0;
     (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);

@@ -14,7 +14,15 @@
 //     and an all-gather-v (counts by ncclAllGather, then one grouped
 //     ncclBroadcast per root and field) concatenates the outputs in rank order,
 //     which is already the globally sorted merged state (a key's LWW / OR-Set
-//     output depends only on that key's tuples).
+//     output depends only on that key's tuples);
+//   * keyed sets of a DISTRIBUTED population (every rank holds only its own
+//     tuples, crdt_shard_*_merge_local): sampled splitters (one ncclAllGather),
+//     each rank's tuples sent to their key-range owner (grouped ncclSend /
+//     ncclRecv, an all-to-all-v), the owner's merge of the received runs,
+//     then the all-gather-v above;
+//   * RefMerge of one batch whose logs are split by ts range over the ranks
+//     (crdt_shard_refmerge): all-reduce(max) of max(L), the local merge, then
+//     integer all-reduces of the replay accumulators (main.go:35-100).
 // A communicator has one or more LOCAL members (device + crdt_ctx + ncclComm):
 // crdt_shard_comm_create drives every listed GPU from one process
 // (ncclCommInitAll, grouped calls); crdt_shard_comm_init_rank makes one member
@@ -467,4 +475,490 @@ extern "C" int crdt_shard_lww_merge(crdt_comm *c, const crdt_tuples *a, size_t n
 extern "C" int crdt_shard_orset_merge(crdt_comm *c, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
                                       const crdt_tuples *out, size_t cap, size_t *n_out) {
     return shard_set_merge(c, false, a, na, b, nb, out, cap, n_out);
+}
+
+// ---------------------------------------------------------------- RefMerge by ts range (§8(e))
+// (*Server).merge() (main.go:35-100) of one batch of replicas whose Diff /
+// RemoteDiff logs are split by ts range over the ranks (global rank g holds
+// the g-th range of every replica, ranks in ascending ts order).  The four
+// steps of crdt_amd/shard.py's sharded_refmerge, on the library's own RCCL
+// communicator and member streams, no host synchronisation:
+//   1. crdt_refmerge_local_maxl, ncclAllReduce(ncclInt64, ncclMax): the GLOBAL
+//      max(L) of every replica (remote ts at or above it are dropped, main.go:49);
+//   2. crdt_refmerge_batch_ex with that max: the member's slice of the new
+//      Diff (slices concatenate in rank order) and its unreduced accumulators;
+//   3. the key's max-ts holder across ranks: ncclMax of shard << 40 | rank
+//      (crdt_refmerge_acc_rank), ncclSum of the owner's string id, ncclSum of
+//      the wrapped sums (int64 two's complement: main.go:95) and of the
+//      parsable counts;
+//   4. crdt_refmerge_finalize: CurrentState, identical on every member.
+// Integer reductions only: bit-exact with crdt_refmerge_batch of the
+// unsharded batch for any rank count.
+extern "C" int crdt_shard_refmerge(crdt_comm *c, const crdt_refmerge_in *in, const crdt_refmerge_out *out) {
+    if (!valid(c) || !in || !out) return CRDT_E_INVAL;
+    const size_t M = c->m.size();
+    const uint32_t P = in[0].replicas, ns = in[0].n_slots;
+    for (size_t i = 0; i < M; ++i)
+        if (in[i].replicas != P || in[i].n_slots != ns) return CRDT_E_INVAL;   // one batch, one slot space
+    if (P == 0) return CRDT_OK;
+    if ((size_t)c->rank0 + M > (1u << 23)) return CRDT_E_RANGE;            // shard << 40 | rank packing
+    struct Bufs {
+        int64_t *maxl, *c, *cmax, *v;
+        crdt_refmerge_acc acc;
+    };
+    std::vector<Bufs> bf(M);
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        const size_t need = Carve::round(P * 8) + Carve::round(ns * 8 + 8) * 5 + Carve::round(ns * 4 + 4) + 1024;
+        int rc = scratch_reserve(mb, need);
+        if (rc) return rc;
+        Carve w(mb.scratch);
+        bf[i].maxl = w.take<int64_t>(P);
+        bf[i].acc.best = w.take<uint64_t>(ns + 1);
+        bf[i].acc.sum = w.take<int64_t>(ns + 1);
+        bf[i].acc.npar = w.take<uint32_t>(ns + 1);
+        bf[i].c = w.take<int64_t>(ns + 1);
+        bf[i].cmax = w.take<int64_t>(ns + 1);
+        bf[i].v = w.take<int64_t>(ns + 1);
+    }
+    auto each = [&](auto fn) -> int {
+        for (size_t i = 0; i < M; ++i) {
+            int rc = bind(c->m[i].ctx);
+            if (!rc) rc = fn(i, c->m[i].ctx);
+            if (rc) return rc;
+        }
+        return CRDT_OK;
+    };
+    auto allreduce = [&](auto ptr_of, size_t n, ncclDataType_t t, ncclRedOp_t op) -> int {
+        ncclResult_t r = ncclGroupStart();
+        for (size_t i = 0; i < M && r == ncclSuccess; ++i)
+            r = ncclAllReduce(ptr_of(i), ptr_of(i), n, t, op, c->m[i].nccl, c->m[i].ctx->stream);
+        ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return nccl_fail(c, r);
+        if (r2 != ncclSuccess) return nccl_fail(c, r2);
+        return CRDT_OK;
+    };
+    // 1. the global max(L) per replica
+    int rc = each([&](size_t i, crdt_ctx *x) { return crdt_refmerge_local_maxl(x, &in[i], bf[i].maxl); });
+    if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].maxl; }, P, ncclInt64, ncclMax);
+    // 2. the local merges (new-Diff slices, unreduced accumulators)
+    if (!rc) rc = each([&](size_t i, crdt_ctx *x) {
+        return crdt_refmerge_batch_ex(x, &in[i], &out[i], bf[i].maxl, &bf[i].acc);
+    });
+    if (rc) return rc;
+    if (ns == 0) return CRDT_OK;
+    // 3. the accumulators reduced across ranks
+    if (c->nranks > 1) {
+        rc = each([&](size_t i, crdt_ctx *x) {
+            int r = crdt_refmerge_acc_rank(x, &bf[i].acc, ns, (uint32_t)(c->rank0 + i), bf[i].c);
+            if (r) return r;
+            hipError_t e = hipMemcpyAsync(bf[i].cmax, bf[i].c, ns * 8, hipMemcpyDeviceToDevice, x->stream);
+            return e == hipSuccess ? CRDT_OK : hip_fail(x, e);
+        });
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].cmax; }, ns, ncclInt64, ncclMax);
+        if (!rc) rc = each([&](size_t i, crdt_ctx *x) {
+            return crdt_refmerge_acc_owner_str(x, &bf[i].acc, ns, bf[i].c, bf[i].cmax, bf[i].v);
+        });
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].v; }, ns, ncclInt64, ncclSum);
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].acc.sum; }, ns, ncclInt64, ncclSum);
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].acc.npar; }, ns, ncclUint32, ncclSum);
+        if (!rc) rc = each([&](size_t i, crdt_ctx *x) {
+            return crdt_refmerge_acc_set_best(x, &bf[i].acc, ns, bf[i].cmax, bf[i].v);
+        });
+        if (rc) return rc;
+    }
+    // 4. CurrentState on every member
+    return each([&](size_t i, crdt_ctx *x) {
+        return crdt_refmerge_finalize(x, &bf[i].acc, ns, in[i].str_bytes, in[i].str_off, in[i].n_str, &out[i]);
+    });
+}
+
+// ---------------------------------------------------------------- all-to-all-v
+// Member i sends send_counts[i * R + q] elements of elem_size bytes to global
+// rank q, from its send buffer's segments in rank order, and receives
+// recv_counts[i * R + p] elements from rank p into its recv buffer, segments
+// in rank order (grouped ncclSend / ncclRecv, enqueued on the member streams).
+extern "C" int crdt_shard_alltoallv(crdt_comm *c, const void *const *send, const size_t *send_counts,
+                                    void *const *recv, const size_t *recv_counts, size_t elem_size) {
+    if (!valid(c) || !send || !send_counts || !recv || !recv_counts || elem_size == 0) return CRDT_E_INVAL;
+    const size_t M = c->m.size(), R = (size_t)c->nranks;
+    for (size_t i = 0; i < M; ++i) {
+        size_t ns = 0, nr = 0;
+        for (size_t q = 0; q < R; ++q) ns += send_counts[i * R + q], nr += recv_counts[i * R + q];
+        if ((ns && !send[i]) || (nr && !recv[i])) return CRDT_E_INVAL;
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
+        const char *sb = (const char *)send[i];
+        char *rb = (char *)recv[i];
+        size_t so = 0, ro = 0;
+        for (size_t q = 0; q < R && r == ncclSuccess; ++q) {
+            const size_t sn = send_counts[i * R + q] * elem_size, rn = recv_counts[i * R + q] * elem_size;
+            if (sn) r = ncclSend(sb + so, sn, ncclUint8, (int)q, c->m[i].nccl, c->m[i].ctx->stream);
+            if (r == ncclSuccess && rn) r = ncclRecv(rb + ro, rn, ncclUint8, (int)q, c->m[i].nccl, c->m[i].ctx->stream);
+            so += sn;
+            ro += rn;
+        }
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail(c, r);
+    if (r2 != ncclSuccess) return nccl_fail(c, r2);
+    return CRDT_OK;
+}
+
+namespace {
+
+// Splitters of a distributed key population from per-rank samples: block p
+// of the gathered samples = [n_a, n_b, S keys of A, S keys of B] (a side
+// with n > 0 sampled at i * n / S, each sample weighing n; an empty side's
+// samples weigh 0).  Inner splitter q = the first sample key (in key order)
+// at which the cumulative weight reaches q / R of the total.  Rank r owns
+// keys [spl[r], spl[r+1]); crdt_amd/shard.py weighted_splitters is the same rule.
+std::vector<uint64_t> weighted_splitters(const uint64_t *blocks, size_t R, size_t S) {
+    std::vector<std::pair<uint64_t, uint64_t>> e;       // (key, weight)
+    e.reserve(2 * S * R);
+    for (size_t p = 0; p < R; ++p) {
+        const uint64_t *b = blocks + p * (2 + 2 * S);
+        for (int side = 0; side < 2; ++side)
+            if (b[side])
+                for (size_t i = 0; i < S; ++i) e.emplace_back(b[2 + side * S + i], b[side]);
+    }
+    std::sort(e.begin(), e.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    unsigned __int128 W = 0;
+    for (auto &x : e) W += x.second;
+    std::vector<uint64_t> spl(R + 1, 0);
+    spl[R] = kKeyEnd;
+    unsigned __int128 cum = 0;
+    size_t k = 0;
+    for (size_t q = 1; q < R; ++q) {
+        const unsigned __int128 target = (unsigned __int128)q * W;
+        while (k < e.size() && (cum + e[k].second) * R < target) cum += e[k++].second;
+        spl[q] = W == 0 ? 0 : (k < e.size() ? e[k].first : e.back().first);
+    }
+    return spl;
+}
+
+__global__ void k_sample_block(const uint64_t *__restrict__ ka, size_t na, const uint64_t *__restrict__ kb, size_t nb,
+                               unsigned S, uint64_t *__restrict__ blk) {
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        blk[0] = na;
+        blk[1] = nb;
+    }
+    if (i < S) {
+        blk[2 + i] = na ? ka[(size_t)((unsigned __int128)i * na / S)] : 0;
+        blk[2 + S + i] = nb ? kb[(size_t)((unsigned __int128)i * nb / S)] : 0;
+    }
+}
+
+struct Run {
+    int arena;           // 0 / 1
+    size_t off, n;
+};
+
+int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
+                          const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out, int gather) {
+    if (!valid(c) || !a || !na || !b || !nb || !out || !n_out) return CRDT_E_INVAL;
+    const size_t M = c->m.size(), R = (size_t)c->nranks, S = kSamplesPerSide;
+    for (size_t i = 0; i < M; ++i)
+        if ((na[i] && !a[i].key) || (nb[i] && !b[i].key)) return CRDT_E_INVAL;
+    if (R == 1 && !g_shard_exchange_always && cap >= na[0] + nb[0]) {   // one rank owns every key: no exchange
+        auto &mb = c->m[0];
+        int rc = scratch_reserve(mb, 64);
+        if (rc) return rc;
+        uint64_t *count = (uint64_t *)mb.scratch;
+        rc = lww ? crdt_lww_merge(mb.ctx, &a[0], na[0], &b[0], nb[0], const_cast<crdt_tuples *>(&out[0]), count)
+                 : crdt_orset_merge(mb.ctx, &a[0], na[0], &b[0], nb[0], const_cast<crdt_tuples *>(&out[0]), count);
+        if (rc) return rc;
+        uint64_t h = 0;
+        hipError_t e = hipMemcpyAsync(&h, count, 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        n_out[0] = h;
+        return check_devices(c);
+    }
+    // scratch layout: [ctrl: samples R x (2 + 2S) | counts 2R x R | bounds] then two tuple arenas
+    const size_t blk = 2 + 2 * S;
+    const size_t ctrl = Carve::round((R + 2) * 8) + Carve::round(R * blk * 8) + Carve::round(2 * R * R * 8) +
+                        Carve::round(4 * (R + 1) * 8) + Carve::round(4 * R * 8 + 8) + 4096;
+    for (size_t i = 0; i < M; ++i) {
+        int rc = scratch_reserve(c->m[i], ctrl);
+        if (rc) return rc;
+    }
+    auto carve_ctrl = [&](crdt_comm::Member &mb, uint64_t **smp, uint64_t **cnt, uint64_t **bnd, uint64_t **mc) {
+        Carve w(mb.scratch);
+        (void)w.take<uint64_t>(R + 2);                   // (crdt_shard_set_allgather_v's counts)
+        *smp = w.take<uint64_t>(R * blk);
+        *cnt = w.take<uint64_t>(2 * R * R);
+        *bnd = w.take<uint64_t>(4 * (R + 1));
+        *mc = w.take<uint64_t>(4 * R + 1);
+        return w.used;
+    };
+    // 1. samples + sizes, all-gathered; every rank derives the same splitters
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        int rc = bind(mb.ctx);
+        if (rc) return rc;
+        k_sample_block<<<(unsigned)((S + 255) / 256), 256, 0, mb.ctx->stream>>>(a[i].key, na[i], b[i].key, nb[i],
+                                                                               (unsigned)S, smp + (c->rank0 + i) * blk);
+        rc = check_launch(mb.ctx);
+        if (rc) return rc;
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
+        auto &mb = c->m[i];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        uint64_t *mine = smp + (c->rank0 + i) * blk;
+        r = ncclAllGather(mine, smp, blk, ncclUint64, mb.nccl, mb.ctx->stream);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail(c, r);
+    if (r2 != ncclSuccess) return nccl_fail(c, r2);
+    std::vector<uint64_t> h_smp(R * blk);
+    {
+        auto &mb = c->m[0];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        int rc = bind(mb.ctx);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(h_smp.data(), smp, R * blk * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+    }
+    const std::vector<uint64_t> spl = weighted_splitters(h_smp.data(), R, S);
+    // 2. each member's send ranges: lower_bound of the inner splitters in its keys
+    std::vector<size_t> sa(M * R), sb(M * R), ra(M * R), rb(M * R);
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        int rc = bind(mb.ctx);
+        if (rc) return rc;
+        std::vector<uint64_t> hb(2 * (R + 1), 0);
+        if (R > 1) {
+            hipError_t e = hipMemcpyAsync(bnd, spl.data() + 1, (R - 1) * 8, hipMemcpyHostToDevice, mb.ctx->stream);
+            if (e != hipSuccess) return hip_fail(mb.ctx, e);
+            if (na[i]) rc = crdt_u64_lower_bound(mb.ctx, a[i].key, na[i], bnd, R - 1, bnd + R);
+            if (!rc && nb[i]) rc = crdt_u64_lower_bound(mb.ctx, b[i].key, nb[i], bnd, R - 1, bnd + 2 * R);
+            if (rc) return rc;
+            e = hipMemcpyAsync(hb.data(), bnd + R, 2 * R * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+            if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        }
+        // cuts of A: 0, lb(spl[1]) .. lb(spl[R-1]), na (lower_bound of 0 is 0, of the end na)
+        std::vector<uint64_t> cutA(R + 1), cutB(R + 1);
+        cutA[0] = cutB[0] = 0;
+        for (size_t q = 1; q < R; ++q) cutA[q] = na[i] ? hb[q - 1] : 0, cutB[q] = nb[i] ? hb[R + q - 1] : 0;
+        cutA[R] = na[i];
+        cutB[R] = nb[i];
+        for (size_t q = 0; q < R; ++q) {
+            sa[i * R + q] = cutA[q + 1] - cutA[q];
+            sb[i * R + q] = cutB[q + 1] - cutB[q];
+        }
+    }
+    // 3. the count matrix, all-gathered: block p = rank p's [send A counts | send B counts]
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        int rc = bind(mb.ctx);
+        if (rc) return rc;
+        std::vector<uint64_t> h(2 * R);
+        for (size_t q = 0; q < R; ++q) h[q] = sa[i * R + q], h[R + q] = sb[i * R + q];
+        hipError_t e = hipMemcpyAsync(cnt + (c->rank0 + i) * 2 * R, h.data(), 2 * R * 8, hipMemcpyHostToDevice,
+                                      mb.ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);     // h is a local
+        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+    }
+    r = ncclGroupStart();
+    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
+        auto &mb = c->m[i];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        uint64_t *mine = cnt + (c->rank0 + i) * 2 * R;
+        r = ncclAllGather(mine, cnt, 2 * R, ncclUint64, mb.nccl, mb.ctx->stream);
+    }
+    r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return nccl_fail(c, r);
+    if (r2 != ncclSuccess) return nccl_fail(c, r2);
+    std::vector<size_t> tot_a(M, 0), tot_b(M, 0);
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        int rc = bind(mb.ctx);
+        if (rc) return rc;
+        std::vector<uint64_t> h(2 * R * R);
+        hipError_t e = hipMemcpyAsync(h.data(), cnt, 2 * R * R * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        const size_t g = (size_t)c->rank0 + i;
+        for (size_t p = 0; p < R; ++p) {
+            ra[i * R + p] = h[p * 2 * R + g];
+            rb[i * R + p] = h[p * 2 * R + R + g];
+            tot_a[i] += ra[i * R + p];
+            tot_b[i] += rb[i * R + p];
+        }
+    }
+    // 4. the exchange into arena 0 (A's runs, then B's, in rank order), field by field
+    std::vector<crdt_tuples> ar0(M), ar1(M);
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        const size_t n = tot_a[i] + tot_b[i] + 1;
+        const size_t need = ctrl + 2 * (Carve::round(n * 8) * 2 + Carve::round(n * 4) + Carve::round(n)) + 4096;
+        int rc = scratch_reserve(mb, need);
+        if (rc) return rc;
+        uint64_t *smp, *cnt, *bnd, *mc;
+        Carve w(mb.scratch);
+        w.used = carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        for (crdt_tuples *t : {&ar0[i], &ar1[i]}) {
+            t->key = w.take<uint64_t>(n);
+            t->ts = w.take<uint64_t>(n);
+            t->rep = w.take<uint32_t>(n);
+            t->tomb = w.take<uint8_t>(n);
+        }
+    }
+    {
+        std::vector<const void *> snd(M);
+        std::vector<void *> rcv(M);
+        const size_t esz[4] = {8, 8, 4, 1};
+        for (int side = 0; side < 2; ++side)
+            for (int f = 0; f < 4; ++f) {
+                for (size_t i = 0; i < M; ++i) {
+                    const crdt_tuples &src = side ? b[i] : a[i];
+                    const void *fs[4] = {src.key, src.ts, src.rep, src.tomb};
+                    void *fd[4] = {ar0[i].key, ar0[i].ts, ar0[i].rep, ar0[i].tomb};
+                    snd[i] = fs[f];
+                    rcv[i] = (char *)fd[f] + (side ? tot_a[i] * esz[f] : 0);
+                }
+                int rc = crdt_shard_alltoallv(c, snd.data(), side ? sb.data() : sa.data(), rcv.data(),
+                                              side ? rb.data() : ra.data(), esz[f]);
+                if (rc) return rc;
+            }
+    }
+    // 5. per member, a tree of merges over the received runs: A's runs in
+    //    rank order pairwise (lower rank left: the stable rank-order merge),
+    //    B's likewise, then merge(A, B); levels alternate between the arenas
+    std::vector<size_t> final_n(M, 0);
+    std::vector<crdt_tuples> fin(M);
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        int rc = bind(mb.ctx);
+        if (rc) return rc;
+        uint64_t *smp, *cnt, *bnd, *mc;
+        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        std::vector<Run> ruA, ruB;
+        size_t o = 0;
+        for (size_t p = 0; p < R; ++p) ruA.push_back(Run{0, o, ra[i * R + p]}), o += ra[i * R + p];
+        for (size_t p = 0; p < R; ++p) ruB.push_back(Run{0, o, rb[i * R + p]}), o += rb[i * R + p];
+        auto view = [&](const Run &x) {
+            const crdt_tuples &ar = x.arena ? ar1[i] : ar0[i];
+            return crdt_tuples{ar.key + x.off, ar.ts + x.off, ar.rep + x.off, ar.tomb + x.off};
+        };
+        auto merge = [&](const Run &x, const Run &y, int dst, uint64_t *count) -> int {
+            crdt_tuples tx = view(x), ty = view(y);
+            const crdt_tuples &ad = dst ? ar1[i] : ar0[i];
+            crdt_tuples to{ad.key + x.off, ad.ts + x.off, ad.rep + x.off, ad.tomb + x.off};   // (x, y adjacent)
+            return lww ? crdt_lww_merge(mb.ctx, &tx, x.n, &ty, y.n, &to, count)
+                       : crdt_orset_merge(mb.ctx, &tx, x.n, &ty, y.n, &to, count);
+        };
+        int level_arena = 0;
+        bool final_done = false;
+        while (!final_done) {
+            // one level: pairs of A runs, pairs of B runs; the last level merges A with B
+            std::vector<std::pair<Run, Run>> jobs;
+            std::vector<int> job_side;
+            const bool last = ruA.size() == 1 && ruB.size() == 1;
+            if (last) {
+                jobs.emplace_back(ruA[0], ruB[0]);
+                job_side.push_back(2);
+            } else {
+                for (int side = 0; side < 2; ++side) {
+                    auto &ru = side ? ruB : ruA;
+                    for (size_t k = 0; k < ru.size(); k += 2) {
+                        Run y = k + 1 < ru.size() ? ru[k + 1] : Run{ru[k].arena, ru[k].off + ru[k].n, 0};
+                        jobs.emplace_back(ru[k], y);
+                        job_side.push_back(side);
+                    }
+                }
+            }
+            const int dst = 1 - level_arena;
+            for (size_t j = 0; j < jobs.size(); ++j) {
+                rc = merge(jobs[j].first, jobs[j].second, dst, mc + j);
+                if (rc) return rc;
+            }
+            std::vector<uint64_t> hn(jobs.size());
+            hipError_t e = hipMemcpyAsync(hn.data(), mc, jobs.size() * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+            if (e != hipSuccess) return hip_fail(mb.ctx, e);
+            std::vector<Run> na_, nb_;
+            for (size_t j = 0; j < jobs.size(); ++j) {
+                const Run nr{dst, jobs[j].first.off, hn[j]};
+                if (job_side[j] == 2) {
+                    fin[i] = view(nr);
+                    final_n[i] = hn[j];
+                    final_done = true;
+                } else {
+                    (job_side[j] ? nb_ : na_).push_back(nr);
+                }
+            }
+            if (!final_done) {
+                ruA.swap(na_);
+                ruB.swap(nb_);
+            }
+            level_arena = dst;
+        }
+    }
+    int rc = check_devices(c);
+    if (rc) return rc;
+    // 6. the whole merged state on every member, or each member's own range
+    if (gather) {
+        size_t tot = 0;
+        rc = crdt_shard_set_allgather_v(c, fin.data(), final_n.data(), out, cap, &tot);
+        if (rc) return rc;
+        for (size_t i = 0; i < M; ++i) n_out[i] = tot;
+        return CRDT_OK;
+    }
+    for (size_t i = 0; i < M; ++i) {
+        auto &mb = c->m[i];
+        n_out[i] = final_n[i];
+        if (final_n[i] > cap) return CRDT_E_RANGE;
+        if (!final_n[i]) continue;
+        rc = bind(mb.ctx);
+        if (rc) return rc;
+        const size_t n = final_n[i];
+        hipError_t e = hipMemcpyAsync(out[i].key, fin[i].key, n * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out[i].ts, fin[i].ts, n * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out[i].rep, fin[i].rep, n * 4, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out[i].tomb, fin[i].tomb, n, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+    }
+    return CRDT_OK;
+}
+
+}  // namespace
+
+// Keyed-set merge of a DISTRIBUTED population: member i
+// holds only its own tuples a[i] (na[i]) and b[i] (nb[i]), each sorted by
+// (key, ts, rep).  The population's A is the stable merge of every rank's A
+// in rank order (likewise B); the result is crdt_lww_merge / crdt_orset_merge
+// of those -- computed by key-range owners: weighted sample splitters (one
+// all-gather), every rank's tuples sent to their owner (all-to-all-v), the
+// owner merges the received runs (rank-order pairwise merges, then A with
+// B).  gather != 0: every member's out[i] receives the whole merged state and
+// n_out[i] its length; gather == 0: out[i] / n_out[i] = the member's own key
+// range of it (ranges ascend with rank).  Synchronises.
+extern "C" int crdt_shard_lww_merge_local(crdt_comm *c, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
+                                          const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out,
+                                          int gather) {
+    return shard_set_merge_local(c, true, a, na, b, nb, out, cap, n_out, gather);
+}
+
+extern "C" int crdt_shard_orset_merge_local(crdt_comm *c, const crdt_tuples *a, const size_t *na,
+                                            const crdt_tuples *b, const size_t *nb, const crdt_tuples *out,
+                                            size_t cap, size_t *n_out, int gather) {
+    return shard_set_merge_local(c, false, a, na, b, nb, out, cap, n_out, gather);
 }

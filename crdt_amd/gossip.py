@@ -19,8 +19,8 @@ as device passes:
 Rounds are synchronous (every replica pulls the Diffs as of the round's
 start), one legal schedule of the reference's asynchronous goroutines.
 Across GPUs (one process per GPU, replicas partitioned by contiguous
-ranges) each rank all-gathers the population's Diffs once per round over
-RCCL and pulls any peer from that import block.
+ranges) each rank fetches only the Diffs its replicas pull, by one
+all-to-all-v per array (sharded_round), and merges from that import block.
 
 Key slots: local replica i's key k is slot i*K + k (K keys per replica).
 """
@@ -35,6 +35,8 @@ import torch.distributed as dist
 
 from . import shard
 from .engine import Engine
+
+LOCAL_MAX_CMD = 4096        # crdt_local_apply: commands per replica per call (its LDS sort)
 
 
 def _p(t: torch.Tensor | None):
@@ -132,24 +134,45 @@ class Population:
                 "kv_val": kval.contiguous()}
 
     # ---------------------------------------------------------------- rounds
-    def round(self, peers: Sequence[int], imp: dict | None = None, peer_first: Sequence[int] | None = None) -> dict:
+    def round(self, peers: Sequence[int], imp: dict | None = None, peer_first: Sequence[int] | None = None,
+              peer_index: Sequence[int] | None = None) -> dict:
         """One pull round: local replica i pulls the Diff of global replica
-        peers[i] and merges.  imp = None: every peer is local (this rank);
-        else peers index the import block (global ids) and peer_first[i] is
-        the global id of the first replica on the peer's rank (for the slot
+        peers[i] and merges (main.go:230-257).  peers[i] == the replica itself
+        is a self-pull (merge() still runs and rebuilds CurrentState,
+        main.go:76); peers[i] < 0 is a dead peer: the request fails and the
+        replica skips the round -- no merge, Diff and CurrentState unchanged
+        (main.go:234-239).  imp = None: every peer is on this rank; else the
+        pulled Diffs come from the import block: peer_index[i] (default
+        peers[i]) is the peer's replica in the block and peer_first[i] the
+        global id of the first replica on the peer's rank (for the slot
         re-basing).  Returns the merge output (new-Diff ranges and state)."""
         eng, dev, K = self.eng, self.eng.device, self.K
         peers = np.asarray(peers, dtype=np.int64)
         assert len(peers) == self.P
+        skip = peers < 0
         if imp is None:
-            lq = peers - self.first
+            lq = np.where(skip, np.arange(self.P) + self.first, peers) - self.first
             assert np.all((lq >= 0) & (lq < self.P)), "peer not on this rank: pass an import block"
-            codes_np = lq
+            codes_np = lq.copy()
             b = {"off": None, "ts": None, "kv_off": None, "kv_key": None, "kv_val": None}
         else:
-            codes_np = -(peers + 1)
+            idx = np.asarray(peer_index if peer_index is not None else peers, dtype=np.int64)
+            codes_np = -(idx + 1)
             b = imp
-            lq = peers - np.asarray(peer_first if peer_first is not None else np.zeros_like(peers), dtype=np.int64)
+            pf = np.asarray(peer_first if peer_first is not None else np.zeros_like(peers), dtype=np.int64)
+            lq = np.where(skip, np.arange(self.P), peers - pf)
+        if skip.any():
+            # a skipped replica "pulls" an empty segment appended to the B block
+            if b["off"] is None:
+                z = torch.zeros(2, dtype=torch.int64, device=dev)
+                e = torch.zeros(0, dtype=torch.int64, device=dev)
+                e32 = torch.zeros(0, dtype=torch.int32, device=dev)
+                b = {"off": z, "ts": e, "kv_off": z[:1], "kv_key": e32, "kv_val": e32}
+            else:
+                b = dict(b, off=torch.cat([b["off"], b["off"][-1:]]))
+            codes_np[skip] = -(b["off"].numel() - 1)       # B's last (empty) segment
+            prev_state = self.state if self.state is not None else self.empty_state()
+            prev_state = {k: v.clone() for k, v in prev_state.items()}
         # the slot re-basing of each pulled pair: (i - local index of q) * K, mod 2^32
         delta_np = ((np.arange(self.P, dtype=np.int64) - lq) * K) % (1 << 32)
         codes = torch.from_numpy(codes_np.copy()).to(dev)
@@ -160,14 +183,15 @@ class Population:
         # source, so every copy is per replica: R's kv offsets are the source's offsets
         # plus a per-replica delta (no per-entry scan).
         a_kr = self.kv_off[self.off]                       # kv range of each local replica's Diff
-        b_kr = b["kv_off"][b["off"]] if imp is not None else None
+        b_kr = b["kv_off"][b["off"]] if b["off"] is not None else None
         r_off = self._seg_offsets(codes, self.off, b["off"])
         n_lkv = self.kv_key.numel()
         r_kb = self._seg_offsets(codes, a_kr, b_kr, base=n_lkv)   # where each replica's pulled kv pairs go
         n_r, n_kv_end = (int(x) for x in torch.stack([r_off[-1], r_kb[-1]]).cpu())
         n_rkv = n_kv_end - n_lkv
         n_b = b["ts"].numel() if b["ts"] is not None else 0
-        src_kr = a_kr[codes.clamp(min=0)] if imp is None else b_kr[(-codes - 1).clamp(min=0)]
+        src_kr = torch.where(codes >= 0, a_kr[codes.clamp(min=0)],
+                             b_kr[(-codes - 1).clamp(min=0)] if b_kr is not None else a_kr[0])
         kdelta = r_kb[:-1] - src_kr
         r_kv = torch.empty(n_r + 1, dtype=torch.int64, device=dev)
         r_ts = torch.empty(n_r, dtype=torch.int64, device=dev)
@@ -182,7 +206,12 @@ class Population:
             bv = b["kv_val"] if n_b else self.kv_val
             self._call("crdt_seg_copy2", self.P, _p(codes), _p(a_kr), _p(b_kr), _p(r_kb), 4,
                        _p(self.kv_key), _p(bk), _p(arena_k), _p(delta), _p(self.kv_val), _p(bv), _p(arena_v), 1)
-        return self._merge_round(r_off, r_ts, r_kv, arena_k, arena_v, n_lkv, n_rkv)
+        out = self._merge_round(r_off, r_ts, r_kv, arena_k, arena_v, n_lkv, n_rkv)
+        if skip.any():                                     # no merge ran for these: CurrentState as it was
+            sl = torch.from_numpy((np.flatnonzero(skip)[:, None] * K + np.arange(K)[None, :]).reshape(-1)).to(dev)
+            for k in ("st_kind", "st_str", "st_sum"):
+                self.state[k][sl] = prev_state[k][sl]
+        return out
 
     def _kv_arena(self, n_lkv: int, n_more: int):
         """A kv arena whose prefix is the Diff's pairs, with room for n_more."""
@@ -294,7 +323,31 @@ class Population:
         slot ids), kv_val}, commands in arrival order per replica, pairs in
         apply order.  The Diffs get the *Command entries (a same-ms write
         replaces, main.go:187), CurrentState the local apply; returns the
-        HTTP status of each command (200 / 500)."""
+        HTTP status of each command (200 / 500).  More than LOCAL_MAX_CMD
+        commands for one replica run as several device calls, each taking the
+        next LOCAL_MAX_CMD of every replica's commands in arrival order."""
+        off = np.asarray(host_cmds["off"], dtype=np.int64)
+        cnt = np.diff(off)
+        if cnt.size == 0 or int(cnt.max()) <= LOCAL_MAX_CMD:
+            return self._apply_local_once(host_cmds)
+        kv_off = np.asarray(host_cmds["kv_off"], dtype=np.int64)
+        ts = np.asarray(host_cmds["ts"], dtype=np.int64)
+        kk, kv = np.asarray(host_cmds["kv_key"]), np.asarray(host_cmds["kv_val"])
+        status = np.zeros(int(off[-1]), dtype=np.int64)
+        for r in range(-(-int(cnt.max()) // LOCAL_MAX_CMD)):
+            lo = np.minimum(off[:-1] + r * LOCAL_MAX_CMD, off[1:])
+            hi = np.minimum(lo + LOCAL_MAX_CMD, off[1:])
+            idx = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)]).astype(np.int64)
+            sub_off = np.concatenate([[0], np.cumsum(hi - lo)])
+            pcnt = kv_off[idx + 1] - kv_off[idx]
+            pidx = np.concatenate([np.arange(kv_off[j], kv_off[j + 1]) for j in idx] or [np.zeros(0, np.int64)])
+            pidx = pidx.astype(np.int64)
+            sub = {"off": sub_off, "ts": ts[idx], "kv_off": np.concatenate([[0], np.cumsum(pcnt)]),
+                   "kv_key": kk[pidx], "kv_val": kv[pidx]}
+            status[idx] = self._apply_local_once(sub)
+        return status
+
+    def _apply_local_once(self, host_cmds: dict) -> np.ndarray:
         dev = self.eng.device
         t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
         cmds = {"off": t(host_cmds["off"], np.int64), "ts": t(host_cmds["ts"], np.int64),
@@ -305,6 +358,7 @@ class Population:
             self.state = self.empty_state()
         out = self.eng.local_apply({"off": self.off, "ts": self.ts, "origin": self.origin}, cmds, self.state,
                                    self.str_bytes, self.str_off, self.P * self.K)
+        self.eng.check_device()        # CRDT_DEV_RANGE: nothing of an over-limit replica was applied
         n_out = int(out["off"][-1].item())
         src = out["src"][:n_out].contiguous()
         new_kv = torch.empty(n_out + 1, dtype=torch.int64, device=dev)
@@ -334,34 +388,101 @@ class Population:
 def random_peers(rng: np.random.Generator, total: int, first: int, count: int) -> np.ndarray:
     """A random peer other than itself for each of replicas [first, first+count).
 
-    The reference draws uniformly from friendList (main.go:230), which is
-    ports 8080..8089 (main.go:219-222): that list holds the server itself
-    and ports no server listens on (the demo starts 8080..8084,
-    main.go:319-321), so some of its rounds fail the request and skip
-    (main.go:234-237: no merge) and some pull its own Diff.  A self-pull
-    inserts nothing (every key equal, the local entry kept, main.go:54-65)
-    but merge() still runs (main.go:257) and rebuilds CurrentState from the
-    remote-origin entries (main.go:76), dropping what local writes applied
-    to it directly (main.go:188-207) -- the same rebuild every merge ends
-    with.  This schedule draws uniformly over the OTHER live replicas only:
-    the Diffs it reaches are the reference's, and its CurrentState is the
-    rebuild after each round's merge; it never produces the reference's
-    merge-without-new-data rounds, so per-round pull rates differ."""
+    A schedule that only pulls live peers: every round of every replica
+    reaches new data.  reference_peers draws like the reference instead."""
     r = rng.integers(0, total - 1, size=total)
     ids = np.arange(total)
     peers = np.where(r >= ids, r + 1, r)
     return peers[first:first + count]
 
 
-def sharded_round(pop: Population, peers_all: np.ndarray, group=None) -> dict:
-    """One round across the ranks of `group`: every rank all-gathers the
-    population's Diffs, then pulls its replicas' peers from that block."""
+def reference_peers(rng: np.random.Generator, total: int, first: int, count: int,
+                    dead: int | None = None) -> np.ndarray:
+    """The reference's draw (main.go:230): uniform over friendList, which
+    holds EVERY replica -- the server itself included -- and ports no server
+    listens on (main.go:219-222: 8080..8089 against the 8080..8084 the demo
+    starts, main.go:319-321; `dead` defaults to `total`, the same ratio).  A
+    dead pick is -1: the request fails and the round is skipped (main.go:234-
+    239, Population.round leaves that replica alone); a self pick is a
+    self-pull, whose merge() inserts nothing and rebuilds CurrentState
+    (main.go:76)."""
+    dead = total if dead is None else dead
+    r = rng.integers(0, total + dead, size=total)
+    peers = np.where(r < total, r, -1)
+    return peers[first:first + count]
+
+
+def pull_plan(peers_all: np.ndarray, world: int) -> tuple:
+    """Who pulls what in a round over `world` ranks (replicas partitioned by
+    contiguous ranges, shard.shard_range): firsts[r] = rank r's first global
+    replica (firsts[world] = total) and need[r] = the sorted distinct live
+    peers rank r's replicas pull.  Every rank derives the same plan from the
+    round's draw (no exchange)."""
+    total = len(peers_all)
+    firsts = [shard.shard_range(total, world, r)[0] for r in range(world)] + [total]
+    need = []
+    for r in range(world):
+        mine = np.asarray(peers_all[firsts[r]:firsts[r + 1]], dtype=np.int64)
+        need.append(np.unique(mine[mine >= 0]))
+    return firsts, need
+
+
+def sharded_round(pop: Population, peers_all: np.ndarray, group=None, comm=None) -> dict:
+    """One round across the ranks of `group` (main.go:226-258 over xGMI):
+    every rank fetches ONLY the Diffs its replicas pull -- rank p sends rank
+    r the Diffs of the replicas p owns among need[r] (pull_plan), as one
+    all-to-all-v per array (the native RCCL communicator `comm`'s
+    crdt_shard_alltoallv when given, else torch.distributed) -- then the
+    round merges as on one GPU.  peers_all: every replica's draw (global
+    ids, -1 = dead peer), identical on every rank."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1:
         return pop.round(peers_all[pop.first:pop.first + pop.P])
-    P_all = len(peers_all)
-    firsts = [shard.shard_range(P_all, world, r)[0] for r in range(world)]
-    owner_first = np.array([max(f for f in firsts if f <= q) for q in range(P_all)], dtype=np.int64)
-    imp = pop.gather_import(group)
-    mine = peers_all[pop.first:pop.first + pop.P]
-    return pop.round(mine, imp=imp, peer_first=owner_first[mine])
+    rank = dist.get_rank(group)
+    dev = pop.eng.device
+    firsts, need = pull_plan(peers_all, world)
+    f0, f1 = firsts[rank], firsts[rank + 1]
+    # what this rank sends: for each destination r, the replicas of need[r] it owns
+    send_ids = [need[r][(need[r] >= f0) & (need[r] < f1)] - f0 for r in range(world)]
+    n_rep = [len(x) for x in send_ids]
+    codes = torch.from_numpy(np.concatenate(send_ids).astype(np.int64)).to(dev)
+    ecnt = pop._counts(pop.off)
+    kvcnt = pop._counts(pop.kv_off)
+    a_kr = pop.kv_off[pop.off]
+    e_off = pop._seg_offsets(codes, pop.off, None)
+    k_off = pop._seg_offsets(codes, a_kr, None)
+    cut = np.concatenate([[0], np.cumsum(n_rep)]).astype(np.int64)
+    eb, kb = (x[torch.from_numpy(cut).to(dev)].cpu().numpy() for x in (e_off, k_off))
+    n_e, n_k = int(eb[-1]), int(kb[-1])
+    s_ecnt = ecnt[codes] if codes.numel() else ecnt[:0]
+    s_ts = pop._seg_copy(codes, pop.off, None, e_off, pop.ts, None, n_e, wide=1) if n_e else pop.ts[:0]
+    s_kvcnt = pop._seg_copy(codes, pop.off, None, e_off, kvcnt, None, n_e, wide=1) if n_e else kvcnt[:0]
+    s_key = pop._seg_copy(codes, a_kr, None, k_off, pop.kv_key, None, n_k) if n_k else pop.kv_key[:0]
+    s_val = pop._seg_copy(codes, a_kr, None, k_off, pop.kv_val, None, n_k) if n_k else pop.kv_val[:0]
+    # per-destination entry / pair counts, all-gathered (replica counts follow from the plan)
+    se = np.diff(eb).tolist()
+    sk = np.diff(kb).tolist()
+    mat = [torch.zeros(2 * world, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(mat, torch.tensor(se + sk, dtype=torch.int64), group=group)
+    mat = torch.stack(mat).numpy()
+    r_rep = [int(((need[rank] >= firsts[p]) & (need[rank] < firsts[p + 1])).sum()) for p in range(world)]
+    r_e, r_k = mat[:, rank].tolist(), mat[:, world + rank].tolist()
+
+    def xchg(t, s_counts, r_counts):
+        if comm is not None:
+            out = torch.empty(max(sum(r_counts), 1), dtype=t.dtype, device=dev)
+            src = t if t.numel() else torch.empty(1, dtype=t.dtype, device=dev)
+            torch.cuda.synchronize(dev)
+            comm.alltoallv([src], [s_counts], [out], [r_counts], t.element_size())
+            comm.sync()
+            return out[:sum(r_counts)]
+        return shard.alltoallv(t, s_counts, r_counts, group)
+
+    imp = pop._make_import(xchg(s_ecnt, n_rep, r_rep), xchg(s_ts, se, r_e), xchg(s_kvcnt, se, r_e),
+                           xchg(s_key, sk, r_k), xchg(s_val, sk, r_k))
+    mine = np.asarray(peers_all[pop.first:pop.first + pop.P], dtype=np.int64)
+    live = mine >= 0
+    idx = np.where(live, np.searchsorted(need[rank], np.maximum(mine, 0)), -1)
+    owner = np.searchsorted(np.asarray(firsts), np.maximum(mine, 0), side="right") - 1
+    pf = np.where(live, np.asarray(firsts)[owner], 0)
+    return pop.round(mine, imp=imp, peer_first=pf, peer_index=idx)

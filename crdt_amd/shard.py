@@ -162,6 +162,136 @@ def sharded_set_merge(eng, a, b, lww: bool = True, group=None, gather: bool = Tr
 
 
 
+# ---------------------------------------------------------------- distributed keyed sets (§8(e) D)
+SAMPLES_PER_SIDE = 256            # = kSamplesPerSide of csrc/shard.hip
+
+
+def weighted_splitters(blocks: np.ndarray, world: int, per: int = SAMPLES_PER_SIDE) -> List[int]:
+    """Splitters of a distributed key population (crdt_shard_*_merge_local's
+    rule): blocks[p] = [n_a, n_b, per keys of A, per keys of B] of rank p; a
+    non-empty side's samples each weigh its size, an empty side's none.  Inner
+    splitter q = the first sample key (in key order) at which the cumulative
+    weight reaches q / world of the total."""
+    e = []
+    for b in np.asarray(blocks, dtype=np.uint64).reshape(world, 2 + 2 * per):
+        for side in range(2):
+            n = int(b[side])
+            if n:
+                e += [(int(k), n) for k in b[2 + side * per: 2 + (side + 1) * per]]
+    e.sort(key=lambda x: x[0])
+    W = sum(w for _, w in e)
+    spl, cum, k = [0], 0, 0
+    for q in range(1, world):
+        while k < len(e) and (cum + e[k][1]) * world < q * W:
+            cum += e[k][1]
+            k += 1
+        spl.append(0 if W == 0 else (e[k][0] if k < len(e) else e[-1][0]))
+    return spl + [KEY_END]
+
+
+def _sample_block(t_a, t_b, per: int) -> torch.Tensor:
+    out = torch.zeros(2 + 2 * per, dtype=torch.int64, device=t_a.key.device)
+    out[0], out[1] = len(t_a), len(t_b)
+    for side, t in ((0, t_a), (1, t_b)):
+        n = len(t)
+        if n:
+            idx = torch.arange(per, dtype=torch.int64, device=t.key.device) * n // per
+            out[2 + side * per: 2 + (side + 1) * per] = t.key[idx]
+    return out
+
+
+def _cuts(eng, t, spl: List[int]) -> List[int]:
+    """0, lower_bound(spl[1]) .. lower_bound(spl[R-1]), n in t's sorted keys."""
+    n, inner = len(t), spl[1:-1]
+    if n == 0 or not inner:
+        return [0] * (len(spl) - 1) + [n]
+    pr = np.array(inner, dtype=np.uint64)
+    if t.key.is_cuda:
+        got = eng.lower_bound_u64(t.key, torch.from_numpy(pr.view(np.int64)).to(t.key.device)).cpu().tolist()
+    else:
+        got = np.searchsorted(t.key.numpy().view(np.uint64), pr, side="left").tolist()
+    return [0] + [int(x) for x in got] + [n]
+
+
+def alltoallv(t: torch.Tensor, send_counts: List[int], recv_counts: List[int], group=None) -> torch.Tensor:
+    """All-to-all-v of a 1-D tensor: segment q of t (send_counts[q] elements,
+    segments in rank order) goes to rank q; the result holds what every rank
+    sent here, in rank order.  Paired isend / irecv (works on gloo and nccl)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if t.is_cuda and dist.get_backend(group) == "gloo":      # gloo's send / recv take host tensors
+        return alltoallv(t.cpu(), send_counts, recv_counts, group).to(t.device)
+    out = torch.empty(sum(recv_counts), dtype=t.dtype, device=t.device)
+    so = np.concatenate([[0], np.cumsum(send_counts)]).astype(np.int64)
+    ro = np.concatenate([[0], np.cumsum(recv_counts)]).astype(np.int64)
+    out[ro[rank]:ro[rank + 1]] = t[so[rank]:so[rank + 1]]
+    reqs = []
+    for q in range(world):
+        if q == rank:
+            continue
+        peer = dist.get_global_rank(group, q) if group is not None else q
+        if send_counts[q]:
+            reqs.append(dist.isend(t[so[q]:so[q + 1]].contiguous(), peer, group=group))
+        if recv_counts[q]:
+            reqs.append(dist.irecv(out[ro[q]:ro[q + 1]], peer, group=group))
+    for r in reqs:
+        r.wait()
+    return out
+
+
+def _tree_merge(runs_a, runs_b, merge):
+    """A's runs pairwise in rank order (lower rank left), B's likewise, then
+    merge(A, B): the order crdt_shard_*_merge_local merges in."""
+    def level(runs):
+        return [merge(runs[k], runs[k + 1]) if k + 1 < len(runs) else merge(runs[k], runs[k].slice(0))
+                for k in range(0, len(runs), 2)]
+    while len(runs_a) > 1 or len(runs_b) > 1:
+        runs_a, runs_b = level(runs_a), level(runs_b)
+    return merge(runs_a[0], runs_b[0])
+
+
+def sharded_set_merge_local(eng, a, b, lww: bool = True, group=None, gather: bool = True, merge=None,
+                            per: int = SAMPLES_PER_SIDE):
+    """Keyed-set merge of a DISTRIBUTED population over torch.distributed
+    (crdt_shard_*_merge_local's protocol): a, b = THIS rank's sorted local
+    tuples.  The population's A = stable rank-order merge of every rank's A
+    (B likewise); returns the merge of the two -- the whole state (gather) or
+    this rank's key range of it.  `merge` (default the engine's LWW / OR-Set
+    merge) is the per-rank compute."""
+    from .engine import TupleSet
+    merge = merge or (eng.lww_merge if lww else eng.orset_merge)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return merge(a, b)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    blk = _sample_block(a, b, per)
+    blocks = [torch.zeros_like(blk) for _ in range(world)]
+    dist.all_gather(blocks, blk, group=group)
+    spl = weighted_splitters(torch.stack(blocks).cpu().numpy().view(np.uint64), world, per)
+    ca, cb = _cuts(eng, a, spl), _cuts(eng, b, spl)
+    sa = [ca[q + 1] - ca[q] for q in range(world)]
+    sb = [cb[q + 1] - cb[q] for q in range(world)]
+    cnt = torch.tensor(sa + sb, dtype=torch.int64, device=a.key.device)
+    mat = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(mat, cnt, group=group)
+    mat = torch.stack(mat).cpu().numpy()
+    ra, rb = mat[:, rank].tolist(), mat[:, world + rank].tolist()
+
+    def xchg(t, s, r):
+        return TupleSet(*(alltoallv(f, s, r, group) for f in (t.key, t.ts, t.rep, t.tomb)))
+
+    ga, gb = xchg(a, sa, ra), xchg(b, sb, rb)
+
+    def runs(t, counts):
+        o = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        return [TupleSet(t.key[o[p]:o[p + 1]], t.ts[o[p]:o[p + 1]], t.rep[o[p]:o[p + 1]], t.tomb[o[p]:o[p + 1]])
+                for p in range(world)]
+
+    m = _tree_merge(runs(ga, ra), runs(gb, rb), merge)
+    if not gather:
+        return m
+    return TupleSet(allgather_v(m.key, group), allgather_v(m.ts, group), allgather_v(m.rep, group),
+                    allgather_v(m.tomb, group))
+
+
 # ---------------------------------------------------------------- RefMerge by ts range (§8(e))
 def sharded_refmerge(eng, packed: dict, group=None) -> dict:
     """(*Server).merge() of one batch of replicas whose Diff/RemoteDiff logs
@@ -326,3 +456,52 @@ class Comm:
         self._call("crdt_shard_lww_merge" if lww else "crdt_shard_orset_merge", self._tuples(a), na,
                    self._tuples(b), nb, self._tuples(outs), cap, C.byref(n))
         return [o.slice(n.value) for o in outs]
+
+    def alltoallv(self, sends, send_counts, recvs, recv_counts, elem_size: int) -> None:
+        """crdt_shard_alltoallv: counts are [members x nranks] nested lists."""
+        flat = lambda x: (C.c_size_t * (self.members * self.nranks))(*[int(v) for row in x for v in row])
+        self._call("crdt_shard_alltoallv", self._ptrs(sends), flat(send_counts), self._ptrs(recvs),
+                   flat(recv_counts), elem_size)
+
+    def set_merge_local(self, a, b, lww: bool = True, gather: bool = True, cap: int | None = None, outs=None):
+        """Keyed-set merge of a distributed population: a[i], b[i] = member
+        i's own sorted tuples (crdt_shard_*_merge_local).  Returns per-member
+        TupleSets: the whole merged state (gather) or the member's key range."""
+        from .engine import TupleSet
+        na = (C.c_size_t * self.members)(*[len(x) for x in a])
+        nb = (C.c_size_t * self.members)(*[len(x) for x in b])
+        if cap is None:                     # a bound needs every rank's sizes: one process holding them all
+            if self.members != self.nranks:
+                raise ValueError("cap is required when other processes hold members")
+            cap = max(sum(len(x) + len(y) for x, y in zip(a, b)), 1)
+        outs = [TupleSet.empty(cap, d) for d in self.devices] if outs is None else outs
+        n = (C.c_size_t * self.members)()
+        self._call("crdt_shard_lww_merge_local" if lww else "crdt_shard_orset_merge_local", self._tuples(a), na,
+                   self._tuples(b), nb, self._tuples(outs), cap, n, 1 if gather else 0)
+        return [o.slice(n[i]) for i, o in enumerate(outs)]
+
+    def refmerge(self, engines, packed_list):
+        """crdt_shard_refmerge: member i merges packed_list[i] (its ts-range
+        slice of one batch, device tensors on member i's GPU; engines[i] only
+        allocates the outputs).  Returns per-member refmerge output dicts
+        (new-Diff slice + the whole CurrentState)."""
+        from ._lib import crdt_refmerge_in, crdt_refmerge_out
+        outs, cins, couts = [], [], []
+        for eng, d in zip(engines, packed_list):
+            n_l, n_r, ns = d["l_ts"].numel(), d["r_ts"].numel(), int(d["n_slots"])
+            dev = eng.device
+            o = {"off": torch.empty(d["replicas"] + 1, dtype=torch.int64, device=dev),
+                 "ts": torch.empty(max(n_l + n_r, 1), dtype=torch.int64, device=dev),
+                 "origin": torch.empty(max(n_l + n_r, 1), dtype=torch.uint8, device=dev),
+                 "src": torch.empty(max(n_l + n_r, 1), dtype=torch.int64, device=dev),
+                 "st_kind": torch.empty(max(ns, 1), dtype=torch.uint8, device=dev),
+                 "st_str": torch.empty(max(ns, 1), dtype=torch.int32, device=dev),
+                 "st_sum": torch.empty(max(ns, 1), dtype=torch.int64, device=dev)}
+            outs.append(o)
+            cins.append(eng._refmerge_in(d))
+            couts.append(crdt_refmerge_out(*(o[k].data_ptr() for k in
+                                             ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum"))))
+        ci = (crdt_refmerge_in * self.members)(*cins)
+        co = (crdt_refmerge_out * self.members)(*couts)
+        self._call("crdt_shard_refmerge", ci, co)
+        return outs

@@ -68,7 +68,8 @@ int crdt_ctx_sync(crdt_ctx *ctx);
  * decoupled look-back exceeded its bounded wait (a scheduling fault, never
  * expected) raises CRDT_DEV_LOOKBACK and its output is invalid. */
 #define CRDT_DEV_LOOKBACK 1u
-#define CRDT_DEV_RANGE 2u          /* a batch exceeded a per-replica kernel limit (its output is invalid) */
+#define CRDT_DEV_RANGE 2u          /* a batch exceeded a per-replica kernel limit, or a pass found its
+                                      inputs inconsistent (merge bitmaps): the output is invalid */
 int crdt_ctx_device_status(crdt_ctx *ctx, uint32_t *flags, int clear);
 int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 /* Pre-size the context's device workspace so that later calls never
@@ -76,10 +77,15 @@ int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
 /* Kernel tuning knobs (process-wide), for A/B runs: "join.unroll" (1,2,4,8),
  * "join.nontemporal" (0/1), "join.blocks_per_cu" (1..64),
- * "vclock.pairs_per_wave" (1,2,4,8), "sets.grid_per_cu" (0 = occupancy query);
- * diagnostics: "sets.stamps" (0/1), "sets.diag_no_lookback" (0/1, WRONG output);
+ * "vclock.pairs_per_wave" (1,2,4,8), "sets.lww_chunk" / "sets.or_chunk"
+ * (tiles per count / write chunk of the set merges, 0 = one chunk),
+ * "sets.streams" (1, 2), "sets.lww_parts", "sets.or_parts",
+ * "refmerge.tile_parts", "refmerge.count_dma";
  * fault injection: "fail.refmerge" (n: the next n RefMerge calls return
- * CRDT_E_NOMEM before touching the device -- error-path tests).
+ * CRDT_E_NOMEM before touching the device -- error-path tests),
+ * "fail.zero_bits" (n: the next n two-pass merges -- set merges, RefMerge --
+ * zero their merge bitmaps between the passes: the write pass must raise
+ * CRDT_DEV_RANGE, never read out of range).
  * Returns CRDT_E_INVAL for an unknown name or value. */
 int crdt_set_option(const char *name, int64_t value);
 
@@ -156,7 +162,9 @@ typedef struct crdt_tuples {
 
 /* LWW: one tuple per distinct key = the max (ts, rep) element (left wins an
  * exact tie; tombstoned winners are kept).  out capacity >= na + nb;
- * *out_count_dev (device uint64) receives the output length. */
+ * *out_count_dev (device uint64) receives the output length.  key / ts / rep
+ * must be naturally aligned (8 / 8 / 4 bytes; CRDT_E_INVAL otherwise): the
+ * passes stage them by LDS-DMA from any element offset. */
 int crdt_lww_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                    size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 /* OR-Set: union of unique tags (key, ts, rep); tomb OR-ed over equal tags. */
@@ -188,12 +196,6 @@ int crdt_u64_lower_bound(crdt_ctx *ctx, const uint64_t *sorted_dev, size_t n, co
                          size_t m, uint64_t *out_dev);
 int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
                                uint64_t *bad_dev);
-/* Diagnostic: after crdt_set_option("sets.stamps", 1), the last set merge
- * records 8 s_memtime stamps per tile at its phase boundaries; copies
- * min(cap, *n) of them to host memory. */
-int crdt_debug_set_stamps(crdt_ctx *ctx, uint64_t *host, size_t cap, size_t *n);
-/* Diagnostic: persistent grid size and occupancy answer of the last set merge. */
-int crdt_debug_set_grid(size_t *grid, int *occ);
 
 /* ------------------------------------------------ RefMerge (a1-a5)
  * Batched, bit-exact (*Server).merge() (main.go:35-100) for many replicas.
@@ -300,8 +302,11 @@ int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_re
  * Atoi failure stops it with status 500.  The new Diff is written like a
  * RefMerge output (src >= 0: Diff index, < 0: command j as -(j+1)); the
  * state (kind/str/sum per key slot, as crdt_refmerge_out) is updated in
- * place.  At most 4096 commands per replica per call (CRDT_DEV_RANGE
- * otherwise); the Alive check (502) is the host's. */
+ * place.  At most 4096 commands per replica per call: a replica over the
+ * limit raises CRDT_DEV_RANGE and nothing of it is applied (its Diff range
+ * is empty, its state untouched, its commands' status 0), so the caller can
+ * split its commands over several calls; the Alive check (502) is the
+ * host's. */
 typedef struct crdt_local_in {
     uint32_t replicas;
     uint32_t n_slots;
@@ -432,6 +437,45 @@ int crdt_shard_lww_merge(crdt_comm *comm, const crdt_tuples *a, size_t na, const
                          const crdt_tuples *out, size_t cap, size_t *n_out);
 int crdt_shard_orset_merge(crdt_comm *comm, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
                            const crdt_tuples *out, size_t cap, size_t *n_out);
+
+/* All-to-all-v: member i sends send_counts[i * nranks + q] elements of
+ * elem_size bytes to global rank q (its send buffer holds the segments in
+ * rank order) and receives recv_counts[i * nranks + p] elements from rank p
+ * into its recv buffer (segments in rank order); grouped ncclSend / ncclRecv
+ * on the member streams, enqueued. */
+int crdt_shard_alltoallv(crdt_comm *comm, const void *const *send, const size_t *send_counts, void *const *recv,
+                         const size_t *recv_counts, size_t elem_size);
+/* Keyed-set merge of a DISTRIBUTED population (the reference
+ * analog is the whole-log exchange of main.go:226-258): member i holds only
+ * its own tuples a[i] (na[i]) and b[i] (nb[i]), each sorted by (key, ts,
+ * rep).  The population's A is the stable merge of every rank's A in rank
+ * order (B likewise) and the result is crdt_lww_merge / crdt_orset_merge of
+ * the two -- computed by key-range owners: sampled splitters weighted by the
+ * ranks' sizes (one ncclAllGather), every rank's tuples sent to their owner
+ * (crdt_shard_alltoallv), the owner's merge of the received runs (rank-order
+ * pairwise merges of A's runs and of B's, then A with B).  gather != 0:
+ * every member's out[i] receives the whole merged state, n_out[i] its
+ * length; gather == 0: out[i] / n_out[i] = the member's own key range of it
+ * (ranges ascend with rank).  CRDT_E_RANGE if a result exceeds cap.
+ * Synchronises. */
+int crdt_shard_lww_merge_local(crdt_comm *comm, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
+                               const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out, int gather);
+int crdt_shard_orset_merge_local(crdt_comm *comm, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
+                                 const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out, int gather);
+/* (*Server).merge() (main.go:35-100) of ONE batch of replicas whose Diff /
+ * RemoteDiff logs are split by ts range over the ranks (global rank g holds
+ * the g-th ts range of every replica; every member's kv_val ids index the
+ * same string table): in[i] / out[i] are member i's slice and outputs in the
+ * crdt_refmerge_batch layout.  One call runs the whole protocol on the
+ * communicator's streams, no host synchronisation: all-reduce(MAX) of each
+ * replica's max(L) (remote ts above the global max are dropped, main.go:49),
+ * the local merge, the replay accumulators reduced across ranks (MAX of the
+ * holder rank, SUM of its string id, of the wrapped sums and of the
+ * parsable counts), CurrentState finalised on every member.  out[i].off /
+ * ts / origin / src = member i's slice of the new Diffs (slices concatenate
+ * in rank order); st_* = the whole CurrentState.  Bit-exact with
+ * crdt_refmerge_batch of the unsharded batch. */
+int crdt_shard_refmerge(crdt_comm *comm, const crdt_refmerge_in *in, const crdt_refmerge_out *out);
 
 /* ------------------------------------------------ synthetic state (bench/tests)
  * SplitMix64-seeded generators; identical to the numpy

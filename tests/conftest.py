@@ -18,7 +18,7 @@ def eng():
     from crdt_amd.engine import Engine
     assert torch.cuda.is_available(), "gpu-marked test without a GPU"
     e = Engine(0)
-    # CRDT_TEST_OPTIONS="sets.grid_per_cu=1,join.unroll=2": run the GPU suite
+    # CRDT_TEST_OPTIONS="sets.streams=1,join.unroll=2": run the GPU suite
     # under non-default kernel knobs (crdt_set_option)
     from crdt_amd import _lib
     for opt in filter(None, os.environ.get("CRDT_TEST_OPTIONS", "").split(",")):

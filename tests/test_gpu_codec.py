@@ -122,6 +122,26 @@ def test_decode_flags(eng):
     bodies.append(bytes(bad_count))
     _, st, _, _ = _decode(eng, bodies, keys, vals)
     assert st.tolist() == [0, 1, 2, 2, 2, 2, 1], st
+    # a valid body AFTER a body whose pair counts disagree with its header
+    # decodes exactly (its kv ranges are rebased per body), and the rejected
+    # body's strings never enter the tables
+    bad = bytearray(_raw_body([(1, [(b"qq", b"77")]), (2, [(b"rr", b"88"), (b"ss", b"99")])]))
+    struct.pack_into("<I", bad, 32 + 16, 7)                          # pairs[0] = 7 != header n_pairs
+    good2 = _raw_body([(4, [(b"a", b"5"), (b"c", b"6")]), (9, [(b"b", b"x")])])
+    k3, v3 = codec.StrTab(eng), codec.StrTab(eng)
+    dec, st, kk, kv = _decode(eng, [good, bytes(bad), good2], k3, v3)
+    assert st.tolist() == [0, 1, 0], st
+    r_off, r_ts, r_kv = (dec[x].cpu().numpy() for x in ("r_off", "r_ts", "r_kv"))
+    ks, vs = k3.strings(), v3.strings()
+    assert not {b"qq", b"rr", b"ss"} & set(ks) and not {b"77", b"88", b"99"} & set(vs)
+    for b, body in ((0, good), (2, good2)):
+        host = Server(None, 9000)
+        assert host.IngestBinary(body) == 0
+        assert r_ts[r_off[b]:r_off[b + 1]].tolist() == host.RemoteDiff.Keys()
+        for e, t in zip(range(r_off[b], r_off[b + 1]), host.RemoteDiff.Keys()):
+            got = {ks[kk[q] - 1000 * b].decode(): vs[kv[q]].decode() for q in range(r_kv[e], r_kv[e + 1])}
+            assert got == host.RemoteDiff.Get(t)[0]
+        host.close()
     # a key id past the replica's slot range takes the host path
     k2, v2 = codec.StrTab(eng), codec.StrTab(eng)
     _, st, _, _ = _decode(eng, [_raw_body([(1, [(b"a", b"1"), (b"b", b"1"), (b"c", b"1")])])], k2, v2, key_cap=2)

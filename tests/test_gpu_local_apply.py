@@ -138,3 +138,39 @@ def test_local_apply_kats(eng):
             elif kind[s] == 2:
                 st[key] = str(int(ssum[s]))
         assert st == kat[5], kat[0]
+
+
+def test_local_apply_over_the_per_call_limit(eng):
+    """More than 4096 commands for one replica (crdt_local_apply's per-call
+    limit): Population.apply_local runs them as several device
+    calls in arrival order, == the restatement; a raw over-limit call raises
+    CRDT_DEV_RANGE and applies nothing of that replica."""
+    rng = np.random.default_rng(11)
+    P = 3
+    diffs = [_rand_diff(rng, 1_000 + 7 * i, 20) for i in range(P)]
+    pop = gossip.Population(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    cmds, exp = [], []
+    for i, n in enumerate((9000, 5, 4097)):
+        lo = min(diffs[i])
+        mine = []
+        for _ in range(n):
+            t = int(rng.integers(lo - 5, lo + 6000))
+            data = {KEYS[int(rng.integers(0, K))]: STRS[int(rng.integers(0, len(STRS)))]}
+            mine.append((t, data))
+            exp.append(pyref.add_command(diffs[i], states[i], t, data))
+        cmds.append(mine)
+    np.testing.assert_array_equal(pop.apply_local(_cmd_block(cmds)), exp)
+    _same_diffs(_unpack(pop), diffs)
+    assert _state(pop) == states
+    # one device call over the limit: flagged, and the replica's Diff range / state untouched
+    before = pop.to_host()
+    st_before = {k: v.clone() for k, v in pop.state.items()}
+    blk = _cmd_block([[(5_000_000 + j, {KEYS[0]: STRS[1]}) for j in range(4097)], [], []])
+    with pytest.raises(Exception, match="device-side failure"):
+        pop._apply_local_once(blk)
+    after = pop.to_host()
+    for k in ("off", "ts", "origin"):
+        np.testing.assert_array_equal(before[k], after[k])
+    for k, v in st_before.items():
+        assert torch.equal(v, pop.state[k]), k

@@ -80,3 +80,41 @@ def test_null_ingest_is_reserved_as_null(eng):
     assert b.Gossip()[1] == b'{"100":{"z":"0"},"1000":{"q":"1"},"5":null,"6":{"a":"1"},"7":{"a":"2"}}'
     s.close()
     b.close()
+
+
+def test_inconsistent_bitmaps_fail_merge_cleanly(eng):
+    """fail.zero_bits: the RefMerge bitmaps zeroed between its count and tile
+    passes.  The tile pass raises CRDT_DEV_RANGE instead of reading past the
+    logs; merge() returns CRDT_E_DEVICE with Diff, RemoteDiff and
+    CurrentState untouched and the server Alive -- on the first (host-built)
+    merge and on a device-resident one -- and the next merge() is exact."""
+    kat = next(k for k in load_kats() if k["name"].startswith("KAT-1"))
+    diff, remote = kat_inputs(kat)
+    s = _server_from(eng, diff, remote)
+    for resident in (False, True):
+        before = (s.DiffSignature, s.RemoteDiff.Keys(), s.CurrentState, [s.RemoteDiff.Get(t) for t in remote])
+        _lib.call("crdt_set_option", b"fail.zero_bits", 1)
+        with pytest.raises(_lib.CrdtError) as ei:
+            s.merge()
+        assert ei.value.status == -8                               # CRDT_E_DEVICE
+        after = (s.DiffSignature, s.RemoteDiff.Keys(), s.CurrentState, [s.RemoteDiff.Get(t) for t in remote])
+        assert after == before, f"resident={resident}"
+        assert s.Gossip()[0] == 200                                # Alive again, lock released
+        s.merge()
+        assert s.DiffSignature == kat["diff"] and s.CurrentState == kat["state"]
+        for t, v in remote.items():                                # the same pull again (KAT-5: idempotent)
+            s.RemoteDiff.Put(t, v)
+    assert eng.device_status(clear=True) & 2                       # the raised flags stay for the caller
+    s.close()
+
+
+def test_refmerge_batch_inconsistent_bitmaps_flag(eng):
+    """The batched call: the flag is raised (crdt_ctx_device_status), no fault."""
+    from crdt_amd import refmerge, synth
+    h = synth.refmerge_packed(17, 6, 9000)
+    d = refmerge.to_device(h, eng.device)
+    _lib.call("crdt_set_option", b"fail.zero_bits", 1)
+    eng.refmerge_batch(d)
+    assert eng.device_status(clear=True) == 2
+    eng.refmerge_batch(d)
+    assert eng.device_status(clear=True) == 0

@@ -102,3 +102,32 @@ def test_resident_diff_put_and_remote_put_between_merges(eng):
     assert s.CurrentState == st and s.DiffSignature == _sig(diff)
     assert s.RemoteDiff.Size() == 0
     s.close()
+
+
+def test_resident_server_many_queued_writes(eng):
+    """More than 4096 distinct-ts local writes queued between merges of a
+    device-resident server: they are applied to the device Diff in
+    chunks and none is lost."""
+    rng = np.random.default_rng(5)
+    s = Server(eng, 8080)
+    diff, state = {}, {}
+    for t in range(10, 400, 7):
+        v = _rand_value(rng)
+        s.Diff.Put(t, v)
+        diff[t] = dict(v)
+    s.RemoteDiff.Put(3, {"k1": "-12"})
+    s.merge()                                                     # device-resident from here on
+    diff, state = pyref.merge(diff, {3: {"k1": "-12"}})
+    assert s.CurrentState == state
+    for j in range(9000):
+        t = 500 + j + (j // 3)                                    # distinct ms, a few gaps
+        v = _rand_value(rng)
+        assert s.AddCommand(t, v) == pyref.add_command(diff, state, t, v)
+    remote = {1: {"k2": "-15"}, 600: {"k2": "-11"}, 20_000: {"k3": "x"}}
+    for t, v in remote.items():
+        s.RemoteDiff.Put(t, v)
+    s.merge()
+    diff, state = pyref.merge(diff, remote)
+    assert s.CurrentState == state
+    assert s.DiffSignature == _sig(diff)
+    s.close()

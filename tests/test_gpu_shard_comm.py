@@ -84,3 +84,85 @@ def test_init_rank_single_process(eng):
         np.testing.assert_array_equal(as_u64(out[0]), oracle.gcounter_fold(as_u64(a).reshape(rows, nodes)))
     finally:
         c.close()
+
+
+# ---------------------------------------------------------------- one-call sharded RefMerge
+def _check_refmerge_vs_oracle(h, out):
+    from refmerge_util import assert_batch_matches_oracle
+    assert_batch_matches_oracle(h, out)
+
+
+@pytest.mark.parametrize("replicas,entries", [(48, 3000), (5, 10_000), (1, 1)])
+def test_comm_refmerge_matches_oracle(comm, eng, replicas, entries):
+    """crdt_shard_refmerge through a 1-device ncclCommInitAll communicator:
+    the whole protocol (max(L) all-reduce, local merge, accumulator
+    all-reduces, finalize) in one C-ABI call == oc_refmerge per replica."""
+    from crdt_amd import refmerge
+    h = synth.refmerge_packed(61 + replicas, replicas, entries)
+    d = refmerge.to_device(h, "cuda:0")
+    torch.cuda.synchronize()
+    out = comm.refmerge([eng], [d])[0]
+    comm.sync()
+    _check_refmerge_vs_oracle(h, out)
+
+
+def test_init_rank_refmerge_and_local_sets(eng):
+    """The same calls through ncclCommInitRank (nranks = 1) on the engine's
+    own context and stream: crdt_shard_refmerge == oracle, and the
+    distributed set merge == the plain merge's oracle."""
+    from crdt_amd import refmerge
+    c = shard.Comm.init_rank(eng)
+    try:
+        h = synth.refmerge_packed(71, 32, 4000)
+        d = refmerge.to_device(h, eng.device)
+        out = c.refmerge([eng], [d])[0]
+        eng.sync()
+        _check_refmerge_vs_oracle(h, out)
+        sa = synth.sort_tuples_np(*synth.set_tuples(72, 0, 30_000, 20_000))
+        sb = synth.sort_tuples_np(*synth.set_tuples(72, 1, 25_000, 20_000))
+        A, B = TupleSet.from_numpy(*sa, eng.device), TupleSet.from_numpy(*sb, eng.device)
+        from crdt_amd import _lib
+        for lww in (True, False):
+            _lib.call("crdt_set_option", b"shard.exchange_always", 1)
+            try:
+                got = c.set_merge_local([A], [B], lww=lww)[0].to_numpy()
+            finally:
+                _lib.call("crdt_set_option", b"shard.exchange_always", 0)
+            exp = (oracle.lww_merge if lww else oracle.orset_merge)(sa, sb)
+            for g, e in zip(got, exp):
+                np.testing.assert_array_equal(g, e)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("lww", [True, False])
+@pytest.mark.parametrize("gather", [True, False])
+@pytest.mark.parametrize("na,nb", [(200_000, 180_000), (0, 5000), (7, 0), (0, 0)])
+@pytest.mark.parametrize("exchange", [0, 1])
+def test_comm_set_merge_local_matches_oracle(comm, lww, gather, na, nb, exchange):
+    """crdt_shard_{lww,orset}_merge_local on a 1-member communicator, with the
+    one-rank shortcut and (shard.exchange_always) through the whole protocol:
+    sample block, splitters, count matrix, the all-to-all (a self send), the
+    tree of merges and the all-gather -- == the oracle's merge."""
+    from crdt_amd import _lib
+    sa = synth.sort_tuples_np(*synth.set_tuples(91, 0, na, 50_000))
+    sb = synth.sort_tuples_np(*synth.set_tuples(91, 1, nb, 50_000))
+    A, B = TupleSet.from_numpy(*sa, "cuda:0"), TupleSet.from_numpy(*sb, "cuda:0")
+    torch.cuda.synchronize()
+    _lib.call("crdt_set_option", b"shard.exchange_always", exchange)
+    try:
+        got = comm.set_merge_local([A], [B], lww=lww, gather=gather)[0].to_numpy()
+    finally:
+        _lib.call("crdt_set_option", b"shard.exchange_always", 0)
+    exp = (oracle.lww_merge if lww else oracle.orset_merge)(sa, sb)
+    for g, e in zip(got, exp):
+        np.testing.assert_array_equal(g, e)
+
+
+def test_comm_alltoallv_single_rank_copies(comm):
+    x = torch.arange(1000, dtype=torch.int64, device="cuda:0")
+    y = torch.zeros(1000, dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    comm.alltoallv([x], [[1000]], [y], [[1000]], 8)
+    comm.sync()
+    assert torch.equal(x, y)

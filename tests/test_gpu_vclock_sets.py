@@ -152,22 +152,44 @@ def test_sets_unaligned_views(eng, off_a, off_b):
             np.testing.assert_array_equal(g, e, err_msg=f"{fn.__name__}.{f}")
 
 
-@pytest.mark.parametrize("knobs", [9, 5])
-def test_sets_alternative_kernels(eng, knobs):
-    """The non-default set-merge forms (sets.knobs): 9 = the two-pass write
-    passes and the LWW count pass with register staging instead of LDS-DMA, 5 = round 1's persistent
-    look-back kernel; same outputs as the oracle on long runs, tile edges and
-    views off a 16-byte boundary."""
+@pytest.mark.parametrize("chunk,streams", [(0, 1), (1, 2), (3, 1), (7, 2), (64, 2)])
+def test_sets_chunked_schedules(eng, chunk, streams):
+    """The count / write passes over chunks of tiles (sets.lww_chunk,
+    sets.or_chunk; 0 = one chunk) on one stream or with the counts on the
+    context's aux stream (sets.streams = 2): chunk edges inside key runs,
+    tile edges, unaligned views; == the oracle."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"sets.knobs", knobs)
+    for name, v in ((b"sets.lww_chunk", chunk), (b"sets.or_chunk", chunk), (b"sets.streams", streams)):
+        _lib.call("crdt_set_option", name, v)
     try:
         _check(eng, *_sets(77, 100_000, 100_000, 50_000))
         _check(eng, *_sets(78, 4097, 4095, 1000))
+        _check(eng, *_sets(79, 40_000, 1, 100))                 # long key runs across chunk edges
         test_sets_long_runs_cross_tiles(eng)
         test_sets_unaligned_views(eng, 3, 5)
         assert eng.device_status(clear=True) == 0
     finally:
-        _lib.call("crdt_set_option", b"sets.knobs", 1)
+        for name, v in ((b"sets.lww_chunk", 0), (b"sets.or_chunk", 0), (b"sets.streams", 1)):
+            _lib.call("crdt_set_option", name, v)
+
+
+def test_sets_inconsistent_bitmaps_raise_range(eng):
+    """fail.zero_bits: the merge bitmaps zeroed between the count and write
+    passes (the GPU fault of DESIGN.md §5.4's timing build): every write-pass
+    workgroup finds them inconsistent with its tile and raises CRDT_DEV_RANGE
+    instead of staging a run past the end of an input; the next merge is
+    exact again."""
+    from crdt_amd import _lib
+    from crdt_amd._lib import CrdtLibraryError
+    sa, sb = _sets(81, 50_000, 30_000, 20_000)
+    A = TupleSet.from_numpy(*sa, eng.device)
+    B = TupleSet.from_numpy(*sb, eng.device)
+    for fn in (eng.lww_merge, eng.orset_merge):
+        _lib.call("crdt_set_option", b"fail.zero_bits", 1)
+        with pytest.raises(CrdtLibraryError, match="0x2"):
+            fn(A, B)
+        assert eng.device_status(clear=True) == 0
+    _check(eng, sa, sb)
 
 
 @pytest.mark.parametrize("parts", [2, 8, 16])
