@@ -17,6 +17,8 @@ int g_lww_chunk = 0;      // LWW tiles per chunk, 0 = one chunk (chunked schedul
 int g_or_chunk = 0;       // OR-Set tiles per chunk (likewise)
 int g_set_streams = 1;
 int g_shard_exchange_always = 0;
+int g_or_count_dma = 1;  // OR-Set count pass staged by LDS-DMA (sets.or_count_dma)
+int g_or_key_sort = 1;   // OR-Set D2: key-only sort + key runs ordered in LDS (0: the 7-pass tag sort)
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
@@ -285,6 +287,12 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "shard.exchange_always")) {   // tests: the keyed-set exchange protocol even on 1 rank
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_shard_exchange_always = (int)v;
+    } else if (!strcmp(name, "sets.or_count_dma")) { // OR-Set count pass: 1 LDS-DMA staging, 0 register staging
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_count_dma = (int)v;
+    } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 1 key-only sort + run sort, 0 full tag sort
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_key_sort = (int)v;
     } else if (!strcmp(name, "sets.lww_parts")) {    // LWW write-pass workgroups per 4096-item tile
         if (v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
         g_lww_parts = (int)v;

@@ -65,7 +65,9 @@ extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmer
 extern int g_lww_chunk;         // set merges: tiles per count / write chunk (sets.lww_chunk, sets.or_chunk;
 extern int g_or_chunk;          //   0 = one chunk), DESIGN.md §5.4
 extern int g_shard_exchange_always;   // keyed-set shard merges run the exchange protocol on 1 rank too (tests)
-extern int g_set_streams;       // set merges: 1 = one stream, 2 = counts beside writes (sets.streams)
+extern int g_set_streams;
+extern int g_or_count_dma;      // OR-Set count pass staging (sets.or_count_dma)
+extern int g_or_key_sort;       // OR-Set D2 key-only sort (sort.or_key_only)       // set merges: 1 = one stream, 2 = counts beside writes (sets.streams)
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests
 extern std::atomic<int> g_fail_zero_bits;  // fault injection ("fail.zero_bits"): bitmaps zeroed between passes
 bool take_fail_zero_bits();                // consumes one "fail.zero_bits" count

@@ -621,6 +621,99 @@ __global__ __launch_bounds__(NT) void k_or_count(crdt_tuples A, crdt_tuples B, s
     }
 }
 
+// k_or_count with the tile's key / ts / rep staged by LDS-DMA (each side's
+// run from the element before the tile, from its 16-byte aligned-down start:
+// no VGPR round trip; sets.or_count_dma).  Same merge, same bitmaps.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_or_count_dma(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                                     const uint64_t *__restrict__ split, uint32_t *__restrict__ tcnt,
+                                                     uint64_t *__restrict__ bits, uint64_t t0) {
+    constexpr int NI = OT / NT, LPW = 64 / NI, CAP = OT + 2;
+    __shared__ alignas(16) uint64_t sk[CAP + 8], st[CAP + 8];
+    __shared__ alignas(16) uint32_t sr[CAP + 16];
+    __shared__ uint32_t s_w[NT / 64];
+    const uint64_t t = t0 + blockIdx.x;
+    const LwwTile b = or_tile(split, t, na + nb);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+    // each side from the element before the tile (when there is one): element
+    // x of the tile's A run (x >= -1) is at field index oa_f + x
+    const uint32_t pa = b.i0 > 0 ? 1u : 0u, pb = b.j0 > 0 ? 1u : 0u;
+    uint32_t at = 0;
+    const int oa_k = dma_run<uint64_t, NT / 64>(A.key, b.i0 - pa, b.na + pa, sk, &at, wv, ln) + (int)pa;
+    const int ob_k = dma_run<uint64_t, NT / 64>(B.key, b.j0 - pb, b.nb + pb, sk, &at, wv, ln) + (int)pb;
+    at = 0;
+    const int oa_t = dma_run<uint64_t, NT / 64>(A.ts, b.i0 - pa, b.na + pa, st, &at, wv, ln) + (int)pa;
+    const int ob_t = dma_run<uint64_t, NT / 64>(B.ts, b.j0 - pb, b.nb + pb, st, &at, wv, ln) + (int)pb;
+    at = 0;
+    const int oa_r = dma_run<uint32_t, NT / 64>(A.rep, b.i0 - pa, b.na + pa, sr, &at, wv, ln) + (int)pa;
+    const int ob_r = dma_run<uint32_t, NT / 64>(B.rep, b.j0 - pb, b.nb + pb, sr, &at, wv, ln) + (int)pb;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
+    __syncthreads();
+#define OA(x) Tag{sk[oa_k + (int)(x)], st[oa_t + (int)(x)], sr[oa_r + (int)(x)]}
+#define OB(x) Tag{sk[ob_k + (int)(x)], st[ob_t + (int)(x)], sr[ob_r + (int)(x)]}
+    const uint32_t k0 = threadIdx.x * NI < b.n ? threadIdx.x * NI : b.n;
+    const uint32_t k1 = k0 + NI < b.n ? k0 + NI : b.n;
+    uint32_t isa = 0, emit = 0;
+    if (k0 < k1) {
+        uint32_t lo = k0 > b.nb ? k0 - b.nb : 0, hi = k0 < b.na ? k0 : b.na;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint64_t ka = sk[oa_k + (int)mid], kb = sk[ob_k + (int)(k0 - 1 - mid)];
+            const bool le = ka != kb ? ka < kb : tag_le(OA(mid), OB(k0 - 1 - mid));
+            if (le) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t ia = lo, ib = k0 - lo;
+        // the merged predecessor of item k0: the later of A[ia-1], B[ib-1]
+        // (A first on an equal tag), each possibly the element before the tile
+        const bool hpa = b.i0 + ia > 0, hpb = b.j0 + ib > 0;
+        const Tag qa = hpa ? OA((int)ia - 1) : Tag{0, 0, 0}, qb = hpb ? OB((int)ib - 1) : Tag{0, 0, 0};
+        bool has_prev = hpa || hpb;
+        Tag prev = tag_sel(hpa && hpb ? tag_le(qa, qb) : !hpa, qb, qa);
+        Tag ha = ia < b.na ? OA(ia) : Tag{0, 0, 0}, hb = ib < b.nb ? OB(ib) : Tag{0, 0, 0};
+        for (uint32_t i = 0; i < k1 - k0; ++i) {
+            const bool take_a = ia < b.na && (ib >= b.nb || tag_le(ha, hb));
+            const Tag cur = tag_sel(take_a, ha, hb);
+            if (!has_prev || !tag_eq(prev, cur)) emit |= 1u << i;
+            prev = cur;
+            has_prev = true;
+            if (take_a) {
+                isa |= 1u << i;
+                ++ia;
+                if (ia < b.na) ha = OA(ia);
+            } else {
+                ++ib;
+                if (ib < b.nb) hb = OB(ib);
+            }
+        }
+    }
+#undef OA
+#undef OB
+    const int lane = threadIdx.x & 63, sh = (lane % LPW) * NI;
+    uint64_t wl = (uint64_t)isa << sh, we = (uint64_t)emit << sh;
+#pragma unroll
+    for (int o = 1; o < LPW; o <<= 1) {
+        wl |= (uint64_t)__shfl_xor((unsigned long long)wl, o);
+        we |= (uint64_t)__shfl_xor((unsigned long long)we, o);
+    }
+    if (lane % LPW == 0) {
+        const uint32_t w = threadIdx.x / LPW;
+        bits[t * 2 * ONW + w] = wl;
+        bits[t * 2 * ONW + ONW + w] = we;
+    }
+    uint32_t x = (uint32_t)__popc(emit);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < NT / 64; ++k) tot += s_w[k];
+        tcnt[t] = tot;
+    }
+}
+
 // WH merge items per workgroup (a 1/P of a tile, P = OT / WH), WT threads
 template <int WH = OT, int WT = OWT>
 __global__ __launch_bounds__(WT) void k_or_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
@@ -852,7 +945,8 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
     // write-pass workgroups per tile (sets.or_parts): 1/P of a tile's items, 4 per thread
     const unsigned P = (unsigned)g_or_parts;
     auto cnt = [&](size_t t0, uint32_t nt, hipStream_t s) {
-        k_or_count<OCB><<<nt, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits, t0);
+        if (g_or_count_dma) k_or_count_dma<OCB><<<nt, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits, t0);
+        else k_or_count<OCB><<<nt, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits, t0);
     };
     auto scn = [&](size_t t0, uint32_t nt, uint64_t *c, hipStream_t s) {
         k_chunk_scan<<<1, 1024, 0, s>>>(tcnt, t0, nt, ic, c);

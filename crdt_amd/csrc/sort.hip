@@ -57,9 +57,12 @@ struct SortMinMax {              // one per minmax workgroup, reduced by k_sort_
 __device__ __forceinline__ uint32_t bitwidth(uint64_t x) { return x ? 64u - (uint32_t)__clzll((long long)x) : 0u; }
 
 // VEC: key / ts / rep 16-byte aligned -- four tuples per lane per step in
-// 16-byte loads (five in flight per lane instead of three 8/4-byte ones)
+// 16-byte loads, two steps in flight (ten 16-byte loads per lane).  One
+// launch covers both inputs of the fused merge: workgroups [0, g_a) read
+// `in`, the rest `in2`.
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, SortMinMax *mm) {
+__global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, crdt_tuples in2, size_t n2,
+                                                     unsigned g_a, SortMinMax *mm) {
     unsigned long long kmin = ~0ULL, kmax = 0, tmin = ~0ULL, tmax = 0, rmin = ~0ULL, rmax = 0;
     auto acc = [&](unsigned long long k, unsigned long long t, unsigned long long r) {
         kmin = k < kmin ? k : kmin;
@@ -69,12 +72,32 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, S
         rmin = r < rmin ? r : rmin;
         rmax = r > rmax ? r : rmax;
     };
+    const bool second = blockIdx.x >= g_a;
+    const crdt_tuples t_in = second ? in2 : in;
+    const size_t m = second ? n2 : n;
+    const size_t b0 = second ? blockIdx.x - g_a : blockIdx.x, gs = second ? gridDim.x - g_a : g_a;
     size_t i0 = 0;
     if constexpr (VEC) {
-        const size_t n4 = n / 4;
-        const ulonglong2 *K = (const ulonglong2 *)in.key, *T = (const ulonglong2 *)in.ts;
-        const uint4 *R = (const uint4 *)in.rep;
-        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+        const size_t n4 = m / 4;
+        const ulonglong2 *K = (const ulonglong2 *)t_in.key, *T = (const ulonglong2 *)t_in.ts;
+        const uint4 *R = (const uint4 *)t_in.rep;
+        const size_t stride = gs * 256;
+        size_t i = b0 * 256 + threadIdx.x;
+        for (; i + stride < n4; i += 2 * stride) {
+            const size_t j = i + stride;
+            const ulonglong2 k0 = K[2 * i], k1 = K[2 * i + 1], k2 = K[2 * j], k3 = K[2 * j + 1];
+            const ulonglong2 t0 = T[2 * i], t1 = T[2 * i + 1], t2 = T[2 * j], t3 = T[2 * j + 1];
+            const uint4 r = R[i], q = R[j];
+            acc(k0.x, t0.x, r.x);
+            acc(k0.y, t0.y, r.y);
+            acc(k1.x, t1.x, r.z);
+            acc(k1.y, t1.y, r.w);
+            acc(k2.x, t2.x, q.x);
+            acc(k2.y, t2.y, q.y);
+            acc(k3.x, t3.x, q.z);
+            acc(k3.y, t3.y, q.w);
+        }
+        if (i < n4) {
             const ulonglong2 k0 = K[2 * i], k1 = K[2 * i + 1];
             const ulonglong2 t0 = T[2 * i], t1 = T[2 * i + 1];
             const uint4 r = R[i];
@@ -85,15 +108,14 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, S
         }
         i0 = n4 * 4;
     }
-    for (size_t i = i0 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-        acc(in.key[i], in.ts[i], in.rep[i]);
-    for (int m = 32; m >= 1; m >>= 1) {
-        kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, m, 64));
-        kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, m, 64));
-        tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, m, 64));
-        tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, m, 64));
-        rmin = min(rmin, (unsigned long long)__shfl_xor(rmin, m, 64));
-        rmax = max(rmax, (unsigned long long)__shfl_xor(rmax, m, 64));
+    for (size_t i = i0 + b0 * 256 + threadIdx.x; i < m; i += gs * 256) acc(t_in.key[i], t_in.ts[i], t_in.rep[i]);
+    for (int w = 32; w >= 1; w >>= 1) {
+        kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, w, 64));
+        kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, w, 64));
+        tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, w, 64));
+        tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, w, 64));
+        rmin = min(rmin, (unsigned long long)__shfl_xor(rmin, w, 64));
+        rmax = max(rmax, (unsigned long long)__shfl_xor(rmax, w, 64));
     }
     // workgroup partials, reduced by k_sort_plan (atomics on six shared
     // addresses serialised: they took as long as the whole read)
@@ -118,13 +140,21 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, S
 
 constexpr unsigned MM_BLOCKS = 1024;   // minmax partials per input (at most)
 
-// returns the number of partials written to mm[0, g)
-static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, SortMinMax *mm) {
-    const bool vec = (((uintptr_t)in.key | (uintptr_t)in.ts | (uintptr_t)in.rep) & 15) == 0;
-    const unsigned g = std::min(MM_BLOCKS, grid_for(vec ? n / 4 + 1 : n, 256, (unsigned)ctx->num_cus * 4));
-    if (vec) k_sort_minmax<true><<<g, 256, 0, ctx->stream>>>(in, n, mm);
-    else k_sort_minmax<false><<<g, 256, 0, ctx->stream>>>(in, n, mm);
-    return g;
+// one launch over `in` (n) and `in2` (n2, may be 0); returns the number of
+// partials written to mm[0, g)
+static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &in2, size_t n2,
+                              SortMinMax *mm) {
+    auto aligned = [](const crdt_tuples &t) {
+        return (((uintptr_t)t.key | (uintptr_t)t.ts | (uintptr_t)t.rep) & 15) == 0;
+    };
+    const bool vec = (!n || aligned(in)) && (!n2 || aligned(in2));
+    auto blocks = [&](size_t m) {
+        return m ? std::min(MM_BLOCKS, grid_for(vec ? m / 8 + 1 : m, 256, (unsigned)ctx->num_cus * 2)) : 0u;
+    };
+    const unsigned ga = blocks(n), gb = blocks(n2);
+    if (vec) k_sort_minmax<true><<<ga + gb, 256, 0, ctx->stream>>>(in, n, in2, n2, ga, mm);
+    else k_sort_minmax<false><<<ga + gb, 256, 0, ctx->stream>>>(in, n, in2, n2, ga, mm);
+    return ga + gb;
 }
 
 // reduces the nmm minmax partials, then thread 0 sizes the composite
@@ -755,6 +785,202 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
     }
 }
 
+// ---------------------------------------------------------------- OR-Set: key runs put in tag order
+// The fused OR-Set merge sorts on the KEY's bits alone (3 passes instead of 7
+// in config D): each key's tuples come out contiguous, in input order.  The
+// dedup needs them in full (key, ts, rep, side, tomb) order, which is a sort
+// of every key run by itself -- runs are short (config D: 2.5 tuples per
+// key), so one pass over run-aligned tiles does it in LDS:
+//   tile t = [first run start >= t RT, first run start >= (t+1) RT);
+//   runs of <= kInsMax tuples: insertion-sorted by one thread each;
+//   longer runs that fit the tile: an in-place rank sort by the workgroup;
+//   a run longer than the LDS tile (adversarial data: many copies of one key):
+//   RCAP-chunks bitonic-sorted in LDS, then merged pairwise through `scratch`.
+constexpr int RT = 2048;                 // nominal tile (composites)
+constexpr int RCAP = 4096;               // LDS capacity of a run-aligned tile
+constexpr int RB = 256;                  // threads
+constexpr uint32_t kInsMax = 32;         // runs up to this length: one thread's insertion sort
+
+// first run start at or after p (keys = composite >> ks): galloping, then binary search
+__device__ __forceinline__ size_t run_start_from(const uint64_t *__restrict__ c, size_t n, size_t p, uint32_t ks) {
+    if (p == 0 || p >= n) return p < n ? p : n;
+    const uint64_t k = c[p - 1] >> ks;
+    if ((c[p] >> ks) != k) return p;
+    size_t lo = p, step = 1, hi = p;         // c[lo] has key k
+    for (;;) {
+        hi = lo + step;
+        if (hi >= n || (c[hi] >> ks) != k) break;
+        lo = hi;
+        step <<= 1;
+    }
+    if (hi > n) hi = n;
+    while (hi - lo > 1) {                    // c[lo] == k, c[hi] != k (or hi == n)
+        const size_t mid = lo + (hi - lo) / 2;
+        if ((c[mid] >> ks) == k) lo = mid;
+        else hi = mid;
+    }
+    return hi;
+}
+
+// in-place rank sort of s[r0, r0 + L) (L <= RCAP) by the workgroup
+__device__ void lds_rank_sort(uint64_t *s, uint32_t r0, uint32_t L) {
+    constexpr int PER = RCAP / RB;
+    uint64_t v[PER];
+    uint32_t rk[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = threadIdx.x + q * RB;
+        v[q] = i < L ? s[r0 + i] : 0;
+        rk[q] = 0;
+    }
+    for (uint32_t j = 0; j < L; ++j) {
+        const uint64_t x = s[r0 + j];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t i = threadIdx.x + q * RB;
+            rk[q] += (x < v[q] || (x == v[q] && j < i)) ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = threadIdx.x + q * RB;
+        if (i < L) s[r0 + rk[q]] = v[q];
+    }
+    __syncthreads();
+}
+
+// bitonic sort of s[0, m) in LDS, m a power of two <= RCAP
+__device__ void lds_bitonic(uint64_t *s, uint32_t m) {
+    for (uint32_t k = 2; k <= m; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < m; i += RB) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = s[i], b = s[l];
+                    if ((a > b) == ((i & k) == 0)) {
+                        s[i] = b;
+                        s[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// sort x[0, L) (L > RCAP) by the workgroup: RCAP chunks in LDS, then merges via tmp
+__device__ void long_run_sort(uint64_t *__restrict__ x, size_t L, uint64_t *__restrict__ tmp, uint64_t *s) {
+    for (size_t c0 = 0; c0 < L; c0 += RCAP) {
+        const uint32_t m = (uint32_t)(L - c0 < (size_t)RCAP ? L - c0 : (size_t)RCAP);
+        uint32_t m2 = 1;
+        while (m2 < m) m2 <<= 1;
+        for (uint32_t i = threadIdx.x; i < m2; i += RB) s[i] = i < m ? x[c0 + i] : ~0ULL;
+        __syncthreads();
+        lds_bitonic(s, m2);
+        for (uint32_t i = threadIdx.x; i < m; i += RB) x[c0 + i] = s[i];
+        __syncthreads();
+    }
+    uint64_t *src = x, *dst = tmp;
+    for (size_t w = RCAP; w < L; w <<= 1) {
+        for (size_t lo = 0; lo < L; lo += 2 * w) {
+            const size_t mid = lo + w < L ? lo + w : L, hi = lo + 2 * w < L ? lo + 2 * w : L;
+            const size_t na = mid - lo, nb = hi - mid, tot = na + nb;
+            const size_t per = (tot + RB - 1) / RB;
+            const size_t d0 = (size_t)threadIdx.x * per < tot ? (size_t)threadIdx.x * per : tot;
+            const size_t d1 = d0 + per < tot ? d0 + per : tot;
+            if (d0 < d1) {
+                size_t a_lo = d0 > nb ? d0 - nb : 0, a_hi = d0 < na ? d0 : na;   // merge path at d0
+                while (a_lo < a_hi) {
+                    const size_t am = (a_lo + a_hi) >> 1;
+                    if (src[lo + am] <= src[mid + (d0 - 1 - am)]) a_lo = am + 1;
+                    else a_hi = am;
+                }
+                size_t ia = a_lo, ib = d0 - a_lo;
+                for (size_t d = d0; d < d1; ++d) {
+                    const bool ta = ia < na && (ib >= nb || src[lo + ia] <= src[mid + ib]);
+                    dst[lo + d] = ta ? src[lo + ia++] : src[mid + ib++];
+                }
+            }
+        }
+        __syncthreads();
+        uint64_t *t = src;
+        src = dst;
+        dst = t;
+    }
+    if (src != x) {
+        for (size_t i = threadIdx.x; i < L; i += RB) x[i] = src[i];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(RB) void k_run_sort(uint64_t *__restrict__ c, size_t n,
+                                                  const SortPlan *__restrict__ plan_, uint64_t *__restrict__ scratch) {
+    __shared__ uint64_t s[RCAP];
+    __shared__ size_t s_rng[2];
+    __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig;
+    const SortPlan p = *plan_;
+    const uint32_t ks = p.s0;                            // the key's bits start here (single-word composites)
+    const size_t t = blockIdx.x;
+    if (threadIdx.x < 2) {
+        const size_t a = (t + threadIdx.x) * (size_t)RT;
+        s_rng[threadIdx.x] = run_start_from(c, n, a < n ? a : n, ks);
+    }
+    if (threadIdx.x == 0) s_nbig = 0;
+    __syncthreads();
+    const size_t start = s_rng[0], end = s_rng[1];
+    if (end <= start) return;
+    const size_t len = end - start;
+    if (len > (size_t)RCAP) {                            // holds a run longer than the tile: run by run
+        for (size_t cur = start; cur < end;) {
+            const size_t re = run_start_from(c, n, cur + 1, ks);
+            const size_t L = re - cur;
+            if (L > (size_t)RCAP) {
+                long_run_sort(c + cur, L, scratch + cur, s);
+            } else if (L > 1) {
+                for (uint32_t i = threadIdx.x; i < L; i += RB) s[i] = c[cur + i];
+                __syncthreads();
+                lds_rank_sort(s, 0, (uint32_t)L);
+                for (uint32_t i = threadIdx.x; i < L; i += RB) c[cur + i] = s[i];
+                __syncthreads();
+            }
+            cur = re;
+        }
+        return;
+    }
+    const uint32_t m = (uint32_t)len;
+    for (uint32_t i = threadIdx.x; i < m; i += RB) s[i] = c[start + i];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += RB) {      // run starts: short runs sorted in place
+        const uint64_t k = s[i] >> ks;
+        if (i > 0 && (s[i - 1] >> ks) == k) continue;
+        uint32_t e = i + 1;
+        while (e < m && (s[e] >> ks) == k && e - i <= kInsMax) ++e;
+        if (e - i > kInsMax) {                           // a longer run: the workgroup sorts it below
+            s_big[atomicAdd(&s_nbig, 1u)] = i;
+            continue;
+        }
+        for (uint32_t a = i + 1; a < e; ++a) {           // insertion sort of s[i, e)
+            const uint64_t x = s[a];
+            uint32_t b = a;
+            while (b > i && s[b - 1] > x) {
+                s[b] = s[b - 1];
+                --b;
+            }
+            s[b] = x;
+        }
+    }
+    __syncthreads();
+    const uint32_t nbig = s_nbig;
+    for (uint32_t q = 0; q < nbig; ++q) {
+        const uint32_t r0 = s_big[q];
+        const uint64_t k = s[r0] >> ks;
+        uint32_t e = r0 + 1;
+        while (e < m && (s[e] >> ks) == k) ++e;          // (every thread: the same answer)
+        lds_rank_sort(s, r0, e - r0);
+    }
+    for (uint32_t i = threadIdx.x; i < m; i += RB) c[start + i] = s[i];
+}
+
 template <int MODE, int WORDS>
 static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPlan *plan, uint32_t *cnt,
                        uint32_t *loc, uint32_t *tot, const crdt_tuples &out, uint64_t *out_count) {
@@ -796,9 +1022,8 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint32_t *loc = w.take<uint32_t>(ncnt);
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
-    unsigned nmm = na ? launch_minmax(ctx, A, na, mm) : 0;
-    if (nb) nmm += launch_minmax(ctx, B, nb, mm + nmm);
-    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, MODE == DD_LWW ? 1u : 0u);
+    const unsigned nmm = launch_minmax(ctx, A, na, B, nb, mm);
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, g_or_key_sort || MODE == DD_LWW ? 1u : 0u);
     SortPlan h;
     hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -806,6 +1031,11 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint64_t *sorted = nullptr;
     if (h.words == 1) {
         rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
+        if (!rc && MODE == DD_OR && h.s0) {               // key-only sort: each key run into tag order
+            uint64_t *scratch = sorted == bufs ? bufs + n : bufs;
+            k_run_sort<<<(unsigned)((n + RT - 1) / RT), RB, 0, s>>>(sorted, n, plan, scratch);
+            rc = check_launch(ctx);
+        }
         return rc ? rc : dedup_words<MODE, 1>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
     }
     if (h.words == 2) {
@@ -850,7 +1080,7 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
     const hipStream_t s = ctx->stream;
-    const unsigned nmm = launch_minmax(ctx, *in, n, mm);
+    const unsigned nmm = launch_minmax(ctx, *in, n, crdt_tuples{nullptr, nullptr, nullptr, nullptr}, 0, mm);
     k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 0, crdt_tuples{nullptr, nullptr, nullptr, nullptr}, n);
     // the pass count and composite width decide the launches: one small read-back
     SortPlan h;

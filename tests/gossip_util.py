@@ -105,7 +105,12 @@ def _local_writes(rng, diffs):
             "kv_key": np.array(kk, np.uint32), "kv_val": np.array(kv, np.uint32)}
 
 
-def _host_round(diffs, peers):
-    pulled = [{t: dict(v) for t, v in diffs[q].items()} for q in peers]   # ToJSON -> map[string]string
-    res = [pyref.merge(d, r) for d, r in zip(diffs, pulled)]
+def _host_round(diffs, peers, states=None):
+    """One synchronous round on pyref: replica i pulls diffs[peers[i]] (its
+    own Diff on a self-pull); peers[i] < 0 is a dead peer, the round is
+    skipped (main.go:234-239): Diff and CurrentState (from `states`, {} when
+    not given) stay as they were."""
+    pulled = [{t: dict(v) for t, v in diffs[q].items()} if q >= 0 else None for q in peers]   # ToJSON -> maps
+    res = [pyref.merge(d, r) if r is not None else (d, (states[i] if states else {}))
+           for i, (d, r) in enumerate(zip(diffs, pulled))]
     return [r[0] for r in res], [r[1] for r in res]

@@ -10,9 +10,10 @@ one GPU) and checks them against the oracle, not against another GPU path:
      all-reduced CurrentState must equal the oracle's, replica by replica
      (oracle/crdt_oracle.c oc_refmerge, main.go:35-100);
   2. gossip.sharded_round -- replicas partitioned over the ranks; every
-     round all-gathers the population's Diffs and each replica pulls its
-     peer; the rank's block must equal a host simulation of the reference's
-     rounds on oracle/pyref.py (main.go:226-258).
+     round each rank fetches only the Diffs its replicas pull (all-to-all-v)
+     and each replica pulls its peer (self-pulls and dead peers included);
+     the rank's block must equal a host simulation of the reference's rounds
+     on oracle/pyref.py (main.go:226-258).
 
 Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT.  Prints one line
 "RANK r OK <checks>" and exits 0, or raises.
@@ -71,10 +72,12 @@ def check_sharded_gossip(eng, rank, world):
     diffs = [_rand_diff(rng, 2_000 + 11 * i, int(rng.integers(3, 35))) for i in range(P)]
     b, e = shard.shard_range(P, world, rank)
     pop = gossip.Population(eng, _pack(diffs[b:e]), K, first=b)
-    for rnd in range(4):
-        peers = gossip.random_peers(rng, P, 0, P)
+    states = [{} for _ in range(P)]
+    for rnd in range(5):
+        # odd rounds draw like the reference: self-pulls and dead peers (-1)
+        peers = gossip.random_peers(rng, P, 0, P) if rnd % 2 == 0 else gossip.reference_peers(rng, P, 0, P)
         gossip.sharded_round(pop, peers)
-        diffs, states = _host_round(diffs, peers)
+        diffs, states = _host_round(diffs, peers, states)
         _same_diffs(_unpack(pop), diffs[b:e])
         assert _state(pop) == states[b:e], f"round {rnd}: state"
         if rnd == 1:                                     # local writes between rounds (main.go:187)

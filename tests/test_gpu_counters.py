@@ -126,3 +126,41 @@ def test_stream_peak_kernels(eng):
         eng.stream_read(src, sink, unroll, 1)
         x = np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint64))
         assert x == np.bitwise_xor.reduce(src.cpu().numpy().view(np.uint64))
+
+
+def test_ctx_set_stream_orders_work_across_streams(eng):
+    """crdt_ctx_set_stream: work queued on the old stream
+    finishes before the new stream's work touches its outputs -- a 512-MB
+    join on stream 1, then (no host sync) the fold of its output on stream 2
+    == the oracle; and the context's workspace is not freed under a set
+    merge still running on the old stream."""
+    from crdt_amd import synth
+    from crdt_amd.engine import TupleSet
+    rows, nodes = 1_000_000, 64
+    a = eng.synth_counters(77, 1, rows, nodes)
+    b = eng.synth_counters(77, 2, rows, nodes)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = torch.empty_like(a)
+    with torch.cuda.stream(s1):
+        eng.gcounter_join(a, b, out=out)
+    with torch.cuda.stream(s2):
+        fold = eng.gcounter_fold(out)          # the context switches to s2 on this call
+    torch.cuda.synchronize()
+    exp = oracle.gcounter_fold(np.maximum(as_u64(a).reshape(rows, nodes), as_u64(b).reshape(rows, nodes)))
+    np.testing.assert_array_equal(as_u64(fold), exp)
+    # a set merge on s1, then a bigger one on s2 (the workspace grows: ws_reserve frees the old one)
+    sa = synth.sort_tuples_np(*synth.set_tuples(3, 0, 200_000, 100_000))
+    sb = synth.sort_tuples_np(*synth.set_tuples(3, 1, 200_000, 100_000))
+    A, B = TupleSet.from_numpy(*sa, eng.device), TupleSet.from_numpy(*sb, eng.device)
+    big_a = eng.synth_set_tuples(4, 0, 3_000_000, 2_000_000)
+    big_b = eng.synth_set_tuples(4, 1, 3_000_000, 2_000_000)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        small, _ = eng.lww_merge(A, B, trim=False)
+    with torch.cuda.stream(s2):
+        eng.lww_merge(big_a, big_b, trim=False)
+    torch.cuda.synchronize()
+    got = small.slice(len(oracle.lww_merge(sa, sb)[0])).to_numpy()
+    for g, e in zip(got, oracle.lww_merge(sa, sb)):
+        np.testing.assert_array_equal(g, e)

@@ -57,3 +57,47 @@ def test_random_peers_never_self():
     for _ in range(50):
         p = gossip.random_peers(rng, 9, 0, 9)
         assert np.all(p != np.arange(9)) and np.all((p >= 0) & (p < 9))
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_reference_friend_list_rounds(eng, seed):
+    """Peers drawn like the reference (main.go:219-222, :230): a friend list
+    holding every replica -- itself included -- and as many dead ports.  A
+    self-pull still merges and rebuilds CurrentState from the remote entries
+    (main.go:76), dropping what local writes applied to it; a dead pick skips
+    the round (main.go:234-239) and keeps the local writes' state.  Local
+    writes go through the device AddCommand (Population.apply_local) between
+    rounds.  == the pyref simulation."""
+    from oracle import pyref
+    from test_gpu_local_apply import _cmd_block
+    from gossip_util import KEYS, STRS
+    rng = np.random.default_rng(seed)
+    P = 8
+    diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 30))) for i in range(P)]
+    pop = gossip.Population(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    saw_self = saw_dead = False
+    for rnd in range(6):
+        cmds, exp = [], []
+        for i in range(P):
+            t0 = max(diffs[i]) if diffs[i] else 1_000
+            mine = [(t0 + int(rng.integers(1, 6)), {KEYS[int(rng.integers(0, K))]: STRS[int(rng.integers(0, 10))]})
+                    for _ in range(int(rng.integers(0, 3)))]
+            exp += [pyref.add_command(diffs[i], states[i], t, d) for t, d in mine]
+            cmds.append(mine)
+        np.testing.assert_array_equal(pop.apply_local(_cmd_block(cmds)), exp)
+        peers = gossip.reference_peers(rng, P, 0, P)
+        saw_self |= bool(np.any(peers == np.arange(P)))
+        saw_dead |= bool(np.any(peers < 0))
+        pop.round(peers)
+        diffs, states = _host_round(diffs, peers, states)
+        _same_diffs(_unpack(pop), diffs)
+        assert _state(pop) == states, f"round {rnd}"
+    assert saw_self and saw_dead
+
+
+def test_reference_peers_distribution():
+    rng = np.random.default_rng(1)
+    d = np.concatenate([gossip.reference_peers(rng, 5, 0, 5) for _ in range(2000)])
+    assert d.min() == -1 and d.max() == 4
+    assert 0.45 < np.mean(d < 0) < 0.55                 # 5 of the 10 friends are dead (main.go:219-222)

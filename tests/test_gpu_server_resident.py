@@ -131,3 +131,36 @@ def test_resident_server_many_queued_writes(eng):
     assert s.CurrentState == state
     assert s.DiffSignature == _sig(diff)
     s.close()
+
+
+@pytest.mark.parametrize("wire", ["json", "bin"])
+def test_self_pull_round_trip(eng, wire):
+    """A server that pulls ITSELF (the reference's friend list holds its own
+    port, main.go:219-222, :230): its Diff -- local *Command entries included
+    -- goes out through Gossip (main.go:159), comes back as remote maps
+    (main.go:245-256) and merges (main.go:257).  Nothing is inserted (every
+    ts is already local, local wins, main.go:54-65) and CurrentState is
+    rebuilt from the remote-origin entries only (main.go:76-80), dropping the
+    local writes' direct applies.  == pyref, twice (resident on the second)."""
+    rng = np.random.default_rng(9)
+    s = Server(eng, 8080)
+    diff, state = {}, {}
+    for t in range(100, 160, 3):
+        v = _rand_value(rng)
+        if rng.random() < 0.5:
+            s.Diff.Put(t, v)
+            diff[t] = dict(v)
+        else:
+            assert s.AddCommand(t, v) == pyref.add_command(diff, state, t, v)
+    for _ in range(2):
+        st, body = s.Gossip() if wire == "json" else s.GossipBinary()
+        assert st == 200
+        assert (s.IngestGossip(body) if wire == "json" else s.IngestBinary(body)) == 0
+        remote = {t: dict(v) for t, v in diff.items()}
+        s.merge()
+        diff, state = pyref.merge(diff, remote)
+        assert s.CurrentState == state
+        assert s.DiffSignature == _sig(diff)
+        assert s.AddCommand(200, {"k1": "-13"}) == pyref.add_command(diff, state, 200, {"k1": "-13"})
+        assert s.CurrentState == state
+    s.close()

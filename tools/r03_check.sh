@@ -6,6 +6,5 @@ timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_server_errors.py t
 rc=$?
 tail -5 gpurun_out/r03_tests.log
 if [ $rc -ne 0 ]; then grep -E "^E |Error|FAILED" gpurun_out/r03_tests.log | head -30; exit $rc; fi
-shift 0
-[ $# -gt 0 ] && bash tools/chunk_ab.sh "$@"
-exit $?
+if [ $# -gt 0 ]; then bash tools/chunk_ab.sh "$@"; exit $?; fi
+exit 0
