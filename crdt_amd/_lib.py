@@ -19,7 +19,7 @@ import threading
 import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 # CRDT_AMD_LIB: another build of the same library (A/B timing of two builds
-# in one GPU call, tools/ab2.sh); never set for tests, smoke or bench lines.
+# in one GPU call, tools/ab_build.sh); never set for tests, smoke or bench lines.
 LIB_PATH = os.environ.get("CRDT_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcrdt_amd.so")
 
 CRDT_OK = 0
@@ -257,6 +257,8 @@ def lib() -> C.CDLL:
         except OSError as e:  # pragma: no cover - depends on the box
             raise CrdtLibraryError(f"cannot load {LIB_PATH}: {e}") from e
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("CRDT_AMD_LIB") and not hasattr(handle, name):
+                continue                      # an older A/B build lacks this round's entry points
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

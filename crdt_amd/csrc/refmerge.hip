@@ -547,8 +547,8 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
         const uint32_t lo = 64u * (uint32_t)lane;
         const uint64_t valid = lo >= n ? 0ull : (n - lo >= 64u ? ~0ull : (1ull << (n - lo)) - 1);
         const bool bad = ((word_l | word_e) & ~valid) != 0;
-        const uint32_t tot_l = (uint32_t)__shfl((int)(pre_l + (uint32_t)__popcll(word_l)), 63);
-        if (__any(bad) || tot_l != na) {
+        const uint32_t tot_l = (uint32_t)__builtin_amdgcn_readlane((int)(pre_l + (uint32_t)__popcll(word_l)), 63);
+        if (__ballot(bad) != 0 || tot_l != na) {
             if (threadIdx.x == 0 && part == 0) atomicOr(err, CRDT_DEV_RANGE);
             if (DELTA && threadIdx.x == 0) cand_n[t] = 0;
             return;

@@ -173,10 +173,13 @@ template <class T> static size_t vbytes(const std::vector<T> &v) { return v.size
 // host wait); at the merge's host synchronisation word 0 holds exactly this
 // merge's flags, and the earlier ones are put back beside them, so flags
 // raised by earlier calls stay for crdt_ctx_device_status.
+__global__ void k_status_mark(uint32_t *st) {
+    st[1] = st[0];
+    st[0] = 0;
+}
 static int status_mark(crdt_ctx *ctx) {
-    hipError_t e = hipMemcpyAsync(ctx->dev_status + 1, ctx->dev_status, 4, hipMemcpyDeviceToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(ctx->dev_status, 0, 4, ctx->stream);
-    return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    k_status_mark<<<1, 1, 0, ctx->stream>>>(ctx->dev_status);   // (one launch: a copy + a memset were two)
+    return check_launch(ctx);
 }
 static hipError_t status_fetch(crdt_ctx *ctx, uint32_t *two) {
     return hipMemcpyAsync(two, ctx->dev_status, 8, hipMemcpyDeviceToHost, ctx->stream);

@@ -72,8 +72,9 @@ __device__ __forceinline__ bool bitmaps_consistent(uint64_t word_a, uint64_t wor
     const uint32_t lo = 64u * (uint32_t)lane;
     const uint64_t valid = lane >= nw || lo >= n ? 0ull : (n - lo >= 64u ? ~0ull : (1ull << (n - lo)) - 1);
     const bool bad = ((word_a | word_e) & ~valid) != 0;
-    const uint32_t tot_a = (uint32_t)__shfl((int)(pre_a + (uint32_t)__popcll(word_a)), 63);
-    return !__any(bad) && tot_a == na;
+    // (readlane: scalar, no LDS round trip in front of the staging loads)
+    const uint32_t tot_a = (uint32_t)__builtin_amdgcn_readlane((int)(pre_a + (uint32_t)__popcll(word_a)), 63);
+    return __ballot(bad) == 0 && tot_a == na;
 }
 
 // ---------------------------------------------------------------- LWW by key runs

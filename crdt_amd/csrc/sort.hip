@@ -149,7 +149,7 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, co
     };
     const bool vec = (!n || aligned(in)) && (!n2 || aligned(in2));
     auto blocks = [&](size_t m) {
-        return m ? std::min(MM_BLOCKS, grid_for(vec ? m / 8 + 1 : m, 256, (unsigned)ctx->num_cus * 2)) : 0u;
+        return m ? std::min(MM_BLOCKS, grid_for(vec ? m / 8 + 1 : m, 256, (unsigned)ctx->num_cus * 4)) : 0u;
     };
     const unsigned ga = blocks(n), gb = blocks(n2);
     if (vec) k_sort_minmax<true><<<ga + gb, 256, 0, ctx->stream>>>(in, n, in2, n2, ga, mm);
@@ -751,7 +751,24 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         uint8_t tomb = tb[r] & 1u;
         CKey<WORDS> win = v[r];
         if (tb[r] & 2u) {
-            if constexpr (MODE == DD_LWW) {
+            if constexpr (MODE == DD_LWW && WORDS == 1) {
+                // one word (key-only sort, b0 = 2: side at bit 1, tomb at bit 0):
+                // the LWW winner is the max over the key's run of c ^ 3 -- the
+                // max (ts, rep), then side A (bit 1 inverted), then its least
+                // tomb (bit 0 inverted) -- so the backward walk is a plain
+                // 64-bit max; the tile's part from LDS, the rest from global memory
+                const uint32_t kb = p.b0 + p.br + p.bt;
+                const uint64_t key = v[r].w[0] >> kb;
+                uint64_t mx = v[r].w[0] ^ 3u;
+                for (size_t j = e; j > 0;) {
+                    --j;
+                    const uint64_t x = j >= base ? s_v[j - base] : c[j];
+                    if ((x >> kb) != key) break;
+                    mx = (x ^ 3u) > mx ? x ^ 3u : mx;
+                }
+                win.w[0] = mx ^ 3u;
+                tomb = (uint8_t)(win.w[0] & 1u);
+            } else if constexpr (MODE == DD_LWW) {
                 // the key's run backwards: the tile's part from LDS, the rest
                 // (a run reaching back past the tile) from global memory
                 const uint32_t kb = p.b0 + p.br + p.bt;
@@ -787,17 +804,26 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
 
 // ---------------------------------------------------------------- OR-Set: key runs put in tag order
 // The fused OR-Set merge sorts on the KEY's bits alone (3 passes instead of 7
-// in config D): each key's tuples come out contiguous, in input order.  The
-// dedup needs them in full (key, ts, rep, side, tomb) order, which is a sort
-// of every key run by itself -- runs are short (config D: 2.5 tuples per
-// key), so one pass over run-aligned tiles does it in LDS:
-//   tile t = [first run start >= t RT, first run start >= (t+1) RT);
-//   runs of <= kInsMax tuples: insertion-sorted by one thread each;
-//   longer runs that fit the tile: an in-place rank sort by the workgroup;
-//   a run longer than the LDS tile (adversarial data: many copies of one key):
-//   RCAP-chunks bitonic-sorted in LDS, then merged pairwise through `scratch`.
+// in config D): each key's tuples come out contiguous, in input order.  Its
+// dedup needs every key run in full (key, ts, rep, side, tomb) order -- a
+// sort of each run by itself; runs are short (config D: 2.5 tuples per key),
+// so the dedup's two passes work on RUN-ALIGNED tiles and sort the runs in
+// LDS themselves (no extra pass over HBM):
+//   k_run_bounds : tile t = [first run start >= t RT, first run start >=
+//                  (t+1) RT), one thread per boundary (galloping search);
+//   k_or_rdd_count: per tile, the runs sorted in LDS (runs of <= kInsMax
+//                  tuples: one thread's insertion sort; longer ones: the
+//                  workgroup's in-place rank sort), the distinct tags counted;
+//   k_sort_colscan of the counts;
+//   k_or_rdd_apply: the same sort, then the first copy of every tag emits at
+//                  its rank with the OR of its copies' tombs (a tag's copies
+//                  never leave the tile: it is run-aligned).
+// A run longer than the LDS tile (adversarial data: many copies of one key)
+// makes its tile take the global path: the count pass sorts it in place
+// (RCAP-chunks bitonic-sorted in LDS, then merged pairwise through a scratch
+// buffer) and both passes read it from HBM.
 constexpr int RT = 2048;                 // nominal tile (composites)
-constexpr int RCAP = 4096;               // LDS capacity of a run-aligned tile
+constexpr int RCAP = 3072;               // LDS capacity of a run-aligned tile
 constexpr int RB = 256;                  // threads
 constexpr uint32_t kInsMax = 32;         // runs up to this length: one thread's insertion sort
 
@@ -820,6 +846,14 @@ __device__ __forceinline__ size_t run_start_from(const uint64_t *__restrict__ c,
         else hi = mid;
     }
     return hi;
+}
+
+__global__ void k_run_bounds(const uint64_t *__restrict__ c, size_t n, const SortPlan *__restrict__ plan_,
+                             size_t ntiles, uint64_t *__restrict__ bounds) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t > ntiles) return;
+    const size_t a = t * (size_t)RT;
+    bounds[t] = run_start_from(c, n, a < n ? a : n, plan_->s0);
 }
 
 // in-place rank sort of s[r0, r0 + L) (L <= RCAP) by the workgroup
@@ -850,7 +884,41 @@ __device__ void lds_rank_sort(uint64_t *s, uint32_t r0, uint32_t L) {
     __syncthreads();
 }
 
-// bitonic sort of s[0, m) in LDS, m a power of two <= RCAP
+// sort every key run of s[0, m) (m <= RCAP, run-aligned) in place
+__device__ void lds_sort_runs(uint64_t *s, uint32_t m, uint32_t ks, uint32_t *s_big, uint32_t *s_nbig) {
+    if (threadIdx.x == 0) *s_nbig = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += RB) {      // run starts: short runs sorted in place
+        const uint64_t k = s[i] >> ks;
+        if (i > 0 && (s[i - 1] >> ks) == k) continue;
+        uint32_t e = i + 1;
+        while (e < m && (s[e] >> ks) == k && e - i <= kInsMax) ++e;
+        if (e - i > kInsMax) {                           // a longer run: the workgroup sorts it below
+            s_big[atomicAdd(s_nbig, 1u)] = i;
+            continue;
+        }
+        for (uint32_t a = i + 1; a < e; ++a) {           // insertion sort of s[i, e)
+            const uint64_t x = s[a];
+            uint32_t b = a;
+            while (b > i && s[b - 1] > x) {
+                s[b] = s[b - 1];
+                --b;
+            }
+            s[b] = x;
+        }
+    }
+    __syncthreads();
+    const uint32_t nbig = *s_nbig;
+    for (uint32_t q = 0; q < nbig; ++q) {
+        const uint32_t r0 = s_big[q];
+        const uint64_t k = s[r0] >> ks;
+        uint32_t e = r0 + 1;
+        while (e < m && (s[e] >> ks) == k) ++e;          // (every thread: the same answer)
+        lds_rank_sort(s, r0, e - r0);
+    }
+}
+
+// bitonic sort of s[0, m) in LDS, m a power of two <= 4096
 __device__ void lds_bitonic(uint64_t *s, uint32_t m) {
     for (uint32_t k = 2; k <= m; k <<= 1)
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -868,10 +936,11 @@ __device__ void lds_bitonic(uint64_t *s, uint32_t m) {
         }
 }
 
-// sort x[0, L) (L > RCAP) by the workgroup: RCAP chunks in LDS, then merges via tmp
+// sort x[0, L) by the workgroup: 2048-chunks in LDS, then merges through tmp
 __device__ void long_run_sort(uint64_t *__restrict__ x, size_t L, uint64_t *__restrict__ tmp, uint64_t *s) {
-    for (size_t c0 = 0; c0 < L; c0 += RCAP) {
-        const uint32_t m = (uint32_t)(L - c0 < (size_t)RCAP ? L - c0 : (size_t)RCAP);
+    constexpr size_t CH = 2048;               // power-of-two chunk (<= RCAP)
+    for (size_t c0 = 0; c0 < L; c0 += CH) {
+        const uint32_t m = (uint32_t)(L - c0 < CH ? L - c0 : CH);
         uint32_t m2 = 1;
         while (m2 < m) m2 <<= 1;
         for (uint32_t i = threadIdx.x; i < m2; i += RB) s[i] = i < m ? x[c0 + i] : ~0ULL;
@@ -881,7 +950,7 @@ __device__ void long_run_sort(uint64_t *__restrict__ x, size_t L, uint64_t *__re
         __syncthreads();
     }
     uint64_t *src = x, *dst = tmp;
-    for (size_t w = RCAP; w < L; w <<= 1) {
+    for (size_t w = CH; w < L; w <<= 1) {
         for (size_t lo = 0; lo < L; lo += 2 * w) {
             const size_t mid = lo + w < L ? lo + w : L, hi = lo + 2 * w < L ? lo + 2 * w : L;
             const size_t na = mid - lo, nb = hi - mid, tot = na + nb;
@@ -913,72 +982,130 @@ __device__ void long_run_sort(uint64_t *__restrict__ x, size_t L, uint64_t *__re
     }
 }
 
-__global__ __launch_bounds__(RB) void k_run_sort(uint64_t *__restrict__ c, size_t n,
-                                                  const SortPlan *__restrict__ plan_, uint64_t *__restrict__ scratch) {
+// the global path of a tile over RCAP: each of its runs sorted in place in c
+__device__ void sort_runs_global(uint64_t *__restrict__ c, size_t n, size_t start, size_t end, uint32_t ks,
+                                 uint64_t *__restrict__ scratch, uint64_t *s) {
+    for (size_t cur = start; cur < end;) {
+        const size_t re = run_start_from(c, n, cur + 1, ks);
+        const size_t L = re - cur;
+        if (L > (size_t)RCAP) {
+            long_run_sort(c + cur, L, scratch + cur, s);
+        } else if (L > 1) {
+            for (uint32_t i = threadIdx.x; i < L; i += RB) s[i] = c[cur + i];
+            __syncthreads();
+            lds_rank_sort(s, 0, (uint32_t)L);
+            for (uint32_t i = threadIdx.x; i < L; i += RB) c[cur + i] = s[i];
+            __syncthreads();
+        }
+        cur = re;
+    }
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *s_w) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < RB / 64; ++w) t += s_w[w];
+    return t;
+}
+
+__global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, size_t n,
+                                                      const SortPlan *__restrict__ plan_,
+                                                      const uint64_t *__restrict__ bounds,
+                                                      uint64_t *__restrict__ scratch, uint32_t *__restrict__ cnt) {
     __shared__ uint64_t s[RCAP];
-    __shared__ size_t s_rng[2];
-    __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig;
+    __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
-    const uint32_t ks = p.s0;                            // the key's bits start here (single-word composites)
-    const size_t t = blockIdx.x;
-    if (threadIdx.x < 2) {
-        const size_t a = (t + threadIdx.x) * (size_t)RT;
-        s_rng[threadIdx.x] = run_start_from(c, n, a < n ? a : n, ks);
+    const uint32_t ks = p.s0, tb = p.b0;                 // key bits from ks; tag bits from b0
+    const size_t t = blockIdx.x, start = bounds[t], end = bounds[t + 1];
+    const size_t len = end > start ? end - start : 0;
+    uint32_t m = 0;
+    if (len <= (size_t)RCAP) {
+        for (uint32_t i = threadIdx.x; i < len; i += RB) s[i] = c[start + i];
+        __syncthreads();
+        lds_sort_runs(s, (uint32_t)len, ks, s_big, &s_nbig);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < len; i += RB) m += (i == 0 || (s[i] >> tb) != (s[i - 1] >> tb)) ? 1u : 0u;
+    } else {
+        sort_runs_global(c, n, start, end, ks, scratch, s);
+        __threadfence();
+        __syncthreads();
+        for (size_t i = start + threadIdx.x; i < end; i += RB)
+            m += (i == start || (c[i] >> tb) != (c[i - 1] >> tb)) ? 1u : 0u;
     }
-    if (threadIdx.x == 0) s_nbig = 0;
-    __syncthreads();
-    const size_t start = s_rng[0], end = s_rng[1];
-    if (end <= start) return;
-    const size_t len = end - start;
-    if (len > (size_t)RCAP) {                            // holds a run longer than the tile: run by run
-        for (size_t cur = start; cur < end;) {
-            const size_t re = run_start_from(c, n, cur + 1, ks);
-            const size_t L = re - cur;
-            if (L > (size_t)RCAP) {
-                long_run_sort(c + cur, L, scratch + cur, s);
-            } else if (L > 1) {
-                for (uint32_t i = threadIdx.x; i < L; i += RB) s[i] = c[cur + i];
-                __syncthreads();
-                lds_rank_sort(s, 0, (uint32_t)L);
-                for (uint32_t i = threadIdx.x; i < L; i += RB) c[cur + i] = s[i];
-                __syncthreads();
+    const uint32_t tot = block_sum(m, s_w);
+    if (threadIdx.x == 0) cnt[t] = tot;
+}
+
+__global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict__ c, size_t n,
+                                                      const SortPlan *__restrict__ plan_,
+                                                      const uint64_t *__restrict__ bounds,
+                                                      const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
+                                                      crdt_tuples out, uint64_t *__restrict__ out_count) {
+    __shared__ uint64_t s[RCAP];
+    __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
+    const SortPlan p = *plan_;
+    const uint32_t ks = p.s0, tb = p.b0, sk = p.b0 + p.br + p.bt;
+    const size_t t = blockIdx.x, start = bounds[t], end = bounds[t + 1];
+    if (t == 0 && threadIdx.x == 0) *out_count = tot[0];
+    const size_t len = end > start ? end - start : 0;
+    if (len == 0) return;
+    const bool in_lds = len <= (size_t)RCAP;
+    if (in_lds) {
+        for (uint32_t i = threadIdx.x; i < len; i += RB) s[i] = c[start + i];
+        __syncthreads();
+        lds_sort_runs(s, (uint32_t)len, ks, s_big, &s_nbig);
+        __syncthreads();
+    }
+    auto at = [&](size_t i) -> uint64_t { return in_lds ? s[i] : c[start + i]; };
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    size_t base = loc[t];
+    for (size_t r0 = 0; r0 < len; r0 += RB) {
+        const size_t i = r0 + threadIdx.x;
+        const uint64_t x = i < len ? at(i) : 0;
+        const bool f = i < len && (i == 0 || (x >> tb) != (at(i - 1) >> tb));
+        const uint64_t em = __ballot(f);
+        __syncthreads();                                 // s_w of the previous round read
+        if (lane == 0) s_w[w] = (uint32_t)__popcll(em);
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int k = 0; k < RB / 64; ++k) {
+            before += k < w ? s_w[k] : 0u;
+            all += s_w[k];
+        }
+        if (f) {
+            uint32_t tomb = (uint32_t)(x & 1u);
+            for (size_t j = i + 1; j < len; ++j) {       // the tag's other copies (never past the tile)
+                const uint64_t y = at(j);
+                if ((y >> tb) != (x >> tb)) break;
+                tomb |= (uint32_t)(y & 1u);
             }
-            cur = re;
+            CKey<1> v;
+            v.w[0] = x;
+            const size_t o = base + before + (uint32_t)__popcll(em & ((1ULL << lane) - 1ULL));
+            out.key[o] = p.kmin + get_bits(v, sk, p.bk);
+            out.ts[o] = p.tmin + get_bits(v, p.b0 + p.br, p.bt);
+            out.rep[o] = (uint32_t)(p.rmin + get_bits(v, p.b0, p.br));
+            out.tomb[o] = (uint8_t)tomb;
         }
-        return;
+        base += all;
     }
-    const uint32_t m = (uint32_t)len;
-    for (uint32_t i = threadIdx.x; i < m; i += RB) s[i] = c[start + i];
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += RB) {      // run starts: short runs sorted in place
-        const uint64_t k = s[i] >> ks;
-        if (i > 0 && (s[i - 1] >> ks) == k) continue;
-        uint32_t e = i + 1;
-        while (e < m && (s[e] >> ks) == k && e - i <= kInsMax) ++e;
-        if (e - i > kInsMax) {                           // a longer run: the workgroup sorts it below
-            s_big[atomicAdd(&s_nbig, 1u)] = i;
-            continue;
-        }
-        for (uint32_t a = i + 1; a < e; ++a) {           // insertion sort of s[i, e)
-            const uint64_t x = s[a];
-            uint32_t b = a;
-            while (b > i && s[b - 1] > x) {
-                s[b] = s[b - 1];
-                --b;
-            }
-            s[b] = x;
-        }
-    }
-    __syncthreads();
-    const uint32_t nbig = s_nbig;
-    for (uint32_t q = 0; q < nbig; ++q) {
-        const uint32_t r0 = s_big[q];
-        const uint64_t k = s[r0] >> ks;
-        uint32_t e = r0 + 1;
-        while (e < m && (s[e] >> ks) == k) ++e;          // (every thread: the same answer)
-        lds_rank_sort(s, r0, e - r0);
-    }
-    for (uint32_t i = threadIdx.x; i < m; i += RB) c[start + i] = s[i];
+}
+
+static int or_run_dedup(crdt_ctx *ctx, uint64_t *c, size_t n, const SortPlan *plan, uint64_t *scratch,
+                        uint64_t *bounds, uint32_t *cnt, uint32_t *loc, uint32_t *tot, const crdt_tuples &out,
+                        uint64_t *out_count) {
+    const hipStream_t st = ctx->stream;
+    const size_t nt = (n + RT - 1) / RT;
+    k_run_bounds<<<(unsigned)((nt + 1 + 255) / 256), 256, 0, st>>>(c, n, plan, nt, bounds);
+    k_or_rdd_count<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, scratch, cnt);
+    k_sort_colscan<<<1, CSB, 0, st>>>(cnt, (uint32_t)nt, loc, tot);
+    k_or_rdd_apply<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, loc, tot, out, out_count);
+    return check_launch(ctx);
 }
 
 template <int MODE, int WORDS>
@@ -1031,11 +1158,9 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint64_t *sorted = nullptr;
     if (h.words == 1) {
         rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
-        if (!rc && MODE == DD_OR && h.s0) {               // key-only sort: each key run into tag order
-            uint64_t *scratch = sorted == bufs ? bufs + n : bufs;
-            k_run_sort<<<(unsigned)((n + RT - 1) / RT), RB, 0, s>>>(sorted, n, plan, scratch);
-            rc = check_launch(ctx);
-        }
+        if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup
+            return or_run_dedup(ctx, sorted, n, plan, sorted == bufs ? bufs + n : bufs, bufs + 2 * n, cnt, loc,
+                                tot, *out, out_count);
         return rc ? rc : dedup_words<MODE, 1>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
     }
     if (h.words == 2) {

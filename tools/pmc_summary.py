@@ -15,11 +15,15 @@ Reads gpurun_out/prof_<workload>/{trace,pmc_fetch,pmc_write} and
   * writes profiles/<round>_<workload>_pmc.json with the per-launch counters,
   * updates profiles/traffic.json[<workload>] (read by bench.py's roofline).
 
-HBM bytes per launch follow MI355X_MICROARCH.md §HBM / cdna_hip_programming.md
-§7 for gfx950: FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE counts HALF
-the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
-WRITE_SIZE is exact for 16 B/lane streaming stores.  Kernels with other
-access widths are flagged "uncalibrated".
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE
+and WRITE_SIZE are in KiB; FETCH_SIZE counts HALF the bytes of a coalesced
+read, so it is doubled; WRITE_SIZE is exact.  The guide calibrates 16 B/lane
+accesses only; round 3 calibrated every width the merge kernels use
+(tools/mb/pmc_cal.hip: 1, 2, 4, 8, 16 B/lane reads and LDS-DMA reads -> factor
+2.00; 2, 4, 8, 16 B/lane stores -> 1.00, 1 B/lane stores 0.99;
+profiles/r03/pmc_calibration.json), so one correction holds for the whole
+step.  Scattered single-element loads (merge-path probes) fetch whole lines:
+their traffic is real, not a counter artefact.
 """
 import csv
 import json
@@ -81,7 +85,8 @@ def main():
         "FETCH_SIZE_KiB_per_launch": fk, "WRITE_SIZE_KiB_per_launch": wk,
         "hbm_bytes_per_launch": int(round(hbm)), "bytes_per_launch_algorithmic": algo,
         "traffic_over_algorithmic": round(hbm / algo, 4),
-        "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE counts 1/2 of 16B/lane reads)",
+        "correction": ("hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE counts 1/2 of coalesced reads "
+                       "of every width the kernels use, WRITE_SIZE exact; profiles/r03/pmc_calibration.json)"),
         "rocprof_avg_duration_us": None if avg_ns is None else round(avg_ns / 1e3, 2),
         "bench_event_avg_launch_us": bench["roofline"]["avg_launch_us"],
         "config": bench["config"],
