@@ -274,6 +274,7 @@ struct PendGet {                   // bytes of pending reference j (key or value
 // and count the claims (ctr[0] keys, ctr[1] values).  kEmptyE slots: done.
 __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
                                                    const uint8_t *__restrict__ first, const uint32_t *__restrict__ flag0,
+                                                   uint32_t *__restrict__ cflag,
                                                    uint32_t key_cap,
                                                    uint64_t kv_base, uint32_t *__restrict__ kslot,
                                                    uint32_t *__restrict__ vslot, uint32_t *__restrict__ kv_key,
@@ -282,9 +283,9 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
     const BodyDesc d = c.bd[b];
     const uint8_t *region = c.data + d.data + 32 + 12 * d.ne + 8 * d.np;
     const uint64_t o0 = c.boff[d.q0];
-    // a body the earlier passes already rejected (flag0: the flags as they
-    // stood before this pass) claims no table entries: its strings never
-    // enter the persistent tables (the host decodes it)
+    // a body the earlier passes already rejected (flag0: their flags, which
+    // this pass only reads -- its own go to cflag) claims no table entries:
+    // its strings never enter the persistent tables (the host decodes it)
     const bool rejected = flag0[b] != 0;
     bool host = false, bad = false, full = false;
     uint32_t nk = 0, nv = 0;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
     uint32_t wfl = fl;
     for (int m = 32; m >= 1; m >>= 1) wfl |= __shfl_xor(wfl, m, 64);
     if ((threadIdx.x & 63) == 0) {
-        if (wfl) atomicOr(&c.flag[b], wfl);
+        if (wfl) atomicOr(&cflag[b], wfl);
         if (nk) atomicAdd(&ctr[0], (unsigned long long)nk);
         if (nv) atomicAdd(&ctr[1], (unsigned long long)nv);
     }
@@ -652,8 +653,7 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     if (rc) return rc;
     Carve w(ctx->ws);
     BodyDesc *d_bd = w.take<BodyDesc>(nb);
-    uint32_t *d_flag = w.take<uint32_t>(nb);
-    uint32_t *d_flag0 = w.take<uint32_t>(nb);
+    uint32_t *d_flag = w.take<uint32_t>(2 * nb);          // [0, nb): the other passes, [nb, 2nb): the claim pass
     uint32_t *cnt = w.take<uint32_t>(n_e + 1);
     uint64_t *pre = w.take<uint64_t>(n_e + 1);
     uint32_t *klen = w.take<uint32_t>(n_p + 1);
@@ -669,7 +669,7 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     unsigned long long *ctr = w.take<unsigned long long>(8);
     void *tmp = w.take<char>(scan_lb_tmp_bytes(std::max(n_p, n_e)));
     e = hipMemcpyAsync(d_bd, bd.data(), nb * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, nb * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, nb * 8, s);
     if (e == hipSuccess) e = hipMemsetAsync(first, 0, n_p + 1, s);
     if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, 64, s);
     if (e == hipSuccess) e = hipMemcpyAsync(out->r_off, r_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s);
@@ -707,18 +707,16 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
     TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
-        e = hipMemcpyAsync(d_flag0, d_flag, nb * 4, hipMemcpyDeviceToDevice, s);
-        if (e != hipSuccess) return hip_fail(ctx, e);
-        k_dec_claim<<<gp, 256, 0, s>>>(c, kt, vt, first, d_flag0, in->key_cap, in->kv_base, kslot, vslot,
+        k_dec_claim<<<gp, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, in->key_cap, in->kv_base, kslot, vslot,
                                        out->kv_key, out->kv_val, ctr);
         rc = check_launch(ctx);
         if (rc) return rc;
     }
     // claims and flags to the host: the id passes run only when new strings arrived
     uint64_t h_ctr[8];
-    std::vector<uint32_t> flags(nb);
+    std::vector<uint32_t> flags(2 * nb);
     e = hipMemcpyAsync(h_ctr, ctr, 64, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     uint64_t new_k = 0, new_kb = 0, new_v = 0, new_vb = 0;
@@ -752,13 +750,13 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
             e = hipMemcpyAsync(&sizes[2], vrank + n_p, 8, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipMemcpyAsync(&sizes[3], vboff + n_p, 8, hipMemcpyDeviceToHost, s);
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 8, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);          // the id pass may flag a body too
         if (e != hipSuccess) return hip_fail(ctx, e);
         new_k = sizes[0], new_kb = sizes[1], new_v = sizes[2], new_vb = sizes[3];
     }
     for (uint32_t b = 0; b < nb; ++b) {
-        body_status[b] |= flags[b];
+        body_status[b] |= flags[b] | flags[nb + b];
         if (body_status[b] & kBodyMalformed) body_status[b] = kBodyMalformed;   // nothing else applies then
     }
     rc = CRDT_OK;

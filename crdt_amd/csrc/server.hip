@@ -168,27 +168,35 @@ struct Batch {
 template <class T> static size_t vbytes(const std::vector<T> &v) { return v.size() * sizeof(T); }
 
 // merge() for a set of servers whose locks the caller holds.
-// Device failure flags raised by the passes of one merge: before the passes
-// the status word moves to word 1 and word 0 starts clear (stream-ordered, no
-// host wait); at the merge's host synchronisation word 0 holds exactly this
-// merge's flags, and the earlier ones are put back beside them, so flags
-// raised by earlier calls stay for crdt_ctx_device_status.
-__global__ void k_status_mark(uint32_t *st) {
-    st[1] = st[0];
-    st[0] = 0;
-}
-static int status_mark(crdt_ctx *ctx) {
-    k_status_mark<<<1, 1, 0, ctx->stream>>>(ctx->dev_status);   // (one launch: a copy + a memset were two)
-    return check_launch(ctx);
-}
-static hipError_t status_fetch(crdt_ctx *ctx, uint32_t *two) {
-    return hipMemcpyAsync(two, ctx->dev_status, 8, hipMemcpyDeviceToHost, ctx->stream);
-}
-// (after the synchronisation) true when this merge raised a flag
-static bool status_raised(crdt_ctx *ctx, const uint32_t *two) {
-    if (two[1]) (void)hipMemsetD32Async((hipDeviceptr_t)ctx->dev_status, (int)(two[0] | two[1]), 1, ctx->stream);
-    return two[0] != 0;
-}
+// Device failure flags raised by the passes of one merge: while a
+// StatusScope lives, the context's kernels raise their flags into a spare
+// word of the status buffer (word 2, zero between merges) -- a host-side
+// pointer swap, no GPU work -- and the merge's one host synchronisation reads
+// it beside the caller's word 0.  A raised flag is folded into word 0 (it
+// stays for crdt_ctx_device_status) and the spare word cleared; so is a
+// scope left on an error path before the check.
+struct StatusScope {
+    crdt_ctx *ctx;
+    uint32_t *saved;
+    bool settled = false;
+    explicit StatusScope(crdt_ctx *c) : ctx(c), saved(c->dev_status) { c->dev_status = saved + 2; }
+    ~StatusScope() {
+        ctx->dev_status = saved;
+        if (!settled) (void)hipMemsetAsync(saved + 2, 0, 4, ctx->stream);   // (an error path: maybe dirty)
+    }
+    // words 0..2 of the status buffer to host memory (before the merge's synchronisation)
+    hipError_t fetch(uint32_t *three) const {
+        return hipMemcpyAsync(three, saved, 12, hipMemcpyDeviceToHost, ctx->stream);
+    }
+    // (after the synchronisation) true when a pass of this merge raised a flag
+    bool raised(const uint32_t *three) {
+        settled = true;
+        if (!three[2]) return false;
+        (void)hipMemsetD32Async((hipDeviceptr_t)saved, (int)(three[0] | three[2]), 1, ctx->stream);
+        (void)hipMemsetAsync(saved + 2, 0, 4, ctx->stream);
+        return true;
+    }
+};
 
 static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
     Batch b;
@@ -249,8 +257,8 @@ static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
     ro.st_kind = (uint8_t *)(d + o_kind);
     ro.st_str = (uint32_t *)(d + o_str);
     ro.st_sum = (int64_t *)(d + o_sum);
-    rc = status_mark(ctx);
-    if (!rc) rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    StatusScope sc(ctx);
+    rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
 
     std::vector<uint64_t> h_off(n + 1);
@@ -267,11 +275,11 @@ static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
             hipError_t e = hipMemcpyAsync(x.dst, d + x.src, x.bytes, hipMemcpyDeviceToHost, ctx->stream);
             if (e != hipSuccess) return hip_fail(ctx, e);
         }
-    uint32_t fl[2] = {0, 0};
-    hipError_t e = status_fetch(ctx, fl);
+    uint32_t fl[3] = {0, 0, 0};
+    hipError_t e = sc.fetch(fl);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
-    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;           // nothing below ran: the servers are untouched
+    if (sc.raised(fl)) return CRDT_E_DEVICE;                     // nothing below ran: the servers are untouched
 
     for (size_t p = 0; p < n; ++p) {
         Server &s = *srv[p];
@@ -552,16 +560,16 @@ static int dev_flush_chunk(crdt_ctx *ctx, Server &s, const std::map<int64_t, std
                      s.c_key.as<uint32_t>(), s.c_val.as<uint32_t>(), sb, so};
     crdt_local_out lo{s.o_off.as<uint64_t>(), s.dd2.ts.as<int64_t>(), s.dd2.origin.as<uint8_t>(),
                       s.o_src.as<int64_t>(), s.c_status.as<uint16_t>(), nullptr, nullptr, nullptr};
-    rc = status_mark(ctx);
-    if (!rc) rc = crdt_local_apply(ctx, &li, &lo);
+    StatusScope sc(ctx);
+    rc = crdt_local_apply(ctx, &li, &lo);
     if (rc) return rc;
     uint64_t oo[2] = {0, 0};
-    uint32_t fl[2] = {0, 0};
+    uint32_t fl[3] = {0, 0, 0};
     e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = status_fetch(ctx, fl);
+    if (e == hipSuccess) e = sc.fetch(fl);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
-    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;       // dd untouched (the swap below never ran)
+    if (sc.raised(fl)) return CRDT_E_DEVICE;                // dd untouched (the swap below never ran)
     const uint64_t n_out = oo[1];
     rc = crdt_seg_gather2(ctx, n_out, s.o_src.as<int64_t>(), s.dd.kv_off.as<uint64_t>(), s.c_kv.as<uint64_t>(), 0,
                           s.dd2.kv_off.as<uint64_t>(), 4, s.dd.kv_key.p, s.c_key.p, s.dd2.kv_key.p, s.dd.kv_val.p,
@@ -669,8 +677,8 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     crdt_refmerge_out ro{s.o_off.as<uint64_t>(), s.dd2.ts.as<int64_t>(), s.dd2.origin.as<uint8_t>(),
                          s.o_src.as<int64_t>(), s.st_kind.as<uint8_t>(), s.st_str.as<uint32_t>(),
                          s.st_sum.as<int64_t>()};
-    rc = status_mark(ctx);
-    if (!rc) rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    StatusScope sc(ctx);
+    rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
     // the new Diff's kv pairs behind the merge, its entry count still on the
     // device (dd2 is sized for |L| + |R|): one host synchronisation per merge
@@ -691,11 +699,11 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     if (e == hipSuccess && nks) e = hipMemcpyAsync(kind.data(), s.st_kind.p, nks, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(sstr.data(), s.st_str.p, nks * 4, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && nks) e = hipMemcpyAsync(ssum.data(), s.st_sum.p, nks * 8, hipMemcpyDeviceToHost, ctx->stream);
-    uint32_t fl[2] = {0, 0};
-    if (e == hipSuccess) e = status_fetch(ctx, fl);
+    uint32_t fl[3] = {0, 0, 0};
+    if (e == hipSuccess) e = sc.fetch(fl);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
-    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;       // dd / RemoteDiff untouched (the swap below never ran)
+    if (sc.raised(fl)) return CRDT_E_DEVICE;                // dd / RemoteDiff untouched (the swap below never ran)
     std::map<std::string, std::string> state;
     for (uint64_t k = 0; k < nks; ++k) {
         if (kind[k] == 1) state.emplace(tab_str(ctx->keys, k), tab_str(ctx->vals, sstr[k]));
@@ -965,8 +973,8 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
         maxs = std::max<uint64_t>(maxs, std::max(nu + 1, qu));
     }
     if (rc) return rc;
-    rc = status_mark(ctx);
-    if (!rc) rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    StatusScope sc(ctx);
+    rc = crdt_refmerge_batch(ctx, &ri, &ro);
     if (rc) return rc;
     pc.mark("refmerge_launch");
     // the new Diff's kv pairs (the entry count stays on the device), each
@@ -997,11 +1005,11 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     if (e == hipSuccess) e = hipMemcpyAsync(kind.data(), bb.st_kind.p, nslots, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(sstr.data(), bb.st_str.p, nslots * 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ssum.data(), bb.st_sum.p, nslots * 8, hipMemcpyDeviceToHost, st);
-    uint32_t fl[2] = {0, 0};
-    if (e == hipSuccess) e = status_fetch(ctx, fl);
+    uint32_t fl[3] = {0, 0, 0};
+    if (e == hipSuccess) e = sc.fetch(fl);
     if (e == hipSuccess) e = hipStreamSynchronize(st);   // (also settles sp / sq, host vectors)
     if (e != hipSuccess) return hip_fail(ctx, e);
-    if (status_raised(ctx, fl)) return CRDT_E_DEVICE;       // no server swapped in anything
+    if (sc.raised(fl)) return CRDT_E_DEVICE;                // no server swapped in anything
     pc.mark("gather+split+state_d2h");
     uint64_t nks = 0;
     (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);
