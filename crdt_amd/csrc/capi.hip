@@ -22,6 +22,9 @@ int g_or_key_sort = 1;   // OR-Set D2: key-only sort + key runs ordered in LDS (
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
+int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
+int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
+int g_mm_bpc = 4;        // sort minmax: workgroups per CU per input
 int g_lww_parts = 4;     // LWW write pass: quarter tiles (half tiles 112 -> 105 us)
 int g_rm_diag = 0;
 int g_scan_items = 8;
@@ -293,6 +296,15 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 1 key-only sort + run sort, 0 full tag sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_key_sort = (int)v;
+    } else if (!strcmp(name, "sort.xcd_tiles")) {    // radix scatter pass: 1 XCD-contiguous tile ranges, 0 blockIdx order
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_sort_xcd = (int)v;
+    } else if (!strcmp(name, "sort.mm_blocks_per_cu")) {   // sort minmax grid: workgroups per CU per input
+        if (v < 1 || v > 16) return CRDT_E_INVAL;
+        g_mm_bpc = (int)v;
+    } else if (!strcmp(name, "sort.vec_up")) {       // fused D2 sort: 1 vectorised composing upsweep, 0 scalar
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_sort_vec_up = (int)v;
     } else if (!strcmp(name, "sets.lww_parts")) {    // LWW write-pass workgroups per 4096-item tile
         if (v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
         g_lww_parts = (int)v;

@@ -58,6 +58,9 @@ extern FoldTuning g_fold;
 extern int g_vclock_pairs_per_wave;
 extern int g_vclock_blocks_per_cu;
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
+extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
+extern int g_sort_vec_up;
+extern int g_mm_bpc;            // sort minmax: workgroups per CU per input (sort.mm_blocks_per_cu)       // fused D2 sort: vectorised composing upsweep (sort.vec_up)
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
@@ -150,6 +153,15 @@ __host__ __device__ inline uint64_t rnd(uint64_t k, uint64_t i) {
     return splitmix64(k + i * 0x9E3779B97F4A7C15ULL);
 }
 
+
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// "Workgroup dispatch": b and b + 8 share an XCD).  Block b -> tile such that
+// each XCD's blocks take one contiguous range of the G tiles, in order (a
+// bijection on [0, G); speed only, never relied on for correctness).
+__device__ __forceinline__ uint32_t xcd_contig(uint32_t b, uint32_t G) {
+    const uint32_t x = b & 7u, q = b >> 3, per = G >> 3, rem = G & 7u;
+    return x * per + (x < rem ? x : rem) + q;
+}
 
 // LDS-DMA staging of one side's run of one field: elements [g0, g0 + cnt) of
 // src into the byte array dst from byte *at (16-byte aligned), in 16-byte

@@ -56,8 +56,8 @@ struct SortMinMax {              // one per minmax workgroup, reduced by k_sort_
 
 __device__ __forceinline__ uint32_t bitwidth(uint64_t x) { return x ? 64u - (uint32_t)__clzll((long long)x) : 0u; }
 
-// VEC: key / ts / rep 16-byte aligned -- four tuples per lane per step in
-// 16-byte loads, two steps in flight (ten 16-byte loads per lane).  One
+// VEC: key / ts / rep 16-byte aligned -- two tuples per lane per unit in
+// 16- / 8-byte loads, four units in flight.  One
 // launch covers both inputs of the fused merge: workgroups [0, g_a) read
 // `in`, the rest `in2`.
 template <bool VEC>
@@ -78,35 +78,38 @@ __global__ __launch_bounds__(256) void k_sort_minmax(crdt_tuples in, size_t n, c
     const size_t b0 = second ? blockIdx.x - g_a : blockIdx.x, gs = second ? gridDim.x - g_a : g_a;
     size_t i0 = 0;
     if constexpr (VEC) {
-        const size_t n4 = m / 4;
+        // units of two tuples: a lane reads 16 B of keys, 16 B of ts, 8 B of
+        // reps per unit, consecutive lanes consecutive units (every load
+        // instruction one contiguous 1 KB / 512 B span), four units in flight
+        // (a lane reading two adjacent 16-B halves of 32 B per array ran at
+        // 4.1 TB/s)
+        const size_t nu = m / 2;
         const ulonglong2 *K = (const ulonglong2 *)t_in.key, *T = (const ulonglong2 *)t_in.ts;
-        const uint4 *R = (const uint4 *)t_in.rep;
+        const uint2 *R = (const uint2 *)t_in.rep;
         const size_t stride = gs * 256;
-        size_t i = b0 * 256 + threadIdx.x;
-        for (; i + stride < n4; i += 2 * stride) {
-            const size_t j = i + stride;
-            const ulonglong2 k0 = K[2 * i], k1 = K[2 * i + 1], k2 = K[2 * j], k3 = K[2 * j + 1];
-            const ulonglong2 t0 = T[2 * i], t1 = T[2 * i + 1], t2 = T[2 * j], t3 = T[2 * j + 1];
-            const uint4 r = R[i], q = R[j];
-            acc(k0.x, t0.x, r.x);
-            acc(k0.y, t0.y, r.y);
-            acc(k1.x, t1.x, r.z);
-            acc(k1.y, t1.y, r.w);
-            acc(k2.x, t2.x, q.x);
-            acc(k2.y, t2.y, q.y);
-            acc(k3.x, t3.x, q.z);
-            acc(k3.y, t3.y, q.w);
+        size_t u = b0 * 256 + threadIdx.x;
+        for (; u + 3 * stride < nu; u += 4 * stride) {
+            ulonglong2 k[4], t[4];
+            uint2 r[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                k[j] = K[u + j * stride];
+                t[j] = T[u + j * stride];
+                r[j] = R[u + j * stride];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc(k[j].x, t[j].x, r[j].x);
+                acc(k[j].y, t[j].y, r[j].y);
+            }
         }
-        if (i < n4) {
-            const ulonglong2 k0 = K[2 * i], k1 = K[2 * i + 1];
-            const ulonglong2 t0 = T[2 * i], t1 = T[2 * i + 1];
-            const uint4 r = R[i];
-            acc(k0.x, t0.x, r.x);
-            acc(k0.y, t0.y, r.y);
-            acc(k1.x, t1.x, r.z);
-            acc(k1.y, t1.y, r.w);
+        for (; u < nu; u += stride) {
+            const ulonglong2 k = K[u], t = T[u];
+            const uint2 r = R[u];
+            acc(k.x, t.x, r.x);
+            acc(k.y, t.y, r.y);
         }
-        i0 = n4 * 4;
+        i0 = nu * 2;
     }
     for (size_t i = i0 + b0 * 256 + threadIdx.x; i < m; i += gs * 256) acc(t_in.key[i], t_in.ts[i], t_in.rep[i]);
     for (int w = 32; w >= 1; w >>= 1) {
@@ -149,7 +152,7 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, co
     };
     const bool vec = (!n || aligned(in)) && (!n2 || aligned(in2));
     auto blocks = [&](size_t m) {
-        return m ? std::min(MM_BLOCKS, grid_for(vec ? m / 8 + 1 : m, 256, (unsigned)ctx->num_cus * 4)) : 0u;
+        return m ? std::min(MM_BLOCKS, grid_for(vec ? m / 8 + 1 : m, 256, (unsigned)(ctx->num_cus * g_mm_bpc))) : 0u;
     };
     const unsigned ga = blocks(n), gb = blocks(n2);
     if (vec) k_sort_minmax<true><<<ga + gb, 256, 0, ctx->stream>>>(in, n, in2, n2, ga, mm);
@@ -319,6 +322,55 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
     cnt[(size_t)tid * ntiles + blockIdx.x] = v;
 }
 
+// The composing upsweep (pass 0) with two tuples per lane per round: 16-B
+// key / ts loads, 8-B reps, 2-B tombs (the scalar form issues four narrow
+// loads per tuple).  Needs key / ts 16-byte, rep 8-byte, tomb 2-byte aligned
+// sides and an even n1 (no pair straddles the two inputs); the histogram
+// counts do not depend on which lane composes which tuple.
+__global__ __launch_bounds__(SB) void k_sort_up_vec(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
+                                                    uint32_t ntiles, uint32_t *__restrict__ cnt,
+                                                    uint64_t *__restrict__ comp) {
+    __shared__ uint32_t h[SWAVES * 256];
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
+    const SortPlan p = *plan_;
+    const size_t base = (size_t)blockIdx.x * ST;
+    uint64_t c[SR];
+#pragma unroll
+    for (int r = 0; r < SR / 2; ++r) {
+        const size_t e = base + 2 * ((size_t)r * SB + tid);
+        c[2 * r] = c[2 * r + 1] = 0;
+        if (e >= n) continue;
+        const bool side = e >= p.n1;
+        const crdt_tuples &T = side ? p.in2 : in;
+        const size_t f = side ? e - p.n1 : e;
+        if (e + 1 < n) {
+            const ulonglong2 k = *(const ulonglong2 *)(T.key + f), t = *(const ulonglong2 *)(T.ts + f);
+            const uint2 rp = *(const uint2 *)(T.rep + f);
+            const uint16_t tb = *(const uint16_t *)(T.tomb + f);
+            c[2 * r] = compose<1>(p, k.x, t.x, rp.x, (uint8_t)(tb & 0xFF), side).w[0];
+            c[2 * r + 1] = compose<1>(p, k.y, t.y, rp.y, (uint8_t)(tb >> 8), side).w[0];
+            *(ulonglong2 *)(comp + e) = ulonglong2{c[2 * r], c[2 * r + 1]};
+        } else {
+            c[2 * r] = compose<1>(p, T.key[f], T.ts[f], T.rep[f], T.tomb[f], side).w[0];
+            comp[e] = c[2 * r];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        const size_t e = base + 2 * ((size_t)(r >> 1) * SB + tid) + (r & 1);
+        CKey<1> v;
+        v.w[0] = c[r];
+        if (e < n) atomicAdd(&h[w * 256 + digit_of(v, 0, p.s0)], 1u);
+    }
+    __syncthreads();
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < SWAVES; ++k) v += h[k * 256 + tid];
+    cnt[(size_t)tid * ntiles + blockIdx.x] = v;
+}
+
 // loc[d * ntiles + t] = tile t's start within digit d's bucket; tot[d] = bucket size.
 // One 1024-thread workgroup per column: 8192 tile counts per block-scan round
 // (one round up to 33M composites; a 256-thread, 2048-per-round form spent
@@ -374,7 +426,7 @@ template <int WORDS, bool FIRST, bool LAST>
 __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
                                                   const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
                                                   const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
-                                                  uint64_t *__restrict__ dst, crdt_tuples out) {
+                                                  uint64_t *__restrict__ dst, crdt_tuples out, int xcd) {
     // wc: per (round, wave, digit) counts, then their exclusive prefix;
     // reused (after the ranks are taken) as the staging area of the tile
     constexpr int WC_BYTES = SR * SWAVES * 256 * 2;
@@ -385,7 +437,10 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
     uint16_t *wc = (uint16_t *)lds;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const SortPlan p = *plan_;
-    const uint32_t t = blockIdx.x;
+    // each XCD's workgroups take one contiguous range of tiles: tile t's and
+    // t + 1's runs of a digit are adjacent in the output, so their partial
+    // lines meet in one L2 instead of two (sort.xcd_tiles; speed only)
+    const uint32_t t = xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x;
     const size_t base = (size_t)t * ST;
     for (int i = tid; i < SR * SWAVES * 256 / 4; i += SB) ((uint64_t *)lds)[i] = 0;
     {
@@ -491,14 +546,15 @@ template <int WORDS>
 static void launch_pass(bool first, bool last, unsigned grid, hipStream_t st, const crdt_tuples &in,
                         const uint64_t *src, size_t n, const SortPlan *plan, uint32_t pass, const uint32_t *loc,
                         const uint32_t *tot, uint64_t *dst, const crdt_tuples &out) {
+    const int x = g_sort_xcd;
     if (first && last)
-        k_sort_pass<WORDS, true, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
+        k_sort_pass<WORDS, true, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
     else if (first)
-        k_sort_pass<WORDS, true, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
+        k_sort_pass<WORDS, true, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
     else if (last)
-        k_sort_pass<WORDS, false, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
+        k_sort_pass<WORDS, false, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
     else
-        k_sort_pass<WORDS, false, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out);
+        k_sort_pass<WORDS, false, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
 }
 
 // P passes; the last decodes into `out`, or (decode = false) leaves the
@@ -506,13 +562,15 @@ static void launch_pass(bool first, bool last, unsigned grid, hipStream_t st, co
 template <int WORDS>
 static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &out, const SortPlan *plan_d,
                       uint32_t P, uint64_t *bufs, uint32_t *cnt, uint32_t *loc, uint32_t *tot, bool decode = true,
-                      uint64_t **result = nullptr) {
+                      uint64_t **result = nullptr, bool vec_first = false) {
     const hipStream_t st = ctx->stream;
     const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
     uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
     for (uint32_t q = 0; q < P; ++q) {
         // pass 0's upsweep composes from the tuples and stores the composites
-        if (q == 0)
+        if (q == 0 && WORDS == 1 && vec_first)
+            k_sort_up_vec<<<ntiles, SB, 0, st>>>(in, n, plan_d, ntiles, cnt, a);
+        else if (q == 0)
             k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a);
         else
             k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr);
@@ -632,46 +690,102 @@ struct LwwWin {                                          // (scalars, not side-i
     __device__ __forceinline__ uint32_t tomb() const { return ha ? ta : tb; }
 };
 
-template <int MODE, int WORDS>
-__global__ __launch_bounds__(DB) void k_dd_count(const uint64_t *__restrict__ c, size_t n,
-                                                 const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt) {
-    __shared__ uint32_t s_w[DB / 64];
-    const SortPlan p = *plan_;
-    const size_t base = (size_t)blockIdx.x * DT;
-    const int lane = threadIdx.x & 63;
-    uint32_t m = 0;
-    CKey<WORDS> v[DI];
+// The neighbours in sorted order come from the adjacent lanes (shuffles);
+// a wave's edge lanes take them from the next / previous wave's edge values
+// exchanged through LDS, the tile's two outer neighbours are loaded once up
+// front.  (A global load per round in the edge lanes put eight dependent HBM
+// round trips in front of every tile's ballots.)
+template <int WORDS>
+struct DdEdges {
+    uint64_t lo[DI][DB / 64][WORDS], hi[DI][DB / 64][WORDS];   // lane 0 / lane 63 composites per (round, wave)
+    uint64_t prev[WORDS], next[WORDS];                         // c[base - 1], c[base + DT]
+};
+template <int WORDS>
+__device__ __forceinline__ void dd_edges_put(DdEdges<WORDS> &x, const CKey<WORDS> *v, int lane, int w) {
+    if (lane == 0 || lane == 63)
+#pragma unroll
+        for (int r = 0; r < DI; ++r)
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) (lane == 0 ? x.lo : x.hi)[r][w][q] = v[r].w[q];
+}
+template <int WORDS>
+__device__ __forceinline__ CKey<WORDS> dd_next(const DdEdges<WORDS> &x, const CKey<WORDS> &v, int r, int lane, int w) {
+    CKey<WORDS> nx;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) {
+        nx.w[q] = (uint64_t)__shfl_down((unsigned long long)v.w[q], 1, 64);
+        if (lane == 63)
+            nx.w[q] = w + 1 < DB / 64 ? x.lo[r][w + 1][q] : (r + 1 < DI ? x.lo[r + 1][0][q] : x.next[q]);
+    }
+    return nx;
+}
+template <int WORDS>
+__device__ __forceinline__ CKey<WORDS> dd_prev(const DdEdges<WORDS> &x, const CKey<WORDS> &v, int r, int lane, int w) {
+    CKey<WORDS> pv;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) {
+        pv.w[q] = (uint64_t)__shfl_up((unsigned long long)v.w[q], 1, 64);
+        if (lane == 0) pv.w[q] = w > 0 ? x.hi[r][w - 1][q] : (r > 0 ? x.hi[r - 1][DB / 64 - 1][q] : x.prev[q]);
+    }
+    return pv;
+}
+// the tile's composites (round-major) and its outer neighbours into LDS
+template <int WORDS>
+__device__ __forceinline__ void dd_load(const uint64_t *__restrict__ c, size_t n, size_t base, CKey<WORDS> *v,
+                                        DdEdges<WORDS> &x) {
+    const int tid = threadIdx.x;
+    CKey<WORDS> pe, ne;
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) pe.w[q] = ne.w[q] = 0;
+    if (tid == 0 && base > 0) pe = ck_load<WORDS>(c, n, base - 1);
+    if (tid == 0 && base + DT < n) ne = ck_load<WORDS>(c, n, base + DT);
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
-        const size_t e = base + (size_t)r * DB + threadIdx.x;
+        const size_t e = base + (size_t)r * DB + tid;
         if (e < n) v[r] = ck_load<WORDS>(c, n, e);
         else
 #pragma unroll
             for (int q = 0; q < WORDS; ++q) v[r].w[q] = 0;
     }
+    if (tid == 0)
 #pragma unroll
-    for (int r = 0; r < DI; ++r) {                // neighbour from the adjacent lane; edge lanes load it
+        for (int q = 0; q < WORDS; ++q) {
+            x.prev[q] = pe.w[q];
+            x.next[q] = ne.w[q];
+        }
+    dd_edges_put<WORDS>(x, v, tid & 63, tid >> 6);
+}
+
+template <int MODE, int WORDS>
+__global__ __launch_bounds__(DB) void k_dd_count(const uint64_t *__restrict__ c, size_t n,
+                                                 const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t s_w[DB / 64];
+    __shared__ DdEdges<WORDS> s_x;
+    const SortPlan p = *plan_;
+    const size_t base = (size_t)blockIdx.x * DT;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t m = 0;
+    CKey<WORDS> v[DI];
+    dd_load<WORDS>(c, n, base, v, s_x);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < DI; ++r) {
         const size_t e = base + (size_t)r * DB + threadIdx.x;
-        CKey<WORDS> nb;
         if constexpr (MODE == DD_LWW) {
-#pragma unroll
-            for (int q = 0; q < WORDS; ++q) nb.w[q] = (uint64_t)__shfl_down((unsigned long long)v[r].w[q], 1, 64);
-            if (lane == 63 && e + 1 < n) nb = ck_load<WORDS>(c, n, e + 1);
+            const CKey<WORDS> nb = dd_next<WORDS>(s_x, v[r], r, lane, w);
             m += (e < n && (e + 1 == n || !eq_from(v[r], nb, p.b0 + p.br + p.bt))) ? 1u : 0u;
         } else {
-#pragma unroll
-            for (int q = 0; q < WORDS; ++q) nb.w[q] = (uint64_t)__shfl_up((unsigned long long)v[r].w[q], 1, 64);
-            if (lane == 0 && e > 0 && e < n) nb = ck_load<WORDS>(c, n, e - 1);
+            const CKey<WORDS> nb = dd_prev<WORDS>(s_x, v[r], r, lane, w);
             m += (e < n && (e == 0 || !eq_from(v[r], nb, p.b0))) ? 1u : 0u;
         }
     }
     for (int o = 32; o >= 1; o >>= 1) m += __shfl_xor(m, o, 64);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = m;
+    if (lane == 0) s_w[w] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t t = 0;
 #pragma unroll
-        for (int w = 0; w < DB / 64; ++w) t += s_w[w];
+        for (int k = 0; k < DB / 64; ++k) t += s_w[k];
         cnt[blockIdx.x] = t;
     }
 }
@@ -683,38 +797,27 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
                                                  uint64_t *__restrict__ out_count) {
     __shared__ uint32_t s_c[DI * (DB / 64)];      // emits per (round, wave), then their exclusive prefix
     __shared__ uint64_t s_v[MODE == DD_LWW ? DT * WORDS : 1];   // LWW: the tile's composites (run walks)
+    __shared__ DdEdges<WORDS> s_x;
     const SortPlan p = *plan_;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const size_t base = (size_t)blockIdx.x * DT;
     if (blockIdx.x == 0 && tid == 0) *out_count = tot[0];
-    // the neighbours in sorted order come from the adjacent lanes (shuffles);
-    // only a wave's edge lanes load them
+    const size_t t0 = loc[blockIdx.x];
     uint64_t em[DI];
     CKey<WORDS> v[DI];
     uint8_t tb[DI];                               // output tomb; bit 1: the tag run continues (rare walk)
+    dd_load<WORDS>(c, n, base, v, s_x);
+    if constexpr (MODE == DD_LWW)
 #pragma unroll
-    for (int r = 0; r < DI; ++r) {
-        const size_t e = base + (size_t)r * DB + tid;
-        if (e < n) v[r] = ck_load<WORDS>(c, n, e);
-        else
-#pragma unroll
-            for (int q = 0; q < WORDS; ++q) v[r].w[q] = 0;
-        if constexpr (MODE == DD_LWW)
+        for (int r = 0; r < DI; ++r)
 #pragma unroll
             for (int q = 0; q < WORDS; ++q) s_v[q * DT + r * DB + tid] = v[r].w[q];
-    }
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
         const size_t e = base + (size_t)r * DB + tid;
-        CKey<WORDS> nx, pv;
-#pragma unroll
-        for (int q = 0; q < WORDS; ++q) {
-            nx.w[q] = (uint64_t)__shfl_down((unsigned long long)v[r].w[q], 1, 64);
-            pv.w[q] = (uint64_t)__shfl_up((unsigned long long)v[r].w[q], 1, 64);
-        }
+        const CKey<WORDS> nx = dd_next<WORDS>(s_x, v[r], r, lane, w), pv = dd_prev<WORDS>(s_x, v[r], r, lane, w);
         const bool valid = e < n, has_next = e + 1 < n, has_prev = e > 0;
-        if (lane == 63 && has_next) nx = ck_load<WORDS>(c, n, e + 1);
-        if (lane == 0 && has_prev && valid) pv = ck_load<WORDS>(c, n, e - 1);
         const bool same_next = has_next && eq_from(nx, v[r], p.b0);
         bool f;
         if constexpr (MODE == DD_LWW) {
@@ -732,16 +835,19 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         if (lane == 0) s_c[r * (DB / 64) + w] = (uint32_t)__popcll(em[r]);
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (int i = 0; i < DI * (DB / 64); ++i) {
-            const uint32_t x = s_c[i];
-            s_c[i] = run;
-            run += x;
+    if (w == 0) {                                 // exclusive prefix of the (round, wave) emit counts
+        constexpr int NC = DI * (DB / 64);
+        static_assert(NC <= 64, "one wave");
+        const uint32_t c0 = lane < NC ? s_c[lane] : 0u;
+        uint32_t x = c0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
+        if (lane < NC) s_c[lane] = x - c0;
     }
     __syncthreads();
-    const size_t t0 = loc[blockIdx.x];
     const uint32_t sk = p.b0 + p.br + p.bt;
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
@@ -811,13 +917,18 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
 // LDS themselves (no extra pass over HBM):
 //   k_run_bounds : tile t = [first run start >= t RT, first run start >=
 //                  (t+1) RT), one thread per boundary (galloping search);
-//   k_or_rdd_count: per tile, the runs sorted in LDS (runs of <= kInsMax
-//                  tuples: one thread's insertion sort; longer ones: the
-//                  workgroup's in-place rank sort), the distinct tags counted;
+//   k_or_rdd_count: per tile (staged in LDS), every element marked by itself
+//                  (or_mark: is it its tag's first copy; runs of more than
+//                  kInsMax tuples are rank-sorted in place first), the marks
+//                  counted;
 //   k_sort_colscan of the counts;
-//   k_or_rdd_apply: the same sort, then the first copy of every tag emits at
-//                  its rank with the OR of its copies' tombs (a tag's copies
-//                  never leave the tile: it is run-aligned).
+//   k_or_rdd_apply: the same marks, an emit bitmap and its prefix, then every
+//                  first copy stores at its tile rank + its rank among its
+//                  run's first copies, with the OR of its copies' tombs (a
+//                  tag's copies never leave the tile: it is run-aligned).
+// (Round 2 sorted every short run by one thread's insertion sort in both
+// passes: count 199 / apply 270 us at config D; one thread per run start
+// left most lanes idle behind a chain of dependent LDS reads.)
 // A run longer than the LDS tile (adversarial data: many copies of one key)
 // makes its tile take the global path: the count pass sorts it in place
 // (RCAP-chunks bitonic-sorted in LDS, then merged pairwise through a scratch
@@ -825,7 +936,7 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
 constexpr int RT = 2048;                 // nominal tile (composites)
 constexpr int RCAP = 3072;               // LDS capacity of a run-aligned tile
 constexpr int RB = 256;                  // threads
-constexpr uint32_t kInsMax = 32;         // runs up to this length: one thread's insertion sort
+constexpr uint32_t kInsMax = 32;         // runs up to this length: element-wise marks, unsorted
 
 // first run start at or after p (keys = composite >> ks): galloping, then binary search
 __device__ __forceinline__ size_t run_start_from(const uint64_t *__restrict__ c, size_t n, size_t p, uint32_t ks) {
@@ -882,40 +993,6 @@ __device__ void lds_rank_sort(uint64_t *s, uint32_t r0, uint32_t L) {
         if (i < L) s[r0 + rk[q]] = v[q];
     }
     __syncthreads();
-}
-
-// sort every key run of s[0, m) (m <= RCAP, run-aligned) in place
-__device__ void lds_sort_runs(uint64_t *s, uint32_t m, uint32_t ks, uint32_t *s_big, uint32_t *s_nbig) {
-    if (threadIdx.x == 0) *s_nbig = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += RB) {      // run starts: short runs sorted in place
-        const uint64_t k = s[i] >> ks;
-        if (i > 0 && (s[i - 1] >> ks) == k) continue;
-        uint32_t e = i + 1;
-        while (e < m && (s[e] >> ks) == k && e - i <= kInsMax) ++e;
-        if (e - i > kInsMax) {                           // a longer run: the workgroup sorts it below
-            s_big[atomicAdd(s_nbig, 1u)] = i;
-            continue;
-        }
-        for (uint32_t a = i + 1; a < e; ++a) {           // insertion sort of s[i, e)
-            const uint64_t x = s[a];
-            uint32_t b = a;
-            while (b > i && s[b - 1] > x) {
-                s[b] = s[b - 1];
-                --b;
-            }
-            s[b] = x;
-        }
-    }
-    __syncthreads();
-    const uint32_t nbig = *s_nbig;
-    for (uint32_t q = 0; q < nbig; ++q) {
-        const uint32_t r0 = s_big[q];
-        const uint64_t k = s[r0] >> ks;
-        uint32_t e = r0 + 1;
-        while (e < m && (s[e] >> ks) == k) ++e;          // (every thread: the same answer)
-        lds_rank_sort(s, r0, e - r0);
-    }
 }
 
 // bitonic sort of s[0, m) in LDS, m a power of two <= 4096
@@ -1012,11 +1089,86 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *s_w) {
     return t;
 }
 
+// Element-wise marks over a run-aligned tile s[0, len) in LDS whose runs of
+// more than kInsMax composites are already sorted (rare; lds_sort_long):
+// element i is the FIRST copy of its tag in (key, ts, rep, side, tomb) order
+// -- in a short run, no other element of its run has its tag and a smaller
+// composite (an equal one: a lower index); in a sorted long run, its
+// predecessor's tag differs -- and its tomb is the OR over the tag's copies.
+// No run is sorted for this: a short run's emitting elements are placed by
+// their rank among the run's emitting tags (or_rank).  Runs average 2.5
+// composites in config D, so every walk below is a few LDS reads, issued by
+// all lanes at once instead of one thread per run.
+struct OrMark {
+    uint32_t rs, re;                                     // the run [rs, re) when short; rs = re = 0 when long
+    bool emit;
+    uint32_t tomb;
+};
+__device__ __forceinline__ OrMark or_mark(const uint64_t *s, uint32_t len, uint32_t i, uint32_t ks, uint32_t tb) {
+    OrMark m;
+    const uint64_t x = s[i], k = x >> ks;
+    uint32_t rs = i, re = i + 1;
+    while (rs > 0 && i - rs <= kInsMax && (s[rs - 1] >> ks) == k) --rs;
+    while (re < len && re - i <= kInsMax && (s[re] >> ks) == k) ++re;
+    m.tomb = (uint32_t)(x & 1u);
+    if (re - rs > kInsMax) {                             // a long run (sorted): neighbours decide
+        m.rs = m.re = 0;
+        m.emit = i == 0 || (s[i - 1] >> tb) != (x >> tb);
+        if (m.emit)
+            for (uint32_t j = i + 1; j < len && (s[j] >> tb) == (x >> tb); ++j) m.tomb |= (uint32_t)(s[j] & 1u);
+        return m;
+    }
+    m.rs = rs;
+    m.re = re;
+    m.emit = true;
+    for (uint32_t j = rs; j < re; ++j) {
+        const uint64_t y = s[j];
+        if ((y >> tb) != (x >> tb)) continue;
+        m.tomb |= (uint32_t)(y & 1u);
+        if (y < x || (y == x && j < i)) m.emit = false;
+    }
+    return m;
+}
+
+// sort the runs of s[0, m) longer than kInsMax in place (the workgroup's
+// rank sort, one run at a time); short runs are left in input order
+__device__ void lds_sort_long(uint64_t *s, uint32_t m, uint32_t ks, uint32_t *s_big, uint32_t *s_nbig) {
+    if (threadIdx.x == 0) *s_nbig = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += RB) {
+        const uint64_t k = s[i] >> ks;
+        if (i > 0 && (s[i - 1] >> ks) == k) continue;
+        if (i + kInsMax < m && (s[i + kInsMax] >> ks) == k) s_big[atomicAdd(s_nbig, 1u)] = i;   // run > kInsMax
+    }
+    __syncthreads();
+    const uint32_t nbig = *s_nbig;
+    for (uint32_t q = 0; q < nbig; ++q) {
+        const uint32_t r0 = s_big[q];
+        const uint64_t k = s[r0] >> ks;
+        uint32_t e = r0 + 1;
+        while (e < m && (s[e] >> ks) == k) ++e;          // (every thread: the same answer)
+        lds_rank_sort(s, r0, e - r0);
+    }
+}
+
+// The run-aligned tile c[start, start + len) (len <= RCAP) into LDS by
+// LDS-DMA from its 16-byte aligned-down start; returns the index of c[start]
+// in dst.  (A strided load / store loop waited one HBM round trip per
+// iteration: the count and apply passes took 221 / 261 us at config D.)
+__device__ __forceinline__ int rdd_stage(const uint64_t *__restrict__ c, size_t start, uint32_t len, uint64_t *dst) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+    uint32_t at = 0;
+    const int o = dma_run<uint64_t, RB / 64>(c, start, len, dst, &at, wv, ln);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    return o;
+}
+
 __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, size_t n,
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       uint64_t *__restrict__ scratch, uint32_t *__restrict__ cnt) {
-    __shared__ uint64_t s[RCAP];
+    __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
     const uint32_t ks = p.s0, tb = p.b0;                 // key bits from ks; tag bits from b0
@@ -1024,13 +1176,12 @@ __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, s
     const size_t len = end > start ? end - start : 0;
     uint32_t m = 0;
     if (len <= (size_t)RCAP) {
-        for (uint32_t i = threadIdx.x; i < len; i += RB) s[i] = c[start + i];
+        uint64_t *s = s_raw + rdd_stage(c, start, (uint32_t)len, s_raw);
+        lds_sort_long(s, (uint32_t)len, ks, s_big, &s_nbig);
         __syncthreads();
-        lds_sort_runs(s, (uint32_t)len, ks, s_big, &s_nbig);
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < len; i += RB) m += (i == 0 || (s[i] >> tb) != (s[i - 1] >> tb)) ? 1u : 0u;
+        for (uint32_t i = threadIdx.x; i < len; i += RB) m += or_mark(s, (uint32_t)len, i, ks, tb).emit ? 1u : 0u;
     } else {
-        sort_runs_global(c, n, start, end, ks, scratch, s);
+        sort_runs_global(c, n, start, end, ks, scratch, s_raw);
         __threadfence();
         __syncthreads();
         for (size_t i = start + threadIdx.x; i < end; i += RB)
@@ -1040,12 +1191,16 @@ __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, s
     if (threadIdx.x == 0) cnt[t] = tot;
 }
 
+constexpr int RNW = (RCAP + 63) / 64;                    // emit bitmap words of an LDS tile
+
 __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict__ c, size_t n,
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
                                                       crdt_tuples out, uint64_t *__restrict__ out_count) {
-    __shared__ uint64_t s[RCAP];
+    __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
+    __shared__ uint64_t s_em[RNW];                       // emit bitmap, index order
+    __shared__ uint32_t s_pre[RNW];                      // emits before each word
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
     const uint32_t ks = p.s0, tb = p.b0, sk = p.b0 + p.br + p.bt;
@@ -1053,46 +1208,93 @@ __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict_
     if (t == 0 && threadIdx.x == 0) *out_count = tot[0];
     const size_t len = end > start ? end - start : 0;
     if (len == 0) return;
-    const bool in_lds = len <= (size_t)RCAP;
-    if (in_lds) {
-        for (uint32_t i = threadIdx.x; i < len; i += RB) s[i] = c[start + i];
-        __syncthreads();
-        lds_sort_runs(s, (uint32_t)len, ks, s_big, &s_nbig);
-        __syncthreads();
-    }
-    auto at = [&](size_t i) -> uint64_t { return in_lds ? s[i] : c[start + i]; };
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     size_t base = loc[t];
-    for (size_t r0 = 0; r0 < len; r0 += RB) {
-        const size_t i = r0 + threadIdx.x;
-        const uint64_t x = i < len ? at(i) : 0;
-        const bool f = i < len && (i == 0 || (x >> tb) != (at(i - 1) >> tb));
-        const uint64_t em = __ballot(f);
-        __syncthreads();                                 // s_w of the previous round read
-        if (lane == 0) s_w[w] = (uint32_t)__popcll(em);
-        __syncthreads();
-        uint32_t before = 0, all = 0;
+    auto store = [&](size_t o, uint64_t x, uint32_t tomb) {
+        CKey<1> v;
+        v.w[0] = x;
+        out.key[o] = p.kmin + get_bits(v, sk, p.bk);
+        out.ts[o] = p.tmin + get_bits(v, p.b0 + p.br, p.bt);
+        out.rep[o] = (uint32_t)(p.rmin + get_bits(v, p.b0, p.br));
+        out.tomb[o] = (uint8_t)tomb;
+    };
+    if (len > (size_t)RCAP) {                            // the global path: runs sorted in c by the count pass
+        for (size_t r0 = 0; r0 < len; r0 += RB) {
+            const size_t i = r0 + threadIdx.x;
+            const uint64_t x = i < len ? c[start + i] : 0;
+            const bool f = i < len && (i == 0 || (x >> tb) != (c[start + i - 1] >> tb));
+            const uint64_t em = __ballot(f);
+            __syncthreads();                             // s_w of the previous round read
+            if (lane == 0) s_w[w] = (uint32_t)__popcll(em);
+            __syncthreads();
+            uint32_t before = 0, all = 0;
 #pragma unroll
-        for (int k = 0; k < RB / 64; ++k) {
-            before += k < w ? s_w[k] : 0u;
-            all += s_w[k];
-        }
-        if (f) {
-            uint32_t tomb = (uint32_t)(x & 1u);
-            for (size_t j = i + 1; j < len; ++j) {       // the tag's other copies (never past the tile)
-                const uint64_t y = at(j);
-                if ((y >> tb) != (x >> tb)) break;
-                tomb |= (uint32_t)(y & 1u);
+            for (int k = 0; k < RB / 64; ++k) {
+                before += k < w ? s_w[k] : 0u;
+                all += s_w[k];
             }
-            CKey<1> v;
-            v.w[0] = x;
-            const size_t o = base + before + (uint32_t)__popcll(em & ((1ULL << lane) - 1ULL));
-            out.key[o] = p.kmin + get_bits(v, sk, p.bk);
-            out.ts[o] = p.tmin + get_bits(v, p.b0 + p.br, p.bt);
-            out.rep[o] = (uint32_t)(p.rmin + get_bits(v, p.b0, p.br));
-            out.tomb[o] = (uint8_t)tomb;
+            if (f) {
+                uint32_t tomb = (uint32_t)(x & 1u);
+                for (size_t j = i + 1; j < len; ++j) {   // the tag's other copies (never past the tile)
+                    const uint64_t y = c[start + j];
+                    if ((y >> tb) != (x >> tb)) break;
+                    tomb |= (uint32_t)(y & 1u);
+                }
+                store(base + before + (uint32_t)__popcll(em & ((1ULL << lane) - 1ULL)), x, tomb);
+            }
+            base += all;
         }
-        base += all;
+        return;
+    }
+    const uint32_t L = (uint32_t)len;
+    uint64_t *s = s_raw + rdd_stage(c, start, L, s_raw);
+    lds_sort_long(s, L, ks, s_big, &s_nbig);
+    __syncthreads();
+    // pass 1: marks; wave w's 64 elements of round r are bitmap word 4 r + w
+    constexpr int RR = (RCAP + RB - 1) / RB;
+    OrMark mk[RR];
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+        const uint32_t i = (uint32_t)r * RB + threadIdx.x;
+        mk[r].emit = false;
+        mk[r].rs = mk[r].re = 0;
+        mk[r].tomb = 0;
+        if (i < L) mk[r] = or_mark(s, L, i, ks, tb);
+        const uint64_t em = __ballot(mk[r].emit);
+        if (lane == 0 && (uint32_t)r * RB + 64u * w < L) s_em[r * (RB / 64) + w] = em;
+    }
+    __syncthreads();
+    const uint32_t nw = (L + 63) / 64;
+    if (w == 0) {                                        // exclusive prefix of the word popcounts (nw <= 64)
+        const uint32_t pc = lane < (int)nw ? (uint32_t)__popcll(s_em[lane]) : 0u;
+        uint32_t x = pc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane < (int)nw) s_pre[lane] = x - pc;
+    }
+    __syncthreads();
+    auto before = [&](uint32_t i) -> uint32_t {          // emits at indices < i
+        const uint32_t q = i >> 6, b = i & 63;
+        return s_pre[q] + (b ? (uint32_t)__popcll(s_em[q] & ((1ULL << b) - 1ULL)) : 0u);
+    };
+    // pass 2: every emitting element at its rank
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+        const uint32_t i = (uint32_t)r * RB + threadIdx.x;
+        if (i >= L || !mk[r].emit) continue;
+        const uint64_t x = s[i];
+        uint32_t o;
+        if (mk[r].re == 0) {
+            o = before(i);                               // a sorted long run: index order is tag order
+        } else {                                         // a short run: rank among its emitting tags
+            o = before(mk[r].rs);
+            for (uint32_t j = mk[r].rs; j < mk[r].re; ++j)
+                if (j != i && ((s_em[j >> 6] >> (j & 63)) & 1u) && (s[j] >> tb) < (x >> tb)) ++o;
+        }
+        store(base + o, x, mk[r].tomb);
     }
 }
 
@@ -1157,7 +1359,12 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     if (e != hipSuccess) return hip_fail(ctx, e);
     uint64_t *sorted = nullptr;
     if (h.words == 1) {
-        rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
+        auto vec_ok = [](const crdt_tuples &t, size_t m) {
+            return m == 0 || !((((uintptr_t)t.key | (uintptr_t)t.ts) & 15) | ((uintptr_t)t.rep & 7) |
+                               ((uintptr_t)t.tomb & 1));
+        };
+        const bool vec = vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
+        rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted, vec);
         if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup
             return or_run_dedup(ctx, sorted, n, plan, sorted == bufs ? bufs + n : bufs, bufs + 2 * n, cnt, loc,
                                 tot, *out, out_count);

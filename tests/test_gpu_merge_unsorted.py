@@ -116,3 +116,24 @@ def test_unsorted_single_tag(eng, n):
     _check(eng, (k, t, r, rng.integers(0, 2, n, dtype=np.uint8)), (k.copy(), t.copy(), r.copy(),
                                                                   rng.integers(0, 2, n, dtype=np.uint8)))
     _check(eng, (k[:0], t[:0], r[:0], np.zeros(0, np.uint8)), (k, t, r, np.ones(n, np.uint8)))
+
+
+def test_unsorted_run_lengths_around_the_mark_limit(eng):
+    """OR-Set D2 marks runs of up to 32 tuples element-wise (unsorted) and
+    rank-sorts longer ones in LDS first: key runs of 1..70 tuples (so 32 / 33
+    on both sides of the limit, and runs crossing the 2048-tuple tile
+    nominal edges), duplicate tags with differing tombs and sides inside
+    every run, shuffled."""
+    rng = np.random.default_rng(33)
+    lens = np.concatenate([np.arange(1, 71), rng.integers(1, 40, 3000)])
+    key = np.repeat(np.arange(len(lens), dtype=np.uint64) * 7, lens)
+    m = len(key)
+    ts = rng.integers(0, 5, m, dtype=np.uint64)
+    rep = rng.integers(0, 3, m, dtype=np.uint64).astype(np.uint32)
+    tomb = rng.integers(0, 2, m, dtype=np.uint8)
+    side = rng.integers(0, 2, m).astype(bool)
+    p = rng.permutation(m)
+    key, ts, rep, tomb, side = key[p], ts[p], rep[p], tomb[p], side[p]
+    a = tuple(np.ascontiguousarray(x[~side]) for x in (key, ts, rep, tomb))
+    b = tuple(np.ascontiguousarray(x[side]) for x in (key, ts, rep, tomb))
+    _check(eng, a, b)
