@@ -184,6 +184,7 @@ SIGNATURES = {
     "crdt_seg_copy": (_I, [_CTX, _SZ, _P, _P, _P, _P, _SZ, _P, _P, _P, _P, _I]),
     "crdt_seg_copy2": (_I, [_CTX, _SZ, _P, _P, _P, _P, _SZ, _P, _P, _P, _P, _P, _P, _P, _I]),
     "crdt_seg_gather2": (_I, [_CTX, _SZ, _P, _P, _P, _U64, _P, _SZ, _P, _P, _P, _P, _P, _P]),
+    "crdt_seg_gather2_n": (_I, [_CTX, _SZ, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "crdt_seg_fill_u32": (_I, [_CTX, _SZ, _P, _P, _P]),
     "crdt_counts_to_offsets": (_I, [_CTX, _P, _SZ, _U64, _P]),
     "crdt_offsets_to_counts": (_I, [_CTX, _P, _SZ, _P]),

@@ -18,13 +18,14 @@ int g_or_chunk = 0;       // OR-Set tiles per chunk (likewise)
 int g_set_streams = 1;
 int g_shard_exchange_always = 0;
 int g_or_count_dma = 1;  // OR-Set count pass staged by LDS-DMA (sets.or_count_dma)
-int g_or_key_sort = 1;   // OR-Set D2: key-only sort + key runs ordered in LDS (0: the 7-pass tag sort)
+int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within groups; 1 key only; 0 the 7-pass tag sort
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
-int g_mm_bpc = 4;        // sort minmax: workgroups per CU per input
+int g_rdd_diag = 0;
+int g_mm_bpc = 1;        // sort minmax: workgroups per CU per input (1: 0.716 ms LWW D2 step, 4: 0.732)
 int g_lww_parts = 4;     // LWW write pass: quarter tiles (half tiles 112 -> 105 us)
 int g_rm_diag = 0;
 int g_scan_items = 8;
@@ -293,8 +294,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.or_count_dma")) { // OR-Set count pass: 1 LDS-DMA staging, 0 register staging
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_count_dma = (int)v;
-    } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 1 key-only sort + run sort, 0 full tag sort
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 2 key + 1-2 tag digits, 1 key-only sort, 0 full tag sort
+        if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_or_key_sort = (int)v;
     } else if (!strcmp(name, "sort.xcd_tiles")) {    // radix scatter pass: 1 XCD-contiguous tile ranges, 0 blockIdx order
         if (v != 0 && v != 1) return CRDT_E_INVAL;
@@ -302,6 +303,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.mm_blocks_per_cu")) {   // sort minmax grid: workgroups per CU per input
         if (v < 1 || v > 16) return CRDT_E_INVAL;
         g_mm_bpc = (int)v;
+    } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: OR-Set D2 dedup stops after 1 staging,
+        if (v < 0 || v > 3) return CRDT_E_INVAL;       //   2 marks, 3 counts (wrong output; never stores)
+        g_rdd_diag = (int)v;
     } else if (!strcmp(name, "sort.vec_up")) {       // fused D2 sort: 1 vectorised composing upsweep, 0 scalar
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sort_vec_up = (int)v;

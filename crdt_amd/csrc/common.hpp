@@ -60,7 +60,8 @@ extern int g_vclock_blocks_per_cu;
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
 extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
 extern int g_sort_vec_up;
-extern int g_mm_bpc;            // sort minmax: workgroups per CU per input (sort.mm_blocks_per_cu)       // fused D2 sort: vectorised composing upsweep (sort.vec_up)
+extern int g_mm_bpc;
+extern int g_rdd_diag;          // OR-Set D2 group dedup timing diagnostic (sort.rdd_diag; 0 = off)            // sort minmax: workgroups per CU per input (sort.mm_blocks_per_cu)       // fused D2 sort: vectorised composing upsweep (sort.vec_up)
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)

@@ -287,6 +287,13 @@ int crdt::seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_d
     return seg_gather<uint32_t>(ctx, n_max, code, a_off, b_off, 0, dst_off, a0, b0, dst0, a1, b1, dst1, n_dev);
 }
 
+extern "C" int crdt_seg_gather2_n(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,
+                                  const uint64_t *a_off, const uint64_t *b_off, uint64_t *dst_off, const uint32_t *a0,
+                                  const uint32_t *b0, uint32_t *dst0, const uint32_t *a1, const uint32_t *b1,
+                                  uint32_t *dst1) {
+    return crdt::seg_gather2_dev_count(ctx, n_max, n_dev, code, a_off, b_off, dst_off, a0, b0, dst0, a1, b1, dst1);
+}
+
 extern "C" int crdt_seg_copy(crdt_ctx *ctx, size_t n_seg, const int64_t *code, const uint64_t *a_off,
                              const uint64_t *b_off, const uint64_t *dst_off, size_t elem_size, const void *a,
                              const void *b, void *dst, const uint32_t *delta, int wide) {

@@ -207,7 +207,14 @@ __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32
     // B's) and the dedup finds the winning tag within the key's run.  Config
     // D: 23 key bits, 3 passes instead of 7.  Single-word composites (a
     // shifted digit never straddles a word there).
-    p.s0 = (key_only && p.words == 1) ? p.W - p.bk : 0;
+    // key_only == 2 (the fused OR-Set merge): the key and the next tag bits
+    // that fill its last digit plus one more digit (config D: 23 + 1 + 8 =
+    // 32 bits, 4 passes) -- a group of equal sorted bits then holds ~1 tuple
+    // instead of a key's ~2.5, so the dedup's in-group marks are nearly free
+    // (key bits alone: the marks cost 200 + 400 us, more than the pass)
+    uint32_t keep = p.bk;
+    if (key_only == 2) keep += (8u - p.bk % 8u) % 8u + 8u;
+    p.s0 = (key_only && p.words == 1 && p.W > keep) ? p.W - keep : 0;
     p.P = p.W - p.s0 ? (p.W - p.s0 + 7) / 8 : 1;        // >= 1: the first pass composes
     *plan = p;
 }
@@ -908,27 +915,29 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
     }
 }
 
-// ---------------------------------------------------------------- OR-Set: key runs put in tag order
-// The fused OR-Set merge sorts on the KEY's bits alone (3 passes instead of 7
-// in config D): each key's tuples come out contiguous, in input order.  Its
-// dedup needs every key run in full (key, ts, rep, side, tomb) order -- a
-// sort of each run by itself; runs are short (config D: 2.5 tuples per key),
-// so the dedup's two passes work on RUN-ALIGNED tiles and sort the runs in
-// LDS themselves (no extra pass over HBM):
-//   k_run_bounds : tile t = [first run start >= t RT, first run start >=
-//                  (t+1) RT), one thread per boundary (galloping search);
-//   k_or_rdd_count: per tile (staged in LDS), every element marked by itself
-//                  (or_mark: is it its tag's first copy; runs of more than
-//                  kInsMax tuples are rank-sorted in place first), the marks
-//                  counted;
+// ---------------------------------------------------------------- OR-Set: groups put in tag order
+// The fused OR-Set merge sorts on the KEY's bits and one more tag digit
+// (sort.or_key_only = 2; config D: 32 of 51 bits, 4 passes instead of 7):
+// tuples with equal sorted bits -- a GROUP -- come out contiguous, in input
+// order, and every tag's copies lie in one group.  The dedup needs each group
+// in full (key, ts, rep, side, tomb) order; groups are nearly all one tuple
+// (config D: 20M tuples over ~2^32 group values), so the dedup's two passes
+// work on GROUP-ALIGNED tiles and order the rare longer groups in LDS
+// themselves (no extra pass over HBM):
+//   k_run_bounds : tile t = [first group start >= t RT, first group start
+//                  >= (t+1) RT), one thread per boundary (galloping search);
+//   k_or_rdd_count: per tile (staged in LDS by LDS-DMA), 1 per one-tuple
+//                  group, and at a longer group's first element its distinct
+//                  tags (groups of more than kInsMax tuples rank-sorted in
+//                  place first);
 //   k_sort_colscan of the counts;
-//   k_or_rdd_apply: the same marks, an emit bitmap and its prefix, then every
-//                  first copy stores at its tile rank + its rank among its
-//                  run's first copies, with the OR of its copies' tombs (a
-//                  tag's copies never leave the tile: it is run-aligned).
-// (Round 2 sorted every short run by one thread's insertion sort in both
-// passes: count 199 / apply 270 us at config D; one thread per run start
-// left most lanes idle behind a chain of dependent LDS reads.)
+//   k_or_rdd_apply: the same counts, their prefix, then one-tuple groups
+//                  store themselves and a longer group's first element
+//                  stores its distinct tags at their ranks with the OR of
+//                  each tag's tombs (a tag never leaves its tile).
+// (sort.or_key_only = 1 keeps key runs of ~2.5 tuples as the groups; round 2
+// sorted each by one thread's insertion sort: count 199 / apply 270 us at
+// config D, instruction- and latency-bound -- the 4th pass costs less.)
 // A run longer than the LDS tile (adversarial data: many copies of one key)
 // makes its tile take the global path: the count pass sorts it in place
 // (RCAP-chunks bitonic-sorted in LDS, then merged pairwise through a scratch
@@ -1089,68 +1098,6 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *s_w) {
     return t;
 }
 
-// Element-wise marks over a run-aligned tile s[0, len) in LDS whose runs of
-// more than kInsMax composites are already sorted (rare; lds_sort_long):
-// element i is the FIRST copy of its tag in (key, ts, rep, side, tomb) order
-// -- in a short run, no other element of its run has its tag and a smaller
-// composite (an equal one: a lower index); in a sorted long run, its
-// predecessor's tag differs -- and its tomb is the OR over the tag's copies.
-// No run is sorted for this: a short run's emitting elements are placed by
-// their rank among the run's emitting tags (or_rank).  Runs average 2.5
-// composites in config D, so every walk below is a few LDS reads, issued by
-// all lanes at once instead of one thread per run.
-struct OrMark {
-    uint32_t rs, re;                                     // the run [rs, re) when short; rs = re = 0 when long
-    bool emit;
-    uint32_t tomb;
-};
-__device__ __forceinline__ OrMark or_mark(const uint64_t *s, uint32_t len, uint32_t i, uint32_t ks, uint32_t tb) {
-    OrMark m;
-    const uint64_t x = s[i], k = x >> ks;
-    uint32_t rs = i, re = i + 1;
-    while (rs > 0 && i - rs <= kInsMax && (s[rs - 1] >> ks) == k) --rs;
-    while (re < len && re - i <= kInsMax && (s[re] >> ks) == k) ++re;
-    m.tomb = (uint32_t)(x & 1u);
-    if (re - rs > kInsMax) {                             // a long run (sorted): neighbours decide
-        m.rs = m.re = 0;
-        m.emit = i == 0 || (s[i - 1] >> tb) != (x >> tb);
-        if (m.emit)
-            for (uint32_t j = i + 1; j < len && (s[j] >> tb) == (x >> tb); ++j) m.tomb |= (uint32_t)(s[j] & 1u);
-        return m;
-    }
-    m.rs = rs;
-    m.re = re;
-    m.emit = true;
-    for (uint32_t j = rs; j < re; ++j) {
-        const uint64_t y = s[j];
-        if ((y >> tb) != (x >> tb)) continue;
-        m.tomb |= (uint32_t)(y & 1u);
-        if (y < x || (y == x && j < i)) m.emit = false;
-    }
-    return m;
-}
-
-// sort the runs of s[0, m) longer than kInsMax in place (the workgroup's
-// rank sort, one run at a time); short runs are left in input order
-__device__ void lds_sort_long(uint64_t *s, uint32_t m, uint32_t ks, uint32_t *s_big, uint32_t *s_nbig) {
-    if (threadIdx.x == 0) *s_nbig = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += RB) {
-        const uint64_t k = s[i] >> ks;
-        if (i > 0 && (s[i - 1] >> ks) == k) continue;
-        if (i + kInsMax < m && (s[i + kInsMax] >> ks) == k) s_big[atomicAdd(s_nbig, 1u)] = i;   // run > kInsMax
-    }
-    __syncthreads();
-    const uint32_t nbig = *s_nbig;
-    for (uint32_t q = 0; q < nbig; ++q) {
-        const uint32_t r0 = s_big[q];
-        const uint64_t k = s[r0] >> ks;
-        uint32_t e = r0 + 1;
-        while (e < m && (s[e] >> ks) == k) ++e;          // (every thread: the same answer)
-        lds_rank_sort(s, r0, e - r0);
-    }
-}
-
 // The run-aligned tile c[start, start + len) (len <= RCAP) into LDS by
 // LDS-DMA from its 16-byte aligned-down start; returns the index of c[start]
 // in dst.  (A strided load / store loop waited one HBM round trip per
@@ -1164,22 +1111,127 @@ __device__ __forceinline__ int rdd_stage(const uint64_t *__restrict__ c, size_t 
     return o;
 }
 
+// A group = a run of equal sorted bits (composite >> ks) in a run-aligned
+// tile s[0, L) in LDS; with the key and one more tag digit sorted (config D)
+// nearly every group is ONE tuple, which emits itself.  Only the first
+// element of a longer group does work: a short group (<= kInsMax, in input
+// order) by pairwise compares -- element j is its tag's first copy when no
+// other element has its tag and a smaller composite (an equal one: a lower
+// index) -- a long one (sorted by lds_sort_long) by one linear walk.  (Marks
+// of every element by itself, with walks or shuffles over its run, were
+// instruction-bound: 87-215 us count, 186-417 us apply at config D.)
+
+// the group starting at g0: its end, and its distinct tags
+__device__ __forceinline__ uint32_t group_end(const uint64_t *s, uint32_t L, uint32_t g0, uint32_t ks) {
+    const uint64_t k = s[g0] >> ks;
+    uint32_t e = g0 + 1;
+    while (e < L && (s[e] >> ks) == k) ++e;
+    return e;
+}
+__device__ __forceinline__ bool group_first(const uint64_t *s, uint32_t g0, uint32_t e, uint32_t j, uint32_t tb) {
+    const uint64_t x = s[j];
+    for (uint32_t k = g0; k < e; ++k) {
+        const uint64_t y = s[k];
+        if (k != j && (y >> tb) == (x >> tb) && (y < x || (y == x && k < j))) return false;
+    }
+    return true;
+}
+__device__ uint32_t group_distinct(const uint64_t *s, uint32_t g0, uint32_t e, uint32_t tb) {
+    uint32_t d = 0;
+    if (e - g0 > kInsMax) {                              // sorted: count tag changes
+        for (uint32_t j = g0; j < e; ++j) d += (j == g0 || (s[j] >> tb) != (s[j - 1] >> tb)) ? 1u : 0u;
+        return d;
+    }
+    for (uint32_t j = g0; j < e; ++j) d += group_first(s, g0, e, j, tb) ? 1u : 0u;
+    return d;
+}
+
+// The tile's group marks, every element's in registers: thread tid holds
+// elements r RB + tid (r < RR), so wave w's lanes hold 64 consecutive ones
+// per round.  All LDS reads of the elements and of each wave-round's two
+// outer neighbours are issued before the first use; a group's start / end
+// come from the neighbours (shuffles).  Groups longer than kInsMax are found
+// at their starts and rank-sorted in LDS (rare; the elements are then read
+// again).  (Per-element walks, shuffle windows and a separate detection pass,
+// each a chain of dependent LDS reads: count 87-215 us, apply 186-417 us.)
+constexpr int RR = (RCAP + RB - 1) / RB;                 // wave-rounds per thread
+struct RddMarks {
+    uint64_t x[RR];
+    uint32_t kind;                                       // 2 bits per round: 1 one-tuple group, 2 a longer group's first
+};
+__device__ __forceinline__ void rdd_marks(uint64_t *s, uint32_t L, uint32_t ks, uint32_t *s_big, uint32_t *s_nbig,
+                                          RddMarks &m) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) *s_nbig = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint32_t i = (uint32_t)r * RB + threadIdx.x;
+            m.x[r] = i < L ? s[i] : 0;
+        }
+        m.kind = 0;
+        bool any_long = false;
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint32_t i0 = (uint32_t)r * RB + 64u * (uint32_t)w, i = i0 + (uint32_t)lane;
+            const uint64_t x = m.x[r], k = x >> ks;
+            uint64_t xp = __shfl_up((unsigned long long)x, 1, 64), xn = __shfl_down((unsigned long long)x, 1, 64);
+            if (lane == 0 && i0 > 0 && i0 < L) xp = s[i0 - 1];     // the wave-round's outer neighbours
+            if (lane == 63 && i + 1 < L) xn = s[i + 1];
+            const bool valid = i < L;
+            const bool st = valid && (i == 0 || (xp >> ks) != k);
+            const bool en = valid && (i + 1 >= L || (xn >> ks) != k);
+            m.kind |= (st ? (en ? 1u : 2u) : 0u) << (2 * r);
+            if (pass == 0 && st && !en && i + kInsMax < L && (s[i + kInsMax] >> ks) == k) {   // > kInsMax
+                s_big[atomicAdd(s_nbig, 1u)] = i;
+                any_long = true;
+            }
+        }
+        (void)any_long;
+        __syncthreads();
+        const uint32_t nbig = *s_nbig;
+        if (pass == 1 || nbig == 0) return;              // (uniform)
+        for (uint32_t q = 0; q < nbig; ++q) {
+            const uint32_t r0 = s_big[q];
+            lds_rank_sort(s, r0, group_end(s, L, r0, ks) - r0);   // (barriers inside)
+        }
+    }
+}
+
 __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, size_t n,
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
-                                                      uint64_t *__restrict__ scratch, uint32_t *__restrict__ cnt) {
+                                                      uint64_t *__restrict__ scratch, uint32_t *__restrict__ cnt,
+                                                      int diag) {
     __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
-    const uint32_t ks = p.s0, tb = p.b0;                 // key bits from ks; tag bits from b0
+    const uint32_t ks = p.s0, tb = p.b0;                 // group bits from ks; tag bits from b0
     const size_t t = blockIdx.x, start = bounds[t], end = bounds[t + 1];
     const size_t len = end > start ? end - start : 0;
     uint32_t m = 0;
     if (len <= (size_t)RCAP) {
         uint64_t *s = s_raw + rdd_stage(c, start, (uint32_t)len, s_raw);
-        lds_sort_long(s, (uint32_t)len, ks, s_big, &s_nbig);
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < len; i += RB) m += or_mark(s, (uint32_t)len, i, ks, tb).emit ? 1u : 0u;
+        if (diag == 1) {                                 // timing diagnostic: staging only, no outputs
+            if (threadIdx.x == 0) cnt[t] = 0;
+            return;
+        }
+        RddMarks mk;
+        rdd_marks(s, (uint32_t)len, ks, s_big, &s_nbig, mk);
+        if (diag == 2) {                                 // timing diagnostic: + the marks
+            if (threadIdx.x == 0) cnt[t] = (uint32_t)mk.kind & 0;
+            return;
+        }
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint32_t kind = (mk.kind >> (2 * r)) & 3u;
+            if (kind == 1) {
+                ++m;
+            } else if (kind == 2) {
+                const uint32_t i = (uint32_t)r * RB + threadIdx.x;
+                m += group_distinct(s, i, group_end(s, (uint32_t)len, i, ks), tb);
+            }
+        }
     } else {
         sort_runs_global(c, n, start, end, ks, scratch, s_raw);
         __threadfence();
@@ -1191,16 +1243,13 @@ __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, s
     if (threadIdx.x == 0) cnt[t] = tot;
 }
 
-constexpr int RNW = (RCAP + 63) / 64;                    // emit bitmap words of an LDS tile
-
 __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict__ c, size_t n,
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
-                                                      crdt_tuples out, uint64_t *__restrict__ out_count) {
+                                                      crdt_tuples out, uint64_t *__restrict__ out_count, int diag) {
     __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
-    __shared__ uint64_t s_em[RNW];                       // emit bitmap, index order
-    __shared__ uint32_t s_pre[RNW];                      // emits before each word
+    __shared__ uint32_t s_c[RR * (RB / 64)];             // outputs per (round, wave), then their exclusive prefix
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
     const uint32_t ks = p.s0, tb = p.b0, sk = p.b0 + p.br + p.bt;
@@ -1248,53 +1297,86 @@ __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict_
     }
     const uint32_t L = (uint32_t)len;
     uint64_t *s = s_raw + rdd_stage(c, start, L, s_raw);
-    lds_sort_long(s, L, ks, s_big, &s_nbig);
-    __syncthreads();
-    // pass 1: marks; wave w's 64 elements of round r are bitmap word 4 r + w
-    constexpr int RR = (RCAP + RB - 1) / RB;
-    OrMark mk[RR];
+    if (diag == 1) return;                               // timing diagnostics (no stores)
+    RddMarks mk;
+    rdd_marks(s, L, ks, s_big, &s_nbig, mk);
+    if (diag == 2) return;
+    // pass 1: every element's output count and its exclusive prefix within
+    // the wave-round (mbcnt when every count is 0 / 1, else a shuffle scan)
+    uint32_t pre[RR];
 #pragma unroll
     for (int r = 0; r < RR; ++r) {
-        const uint32_t i = (uint32_t)r * RB + threadIdx.x;
-        mk[r].emit = false;
-        mk[r].rs = mk[r].re = 0;
-        mk[r].tomb = 0;
-        if (i < L) mk[r] = or_mark(s, L, i, ks, tb);
-        const uint64_t em = __ballot(mk[r].emit);
-        if (lane == 0 && (uint32_t)r * RB + 64u * w < L) s_em[r * (RB / 64) + w] = em;
+        const uint32_t kind = (mk.kind >> (2 * r)) & 3u, i = (uint32_t)r * RB + threadIdx.x;
+        const uint32_t cn = kind == 1 ? 1u : kind == 2 ? group_distinct(s, i, group_end(s, L, i, ks), tb) : 0u;
+        uint32_t ex, all;
+        if (__ballot(cn > 1) == 0) {
+            const uint64_t one = __ballot(cn == 1);
+            ex = __builtin_amdgcn_mbcnt_hi((uint32_t)(one >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)one, 0u));
+            all = (uint32_t)__popcll(one);
+        } else {
+            uint32_t x = cn;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            ex = x - cn;
+            all = (uint32_t)__shfl((int)x, 63, 64);
+        }
+        pre[r] = ex;
+        if (lane == 0) s_c[r * (RB / 64) + w] = all;
     }
     __syncthreads();
-    const uint32_t nw = (L + 63) / 64;
-    if (w == 0) {                                        // exclusive prefix of the word popcounts (nw <= 64)
-        const uint32_t pc = lane < (int)nw ? (uint32_t)__popcll(s_em[lane]) : 0u;
-        uint32_t x = pc;
+    if (diag == 3) return;
+    if (w == 0) {                                        // exclusive prefix over (round, wave), tile order
+        constexpr int NC = RR * (RB / 64);
+        static_assert(NC <= 64, "one wave");
+        const uint32_t c0 = lane < NC ? s_c[lane] : 0u;
+        uint32_t x = c0;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o, 64);
             if (lane >= o) x += y;
         }
-        if (lane < (int)nw) s_pre[lane] = x - pc;
+        if (lane < NC) s_c[lane] = x - c0;
     }
     __syncthreads();
-    auto before = [&](uint32_t i) -> uint32_t {          // emits at indices < i
-        const uint32_t q = i >> 6, b = i & 63;
-        return s_pre[q] + (b ? (uint32_t)__popcll(s_em[q] & ((1ULL << b) - 1ULL)) : 0u);
-    };
-    // pass 2: every emitting element at its rank
+    // pass 2: one-tuple groups store themselves; a longer group's first
+    // element stores the group's distinct tags in tag order
 #pragma unroll
     for (int r = 0; r < RR; ++r) {
+        const uint32_t kind = (mk.kind >> (2 * r)) & 3u;
+        if (!kind) continue;
         const uint32_t i = (uint32_t)r * RB + threadIdx.x;
-        if (i >= L || !mk[r].emit) continue;
-        const uint64_t x = s[i];
-        uint32_t o;
-        if (mk[r].re == 0) {
-            o = before(i);                               // a sorted long run: index order is tag order
-        } else {                                         // a short run: rank among its emitting tags
-            o = before(mk[r].rs);
-            for (uint32_t j = mk[r].rs; j < mk[r].re; ++j)
-                if (j != i && ((s_em[j >> 6] >> (j & 63)) & 1u) && (s[j] >> tb) < (x >> tb)) ++o;
+        const size_t o = base + s_c[r * (RB / 64) + w] + pre[r];
+        const uint64_t x = mk.x[r];
+        if (kind == 1) {
+            store(o, x, (uint32_t)(x & 1u));
+            continue;
         }
-        store(base + o, x, mk[r].tomb);
+        const uint32_t e = group_end(s, L, i, ks);
+        if (e - i > kInsMax) {                           // sorted long group: one walk
+            uint32_t q = 0;
+            for (uint32_t j = i; j < e;) {
+                const uint64_t y = s[j];
+                uint32_t tomb = (uint32_t)(y & 1u), k = j + 1;
+                for (; k < e && (s[k] >> tb) == (y >> tb); ++k) tomb |= (uint32_t)(s[k] & 1u);
+                store(o + q++, y, tomb);
+                j = k;
+            }
+            continue;
+        }
+        for (uint32_t j = i; j < e; ++j) {               // short group, input order: rank the first copies
+            if (!group_first(s, i, e, j, tb)) continue;
+            const uint64_t y = s[j];
+            uint32_t rk = 0, tomb = 0;
+            for (uint32_t k = i; k < e; ++k) {
+                const uint64_t z = s[k];
+                if ((z >> tb) == (y >> tb)) tomb |= (uint32_t)(z & 1u);
+                else if ((z >> tb) < (y >> tb) && group_first(s, i, e, k, tb)) ++rk;
+            }
+            store(o + rk, y, tomb);
+        }
     }
 }
 
@@ -1304,9 +1386,9 @@ static int or_run_dedup(crdt_ctx *ctx, uint64_t *c, size_t n, const SortPlan *pl
     const hipStream_t st = ctx->stream;
     const size_t nt = (n + RT - 1) / RT;
     k_run_bounds<<<(unsigned)((nt + 1 + 255) / 256), 256, 0, st>>>(c, n, plan, nt, bounds);
-    k_or_rdd_count<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, scratch, cnt);
+    k_or_rdd_count<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, scratch, cnt, g_rdd_diag);
     k_sort_colscan<<<1, CSB, 0, st>>>(cnt, (uint32_t)nt, loc, tot);
-    k_or_rdd_apply<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, loc, tot, out, out_count);
+    k_or_rdd_apply<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, loc, tot, out, out_count, g_rdd_diag);
     return check_launch(ctx);
 }
 
@@ -1352,7 +1434,7 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
     const unsigned nmm = launch_minmax(ctx, A, na, B, nb, mm);
-    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, g_or_key_sort || MODE == DD_LWW ? 1u : 0u);
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u);
     SortPlan h;
     hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -70,6 +70,14 @@ class Population:
         self.str_bytes = t(host["str_bytes"], np.uint8)
         self.str_off = t(host["str_off"], np.int64)
         self.state = None
+        # per-replica entry / kv-pair counts of the Diffs on the host: a round
+        # sizes the pulled arrays from them (no host round trip up front) and
+        # refreshes them in its one read-back at the end; None = unknown (after
+        # a local write), the round then reads the sizes back first
+        l_off = np.asarray(host["l_off"], dtype=np.int64)
+        l_kv = np.asarray(host["l_kv"], dtype=np.int64)
+        self._cnt = np.diff(l_off)
+        self._kvcnt = np.diff(l_kv[l_off])
         # kv arena of the next round: the current Diff's kv pairs are its
         # prefix (written there by the last round's gather), spare capacity
         # behind them takes the pulled pairs -- no copy of the Diff's pairs
@@ -77,10 +85,12 @@ class Population:
 
     def snapshot(self) -> tuple:
         """The population's Diffs (device views; a round never writes them)."""
-        return (self.off, self.ts, self.origin, self.kv_off, self.kv_key, self.kv_val, self._arena)
+        return (self.off, self.ts, self.origin, self.kv_off, self.kv_key, self.kv_val, self._arena, self._cnt,
+                self._kvcnt)
 
     def restore(self, snap: tuple) -> None:
-        (self.off, self.ts, self.origin, self.kv_off, self.kv_key, self.kv_val, self._arena) = snap
+        (self.off, self.ts, self.origin, self.kv_off, self.kv_key, self.kv_val, self._arena, self._cnt,
+         self._kvcnt) = snap
 
     # ---------------------------------------------------------------- helpers
     def _call(self, fn, *args):
@@ -187,8 +197,13 @@ class Population:
         r_off = self._seg_offsets(codes, self.off, b["off"])
         n_lkv = self.kv_key.numel()
         r_kb = self._seg_offsets(codes, a_kr, b_kr, base=n_lkv)   # where each replica's pulled kv pairs go
-        n_r, n_kv_end = (int(x) for x in torch.stack([r_off[-1], r_kb[-1]]).cpu())
-        n_rkv = n_kv_end - n_lkv
+        if imp is None and self._cnt is not None:          # sizes from the host counts: no read-back
+            pull = np.where(skip, 0, 1)
+            n_r = int((self._cnt[lq] * pull).sum())
+            n_rkv = int((self._kvcnt[lq] * pull).sum())
+        else:
+            n_r, n_kv_end = (int(x) for x in torch.stack([r_off[-1], r_kb[-1]]).cpu())
+            n_rkv = n_kv_end - n_lkv
         n_b = b["ts"].numel() if b["ts"] is not None else 0
         src_kr = torch.where(codes >= 0, a_kr[codes.clamp(min=0)],
                              b_kr[(-codes - 1).clamp(min=0)] if b_kr is not None else a_kr[0])
@@ -255,20 +270,23 @@ class Population:
                   "kv_key": arena_k[: n_lkv + n_rkv], "kv_val": arena_v[: n_lkv + n_rkv],
                   "str_bytes": self.str_bytes, "str_off": self.str_off}
         out = eng.refmerge_batch(packed)
-        # 3. the next Diff: entries from the merge, kv pairs gathered by src
-        n_out = int(out["off"][-1].item())
-        src = out["src"][:n_out].contiguous()
-        # offsets and kv gather in one pass; the arena size bounds the new Diff's kv count
-        # into fresh buffers with room behind the pairs for the next round's pulled pairs
-        # (a pull round moves about one population's worth of pairs; short capacity
-        # falls back to a copy into a new arena)
-        new_kv = torch.empty(n_out + 1, dtype=torch.int64, device=dev)
+        # 3. the next Diff: entries from the merge, kv pairs gathered by src.
+        # The entry count stays on the device (it bounds the gather, segments
+        # past it scan as empty); the arrays are sized for its upper bound
+        # |L| + |R|; ONE read-back at the end brings the new Diffs' entry and
+        # kv offsets per replica (the next round's sizes).  The fresh kv arena
+        # has room behind the pairs for the next round's pulled pairs.
+        n_max = self.ts.numel() + r_ts.numel()
+        new_kv = torch.empty(n_max + 1, dtype=torch.int64, device=dev)
         cap = 2 * max(n_lkv + n_rkv, 1)
         nk = torch.empty(cap, dtype=torch.int32, device=dev)
         nv = torch.empty(cap, dtype=torch.int32, device=dev)
-        self._call("crdt_seg_gather2", n_out, _p(src), _p(self.kv_off), _p(r_kv), 0, _p(new_kv), 4, _p(arena_k),
-                   _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
-        n_kv = int(new_kv[-1].item())
+        self._call("crdt_seg_gather2_n", n_max, _p(out["off"][self.P:]), _p(out["src"]), _p(self.kv_off), _p(r_kv),
+                   _p(new_kv), _p(arena_k), _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
+        ho = torch.cat([out["off"], new_kv[out["off"]]]).cpu().numpy()
+        n_out, n_kv = int(ho[self.P]), int(ho[-1])
+        self._cnt, self._kvcnt = np.diff(ho[: self.P + 1]), np.diff(ho[self.P + 1:])
+        new_kv = new_kv[: n_out + 1]
         self.kv_key, self.kv_val = nk[:n_kv], nv[:n_kv]
         self._arena = (nk, nv)
         self.kv_off = new_kv
@@ -307,6 +325,7 @@ class Population:
         self.kv_val = self._seg_copy(ecodes, self.kv_off, b_kv, kv, self.kv_val, b_val, m)
         self.kv_off, self.ts, self.origin = kv, ts, org
         self.off = d_off[0::2].contiguous()
+        self._cnt = self._kvcnt = None
 
     def empty_state(self) -> dict:
         """CurrentState with every key slot absent (NewServer with an empty
@@ -376,6 +395,7 @@ class Population:
         self.off = out["off"]
         self.ts = out["ts"][:n_out]
         self.origin = out["origin"][:n_out]
+        self._cnt = self._kvcnt = None
         return out["status"][: cmds["ts"].numel()].cpu().numpy().astype(np.int64)
 
     # ---------------------------------------------------------------- readback

@@ -515,6 +515,15 @@ int crdt_seg_gather2(crdt_ctx *ctx, size_t n_seg, const int64_t *code_dev, const
                      const uint64_t *b_off_dev, uint64_t base, uint64_t *dst_off_dev, size_t elem_size,
                      const void *a0_dev, const void *b0_dev, void *dst0_dev, const void *a1_dev,
                      const void *b1_dev, void *dst1_dev);
+/* crdt_seg_gather2 for 4-byte elements over the first *n_dev (device
+ * memory, <= n_max) of n_max segments, base 0: the count stays on the device
+ * (segments past it scan as empty, dst_off[i] = the total for i >= *n_dev),
+ * so a caller needs no host round trip between the merge that wrote the
+ * count and this gather (the gossip round's next-Diff kv pairs). */
+int crdt_seg_gather2_n(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code_dev,
+                       const uint64_t *a_off_dev, const uint64_t *b_off_dev, uint64_t *dst_off_dev,
+                       const uint32_t *a0_dev, const uint32_t *b0_dev, uint32_t *dst0_dev, const uint32_t *a1_dev,
+                       const uint32_t *b1_dev, uint32_t *dst1_dev);
 /* dst[dst_off[s] .. dst_off[s+1]) = val[s] */
 int crdt_seg_fill_u32(crdt_ctx *ctx, size_t n_seg, const uint64_t *dst_off_dev, const uint32_t *val_dev,
                       uint32_t *dst_dev);

@@ -137,3 +137,20 @@ def test_unsorted_run_lengths_around_the_mark_limit(eng):
     a = tuple(np.ascontiguousarray(x[~side]) for x in (key, ts, rep, tomb))
     b = tuple(np.ascontiguousarray(x[side]) for x in (key, ts, rep, tomb))
     _check(eng, a, b)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_unsorted_orset_sort_modes(eng, mode):
+    """sort.or_key_only: 0 the full tag sort + neighbour dedup; 1 key bits only,
+    key runs marked in LDS; 2 (default) the key and one more tag digit, groups
+    of equal sorted bits marked in LDS.  All == the oracle."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"sort.or_key_only", mode)
+    try:
+        ks = 30_000
+        _check(eng, synth.set_tuples(71, 0, 100_000, ks), synth.set_tuples(71, 1, 90_000, ks))
+        test_unsorted_cross_side_duplicates(eng)
+        test_unsorted_run_lengths_around_the_mark_limit(eng)
+        test_unsorted_single_tag(eng, 5000)
+    finally:
+        _lib.call("crdt_set_option", b"sort.or_key_only", 2)

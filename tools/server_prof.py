@@ -15,7 +15,8 @@ from crdt_amd import engine as E  # noqa: E402
 
 def main():
     eng = E.Engine(0)
-    wl = bench.ServerMerge(eng, 0, 1, 5, 10_000)
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    wl = bench.ServerMerge(eng, 0, 1, reps, 10_000)
     t_in, t_m = [], []
     for _ in range(30):
         t0 = time.perf_counter()
