@@ -813,6 +813,8 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
     uint64_t em[DI];
     CKey<WORDS> v[DI];
     uint8_t tb[DI];                               // output tomb; bit 1: the tag run continues (rare walk)
+    constexpr bool SEG = MODE == DD_LWW && WORDS == 1;
+    uint64_t mxr[SEG ? DI : 1];                   // LWW, one word: max of c ^ 3 over the key run's part in the wave-round
     dd_load<WORDS>(c, n, base, v, s_x);
     if constexpr (MODE == DD_LWW)
 #pragma unroll
@@ -833,7 +835,25 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
             const uint32_t kb = p.b0 + p.br + p.bt;
             f = valid && (!has_next || !eq_from(v[r], nx, kb));
             // bit 1: an earlier tuple of the same key -- the emit walks the run
-            tb[r] = (uint8_t)((v[r].w[0] & 1u) | (valid && has_prev && eq_from(pv, v[r], kb) ? 2u : 0u));
+            const bool cont = valid && has_prev && eq_from(pv, v[r], kb);
+            tb[r] = (uint8_t)((v[r].w[0] & 1u) | (cont ? 2u : 0u));
+            if constexpr (SEG) {
+                // the run's max of c ^ 3 by a segmented max-scan over the
+                // wave-round's 64 consecutive tuples (shuffles, no walk); bit
+                // 2: the run began before the wave-round (its earlier part is
+                // walked from LDS, at most one run per wave-round)
+                const uint64_t S = __ballot(!cont);
+                const uint64_t sm = S & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+                const int head = sm ? 63 - __clzll((long long)sm) : -1;
+                uint64_t mx = v[r].w[0] ^ 3u;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint64_t y = __shfl_up((unsigned long long)mx, d, 64);
+                    if (lane >= d && lane - d >= head) mx = y > mx ? y : mx;
+                }
+                mxr[r] = mx;
+                if (head < 0 && cont) tb[r] |= 4u;
+            }
         } else {
             f = valid && !(has_prev && eq_from(pv, v[r], p.b0));     // the first copy of its tag
             tb[r] = (uint8_t)((v[r].w[0] & 1u) | (same_next ? 2u : 0u));
@@ -872,13 +892,14 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
                 // 64-bit max; the tile's part from LDS, the rest from global memory
                 const uint32_t kb = p.b0 + p.br + p.bt;
                 const uint64_t key = v[r].w[0] >> kb;
-                uint64_t mx = v[r].w[0] ^ 3u;
-                for (size_t j = e; j > 0;) {
-                    --j;
-                    const uint64_t x = j >= base ? s_v[j - base] : c[j];
-                    if ((x >> kb) != key) break;
-                    mx = (x ^ 3u) > mx ? x ^ 3u : mx;
-                }
+                uint64_t mx = mxr[r];
+                if (tb[r] & 4u)                           // the run's part before the wave-round
+                    for (size_t j = e - (size_t)lane; j > 0;) {
+                        --j;
+                        const uint64_t x = j >= base ? s_v[j - base] : c[j];
+                        if ((x >> kb) != key) break;
+                        mx = (x ^ 3u) > mx ? x ^ 3u : mx;
+                    }
                 win.w[0] = mx ^ 3u;
                 tomb = (uint8_t)(win.w[0] & 1u);
             } else if constexpr (MODE == DD_LWW) {
@@ -1157,8 +1178,8 @@ __device__ uint32_t group_distinct(const uint64_t *s, uint32_t g0, uint32_t e, u
 constexpr int RR = (RCAP + RB - 1) / RB;                 // wave-rounds per thread
 struct RddMarks {
     uint64_t x[RR];
-    uint32_t kind;                                       // 2 bits per round: 1 one-tuple group, 2 a longer group's first
-};
+    uint32_t kind;                                       // 2 bits per round: 1 one-tuple group, 2 a pair's first
+};                                                       // (its mate in the next lane), 3 a longer group's first
 __device__ __forceinline__ void rdd_marks(uint64_t *s, uint32_t L, uint32_t ks, uint32_t *s_big, uint32_t *s_nbig,
                                           RddMarks &m) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1181,7 +1202,11 @@ __device__ __forceinline__ void rdd_marks(uint64_t *s, uint32_t L, uint32_t ks, 
             const bool valid = i < L;
             const bool st = valid && (i == 0 || (xp >> ks) != k);
             const bool en = valid && (i + 1 >= L || (xn >> ks) != k);
-            m.kind |= (st ? (en ? 1u : 2u) : 0u) << (2 * r);
+            // a pair: the group is this lane's element and the next lane's (the
+            // common longer group: an A tuple and its B copy)
+            const bool en1 = ((__ballot(en) >> 1) >> lane) & 1u;   // the next lane ends a group
+            const uint32_t kd = !st ? 0u : en ? 1u : (lane < 63 && en1) ? 2u : 3u;
+            m.kind |= kd << (2 * r);
             if (pass == 0 && st && !en && i + kInsMax < L && (s[i + kInsMax] >> ks) == k) {   // > kInsMax
                 s_big[atomicAdd(s_nbig, 1u)] = i;
                 any_long = true;
@@ -1225,9 +1250,12 @@ __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, s
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
             const uint32_t kind = (mk.kind >> (2 * r)) & 3u;
+            const uint64_t x1 = __shfl_down((unsigned long long)mk.x[r], 1, 64);   // (uniform)
             if (kind == 1) {
                 ++m;
             } else if (kind == 2) {
+                m += (mk.x[r] >> tb) == (x1 >> tb) ? 1u : 2u;
+            } else if (kind == 3) {
                 const uint32_t i = (uint32_t)r * RB + threadIdx.x;
                 m += group_distinct(s, i, group_end(s, (uint32_t)len, i, ks), tb);
             }
@@ -1307,7 +1335,9 @@ __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict_
 #pragma unroll
     for (int r = 0; r < RR; ++r) {
         const uint32_t kind = (mk.kind >> (2 * r)) & 3u, i = (uint32_t)r * RB + threadIdx.x;
-        const uint32_t cn = kind == 1 ? 1u : kind == 2 ? group_distinct(s, i, group_end(s, L, i, ks), tb) : 0u;
+        const uint64_t x1 = __shfl_down((unsigned long long)mk.x[r], 1, 64);   // (uniform)
+        uint32_t cn = kind == 1 ? 1u : kind == 2 ? ((mk.x[r] >> tb) == (x1 >> tb) ? 1u : 2u) : 0u;
+        if (kind == 3) cn = group_distinct(s, i, group_end(s, L, i, ks), tb);
         uint32_t ex, all;
         if (__ballot(cn > 1) == 0) {
             const uint64_t one = __ballot(cn == 1);
@@ -1346,12 +1376,23 @@ __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict_
 #pragma unroll
     for (int r = 0; r < RR; ++r) {
         const uint32_t kind = (mk.kind >> (2 * r)) & 3u;
+        const uint64_t x1 = __shfl_down((unsigned long long)mk.x[r], 1, 64);   // (uniform)
         if (!kind) continue;
         const uint32_t i = (uint32_t)r * RB + threadIdx.x;
         const size_t o = base + s_c[r * (RB / 64) + w] + pre[r];
         const uint64_t x = mk.x[r];
         if (kind == 1) {
             store(o, x, (uint32_t)(x & 1u));
+            continue;
+        }
+        if (kind == 2) {                                 // a pair, from registers
+            if ((x >> tb) == (x1 >> tb)) {
+                store(o, x < x1 ? x : x1, (uint32_t)((x | x1) & 1u));
+            } else {
+                const uint64_t lo = x < x1 ? x : x1, hi = x < x1 ? x1 : x;
+                store(o, lo, (uint32_t)(lo & 1u));
+                store(o + 1, hi, (uint32_t)(hi & 1u));
+            }
             continue;
         }
         const uint32_t e = group_end(s, L, i, ks);

@@ -78,6 +78,9 @@ class Population:
         l_kv = np.asarray(host["l_kv"], dtype=np.int64)
         self._cnt = np.diff(l_off)
         self._kvcnt = np.diff(l_kv[l_off])
+        if len(l_kv) and l_kv[0] != 0:                     # the fast path assumes kv ranges from 0
+            self._cnt = self._kvcnt = None
+        self._pin = None                                   # pinned staging of a round's per-replica arrays
         # kv arena of the next round: the current Diff's kv pairs are its
         # prefix (written there by the last round's gather), spare capacity
         # behind them takes the pulled pairs -- no copy of the Diff's pairs
@@ -160,6 +163,8 @@ class Population:
         peers = np.asarray(peers, dtype=np.int64)
         assert len(peers) == self.P
         skip = peers < 0
+        if imp is None and self._cnt is not None and not skip.any():
+            return self._round_local(peers - self.first)
         if imp is None:
             lq = np.where(skip, np.arange(self.P) + self.first, peers) - self.first
             assert np.all((lq >= 0) & (lq < self.P)), "peer not on this rank: pass an import block"
@@ -227,6 +232,52 @@ class Population:
             for k in ("st_kind", "st_str", "st_sum"):
                 self.state[k][sl] = prev_state[k][sl]
         return out
+
+    def _round_local(self, lq: np.ndarray) -> dict:
+        """round() when every peer is on this rank, none is dead, and the
+        per-replica counts are on the host: the per-replica arrays of the
+        pull assembly (source codes, R entry and kv offsets, kv re-basing
+        deltas, slot deltas) are computed on the host and uploaded in one
+        pinned asynchronous copy -- no scans or index kernels on the device,
+        no host round trip before the merge."""
+        P, K, dev = self.P, self.K, self.eng.device
+        assert np.all((lq >= 0) & (lq < P)), "peer not on this rank: pass an import block"
+        n_lkv = self.kv_key.numel()
+        cnt, kvc = self._cnt[lq], self._kvcnt[lq]
+        n_r, n_rkv = int(cnt.sum()), int(kvc.sum())
+        # int64 fields: codes P | a_kr P+1 | r_off P+1 | r_kb P+1 | kdelta P | delta (int32, P)
+        n64 = 5 * P + 3 + (P + 1) // 2
+        if self._pin is None or self._pin.numel() < n64:
+            self._pin = torch.empty(n64, dtype=torch.int64).pin_memory()
+        h = self._pin.numpy()
+        h[:P] = lq
+        a_kr = h[P:2 * P + 1]
+        a_kr[0] = 0
+        np.cumsum(self._kvcnt, out=a_kr[1:])
+        r_off = h[2 * P + 1:3 * P + 2]
+        r_off[0] = 0
+        np.cumsum(cnt, out=r_off[1:])
+        r_kb = h[3 * P + 2:4 * P + 3]
+        r_kb[0] = n_lkv
+        np.cumsum(kvc, out=r_kb[1:])
+        r_kb[1:] += n_lkv
+        h[4 * P + 3:5 * P + 3] = r_kb[:-1] - a_kr[lq]
+        h[5 * P + 3:].view(np.int32)[:P] = (((np.arange(P, dtype=np.int64) - lq) * K) % (1 << 32)).astype(
+            np.uint32).view(np.int32)
+        d = self._pin[:n64].to(dev, non_blocking=True)
+        codes, a_kr_d, r_off_d, r_kb_d = d[:P], d[P:2 * P + 1], d[2 * P + 1:3 * P + 2], d[3 * P + 2:4 * P + 3]
+        kdelta = d[4 * P + 3:5 * P + 3]
+        delta = d[5 * P + 3:].view(torch.int32)[:P]
+        r_kv = torch.empty(n_r + 1, dtype=torch.int64, device=dev)
+        r_ts = torch.empty(n_r, dtype=torch.int64, device=dev)
+        r_kv[n_r:].copy_(r_kb_d[-1:])
+        arena_k, arena_v = self._kv_arena(n_lkv, n_rkv)
+        if n_r:
+            self._call("crdt_seg_copy2", P, _p(codes), _p(self.off), None, _p(r_off_d), 8,
+                       _p(self.kv_off), None, _p(r_kv), _p(kdelta), _p(self.ts), None, _p(r_ts), 1)
+            self._call("crdt_seg_copy2", P, _p(codes), _p(a_kr_d), None, _p(r_kb_d), 4,
+                       _p(self.kv_key), None, _p(arena_k), _p(delta), _p(self.kv_val), None, _p(arena_v), 1)
+        return self._merge_round(r_off_d, r_ts, r_kv, arena_k, arena_v, n_lkv, n_rkv)
 
     def _kv_arena(self, n_lkv: int, n_more: int):
         """A kv arena whose prefix is the Diff's pairs, with room for n_more."""

@@ -5,14 +5,13 @@ RemoteDiff cut at the same ts splitters, kv pairs carried along); each shard
 runs the per-rank steps of crdt_amd.shard.sharded_refmerge, with the
 all-reduces done here across the W shard results; the concatenated new-Diff
 slices and the reduced CurrentState must equal the unsharded merge bit for
-bit (the unsharded merge itself is pinned to the oracle by
-test_gpu_refmerge.py)."""
+bit, and that unsharded merge == the oracle per replica in the same test."""
 import numpy as np
 import pytest
 import torch
 
 from crdt_amd import refmerge, synth
-from refmerge_util import split_ts_range as _split, ts_splitters
+from refmerge_util import assert_batch_matches_oracle, split_ts_range as _split, ts_splitters
 
 pytestmark = pytest.mark.gpu
 
@@ -38,6 +37,7 @@ def _run_sharded(eng, shards):
 def test_ts_range_sharded_refmerge_equals_unsharded(eng, world):
     h = synth.refmerge_packed(41, 64, 3000)
     full = eng.refmerge_batch(refmerge.to_device(h, eng.device))
+    assert_batch_matches_oracle(h, full)                     # the reference result itself == the oracle
     spl = ts_splitters(h, world)
     shards = [_split(h, spl[r], spl[r + 1]) for r in range(world)]
     # the top shard's exclusive end must not lose ts == INT64_MAX (none in this data)
@@ -80,6 +80,7 @@ def test_sharded_refmerge_single_rank_is_plain_merge(eng):
     h = synth.refmerge_packed(5, 16, 2000)
     d = refmerge.to_device(h, eng.device)
     full = eng.refmerge_batch(d)
+    assert_batch_matches_oracle(h, full)
     got = shard.sharded_refmerge(eng, d)
     for k in ("off", "ts", "origin", "src", "st_kind"):
         n = int(full["off"][-1]) if k in ("ts", "origin", "src") else None

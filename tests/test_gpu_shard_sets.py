@@ -1,7 +1,8 @@
 """GPU: key-range sharding of the set merges -- the device
 lower_bound behind the shard slices, and the per-rank merges of a W-way
-key-range split concatenated in rank order == the unsharded merge, bit for
-bit (the all-gather-v step is covered on CPU by test_shard_gloo.py)."""
+key-range split concatenated in rank order == the oracle's merge of the whole
+sides, bit for bit (the all-gather-v step is covered on CPU by
+test_shard_gloo.py)."""
 import numpy as np
 import pytest
 import torch
@@ -9,6 +10,7 @@ import torch
 from crdt_amd import shard, synth
 from crdt_amd.engine import TupleSet, u64_tensor
 
+from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 
@@ -52,7 +54,7 @@ def test_key_range_shards_concat_to_full_merge(eng, kind, world, lww):
     sa, sb = _sets(kind)
     A = TupleSet.from_numpy(*sa, eng.device)
     B = TupleSet.from_numpy(*sb, eng.device)
-    full = (eng.lww_merge if lww else eng.orset_merge)(A, B).to_numpy()
+    full = (oracle.lww_merge if lww else oracle.orset_merge)(sa, sb)       # the oracle, not the unsharded GPU merge
     samples = torch.cat([shard.sample_keys(A, 256), shard.sample_keys(B, 256)]).cpu().numpy().view(np.uint64)
     spl = shard.splitters_from_samples(samples, world)
     parts = [shard.merge_key_range(eng, A, B, spl[r], spl[r + 1], lww).to_numpy() for r in range(world)]
@@ -70,7 +72,7 @@ def test_splitters_on_exact_keys_and_empty_ranges(eng):
     spl = [0, int(k[1000]), int(k[1000]), int(k[50_000]) + 1, int(k[-1]), shard.KEY_END]   # equal + exact keys
     parts = [shard.merge_key_range(eng, A, B, spl[r], spl[r + 1]).to_numpy() for r in range(len(spl) - 1)]
     assert len(parts[1][0]) == 0
-    for g, e in zip(_cat(parts), eng.lww_merge(A, B).to_numpy()):
+    for g, e in zip(_cat(parts), oracle.lww_merge(sa, sb)):
         np.testing.assert_array_equal(g, e)
 
 
@@ -79,5 +81,5 @@ def test_sharded_set_merge_single_rank(eng):
     A = TupleSet.from_numpy(*sa, eng.device)
     B = TupleSet.from_numpy(*sb, eng.device)
     got = shard.sharded_set_merge(eng, A, B, lww=False).to_numpy()
-    for g, e in zip(got, eng.orset_merge(A, B).to_numpy()):
+    for g, e in zip(got, oracle.orset_merge(sa, sb)):
         np.testing.assert_array_equal(g, e)

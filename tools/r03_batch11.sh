@@ -1,7 +1,7 @@
 #!/bin/bash
 # gossip rounds with one read-back per round: their GPU tests, then the bench lines
 mkdir -p gpurun_out/gos
-timeout -k 10 600 python -u -m pytest tests/test_gpu_gossip.py tests/test_gpu_multirank.py tests/test_gpu_seg.py tests/test_gpu_codec.py -m gpu -x -q \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_gossip.py tests/test_gpu_multirank.py tests/test_gpu_seg.py tests/test_gpu_codec.py tests/test_gpu_shard_sets.py tests/test_gpu_shard_refmerge.py -m gpu -x -q \
   --timeout 300 --timeout-method thread > gpurun_out/gos/tests.log 2>&1
 rc=$?; tail -3 gpurun_out/gos/tests.log
 if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error" gpurun_out/gos/tests.log | head -30; exit $rc; fi
