@@ -22,6 +22,8 @@ int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within 
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
+int g_set_xcd = 0;
+int g_rm_xcd = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_rdd_diag = 0;
@@ -297,6 +299,12 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 2 key + 1-2 tag digits, 1 key-only sort, 0 full tag sort
         if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_or_key_sort = (int)v;
+    } else if (!strcmp(name, "sets.xcd_tiles")) {    // D1 count / write passes: 1 XCD-contiguous tile ranges
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_set_xcd = (int)v;
+    } else if (!strcmp(name, "refmerge.xcd_tiles")) {   // RefMerge count / tile passes: 1 XCD-contiguous tiles
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_rm_xcd = (int)v;
     } else if (!strcmp(name, "sort.xcd_tiles")) {    // radix scatter pass: 1 XCD-contiguous tile ranges, 0 blockIdx order
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sort_xcd = (int)v;
