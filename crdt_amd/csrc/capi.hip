@@ -22,8 +22,6 @@ int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within 
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
-int g_set_xcd = 0;
-int g_rm_xcd = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_rdd_diag = 0;
@@ -299,20 +297,14 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 2 key + 1-2 tag digits, 1 key-only sort, 0 full tag sort
         if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_or_key_sort = (int)v;
-    } else if (!strcmp(name, "sets.xcd_tiles")) {    // D1 count / write passes: 1 XCD-contiguous tile ranges
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_set_xcd = (int)v;
-    } else if (!strcmp(name, "refmerge.xcd_tiles")) {   // RefMerge count / tile passes: 1 XCD-contiguous tiles
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_rm_xcd = (int)v;
     } else if (!strcmp(name, "sort.xcd_tiles")) {    // radix scatter pass: 1 XCD-contiguous tile ranges, 0 blockIdx order
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sort_xcd = (int)v;
     } else if (!strcmp(name, "sort.mm_blocks_per_cu")) {   // sort minmax grid: workgroups per CU per input
         if (v < 1 || v > 16) return CRDT_E_INVAL;
         g_mm_bpc = (int)v;
-    } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: OR-Set D2 dedup stops after 1 staging,
-        if (v < 0 || v > 3) return CRDT_E_INVAL;       //   2 marks, 3 counts (wrong output; never stores)
+    } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: the D2 dedup apply (OR-Set: and count)
+        if (v < 0 || v > 3) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores)
         g_rdd_diag = (int)v;
     } else if (!strcmp(name, "sort.vec_up")) {       // fused D2 sort: 1 vectorised composing upsweep, 0 scalar
         if (v != 0 && v != 1) return CRDT_E_INVAL;

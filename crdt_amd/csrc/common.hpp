@@ -58,8 +58,6 @@ extern FoldTuning g_fold;
 extern int g_vclock_pairs_per_wave;
 extern int g_vclock_blocks_per_cu;
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
-extern int g_set_xcd;           // D1 count / write passes: XCD-contiguous tiles (sets.xcd_tiles)
-extern int g_rm_xcd;            // RefMerge count / tile passes: XCD-contiguous tiles (refmerge.xcd_tiles)
 extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
 extern int g_sort_vec_up;
 extern int g_mm_bpc;

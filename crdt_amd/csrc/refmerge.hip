@@ -399,12 +399,12 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
-                                                 uint32_t *__restrict__ zero, int dma, int xcd = 0) {
+                                                 uint32_t *__restrict__ zero, int dma) {
     constexpr int NI = MT / NT, LPW = 64 / NI;           // items per thread, lanes per bitmap word
     static_assert(NI * LPW == 64, "a bitmap word is LPW lanes' items");
     __shared__ alignas(16) int64_t sm[MT + 8];           // (DMA: each run from its 16-byte aligned-down start)
     __shared__ uint32_t s_w[NT / 64];
-    const uint64_t t = xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x;   // (refmerge.xcd_tiles)
+    const uint64_t t = blockIdx.x;
     if (zero && t == 0 && threadIdx.x == 0) *zero = 0;   // (the delta fold's overflow flag)
     const TileDesc d = desc[t], dn = desc[t + 1];
     uint32_t na, nb;
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
                                                 const uint64_t *__restrict__ ic, crdt_refmerge_out out,
                                                 crdt_replay_state st, RpCand *__restrict__ cand,
                                                 uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf,
-                                                uint32_t *__restrict__ err, int xcd = 0) {
+                                                uint32_t *__restrict__ err) {
     // PARTS > 1: each workgroup takes 1/PARTS of the tile's items (words
     // WPP h .. WPP h + WPP - 1) with FB / PARTS threads and its own slot table
     constexpr int WT = FB / PARTS, NWV = WT / 64, WPP = NW / PARTS;   // threads, waves, words per workgroup
@@ -509,9 +509,8 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
     __shared__ uint32_t t_npar[TN];
     __shared__ int64_t s_okval[FOLDS ? OKC : 1];
     __shared__ uint8_t s_okok[FOLDS ? OKC : 1];
-    const uint32_t bx = xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x;   // (refmerge.xcd_tiles)
-    const uint64_t t = bx / PARTS;
-    const int part = (int)(bx % PARTS);
+    const uint64_t t = blockIdx.x / PARTS;
+    const int part = (int)(blockIdx.x % PARTS);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     // the descriptors, the tile's bitmap words (one of each bitmap per lane),
     // its offset and the staged Atoi records are independent loads: all issued
@@ -1014,7 +1013,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // (count-pass shapes at 4096-item tiles: 256 x 16 51 us, 512 x 8 45 us, 1024 x 4 67 us)
     // LDS-DMA staging of the ts runs when both logs are 8-byte aligned (refmerge.count_dma)
     const int cdma = g_rm_count_dma && !((((uintptr_t)in.l_ts) | ((uintptr_t)in.r_ts)) & 7);
-    k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma, g_rm_xcd);
+    k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma);
     rc = check_launch(ctx);
     if (rc) return rc;
     // (a completion ticket letting the count pass's last block do this scan
@@ -1035,7 +1034,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     const unsigned tg = (unsigned)tmax;
     if (delta && ns) {                                            // incremental replay: fold only the inserted R
         k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, 0, ic, out, *delta, cand, cand_n,
-                                                   ovf, ctx->dev_status, g_rm_xcd);
+                                                   ovf, ctx->dev_status);
         rc = check_launch(ctx);
         if (rc) return rc;
         k_rp_holder<<<tg, 64, 0, s>>>(in, r_dk, *delta, cand, cand_n, ovf, tmax);   // the candidates' holders
@@ -1046,7 +1045,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
 #define RM_TILE(F, P, DIAG)                                                                                   \
     k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out, crdt_replay_state{}, \
-                                              nullptr, nullptr, nullptr, ctx->dev_status, g_rm_xcd)
+                                              nullptr, nullptr, nullptr, ctx->dev_status)
     if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
         if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, 0);
         else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, 0);

@@ -158,11 +158,11 @@ __device__ __forceinline__ LwwTile lww_tile(const uint64_t *__restrict__ split, 
 __global__ __launch_bounds__(LCB) void k_lww_count(const uint64_t *__restrict__ ka, const uint64_t *__restrict__ kb,
                                                    size_t na, size_t nb, const uint64_t *__restrict__ split,
                                                    uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
-                                                   uint64_t t0, int xcd = 0) {
+                                                   uint64_t t0) {
     constexpr int NI = LT / LCB, LPW = 64 / NI;
     __shared__ alignas(16) uint64_t sk[LT + 8];          // A's run, then B's, each from its 16-byte aligned-down start
     __shared__ uint32_t s_w[LCB / 64];
-    const uint64_t t = t0 + (xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x);   // (sets.xcd_tiles)
+    const uint64_t t = t0 + blockIdx.x;
     const LwwTile b = lww_tile(split, t, na + nb);
     const int lane0 = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t at = 0;
@@ -306,8 +306,7 @@ template <int WH = LWH, int WT = LWT>
 __global__ __launch_bounds__(WT) void k_lww_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
                                                   const uint64_t *__restrict__ split,
                                                   const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
-                                                  crdt_tuples out, uint64_t t0, uint32_t *__restrict__ err,
-                                                  int xcd = 0) {
+                                                  crdt_tuples out, uint64_t t0, uint32_t *__restrict__ err) {
     constexpr int NWV = WT / 64, FI = (WH / 64) / NWV, CAP = WH + 3, P = LT / WH, WPP = LNW / P;
     static_assert(LNW == 64 && WH * P == LT && FI * NWV * 64 == WH && WH == 4 * WT, "shape");
     // (each field holds A's run then B's, each from its 16-byte aligned-down
@@ -316,9 +315,8 @@ __global__ __launch_bounds__(WT) void k_lww_write(crdt_tuples A, crdt_tuples B, 
     __shared__ alignas(16) uint64_t s_ts[CAP + 8];
     __shared__ alignas(16) uint32_t s_rep[CAP + 16];
     __shared__ alignas(16) uint8_t s_tomb[CAP + 64];
-    const uint32_t bx = xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x;   // (sets.xcd_tiles)
-    const uint64_t t = t0 + bx / P;
-    const uint32_t h = bx % P;
+    const uint64_t t = t0 + blockIdx.x / P;
+    const uint32_t h = blockIdx.x % P;
     const LwwTile b = lww_tile(split, t, na + nb);
     const int lane = threadIdx.x & 63;
     const uint64_t word_a = bits[t * 2 * LNW + lane], word_e = bits[t * 2 * LNW + LNW + lane];
@@ -337,7 +335,7 @@ __global__ __launch_bounds__(WT) void k_lww_write(crdt_tuples A, crdt_tuples B, 
     // every index below derives from the bitmaps: a tile whose bitmaps do not
     // describe its counts raises CRDT_DEV_RANGE instead of reading out of range
     if (!bitmaps_consistent(word_a, word_e, pre_a, LNW, b.na, b.n, lane)) {
-        if (threadIdx.x == 0 && h == 0) atomicOr(err, CRDT_DEV_RANGE);
+        if (threadIdx.x == 0 && blockIdx.x % P == 0) atomicOr(err, CRDT_DEV_RANGE);
         return;
     }
     // the half's runs: A [ra, ra + ca), B [rb, rb + cb); staged from ra - 2 / rb - 1
@@ -630,12 +628,12 @@ __global__ __launch_bounds__(NT) void k_or_count(crdt_tuples A, crdt_tuples B, s
 template <int NT>
 __global__ __launch_bounds__(NT) void k_or_count_dma(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
                                                      const uint64_t *__restrict__ split, uint32_t *__restrict__ tcnt,
-                                                     uint64_t *__restrict__ bits, uint64_t t0, int xcd = 0) {
+                                                     uint64_t *__restrict__ bits, uint64_t t0) {
     constexpr int NI = OT / NT, LPW = 64 / NI, CAP = OT + 2;
     __shared__ alignas(16) uint64_t sk[CAP + 8], st[CAP + 8];
     __shared__ alignas(16) uint32_t sr[CAP + 16];
     __shared__ uint32_t s_w[NT / 64];
-    const uint64_t t = t0 + (xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x);   // (sets.xcd_tiles)
+    const uint64_t t = t0 + blockIdx.x;
     const LwwTile b = or_tile(split, t, na + nb);
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
     // each side from the element before the tile (when there is one): element
@@ -722,17 +720,15 @@ template <int WH = OT, int WT = OWT>
 __global__ __launch_bounds__(WT) void k_or_write(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
                                                  const uint64_t *__restrict__ split,
                                                  const uint64_t *__restrict__ bits, const uint64_t *__restrict__ ic,
-                                                 crdt_tuples out, uint64_t t0, uint32_t *__restrict__ err,
-                                                 int xcd = 0) {
+                                                 crdt_tuples out, uint64_t t0, uint32_t *__restrict__ err) {
     constexpr int NWV = WT / 64, P = OT / WH, WPP = ONW / P, FI = WPP / NWV, CAP = WH + 2;
     static_assert(FI * NWV == WPP && WH * P == OT && ONW <= 64 && WH == 4 * WT, "shape");
     __shared__ alignas(16) uint64_t s_key[CAP + 8];
     __shared__ alignas(16) uint64_t s_ts[CAP + 8];
     __shared__ alignas(16) uint32_t s_rep[CAP + 16];
     __shared__ alignas(16) uint8_t s_tomb[CAP + 64];
-    const uint32_t bx = xcd ? xcd_contig(blockIdx.x, gridDim.x) : blockIdx.x;   // (sets.xcd_tiles)
-    const uint64_t t = t0 + bx / P;
-    const uint32_t h = bx % P;
+    const uint64_t t = t0 + blockIdx.x / P;
+    const uint32_t h = blockIdx.x % P;
     const LwwTile b = or_tile(split, t, na + nb);
     const int lane = threadIdx.x & 63;
     const bool wl_ok = lane < ONW;
@@ -751,7 +747,7 @@ __global__ __launch_bounds__(WT) void k_or_write(crdt_tuples A, crdt_tuples B, s
     pre_a -= (uint32_t)__popcll(word_a);
     pre_e -= (uint32_t)__popcll(word_e);
     if (!bitmaps_consistent(word_a, word_e, pre_a, ONW, b.na, b.n, lane)) {   // (see k_lww_write)
-        if (threadIdx.x == 0 && h == 0) atomicOr(err, CRDT_DEV_RANGE);
+        if (threadIdx.x == 0 && blockIdx.x % P == 0) atomicOr(err, CRDT_DEV_RANGE);
         return;
     }
     // the part's runs: A [pa0, pa0 + ca), B [pb0, pb0 + cb) (tile-relative)
@@ -914,17 +910,17 @@ static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, con
     // write-pass workgroups per tile (sets.lww_parts): 1/P of a tile's items, 4 per thread
     const unsigned P = (unsigned)g_lww_parts;
     auto cnt = [&](size_t t0, uint32_t nt, hipStream_t s) {
-        k_lww_count<<<nt, LCB, 0, s>>>(ka, kb, na, nb, split, tcnt, bits, t0, g_set_xcd);
+        k_lww_count<<<nt, LCB, 0, s>>>(ka, kb, na, nb, split, tcnt, bits, t0);
     };
     auto scn = [&](size_t t0, uint32_t nt, uint64_t *c, hipStream_t s) {
         k_chunk_scan<<<1, 1024, 0, s>>>(tcnt, t0, nt, ic, c);
     };
     auto wr = [&](size_t t0, uint32_t nt, hipStream_t s) {
         const unsigned g = P * nt;
-        if (P == 2) k_lww_write<2048, 512><<<g, 512, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
-        else if (P == 8) k_lww_write<512, 128><<<g, 128, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
-        else if (P == 16) k_lww_write<256, 64><<<g, 64, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
-        else k_lww_write<1024, 256><<<g, 256, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
+        if (P == 2) k_lww_write<2048, 512><<<g, 512, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
+        else if (P == 8) k_lww_write<512, 128><<<g, 128, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
+        else if (P == 16) k_lww_write<256, 64><<<g, 64, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
+        else k_lww_write<1024, 256><<<g, 256, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
     };
     return two_pass(ctx, ntiles, out_count, cnt, scn, wr, (size_t)g_lww_chunk, take_fail_zero_bits(), bits,
                     ntiles * 2 * LNW * 8);
@@ -950,7 +946,7 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
     // write-pass workgroups per tile (sets.or_parts): 1/P of a tile's items, 4 per thread
     const unsigned P = (unsigned)g_or_parts;
     auto cnt = [&](size_t t0, uint32_t nt, hipStream_t s) {
-        if (g_or_count_dma) k_or_count_dma<OCB><<<nt, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits, t0, g_set_xcd);
+        if (g_or_count_dma) k_or_count_dma<OCB><<<nt, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits, t0);
         else k_or_count<OCB><<<nt, OCB, 0, s>>>(A, B, na, nb, split, tcnt, bits, t0);
     };
     auto scn = [&](size_t t0, uint32_t nt, uint64_t *c, hipStream_t s) {
@@ -958,9 +954,9 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
     };
     auto wr = [&](size_t t0, uint32_t nt, hipStream_t s) {
         const unsigned g = P * nt;
-        if (P == 2) k_or_write<1024, 256><<<g, 256, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
-        else if (P == 4) k_or_write<512, 128><<<g, 128, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
-        else k_or_write<2048, 512><<<g, 512, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err, g_set_xcd);
+        if (P == 2) k_or_write<1024, 256><<<g, 256, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
+        else if (P == 4) k_or_write<512, 128><<<g, 128, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
+        else k_or_write<2048, 512><<<g, 512, 0, s>>>(A, B, na, nb, split, bits, ic, O, t0, err);
     };
     return two_pass(ctx, ntiles, out_count, cnt, scn, wr, (size_t)g_or_chunk, take_fail_zero_bits(), bits,
                     ntiles * 2 * ONW * 8);

@@ -801,7 +801,7 @@ template <int MODE, int WORDS>
 __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c, size_t n,
                                                  const SortPlan *__restrict__ plan_, const uint32_t *__restrict__ loc,
                                                  const uint32_t *__restrict__ tot, crdt_tuples out,
-                                                 uint64_t *__restrict__ out_count) {
+                                                 uint64_t *__restrict__ out_count, int diag = 0) {
     __shared__ uint32_t s_c[DI * (DB / 64)];      // emits per (round, wave), then their exclusive prefix
     __shared__ uint64_t s_v[MODE == DD_LWW ? DT * WORDS : 1];   // LWW: the tile's composites (run walks)
     __shared__ DdEdges<WORDS> s_x;
@@ -822,6 +822,7 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
 #pragma unroll
             for (int q = 0; q < WORDS; ++q) s_v[q * DT + r * DB + tid] = v[r].w[q];
     __syncthreads();
+    if (diag == 1) return;                        // timing diagnostics (sort.rdd_diag): no stores
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
         const size_t e = base + (size_t)r * DB + tid;
@@ -875,6 +876,7 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         if (lane < NC) s_c[lane] = x - c0;
     }
     __syncthreads();
+    if (diag == 2) return;
     const uint32_t sk = p.b0 + p.br + p.bt;
 #pragma unroll
     for (int r = 0; r < DI; ++r) {
@@ -1440,7 +1442,7 @@ static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPla
     const unsigned nt = (unsigned)((n + DT - 1) / DT);
     k_dd_count<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, cnt);
     k_sort_colscan<<<1, CSB, 0, st>>>(cnt, nt, loc, tot);
-    k_dd_apply<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, loc, tot, out, out_count);
+    k_dd_apply<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, loc, tot, out, out_count, g_rdd_diag);
     return check_launch(ctx);
 }
 

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-3 evidence: GPU suite + default bench (tools/gpu_suite.sh), smoke, then rocprofv3 stats + FETCH/WRITE PMC
+# Round evidence: GPU suite + default bench (tools/gpu_suite.sh), smoke, then rocprofv3 stats + FETCH/WRITE PMC
 # per workload (tools/profile.sh), then one bench line per workload with the CPU baseline.
 bash tools/gpu_suite.sh || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -5 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
-WLS="shard_fold lww_merge orset_merge lww_merge_d2 orset_merge_d2 refmerge refmerge_delta gossip_round" bash tools/r03_profiles.sh || exit $?
+WLS="shard_fold lww_merge orset_merge lww_merge_d2 orset_merge_d2 refmerge refmerge_delta gossip_round" bash tools/profiles_all.sh || exit $?
 O=gpurun_out/r03_bench; mkdir -p $O
 for wl in lww_merge orset_merge lww_merge_d2 orset_merge_d2 refmerge refmerge_delta gossip_round gossip_round_wire server_merge shard_set_merge; do
   timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 3 > $O/$wl.json 2> $O/$wl.err || { echo "$wl failed"; tail -3 $O/$wl.err; exit 1; }
