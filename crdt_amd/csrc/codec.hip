@@ -82,6 +82,30 @@ __device__ __forceinline__ bool bytes_lt(const uint8_t *a, uint32_t na, const ui
     return na < nb;
 }
 
+// Bytes [p, p + n) (n <= 8) as a zero-padded little-endian u64, read by the
+// one or two naturally aligned 8-byte words that hold them: one load (two
+// when the string crosses a word) instead of a dependent load per byte; an
+// aligned word that holds a byte of the string never leaves its page.
+__device__ __forceinline__ uint64_t load_short(const uint8_t *p, uint32_t n) {
+    if (n == 0) return 0;
+    const uintptr_t a = (uintptr_t)p, base = a & ~(uintptr_t)7;
+    const uint32_t sh = (uint32_t)(a - base);
+    uint64_t v = *(const uint64_t *)base >> (8 * sh);
+    if (sh + n > 8) v |= *(const uint64_t *)(base + 8) << (8 * (8 - sh));
+    return n == 8 ? v : (v & ((1ull << (8 * n)) - 1));
+}
+__device__ __forceinline__ uint32_t hash32_short(uint64_t v, uint32_t n) {   // == hash32 of the n bytes
+    uint32_t h = 2166136261u;
+    for (uint32_t i = 0; i < n; ++i) h = (h ^ (uint32_t)((v >> (8 * i)) & 0xFF)) * 16777619u;
+    return h;
+}
+// a < b as byte strings, both packed by load_short: big-endian order of the
+// zero-padded bytes, the shorter first on equal padded values (a prefix)
+__device__ __forceinline__ bool short_lt(uint64_t a, uint32_t na, uint64_t b, uint32_t nb) {
+    const uint64_t A = __builtin_bswap64(a), B = __builtin_bswap64(b);
+    return A != B ? A < B : na < nb;
+}
+
 struct TabView {
     uint64_t *tab;
     uint64_t mask;
@@ -94,7 +118,9 @@ struct TabView {
 // Returns the entry index (kEmptyE as uint64 on a full table); *rep = claimed.
 template <class Get>
 __device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, uint32_t len, uint32_t self,
-                              const Get &get, bool *rep, uint64_t *ent) {
+                              const Get &get, bool *rep, uint64_t *ent, uint64_t sv) {
+    // sv: the string packed by load_short when len <= 8 (compares then load
+    // the candidate's bytes as one word too)
     *rep = false;
     uint64_t i = h & t.mask;
     for (uint64_t probe = 0; probe <= t.mask; ++probe, i = (i + 1) & t.mask) {
@@ -124,7 +150,7 @@ __device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, ui
             q = t.bytes + t.off[id];
             qn = (uint32_t)(t.off[id + 1] - t.off[id]);
         }
-        if (qn == len && bytes_eq(q, s, len)) {
+        if (qn == len && (len <= 8 ? load_short(q, qn) == sv : bytes_eq(q, s, len))) {
             *ent = e;
             return i;
         }
@@ -241,18 +267,25 @@ __global__ void k_dec_bodies(DecodeCtx c, const uint64_t *__restrict__ pre) {
 // r_kv = kv_base + the body's first pair + pre rebased to the body's first
 // entry, so a body whose pair counts disagree with its header (flagged by
 // k_dec_bodies) cannot shift the ranges of the bodies after it; mark the
-// first pair of each entry within its own body's pair range.
-__global__ void k_dec_kv(DecodeCtx c, const uint64_t *__restrict__ pre, uint64_t n_e, uint64_t n_p,
-                         uint64_t kv_base, uint64_t *__restrict__ r_kv, uint8_t *__restrict__ first) {
-    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= n_e; e += (uint64_t)gridDim.x * 256) {
-        if (e == n_e) {
-            r_kv[e] = kv_base + n_p;
-            continue;
-        }
-        const BodyDesc d = c.bd[find_body(c.bd, c.nbody, e, false)];
-        const uint64_t p = pre[e] - pre[d.e0];
+// first pair of each entry within its own body's pair range.  Body-major
+// (grid.y = body, like k_dec_entries): an entry's body is its workgroup's,
+// no search (a flat grid's per-entry binary search over the body table put
+// ten dependent loads in front of every entry: 124 us for 1000 x 10k).
+__global__ __launch_bounds__(256) void k_dec_kv(DecodeCtx c, const uint64_t *__restrict__ pre, uint64_t n_e,
+                                                uint64_t n_p, uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                                uint8_t *__restrict__ first) {
+    const uint32_t b = blockIdx.y;
+    const BodyDesc d = c.bd[b];
+    if (b == 0 && blockIdx.x == 0 && threadIdx.x == 0) r_kv[n_e] = kv_base + n_p;
+    if (d.ne == 0) return;
+    const uint64_t p0 = pre[d.e0];
+    for (uint64_t i = (uint64_t)blockIdx.x * kChunk + threadIdx.x; i < d.ne && i < (uint64_t)(blockIdx.x + 1) * kChunk;
+         i += 256) {
+        const uint64_t e = d.e0 + i;
+        const uint64_t a = pre[e], z = pre[e + 1];
+        const uint64_t p = a - p0;
         r_kv[e] = kv_base + d.q0 + p;
-        if (pre[e + 1] > pre[e] && p < d.np) first[d.q0 + p] = 1;
+        if (z > a && p < d.np) first[d.q0 + p] = 1;
     }
 }
 
@@ -302,14 +335,22 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
             bad = true;
         } else {
             const uint8_t *kp = region + o, *vp = region + o + k;
+            // short strings (the reference's one-byte keys and short values)
+            // packed in registers: one word load each, hash and compares on it
+            const uint64_t ksv = k <= 8 ? load_short(kp, (uint32_t)k) : 0, vsv = v <= 8 ? load_short(vp, (uint32_t)v) : 0;
             if (q && !first[j]) {                            // keys of an entry strictly ascending
                 const uint64_t po = c.boff[j - 1] - o0, pk = c.klen[j - 1];
-                if (po + pk <= o && !bytes_lt(region + po, (uint32_t)pk, kp, (uint32_t)k)) host = true;
+                if (po + pk <= o) {
+                    const bool lt = pk <= 8 && k <= 8
+                                        ? short_lt(load_short(region + po, (uint32_t)pk), (uint32_t)pk, ksv, (uint32_t)k)
+                                        : bytes_lt(region + po, (uint32_t)pk, kp, (uint32_t)k);
+                    if (!lt) host = true;
+                }
             }
             bool r;
             uint64_t e;
-            const uint64_t si = tab_claim(kt, hash32(kp, (uint32_t)k), kp, (uint32_t)k, (uint32_t)j,
-                                          PendGet{c, false}, &r, &e);
+            const uint32_t kh = k <= 8 ? hash32_short(ksv, (uint32_t)k) : hash32(kp, (uint32_t)k);
+            const uint64_t si = tab_claim(kt, kh, kp, (uint32_t)k, (uint32_t)j, PendGet{c, false}, &r, &e, ksv);
             if (si == kEmptyE) {
                 full = true;
             } else {
@@ -322,8 +363,8 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
                     nk += r;
                 }
             }
-            const uint64_t sv = tab_claim(vt, hash32(vp, (uint32_t)v), vp, (uint32_t)v, (uint32_t)j,
-                                          PendGet{c, true}, &r, &e);
+            const uint32_t vh = v <= 8 ? hash32_short(vsv, (uint32_t)v) : hash32(vp, (uint32_t)v);
+            const uint64_t sv = tab_claim(vt, vh, vp, (uint32_t)v, (uint32_t)j, PendGet{c, true}, &r, &e, vsv);
             if (sv == kEmptyE) {
                 full = true;
             } else {
@@ -700,7 +741,7 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     rc = scan_lb(ctx, CountSrc32{plen}, NoAct(), n_p, 0, boff, tmp);
     if (rc) return rc;
     k_dec_bodies<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(c, pre);
-    k_dec_kv<<<grid_for(n_e + 1, 256, cap), 256, 0, s>>>(c, pre, n_e, n_p, in->kv_base, out->r_kv, first);
+    k_dec_kv<<<ge, 256, 0, s>>>(c, pre, n_e, n_p, in->kv_base, out->r_kv, first);
     rc = check_launch(ctx);
     if (rc) return rc;
     const uint64_t kn0 = keys->n, kb0 = keys->nbytes, vn0 = vals->n, vb0 = vals->nbytes;

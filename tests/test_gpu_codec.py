@@ -171,3 +171,33 @@ def test_wire_rounds_match_reference_simulation(eng, seed):
         _same_diffs(_unpack(pop), diffs)
         assert _state(pop) == states, f"round {rnd}"
     assert len(keys) == K and len(vals) == len(STRS)                     # nothing new was interned
+
+
+def test_decode_short_string_order_and_interning(eng):
+    """The claim pass packs strings of <= 8 bytes into one word (hash, table
+    compares, the keys-ascending check): NUL bytes, prefixes, 8 / 9-byte
+    strings and strings that straddle an 8-byte word of the body all intern
+    to the host decode's strings, and the ascending check orders them like
+    Go strings (a prefix first; "a" < "a\\x00" < "a\\x01" < "b")."""
+    keys, vals = codec.StrTab(eng), codec.StrTab(eng)
+    ok = _raw_body([(1, [(b"a", b""), (b"a\x00", b"\x00"), (b"a\x01", b"12345678"), (b"b", b"123456789")]),
+                    (2, [(b"x" * 7, b"y" * 7), (b"x" * 8, b"y" * 8), (b"x" * 9, b"y" * 9)]),
+                    (3, [(b"\x00", b"\x00\x00"), (b"\x00\x00", b"\xff" * 3)])])
+    # (host-path bodies may still intern their strings: these reuse body 0's)
+    bad1 = _raw_body([(1, [(b"a\x00", b""), (b"a", b"\x00")])])      # prefix after the longer key: not ascending
+    bad2 = _raw_body([(1, [(b"x" * 8, b""), (b"x" * 7, b"\x00")])])
+    pad = _raw_body([(1, [(b"q", b"r")])])                           # shifts the next bodies' byte alignment
+    dec, st, kk, kv = _decode(eng, [ok, bad1, pad, ok, bad2], keys, vals)
+    assert st.tolist() == [0, 2, 0, 0, 2], st
+    ks, vs = keys.strings(), vals.strings()
+    want_k = [b"a", b"a\x00", b"a\x01", b"b", b"x" * 7, b"x" * 8, b"x" * 9, b"\x00", b"\x00\x00", b"q"]
+    want_v = [b"", b"\x00", b"12345678", b"123456789", b"y" * 7, b"y" * 8, b"y" * 9, b"\x00\x00", b"\xff" * 3, b"r"]
+    assert set(ks) == set(want_k) and len(ks) == len(want_k), ks
+    assert set(vs) == set(want_v) and len(vs) == len(want_v), vs
+    # body 3 (the same strings as body 0, at another alignment) resolves to the same ids
+    r_kv = dec["r_kv"].cpu().numpy()
+    r_off = dec["r_off"].cpu().numpy()
+    b0 = slice(int(r_kv[r_off[0]]), int(r_kv[r_off[1]]))
+    b3 = slice(int(r_kv[r_off[3]]), int(r_kv[r_off[4]]))
+    assert np.array_equal(kv[b0], kv[b3])
+    assert np.array_equal(kk[b0] - 0, kk[b3] - 3000)               # key ids rebased into each body's slot range
