@@ -136,6 +136,25 @@ struct SlotAcc {                          // global replay accumulators, by slot
     unsigned *npar;
 };
 
+// The new Diff's kv pairs (crdt_refmerge_batch_kv): the count pass sums the
+// kv pairs of each tile's emitted entries (tkv), the scan turns the sums into
+// tile bases (ikv), and the tile pass writes each emitted entry's kv offset
+// and copies its pairs -- no separate segmented gather over out.src.
+struct KvOut {
+    uint64_t *off;                        // nullptr: no kv output
+    uint32_t *key, *val;
+    uint64_t cap;
+    const uint64_t *ikv;                  // per-tile kv base (exclusive scan of tkv)
+    const uint32_t *tone;                 // per tile: every emitted entry has exactly one pair
+};
+
+// kv pairs of an entry's range [kb, ke), clamped to the arena (malformed
+// ranges stay in bounds); the count and tile passes both use this
+__device__ __forceinline__ uint64_t kv_len(uint64_t kb, uint64_t ke, uint64_t n_kv) {
+    const uint64_t e = ke < n_kv ? ke : n_kv;
+    return kb < e ? e - kb : 0;
+}
+
 __global__ void k_rm_ntiles(crdt_refmerge_in in, uint32_t *__restrict__ nt) {
     for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
         const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (in.r_off[p + 1] - in.r_off[p]);
@@ -396,14 +415,17 @@ __device__ __forceinline__ void fold_pair(uint32_t *t_slot, unsigned long long *
 // reads every entry's position from them instead of merging again (a
 // second merge in the tile pass, or a 2-byte rank per entry written and
 // read back, each cost more).  Grid = the tile-count upper bound.
-template <int NT>
+template <int NT, bool KV = false>
 __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
-                                                 uint32_t *__restrict__ zero, int dma) {
+                                                 uint32_t *__restrict__ zero, int dma, uint64_t *__restrict__ tkv,
+                                                 uint32_t *__restrict__ tone, uint32_t *__restrict__ err) {
     constexpr int NI = MT / NT, LPW = 64 / NI;           // items per thread, lanes per bitmap word
     static_assert(NI * LPW == 64, "a bitmap word is LPW lanes' items");
     __shared__ alignas(16) int64_t sm[MT + 8];           // (DMA: each run from its 16-byte aligned-down start)
     __shared__ uint32_t s_w[NT / 64];
+    __shared__ uint64_t s_k[KV ? NT / 64 : 1];
+    __shared__ uint8_t s_emr[KV ? MT : 1];               // KV: emitted flag of each R entry of the tile
     const uint64_t t = blockIdx.x;
     if (zero && t == 0 && threadIdx.x == 0) *zero = 0;   // (the delta fold's overflow flag)
     const TileDesc d = desc[t], dn = desc[t + 1];
@@ -411,7 +433,13 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
     tile_counts(d, dn, &na, &nb);
     const uint32_t n = na + nb;
     if (n == 0) {
-        if (threadIdx.x == 0) tcnt[t] = 0;              // the scan runs over the whole grid
+        if (threadIdx.x == 0) {
+            tcnt[t] = 0;                                 // the scans run over the whole grid
+            if (KV) {
+                tkv[t] = 0;
+                tone[t] = 1;
+            }
+        }
         return;
     }
     const int64_t *SA, *SB;
@@ -431,8 +459,51 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
     }
     const uint32_t k0 = threadIdx.x * NI < n ? threadIdx.x * NI : n;
     const uint32_t k1 = k0 + NI < n ? k0 + NI : n;
-    uint32_t isl = 0, emit = 0;
-    if (k0 < k1) (void)thread_merge(SA, SB, d.lprev, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
+    uint32_t isl = 0, emit = 0, ia0 = 0;
+    if (k0 < k1) ia0 = thread_merge(SA, SB, d.lprev, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
+    uint64_t ks = 0;                                     // KV: kv pairs of the tile's emitted entries
+    int one = 1;                                         // KV: every emitted entry has exactly one pair
+    if (KV) {
+        // the merge marks its emitted R entries by R index in LDS; then the
+        // kv ranges are read in index order (coalesced, all loads in flight):
+        // every L entry of the tile, the marked R entries
+        if (k0 < k1) {
+            const uint32_t ib0 = k0 - ia0;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const uint32_t nlb = (uint32_t)__popc(isl & ((1u << i) - 1u));
+                if (k0 + i < k1 && !((isl >> i) & 1u)) s_emr[ib0 + (uint32_t)i - nlb] = (uint8_t)((emit >> i) & 1u);
+            }
+        }
+        __syncthreads();
+        // an item's range end is the next item's start (the next lane's
+        // load) except at a wave's last lane and the ends of the L and R runs
+        uint64_t kb[NI], ke[NI];
+        bool on[NI];
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const uint32_t k = threadIdx.x + (uint32_t)j * NT;
+            const bool il = k < na;
+            const uint32_t idx = il ? k : k - na;
+            on[j] = k < n && (il || s_emr[idx]);
+            const uint64_t *kp = il ? in.l_kv + (d.l0 + idx) : in.r_kv + (d.r0 + idx);
+            kb[j] = k < n ? kp[0] : 0;
+            ke[j] = (k < n && (lane == 63 || k + 1 == na || k + 1 == n)) ? kp[1] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const uint32_t k = threadIdx.x + (uint32_t)j * NT;
+            const uint64_t nx = __shfl_down(kb[j], 1);
+            if (!(lane == 63 || k + 1 == na || k + 1 == n)) ke[j] = nx;
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const uint64_t len = on[j] ? kv_len(kb[j], ke[j], in.n_kv) : 0;
+            ks += len;
+            one &= !on[j] || len == 1;
+        }
+    }
     // LPW lanes' item bits -> one 64-bit word of each bitmap
     const int lane = threadIdx.x & 63, sh = (lane % LPW) * NI;
     uint64_t wl = (uint64_t)isl << sh, we = (uint64_t)emit << sh;
@@ -448,14 +519,30 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
     }
     uint32_t x = (uint32_t)__popc(emit & ~isl);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    if (lane == 0) s_w[threadIdx.x >> 6] = x;
-    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) {
+        x += __shfl_xor(x, o);
+        if (KV) ks += __shfl_xor(ks, o);
+    }
+    if (lane == 0) {
+        s_w[threadIdx.x >> 6] = x;
+        if (KV) s_k[threadIdx.x >> 6] = ks;
+    }
+    if (KV) one = __syncthreads_and(one);
+    else __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
+        uint64_t ktot = 0;
 #pragma unroll
-        for (int k = 0; k < NT / 64; ++k) tot += s_w[k];
+        for (int k = 0; k < NT / 64; ++k) {
+            tot += s_w[k];
+            if (KV) ktot += s_k[k];
+        }
         tcnt[t] = tot;
+        if (KV) {
+            tkv[t] = ktot;
+            tone[t] = (uint32_t)one;
+            if (ktot >= 0xFFFFFFFFull) atomicOr(err, CRDT_DEV_RANGE);   // (the tile pass sums in 32 bits)
+        }
     }
 }
 
@@ -484,20 +571,21 @@ enum { RM_FOLD_NONE = 0, RM_FOLD_FULL = 1, RM_FOLD_DELTA = 2 };
 //        (max, holder count, wrapped sum, parsable count); each R entry's
 //        rank (0: not inserted) goes to r_dk for the holder pass's
 //        overflow walk.
-template <int FOLD, int PARTS = 1>
-__global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
-                                                const uint64_t *__restrict__ bits, uint16_t *__restrict__ r_dk,
-                                                const OkVal *__restrict__ okv, SlotAcc acc, int diag,
-                                                const uint64_t *__restrict__ ic, crdt_refmerge_out out,
-                                                crdt_replay_state st, RpCand *__restrict__ cand,
-                                                uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf,
-                                                uint32_t *__restrict__ err) {
+template <int FOLD, int PARTS, bool KV, bool ONE = false>
+__device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDesc *__restrict__ desc,
+                                        const uint64_t *__restrict__ bits, uint16_t *__restrict__ r_dk,
+                                        const OkVal *__restrict__ okv, const SlotAcc &acc, int diag,
+                                        const uint64_t *__restrict__ ic, const crdt_refmerge_out &out,
+                                        const crdt_replay_state &st, RpCand *__restrict__ cand,
+                                        uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf,
+                                        uint32_t *__restrict__ err, const KvOut &kvo) {
     // PARTS > 1: each workgroup takes 1/PARTS of the tile's items (words
     // WPP h .. WPP h + WPP - 1) with FB / PARTS threads and its own slot table
     constexpr int WT = FB / PARTS, NWV = WT / 64, WPP = NW / PARTS;   // threads, waves, words per workgroup
     static_assert(FI * NWV == WPP, "each wave takes FI words of 64 items");
     constexpr bool DELTA = FOLD == RM_FOLD_DELTA, FOLDS = FOLD != RM_FOLD_NONE;
     static_assert(!DELTA || PARTS == 1, "the delta fold keeps one candidate list per tile");
+    static_assert(!KV || (PARTS == 1 && !DELTA), "the kv prefix spans the whole tile");
     static_assert(WT >= (int)OKC, "one thread per staged Atoi record");
     constexpr int TN = FOLDS ? TT : 1;
     __shared__ uint32_t t_slot[TN];
@@ -509,9 +597,13 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
     __shared__ uint32_t t_npar[TN];
     __shared__ int64_t s_okval[FOLDS ? OKC : 1];
     __shared__ uint8_t s_okok[FOLDS ? OKC : 1];
+    __shared__ uint32_t s_wk[KV ? NW : 1];              // KV: kv pairs per bitmap word
     const uint64_t t = blockIdx.x / PARTS;
     const int part = (int)(blockIdx.x % PARTS);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // KV: one-pair tiles (the common case: offset = tile base + rank, no
+    // prefix pass) and the rest go to two launches of the pass
+    if (KV && (kvo.tone[t] != 0) != ONE) return;
     // the descriptors, the tile's bitmap words (one of each bitmap per lane),
     // its offset and the staged Atoi records are independent loads: all issued
     // before the first use (the empty-tile exit would otherwise order them)
@@ -519,6 +611,7 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
     const TileDesc d = desc[t], dn = desc[t + 1];
     const uint64_t word_l = bits[t * 2 * NW + lane], word_e = bits[t * 2 * NW + NW + lane];
     const uint64_t ict = ic[t];
+    const uint64_t ikt = KV ? kvo.ikv[t] : 0;
     const bool okc = FOLDS && in.n_str <= OKC;
     OkVal ok0 = OkVal{0, 0};
     if (okc && threadIdx.x < in.n_str) ok0 = okv[threadIdx.x];
@@ -603,8 +696,10 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
         return it_l(f) ? d.l0 + li : d.r0 + (64u * (uint32_t)(wvu + NWV * f) + (uint32_t)lane - li);
     };
     uint64_t e_kb[FI], e_ke[FI];
+    uint32_t k_c[FI];
     int64_t e_ts[FI];
     uint32_t e_cnt[FI], e_slot[FI], e_v[FI];
+    uint32_t cmask = 0;                                  // KV: bit f = replay candidate (its count is k_c[f])
     uint8_t e_org[FI];
 #pragma unroll
     for (int f = 0; f < FI; ++f) {                       // every entry load issued before the first use
@@ -613,30 +708,82 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
         const uint64_t *kv = (il ? in.l_kv : in.r_kv) + gi;
         e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
         e_org[f] = (in_tile && il) ? in.l_origin[gi] : 0;
-        e_kb[f] = (FOLDS && in_tile) ? kv[0] : 0;
-        e_ke[f] = (FOLDS && in_tile) ? kv[1] : 0;
+        e_kb[f] = ((FOLDS || KV) && in_tile) ? kv[0] : 0;
+        e_ke[f] = ((FOLDS || KV) && !ONE && in_tile) ? kv[1] : 0;   // (ONE: every emitted range has one pair)
     }
-    if (FOLDS) {
+    if (FOLDS || KV) {
 #pragma unroll
         for (int f = 0; f < FI; ++f) {
             // *Command values are skipped by the replay (main.go:80); the
             // delta folds only the inserted R entries
-            const bool cand_e = it_em(f) && !e_org[f] && !(DELTA && it_l(f));
-            const uint64_t kb = e_kb[f], ke = e_ke[f] < in.n_kv ? e_ke[f] : in.n_kv;   // malformed ranges stay in bounds
-            e_cnt[f] = (cand_e && kb < ke) ? (uint32_t)(ke - kb < 0xFFFFFFFFull ? ke - kb : 0xFFFFFFFFull) : 0;
+            const bool cand_e = FOLDS && it_em(f) && !e_org[f] && !(DELTA && it_l(f));
+            const uint64_t len = ONE ? 1 : kv_len(e_kb[f], e_ke[f], in.n_kv);
+            e_cnt[f] = (!KV && cand_e) ? (uint32_t)(len < 0xFFFFFFFFull ? len : 0xFFFFFFFFull) : 0;
+            if (KV && cand_e) cmask |= 1u << f;
+            // KV: every emitted entry's pairs are copied (a tile of >= 2^32
+            // pairs is flagged below, so 32-bit counts are exact where used)
+            k_c[f] = (KV && it_em(f)) ? (uint32_t)(len < 0xFFFFFFFFull ? len : 0xFFFFFFFFull) : 0;
         }
 #pragma unroll
         for (int f = 0; f < FI; ++f) {
-            e_slot[f] = e_cnt[f] ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
-            e_v[f] = e_cnt[f] ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
+            const bool first = KV ? k_c[f] != 0 : e_cnt[f] != 0;
+            e_slot[f] = first ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
+            e_v[f] = first ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
         }
     }
+    // KV: each emitted entry's kv offset = the tile's base + the pairs of the
+    // emitted entries before it in merge order (word-major: word w, then
+    // lane): a count per word through LDS (one barrier, while the kv pairs
+    // are still in flight), its prefix over the words, then the lane's
+    // prefix within its word.  (32-bit sums: a tile of >= 2^32 pairs is
+    // flagged by the count pass; its offsets are then garbage, but every
+    // write stays in bounds.)  One pair per entry (the reference's load
+    // generator): the lane's prefix is a ballot count; otherwise a wave scan.
+    auto lane_pre = [&](int f, uint32_t *tot) -> uint32_t {
+        const uint64_t one = __ballot(k_c[f] != 0), multi = __ballot(k_c[f] > 1);
+        if (!multi) {
+            *tot = (uint32_t)__popcll(one);
+            return below(one);
+        }
+        uint32_t x = k_c[f];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        *tot = (uint32_t)__builtin_amdgcn_readlane(x, 63);
+        return x - k_c[f];
+    };
+    uint32_t wx = 0;                                     // KV: lane w = pairs of words before word w
+    if constexpr (KV && !ONE) {
+#pragma unroll
+        for (int f = 0; f < FI; ++f) {
+            uint32_t tot;
+            (void)lane_pre(f, &tot);
+            if (lane == 0) s_wk[wvu + NWV * f] = tot;
+        }
+        __syncthreads();
+        uint32_t wi = s_wk[lane];
+        wx = wi;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(wi, o);
+            if (lane >= o) wi += y;
+        }
+        wx = wi - wx;
+    }
     // the slice, straight from registers (every L entry of the tile and its
-    // inserted R entries, at their rank)
+    // inserted R entries, at their rank), and (KV) each entry's kv offset and pairs
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
         const bool il = it_l(f), em = it_em(f);
         const uint64_t gi = it_gi(f);
+        uint32_t wb = 0, lp = 0;
+        if (KV && !ONE) {                                // (wave-uniform parts before any lane leaves)
+            uint32_t tot;
+            wb = (uint32_t)__builtin_amdgcn_readlane(wx, wvu + NWV * f);
+            lp = lane_pre(f, &tot);
+        }
         if (em) {
             const uint64_t o = ob + it_rk(f);
             if (o >= in.n_l + in.n_r) {                  // (consistent bitmaps never get here)
@@ -646,35 +793,55 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
             out.ts[o] = e_ts[f];                         // (nontemporal stores: no change, 153 us)
             out.src[o] = il ? (int64_t)gi : -(int64_t)gi - 1;
             out.origin[o] = e_org[f];
+            if (KV) {
+                const uint64_t pos = ONE ? ikt + it_rk(f) : ikt + wb + lp;
+                kvo.off[o] = pos;
+                if (k_c[f] && pos + k_c[f] > kvo.cap) {
+                    atomicOr(err, CRDT_DEV_RANGE);
+                } else if (k_c[f]) {
+                    kvo.key[pos] = e_slot[f];
+                    kvo.val[pos] = e_v[f];
+                    for (uint32_t j = 1; j < k_c[f]; ++j) {   // further kvs of the entry (rare)
+                        kvo.key[pos + j] = in.kv_key[e_kb[f] + j];
+                        kvo.val[pos + j] = in.kv_val[e_kb[f] + j];
+                    }
+                }
+            }
         }
         if (DELTA && it_in(f) && !il) r_dk[gi] = em ? (uint16_t)(it_rk(f) + 1) : (uint16_t)0;
     }
     if (!FOLDS) return;
+    if constexpr (KV) {                                  // (the candidates' counts, from k_c)
+#pragma unroll
+        for (int f = 0; f < FI; ++f) e_cnt[f] = ((cmask >> f) & 1u) ? k_c[f] : 0;
+    }
     OkVal e_o[FI];
     if (!okc)
 #pragma unroll
         for (int f = 0; f < FI; ++f) {
             e_o[f] = OkVal{0, 0};
-            if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
+            if (e_cnt[f] && e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = okv[e_v[f]];
         }
     __syncthreads();                                     // table initialised, Atoi records staged
     if (okc)
 #pragma unroll
         for (int f = 0; f < FI; ++f) {
             e_o[f] = OkVal{0, 0};
-            if (e_slot[f] < in.n_slots && e_v[f] < in.n_str) e_o[f] = OkVal{s_okval[e_v[f]], s_okok[e_v[f]]};
+            if (e_cnt[f] && e_slot[f] < in.n_slots && e_v[f] < in.n_str)
+                e_o[f] = OkVal{s_okval[e_v[f]], s_okok[e_v[f]]};
         }
 #pragma unroll
     for (int f = 0; f < FI; ++f) {
         if (!e_cnt[f]) continue;
         const uint64_t rank = d.d0 + it_rk(f) + 1;
         const uint64_t key = (uint64_t)e_ts[f] ^ 0x8000000000000000ull;   // DELTA: the ts-keyed max
+        const uint64_t kb = e_kb[f];
         for (uint32_t j = 0; j < e_cnt[f]; ++j) {
             uint32_t slot = e_slot[f], v = e_v[f];
             OkVal o = e_o[f];
             if (j) {                                     // further kvs of the entry (rare)
-                slot = in.kv_key[e_kb[f] + j];
-                v = in.kv_val[e_kb[f] + j];
+                slot = in.kv_key[kb + j];
+                v = in.kv_val[kb + j];
                 if (slot < in.n_slots && v < in.n_str) o = okv[v];
             }
             if (slot >= in.n_slots || v >= in.n_str) continue;
@@ -733,6 +900,38 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
             if (s_ovf) *ovf = 1;
         }
     }
+}
+
+template <int FOLD, int PARTS = 1>
+__global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                const uint64_t *__restrict__ bits, uint16_t *__restrict__ r_dk,
+                                                const OkVal *__restrict__ okv, SlotAcc acc, int diag,
+                                                const uint64_t *__restrict__ ic, crdt_refmerge_out out,
+                                                crdt_replay_state st, RpCand *__restrict__ cand,
+                                                uint32_t *__restrict__ cand_n, uint32_t *__restrict__ ovf,
+                                                uint32_t *__restrict__ err) {
+    rm_tile<FOLD, PARTS, false>(in, desc, bits, r_dk, okv, acc, diag, ic, out, st, cand, cand_n, ovf, err, KvOut{});
+}
+
+// the tile pass with the kv output, one-pair tiles (two workgroups per CU)
+template <int FOLD>
+__global__ __launch_bounds__(FB, 8) void k_rm_tile_kv1(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                       const uint64_t *__restrict__ bits, const OkVal *__restrict__ okv,
+                                                       SlotAcc acc, int diag, const uint64_t *__restrict__ ic,
+                                                       crdt_refmerge_out out, uint32_t *__restrict__ err, KvOut kvo) {
+    rm_tile<FOLD, 1, true, true>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                 nullptr, nullptr, err, kvo);
+}
+
+// ... and the other tiles: one workgroup per CU (the kv prefix pass needs
+// more than the 64 registers two resident tiles leave a thread)
+template <int FOLD>
+__global__ __launch_bounds__(FB, 4) void k_rm_tile_kv(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                      const uint64_t *__restrict__ bits, const OkVal *__restrict__ okv,
+                                                      SlotAcc acc, int diag, const uint64_t *__restrict__ ic,
+                                                      crdt_refmerge_out out, uint32_t *__restrict__ err, KvOut kvo) {
+    rm_tile<FOLD, 1, true, false>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                  nullptr, nullptr, err, kvo);
 }
 
 // Delta replay, second phase: the global max holder of each slot writes its
@@ -851,14 +1050,19 @@ __global__ __launch_bounds__(SB) void k_rm_plan_small(crdt_refmerge_in in, uint6
 
 // ic = exclusive scan of tcnt[0..n) (ic[n] = total), then
 // out.off[p] = l_off[p] + ic[tbase[p]]
+// KV (tkv non-null): also ikv = exclusive scan of tkv, and the new Diff's
+// closing kv offset kv_off[out_off[replicas]] = the kv total.
 __global__ __launch_bounds__(SB) void k_rm_scan_small(const uint32_t *__restrict__ tcnt, uint32_t n,
                                                       uint64_t *__restrict__ ic, crdt_refmerge_in in,
                                                       const uint64_t *__restrict__ tbase,
-                                                      uint64_t *__restrict__ out_off) {
+                                                      uint64_t *__restrict__ out_off, const uint64_t *__restrict__ tkv,
+                                                      uint64_t *__restrict__ ikv, uint64_t *__restrict__ kv_off) {
     __shared__ uint64_t s_w[SB / 64];
     small_scan([&](uint32_t i) -> uint64_t { return tcnt[i]; }, n, ic, s_w);
-    __syncthreads();                                     // ic visible to the whole workgroup
+    if (tkv) small_scan([&](uint32_t i) -> uint64_t { return tkv[i]; }, n, ikv, s_w);
+    __syncthreads();                                     // ic / ikv visible to the whole workgroup
     for (uint32_t p = threadIdx.x; p <= in.replicas; p += SB) out_off[p] = in.l_off[p] + ic[tbase[p]];
+    if (tkv && threadIdx.x == 0) kv_off[in.l_off[in.replicas] + ic[tbase[in.replicas]]] = ikv[n];
 }
 
 // Go Atoi over the string arena and the replay accumulators' reset, one launch.
@@ -868,10 +1072,14 @@ __global__ void k_rm_prep(const uint8_t *__restrict__ bytes, const uint64_t *__r
 }
 
 // out.off[p] = l_off[p] + inserted R entries of replicas before p
+// (KV: kv_off[out_off[replicas]] = kv total, ikv_total = &ikv[tiles])
 __global__ void k_out_off(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, const uint64_t *__restrict__ ic,
-                          uint64_t *__restrict__ out_off) {
-    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p <= in.replicas; p += gridDim.x * 256)
+                          uint64_t *__restrict__ out_off, const uint64_t *__restrict__ ikv_total,
+                          uint64_t *__restrict__ kv_off) {
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p <= in.replicas; p += gridDim.x * 256) {
         out_off[p] = in.l_off[p] + ic[tbase[p]];
+        if (kv_off && p == in.replicas) kv_off[out_off[p]] = *ikv_total;
+    }
 }
 
 // Per-key closed form (main.go:82-96): verbatim base unless the base parses
@@ -908,10 +1116,17 @@ extern "C" int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *bytes, const uint64
 }
 
 static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
-                        const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta);
+                        const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta,
+                        const crdt_refmerge_kv_out *kv = nullptr);
 
 extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp) {
     return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr);
+}
+
+extern "C" int crdt_refmerge_batch_kv(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                                      const crdt_refmerge_kv_out *kv) {
+    if (!kv) return CRDT_E_INVAL;
+    return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr, kv);
 }
 
 namespace crdt {
@@ -931,7 +1146,8 @@ extern "C" int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
 }
 
 static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
-                        const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta) {
+                        const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta,
+                        const crdt_refmerge_kv_out *kv) {
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
@@ -953,6 +1169,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     if (!acc_out && in.n_slots && (!out.st_kind || !out.st_str || !out.st_sum)) return CRDT_E_INVAL;
     if (in.n_str && (!in.str_bytes || !in.str_off)) return CRDT_E_INVAL;
     if (in.n_kv && !in.n_str) return CRDT_E_INVAL;
+    if (kv && (delta || !kv->kv_off || (in.n_kv && (!kv->kv_key || !kv->kv_val)))) return CRDT_E_INVAL;
 
     const size_t nr = in.n_r, ns = in.n_slots, nstr = in.n_str, np = in.replicas;
     // The replay keys a holder as best = rank << 32 | string id, rank = its
@@ -968,7 +1185,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
                         Carve::round(tmax * 4 + 4) + Carve::round(tmax * 2 * NW * 8) + Carve::round((nstr + 1) * sizeof(OkVal)) +
                         (delta ? Carve::round(nr * 2 + 2) : 0) +
                         Carve::round(ns * 8 + 8) * 2 + Carve::round(ns * 4 + 4) + 4096 +
-                        (delta ? Carve::round(tmax * TT * sizeof(RpCand)) + Carve::round(tmax * 4 + 4) + 256 : 0);
+                        (delta ? Carve::round(tmax * TT * sizeof(RpCand)) + Carve::round(tmax * 4 + 4) + 256 : 0) +
+                        (kv ? 2 * Carve::round((tmax + 1) * 8) + Carve::round((tmax + 1) * 4) : 0);
     rc = ws_reserve(ctx, need);
     if (rc) return rc;
     Carve w(ctx->ws);
@@ -985,6 +1203,9 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     uint32_t *cand_n = delta ? w.take<uint32_t>(tmax + 1) : nullptr;
     uint32_t *ovf = delta ? w.take<uint32_t>(4) : nullptr;        // a tile's LDS table overflowed
     OkVal *okv = w.take<OkVal>(nstr + 1);
+    uint64_t *tkv = kv ? w.take<uint64_t>(tmax + 1) : nullptr;   // KV: kv pairs per tile, then (ikv) their scan
+    uint64_t *ikv = kv ? w.take<uint64_t>(tmax + 1) : nullptr;
+    uint32_t *tone = kv ? w.take<uint32_t>(tmax + 1) : nullptr;   // KV: tile whose emitted entries have one pair each
     SlotAcc acc;
     acc.best = w.take<unsigned long long>(ns + 1);
     acc.sum = w.take<unsigned long long>(ns + 1);
@@ -1013,18 +1234,26 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // (count-pass shapes at 4096-item tiles: 256 x 16 51 us, 512 x 8 45 us, 1024 x 4 67 us)
     // LDS-DMA staging of the ts runs when both logs are 8-byte aligned (refmerge.count_dma)
     const int cdma = g_rm_count_dma && !((((uintptr_t)in.l_ts) | ((uintptr_t)in.r_ts)) & 7);
-    k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma);
+    if (kv) k_rm_count<MB, true><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma, tkv, tone, ctx->dev_status);
+    else k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma, nullptr, nullptr, nullptr);
     rc = check_launch(ctx);
     if (rc) return rc;
     // (a completion ticket letting the count pass's last block do this scan
     // measured 95 us against 56 + 11.5: same-address arrivals serialise at
     // ~11 ns each and the tail runs alone after the grid)
     if (tmax <= kSmallPlan) {
-        k_rm_scan_small<<<1, SB, 0, s>>>(tcnt, (uint32_t)tmax, ic, in, tbase, out.off);
+        k_rm_scan_small<<<1, SB, 0, s>>>(tcnt, (uint32_t)tmax, ic, in, tbase, out.off, tkv, ikv,
+                                         kv ? kv->kv_off : nullptr);
     } else {
         rc = exclusive_scan_u32(ctx, tcnt, ic, tmax, tmp);
         if (rc) return rc;
-        k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off);
+        if (kv) {                                                 // (in place: one workgroup, any tile count)
+            hipError_t e = hipMemcpyAsync(ikv, tkv, tmax * 8, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+            k_scan_tsums<<<1, 256, 0, s>>>(ikv, tmax, 0, ikv + tmax);
+        }
+        k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off, kv ? ikv + tmax : nullptr,
+                                                              kv ? kv->kv_off : nullptr);
     }
     if (take_fail_zero_bits()) {                                  // failpoint: the tile pass must flag, not fault
         hipError_t e = hipMemsetAsync(bits, 0, tmax * 2 * NW * 8, s);
@@ -1032,6 +1261,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     }
     // the tile pass: slice write and (with slots) the replay fold
     const unsigned tg = (unsigned)tmax;
+    const KvOut kvo = kv ? KvOut{kv->kv_off, kv->kv_key, kv->kv_val, kv->kv_cap, ikv, tone} : KvOut{};
     if (delta && ns) {                                            // incremental replay: fold only the inserted R
         k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, 0, ic, out, *delta, cand, cand_n,
                                                    ovf, ctx->dev_status);
@@ -1043,18 +1273,25 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         return rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, true);
     }
     // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
-#define RM_TILE(F, P, DIAG)                                                                                   \
-    k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out, crdt_replay_state{}, \
-                                              nullptr, nullptr, nullptr, ctx->dev_status)
+#define RM_TILE(F, P, KV, DIAG)                                                                                \
+    if (KV) {                                                                                                  \
+        k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
+        k_rm_tile_kv<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);       \
+    } else                                                                                                       \
+        k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out,            \
+                                                  crdt_replay_state{}, nullptr, nullptr, nullptr, ctx->dev_status)
+    // (the kv output needs the whole tile in one workgroup: refmerge.tile_parts ignored)
     if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
-        if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, 0);
-        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, 0);
-        else RM_TILE(RM_FOLD_NONE, 1, 0);
+        if (kv) RM_TILE(RM_FOLD_NONE, 1, true, 0);
+        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, false, 0);
+        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, false, 0);
+        else RM_TILE(RM_FOLD_NONE, 1, false, 0);
         if (!ns || delta) return check_launch(ctx);
     } else {
-        if (g_rm_parts == 2) RM_TILE(RM_FOLD_FULL, 2, g_rm_diag);
-        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_FULL, 4, g_rm_diag);
-        else RM_TILE(RM_FOLD_FULL, 1, g_rm_diag);
+        if (kv) RM_TILE(RM_FOLD_FULL, 1, true, g_rm_diag);
+        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_FULL, 2, false, g_rm_diag);
+        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_FULL, 4, false, g_rm_diag);
+        else RM_TILE(RM_FOLD_FULL, 1, false, g_rm_diag);
     }
 #undef RM_TILE
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);

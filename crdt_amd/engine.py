@@ -14,8 +14,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import (call, crdt_local_in, crdt_local_out, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_out,
-                   crdt_replay_state, crdt_tuples)
+from ._lib import (call, crdt_local_in, crdt_local_out, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_kv_out,
+                   crdt_refmerge_out, crdt_replay_state, crdt_tuples)
 
 VC_EQUAL, VC_BEFORE, VC_AFTER, VC_CONCURRENT = 0, 1, 2, 3
 
@@ -294,13 +294,16 @@ class Engine:
             _ptr(d["kv_key"]), _ptr(d["kv_val"]), _ptr(d["str_bytes"]), _ptr(d["str_off"]))
 
     def refmerge_batch(self, packed: dict, maxl: torch.Tensor | None = None,
-                       acc: dict | None = None, _delta: dict | None = None) -> dict:
+                       acc: dict | None = None, _delta: dict | None = None, kv: dict | None = None) -> dict:
         """Run the batched bit-exact reference merge on a packed batch.
 
         ``packed`` holds device tensors produced by
         :func:`crdt_amd.refmerge.pack_batch`; returns device output tensors.
         ``maxl`` / ``acc``: the ts-range-sharded form (crdt_refmerge_batch_ex;
         see :func:`crdt_amd.shard.sharded_refmerge`).
+        ``kv`` = {"off": int64 [n_l + n_r + 1], "key", "val": int32 [cap]}:
+        also the new Diff's kv pairs (crdt_refmerge_batch_kv): entry i owns
+        key/val[off[i] .. off[i+1]), off[out["off"][-1]] = the total.
         """
         d = packed
         n_l, n_r = d["l_ts"].numel(), d["r_ts"].numel()
@@ -318,7 +321,17 @@ class Engine:
         cin = self._refmerge_in(d)
         cout = crdt_refmerge_out(*(out[k].data_ptr() for k in
                                    ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum")))
-        if _delta is not None:
+        if kv is not None:
+            if _delta is not None or maxl is not None or acc is not None:
+                raise ValueError("refmerge_batch: kv output only with the plain batch merge")
+            self._check(kv["off"], itemsize=8)
+            self._check(kv["key"], kv["val"], itemsize=4)
+            if kv["off"].numel() < n_l + n_r + 1 or kv["val"].numel() < kv["key"].numel():
+                raise ValueError("refmerge_batch: kv output too small")
+            ckv = crdt_refmerge_kv_out(kv["off"].data_ptr(), kv["key"].data_ptr(), kv["val"].data_ptr(),
+                                       kv["key"].numel())
+            self._call("crdt_refmerge_batch_kv", C.byref(cin), C.byref(cout), C.byref(ckv))
+        elif _delta is not None:
             cs = self._rstate(_delta)
             self._call("crdt_refmerge_delta", C.byref(cin), C.byref(cout), C.byref(cs))
         elif maxl is None and acc is None:

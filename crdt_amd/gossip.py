@@ -70,6 +70,7 @@ class Population:
         self.str_bytes = t(host["str_bytes"], np.uint8)
         self.str_off = t(host["str_off"], np.int64)
         self.state = None
+        self.kv_fused = True                  # new Diff's kv pairs from the merge's tile pass
         # per-replica entry / kv-pair counts of the Diffs on the host: a round
         # sizes the pulled arrays from them (no host round trip up front) and
         # refreshes them in its one read-back at the end; None = unknown (after
@@ -320,20 +321,25 @@ class Population:
                   "l_origin": self.origin, "l_kv": self.kv_off, "r_off": r_off, "r_ts": r_ts, "r_kv": r_kv,
                   "kv_key": arena_k[: n_lkv + n_rkv], "kv_val": arena_v[: n_lkv + n_rkv],
                   "str_bytes": self.str_bytes, "str_off": self.str_off}
-        out = eng.refmerge_batch(packed)
-        # 3. the next Diff: entries from the merge, kv pairs gathered by src.
-        # The entry count stays on the device (it bounds the gather, segments
-        # past it scan as empty); the arrays are sized for its upper bound
-        # |L| + |R|; ONE read-back at the end brings the new Diffs' entry and
-        # kv offsets per replica (the next round's sizes).  The fresh kv arena
-        # has room behind the pairs for the next round's pulled pairs.
+        # 3. the next Diff: entries from the merge, kv pairs copied by the
+        # merge's own tile pass (crdt_refmerge_batch_kv; kv_fused = False:
+        # a segmented gather by src after the merge, crdt_seg_gather2_n).
+        # The entry count stays on the device; the arrays are sized for its
+        # upper bound |L| + |R|; ONE read-back at the end brings the new
+        # Diffs' entry and kv offsets per replica (the next round's sizes).
+        # The fresh kv arena has room behind the pairs for the next round's
+        # pulled pairs.
         n_max = self.ts.numel() + r_ts.numel()
         new_kv = torch.empty(n_max + 1, dtype=torch.int64, device=dev)
         cap = 2 * max(n_lkv + n_rkv, 1)
         nk = torch.empty(cap, dtype=torch.int32, device=dev)
         nv = torch.empty(cap, dtype=torch.int32, device=dev)
-        self._call("crdt_seg_gather2_n", n_max, _p(out["off"][self.P:]), _p(out["src"]), _p(self.kv_off), _p(r_kv),
-                   _p(new_kv), _p(arena_k), _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
+        if self.kv_fused:
+            out = eng.refmerge_batch(packed, kv={"off": new_kv, "key": nk, "val": nv})
+        else:
+            out = eng.refmerge_batch(packed)
+            self._call("crdt_seg_gather2_n", n_max, _p(out["off"][self.P:]), _p(out["src"]), _p(self.kv_off),
+                       _p(r_kv), _p(new_kv), _p(arena_k), _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
         ho = torch.cat([out["off"], new_kv[out["off"]]]).cpu().numpy()
         n_out, n_kv = int(ho[self.P]), int(ho[-1])
         self._cnt, self._kvcnt = np.diff(ho[: self.P + 1]), np.diff(ho[self.P + 1:])

@@ -237,6 +237,22 @@ typedef struct crdt_refmerge_out {
 
 /* All pointers in `in` / `out` are device pointers. */
 int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out);
+/* crdt_refmerge_batch that also materialises the new Diff's kv pairs (the
+ * values the reference's Diff.Put carries along with each key, main.go:60-64):
+ * new entry i owns kv_key/kv_val[kv_off[i] .. kv_off[i+1]), a copy of its
+ * source entry's pairs (out.src), and kv_off[out.off[replicas]] = the total.
+ * The kv offsets come out of the merge's own passes, so the separate
+ * segmented gather over out.src (crdt_seg_gather2_n) is not needed.
+ * kv_off: capacity n_l + n_r + 1; kv_key / kv_val: capacity kv_cap (a total
+ * over kv_cap raises CRDT_DEV_RANGE, nothing written past it). */
+typedef struct crdt_refmerge_kv_out {
+    uint64_t *kv_off;
+    uint32_t *kv_key;
+    uint32_t *kv_val;
+    uint64_t kv_cap;
+} crdt_refmerge_kv_out;
+int crdt_refmerge_batch_kv(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out,
+                           const crdt_refmerge_kv_out *kv);
 /* ts-range-sharded RefMerge (§8(e)): one batch of replicas whose logs are
  * split by ts range over G shards (one per GPU).  Steps per shard:
  *   1. crdt_refmerge_local_maxl -> all-reduce(MAX) over shards: max(L) per replica;

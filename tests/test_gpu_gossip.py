@@ -13,12 +13,16 @@ from gossip_util import K, _host_round, _local_writes, _pack, _rand_diff, _same_
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("kv_fused", [True, False], ids=["kv_from_merge", "kv_gather"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_gossip_rounds_match_reference_simulation(eng, seed):
+def test_gossip_rounds_match_reference_simulation(eng, seed, kv_fused):
+    """kv_fused: the new Diff's kv pairs copied by the merge's tile pass
+    (crdt_refmerge_batch_kv, the default) or gathered by src afterwards."""
     rng = np.random.default_rng(seed)
     P = 7
     diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 40))) for i in range(P)]
     pop = gossip.Population(eng, _pack(diffs), K)
+    pop.kv_fused = kv_fused
     for rnd in range(5):
         peers = gossip.random_peers(rng, P, 0, P)
         pop.round(peers)

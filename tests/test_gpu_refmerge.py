@@ -250,3 +250,91 @@ def test_count_pass_register_staging(eng):
         test_all_kats_in_one_batch(eng)
     finally:
         _lib.call("crdt_set_option", b"refmerge.count_dma", 1)
+
+
+def _expected_kv(h, src, n_out):
+    """The new Diff's kv pairs by definition: entry i's pairs are its source
+    entry's (src >= 0: L index, < 0: R index -src-1), ranges clamped to the
+    arena like the device does; offsets are their running sum."""
+    n_kv = len(h["kv_key"])
+    kk, vv = np.asarray(h["kv_key"]).view(np.uint32), np.asarray(h["kv_val"]).view(np.uint32)
+    off, keys, vals = [0], [], []
+    for s in src[:n_out].tolist():
+        kvo = h["l_kv"] if s >= 0 else h["r_kv"]
+        j = s if s >= 0 else -s - 1
+        b, e = int(kvo[j]), min(int(kvo[j + 1]), n_kv)
+        if b < e:
+            keys.append(kk[b:e])
+            vals.append(vv[b:e])
+        off.append(off[-1] + max(e - b, 0))
+    cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.uint32)
+    return np.array(off, np.int64), cat(keys), cat(vals)
+
+
+def _run_kv(eng, h, cap=None):
+    d = refmerge.to_device(h, eng.device)
+    n = len(h["l_ts"]) + len(h["r_ts"])
+    cap = 2 * max(len(h["kv_key"]), 1) if cap is None else cap
+    kv = {"off": torch.full((n + 1,), -1, dtype=torch.int64, device=eng.device),
+          "key": torch.zeros(max(cap, 1), dtype=torch.int32, device=eng.device),
+          "val": torch.zeros(max(cap, 1), dtype=torch.int32, device=eng.device)}
+    if cap == 0:
+        kv["key"], kv["val"] = kv["key"][:0], kv["val"][:0]
+    return eng.refmerge_batch(d, kv=kv), eng.refmerge_batch(d), kv
+
+
+def _assert_kv_output(h, out, plain, kv):
+    """crdt_refmerge_batch_kv: the merge outputs equal the plain call's
+    (themselves oracle-checked above) and the kv pairs equal the host gather."""
+    for k in ("off", "ts", "origin", "src", "st_kind", "st_str", "st_sum"):
+        n = int(plain["off"][-1]) if k in ("ts", "origin", "src") else None
+        assert torch.equal(out[k][:n], plain[k][:n]), k
+    n_out = int(plain["off"][-1])
+    e_off, e_key, e_val = _expected_kv(h, plain["src"].cpu().numpy(), n_out)
+    np.testing.assert_array_equal(kv["off"][: n_out + 1].cpu().numpy(), e_off)
+    m = int(e_off[-1])
+    np.testing.assert_array_equal(kv["key"][:m].cpu().numpy().view(np.uint32), e_key)
+    np.testing.assert_array_equal(kv["val"][:m].cpu().numpy().view(np.uint32), e_val)
+
+
+@pytest.mark.parametrize("case", ["packed", "multi_key", "ragged_ranges", "many_replicas"])
+def test_batch_kv_output(eng, case):
+    """The new Diff's kv pairs out of the merge's own passes (count pass:
+    pairs per tile; tile pass: offsets and copies) == a host gather by src:
+    the bench's packed batch (one pair per entry), multi-pair entries, empty
+    / overlapping / past-the-arena ranges, and > 65536 tiles (the
+    multi-kernel scan path)."""
+    if case == "packed":
+        h = synth.refmerge_packed(11, 48, 5000)
+    elif case == "many_replicas":
+        h = synth.refmerge_packed(23, 70_000, 12)
+    else:
+        pk = refmerge.Packer()
+        for d, r in synth.refmerge_demo(31, replicas=40, entries=700, multi_key=0.4):
+            pk.add_replica(d, r)
+        h = pk.arrays()
+        if case == "ragged_ranges":
+            rng = np.random.default_rng(5)
+            n_kv = len(h["kv_key"])
+            for a in ("l_kv", "r_kv"):
+                x = h[a].copy()
+                i = rng.choice(len(x), size=len(x) // 7, replace=False)
+                # shifted ends: empty, reversed, overlapping and past-the-arena ranges
+                x[i] = np.clip(x[i] + rng.integers(-3, 4, size=len(i)), 0, n_kv + 5)
+                h[a] = x
+    out, plain, kv = _run_kv(eng, h)
+    assert eng.device_status(clear=True) == 0
+    _assert_kv_output(h, out, plain, kv)
+
+
+def test_batch_kv_output_capacity(eng):
+    """A kv total over kv_cap raises CRDT_DEV_RANGE (nothing written past
+    the arena); an exact-size arena is enough."""
+    h = synth.refmerge_packed(7, 9, 3000)
+    _, plain, _ = _run_kv(eng, h)
+    total = len(_expected_kv(h, plain["src"].cpu().numpy(), int(plain["off"][-1]))[1])
+    out, _, kv = _run_kv(eng, h, cap=total)
+    assert eng.device_status(clear=True) == 0
+    _assert_kv_output(h, out, plain, kv)
+    _run_kv(eng, h, cap=total - 1)
+    assert eng.device_status(clear=True) == 2
