@@ -796,7 +796,7 @@ class GossipRound(Workload):
     name = "gossip_round"
     unit = "remote-entries/s"
     dtype = "int64"
-    kernel = "gossip round (crdt_seg_* assembly + refmerge + Diff materialisation)"
+    kernel = "gossip round (refmerge over the peers' Diffs in place + the new Diffs' kv pairs)"
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         from crdt_amd import gossip, synth
@@ -806,6 +806,8 @@ class GossipRound(Workload):
                 "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
                 "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
         self.pop = gossip.Population(eng, host, 62)
+        # (A/B: CRDT_GOSSIP_PULL=inplace reads the peers' Diffs in place, crdt_refmerge_batch_pull)
+        self.pop.pull_inplace = os.environ.get("CRDT_GOSSIP_PULL", "assembled") != "assembled"
         self.host = h
         self.init = self.pop.snapshot()
         self.rng = np.random.default_rng(seed)
@@ -823,10 +825,13 @@ class GossipRound(Workload):
         return self.n_l                      # every pulled entry (a peer's whole Diff per replica)
 
     def bytes_per_launch(self):
-        # R assembly (read + write ts, kv range, kv pair), the merge (inputs + outputs once),
-        # the next Diff's kv gather (read + write kv pair, write kv range)
+        # the merge (inputs + outputs once; R read in place from the peers' Diffs),
+        # the next Diff's kv pairs (read + write kv pair, write kv range); with
+        # assembled pulls (pull_inplace False) also the R assembly (read + write
+        # ts, kv range, kv pair)
         n_r, n_out = self.n_l, self.n_out
-        return n_r * 24 * 2 + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
+        asm = 0 if self.pop.pull_inplace else n_r * 24 * 2
+        return asm + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
 
     def step(self):
         self.pop.restore(self.init)           # every step is the same round from the same Diffs

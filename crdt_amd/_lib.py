@@ -79,6 +79,10 @@ class crdt_refmerge_kv_out(C.Structure):
     _fields_ = [("kv_off", C.c_void_p), ("kv_key", C.c_void_p), ("kv_val", C.c_void_p), ("kv_cap", C.c_uint64)]
 
 
+class crdt_refmerge_pull(C.Structure):
+    _fields_ = [("r_end", C.c_void_p), ("r_slot_delta", C.c_void_p)]
+
+
 class crdt_replay_state(C.Structure):
     _fields_ = [("best_key", C.c_void_p), ("best_str", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p),
                 ("nhold", C.c_void_p)]
@@ -164,6 +168,8 @@ SIGNATURES = {
     "crdt_local_apply": (_I, [_CTX, C.POINTER(crdt_local_in), C.POINTER(crdt_local_out)]),
     "crdt_refmerge_batch_kv": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out),
                                     C.POINTER(crdt_refmerge_kv_out)]),
+    "crdt_refmerge_batch_pull": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out),
+                                      C.POINTER(crdt_refmerge_pull), C.POINTER(crdt_refmerge_kv_out)]),
     "crdt_refmerge_batch_ex": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out), _P,
                                     C.POINTER(crdt_refmerge_acc)]),
     "crdt_refmerge_local_maxl": (_I, [_CTX, C.POINTER(crdt_refmerge_in), _P]),

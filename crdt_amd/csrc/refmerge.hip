@@ -109,8 +109,22 @@ struct TileDesc {                         // 64 B per tile; a tile pass loads it
     int64_t lprev;                        // L entry just before the tile (valid if has_prev)
     uint64_t lend;                        // end of the replica's L (global index)
     uint32_t n;                           // merge items of the tile; 0: no tile
-    uint32_t has_prev, pad[2];
+    uint32_t has_prev;
+    uint32_t rsd;                         // added (mod 2^32) to the key slot of every R pair (in-place pulls)
+    uint32_t pad;
 };
+
+// The batch as the planning kernels see it: the ABI struct plus the
+// in-place pull form (crdt_refmerge_batch_pull) -- replica p's R is
+// r_ts[r_off[p] .. r_end[p]) (ranges may overlap: R aliases the peers'
+// Diffs) and its R pairs' key slots are re-based by r_sd[p].
+struct RmIn : crdt_refmerge_in {
+    const uint64_t *r_end = nullptr;      // nullptr: CSR, r_off[p + 1]
+    const uint32_t *r_sd = nullptr;
+};
+__device__ __forceinline__ uint64_t r_hi(const RmIn &in, uint32_t p) {
+    return in.r_end ? in.r_end[p] : in.r_off[p + 1];
+}
 
 // The tile's L / R entry counts: its L range ends where the next tile's
 // begins (same replica: d0 > 0) or at the replica's L end.
@@ -155,9 +169,9 @@ __device__ __forceinline__ uint64_t kv_len(uint64_t kb, uint64_t ke, uint64_t n_
     return kb < e ? e - kb : 0;
 }
 
-__global__ void k_rm_ntiles(crdt_refmerge_in in, uint32_t *__restrict__ nt) {
+__global__ void k_rm_ntiles(RmIn in, uint32_t *__restrict__ nt) {
     for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
-        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (in.r_off[p + 1] - in.r_off[p]);
+        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (r_hi(in, p) - in.r_off[p]);
         nt[p] = (uint32_t)((n + MT - 1) / MT);
     }
 }
@@ -236,7 +250,7 @@ __device__ __forceinline__ uint64_t wave_split(const int64_t *L, uint64_t nl, co
 // tile share their successor's tbase and are skipped by the search).
 // maxl_ovr (nullable): per-replica max(L) to insert below, instead of the
 // local L's last key (the ts-range-sharded merge passes the global max).
-__device__ __forceinline__ TileGeo tile_geo(const crdt_refmerge_in &in, const uint64_t *__restrict__ tbase,
+__device__ __forceinline__ TileGeo tile_geo(const RmIn &in, const uint64_t *__restrict__ tbase,
                                             const int64_t *__restrict__ maxl_ovr, uint64_t t) {
     uint32_t lo = 0, hi = in.replicas;
     while (hi - lo > 1) {
@@ -249,7 +263,7 @@ __device__ __forceinline__ TileGeo tile_geo(const crdt_refmerge_in &in, const ui
     g.lb = in.l_off[lo];
     g.nl = in.l_off[lo + 1] - g.lb;
     g.rb = in.r_off[lo];
-    g.nr = in.r_off[lo + 1] - g.rb;
+    g.nr = r_hi(in, lo) - g.rb;
     g.maxl = maxl_ovr ? maxl_ovr[lo] : g.nl ? in.l_ts[g.lb + g.nl - 1] : INT64_MIN;   // empty L: nothing inserted
     g.first = (uint32_t)tbase[lo];
     g.d0 = (t - tbase[lo]) * MT;
@@ -262,7 +276,7 @@ __device__ __forceinline__ TileGeo tile_geo(const crdt_refmerge_in &in, const ui
 // end is the next descriptor's start); slots past the tile count get an
 // empty descriptor.  The same launch runs the Atoi / accumulator-reset prep
 // (independent work).
-__global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t replicas,
+__global__ __launch_bounds__(256) void k_rm_split(RmIn in, uint32_t replicas,
                                                   const uint64_t *__restrict__ tbase,
                                                   const int64_t *__restrict__ maxl_ovr, uint64_t tmax,
                                                   TileDesc *__restrict__ desc, OkVal *__restrict__ okv, SlotAcc acc,
@@ -285,6 +299,7 @@ __global__ __launch_bounds__(256) void k_rm_split(crdt_refmerge_in in, uint32_t 
         d.n = (uint32_t)(g.d1 - g.d0);
         d.has_prev = a0 > 0;
         d.lprev = lprev;
+        d.rsd = in.r_sd ? in.r_sd[g.p] : 0u;
     }
     if (lane == 0) desc[t] = d;
 }
@@ -727,7 +742,7 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
 #pragma unroll
         for (int f = 0; f < FI; ++f) {
             const bool first = KV ? k_c[f] != 0 : e_cnt[f] != 0;
-            e_slot[f] = first ? in.kv_key[e_kb[f]] : 0xFFFFFFFFu;
+            e_slot[f] = first ? in.kv_key[e_kb[f]] + (it_l(f) ? 0u : d.rsd) : 0xFFFFFFFFu;
             e_v[f] = first ? in.kv_val[e_kb[f]] : 0xFFFFFFFFu;
         }
     }
@@ -802,7 +817,7 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
                     kvo.key[pos] = e_slot[f];
                     kvo.val[pos] = e_v[f];
                     for (uint32_t j = 1; j < k_c[f]; ++j) {   // further kvs of the entry (rare)
-                        kvo.key[pos + j] = in.kv_key[e_kb[f] + j];
+                        kvo.key[pos + j] = in.kv_key[e_kb[f] + j] + (il ? 0u : d.rsd);
                         kvo.val[pos + j] = in.kv_val[e_kb[f] + j];
                     }
                 }
@@ -840,7 +855,7 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
             uint32_t slot = e_slot[f], v = e_v[f];
             OkVal o = e_o[f];
             if (j) {                                     // further kvs of the entry (rare)
-                slot = in.kv_key[kb + j];
+                slot = in.kv_key[kb + j] + (it_l(f) ? 0u : d.rsd);
                 v = in.kv_val[kb + j];
                 if (slot < in.n_slots && v < in.n_str) o = okv[v];
             }
@@ -1040,10 +1055,10 @@ __device__ __forceinline__ void small_scan(Get get, uint32_t n, uint64_t *__rest
 }
 
 // tbase = exclusive scan of the per-replica tile counts (tbase[np] = tiles)
-__global__ __launch_bounds__(SB) void k_rm_plan_small(crdt_refmerge_in in, uint64_t *__restrict__ tbase) {
+__global__ __launch_bounds__(SB) void k_rm_plan_small(RmIn in, uint64_t *__restrict__ tbase) {
     __shared__ uint64_t s_w[SB / 64];
     small_scan([&](uint32_t p) -> uint64_t {
-        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (in.r_off[p + 1] - in.r_off[p]);
+        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (r_hi(in, p) - in.r_off[p]);
         return (n + MT - 1) / MT;
     }, in.replicas, tbase, s_w);
 }
@@ -1062,7 +1077,10 @@ __global__ __launch_bounds__(SB) void k_rm_scan_small(const uint32_t *__restrict
     if (tkv) small_scan([&](uint32_t i) -> uint64_t { return tkv[i]; }, n, ikv, s_w);
     __syncthreads();                                     // ic / ikv visible to the whole workgroup
     for (uint32_t p = threadIdx.x; p <= in.replicas; p += SB) out_off[p] = in.l_off[p] + ic[tbase[p]];
-    if (tkv && threadIdx.x == 0) kv_off[in.l_off[in.replicas] + ic[tbase[in.replicas]]] = ikv[n];
+    if (tkv && threadIdx.x == 0) {                       // (and at the capacity end: a fixed place to read it)
+        kv_off[in.l_off[in.replicas] + ic[tbase[in.replicas]]] = ikv[n];
+        kv_off[in.n_l + in.n_r] = ikv[n];
+    }
 }
 
 // Go Atoi over the string arena and the replay accumulators' reset, one launch.
@@ -1078,7 +1096,10 @@ __global__ void k_out_off(crdt_refmerge_in in, const uint64_t *__restrict__ tbas
                           uint64_t *__restrict__ kv_off) {
     for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p <= in.replicas; p += gridDim.x * 256) {
         out_off[p] = in.l_off[p] + ic[tbase[p]];
-        if (kv_off && p == in.replicas) kv_off[out_off[p]] = *ikv_total;
+        if (kv_off && p == in.replicas) {
+            kv_off[out_off[p]] = *ikv_total;
+            kv_off[in.n_l + in.n_r] = *ikv_total;
+        }
     }
 }
 
@@ -1117,7 +1138,7 @@ extern "C" int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *bytes, const uint64
 
 static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
                         const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta,
-                        const crdt_refmerge_kv_out *kv = nullptr);
+                        const crdt_refmerge_kv_out *kv = nullptr, const crdt_refmerge_pull *pull = nullptr);
 
 extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp) {
     return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr);
@@ -1127,6 +1148,12 @@ extern "C" int crdt_refmerge_batch_kv(crdt_ctx *ctx, const crdt_refmerge_in *inp
                                       const crdt_refmerge_kv_out *kv) {
     if (!kv) return CRDT_E_INVAL;
     return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr, kv);
+}
+
+extern "C" int crdt_refmerge_batch_pull(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                                        const crdt_refmerge_pull *pull, const crdt_refmerge_kv_out *kv) {
+    if (!pull || !pull->r_end) return CRDT_E_INVAL;
+    return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr, kv, pull);
 }
 
 namespace crdt {
@@ -1147,7 +1174,7 @@ extern "C" int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
 
 static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
                         const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta,
-                        const crdt_refmerge_kv_out *kv) {
+                        const crdt_refmerge_kv_out *kv, const crdt_refmerge_pull *pull) {
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
@@ -1157,7 +1184,13 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
                                   !delta->nhold))
         return CRDT_E_INVAL;
     if (acc_out && inp->n_slots && (!acc_out->best || !acc_out->sum || !acc_out->npar)) return CRDT_E_INVAL;
-    const crdt_refmerge_in in = *inp;
+    RmIn in;
+    static_cast<crdt_refmerge_in &>(in) = *inp;
+    if (pull) {                                                  // in-place pulls: R ranges by (r_off, r_end)
+        if (delta || maxl_dev || acc_out) return CRDT_E_INVAL;
+        in.r_end = pull->r_end;
+        in.r_sd = pull->r_slot_delta;
+    }
     const crdt_refmerge_out out = *outp;
     if (in.replicas == 0) return CRDT_OK;
     if (!in.l_off || !in.r_off || !out.off) return CRDT_E_INVAL;

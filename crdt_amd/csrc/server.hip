@@ -678,14 +678,12 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
                          s.o_src.as<int64_t>(), s.st_kind.as<uint8_t>(), s.st_str.as<uint32_t>(),
                          s.st_sum.as<int64_t>()};
     StatusScope sc(ctx);
-    rc = crdt_refmerge_batch(ctx, &ri, &ro);
-    if (rc) return rc;
-    // the new Diff's kv pairs behind the merge, its entry count still on the
-    // device (dd2 is sized for |L| + |R|): one host synchronisation per merge
-    rc = seg_gather2_dev_count(ctx, nl + ne, s.o_off.as<uint64_t>() + 1, s.o_src.as<int64_t>(),
-                               s.dd.kv_off.as<uint64_t>(), s.r_kv.as<uint64_t>(), s.dd2.kv_off.as<uint64_t>(),
-                               s.dd.kv_key.as<uint32_t>(), s.dd.kv_key.as<uint32_t>(), s.dd2.kv_key.as<uint32_t>(),
-                               s.dd.kv_val.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), s.dd2.kv_val.as<uint32_t>());
+    // the merge and the new Diff's kv pairs (copied by the merge's tile pass;
+    // its entry count stays on the device, dd2 is sized for |L| + |R| and the
+    // pair total also lands at kv_off[|L| + |R|]): one host synchronisation
+    const crdt_refmerge_kv_out kvo{s.dd2.kv_off.as<uint64_t>(), s.dd2.kv_key.as<uint32_t>(),
+                                   s.dd2.kv_val.as<uint32_t>(), nkv + np};
+    rc = crdt_refmerge_batch_kv(ctx, &ri, &ro, &kvo);
     if (rc) return rc;
     // CurrentState (main.go:76-96: rebuilt from empty), the entry count and
     // the new pair count (every dst offset from the entry count on = the total)
@@ -974,16 +972,14 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     }
     if (rc) return rc;
     StatusScope sc(ctx);
-    rc = crdt_refmerge_batch(ctx, &ri, &ro);
+    // the merge with the new Diffs' kv pairs (copied by its tile pass; the
+    // entry count stays on the device), then each server's pair range, the
+    // split into its next buffers, then CurrentState
+    const crdt_refmerge_kv_out kvo{bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>(),
+                                   nkl + nkr};
+    rc = crdt_refmerge_batch_kv(ctx, &ri, &ro, &kvo);
     if (rc) return rc;
     pc.mark("refmerge_launch");
-    // the new Diff's kv pairs (the entry count stays on the device), each
-    // server's pair range, the split into its next buffers, then CurrentState
-    rc = seg_gather2_dev_count(ctx, nl + nr, bb.o_off.as<uint64_t>() + S, bb.o_src.as<int64_t>(),
-                               bb.l_kv.as<uint64_t>(), bb.r_kv.as<uint64_t>(), bb.n_kv.as<uint64_t>(),
-                               bb.kv_key.as<uint32_t>(), bb.kv_key.as<uint32_t>(), bb.n_key.as<uint32_t>(),
-                               bb.kv_val.as<uint32_t>(), bb.kv_val.as<uint32_t>(), bb.n_val.as<uint32_t>());
-    if (rc) return rc;
     k_gather_at<<<grid_for(S + 1, 256, 1u << 20), 256, 0, st>>>(bb.n_kv.as<uint64_t>(), bb.o_off.as<uint64_t>(),
                                                                  S + 1, bb.kb.as<uint64_t>());
     rc = check_launch(ctx);

@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from ._lib import (call, crdt_local_in, crdt_local_out, crdt_refmerge_acc, crdt_refmerge_in, crdt_refmerge_kv_out,
-                   crdt_refmerge_out, crdt_replay_state, crdt_tuples)
+                   crdt_refmerge_out, crdt_refmerge_pull, crdt_replay_state, crdt_tuples)
 
 VC_EQUAL, VC_BEFORE, VC_AFTER, VC_CONCURRENT = 0, 1, 2, 3
 
@@ -287,14 +287,16 @@ class Engine:
     # ------------------------------------------------------------ RefMerge (a1-a3)
     def _refmerge_in(self, d: dict) -> crdt_refmerge_in:
         return crdt_refmerge_in(
-            d["replicas"], int(d["n_slots"]), d["l_ts"].numel(), d["r_ts"].numel(), d["kv_key"].numel(),
+            d["replicas"], int(d["n_slots"]), d["l_ts"].numel(), int(d.get("n_r", d["r_ts"].numel())),
+            d["kv_key"].numel(),
             d["str_off"].numel() - 1,
             _ptr(d["l_off"]), _ptr(d["l_ts"]), _ptr(d["l_origin"]), _ptr(d["l_kv"]),
             _ptr(d["r_off"]), _ptr(d["r_ts"]), _ptr(d["r_kv"]),
             _ptr(d["kv_key"]), _ptr(d["kv_val"]), _ptr(d["str_bytes"]), _ptr(d["str_off"]))
 
     def refmerge_batch(self, packed: dict, maxl: torch.Tensor | None = None,
-                       acc: dict | None = None, _delta: dict | None = None, kv: dict | None = None) -> dict:
+                       acc: dict | None = None, _delta: dict | None = None, kv: dict | None = None,
+                       pull: dict | None = None) -> dict:
         """Run the batched bit-exact reference merge on a packed batch.
 
         ``packed`` holds device tensors produced by
@@ -304,9 +306,13 @@ class Engine:
         ``kv`` = {"off": int64 [n_l + n_r + 1], "key", "val": int32 [cap]}:
         also the new Diff's kv pairs (crdt_refmerge_batch_kv): entry i owns
         key/val[off[i] .. off[i+1]), off[out["off"][-1]] = the total.
+        ``pull`` = {"r_end": int64 [replicas], "r_slot_delta": int32
+        [replicas] or None}: in-place pulls (crdt_refmerge_batch_pull) --
+        replica p's R is r_ts[r_off[p] .. r_end[p]) (may alias L), and
+        ``packed["n_r"]`` the total of the R ranges.
         """
         d = packed
-        n_l, n_r = d["l_ts"].numel(), d["r_ts"].numel()
+        n_l, n_r = d["l_ts"].numel(), int(d.get("n_r", d["r_ts"].numel()))
         n_slots = int(d["n_slots"])
         dev = self.device
         out = {
@@ -330,6 +336,17 @@ class Engine:
                 raise ValueError("refmerge_batch: kv output too small")
             ckv = crdt_refmerge_kv_out(kv["off"].data_ptr(), kv["key"].data_ptr(), kv["val"].data_ptr(),
                                        kv["key"].numel())
+        if pull is not None:
+            if _delta is not None or maxl is not None or acc is not None:
+                raise ValueError("refmerge_batch: in-place pulls only with the plain batch merge")
+            self._check(pull["r_end"], itemsize=8)
+            sd = pull.get("r_slot_delta")
+            if sd is not None:
+                self._check(sd, itemsize=4)
+            cp = crdt_refmerge_pull(pull["r_end"].data_ptr(), sd.data_ptr() if sd is not None else None)
+            self._call("crdt_refmerge_batch_pull", C.byref(cin), C.byref(cout), C.byref(cp),
+                       C.byref(ckv) if kv is not None else None)
+        elif kv is not None:
             self._call("crdt_refmerge_batch_kv", C.byref(cin), C.byref(cout), C.byref(ckv))
         elif _delta is not None:
             cs = self._rstate(_delta)

@@ -71,6 +71,7 @@ class Population:
         self.str_off = t(host["str_off"], np.int64)
         self.state = None
         self.kv_fused = True                  # new Diff's kv pairs from the merge's tile pass
+        self.pull_inplace = False             # local rounds: the merge reads the peers' Diffs in place
         # per-replica entry / kv-pair counts of the Diffs on the host: a round
         # sizes the pulled arrays from them (no host round trip up front) and
         # refreshes them in its one read-back at the end; None = unknown (after
@@ -246,6 +247,25 @@ class Population:
         n_lkv = self.kv_key.numel()
         cnt, kvc = self._cnt[lq], self._kvcnt[lq]
         n_r, n_rkv = int(cnt.sum()), int(kvc.sum())
+        if self.pull_inplace:
+            # every replica's RemoteDiff is its peer's Diff where it lies in
+            # HBM: the merge reads R ranges (r_off, r_end) of the population's
+            # own arrays and re-bases the pulled key slots (r_slot_delta), so
+            # nothing is assembled.  int64 fields: r_off P | r_end P | delta (int32, P)
+            n64 = 2 * P + (P + 1) // 2
+            if self._pin is None or self._pin.numel() < n64:
+                self._pin = torch.empty(n64, dtype=torch.int64).pin_memory()
+            h = self._pin.numpy()
+            l_off = np.zeros(P + 1, np.int64)
+            np.cumsum(self._cnt, out=l_off[1:])
+            h[:P] = l_off[lq]
+            h[P:2 * P] = l_off[lq + 1]
+            h[2 * P:n64].view(np.int32)[:P] = (((np.arange(P, dtype=np.int64) - lq) * K) % (1 << 32)).astype(
+                np.uint32).view(np.int32)
+            d = self._pin[:n64].to(dev, non_blocking=True)
+            pull = {"r_end": d[P:2 * P], "r_slot_delta": d[2 * P:].view(torch.int32)[:P]}
+            return self._merge_round(d[:P], self.ts, self.kv_off, self.kv_key, self.kv_val, n_lkv, 0,
+                                     pull=pull, n_r=n_r, n_pull_kv=n_rkv)
         # int64 fields: codes P | a_kr P+1 | r_off P+1 | r_kb P+1 | kdelta P | delta (int32, P)
         n64 = 5 * P + 3 + (P + 1) // 2
         if self._pin is None or self._pin.numel() < n64:
@@ -314,13 +334,20 @@ class Population:
         self.str_bytes, self.str_off = vals.arena()
         return self._merge_round(dec["r_off"], dec["r_ts"], dec["r_kv"], arena_k, arena_v, n_lkv, n_pairs)
 
-    def _merge_round(self, r_off, r_ts, r_kv, arena_k, arena_v, n_lkv: int, n_rkv: int) -> dict:
+    def _merge_round(self, r_off, r_ts, r_kv, arena_k, arena_v, n_lkv: int, n_rkv: int, pull: dict | None = None,
+                     n_r: int | None = None, n_pull_kv: int = 0) -> dict:
+        """pull: in-place R ranges (crdt_refmerge_batch_pull; r_ts / r_kv /
+        the arena are the population's own arrays, n_r the total of the
+        ranges, n_pull_kv their kv pairs)."""
         eng, dev, K = self.eng, self.eng.device, self.K
         # 2. the merge of every local replica
         packed = {"replicas": self.P, "n_slots": self.P * K, "l_off": self.off, "l_ts": self.ts,
                   "l_origin": self.origin, "l_kv": self.kv_off, "r_off": r_off, "r_ts": r_ts, "r_kv": r_kv,
                   "kv_key": arena_k[: n_lkv + n_rkv], "kv_val": arena_v[: n_lkv + n_rkv],
                   "str_bytes": self.str_bytes, "str_off": self.str_off}
+        if n_r is not None:
+            packed["n_r"] = n_r
+        n_rkv += n_pull_kv
         # 3. the next Diff: entries from the merge, kv pairs copied by the
         # merge's own tile pass (crdt_refmerge_batch_kv; kv_fused = False:
         # a segmented gather by src after the merge, crdt_seg_gather2_n).
@@ -329,15 +356,15 @@ class Population:
         # Diffs' entry and kv offsets per replica (the next round's sizes).
         # The fresh kv arena has room behind the pairs for the next round's
         # pulled pairs.
-        n_max = self.ts.numel() + r_ts.numel()
+        n_max = self.ts.numel() + (r_ts.numel() if n_r is None else n_r)
         new_kv = torch.empty(n_max + 1, dtype=torch.int64, device=dev)
         cap = 2 * max(n_lkv + n_rkv, 1)
         nk = torch.empty(cap, dtype=torch.int32, device=dev)
         nv = torch.empty(cap, dtype=torch.int32, device=dev)
         if self.kv_fused:
-            out = eng.refmerge_batch(packed, kv={"off": new_kv, "key": nk, "val": nv})
+            out = eng.refmerge_batch(packed, kv={"off": new_kv, "key": nk, "val": nv}, pull=pull)
         else:
-            out = eng.refmerge_batch(packed)
+            out = eng.refmerge_batch(packed, pull=pull)
             self._call("crdt_seg_gather2_n", n_max, _p(out["off"][self.P:]), _p(out["src"]), _p(self.kv_off),
                        _p(r_kv), _p(new_kv), _p(arena_k), _p(arena_k), _p(nk), _p(arena_v), _p(arena_v), _p(nv))
         ho = torch.cat([out["off"], new_kv[out["off"]]]).cpu().numpy()

@@ -240,7 +240,8 @@ int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_re
 /* crdt_refmerge_batch that also materialises the new Diff's kv pairs (the
  * values the reference's Diff.Put carries along with each key, main.go:60-64):
  * new entry i owns kv_key/kv_val[kv_off[i] .. kv_off[i+1]), a copy of its
- * source entry's pairs (out.src), and kv_off[out.off[replicas]] = the total.
+ * source entry's pairs (out.src), and kv_off[out.off[replicas]] = the total
+ * (also written at kv_off[n_l + n_r]).
  * The kv offsets come out of the merge's own passes, so the separate
  * segmented gather over out.src (crdt_seg_gather2_n) is not needed.
  * kv_off: capacity n_l + n_r + 1; kv_key / kv_val: capacity kv_cap (a total
@@ -253,6 +254,20 @@ typedef struct crdt_refmerge_kv_out {
 } crdt_refmerge_kv_out;
 int crdt_refmerge_batch_kv(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out,
                            const crdt_refmerge_kv_out *kv);
+/* In-place pulls (an anti-entropy round, main.go:226-261, where every
+ * replica's RemoteDiff is a peer's whole Diff already in HBM): replica p's R
+ * is r_ts / r_kv [r_off[p] .. r_end[p]) -- ranges may overlap and r_ts /
+ * r_kv / the kv arena may alias the L arrays, so no RemoteDiff is
+ * assembled.  r_slot_delta (nullable) is added (mod 2^32) to the key slot
+ * of every R pair of replica p (a peer's slots re-based to p's).  in->n_r =
+ * the total of the R ranges (outputs sized n_l + n_r); out.src of an R entry
+ * is -(its index in r_ts) - 1.  kv: nullable, as crdt_refmerge_batch_kv. */
+typedef struct crdt_refmerge_pull {
+    const uint64_t *r_end;          /* [replicas] */
+    const uint32_t *r_slot_delta;   /* [replicas] or NULL */
+} crdt_refmerge_pull;
+int crdt_refmerge_batch_pull(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt_refmerge_out *out,
+                             const crdt_refmerge_pull *pull, const crdt_refmerge_kv_out *kv);
 /* ts-range-sharded RefMerge (§8(e)): one batch of replicas whose logs are
  * split by ts range over G shards (one per GPU).  Steps per shard:
  *   1. crdt_refmerge_local_maxl -> all-reduce(MAX) over shards: max(L) per replica;

@@ -13,16 +13,19 @@ from gossip_util import K, _host_round, _local_writes, _pack, _rand_diff, _same_
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kv_fused", [True, False], ids=["kv_from_merge", "kv_gather"])
+@pytest.mark.parametrize("mode", ["inplace_kv", "inplace_gather", "assembled_kv", "assembled_gather"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_gossip_rounds_match_reference_simulation(eng, seed, kv_fused):
-    """kv_fused: the new Diff's kv pairs copied by the merge's tile pass
-    (crdt_refmerge_batch_kv, the default) or gathered by src afterwards."""
+def test_gossip_rounds_match_reference_simulation(eng, seed, mode):
+    """inplace: the merge reads the peers' Diffs where they lie
+    (crdt_refmerge_batch_pull, the default) / assembled: RemoteDiffs built by
+    segmented copies first; kv: the new Diff's kv pairs copied by the merge's
+    tile pass (the default) / gather: gathered by src afterwards."""
     rng = np.random.default_rng(seed)
     P = 7
     diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 40))) for i in range(P)]
     pop = gossip.Population(eng, _pack(diffs), K)
-    pop.kv_fused = kv_fused
+    pop.pull_inplace = mode.startswith("inplace")
+    pop.kv_fused = mode.endswith("_kv")
     for rnd in range(5):
         peers = gossip.random_peers(rng, P, 0, P)
         pop.round(peers)

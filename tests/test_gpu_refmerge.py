@@ -338,3 +338,63 @@ def test_batch_kv_output_capacity(eng):
     _assert_kv_output(h, out, plain, kv)
     _run_kv(eng, h, cap=total - 1)
     assert eng.device_status(clear=True) == 2
+
+
+def test_batch_pull_in_place_equals_assembled(eng):
+    """crdt_refmerge_batch_pull: every replica's R is a peer's L read in
+    place (overlapping ranges, self-pulls, key slots re-based by
+    r_slot_delta) == the same batch with each RemoteDiff assembled as a copy
+    (the peer's entries, its pairs' slots re-based) through
+    crdt_refmerge_batch_kv: same new Diffs, kv pairs and CurrentState."""
+    h = synth.refmerge_packed(13, 24, 3000)
+    P, S = h["replicas"], h["n_slots"] // h["replicas"]
+    q = (np.arange(P) * 7 + 3) % P                      # peers (replica 5: itself)
+    l_off, l_kv = h["l_off"], h["l_kv"]
+    kk, kv_val = np.asarray(h["kv_key"]).view(np.uint32), np.asarray(h["kv_val"])
+    sd = ((np.arange(P) - q) * S) % (1 << 32)
+    # assembled: R_p = a copy of L_q, its pairs appended to the arena with re-based slots
+    r_off, r_ts, r_kv, ek, ev = [0], [], [], [], []
+    base = len(kk)
+    for p in range(P):
+        a, b = int(l_off[q[p]]), int(l_off[q[p] + 1])
+        r_ts.append(h["l_ts"][a:b])
+        for e in range(a, b):
+            r_kv.append(base)
+            x, y = int(l_kv[e]), int(l_kv[e + 1])
+            ek.append(((kk[x:y].astype(np.int64) + int(sd[p])) % (1 << 32)).astype(np.uint32))
+            ev.append(kv_val[x:y])
+            base += y - x
+        r_off.append(r_off[-1] + b - a)
+    r_kv.append(base)
+    ha = dict(h, r_off=np.array(r_off, np.int64), r_ts=np.concatenate(r_ts), r_kv=np.array(r_kv, np.int64),
+              kv_key=np.concatenate([kk] + ek).view(np.int32), kv_val=np.concatenate([kv_val] + ev))
+    out_a, _, kv_a = _run_kv(eng, ha)
+    # in place: R ranges of the L arrays
+    hi = dict(h, r_off=l_off[q].copy(), r_ts=h["l_ts"], r_kv=l_kv)
+    d = refmerge.to_device(hi, eng.device)
+    d["n_r"] = int(r_off[-1])
+    n = len(h["l_ts"]) + d["n_r"]
+    kv_i = {"off": torch.full((n + 1,), -1, dtype=torch.int64, device=eng.device),
+            "key": torch.zeros(2 * base, dtype=torch.int32, device=eng.device),
+            "val": torch.zeros(2 * base, dtype=torch.int32, device=eng.device)}
+    pull = {"r_end": torch.from_numpy(l_off[q + 1].copy()).to(eng.device),
+            "r_slot_delta": torch.from_numpy(sd.astype(np.uint32).view(np.int32)).to(eng.device)}
+    out_i = eng.refmerge_batch(d, kv=kv_i, pull=pull)
+    assert eng.device_status(clear=True) == 0
+    n_out = int(out_a["off"][-1])
+    for k in ("off", "st_kind", "st_str", "st_sum"):
+        assert torch.equal(out_i[k], out_a[k]), k
+    for k in ("ts", "origin"):
+        assert torch.equal(out_i[k][:n_out], out_a[k][:n_out]), k
+    # src: an R entry's index in the assembled R <-> its L index in place
+    sa, si = out_a["src"][:n_out].cpu().numpy(), out_i["src"][:n_out].cpu().numpy()
+    np.testing.assert_array_equal(si >= 0, sa >= 0)
+    np.testing.assert_array_equal(si[sa >= 0], sa[sa >= 0])
+    ra = np.array(r_off, np.int64)
+    j = -sa[sa < 0] - 1
+    p_of = np.searchsorted(ra, j, side="right") - 1
+    np.testing.assert_array_equal(-si[sa < 0] - 1, l_off[q[p_of]] + (j - ra[p_of]))
+    m = int(kv_a["off"][n_out])
+    assert int(kv_i["off"][n_out]) == m and int(kv_i["off"][n]) == m
+    assert torch.equal(kv_i["off"][: n_out + 1], kv_a["off"][: n_out + 1])
+    assert torch.equal(kv_i["key"][:m], kv_a["key"][:m]) and torch.equal(kv_i["val"][:m], kv_a["val"][:m])
