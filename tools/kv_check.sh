@@ -11,4 +11,4 @@ for wl in gossip_round gossip_round_wire; do
   echo "$wl $(python -c "import json; d=json.load(open('gpurun_out/kv_$wl.json')); print(d['ms_per_step'], d['roofline']['frac'])")"
 done
 bash tools/kstats.sh gossip_round
-CRDT_GOSSIP_PULL=inplace timeout -k 10 300 python bench.py --workload gossip_round --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/kv_gossip_inplace.json 2>/dev/null && python -c "import json; d=json.load(open('gpurun_out/kv_gossip_inplace.json')); print("inplace", d['ms_per_step'], d['roofline']['frac'])"
+CRDT_GOSSIP_PULL=inplace timeout -k 10 300 python bench.py --workload gossip_round --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/kv_gossip_inplace.json 2>/dev/null && python -c "import json; d=json.load(open('gpurun_out/kv_gossip_inplace.json')); print('inplace', d['ms_per_step'], d['roofline']['frac'])"
