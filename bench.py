@@ -806,8 +806,8 @@ class GossipRound(Workload):
                 "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
                 "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
         self.pop = gossip.Population(eng, host, 62)
-        # (A/B: CRDT_GOSSIP_PULL=inplace reads the peers' Diffs in place, crdt_refmerge_batch_pull)
-        self.pop.pull_inplace = os.environ.get("CRDT_GOSSIP_PULL", "assembled") != "assembled"
+        # (A/B: CRDT_GOSSIP_PULL=assembled builds each RemoteDiff by segmented copies first)
+        self.pop.pull_inplace = os.environ.get("CRDT_GOSSIP_PULL", "inplace") != "assembled"
         self.host = h
         self.init = self.pop.snapshot()
         self.rng = np.random.default_rng(seed)

@@ -71,7 +71,7 @@ class Population:
         self.str_off = t(host["str_off"], np.int64)
         self.state = None
         self.kv_fused = True                  # new Diff's kv pairs from the merge's tile pass
-        self.pull_inplace = False             # local rounds: the merge reads the peers' Diffs in place
+        self.pull_inplace = True              # local rounds: the merge reads the peers' Diffs in place
         # per-replica entry / kv-pair counts of the Diffs on the host: a round
         # sizes the pulled arrays from them (no host round trip up front) and
         # refreshes them in its one read-back at the end; None = unknown (after
@@ -247,7 +247,7 @@ class Population:
         n_lkv = self.kv_key.numel()
         cnt, kvc = self._cnt[lq], self._kvcnt[lq]
         n_r, n_rkv = int(cnt.sum()), int(kvc.sum())
-        if self.pull_inplace:
+        if self.pull_inplace and self.kv_fused:             # (the gather by src cannot re-base slots)
             # every replica's RemoteDiff is its peer's Diff where it lies in
             # HBM: the merge reads R ranges (r_off, r_end) of the population's
             # own arrays and re-bases the pulled key slots (r_slot_delta), so
