@@ -163,6 +163,8 @@ SIGNATURES = {
     "crdt_tuples_sort": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples)]),
     "crdt_u64_lower_bound": (_I, [_CTX, _P, _SZ, _P, _SZ, _P]),
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),
+    "crdt_tuples_merge": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
+                               C.POINTER(crdt_tuples)]),
     "crdt_refmerge_batch": (_I, [_CTX, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_atoi_batch": (_I, [_CTX, _P, _P, _U64, _P, _P]),
     "crdt_local_apply": (_I, [_CTX, C.POINTER(crdt_local_in), C.POINTER(crdt_local_out)]),
@@ -224,6 +226,8 @@ SIGNATURES = {
     "crdt_shard_unique_id": (_I, [_P, _SZ]),
     "crdt_shard_comm_create": (_I, [C.POINTER(_I), _I, C.POINTER(_P)]),
     "crdt_shard_comm_init_rank": (_I, [_CTX, _P, _I, _I, C.POINTER(_P)]),
+    "crdt_shard_comm_create_loopback": (_I, [_I, _I, C.POINTER(_P)]),
+    "crdt_shard_comm_transport": (_I, [_P, C.POINTER(_I)]),
     "crdt_shard_comm_destroy": (_I, [_P]),
     "crdt_shard_comm_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     "crdt_shard_member_ctx": (_I, [_P, _I, C.POINTER(_P)]),
@@ -243,6 +247,10 @@ SIGNATURES = {
                                         C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ), _I]),
     "crdt_shard_orset_merge_local": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples),
                                           C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_SZ), _I]),
+    "crdt_shard_lww_merge_local_dev": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples),
+                                            C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_P)]),
+    "crdt_shard_orset_merge_local_dev": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples),
+                                              C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_P)]),
     "crdt_shard_refmerge": (_I, [_P, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
     "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
     "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),

@@ -59,9 +59,9 @@ extern int g_vclock_pairs_per_wave;
 extern int g_vclock_blocks_per_cu;
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
 extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
-extern int g_sort_vec_up;
-extern int g_mm_bpc;
-extern int g_rdd_diag;          // OR-Set D2 group dedup timing diagnostic (sort.rdd_diag; 0 = off)            // sort minmax: workgroups per CU per input (sort.mm_blocks_per_cu)       // fused D2 sort: vectorised composing upsweep (sort.vec_up)
+extern int g_sort_vec_up;       // fused D2 sort: vectorised composing upsweep (sort.vec_up)
+extern int g_mm_bpc;            // sort minmax: workgroups per CU per input (sort.mm_blocks_per_cu)
+extern int g_rdd_diag;          // OR-Set D2 group dedup timing diagnostic (sort.rdd_diag; 0 = off)
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
@@ -69,9 +69,9 @@ extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmer
 extern int g_lww_chunk;         // set merges: tiles per count / write chunk (sets.lww_chunk, sets.or_chunk;
 extern int g_or_chunk;          //   0 = one chunk), DESIGN.md §5.4
 extern int g_shard_exchange_always;   // keyed-set shard merges run the exchange protocol on 1 rank too (tests)
-extern int g_set_streams;
+extern int g_set_streams;       // set merges: 1 = one stream, 2 = counts beside writes (sets.streams)
 extern int g_or_count_dma;      // OR-Set count pass staging (sets.or_count_dma)
-extern int g_or_key_sort;       // OR-Set D2 key-only sort (sort.or_key_only)       // set merges: 1 = one stream, 2 = counts beside writes (sets.streams)
+extern int g_or_key_sort;       // OR-Set D2 key-only sort (sort.or_key_only)
 extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests
 extern std::atomic<int> g_fail_zero_bits;  // fault injection ("fail.zero_bits"): bitmaps zeroed between passes
 bool take_fail_zero_bits();                // consumes one "fail.zero_bits" count
@@ -81,6 +81,9 @@ int ctx_aux(crdt_ctx *ctx);
 int ctx_events(crdt_ctx *ctx, size_t n);
 
 void server_ctx_release(crdt_ctx *ctx);   // server.hip: the context's Server-merge scratch
+// sets.hip: out = the stable merge of A and B, all na + nb tuples (crdt_tuples_merge)
+int tuples_merge_stable(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
+                        const crdt_tuples &O);
 // gossip.hip: crdt_seg_gather2 (4-byte elements, base 0) over n_max segments
 // of which the first *n_dev are real (a count still on the device)
 int seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,

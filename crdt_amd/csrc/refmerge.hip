@@ -125,6 +125,12 @@ struct RmIn : crdt_refmerge_in {
 __device__ __forceinline__ uint64_t r_hi(const RmIn &in, uint32_t p) {
     return in.r_end ? in.r_end[p] : in.r_off[p + 1];
 }
+// R entries of replica p; a reversed range (r_end < r_off) counts as empty
+// and the planning passes raise CRDT_DEV_RANGE for it
+__device__ __forceinline__ uint64_t r_len(const RmIn &in, uint32_t p) {
+    const uint64_t b = in.r_off[p], e = r_hi(in, p);
+    return e > b ? e - b : 0;
+}
 
 // The tile's L / R entry counts: its L range ends where the next tile's
 // begins (same replica: d0 > 0) or at the replica's L end.
@@ -169,9 +175,10 @@ __device__ __forceinline__ uint64_t kv_len(uint64_t kb, uint64_t ke, uint64_t n_
     return kb < e ? e - kb : 0;
 }
 
-__global__ void k_rm_ntiles(RmIn in, uint32_t *__restrict__ nt) {
+__global__ void k_rm_ntiles(RmIn in, uint32_t *__restrict__ nt, uint32_t *__restrict__ err) {
     for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < in.replicas; p += gridDim.x * 256) {
-        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (r_hi(in, p) - in.r_off[p]);
+        if (r_hi(in, p) < in.r_off[p]) atomicOr(err, CRDT_DEV_RANGE);
+        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + r_len(in, p);
         nt[p] = (uint32_t)((n + MT - 1) / MT);
     }
 }
@@ -263,7 +270,7 @@ __device__ __forceinline__ TileGeo tile_geo(const RmIn &in, const uint64_t *__re
     g.lb = in.l_off[lo];
     g.nl = in.l_off[lo + 1] - g.lb;
     g.rb = in.r_off[lo];
-    g.nr = r_hi(in, lo) - g.rb;
+    g.nr = r_len(in, lo);
     g.maxl = maxl_ovr ? maxl_ovr[lo] : g.nl ? in.l_ts[g.lb + g.nl - 1] : INT64_MIN;   // empty L: nothing inserted
     g.first = (uint32_t)tbase[lo];
     g.d0 = (t - tbase[lo]) * MT;
@@ -280,14 +287,18 @@ __global__ __launch_bounds__(256) void k_rm_split(RmIn in, uint32_t replicas,
                                                   const uint64_t *__restrict__ tbase,
                                                   const int64_t *__restrict__ maxl_ovr, uint64_t tmax,
                                                   TileDesc *__restrict__ desc, OkVal *__restrict__ okv, SlotAcc acc,
-                                                  uint32_t ns) {
+                                                  uint32_t ns, uint32_t *__restrict__ err) {
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     prep_items(in.str_bytes, in.str_off, in.n_str, okv, acc, ns, (uint64_t)blockIdx.x * 256 + threadIdx.x,
                (uint64_t)gridDim.x * 256);
     if (t > tmax) return;                                // desc[tmax]: always an empty sentinel
     TileDesc d = {};
-    if (t < tbase[replicas]) {
+    // more tiles than planned (R ranges summing past n_r): every tile left
+    // empty -- nothing is read or written past the sizes the call was given
+    const uint64_t tiles = tbase[replicas];
+    if (tiles > tmax && t == 0 && lane == 0) atomicOr(err, CRDT_DEV_RANGE);
+    if (t < tiles && tiles <= tmax) {
         const TileGeo g = tile_geo(in, tbase, maxl_ovr, t);
         int64_t lprev;
         const uint64_t a0 = wave_split<RM_SPLIT_PW>(in.l_ts + g.lb, g.nl, in.r_ts + g.rb, g.nr, g.d0, lane, &lprev);
@@ -1055,24 +1066,32 @@ __device__ __forceinline__ void small_scan(Get get, uint32_t n, uint64_t *__rest
 }
 
 // tbase = exclusive scan of the per-replica tile counts (tbase[np] = tiles)
-__global__ __launch_bounds__(SB) void k_rm_plan_small(RmIn in, uint64_t *__restrict__ tbase) {
+__global__ __launch_bounds__(SB) void k_rm_plan_small(RmIn in, uint64_t *__restrict__ tbase,
+                                                      uint32_t *__restrict__ err) {
     __shared__ uint64_t s_w[SB / 64];
     small_scan([&](uint32_t p) -> uint64_t {
-        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + (r_hi(in, p) - in.r_off[p]);
+        if (r_hi(in, p) < in.r_off[p]) atomicOr(err, CRDT_DEV_RANGE);
+        const uint64_t n = (in.l_off[p + 1] - in.l_off[p]) + r_len(in, p);
         return (n + MT - 1) / MT;
     }, in.replicas, tbase, s_w);
 }
 
 // ic = exclusive scan of tcnt[0..n) (ic[n] = total), then
-// out.off[p] = l_off[p] + ic[tbase[p]]
+// out.off[p] = l_off[p] + ic[tbase[p]].  More tiles than the n planned (R
+// ranges summing past n_r): CRDT_DEV_RANGE, no offsets written.
 // KV (tkv non-null): also ikv = exclusive scan of tkv, and the new Diff's
 // closing kv offset kv_off[out_off[replicas]] = the kv total.
 __global__ __launch_bounds__(SB) void k_rm_scan_small(const uint32_t *__restrict__ tcnt, uint32_t n,
                                                       uint64_t *__restrict__ ic, crdt_refmerge_in in,
                                                       const uint64_t *__restrict__ tbase,
                                                       uint64_t *__restrict__ out_off, const uint64_t *__restrict__ tkv,
-                                                      uint64_t *__restrict__ ikv, uint64_t *__restrict__ kv_off) {
+                                                      uint64_t *__restrict__ ikv, uint64_t *__restrict__ kv_off,
+                                                      uint32_t *__restrict__ err) {
     __shared__ uint64_t s_w[SB / 64];
+    if (tbase[in.replicas] > n) {                        // (uniform: every thread reads the same word)
+        if (threadIdx.x == 0) atomicOr(err, CRDT_DEV_RANGE);
+        return;
+    }
     small_scan([&](uint32_t i) -> uint64_t { return tcnt[i]; }, n, ic, s_w);
     if (tkv) small_scan([&](uint32_t i) -> uint64_t { return tkv[i]; }, n, ikv, s_w);
     __syncthreads();                                     // ic / ikv visible to the whole workgroup
@@ -1093,7 +1112,11 @@ __global__ void k_rm_prep(const uint8_t *__restrict__ bytes, const uint64_t *__r
 // (KV: kv_off[out_off[replicas]] = kv total, ikv_total = &ikv[tiles])
 __global__ void k_out_off(crdt_refmerge_in in, const uint64_t *__restrict__ tbase, const uint64_t *__restrict__ ic,
                           uint64_t *__restrict__ out_off, const uint64_t *__restrict__ ikv_total,
-                          uint64_t *__restrict__ kv_off) {
+                          uint64_t *__restrict__ kv_off, uint64_t tmax, uint32_t *__restrict__ err) {
+    if (tbase[in.replicas] > tmax) {                     // (see k_rm_scan_small)
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, CRDT_DEV_RANGE);
+        return;
+    }
     for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p <= in.replicas; p += gridDim.x * 256) {
         out_off[p] = in.l_off[p] + ic[tbase[p]];
         if (kv_off && p == in.replicas) {
@@ -1152,7 +1175,9 @@ extern "C" int crdt_refmerge_batch_kv(crdt_ctx *ctx, const crdt_refmerge_in *inp
 
 extern "C" int crdt_refmerge_batch_pull(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
                                         const crdt_refmerge_pull *pull, const crdt_refmerge_kv_out *kv) {
-    if (!pull || !pull->r_end) return CRDT_E_INVAL;
+    // re-based key slots need the fused kv output: a caller gathering the new
+    // Diff's pairs by src afterwards cannot re-base them
+    if (!pull || !pull->r_end || (pull->r_slot_delta && !kv)) return CRDT_E_INVAL;
     return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr, kv, pull);
 }
 
@@ -1253,16 +1278,16 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     const unsigned cap = (unsigned)ctx->num_cus * 8;
     const uint32_t reps = in.replicas;
     if (np <= kSmallPlan) {
-        k_rm_plan_small<<<1, SB, 0, s>>>(in, tbase);
+        k_rm_plan_small<<<1, SB, 0, s>>>(in, tbase, ctx->dev_status);
     } else {
-        k_rm_ntiles<<<grid_for(np, 256, cap), 256, 0, s>>>(in, nt);
+        k_rm_ntiles<<<grid_for(np, 256, cap), 256, 0, s>>>(in, nt, ctx->dev_status);
         rc = check_launch(ctx);
         if (rc) return rc;
         rc = exclusive_scan_u32(ctx, nt, tbase, np, tmp);         // tbase[np] = tile count
         if (rc) return rc;
     }
     k_rm_split<<<(unsigned)((tmax + 4) / 4), 256, 0, s>>>(in, reps, tbase, maxl_dev, tmax, desc, okv, acc,
-                                                           (uint32_t)ns);
+                                                           (uint32_t)ns, ctx->dev_status);
     // tile grids = the tile-count upper bound; empty descriptors exit at once
     // (count-pass shapes at 4096-item tiles: 256 x 16 51 us, 512 x 8 45 us, 1024 x 4 67 us)
     // LDS-DMA staging of the ts runs when both logs are 8-byte aligned (refmerge.count_dma)
@@ -1276,7 +1301,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // ~11 ns each and the tail runs alone after the grid)
     if (tmax <= kSmallPlan) {
         k_rm_scan_small<<<1, SB, 0, s>>>(tcnt, (uint32_t)tmax, ic, in, tbase, out.off, tkv, ikv,
-                                         kv ? kv->kv_off : nullptr);
+                                         kv ? kv->kv_off : nullptr, ctx->dev_status);
     } else {
         rc = exclusive_scan_u32(ctx, tcnt, ic, tmax, tmp);
         if (rc) return rc;
@@ -1286,7 +1311,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
             k_scan_tsums<<<1, 256, 0, s>>>(ikv, tmax, 0, ikv + tmax);
         }
         k_out_off<<<grid_for(np + 1, 256, cap), 256, 0, s>>>(in, tbase, ic, out.off, kv ? ikv + tmax : nullptr,
-                                                              kv ? kv->kv_off : nullptr);
+                                                              kv ? kv->kv_off : nullptr, tmax, ctx->dev_status);
     }
     if (take_fail_zero_bits()) {                                  // failpoint: the tile pass must flag, not fault
         hipError_t e = hipMemsetAsync(bits, 0, tmax * 2 * NW * 8, s);

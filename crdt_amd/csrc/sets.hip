@@ -962,6 +962,83 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
                     ntiles * 2 * ONW * 8);
 }
 
+// ---------------------------------------------------------------- stable merge (no dedup)
+// out = the stable merge of A and B (every tuple kept; on an equal tag A's
+// copies first) -- the rank-order merge of the runs a key-range owner
+// receives in crdt_shard_*_merge_local.  Its length is na + nb, known on the
+// host, so a tree of these merges needs no read-back between levels.  Tiles
+// of OT merge items from k_or_split; per tile both runs staged in LDS, every
+// item's output position = its index in its run + its rank in the other run
+// (B elements strictly below an A tag, A elements at or below a B tag).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_tmerge(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                               const uint64_t *__restrict__ split, crdt_tuples out) {
+    constexpr int NI = OT / NT;
+    __shared__ uint64_t sk[OT], st[OT];
+    __shared__ uint32_t sr[OT];
+    const uint64_t t = blockIdx.x;
+    const LwwTile b = or_tile(split, t, na + nb);
+    uint64_t k[NI], ts[NI];
+    uint32_t r[NI];
+    uint8_t m[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {                       // A run at slots [0, na), B run at [na, n)
+        const uint32_t x = threadIdx.x + (uint32_t)j * NT;
+        const bool v = x < b.n, on_a = x < b.na;
+        const size_t g = on_a ? b.i0 + x : b.j0 + (x - b.na);
+        const crdt_tuples &S = on_a ? A : B;
+        k[j] = v ? S.key[g] : 0;
+        ts[j] = v ? S.ts[g] : 0;
+        r[j] = v ? S.rep[g] : 0;
+        m[j] = v ? S.tomb[g] : 0;
+        if (v) {
+            sk[x] = k[j];
+            st[x] = ts[j];
+            sr[x] = r[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const uint32_t x = threadIdx.x + (uint32_t)j * NT;
+        if (x >= b.n) continue;
+        const Tag me{k[j], ts[j], r[j]};
+        const bool on_a = x < b.na;
+        // rank in the other run: B below an A tag (strict), A at or below a B tag
+        uint32_t lo = 0, hi = on_a ? b.nb : b.na;
+        const uint32_t base = on_a ? b.na : 0;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const Tag o{sk[base + mid], st[base + mid], sr[base + mid]};
+            const bool before = on_a ? !tag_le(me, o) : tag_le(o, me);
+            if (before) lo = mid + 1;
+            else hi = mid;
+        }
+        const size_t pos = (size_t)t * OT + (on_a ? x : x - b.na) + lo;
+        out.key[pos] = k[j];
+        out.ts[pos] = ts[j];
+        out.rep[pos] = r[j];
+        out.tomb[pos] = m[j];
+    }
+}
+
+int tuples_merge_stable(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
+                        const crdt_tuples &O) {
+    const size_t n = na + nb;
+    if (n == 0) return CRDT_OK;
+    const size_t ntiles = (n + OT - 1) / OT;
+    if (ntiles >= 0x7fffffffULL || n >= (1ULL << 62)) return CRDT_E_RANGE;
+    int rc = ws_reserve(ctx, Carve::round((ntiles + 1) * 8) + 1024);
+    if (rc) return rc;
+    Carve w(ctx->ws);
+    uint64_t *split = w.take<uint64_t>(ntiles + 1);
+    const crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
+    const crdt_tuples &a = na ? A : empty, &b = nb ? B : empty;
+    k_or_split<<<(unsigned)((ntiles + 1 + 15) / 16), 256, 0, ctx->stream>>>(a, b, na, nb, ntiles, split);
+    k_tmerge<512><<<(unsigned)ntiles, 512, 0, ctx->stream>>>(a, b, na, nb, split, O);
+    return check_launch(ctx);
+}
+
 // Adjacent pairs out of (key, ts, rep) order.
 __global__ void k_count_unsorted(crdt_tuples T, size_t n, unsigned long long *bad) {
     unsigned long long c = 0;
@@ -1009,6 +1086,15 @@ extern "C" int crdt_lww_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
 extern "C" int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
                                 crdt_tuples *out, uint64_t *out_count_dev) {
     return set_merge<false>(ctx, a, na, b, nb, out, out_count_dev);
+}
+
+extern "C" int crdt_tuples_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
+                                 const crdt_tuples *out) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if ((na + nb && !tuples_ok(out)) || (na && !tuples_ok(a)) || (nb && !tuples_ok(b))) return CRDT_E_INVAL;
+    const crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
+    return tuples_merge_stable(ctx, na ? *a : empty, na, nb ? *b : empty, nb, na + nb ? *out : empty);
 }
 
 extern "C" int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n, uint64_t *bad) {

@@ -1,32 +1,42 @@
-// shard.hip -- replica-sharded joins over RCCL (SURVEY §8(a) a9, §8(b) crdt_shard_*, §8(e)).
+// shard.hip -- replica-sharded joins over a collective transport (SURVEY §8(a) a9, §8(b) crdt_shard_*, §8(e)).
 //
 // The reference has no collective: its replicas exchange whole logs by HTTP
 // pull gossip (main.go:226-258).  Here a replica population is sharded over
-// the GPUs of one node and the cross-shard join is one RCCL collective over
-// xGMI:
+// the GPUs of one node and the cross-shard join is a collective over xGMI:
 //   * counters / clocks: every member folds its contiguous row shard
-//     (crdt_gcounter_fold), then ONE ncclAllReduce(ncclUint64, ncclMax) of the
-//     `nodes`-long fold -- RCCL's unsigned 64-bit max is exactly the join, so
-//     no order map is needed on this path;
-//   * divergent full-state copies (config E2): ncclAllReduce(ncclUint64,
-//     ncclMax) in place;
-//   * keyed sets: members own disjoint ordered key ranges, merge them locally
-//     and an all-gather-v (counts by ncclAllGather, then one grouped
-//     ncclBroadcast per root and field) concatenates the outputs in rank order,
-//     which is already the globally sorted merged state (a key's LWW / OR-Set
-//     output depends only on that key's tuples);
+//     (crdt_gcounter_fold), then ONE all-reduce(max) of the `nodes`-long fold
+//     -- RCCL's unsigned 64-bit max is exactly the join, no order map;
+//   * divergent full-state copies (config E2): all-reduce(max) in place;
+//   * keyed sets: members own disjoint ordered key ranges, merge them locally,
+//     and an all-gather-v (counts by an all-gather, then ONE group of
+//     point-to-point transfers) concatenates the outputs in rank order, which
+//     is already the globally sorted merged state (a key's LWW / OR-Set output
+//     depends only on that key's tuples);
 //   * keyed sets of a DISTRIBUTED population (every rank holds only its own
-//     tuples, crdt_shard_*_merge_local): sampled splitters (one ncclAllGather),
-//     each rank's tuples sent to their key-range owner (grouped ncclSend /
-//     ncclRecv, an all-to-all-v), the owner's merge of the received runs,
-//     then the all-gather-v above;
+//     tuples, crdt_shard_*_merge_local): sampled splitters (one all-gather),
+//     the count matrix (one all-gather), every rank's tuples sent to their
+//     key-range owner in ONE point-to-point group (an all-to-all-v of every
+//     field of both sides), the owner's stable rank-order merges of the
+//     received runs (lengths known on the host: no read-back between levels)
+//     and one set merge;
 //   * RefMerge of one batch whose logs are split by ts range over the ranks
 //     (crdt_shard_refmerge): all-reduce(max) of max(L), the local merge, then
 //     integer all-reduces of the replay accumulators (main.go:35-100).
-// A communicator has one or more LOCAL members (device + crdt_ctx + ncclComm):
-// crdt_shard_comm_create drives every listed GPU from one process
-// (ncclCommInitAll, grouped calls); crdt_shard_comm_init_rank makes one member
-// per process (ncclCommInitRank; torchrun-style one process per GPU).
+//
+// Transport (SURVEY §4's pluggable collective): every protocol above is
+// written against three collectives -- in-place all-reduce (sum / max),
+// all-gather, and a group of point-to-point sends / receives -- that a
+// communicator's transport implements:
+//   * RCCL (crdt_shard_comm_create: ncclCommInitAll, one process drives every
+//     listed GPU; crdt_shard_comm_init_rank: ncclCommInitRank, one process per
+//     GPU) -- the transport of every real multi-GPU communicator;
+//   * loopback (crdt_shard_comm_create_loopback): M members on ONE device in
+//     one process, each with its own crdt_ctx and stream; the collectives are
+//     device copies and a reduction kernel on a transport stream, fenced by
+//     events against the member streams (no host synchronisation).  It runs
+//     the same planning, offsets, tree merges and reductions at R > 1 on a
+//     one-GPU machine.
+// The compute (folds, merges, RefMerge) is the same code on either transport.
 #include <rccl/rccl.h>
 #include <string.h>
 
@@ -38,30 +48,243 @@
 
 static_assert(sizeof(ncclUniqueId) == CRDT_SHARD_ID_BYTES, "RCCL unique id size");
 
+namespace crdt {
+enum class XType { U8, U32, I32, U64, I64 };
+enum class XOp { Sum, Max };
+// One point-to-point transfer of a group: member `member` sends `bytes` from
+// sbuf to global rank `peer`, or receives `bytes` from it into rbuf.  Sends
+// and receives of one (sender, receiver) pair are matched in issue order.
+struct XP2P {
+    size_t member;
+    int peer;
+    bool send;
+    const void *sbuf;
+    void *rbuf;
+    size_t bytes;
+};
+struct Transport;
+}  // namespace crdt
+
 struct crdt_comm {
     struct Member {
         int device = 0;
         crdt_ctx *ctx = nullptr;
         bool own_ctx = false;
-        ncclComm_t nccl = nullptr;
+        ncclComm_t nccl = nullptr;    // RCCL transport only
         void *scratch = nullptr;      // per-member device scratch (set-merge slices, counts)
         size_t scratch_bytes = 0;
     };
     int nranks = 0;                   // ranks over all processes
     int rank0 = 0;                    // global rank of local member 0
     int last_nccl_error = 0;
+    int kind = CRDT_SHARD_RCCL;
     std::vector<Member> m;
+    crdt::Transport *x = nullptr;     // owned
 };
 
 namespace crdt {
-namespace {
 
 int nccl_fail(crdt_comm *c, ncclResult_t r) {
     if (c) c->last_nccl_error = (int)r;
     return CRDT_E_COMM;
 }
 
-// Grow a member's scratch to `bytes` (the member's stream is drained first).
+// The collectives every protocol of this file is written against.  Per-member
+// arguments are indexed by local member; all work is enqueued on the member
+// streams (stream-ordered with the member's earlier and later work).
+struct Transport {
+    virtual ~Transport() {}
+    // buf[i] (n elements) := elementwise op over every rank's buf, in place
+    virtual int allreduce(crdt_comm *c, void *const *buf, size_t n, XType t, XOp op) = 0;
+    // every member's recv[i] + r * bytes := rank r's `bytes` at its send
+    // (a send may alias its own rank's slot of recv)
+    virtual int allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes) = 0;
+    // one group of point-to-point transfers
+    virtual int p2p(crdt_comm *c, const std::vector<XP2P> &ops) = 0;
+};
+
+namespace {
+
+// ---------------------------------------------------------------- RCCL transport
+ncclDataType_t nccl_type(XType t) {
+    switch (t) {
+        case XType::U8: return ncclUint8;
+        case XType::U32: return ncclUint32;
+        case XType::I32: return ncclInt32;
+        case XType::U64: return ncclUint64;
+        default: return ncclInt64;
+    }
+}
+
+struct RcclTransport final : Transport {
+    static int group_end(crdt_comm *c, ncclResult_t r) {
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess) return nccl_fail(c, r);
+        if (r2 != ncclSuccess) return nccl_fail(c, r2);
+        return CRDT_OK;
+    }
+    int allreduce(crdt_comm *c, void *const *buf, size_t n, XType t, XOp op) override {
+        ncclResult_t r = ncclGroupStart();
+        for (size_t i = 0; i < c->m.size() && r == ncclSuccess; ++i)
+            r = ncclAllReduce(buf[i], buf[i], n, nccl_type(t), op == XOp::Max ? ncclMax : ncclSum, c->m[i].nccl,
+                              c->m[i].ctx->stream);
+        return group_end(c, r);
+    }
+    int allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes) override {
+        ncclResult_t r = ncclGroupStart();
+        for (size_t i = 0; i < c->m.size() && r == ncclSuccess; ++i)
+            r = ncclAllGather(send[i], recv[i], bytes, ncclUint8, c->m[i].nccl, c->m[i].ctx->stream);
+        return group_end(c, r);
+    }
+    int p2p(crdt_comm *c, const std::vector<XP2P> &ops) override {
+        ncclResult_t r = ncclGroupStart();
+        for (size_t k = 0; k < ops.size() && r == ncclSuccess; ++k) {
+            const XP2P &o = ops[k];
+            const auto &mb = c->m[o.member];
+            r = o.send ? ncclSend(o.sbuf, o.bytes, ncclUint8, o.peer, mb.nccl, mb.ctx->stream)
+                       : ncclRecv(o.rbuf, o.bytes, ncclUint8, o.peer, mb.nccl, mb.ctx->stream);
+        }
+        return group_end(c, r);
+    }
+};
+
+// ---------------------------------------------------------------- loopback transport
+constexpr int kLoopMax = 64;              // members of a loopback communicator
+struct PtrTab {
+    void *p[kLoopMax];
+};
+
+// buf[m][i] := op over m of buf[m][i], for every member m (in place: each
+// element's inputs are read before any of its outputs is written).  Sums are
+// taken in the unsigned type (two's complement wrap, main.go:95).
+template <class T, bool MAX>
+__global__ void k_loop_allreduce(PtrTab t, int M, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        T acc = ((const T *)t.p[0])[i];
+        for (int m = 1; m < M; ++m) {
+            const T v = ((const T *)t.p[m])[i];
+            acc = MAX ? (v > acc ? v : acc) : (T)(acc + v);
+        }
+        for (int m = 0; m < M; ++m) ((T *)t.p[m])[i] = acc;
+    }
+}
+
+struct LoopTransport final : Transport {
+    crdt_ctx *ctx = nullptr;              // the transport's own stream (a context for its errors)
+    hipEvent_t done = nullptr;
+    std::vector<hipEvent_t> ev;           // one per member
+
+    ~LoopTransport() override {
+        if (ctx) {
+            (void)bind(ctx);
+            (void)hipStreamSynchronize(ctx->stream);
+        }
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (done) (void)hipEventDestroy(done);
+        if (ctx) (void)crdt_ctx_destroy(ctx);
+    }
+    int init(int device, size_t members) {
+        void *s = nullptr;
+        int rc = crdt_stream_create(device, &s);
+        if (rc) return rc;
+        rc = crdt_ctx_create(device, s, &ctx);
+        if (rc) {
+            (void)crdt_stream_destroy(s);
+            return rc;
+        }
+        ctx->own_stream = true;
+        rc = bind(ctx);
+        if (rc) return rc;
+        ev.assign(members, nullptr);
+        hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+        for (size_t i = 0; i < members && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    }
+    // the transport stream waits for every member's earlier work ...
+    int fence_in(crdt_comm *c) {
+        int rc = bind(ctx);
+        if (rc) return rc;
+        hipError_t e = hipSuccess;
+        for (size_t i = 0; i < c->m.size() && e == hipSuccess; ++i) {
+            e = hipEventRecord(ev[i], c->m[i].ctx->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, ev[i], 0);
+        }
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    }
+    // ... and every member's later work waits for the collective
+    int fence_out(crdt_comm *c) {
+        hipError_t e = hipEventRecord(done, ctx->stream);
+        for (size_t i = 0; i < c->m.size() && e == hipSuccess; ++i) e = hipStreamWaitEvent(c->m[i].ctx->stream, done, 0);
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    }
+    int copy(void *dst, const void *src, size_t bytes) {
+        if (!bytes || dst == src) return CRDT_OK;
+        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    }
+    int allreduce(crdt_comm *c, void *const *buf, size_t n, XType t, XOp op) override {
+        const int M = (int)c->m.size();
+        PtrTab p{};
+        for (int i = 0; i < M; ++i) p.p[i] = buf[i];
+        int rc = fence_in(c);
+        if (rc) return rc;
+        const unsigned g = grid_for(n, 256, (unsigned)ctx->num_cus * 4);
+        const hipStream_t s = ctx->stream;
+        const bool mx = op == XOp::Max;
+        switch (t) {
+            case XType::U8:
+                mx ? k_loop_allreduce<uint8_t, true><<<g, 256, 0, s>>>(p, M, n)
+                   : k_loop_allreduce<uint8_t, false><<<g, 256, 0, s>>>(p, M, n);
+                break;
+            case XType::U32:
+                mx ? k_loop_allreduce<uint32_t, true><<<g, 256, 0, s>>>(p, M, n)
+                   : k_loop_allreduce<uint32_t, false><<<g, 256, 0, s>>>(p, M, n);
+                break;
+            case XType::I32:
+                mx ? k_loop_allreduce<int32_t, true><<<g, 256, 0, s>>>(p, M, n)
+                   : k_loop_allreduce<uint32_t, false><<<g, 256, 0, s>>>(p, M, n);
+                break;
+            case XType::U64:
+                mx ? k_loop_allreduce<uint64_t, true><<<g, 256, 0, s>>>(p, M, n)
+                   : k_loop_allreduce<uint64_t, false><<<g, 256, 0, s>>>(p, M, n);
+                break;
+            case XType::I64:
+                mx ? k_loop_allreduce<int64_t, true><<<g, 256, 0, s>>>(p, M, n)
+                   : k_loop_allreduce<uint64_t, false><<<g, 256, 0, s>>>(p, M, n);
+                break;
+        }
+        rc = check_launch(ctx);
+        return rc ? rc : fence_out(c);
+    }
+    int allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes) override {
+        int rc = fence_in(c);
+        for (size_t j = 0; j < c->m.size() && !rc; ++j)
+            for (size_t q = 0; q < c->m.size() && !rc; ++q) rc = copy((char *)recv[j] + q * bytes, send[q], bytes);
+        return rc ? rc : fence_out(c);
+    }
+    int p2p(crdt_comm *c, const std::vector<XP2P> &ops) override {
+        const size_t M = c->m.size();
+        std::vector<std::vector<const XP2P *>> snd(M * M), rcv(M * M);   // [from * M + to]
+        for (const XP2P &o : ops) {
+            if (o.peer < 0 || (size_t)o.peer >= M || o.member >= M) return CRDT_E_INVAL;
+            (o.send ? snd[o.member * M + o.peer] : rcv[(size_t)o.peer * M + o.member]).push_back(&o);
+        }
+        for (size_t k = 0; k < M * M; ++k) {
+            if (snd[k].size() != rcv[k].size()) return nccl_fail(c, ncclInvalidUsage);
+            for (size_t j = 0; j < snd[k].size(); ++j)
+                if (snd[k][j]->bytes != rcv[k][j]->bytes) return nccl_fail(c, ncclInvalidUsage);
+        }
+        int rc = fence_in(c);
+        for (size_t k = 0; k < M * M && !rc; ++k)
+            for (size_t j = 0; j < snd[k].size() && !rc; ++j) rc = copy(rcv[k][j]->rbuf, snd[k][j]->sbuf, snd[k][j]->bytes);
+        return rc ? rc : fence_out(c);
+    }
+};
+
+// ---------------------------------------------------------------- helpers
+// Grow a member's scratch to `bytes` (the member's stream is drained first;
+// the old contents are lost).
 int scratch_reserve(crdt_comm::Member &mb, size_t bytes) {
     if (bytes <= mb.scratch_bytes) return CRDT_OK;
     int rc = bind(mb.ctx);
@@ -101,7 +324,17 @@ int check_devices(crdt_comm *c) {
     return CRDT_OK;
 }
 
-bool valid(const crdt_comm *c) { return c && !c->m.empty(); }
+// Copy n words of member 0's device buffer to the host (synchronises member 0).
+int read_member0(crdt_comm *c, const uint64_t *src, uint64_t *dst, size_t n) {
+    auto &mb = c->m[0];
+    int rc = bind(mb.ctx);
+    if (rc || n == 0) return rc;
+    hipError_t e = hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+    return e == hipSuccess ? CRDT_OK : hip_fail(mb.ctx, e);
+}
+
+bool valid(const crdt_comm *c) { return c && !c->m.empty() && c->x; }
 
 // out[i] = key[i * n / per], i < per (evenly spaced sample of a sorted key array).
 __global__ void k_sample_keys(const uint64_t *__restrict__ key, size_t n, unsigned per, uint64_t *__restrict__ out) {
@@ -112,10 +345,30 @@ __global__ void k_sample_keys(const uint64_t *__restrict__ key, size_t n, unsign
 constexpr unsigned kSamplesPerSide = 256;
 constexpr uint64_t kKeyEnd = ~0ULL;       // splitter sentinel: "to the end of the key space"
 
-template <class T> ncclDataType_t nccl_type();
-template <> ncclDataType_t nccl_type<uint64_t>() { return ncclUint64; }
-template <> ncclDataType_t nccl_type<uint32_t>() { return ncclUint32; }
-template <> ncclDataType_t nccl_type<uint8_t>() { return ncclUint8; }
+int comm_new(int n, crdt_comm **out) {
+    crdt_comm *c = new (std::nothrow) crdt_comm();
+    if (!c) return CRDT_E_NOMEM;
+    c->nranks = n;
+    c->m.resize(n);
+    *out = c;
+    return CRDT_OK;
+}
+
+// member i: a context on its own library-owned stream
+int member_own_ctx(crdt_comm::Member &mb, int device) {
+    void *s = nullptr;
+    int rc = crdt_stream_create(device, &s);
+    if (rc) return rc;
+    rc = crdt_ctx_create(device, s, &mb.ctx);
+    if (rc) {
+        (void)crdt_stream_destroy(s);
+        return rc;
+    }
+    mb.ctx->own_stream = true;                          // destroyed with the context
+    mb.own_ctx = true;
+    mb.device = device;
+    return CRDT_OK;
+}
 
 }  // namespace
 }  // namespace crdt
@@ -135,26 +388,15 @@ extern "C" int crdt_shard_comm_create(const int *devices, int n, crdt_comm **out
     if (!out) return CRDT_E_INVAL;
     *out = nullptr;
     if (!devices || n <= 0) return CRDT_E_INVAL;
-    crdt_comm *c = new (std::nothrow) crdt_comm();
-    if (!c) return CRDT_E_NOMEM;
-    c->nranks = n;
-    c->m.resize(n);
-    int rc = CRDT_OK;
+    crdt_comm *c = nullptr;
+    int rc = comm_new(n, &c);
+    if (rc) return rc;
+    c->x = new (std::nothrow) RcclTransport();
+    if (!c->x) rc = CRDT_E_NOMEM;
     for (int i = 0; i < n && rc == CRDT_OK; ++i) {
         for (int j = 0; j < i; ++j)
-            if (devices[j] == devices[i]) rc = CRDT_E_INVAL;      // RCCL: one rank per GPU
-        if (rc) break;
-        void *s = nullptr;
-        rc = crdt_stream_create(devices[i], &s);
-        if (rc) break;
-        rc = crdt_ctx_create(devices[i], s, &c->m[i].ctx);
-        if (rc) {
-            (void)crdt_stream_destroy(s);
-            break;
-        }
-        c->m[i].ctx->own_stream = true;                        // destroyed with the context
-        c->m[i].own_ctx = true;
-        c->m[i].device = devices[i];
+            if (devices[j] == devices[i]) rc = CRDT_E_INVAL;      // RCCL: one rank per GPU (loopback: one GPU)
+        if (!rc) rc = member_own_ctx(c->m[i], devices[i]);
     }
     if (rc == CRDT_OK) {
         std::vector<ncclComm_t> comms(n);
@@ -171,19 +413,44 @@ extern "C" int crdt_shard_comm_create(const int *devices, int n, crdt_comm **out
     return CRDT_OK;
 }
 
+extern "C" int crdt_shard_comm_create_loopback(int device, int members, crdt_comm **out) {
+    if (!out) return CRDT_E_INVAL;
+    *out = nullptr;
+    if (members <= 0 || members > kLoopMax) return CRDT_E_INVAL;
+    crdt_comm *c = nullptr;
+    int rc = comm_new(members, &c);
+    if (rc) return rc;
+    c->kind = CRDT_SHARD_LOOPBACK;
+    LoopTransport *lt = new (std::nothrow) LoopTransport();
+    c->x = lt;
+    rc = lt ? lt->init(device, (size_t)members) : CRDT_E_NOMEM;
+    for (int i = 0; i < members && rc == CRDT_OK; ++i) rc = member_own_ctx(c->m[i], device);
+    if (rc) {
+        (void)crdt_shard_comm_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return CRDT_OK;
+}
+
 extern "C" int crdt_shard_comm_init_rank(crdt_ctx *ctx, const void *id, int nranks, int rank, crdt_comm **out) {
     if (!out) return CRDT_E_INVAL;
     *out = nullptr;
     if (!ctx || !id || nranks <= 0 || rank < 0 || rank >= nranks) return CRDT_E_INVAL;
     int rc = bind(ctx);
     if (rc) return rc;
-    crdt_comm *c = new (std::nothrow) crdt_comm();
-    if (!c) return CRDT_E_NOMEM;
+    crdt_comm *c = nullptr;
+    rc = comm_new(1, &c);
+    if (rc) return rc;
     c->nranks = nranks;
     c->rank0 = rank;
-    c->m.resize(1);
     c->m[0].device = ctx->device;
     c->m[0].ctx = ctx;                      // borrowed: the caller's context and stream
+    c->x = new (std::nothrow) RcclTransport();
+    if (!c->x) {
+        (void)crdt_shard_comm_destroy(c);
+        return CRDT_E_NOMEM;
+    }
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
     ncclResult_t r = ncclCommInitRank(&c->m[0].nccl, nranks, u, rank);
@@ -204,6 +471,9 @@ extern "C" int crdt_shard_comm_destroy(crdt_comm *c) {
             (void)bind(mb.ctx);
             (void)hipStreamSynchronize(mb.ctx->stream);
         }
+    }
+    delete c->x;                            // (loopback: drains its stream)
+    for (auto &mb : c->m) {
         if (mb.nccl) (void)ncclCommDestroy(mb.nccl);
         if (mb.scratch) (void)hipFree(mb.scratch);
         if (mb.own_ctx && mb.ctx) (void)crdt_ctx_destroy(mb.ctx);
@@ -217,6 +487,12 @@ extern "C" int crdt_shard_comm_info(const crdt_comm *c, int *members, int *nrank
     *members = (int)c->m.size();
     *nranks = c->nranks;
     *rank0 = c->rank0;
+    return CRDT_OK;
+}
+
+extern "C" int crdt_shard_comm_transport(const crdt_comm *c, int *kind) {
+    if (!valid(c) || !kind) return CRDT_E_INVAL;
+    *kind = c->kind;
     return CRDT_OK;
 }
 
@@ -234,47 +510,35 @@ extern "C" int crdt_shard_sync(crdt_comm *c) {
 }
 
 // buf[i] (member i, n uint64 on its device) := elementwise unsigned max over
-// every rank's buf: ncclAllReduce(ncclUint64, ncclMax), in place.
+// every rank's buf (RCCL: ncclAllReduce(ncclUint64, ncclMax)), in place.
 extern "C" int crdt_shard_allreduce_max_u64(crdt_comm *c, uint64_t *const *buf, size_t n) {
     if (!valid(c) || !buf) return CRDT_E_INVAL;
     if (n == 0) return CRDT_OK;
     for (size_t i = 0; i < c->m.size(); ++i)
         if (!buf[i]) return CRDT_E_INVAL;
-    ncclResult_t r = ncclGroupStart();
-    for (size_t i = 0; i < c->m.size() && r == ncclSuccess; ++i)
-        r = ncclAllReduce(buf[i], buf[i], n, ncclUint64, ncclMax, c->m[i].nccl, c->m[i].ctx->stream);
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
-    return CRDT_OK;
+    return c->x->allreduce(c, (void *const *)buf, n, XType::U64, XOp::Max);
 }
 
 extern "C" int crdt_shard_allreduce(crdt_comm *c, void *const *buf, size_t n, int type, int op) {
     if (!valid(c) || !buf) return CRDT_E_INVAL;
-    ncclDataType_t t;
+    XType t;
     switch (type) {
-        case CRDT_SHARD_I64: t = ncclInt64; break;
-        case CRDT_SHARD_U64: t = ncclUint64; break;
-        case CRDT_SHARD_U32: t = ncclUint32; break;
-        case CRDT_SHARD_I32: t = ncclInt32; break;
+        case CRDT_SHARD_I64: t = XType::I64; break;
+        case CRDT_SHARD_U64: t = XType::U64; break;
+        case CRDT_SHARD_U32: t = XType::U32; break;
+        case CRDT_SHARD_I32: t = XType::I32; break;
         default: return CRDT_E_INVAL;
     }
-    ncclRedOp_t o;
+    XOp o;
     switch (op) {
-        case CRDT_SHARD_SUM: o = ncclSum; break;
-        case CRDT_SHARD_MAX: o = ncclMax; break;
+        case CRDT_SHARD_SUM: o = XOp::Sum; break;
+        case CRDT_SHARD_MAX: o = XOp::Max; break;
         default: return CRDT_E_INVAL;
     }
     if (n == 0) return CRDT_OK;
     for (size_t i = 0; i < c->m.size(); ++i)
         if (!buf[i]) return CRDT_E_INVAL;
-    ncclResult_t r = ncclGroupStart();
-    for (size_t i = 0; i < c->m.size() && r == ncclSuccess; ++i)
-        r = ncclAllReduce(buf[i], buf[i], n, t, o, c->m[i].nccl, c->m[i].ctx->stream);
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
-    return CRDT_OK;
+    return c->x->allreduce(c, buf, n, t, o);
 }
 
 // Whole-population G-Counter / vector-clock join (config E1): member i folds
@@ -290,18 +554,65 @@ extern "C" int crdt_shard_fold_max_u64(crdt_comm *c, const uint64_t *const *shar
     return crdt_shard_allreduce_max_u64(c, out, nodes);
 }
 
+namespace {
+
+// The scratch head every keyed-set protocol keeps: word 0 = the member's own
+// tuple count (device), words 1 .. R = every rank's (all-gathered).
+size_t head_bytes(size_t R) { return Carve::round((R + 2) * 8); }
+
+// Keyed-set all-gather-v from the counts in every member's scratch word 0:
+// one all-gather of the counts, one read-back (member 0), then every field of
+// every rank's tuples in ONE point-to-point group (send to every rank, receive
+// from every rank at its offset) -- not one broadcast per root and field.
+int allgather_v_head(crdt_comm *c, const crdt_tuples *local, const crdt_tuples *out, size_t cap, size_t *n_total) {
+    const size_t M = c->m.size(), R = (size_t)c->nranks;
+    std::vector<const void *> snd(M);
+    std::vector<void *> rcv(M);
+    for (size_t i = 0; i < M; ++i) {
+        snd[i] = c->m[i].scratch;
+        rcv[i] = (uint64_t *)c->m[i].scratch + 1;
+    }
+    int rc = c->x->allgather(c, snd.data(), rcv.data(), 8);
+    if (rc) return rc;
+    std::vector<uint64_t> cnt(R), off(R + 1, 0);
+    rc = read_member0(c, (const uint64_t *)c->m[0].scratch + 1, cnt.data(), R);
+    if (rc) return rc;
+    for (size_t q = 0; q < R; ++q) off[q + 1] = off[q] + cnt[q];
+    *n_total = off[R];
+    if (off[R] > cap) return CRDT_E_RANGE;
+    for (size_t i = 0; i < M; ++i) {
+        const size_t g = (size_t)c->rank0 + i;
+        if (off[R] && (!out[i].key || !out[i].ts || !out[i].rep || !out[i].tomb)) return CRDT_E_INVAL;
+        if (cnt[g] && (!local[i].key || !local[i].ts || !local[i].rep || !local[i].tomb)) return CRDT_E_INVAL;
+    }
+    std::vector<XP2P> ops;
+    const size_t esz[4] = {8, 8, 4, 1};
+    for (size_t i = 0; i < M; ++i) {
+        const size_t g = (size_t)c->rank0 + i;
+        const void *fs[4] = {local[i].key, local[i].ts, local[i].rep, local[i].tomb};
+        char *fd[4] = {(char *)out[i].key, (char *)out[i].ts, (char *)out[i].rep, (char *)out[i].tomb};
+        for (size_t q = 0; q < R; ++q)
+            for (int f = 0; f < 4; ++f) {
+                if (cnt[g]) ops.push_back(XP2P{i, (int)q, true, fs[f], nullptr, cnt[g] * esz[f]});
+                if (cnt[q]) ops.push_back(XP2P{i, (int)q, false, nullptr, fd[f] + off[q] * esz[f], cnt[q] * esz[f]});
+            }
+    }
+    return c->x->p2p(c, ops);
+}
+
+}  // namespace
+
 // Keyed-set all-gather-v: member i contributes local[i] (n_local[i] tuples on
 // its device); every member's out[i] receives the concatenation in global
 // rank order.  *n_total (host) = the gathered length.  Synchronises once (the
-// counts travel by ncclAllGather and are read back before the broadcasts).
+// counts are all-gathered and read back before the transfers are sized).
 extern "C" int crdt_shard_set_allgather_v(crdt_comm *c, const crdt_tuples *local, const size_t *n_local,
                                           const crdt_tuples *out, size_t cap, size_t *n_total) {
     if (!valid(c) || !local || !n_local || !out || !n_total) return CRDT_E_INVAL;
     const size_t M = c->m.size(), R = (size_t)c->nranks;
-    // counts: member scratch = [my count | R gathered counts]
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
-        int rc = scratch_reserve(mb, (R + 1) * sizeof(uint64_t));
+        int rc = scratch_reserve(mb, head_bytes(R));
         if (rc) return rc;
         rc = bind(mb.ctx);
         if (rc) return rc;
@@ -310,52 +621,7 @@ extern "C" int crdt_shard_set_allgather_v(crdt_comm *c, const crdt_tuples *local
         if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);    // v is a stack value
         if (e != hipSuccess) return hip_fail(mb.ctx, e);
     }
-    ncclResult_t r = ncclGroupStart();
-    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
-        uint64_t *s = (uint64_t *)c->m[i].scratch;
-        r = ncclAllGather(s, s + 1, 1, ncclUint64, c->m[i].nccl, c->m[i].ctx->stream);
-    }
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
-    std::vector<uint64_t> cnt(R), off(R + 1, 0);
-    {
-        auto &mb = c->m[0];
-        int rc = bind(mb.ctx);
-        if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(cnt.data(), (uint64_t *)mb.scratch + 1, R * sizeof(uint64_t),
-                                      hipMemcpyDeviceToHost, mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
-    }
-    for (size_t q = 0; q < R; ++q) off[q + 1] = off[q] + cnt[q];
-    *n_total = off[R];
-    if (off[R] > cap) return CRDT_E_RANGE;
-    for (size_t i = 0; i < M; ++i) {
-        if (cnt[c->rank0 + i] != n_local[i]) return CRDT_E_COMM;
-        if (off[R] && (!out[i].key || !out[i].ts || !out[i].rep || !out[i].tomb)) return CRDT_E_INVAL;
-        if (n_local[i] && (!local[i].key || !local[i].ts || !local[i].rep || !local[i].tomb)) return CRDT_E_INVAL;
-    }
-    r = ncclGroupStart();
-    for (size_t q = 0; q < R && r == ncclSuccess; ++q) {
-        if (cnt[q] == 0) continue;
-        for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
-            const bool root = (size_t)c->rank0 + i == q;
-            const crdt_tuples &src = root ? local[i] : out[i];   // sendbuff is read on the root only
-            const crdt_tuples &dst = out[i];
-            ncclComm_t cm = c->m[i].nccl;
-            hipStream_t st = c->m[i].ctx->stream;
-            const size_t n = cnt[q], o = off[q];
-            r = ncclBroadcast(src.key, dst.key + o, n, ncclUint64, (int)q, cm, st);
-            if (r == ncclSuccess) r = ncclBroadcast(src.ts, dst.ts + o, n, ncclUint64, (int)q, cm, st);
-            if (r == ncclSuccess) r = ncclBroadcast(src.rep, dst.rep + o, n, ncclUint32, (int)q, cm, st);
-            if (r == ncclSuccess) r = ncclBroadcast(src.tomb, dst.tomb + o, n, ncclUint8, (int)q, cm, st);
-        }
-    }
-    r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
-    return CRDT_OK;
+    return allgather_v_head(c, local, out, cap, n_total);
 }
 
 namespace {
@@ -388,20 +654,16 @@ int shard_set_merge(crdt_comm *c, bool lww, const crdt_tuples *a, size_t na, con
         rc = check_launch(mb.ctx);
         if (rc) return rc;
         std::vector<uint64_t> h(pa + pb);
-        if (!h.empty()) {
-            hipError_t e = hipMemcpyAsync(h.data(), smp, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                                          mb.ctx->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-            if (e != hipSuccess) return hip_fail(mb.ctx, e);
-            std::sort(h.begin(), h.end());
+        rc = read_member0(c, smp, h.data(), h.size());
+        if (rc) return rc;
+        std::sort(h.begin(), h.end());
+        if (!h.empty())
             for (size_t q = 1; q < R; ++q) spl[q] = h[q * h.size() / R];
-        }
     }
     // 2. each member's key range [spl[g], spl[g+1]) of both inputs (lower_bound
     //    of the splitters on the member's own copy), merged on its device into
     //    its scratch
     std::vector<crdt_tuples> loc(M);
-    std::vector<size_t> nloc(M, 0);
     std::vector<uint64_t> bounds(4 * M);
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
@@ -431,13 +693,13 @@ int shard_set_merge(crdt_comm *c, bool lww, const crdt_tuples *a, size_t na, con
         auto &mb = c->m[i];
         const uint64_t *hb = &bounds[4 * i];
         const size_t ma = hb[1] - hb[0], mb_n = hb[3] - hb[2], cap_i = ma + mb_n;
-        // scratch: [count | key | ts | rep | tomb] of capacity cap_i
-        const size_t need = Carve::round(8) + Carve::round(cap_i * 8) * 2 + Carve::round(cap_i * 4) +
+        // scratch: [head (word 0: the merged count) | key | ts | rep | tomb] of capacity cap_i
+        const size_t need = head_bytes(R) + Carve::round(cap_i * 8) * 2 + Carve::round(cap_i * 4) +
                             Carve::round(cap_i) + 1024;
         int rc = scratch_reserve(mb, need);
         if (rc) return rc;
         Carve w(mb.scratch);
-        uint64_t *count = w.take<uint64_t>(1);
+        uint64_t *count = w.take<uint64_t>(R + 2);
         loc[i].key = w.take<uint64_t>(cap_i);
         loc[i].ts = w.take<uint64_t>(cap_i);
         loc[i].rep = w.take<uint32_t>(cap_i);
@@ -450,19 +712,10 @@ int shard_set_merge(crdt_comm *c, bool lww, const crdt_tuples *a, size_t na, con
                  : crdt_orset_merge(mb.ctx, &sa, ma, &sb, mb_n, &loc[i], count);
         if (rc) return rc;
     }
-    // 3. local counts (the device status read synchronises each member)
-    int rc = check_devices(c);
+    // 3. all-gather-v in rank order (the merged counts travel from the scratch heads)
+    int rc = allgather_v_head(c, loc.data(), out, cap, n_out);
     if (rc) return rc;
-    for (size_t i = 0; i < M; ++i) {
-        auto &mb = c->m[i];
-        uint64_t v = 0;
-        hipError_t e = hipMemcpyAsync(&v, mb.scratch, sizeof v, hipMemcpyDeviceToHost, mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
-        nloc[i] = v;
-    }
-    // 4. all-gather-v in rank order
-    return crdt_shard_set_allgather_v(c, loc.data(), nloc.data(), out, cap, n_out);
+    return check_devices(c);
 }
 
 }  // namespace
@@ -481,16 +734,16 @@ extern "C" int crdt_shard_orset_merge(crdt_comm *c, const crdt_tuples *a, size_t
 // (*Server).merge() (main.go:35-100) of one batch of replicas whose Diff /
 // RemoteDiff logs are split by ts range over the ranks (global rank g holds
 // the g-th range of every replica, ranks in ascending ts order).  The four
-// steps of crdt_amd/shard.py's sharded_refmerge, on the library's own RCCL
-// communicator and member streams, no host synchronisation:
-//   1. crdt_refmerge_local_maxl, ncclAllReduce(ncclInt64, ncclMax): the GLOBAL
-//      max(L) of every replica (remote ts at or above it are dropped, main.go:49);
+// steps of crdt_amd/shard.py's sharded_refmerge, on the communicator's
+// transport and member streams, no host synchronisation:
+//   1. crdt_refmerge_local_maxl, all-reduce(max, int64): the GLOBAL max(L) of
+//      every replica (remote ts at or above it are dropped, main.go:49);
 //   2. crdt_refmerge_batch_ex with that max: the member's slice of the new
 //      Diff (slices concatenate in rank order) and its unreduced accumulators;
-//   3. the key's max-ts holder across ranks: ncclMax of shard << 40 | rank
-//      (crdt_refmerge_acc_rank), ncclSum of the owner's string id, ncclSum of
-//      the wrapped sums (int64 two's complement: main.go:95) and of the
-//      parsable counts;
+//   3. the key's max-ts holder across ranks: max of shard << 40 | rank
+//      (crdt_refmerge_acc_rank), sum of the owner's string id, sum of the
+//      wrapped sums (int64 two's complement: main.go:95) and of the parsable
+//      counts;
 //   4. crdt_refmerge_finalize: CurrentState, identical on every member.
 // Integer reductions only: bit-exact with crdt_refmerge_batch of the
 // unsharded batch for any rank count.
@@ -529,18 +782,14 @@ extern "C" int crdt_shard_refmerge(crdt_comm *c, const crdt_refmerge_in *in, con
         }
         return CRDT_OK;
     };
-    auto allreduce = [&](auto ptr_of, size_t n, ncclDataType_t t, ncclRedOp_t op) -> int {
-        ncclResult_t r = ncclGroupStart();
-        for (size_t i = 0; i < M && r == ncclSuccess; ++i)
-            r = ncclAllReduce(ptr_of(i), ptr_of(i), n, t, op, c->m[i].nccl, c->m[i].ctx->stream);
-        ncclResult_t r2 = ncclGroupEnd();
-        if (r != ncclSuccess) return nccl_fail(c, r);
-        if (r2 != ncclSuccess) return nccl_fail(c, r2);
-        return CRDT_OK;
+    std::vector<void *> ptr(M);
+    auto allreduce = [&](auto ptr_of, size_t n, XType t, XOp op) -> int {
+        for (size_t i = 0; i < M; ++i) ptr[i] = ptr_of(i);
+        return c->x->allreduce(c, ptr.data(), n, t, op);
     };
     // 1. the global max(L) per replica
     int rc = each([&](size_t i, crdt_ctx *x) { return crdt_refmerge_local_maxl(x, &in[i], bf[i].maxl); });
-    if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].maxl; }, P, ncclInt64, ncclMax);
+    if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].maxl; }, P, XType::I64, XOp::Max);
     // 2. the local merges (new-Diff slices, unreduced accumulators)
     if (!rc) rc = each([&](size_t i, crdt_ctx *x) {
         return crdt_refmerge_batch_ex(x, &in[i], &out[i], bf[i].maxl, &bf[i].acc);
@@ -555,13 +804,13 @@ extern "C" int crdt_shard_refmerge(crdt_comm *c, const crdt_refmerge_in *in, con
             hipError_t e = hipMemcpyAsync(bf[i].cmax, bf[i].c, ns * 8, hipMemcpyDeviceToDevice, x->stream);
             return e == hipSuccess ? CRDT_OK : hip_fail(x, e);
         });
-        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].cmax; }, ns, ncclInt64, ncclMax);
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].cmax; }, ns, XType::I64, XOp::Max);
         if (!rc) rc = each([&](size_t i, crdt_ctx *x) {
             return crdt_refmerge_acc_owner_str(x, &bf[i].acc, ns, bf[i].c, bf[i].cmax, bf[i].v);
         });
-        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].v; }, ns, ncclInt64, ncclSum);
-        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].acc.sum; }, ns, ncclInt64, ncclSum);
-        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].acc.npar; }, ns, ncclUint32, ncclSum);
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].v; }, ns, XType::I64, XOp::Sum);
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].acc.sum; }, ns, XType::I64, XOp::Sum);
+        if (!rc) rc = allreduce([&](size_t i) { return (void *)bf[i].acc.npar; }, ns, XType::U32, XOp::Sum);
         if (!rc) rc = each([&](size_t i, crdt_ctx *x) {
             return crdt_refmerge_acc_set_best(x, &bf[i].acc, ns, bf[i].cmax, bf[i].v);
         });
@@ -577,33 +826,28 @@ extern "C" int crdt_shard_refmerge(crdt_comm *c, const crdt_refmerge_in *in, con
 // Member i sends send_counts[i * R + q] elements of elem_size bytes to global
 // rank q, from its send buffer's segments in rank order, and receives
 // recv_counts[i * R + p] elements from rank p into its recv buffer, segments
-// in rank order (grouped ncclSend / ncclRecv, enqueued on the member streams).
+// in rank order (one point-to-point group, enqueued on the member streams).
 extern "C" int crdt_shard_alltoallv(crdt_comm *c, const void *const *send, const size_t *send_counts,
                                     void *const *recv, const size_t *recv_counts, size_t elem_size) {
     if (!valid(c) || !send || !send_counts || !recv || !recv_counts || elem_size == 0) return CRDT_E_INVAL;
     const size_t M = c->m.size(), R = (size_t)c->nranks;
+    std::vector<XP2P> ops;
     for (size_t i = 0; i < M; ++i) {
         size_t ns = 0, nr = 0;
         for (size_t q = 0; q < R; ++q) ns += send_counts[i * R + q], nr += recv_counts[i * R + q];
         if ((ns && !send[i]) || (nr && !recv[i])) return CRDT_E_INVAL;
-    }
-    ncclResult_t r = ncclGroupStart();
-    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
         const char *sb = (const char *)send[i];
         char *rb = (char *)recv[i];
         size_t so = 0, ro = 0;
-        for (size_t q = 0; q < R && r == ncclSuccess; ++q) {
+        for (size_t q = 0; q < R; ++q) {
             const size_t sn = send_counts[i * R + q] * elem_size, rn = recv_counts[i * R + q] * elem_size;
-            if (sn) r = ncclSend(sb + so, sn, ncclUint8, (int)q, c->m[i].nccl, c->m[i].ctx->stream);
-            if (r == ncclSuccess && rn) r = ncclRecv(rb + ro, rn, ncclUint8, (int)q, c->m[i].nccl, c->m[i].ctx->stream);
+            if (sn) ops.push_back(XP2P{i, (int)q, true, sb + so, nullptr, sn});
+            if (rn) ops.push_back(XP2P{i, (int)q, false, nullptr, rb + ro, rn});
             so += sn;
             ro += rn;
         }
     }
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
-    return CRDT_OK;
+    return c->x->p2p(c, ops);
 }
 
 namespace {
@@ -651,292 +895,243 @@ __global__ void k_sample_block(const uint64_t *__restrict__ ka, size_t na, const
     }
 }
 
-struct Run {
-    int arena;           // 0 / 1
-    size_t off, n;
-};
+// A member's row of the count matrix from the lower bounds of the R - 1
+// inner splitters in its sorted keys: out = [A tuples to rank 0 .. R-1 | B
+// tuples to rank 0 .. R-1] (cut q of a side = lb[q-1]; cut 0 = 0, cut R = n).
+__global__ void k_cut_counts(const uint64_t *__restrict__ lb, unsigned R, size_t na, size_t nb,
+                             uint64_t *__restrict__ out) {
+    const unsigned q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= R) return;
+    const uint64_t *la = lb, *lbb = lb + (R - 1);
+    const uint64_t a0 = q ? la[q - 1] : 0, a1 = q + 1 < R ? la[q] : na;
+    const uint64_t b0 = q ? lbb[q - 1] : 0, b1 = q + 1 < R ? lbb[q] : nb;
+    out[q] = a1 - a0;
+    out[R + q] = b1 - b0;
+}
 
 int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
-                          const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out, int gather) {
-    if (!valid(c) || !a || !na || !b || !nb || !out || !n_out) return CRDT_E_INVAL;
+                          const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out,
+                          uint64_t *const *n_dev, int gather) {
+    if (!valid(c) || !a || !na || !b || !nb || !out || (!n_out && !n_dev)) return CRDT_E_INVAL;
+    if (n_dev && gather) return CRDT_E_INVAL;
     const size_t M = c->m.size(), R = (size_t)c->nranks, S = kSamplesPerSide;
-    for (size_t i = 0; i < M; ++i)
+    for (size_t i = 0; i < M; ++i) {
         if ((na[i] && !a[i].key) || (nb[i] && !b[i].key)) return CRDT_E_INVAL;
+        if (n_dev && !n_dev[i]) return CRDT_E_INVAL;
+    }
+    auto set_merge = [&](crdt_ctx *x, const crdt_tuples &A, size_t n_a, const crdt_tuples &B, size_t n_b,
+                         const crdt_tuples &O, uint64_t *count) {
+        return lww ? crdt_lww_merge(x, &A, n_a, &B, n_b, const_cast<crdt_tuples *>(&O), count)
+                   : crdt_orset_merge(x, &A, n_a, &B, n_b, const_cast<crdt_tuples *>(&O), count);
+    };
     if (R == 1 && !g_shard_exchange_always && cap >= na[0] + nb[0]) {   // one rank owns every key: no exchange
         auto &mb = c->m[0];
-        int rc = scratch_reserve(mb, 64);
+        int rc = scratch_reserve(mb, head_bytes(R));
         if (rc) return rc;
-        uint64_t *count = (uint64_t *)mb.scratch;
-        rc = lww ? crdt_lww_merge(mb.ctx, &a[0], na[0], &b[0], nb[0], const_cast<crdt_tuples *>(&out[0]), count)
-                 : crdt_orset_merge(mb.ctx, &a[0], na[0], &b[0], nb[0], const_cast<crdt_tuples *>(&out[0]), count);
-        if (rc) return rc;
+        uint64_t *count = n_dev ? n_dev[0] : (uint64_t *)mb.scratch;
+        rc = set_merge(mb.ctx, a[0], na[0], b[0], nb[0], out[0], count);
+        if (rc || n_dev) return rc;                      // (counts stay on the device: no synchronisation)
         uint64_t h = 0;
-        hipError_t e = hipMemcpyAsync(&h, count, 8, hipMemcpyDeviceToHost, mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        rc = read_member0(c, count, &h, 1);
+        if (rc) return rc;
         n_out[0] = h;
         return check_devices(c);
     }
-    // scratch layout: [ctrl: samples R x (2 + 2S) | counts 2R x R | bounds] then two tuple arenas
+    // control block after the head: [samples R x blk | count matrix R x 2R | probes R | bounds 2R]
     const size_t blk = 2 + 2 * S;
-    const size_t ctrl = Carve::round((R + 2) * 8) + Carve::round(R * blk * 8) + Carve::round(2 * R * R * 8) +
-                        Carve::round(4 * (R + 1) * 8) + Carve::round(4 * R * 8 + 8) + 4096;
-    for (size_t i = 0; i < M; ++i) {
-        int rc = scratch_reserve(c->m[i], ctrl);
-        if (rc) return rc;
-    }
-    auto carve_ctrl = [&](crdt_comm::Member &mb, uint64_t **smp, uint64_t **cnt, uint64_t **bnd, uint64_t **mc) {
+    struct Ctrl {
+        uint64_t *smp, *cnt, *prb, *lb;
+    };
+    const size_t ctrl_bytes = head_bytes(R) + Carve::round(R * blk * 8) + Carve::round(2 * R * R * 8) +
+                              Carve::round(R * 8) + Carve::round(2 * R * 8) + 1024;
+    auto carve_ctrl = [&](crdt_comm::Member &mb, Ctrl *k) {
         Carve w(mb.scratch);
-        (void)w.take<uint64_t>(R + 2);                   // (crdt_shard_set_allgather_v's counts)
-        *smp = w.take<uint64_t>(R * blk);
-        *cnt = w.take<uint64_t>(2 * R * R);
-        *bnd = w.take<uint64_t>(4 * (R + 1));
-        *mc = w.take<uint64_t>(4 * R + 1);
+        (void)w.take<uint64_t>(R + 2);                   // the head
+        k->smp = w.take<uint64_t>(R * blk);
+        k->cnt = w.take<uint64_t>(2 * R * R);
+        k->prb = w.take<uint64_t>(R);
+        k->lb = w.take<uint64_t>(2 * R);
         return w.used;
     };
-    // 1. samples + sizes, all-gathered; every rank derives the same splitters
+    std::vector<Ctrl> ct(M);
+    for (size_t i = 0; i < M; ++i) {
+        int rc = scratch_reserve(c->m[i], ctrl_bytes);
+        if (rc) return rc;
+        carve_ctrl(c->m[i], &ct[i]);
+    }
+    // 1. samples + sizes, all-gathered; every rank derives the same splitters (read-back 1)
+    std::vector<const void *> snd(M);
+    std::vector<void *> rcv(M);
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
         int rc = bind(mb.ctx);
         if (rc) return rc;
+        uint64_t *mine = ct[i].smp + (c->rank0 + i) * blk;
         k_sample_block<<<(unsigned)((S + 255) / 256), 256, 0, mb.ctx->stream>>>(a[i].key, na[i], b[i].key, nb[i],
-                                                                               (unsigned)S, smp + (c->rank0 + i) * blk);
+                                                                               (unsigned)S, mine);
         rc = check_launch(mb.ctx);
         if (rc) return rc;
+        snd[i] = mine;
+        rcv[i] = ct[i].smp;
     }
-    ncclResult_t r = ncclGroupStart();
-    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
-        auto &mb = c->m[i];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        uint64_t *mine = smp + (c->rank0 + i) * blk;
-        r = ncclAllGather(mine, smp, blk, ncclUint64, mb.nccl, mb.ctx->stream);
-    }
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
+    int rc = c->x->allgather(c, snd.data(), rcv.data(), blk * 8);
+    if (rc) return rc;
     std::vector<uint64_t> h_smp(R * blk);
-    {
-        auto &mb = c->m[0];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        int rc = bind(mb.ctx);
-        if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(h_smp.data(), smp, R * blk * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
-    }
+    rc = read_member0(c, ct[0].smp, h_smp.data(), R * blk);
+    if (rc) return rc;
     const std::vector<uint64_t> spl = weighted_splitters(h_smp.data(), R, S);
-    // 2. each member's send ranges: lower_bound of the inner splitters in its keys
-    std::vector<size_t> sa(M * R), sb(M * R), ra(M * R), rb(M * R);
+    // 2. each member's cuts (device lower_bound of the inner splitters) -> its
+    //    row of the count matrix on the device; the matrix all-gathered (read-back 2)
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        int rc = bind(mb.ctx);
+        rc = bind(mb.ctx);
         if (rc) return rc;
-        std::vector<uint64_t> hb(2 * (R + 1), 0);
         if (R > 1) {
-            hipError_t e = hipMemcpyAsync(bnd, spl.data() + 1, (R - 1) * 8, hipMemcpyHostToDevice, mb.ctx->stream);
+            hipError_t e = hipMemcpyAsync(ct[i].prb, spl.data() + 1, (R - 1) * 8, hipMemcpyHostToDevice,
+                                          mb.ctx->stream);
             if (e != hipSuccess) return hip_fail(mb.ctx, e);
-            if (na[i]) rc = crdt_u64_lower_bound(mb.ctx, a[i].key, na[i], bnd, R - 1, bnd + R);
-            if (!rc && nb[i]) rc = crdt_u64_lower_bound(mb.ctx, b[i].key, nb[i], bnd, R - 1, bnd + 2 * R);
+            rc = crdt_u64_lower_bound(mb.ctx, a[i].key, na[i], ct[i].prb, R - 1, ct[i].lb);
+            if (!rc) rc = crdt_u64_lower_bound(mb.ctx, b[i].key, nb[i], ct[i].prb, R - 1, ct[i].lb + (R - 1));
             if (rc) return rc;
-            e = hipMemcpyAsync(hb.data(), bnd + R, 2 * R * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-            if (e != hipSuccess) return hip_fail(mb.ctx, e);
         }
-        // cuts of A: 0, lb(spl[1]) .. lb(spl[R-1]), na (lower_bound of 0 is 0, of the end na)
-        std::vector<uint64_t> cutA(R + 1), cutB(R + 1);
-        cutA[0] = cutB[0] = 0;
-        for (size_t q = 1; q < R; ++q) cutA[q] = na[i] ? hb[q - 1] : 0, cutB[q] = nb[i] ? hb[R + q - 1] : 0;
-        cutA[R] = na[i];
-        cutB[R] = nb[i];
-        for (size_t q = 0; q < R; ++q) {
-            sa[i * R + q] = cutA[q + 1] - cutA[q];
-            sb[i * R + q] = cutB[q + 1] - cutB[q];
-        }
-    }
-    // 3. the count matrix, all-gathered: block p = rank p's [send A counts | send B counts]
-    for (size_t i = 0; i < M; ++i) {
-        auto &mb = c->m[i];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        int rc = bind(mb.ctx);
+        uint64_t *row = ct[i].cnt + (c->rank0 + i) * 2 * R;
+        k_cut_counts<<<(unsigned)((R + 255) / 256), 256, 0, mb.ctx->stream>>>(ct[i].lb, (unsigned)R, na[i], nb[i], row);
+        rc = check_launch(mb.ctx);
         if (rc) return rc;
-        std::vector<uint64_t> h(2 * R);
-        for (size_t q = 0; q < R; ++q) h[q] = sa[i * R + q], h[R + q] = sb[i * R + q];
-        hipError_t e = hipMemcpyAsync(cnt + (c->rank0 + i) * 2 * R, h.data(), 2 * R * 8, hipMemcpyHostToDevice,
-                                      mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);     // h is a local
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        snd[i] = row;
+        rcv[i] = ct[i].cnt;
     }
-    r = ncclGroupStart();
-    for (size_t i = 0; i < M && r == ncclSuccess; ++i) {
-        auto &mb = c->m[i];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        uint64_t *mine = cnt + (c->rank0 + i) * 2 * R;
-        r = ncclAllGather(mine, cnt, 2 * R, ncclUint64, mb.nccl, mb.ctx->stream);
-    }
-    r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(c, r);
-    if (r2 != ncclSuccess) return nccl_fail(c, r2);
+    rc = c->x->allgather(c, snd.data(), rcv.data(), 2 * R * 8);
+    if (rc) return rc;
+    std::vector<uint64_t> mat(2 * R * R);               // row p = rank p's [A counts | B counts] by destination
+    rc = read_member0(c, ct[0].cnt, mat.data(), mat.size());
+    if (rc) return rc;
     std::vector<size_t> tot_a(M, 0), tot_b(M, 0);
     for (size_t i = 0; i < M; ++i) {
-        auto &mb = c->m[i];
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        int rc = bind(mb.ctx);
-        if (rc) return rc;
-        std::vector<uint64_t> h(2 * R * R);
-        hipError_t e = hipMemcpyAsync(h.data(), cnt, 2 * R * R * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
         const size_t g = (size_t)c->rank0 + i;
-        for (size_t p = 0; p < R; ++p) {
-            ra[i * R + p] = h[p * 2 * R + g];
-            rb[i * R + p] = h[p * 2 * R + R + g];
-            tot_a[i] += ra[i * R + p];
-            tot_b[i] += rb[i * R + p];
-        }
+        size_t sa = 0, sb = 0;
+        for (size_t q = 0; q < R; ++q) sa += mat[g * 2 * R + q], sb += mat[g * 2 * R + R + q];
+        if (sa != na[i] || sb != nb[i]) return CRDT_E_COMM;    // the matrix must describe the member's own sides
+        for (size_t p = 0; p < R; ++p) tot_a[i] += mat[p * 2 * R + g], tot_b[i] += mat[p * 2 * R + R + g];
     }
-    // 4. the exchange into arena 0 (A's runs, then B's, in rank order), field by field
+    // 3. per member two tuple arenas of n = received tuples after the control
+    //    block (the scratch is re-carved: nothing in it is needed any more)
     std::vector<crdt_tuples> ar0(M), ar1(M);
+    std::vector<bool> direct(M);
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
-        const size_t n = tot_a[i] + tot_b[i] + 1;
-        const size_t need = ctrl + 2 * (Carve::round(n * 8) * 2 + Carve::round(n * 4) + Carve::round(n)) + 4096;
-        int rc = scratch_reserve(mb, need);
+        const size_t n = tot_a[i] + tot_b[i];
+        direct[i] = !gather && cap >= n;                 // the final merge writes straight into out[i]
+        if (n_dev && !direct[i]) return CRDT_E_RANGE;
+        const size_t ab = Carve::round(n * 8 + 8) * 2 + Carve::round(n * 4 + 4) + Carve::round(n + 1);
+        rc = scratch_reserve(mb, ctrl_bytes + 2 * ab + 2048);
         if (rc) return rc;
-        uint64_t *smp, *cnt, *bnd, *mc;
         Carve w(mb.scratch);
-        w.used = carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
+        w.used = carve_ctrl(mb, &ct[i]);
         for (crdt_tuples *t : {&ar0[i], &ar1[i]}) {
-            t->key = w.take<uint64_t>(n);
-            t->ts = w.take<uint64_t>(n);
-            t->rep = w.take<uint32_t>(n);
-            t->tomb = w.take<uint8_t>(n);
+            t->key = w.take<uint64_t>(n + 1);
+            t->ts = w.take<uint64_t>(n + 1);
+            t->rep = w.take<uint32_t>(n + 1);
+            t->tomb = w.take<uint8_t>(n + 1);
         }
     }
+    // 4. the exchange: every field of both sides to its key-range owner, ONE
+    //    point-to-point group; arena 0 receives A's runs then B's, rank order
     {
-        std::vector<const void *> snd(M);
-        std::vector<void *> rcv(M);
+        std::vector<XP2P> ops;
         const size_t esz[4] = {8, 8, 4, 1};
-        for (int side = 0; side < 2; ++side)
-            for (int f = 0; f < 4; ++f) {
-                for (size_t i = 0; i < M; ++i) {
+        for (size_t i = 0; i < M; ++i) {
+            const size_t g = (size_t)c->rank0 + i;
+            size_t so[2] = {0, 0}, ro[2] = {0, tot_a[i]};
+            for (size_t q = 0; q < R; ++q)
+                for (int side = 0; side < 2; ++side) {
                     const crdt_tuples &src = side ? b[i] : a[i];
-                    const void *fs[4] = {src.key, src.ts, src.rep, src.tomb};
-                    void *fd[4] = {ar0[i].key, ar0[i].ts, ar0[i].rep, ar0[i].tomb};
-                    snd[i] = fs[f];
-                    rcv[i] = (char *)fd[f] + (side ? tot_a[i] * esz[f] : 0);
+                    const char *fs[4] = {(const char *)src.key, (const char *)src.ts, (const char *)src.rep,
+                                         (const char *)src.tomb};
+                    char *fd[4] = {(char *)ar0[i].key, (char *)ar0[i].ts, (char *)ar0[i].rep, (char *)ar0[i].tomb};
+                    const size_t sn = mat[g * 2 * R + side * R + q], rn = mat[q * 2 * R + side * R + g];
+                    for (int f = 0; f < 4; ++f) {
+                        if (sn) ops.push_back(XP2P{i, (int)q, true, fs[f] + so[side] * esz[f], nullptr, sn * esz[f]});
+                        if (rn) ops.push_back(XP2P{i, (int)q, false, nullptr, fd[f] + ro[side] * esz[f], rn * esz[f]});
+                    }
+                    so[side] += sn;
+                    ro[side] += rn;
                 }
-                int rc = crdt_shard_alltoallv(c, snd.data(), side ? sb.data() : sa.data(), rcv.data(),
-                                              side ? rb.data() : ra.data(), esz[f]);
-                if (rc) return rc;
-            }
+        }
+        rc = c->x->p2p(c, ops);
+        if (rc) return rc;
     }
-    // 5. per member, a tree of merges over the received runs: A's runs in
-    //    rank order pairwise (lower rank left: the stable rank-order merge),
-    //    B's likewise, then merge(A, B); levels alternate between the arenas
-    std::vector<size_t> final_n(M, 0);
+    // 5. per member: each side's R runs merged stably in rank order (lower rank
+    //    left) by a tree of crdt_tuples_merge levels -- every length known on
+    //    the host, so no read-back -- then ONE set merge of the two sides.
+    //    Both sides have R runs, so they finish in the same arena.
     std::vector<crdt_tuples> fin(M);
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
-        int rc = bind(mb.ctx);
+        rc = bind(mb.ctx);
         if (rc) return rc;
-        uint64_t *smp, *cnt, *bnd, *mc;
-        carve_ctrl(mb, &smp, &cnt, &bnd, &mc);
-        std::vector<Run> ruA, ruB;
+        struct Run {
+            size_t off, n;
+        };
+        std::vector<Run> ru[2];
         size_t o = 0;
-        for (size_t p = 0; p < R; ++p) ruA.push_back(Run{0, o, ra[i * R + p]}), o += ra[i * R + p];
-        for (size_t p = 0; p < R; ++p) ruB.push_back(Run{0, o, rb[i * R + p]}), o += rb[i * R + p];
-        auto view = [&](const Run &x) {
-            const crdt_tuples &ar = x.arena ? ar1[i] : ar0[i];
-            return crdt_tuples{ar.key + x.off, ar.ts + x.off, ar.rep + x.off, ar.tomb + x.off};
+        for (int side = 0; side < 2; ++side)
+            for (size_t p = 0; p < R; ++p) {
+                const size_t n = mat[p * 2 * R + side * R + (size_t)c->rank0 + i];
+                ru[side].push_back(Run{o, n});
+                o += n;
+            }
+        auto view = [&](int arena, size_t off) {
+            const crdt_tuples &t = arena ? ar1[i] : ar0[i];
+            return crdt_tuples{t.key + off, t.ts + off, t.rep + off, t.tomb + off};
         };
-        auto merge = [&](const Run &x, const Run &y, int dst, uint64_t *count) -> int {
-            crdt_tuples tx = view(x), ty = view(y);
-            const crdt_tuples &ad = dst ? ar1[i] : ar0[i];
-            crdt_tuples to{ad.key + x.off, ad.ts + x.off, ad.rep + x.off, ad.tomb + x.off};   // (x, y adjacent)
-            return lww ? crdt_lww_merge(mb.ctx, &tx, x.n, &ty, y.n, &to, count)
-                       : crdt_orset_merge(mb.ctx, &tx, x.n, &ty, y.n, &to, count);
-        };
-        int level_arena = 0;
-        bool final_done = false;
-        while (!final_done) {
-            // one level: pairs of A runs, pairs of B runs; the last level merges A with B
-            std::vector<std::pair<Run, Run>> jobs;
-            std::vector<int> job_side;
-            const bool last = ruA.size() == 1 && ruB.size() == 1;
-            if (last) {
-                jobs.emplace_back(ruA[0], ruB[0]);
-                job_side.push_back(2);
-            } else {
-                for (int side = 0; side < 2; ++side) {
-                    auto &ru = side ? ruB : ruA;
-                    for (size_t k = 0; k < ru.size(); k += 2) {
-                        Run y = k + 1 < ru.size() ? ru[k + 1] : Run{ru[k].arena, ru[k].off + ru[k].n, 0};
-                        jobs.emplace_back(ru[k], y);
-                        job_side.push_back(side);
-                    }
+        int cur = 0;
+        while (ru[0].size() > 1) {
+            for (int side = 0; side < 2; ++side) {
+                std::vector<Run> nx;
+                for (size_t k = 0; k < ru[side].size(); k += 2) {
+                    const Run x = ru[side][k], y = k + 1 < ru[side].size() ? ru[side][k + 1] : Run{x.off + x.n, 0};
+                    rc = tuples_merge_stable(mb.ctx, view(cur, x.off), x.n, view(cur, y.off), y.n, view(1 - cur, x.off));
+                    if (rc) return rc;
+                    nx.push_back(Run{x.off, x.n + y.n});
                 }
+                ru[side].swap(nx);
             }
-            const int dst = 1 - level_arena;
-            for (size_t j = 0; j < jobs.size(); ++j) {
-                rc = merge(jobs[j].first, jobs[j].second, dst, mc + j);
-                if (rc) return rc;
-            }
-            std::vector<uint64_t> hn(jobs.size());
-            hipError_t e = hipMemcpyAsync(hn.data(), mc, jobs.size() * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-            if (e != hipSuccess) return hip_fail(mb.ctx, e);
-            std::vector<Run> na_, nb_;
-            for (size_t j = 0; j < jobs.size(); ++j) {
-                const Run nr{dst, jobs[j].first.off, hn[j]};
-                if (job_side[j] == 2) {
-                    fin[i] = view(nr);
-                    final_n[i] = hn[j];
-                    final_done = true;
-                } else {
-                    (job_side[j] ? nb_ : na_).push_back(nr);
-                }
-            }
-            if (!final_done) {
-                ruA.swap(na_);
-                ruB.swap(nb_);
-            }
-            level_arena = dst;
+            cur = 1 - cur;
         }
+        uint64_t *count = n_dev ? n_dev[i] : (uint64_t *)mb.scratch;   // (the head's word 0)
+        fin[i] = direct[i] ? out[i] : view(1 - cur, 0);
+        crdt_tuples A = view(cur, 0), B = view(cur, tot_a[i]);
+        rc = set_merge(mb.ctx, A, tot_a[i], B, tot_b[i], fin[i], count);
+        if (rc) return rc;
     }
-    int rc = check_devices(c);
-    if (rc) return rc;
+    if (n_dev) return CRDT_OK;                           // enqueued; counts on the device
     // 6. the whole merged state on every member, or each member's own range
     if (gather) {
         size_t tot = 0;
-        rc = crdt_shard_set_allgather_v(c, fin.data(), final_n.data(), out, cap, &tot);
+        rc = allgather_v_head(c, fin.data(), out, cap, &tot);
         if (rc) return rc;
         for (size_t i = 0; i < M; ++i) n_out[i] = tot;
-        return CRDT_OK;
+        return check_devices(c);
     }
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
-        n_out[i] = final_n[i];
-        if (final_n[i] > cap) return CRDT_E_RANGE;
-        if (!final_n[i]) continue;
         rc = bind(mb.ctx);
         if (rc) return rc;
-        const size_t n = final_n[i];
-        hipError_t e = hipMemcpyAsync(out[i].key, fin[i].key, n * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(out[i].ts, fin[i].ts, n * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(out[i].rep, fin[i].rep, n * 4, hipMemcpyDeviceToDevice, mb.ctx->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(out[i].tomb, fin[i].tomb, n, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        uint64_t h = 0;
+        hipError_t e = hipMemcpyAsync(&h, mb.scratch, 8, hipMemcpyDeviceToHost, mb.ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
+        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        n_out[i] = h;
+        if (direct[i] || !h) continue;
+        if (h > cap) return CRDT_E_RANGE;
+        e = hipMemcpyAsync(out[i].key, fin[i].key, h * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out[i].ts, fin[i].ts, h * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out[i].rep, fin[i].rep, h * 4, hipMemcpyDeviceToDevice, mb.ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(out[i].tomb, fin[i].tomb, h, hipMemcpyDeviceToDevice, mb.ctx->stream);
         if (e != hipSuccess) return hip_fail(mb.ctx, e);
     }
-    return CRDT_OK;
+    return check_devices(c);
 }
 
 }  // namespace
@@ -946,19 +1141,37 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
 // (key, ts, rep).  The population's A is the stable merge of every rank's A
 // in rank order (likewise B); the result is crdt_lww_merge / crdt_orset_merge
 // of those -- computed by key-range owners: weighted sample splitters (one
-// all-gather), every rank's tuples sent to their owner (all-to-all-v), the
-// owner merges the received runs (rank-order pairwise merges, then A with
-// B).  gather != 0: every member's out[i] receives the whole merged state and
-// n_out[i] its length; gather == 0: out[i] / n_out[i] = the member's own key
-// range of it (ranges ascend with rank).  Synchronises.
+// all-gather), the count matrix (one all-gather), every rank's tuples sent to
+// their owner (one point-to-point group), the owner's rank-order stable
+// merges of the received runs and one set merge.  gather != 0: every
+// member's out[i] receives the whole merged state and n_out[i] its length;
+// gather == 0: out[i] / n_out[i] = the member's own key range of it (ranges
+// ascend with rank).  Synchronises.
 extern "C" int crdt_shard_lww_merge_local(crdt_comm *c, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
                                           const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out,
                                           int gather) {
-    return shard_set_merge_local(c, true, a, na, b, nb, out, cap, n_out, gather);
+    return shard_set_merge_local(c, true, a, na, b, nb, out, cap, n_out, nullptr, gather);
 }
 
 extern "C" int crdt_shard_orset_merge_local(crdt_comm *c, const crdt_tuples *a, const size_t *na,
                                             const crdt_tuples *b, const size_t *nb, const crdt_tuples *out,
                                             size_t cap, size_t *n_out, int gather) {
-    return shard_set_merge_local(c, false, a, na, b, nb, out, cap, n_out, gather);
+    return shard_set_merge_local(c, false, a, na, b, nb, out, cap, n_out, nullptr, gather);
+}
+
+// The same without the trailing synchronisation: each member's own key range
+// (gather == 0) into out[i], its length written to n_out_dev[i] (a device
+// word on the member's GPU) on the member stream.  Planning still reads back
+// the samples and the count matrix when nranks > 1; with one rank nothing is
+// read back.  CRDT_E_RANGE if cap is below the member's received tuples.
+extern "C" int crdt_shard_lww_merge_local_dev(crdt_comm *c, const crdt_tuples *a, const size_t *na,
+                                              const crdt_tuples *b, const size_t *nb, const crdt_tuples *out,
+                                              size_t cap, uint64_t *const *n_out_dev) {
+    return shard_set_merge_local(c, true, a, na, b, nb, out, cap, nullptr, n_out_dev, 0);
+}
+
+extern "C" int crdt_shard_orset_merge_local_dev(crdt_comm *c, const crdt_tuples *a, const size_t *na,
+                                                const crdt_tuples *b, const size_t *nb, const crdt_tuples *out,
+                                                size_t cap, uint64_t *const *n_out_dev) {
+    return shard_set_merge_local(c, false, a, na, b, nb, out, cap, nullptr, n_out_dev, 0);
 }

@@ -278,6 +278,18 @@ class Engine:
                    probes.numel(), out.data_ptr())
         return out
 
+    def tuples_merge(self, a: TupleSet, b: TupleSet, out: TupleSet | None = None) -> TupleSet:
+        """Stable merge of two sorted tuple arrays, every tuple kept (a's
+        copies first on an equal tag): crdt_tuples_merge."""
+        out = TupleSet.empty(max(len(a) + len(b), 1), self.device) if out is None else out
+        for s in (a, b, out):
+            self._check(s.key, s.ts, itemsize=8)
+            self._check(s.rep, itemsize=4)
+            self._check(s.tomb, itemsize=1)
+        ca, cb, co = a.c(), b.c(), out.c()
+        self._call("crdt_tuples_merge", C.byref(ca), len(a), C.byref(cb), len(b), C.byref(co))
+        return out.slice(len(a) + len(b))
+
     def count_unsorted(self, t: TupleSet) -> int:
         bad = torch.empty(1, dtype=torch.int64, device=self.device)
         ct = t.c()

@@ -80,7 +80,8 @@ class Population:
         l_kv = np.asarray(host["l_kv"], dtype=np.int64)
         self._cnt = np.diff(l_off)
         self._kvcnt = np.diff(l_kv[l_off])
-        if len(l_kv) and l_kv[0] != 0:                     # the fast path assumes kv ranges from 0
+        # the fast path rebuilds entry / kv offsets as cumulative sums from 0
+        if (len(l_off) and l_off[0] != 0) or (len(l_kv) and len(l_off) and l_kv[l_off[0]] != 0):
             self._cnt = self._kvcnt = None
         self._pin = None                                   # pinned staging of a round's per-replica arrays
         # kv arena of the next round: the current Diff's kv pairs are its
@@ -457,11 +458,14 @@ class Population:
                 "kv_off": t(host_cmds["kv_off"], np.int64),
                 "kv_key": t(np.asarray(host_cmds["kv_key"]).astype(np.uint32).view(np.int32), np.int32),
                 "kv_val": t(np.asarray(host_cmds["kv_val"]).astype(np.uint32).view(np.int32), np.int32)}
-        if self.state is None:
-            self.state = self.empty_state()
-        out = self.eng.local_apply({"off": self.off, "ts": self.ts, "origin": self.origin}, cmds, self.state,
+        # the apply updates CurrentState in place: run it on a copy and commit
+        # the copy only after the device status is clean, so a raised flag
+        # leaves CurrentState and the Diffs of the population consistent
+        state = {k: v.clone() for k, v in (self.state or self.empty_state()).items()}
+        out = self.eng.local_apply({"off": self.off, "ts": self.ts, "origin": self.origin}, cmds, state,
                                    self.str_bytes, self.str_off, self.P * self.K)
         self.eng.check_device()        # CRDT_DEV_RANGE: nothing of an over-limit replica was applied
+        self.state = state
         n_out = int(out["off"][-1].item())
         src = out["src"][:n_out].contiguous()
         new_kv = torch.empty(n_out + 1, dtype=torch.int64, device=dev)
@@ -566,9 +570,10 @@ def sharded_round(pop: Population, peers_all: np.ndarray, group=None, comm=None)
     # per-destination entry / pair counts, all-gathered (replica counts follow from the plan)
     se = np.diff(eb).tolist()
     sk = np.diff(kb).tolist()
-    mat = [torch.zeros(2 * world, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(mat, torch.tensor(se + sk, dtype=torch.int64), group=group)
-    mat = torch.stack(mat).numpy()
+    # (device tensors: the collective runs on NCCL / RCCL as well as gloo)
+    mat = [torch.zeros(2 * world, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(mat, torch.tensor(se + sk, dtype=torch.int64, device=dev), group=group)
+    mat = torch.stack(mat).cpu().numpy()
     r_rep = [int(((need[rank] >= firsts[p]) & (need[rank] < firsts[p + 1])).sum()) for p in range(world)]
     r_e, r_k = mat[:, rank].tolist(), mat[:, world + rank].tolist()
 

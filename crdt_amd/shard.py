@@ -340,8 +340,10 @@ class Comm:
     * ``Comm.init_rank(eng, group)``: one member per process (one process per
       GPU, as torchrun launches the bench); rank 0's RCCL unique id travels
       over the torch.distributed group once, after that every data-path
-      collective is the library's own ncclAllReduce / ncclBroadcast on the
-      engine's stream.
+      collective is the library's own ncclAllReduce / ncclAllGather /
+      grouped ncclSend-ncclRecv on the engine's stream.
+    * ``Comm.loopback(device, members)``: ``members`` ranks on one GPU (the
+      loopback transport), for the multi-rank protocols on a one-GPU box.
 
     uint64 state travels as ncclUint64 with ncclMax: RCCL's unsigned max is
     exactly the G-Counter / vector-clock join.
@@ -361,6 +363,22 @@ class Comm:
         h = C.c_void_p()
         _lib.call("crdt_shard_comm_create", arr, len(devices), C.byref(h))
         return cls(h, [torch.device("cuda", d) for d in devices])
+
+    @classmethod
+    def loopback(cls, device: int, members: int) -> "Comm":
+        """``members`` ranks on ONE GPU in this process (the loopback
+        transport: device copies and a reduction kernel fenced by events
+        against the member streams) -- the multi-rank protocols at R > 1 on a
+        one-GPU machine, with the same compute as over RCCL."""
+        h = C.c_void_p()
+        _lib.call("crdt_shard_comm_create_loopback", device, members, C.byref(h))
+        return cls(h, [torch.device("cuda", device)] * members)
+
+    @property
+    def transport(self) -> str:
+        k = C.c_int()
+        _lib.call("crdt_shard_comm_transport", self._h, C.byref(k))
+        return {0: "rccl", 1: "loopback"}[k.value]
 
     @classmethod
     def init_rank(cls, eng, group=None) -> "Comm":
@@ -479,6 +497,24 @@ class Comm:
         self._call("crdt_shard_lww_merge_local" if lww else "crdt_shard_orset_merge_local", self._tuples(a), na,
                    self._tuples(b), nb, self._tuples(outs), cap, n, 1 if gather else 0)
         return [o.slice(n[i]) for i, o in enumerate(outs)]
+
+    def set_merge_local_dev(self, a, b, lww: bool = True, cap: int | None = None, outs=None):
+        """crdt_shard_*_merge_local_dev: each member's own key range, its
+        length left on the device (no trailing synchronisation).  Returns
+        (outs, counts): per-member TupleSets of capacity cap and int64[1]
+        device counts."""
+        from .engine import TupleSet
+        na = (C.c_size_t * self.members)(*[len(x) for x in a])
+        nb = (C.c_size_t * self.members)(*[len(x) for x in b])
+        if cap is None:
+            if self.members != self.nranks:
+                raise ValueError("cap is required when other processes hold members")
+            cap = max(sum(len(x) + len(y) for x, y in zip(a, b)), 1)
+        outs = [TupleSet.empty(cap, d) for d in self.devices] if outs is None else outs
+        counts = [torch.zeros(1, dtype=torch.int64, device=d) for d in self.devices]
+        self._call("crdt_shard_lww_merge_local_dev" if lww else "crdt_shard_orset_merge_local_dev", self._tuples(a),
+                   na, self._tuples(b), nb, self._tuples(outs), cap, self._ptrs(counts))
+        return outs, counts
 
     def refmerge(self, engines, packed_list):
         """crdt_shard_refmerge: member i merges packed_list[i] (its ts-range

@@ -181,8 +181,6 @@ int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, cons
                             size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                               size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
-/* Sortedness check (host-facing validation): *bad_dev = number of adjacent
- * pairs with t[i] > t[i+1]. */
 /* Sort n SoA tuples (device) into ascending (key, ts, rep, tomb) order --
  * the merge input order, with tomb (0/1) breaking exact tag ties so the
  * result does not depend on the input order (config D2: unsorted state).
@@ -194,8 +192,17 @@ int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, crdt_tuples
  * probes (device arrays): key-range sharding of a sorted set (§8(e) D). */
 int crdt_u64_lower_bound(crdt_ctx *ctx, const uint64_t *sorted_dev, size_t n, const uint64_t *probes_dev,
                          size_t m, uint64_t *out_dev);
+/* Sortedness check (host-facing validation): *bad_dev = number of adjacent
+ * pairs with t[i] > t[i+1]. */
 int crdt_tuples_count_unsorted(crdt_ctx *ctx, const crdt_tuples *t, size_t n,
                                uint64_t *bad_dev);
+/* Stable merge of two sorted tuple arrays, every tuple kept (on an equal tag
+ * a's copies first): out[0 .. na + nb).  The key-range owner's rank-order
+ * merge of received runs in crdt_shard_*_merge_local (the population's side
+ * = the stable merge of every rank's side in rank order); its length is known
+ * on the host, so a tree of these merges needs no read-back. */
+int crdt_tuples_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
+                      const crdt_tuples *out);
 
 /* ------------------------------------------------ RefMerge (a1-a5)
  * Batched, bit-exact (*Server).merge() (main.go:35-100) for many replicas.
@@ -259,9 +266,13 @@ int crdt_refmerge_batch_kv(crdt_ctx *ctx, const crdt_refmerge_in *in, const crdt
  * is r_ts / r_kv [r_off[p] .. r_end[p]) -- ranges may overlap and r_ts /
  * r_kv / the kv arena may alias the L arrays, so no RemoteDiff is
  * assembled.  r_slot_delta (nullable) is added (mod 2^32) to the key slot
- * of every R pair of replica p (a peer's slots re-based to p's).  in->n_r =
- * the total of the R ranges (outputs sized n_l + n_r); out.src of an R entry
- * is -(its index in r_ts) - 1.  kv: nullable, as crdt_refmerge_batch_kv. */
+ * of every R pair of replica p (a peer's slots re-based to p's).  in->n_r
+ * MUST equal the total of the R ranges (outputs sized n_l + n_r): ranges
+ * summing past it, or a reversed range (r_end < r_off), raise CRDT_DEV_RANGE
+ * and nothing is merged.  out.src of an R entry is -(its index in r_ts) - 1.
+ * kv: as crdt_refmerge_batch_kv; REQUIRED (CRDT_E_INVAL otherwise) when
+ * r_slot_delta is given -- a gather of the new Diff's pairs by src after
+ * the merge cannot re-base the pulled slots. */
 typedef struct crdt_refmerge_pull {
     const uint64_t *r_end;          /* [replicas] */
     const uint32_t *r_slot_delta;   /* [replicas] or NULL */
@@ -437,13 +448,24 @@ typedef struct crdt_comm crdt_comm;
 int crdt_shard_unique_id(void *id, size_t cap);
 int crdt_shard_comm_create(const int *devices, int n, crdt_comm **out);
 int crdt_shard_comm_init_rank(crdt_ctx *ctx, const void *id, int nranks, int rank, crdt_comm **out);
+/* Loopback communicator: `members` ranks (1 .. 64) on ONE device in this
+ * process, each with its own context and stream; the collectives are device
+ * copies and a reduction kernel on a transport stream, ordered against the
+ * member streams by events (no host synchronisation).  Every crdt_shard_*
+ * protocol runs unchanged on it, so its multi-rank planning, offsets, tree
+ * merges and reductions run at R > 1 on one GPU.  Real multi-GPU
+ * communicators (the two calls above) use RCCL. */
+int crdt_shard_comm_create_loopback(int device, int members, crdt_comm **out);
 int crdt_shard_comm_destroy(crdt_comm *comm);
 int crdt_shard_comm_info(const crdt_comm *comm, int *members, int *nranks, int *rank0);
+enum { CRDT_SHARD_RCCL = 0, CRDT_SHARD_LOOPBACK = 1 };
+int crdt_shard_comm_transport(const crdt_comm *comm, int *kind);
 int crdt_shard_member_ctx(crdt_comm *comm, int member, crdt_ctx **ctx);
 int crdt_shard_comm_last_error(const crdt_comm *comm);     /* last ncclResult_t */
 int crdt_shard_sync(crdt_comm *comm);
 /* Config E1: member i folds its [rows[i] x nodes] row shard (crdt_gcounter_fold),
- * then ncclAllReduce(ncclUint64, ncclMax) of the nodes-long folds: every
+ * then an all-reduce(max) of the nodes-long folds (RCCL: ncclAllReduce(ncclUint64,
+ * ncclMax)): every
  * member's out[i] holds the global join of the whole population. */
 int crdt_shard_fold_max_u64(crdt_comm *comm, const uint64_t *const *shard_dev, const size_t *rows, size_t nodes,
                             uint64_t *const *out_dev);
@@ -493,6 +515,16 @@ int crdt_shard_lww_merge_local(crdt_comm *comm, const crdt_tuples *a, const size
                                const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out, int gather);
 int crdt_shard_orset_merge_local(crdt_comm *comm, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
                                  const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out, int gather);
+/* The same, each member's own key range only (gather == 0), its length
+ * written to n_out_dev[i] (a device uint64 on member i's GPU) on the member
+ * stream: no trailing synchronisation (with nranks > 1 planning still reads
+ * back the samples and the count matrix).  CRDT_E_RANGE if cap is below a
+ * member's received tuples.  Device-side failures: crdt_ctx_device_status. */
+int crdt_shard_lww_merge_local_dev(crdt_comm *comm, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
+                                   const size_t *nb, const crdt_tuples *out, size_t cap, uint64_t *const *n_out_dev);
+int crdt_shard_orset_merge_local_dev(crdt_comm *comm, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
+                                     const size_t *nb, const crdt_tuples *out, size_t cap,
+                                     uint64_t *const *n_out_dev);
 /* (*Server).merge() (main.go:35-100) of ONE batch of replicas whose Diff /
  * RemoteDiff logs are split by ts range over the ranks (global rank g holds
  * the g-th ts range of every replica; every member's kv_val ids index the

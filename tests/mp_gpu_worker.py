@@ -13,7 +13,10 @@ one GPU) and checks them against the oracle, not against another GPU path:
      round each rank fetches only the Diffs its replicas pull (all-to-all-v)
      and each replica pulls its peer (self-pulls and dead peers included);
      the rank's block must equal a host simulation of the reference's rounds
-     on oracle/pyref.py (main.go:226-258).
+     on oracle/pyref.py (main.go:226-258);
+  3. shard.sharded_set_merge_local with the HIP set merges as the per-rank
+     compute -- the gathered state must equal the oracle's merge of the
+     rank-order stable merges of every rank's own tuples.
 
 Env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT.  Prints one line
 "RANK r OK <checks>" and exits 0, or raises.
@@ -92,13 +95,42 @@ def check_sharded_gossip(eng, rank, world):
     return "sharded_round"
 
 
+def check_sharded_set_merge_local(eng, rank, world):
+    """shard.sharded_set_merge_local with the HIP LWW / OR-Set merge as the
+    per-rank compute (the default): the gathered state == the oracle's merge
+    of the rank-order stable merges of every rank's own tuples, and the
+    ungathered per-rank ranges partition it."""
+    from crdt_amd import shard
+    from crdt_amd.engine import TupleSet
+    from oracle import oracle
+    from test_shard_gloo import SIZES, rank_sets, stable_rank_merge
+    done = []
+    for lww in (True, False):
+        sizes = [SIZES[p % len(SIZES)] for p in range(world)]
+        a, b = rank_sets(13, rank, *sizes[rank], 3000)
+        A, B = TupleSet.from_numpy(*a, eng.device), TupleSet.from_numpy(*b, eng.device)
+        got = shard.sharded_set_merge_local(eng, A, B, lww=lww)
+        mine = shard.sharded_set_merge_local(eng, A, B, lww=lww, gather=False)
+        everyone = [rank_sets(13, p, *sizes[p], 3000) for p in range(world)]
+        exp = (oracle.lww_merge if lww else oracle.orset_merge)(stable_rank_merge([e[0] for e in everyone]),
+                                                                 stable_rank_merge([e[1] for e in everyone]))
+        for g, e in zip(got.to_numpy(), exp):
+            np.testing.assert_array_equal(g, e)
+        tot = torch.tensor([len(mine)], dtype=torch.int64)
+        dist.all_reduce(tot)
+        assert int(tot) == len(exp[0])
+        done.append("lww" if lww else "orset")
+    return "sharded_set_merge_local(" + ",".join(done) + ")"
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from crdt_amd.engine import Engine
     eng = Engine(0)
     try:
-        done = [check_sharded_refmerge(eng, rank, world), check_sharded_gossip(eng, rank, world)]
+        done = [check_sharded_refmerge(eng, rank, world), check_sharded_gossip(eng, rank, world),
+                check_sharded_set_merge_local(eng, rank, world)]
         torch.cuda.synchronize()
         dist.barrier()
         print(f"RANK {rank} OK {' '.join(done)}", flush=True)

@@ -41,4 +41,4 @@ def test_two_fresh_ranks_match_oracle(world):
                 p.kill()
     for r, (rc, out) in enumerate(outs):
         assert rc == 0, f"rank {r} failed:\n{out[-4000:]}"
-        assert f"RANK {r} OK sharded_refmerge sharded_round" in out, out[-2000:]
+        assert f"RANK {r} OK sharded_refmerge sharded_round sharded_set_merge_local(lww,orset)" in out, out[-2000:]

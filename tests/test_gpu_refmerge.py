@@ -398,3 +398,55 @@ def test_batch_pull_in_place_equals_assembled(eng):
     assert int(kv_i["off"][n_out]) == m and int(kv_i["off"][n]) == m
     assert torch.equal(kv_i["off"][: n_out + 1], kv_a["off"][: n_out + 1])
     assert torch.equal(kv_i["key"][:m], kv_a["key"][:m]) and torch.equal(kv_i["val"][:m], kv_a["val"][:m])
+
+
+def _pull_batch(eng, seed=19, P=12):
+    h = synth.refmerge_packed(seed, P, 2000)
+    q = (np.arange(P) * 5 + 1) % P
+    l_off = h["l_off"]
+    hi = dict(h, r_off=l_off[q].copy(), r_ts=h["l_ts"], r_kv=h["l_kv"])
+    d = refmerge.to_device(hi, eng.device)
+    d["n_r"] = int((l_off[q + 1] - l_off[q]).sum())
+    n = len(h["l_ts"]) + d["n_r"]
+    kv = {"off": torch.zeros(n + 1, dtype=torch.int64, device=eng.device),
+          "key": torch.zeros(2 * len(h["kv_key"]) + 2, dtype=torch.int32, device=eng.device),
+          "val": torch.zeros(2 * len(h["kv_key"]) + 2, dtype=torch.int32, device=eng.device)}
+    sd = ((np.arange(P) - q) * (h["n_slots"] // P)) % (1 << 32)
+    pull = {"r_end": torch.from_numpy(l_off[q + 1].copy()).to(eng.device),
+            "r_slot_delta": torch.from_numpy(sd.astype(np.uint32).view(np.int32)).to(eng.device)}
+    return d, kv, pull, q
+
+
+def test_batch_pull_slot_delta_requires_kv_output(eng):
+    """crdt_refmerge_batch_pull with re-based key slots (r_slot_delta) but no
+    fused kv output is CRDT_E_INVAL: a gather of the new Diff's pairs by src
+    afterwards could not re-base the pulled slots (the boundary hazard of a
+    cgo caller, include/crdt_amd.h)."""
+    from crdt_amd import _lib
+    d, kv, pull, _ = _pull_batch(eng)
+    with pytest.raises(_lib.CrdtError) as ei:
+        eng.refmerge_batch(d, pull=pull)
+    assert ei.value.status == -1                         # CRDT_E_INVAL
+    eng.refmerge_batch(d, pull={"r_end": pull["r_end"], "r_slot_delta": None})   # no re-basing: allowed
+    assert eng.device_status(clear=True) == 0
+    eng.refmerge_batch(d, kv=kv, pull=pull)
+    assert eng.device_status(clear=True) == 0
+
+
+@pytest.mark.parametrize("bad", ["reversed", "past_n_r"])
+def test_batch_pull_bad_ranges_raise_range_flag(eng, bad):
+    """R ranges the call was not sized for -- a reversed range (r_end < r_off)
+    or ranges summing past n_r -- raise CRDT_DEV_RANGE on the device instead
+    of reading / writing out of range (the planning passes clamp and the
+    offset passes write nothing)."""
+    d, kv, pull, q = _pull_batch(eng, seed=23)
+    if bad == "reversed":
+        r_end = pull["r_end"].clone()
+        r_end[3] = d["r_off"][3] - 1 if int(d["r_off"][3]) > 0 else 0
+        d["r_off"][3] = r_end[3] + 1
+        pull = dict(pull, r_end=r_end)
+    else:
+        d["n_r"] = d["n_r"] // 3
+        kv["off"] = kv["off"][: len(d["l_ts"]) + d["n_r"] + 1].clone()
+    eng.refmerge_batch(d, kv=kv, pull=pull)
+    assert eng.device_status(clear=True) & 2            # CRDT_DEV_RANGE

@@ -1,0 +1,238 @@
+"""GPU: the native multi-rank protocols (crdt_shard_*, csrc/shard.hip) at R > 1
+on ONE GPU, through the loopback transport (crdt_shard_comm_create_loopback:
+R ranks in one process, each with its own context and stream; collectives are
+device copies and a reduction kernel fenced by events).  The planning,
+offsets, count matrices, tree merges and cross-rank reductions are the same
+code the RCCL transport runs on a multi-GPU node; every result is checked
+against the oracle (oracle/crdt_oracle.c), never against another GPU path.
+Reference analog: the cross-replica exchange of main.go:226-258."""
+import numpy as np
+import pytest
+import torch
+
+from crdt_amd import refmerge, shard, synth
+from crdt_amd.engine import TupleSet, as_u64, u64_tensor
+from oracle import oracle
+from refmerge_util import oracle_packed_replica, split_ts_range, ts_splitters
+from test_shard_gloo import rank_sets, stable_rank_merge
+
+pytestmark = pytest.mark.gpu
+
+EDGE = np.array([0, 1, 2**63 - 1, 2**63, 2**64 - 2, 2**64 - 1], dtype=np.uint64)
+WORLDS = [2, 3, 8]
+
+
+@pytest.fixture(scope="module", params=WORLDS)
+def comm(request):
+    c = shard.Comm.loopback(0, request.param)
+    yield c
+    c.close()
+
+
+def _np_tuples(ts):
+    return tuple(np.asarray(x) for x in ts)
+
+
+def test_loopback_info(comm):
+    assert comm.transport == "loopback"
+    assert comm.members == comm.nranks and comm.rank0 == 0
+
+
+def test_fold_max_uneven_row_shards(comm):
+    """crdt_shard_fold_max_u64 over uneven row shards (one of a single row),
+    the unsigned edges in the last shard == oc_gcounter_fold of the whole."""
+    R, nodes = comm.nranks, 64
+    rows = [1 + 997 * r + (r % 2) * 5003 for r in range(R)]
+    full = synth.counters(23, 1, sum(rows) * nodes).reshape(sum(rows), nodes)
+    full[-1, : len(EDGE)] = EDGE
+    cuts = np.concatenate([[0], np.cumsum(rows)])
+    shards = [u64_tensor(full[cuts[r]:cuts[r + 1]], "cuda:0") for r in range(R)]
+    torch.cuda.synchronize()
+    outs = comm.fold_max(shards)
+    comm.sync()
+    exp = oracle.gcounter_fold(full)
+    for o in outs:
+        np.testing.assert_array_equal(as_u64(o), exp)
+
+
+def test_allreduce_typed(comm):
+    """crdt_shard_allreduce: int64 SUM wraps (main.go:95), signed MAX; int32
+    likewise; crdt_shard_allreduce_max_u64 is the unsigned max."""
+    R = comm.nranks
+    rng = np.random.default_rng(5 + R)
+    x64 = [rng.integers(-2**63, 2**63 - 1, 4099, dtype=np.int64) for _ in range(R)]
+    x64[0][:3] = (2**63 - 1, -2**63, -1)
+    x32 = [rng.integers(-2**31, 2**31 - 1, 777, dtype=np.int32) for _ in range(R)]
+    u64 = [rng.integers(0, 2**64 - 1, 1000, dtype=np.uint64, endpoint=True) for _ in range(R)]
+    u64[R - 1][:len(EDGE)] = EDGE
+    with np.errstate(over="ignore"):
+        s64 = np.sum(np.stack(x64), axis=0, dtype=np.int64)
+        s32 = np.sum(np.stack(x32), axis=0, dtype=np.int32)
+    for op, exp64, exp32 in (("sum", s64, s32), ("max", np.max(np.stack(x64), 0), np.max(np.stack(x32), 0))):
+        t64 = [torch.from_numpy(v.copy()).cuda() for v in x64]
+        t32 = [torch.from_numpy(v.copy()).cuda() for v in x32]
+        torch.cuda.synchronize()
+        comm.allreduce(t64, op)
+        comm.allreduce(t32, op)
+        comm.sync()
+        for t in t64:
+            np.testing.assert_array_equal(t.cpu().numpy(), exp64)
+        for t in t32:
+            np.testing.assert_array_equal(t.cpu().numpy(), exp32)
+    tu = [u64_tensor(v, "cuda:0") for v in u64]
+    torch.cuda.synchronize()
+    comm.allreduce_max_u64(tu)
+    comm.sync()
+    for t in tu:
+        np.testing.assert_array_equal(as_u64(t), np.max(np.stack(u64), 0))
+
+
+def test_set_allgather_v(comm):
+    """Every member receives all ranks' tuples in rank order (empty ranks
+    included); one count all-gather + one point-to-point group."""
+    R = comm.nranks
+    sizes = [(1234 * (r + 1)) % 3001 if r % 3 != 1 else 0 for r in range(R)]
+    locs = [synth.sort_tuples_np(*synth.set_tuples(40 + r, 0, n, 999)) for r, n in enumerate(sizes)]
+    tl = [TupleSet.from_numpy(*s, "cuda:0") for s in locs]
+    cap = sum(sizes) + 3
+    outs = [TupleSet.empty(cap, "cuda:0") for _ in range(R)]
+    torch.cuda.synchronize()
+    n = comm.set_allgather_v(tl, outs, cap)
+    comm.sync()
+    assert n == sum(sizes)
+    exp = [np.concatenate([s[f] for s in locs]) for f in range(4)]
+    for o in outs:
+        for g, e in zip(o.slice(n).to_numpy(), exp):
+            np.testing.assert_array_equal(g, e)
+    with pytest.raises(Exception):
+        comm.set_allgather_v(tl, outs, sum(sizes) - 1)     # CRDT_E_RANGE: capacity too small
+
+
+def test_alltoallv(comm):
+    """crdt_shard_alltoallv with a random count matrix (zeros included): rank
+    q's receive buffer = every rank's q-th segment in rank order."""
+    R = comm.nranks
+    rng = np.random.default_rng(R)
+    cnt = rng.integers(0, 300, (R, R))
+    cnt[0, R - 1] = 0
+    sends, recvs, exp = [], [], [[] for _ in range(R)]
+    for i in range(R):
+        x = rng.integers(0, 2**62, int(cnt[i].sum()), dtype=np.int64)
+        sends.append(torch.from_numpy(x).cuda())
+        o = 0
+        for q in range(R):
+            exp[q].append(x[o:o + cnt[i, q]])
+            o += cnt[i, q]
+    for q in range(R):
+        recvs.append(torch.full((max(int(cnt[:, q].sum()), 1),), -1, dtype=torch.int64, device="cuda:0"))
+    torch.cuda.synchronize()
+    comm.alltoallv(sends, cnt.tolist(), recvs, cnt.T.tolist(), 8)
+    comm.sync()
+    for q in range(R):
+        np.testing.assert_array_equal(recvs[q].cpu().numpy()[: int(cnt[:, q].sum())], np.concatenate(exp[q]))
+
+
+@pytest.mark.parametrize("lww", [True, False])
+def test_set_merge_full_inputs(comm, lww):
+    """crdt_shard_{lww,orset}_merge (every member holds the whole inputs):
+    key-range shards merged per member, all-gathered == the oracle's merge."""
+    R = comm.nranks
+    sa = synth.sort_tuples_np(*synth.set_tuples(33, 0, 60_000, 40_000))
+    sb = synth.sort_tuples_np(*synth.set_tuples(33, 1, 55_000, 40_000))
+    A = [TupleSet.from_numpy(*sa, "cuda:0") for _ in range(R)]
+    B = [TupleSet.from_numpy(*sb, "cuda:0") for _ in range(R)]
+    torch.cuda.synchronize()
+    got = comm.set_merge(A, B, lww=lww)
+    exp = (oracle.lww_merge if lww else oracle.orset_merge)(sa, sb)
+    for g in got:
+        for x, e in zip(g.to_numpy(), exp):
+            np.testing.assert_array_equal(x, e)
+
+
+def _local_sizes(R, case):
+    if case == "uneven":
+        return [(3000 + 1700 * r, 2500 + 900 * ((r * 7) % 5)) for r in range(R)]
+    if case == "empty_sides":
+        return [((0, 4000), (5000, 1), (2200, 0), (0, 0))[r % 4] for r in range(R)]
+    return [(0, 0)] * (R - 1) + [(6000, 5000)]               # one rank holds everything
+
+
+@pytest.mark.parametrize("lww", [True, False])
+@pytest.mark.parametrize("case", ["uneven", "empty_sides", "one_rank"])
+def test_set_merge_local(comm, lww, case):
+    """crdt_shard_{lww,orset}_merge_local at R > 1: weighted splitters, count
+    matrix, one all-to-all group, the rank-order stable-merge tree, one set
+    merge -- gather: every member holds the oracle's merge of the rank-order
+    stable merges of every rank's sides; no gather: the members' ranges
+    concatenate to it; the _dev form (counts left on the device) likewise."""
+    R = comm.nranks
+    sizes = _local_sizes(R, case)
+    ks = 4000                                                # many keys shared across ranks
+    sets = [rank_sets(11, r, na, nb, ks) for r, (na, nb) in enumerate(sizes)]
+    A = [TupleSet.from_numpy(*s[0], "cuda:0") for s in sets]
+    B = [TupleSet.from_numpy(*s[1], "cuda:0") for s in sets]
+    pa = stable_rank_merge([s[0] for s in sets])
+    pb = stable_rank_merge([s[1] for s in sets])
+    exp = (oracle.lww_merge if lww else oracle.orset_merge)(pa, pb)
+    torch.cuda.synchronize()
+    for g in comm.set_merge_local(A, B, lww=lww, gather=True):
+        for x, e in zip(g.to_numpy(), exp):
+            np.testing.assert_array_equal(x, e)
+    mine = comm.set_merge_local(A, B, lww=lww, gather=False)
+    cat = [np.concatenate([m.to_numpy()[f] for m in mine]) for f in range(4)]
+    for x, e in zip(cat, exp):
+        np.testing.assert_array_equal(x, e)
+    outs, counts = comm.set_merge_local_dev(A, B, lww=lww)
+    comm.sync()
+    dev = [o.slice(int(c.item())).to_numpy() for o, c in zip(outs, counts)]
+    cat = [np.concatenate([d[f] for d in dev]) for f in range(4)]
+    for x, e in zip(cat, exp):
+        np.testing.assert_array_equal(x, e)
+
+
+def test_refmerge_ts_range_shards(comm, eng):
+    """crdt_shard_refmerge over R ts-range shards of one batch (rank r holds
+    the r-th ts range of every replica): each member's slice of the new Diff
+    == the oracle's new Diff restricted to that range, and every member's
+    all-reduced CurrentState == the oracle's, replica by replica."""
+    R = comm.nranks
+    h = synth.refmerge_packed(47 + R, 40, 2500)
+    spl = ts_splitters(h, R)
+    parts = [split_ts_range(h, spl[r], spl[r + 1]) for r in range(R)]
+    devs = [refmerge.to_device({k: v for k, v in p.items() if not k.endswith("_sel")}, "cuda:0") for p in parts]
+    torch.cuda.synchronize()
+    outs = comm.refmerge([eng] * R, devs)
+    comm.sync()
+    host = [{k: o[k].cpu().numpy() for k in o} for o in outs]
+    total = 0
+    for p in range(h["replicas"]):
+        o_ts, o_or, o_src, k, s, v = oracle_packed_replica(h, p)
+        sl = slice(p * 62, (p + 1) * 62)
+        for r in range(R):
+            lo, hi = spl[r], spl[r + 1]
+            keep = (o_ts >= lo) & (o_ts < hi) if r + 1 < R else (o_ts >= lo)
+            off = host[r]["off"]
+            a, b = int(off[p]), int(off[p + 1])
+            np.testing.assert_array_equal(host[r]["ts"][a:b], o_ts[keep])
+            np.testing.assert_array_equal(host[r]["origin"][a:b], o_or[keep])
+            loc = host[r]["src"][a:b]
+            glob = np.where(loc >= 0, parts[r]["l_sel"][np.maximum(loc, 0)],
+                            -parts[r]["r_sel"][np.maximum(-loc - 1, 0)] - 1)
+            np.testing.assert_array_equal(glob, o_src[keep])
+            np.testing.assert_array_equal(host[r]["st_kind"][sl], k)
+            np.testing.assert_array_equal(host[r]["st_str"][sl].view(np.uint32)[k == 1], s[k == 1])
+            np.testing.assert_array_equal(host[r]["st_sum"][sl][k == 2], v[k == 2])
+            total += b - a
+    assert total == sum(len(oracle_packed_replica(h, p)[0]) for p in range(h["replicas"]))
+
+
+@pytest.mark.parametrize("na,nb", [(50_000, 47_000), (0, 3000), (2049, 0), (1, 1)])
+def test_tuples_merge_stable(eng, na, nb):
+    """crdt_tuples_merge == numpy's stable lexsort of the concatenation (A
+    first on equal tags: duplicated tags across the sides keep A's first)."""
+    sa = synth.sort_tuples_np(*synth.set_tuples(7, 0, na, 5000))
+    sb = synth.sort_tuples_np(*synth.set_tuples(7, 1, nb, 5000))
+    got = eng.tuples_merge(TupleSet.from_numpy(*sa, eng.device), TupleSet.from_numpy(*sb, eng.device)).to_numpy()
+    exp = stable_rank_merge([sa, sb])
+    for g, e in zip(got, exp):
+        np.testing.assert_array_equal(g, e)
