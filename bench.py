@@ -576,7 +576,7 @@ class ShardSetMerge(SetMerge):
         self.gout = E.TupleSet.empty(self.cap, eng.device)
         self.step()
         torch.cuda.synchronize()
-        self.n_total = len(self.last)
+        self.n_total = len(self.last) if self.last_count is None else int(self.last_count.item())
         self.config = dict(self.config, workload=(
             f"{'LWW-Element-Set' if lww else 'OR-Set'} merge of a distributed population: {n} tuples per side "
             f"per GPU (sorted), key space {key_space}, key-range all-to-all + local merge + all-gather-v "
@@ -587,8 +587,17 @@ class ShardSetMerge(SetMerge):
     e2e_skip = "the step's outputs are the whole population's merged state on every rank: no host-staged form"
 
     def step(self):
+        if self.world == 1:
+            # one rank: the whole merged state IS the rank's own key range, so
+            # the count-on-device form returns the same state without the
+            # trailing read-back (crdt_shard_*_merge_local_dev)
+            outs, cnt = self.comm.set_merge_local_dev([self.A], [self.B], lww=self.lww, cap=self.cap,
+                                                      outs=[self.gout])
+            self.last, self.last_count = outs[0], cnt[0]
+            return
         self.last = self.comm.set_merge_local([self.A], [self.B], lww=self.lww, gather=True, cap=self.cap,
                                               outs=[self.gout])[0]
+        self.last_count = None
 
     def extra(self, avg_ms):
         return {"exchange": {"n_out_total": self.n_total, "ranks": self.world,

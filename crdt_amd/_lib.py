@@ -117,6 +117,13 @@ class crdt_refmerge_acc(C.Structure):
     _fields_ = [("best", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p)]
 
 
+class crdt_population_init(C.Structure):
+    _fields_ = [("replicas", C.c_uint32), ("keys_per_replica", C.c_uint32), ("first", C.c_uint64),
+                ("n_str", C.c_uint64), ("l_off", C.c_void_p), ("l_ts", C.c_void_p), ("l_origin", C.c_void_p),
+                ("l_kv", C.c_void_p), ("kv_key", C.c_void_p), ("kv_val", C.c_void_p), ("str_bytes", C.c_void_p),
+                ("str_off", C.c_void_p)]
+
+
 _P = C.c_void_p
 _SZ = C.c_size_t
 _U64 = C.c_uint64
@@ -252,6 +259,12 @@ SIGNATURES = {
     "crdt_shard_orset_merge_local_dev": (_I, [_P, C.POINTER(crdt_tuples), C.POINTER(_SZ), C.POINTER(crdt_tuples),
                                               C.POINTER(_SZ), C.POINTER(crdt_tuples), _SZ, C.POINTER(_P)]),
     "crdt_shard_refmerge": (_I, [_P, C.POINTER(crdt_refmerge_in), C.POINTER(crdt_refmerge_out)]),
+    "crdt_population_create": (_I, [_CTX, C.POINTER(crdt_population_init), C.POINTER(_P)]),
+    "crdt_population_destroy": (_I, [_P]),
+    "crdt_population_info": (_I, [_P, C.POINTER(C.c_uint32), C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "crdt_population_read": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "crdt_population_round": (_I, [_P, _P]),
+    "crdt_population_round_sharded": (_I, [_P, C.POINTER(_P), _P, _U64]),
     "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
     "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),
     "crdt_synth_set_tuples": (_I, [_CTX, _U64, C.c_uint32, C.POINTER(crdt_tuples), _SZ, _U64]),

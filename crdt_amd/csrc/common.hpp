@@ -6,6 +6,7 @@
 #include <atomic>
 #include <stddef.h>
 #include <stdint.h>
+#include <vector>
 
 #include "../../include/crdt_amd.h"
 
@@ -89,6 +90,26 @@ int tuples_merge_stable(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const cr
 int seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,
                           const uint64_t *a_off, const uint64_t *b_off, uint64_t *dst_off, const uint32_t *a0,
                           const uint32_t *b0, uint32_t *dst0, const uint32_t *a1, const uint32_t *b1, uint32_t *dst1);
+
+// shard.hip: the communicator's collective transport for other protocols
+// (population.hip's sharded rounds).  One point-to-point transfer of a group:
+// member `member` sends `bytes` from sbuf to global rank `peer`, or receives
+// `bytes` from it into rbuf; sends and receives of one (sender, receiver)
+// pair are matched in issue order.
+struct XP2P {
+    size_t member;
+    int peer;
+    bool send;
+    const void *sbuf;
+    void *rbuf;
+    size_t bytes;
+};
+size_t comm_members(const crdt_comm *c);        // local members (0: not a valid communicator)
+int comm_nranks(const crdt_comm *c);
+int comm_rank0(const crdt_comm *c);
+crdt_ctx *comm_member_ctx(crdt_comm *c, size_t i);
+int comm_allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes);
+int comm_p2p(crdt_comm *c, const std::vector<XP2P> &ops);
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

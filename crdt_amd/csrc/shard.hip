@@ -51,17 +51,6 @@ static_assert(sizeof(ncclUniqueId) == CRDT_SHARD_ID_BYTES, "RCCL unique id size"
 namespace crdt {
 enum class XType { U8, U32, I32, U64, I64 };
 enum class XOp { Sum, Max };
-// One point-to-point transfer of a group: member `member` sends `bytes` from
-// sbuf to global rank `peer`, or receives `bytes` from it into rbuf.  Sends
-// and receives of one (sender, receiver) pair are matched in issue order.
-struct XP2P {
-    size_t member;
-    int peer;
-    bool send;
-    const void *sbuf;
-    void *rbuf;
-    size_t bytes;
-};
 struct Transport;
 }  // namespace crdt
 
@@ -371,6 +360,16 @@ int member_own_ctx(crdt_comm::Member &mb, int device) {
 }
 
 }  // namespace
+
+size_t comm_members(const crdt_comm *c) { return valid(c) ? c->m.size() : 0; }
+int comm_nranks(const crdt_comm *c) { return c->nranks; }
+int comm_rank0(const crdt_comm *c) { return c->rank0; }
+crdt_ctx *comm_member_ctx(crdt_comm *c, size_t i) { return c->m[i].ctx; }
+int comm_allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes) {
+    return c->x->allgather(c, send, recv, bytes);
+}
+int comm_p2p(crdt_comm *c, const std::vector<XP2P> &ops) { return c->x->p2p(c, ops); }
+
 }  // namespace crdt
 
 using namespace crdt;

@@ -595,3 +595,93 @@ def sharded_round(pop: Population, peers_all: np.ndarray, group=None, comm=None)
     owner = np.searchsorted(np.asarray(firsts), np.maximum(mine, 0), side="right") - 1
     pf = np.where(live, np.asarray(firsts)[owner], 0)
     return pop.round(mine, imp=imp, peer_first=pf, peer_index=idx)
+
+
+# ---------------------------------------------------------------- the C-ABI population
+class NativePopulation:
+    """A replica population whose anti-entropy rounds run entirely behind the
+    C-ABI (crdt_population_*, csrc/population.hip) -- what a cgo host of the
+    gossip loop (main.go:226-261) binds.  Same rounds as :class:`Population`
+    (in-place pulls, kv pairs from the merge's passes, dead peers skipped),
+    with the per-replica planning in C++.
+
+    * ``NativePopulation(eng, host, K, first)``: on an Engine's context;
+    * ``NativePopulation.on_member(comm, i, host, K, first)``: on member i of
+      a shard.Comm, for :meth:`round_sharded`.
+    ``host``: the Population host arrays (replicas, l_off, l_ts, l_origin,
+    l_kv, kv_key as local slot ids, kv_val, str_bytes, str_off)."""
+
+    def __init__(self, eng, host: dict, keys_per_replica: int, first: int = 0, _ctx=None, _owner=None):
+        from ._lib import crdt_population_init
+        self._owner = eng if eng is not None else _owner
+        ctx = eng.ctx if eng is not None else _ctx
+        if eng is not None:
+            eng._bind()
+        self.K, self.first = int(keys_per_replica), int(first)
+        self.P = int(host["replicas"])
+        a = lambda x, dt: np.ascontiguousarray(np.asarray(x).astype(dt) if np.asarray(x).dtype != dt
+                                               else np.asarray(x))
+        self._keep = [a(host["l_off"], np.uint64), a(host["l_ts"], np.int64), a(host["l_origin"], np.uint8),
+                      a(host["l_kv"], np.uint64), a(np.asarray(host["kv_key"]).view(np.uint32), np.uint32),
+                      a(np.asarray(host["kv_val"]).view(np.uint32), np.uint32), a(host["str_bytes"], np.uint8),
+                      a(host["str_off"], np.uint64)]
+        ptr = lambda x: x.ctypes.data if x.size else None
+        ini = crdt_population_init(self.P, self.K, self.first, len(self._keep[7]) - 1,
+                                   *[ptr(x) for x in self._keep])
+        h = C.c_void_p()
+        from . import _lib
+        _lib.call("crdt_population_create", ctx, C.byref(ini), C.byref(h), ctx=ctx)
+        self._h = h
+        self._ctx = ctx
+
+    @classmethod
+    def on_member(cls, comm, member: int, host: dict, keys_per_replica: int, first: int):
+        from . import _lib
+        ctx = C.c_void_p()
+        _lib.call("crdt_shard_member_ctx", comm._h, member, C.byref(ctx))
+        return cls(None, host, keys_per_replica, first, _ctx=ctx, _owner=comm)
+
+    def close(self) -> None:
+        from . import _lib
+        if getattr(self, "_h", None):
+            _lib.lib().crdt_population_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def round(self, peers) -> None:
+        """One round, every peer on this population (global ids, -1 = dead)."""
+        from . import _lib
+        pk = np.ascontiguousarray(np.asarray(peers, dtype=np.int64))
+        assert len(pk) == self.P
+        if hasattr(self._owner, "_bind"):
+            self._owner._bind()
+        _lib.call("crdt_population_round", self._h, pk.ctypes.data, ctx=self._ctx)
+
+    @staticmethod
+    def round_sharded(comm, pops, peers_all) -> None:
+        """One round over the communicator: pops[i] = member i's population."""
+        from . import _lib
+        pk = np.ascontiguousarray(np.asarray(peers_all, dtype=np.int64))
+        arr = (C.c_void_p * len(pops))(*[p._h.value for p in pops])
+        comm._call("crdt_population_round_sharded", arr, pk.ctypes.data, len(pk))
+
+    def read(self) -> dict:
+        """The Diffs (Population.to_host layout) and CurrentState, on the host."""
+        from . import _lib
+        P, n_e, n_kv = C.c_uint32(), C.c_size_t(), C.c_size_t()
+        _lib.call("crdt_population_info", self._h, C.byref(P), C.byref(n_e), C.byref(n_kv))
+        ns = self.P * self.K
+        out = {"off": np.empty(self.P + 1, np.uint64), "ts": np.empty(n_e.value, np.int64),
+               "origin": np.empty(n_e.value, np.uint8), "kv_off": np.empty(n_e.value + 1, np.uint64),
+               "kv_key": np.empty(n_kv.value, np.uint32), "kv_val": np.empty(n_kv.value, np.uint32),
+               "st_kind": np.empty(ns, np.uint8), "st_str": np.empty(ns, np.uint32), "st_sum": np.empty(ns, np.int64)}
+        ptr = lambda x: x.ctypes.data if x.size else None
+        _lib.call("crdt_population_read", self._h, *[ptr(out[k]) for k in
+                                                      ("off", "ts", "origin", "kv_off", "kv_key", "kv_val",
+                                                       "st_kind", "st_str", "st_sum")], ctx=self._ctx)
+        return out

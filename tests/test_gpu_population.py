@@ -1,0 +1,128 @@
+"""GPU: anti-entropy rounds behind the C-ABI (crdt_population_*,
+csrc/population.hip) against the host simulation of the
+reference's rounds on oracle/pyref.py (main.go:226-258): every replica pulls
+its peer's whole Diff as remote maps and merges; self-pulls rebuild
+CurrentState, dead peers (-1) skip the round.
+
+* crdt_population_round on one population;
+* crdt_population_round_sharded over a 1-member RCCL communicator and over
+  loopback communicators of 2, 3 and 5 ranks on the one GPU (replicas split
+  by crdt_shard_range; every rank receives only the Diffs its replicas pull).
+"""
+import numpy as np
+import pytest
+
+from crdt_amd import gossip, shard
+from gossip_util import K, KEYS, STRS, _host_round, _pack, _rand_diff, _same_diffs
+from oracle import pyref
+
+pytestmark = pytest.mark.gpu
+
+
+def _unpack_native(h, P):
+    out = []
+    for i in range(P):
+        d = {}
+        for e in range(int(h["off"][i]), int(h["off"][i + 1])):
+            kv = {KEYS[int(h["kv_key"][q]) - i * K]: STRS[int(h["kv_val"][q])]
+                  for q in range(int(h["kv_off"][e]), int(h["kv_off"][e + 1]))}
+            d[int(h["ts"][e])] = pyref.Command(kv) if h["origin"][e] else kv
+        out.append(d)
+    return out
+
+
+def _state_native(h, P):
+    out = []
+    for i in range(P):
+        st = {}
+        for k in range(K):
+            s = i * K + k
+            if h["st_kind"][s] == 1:
+                st[KEYS[k]] = STRS[int(h["st_str"][s])]
+            elif h["st_kind"][s] == 2:
+                st[KEYS[k]] = str(int(h["st_sum"][s]))
+        out.append(st)
+    return out
+
+
+@pytest.mark.parametrize("draw", ["random", "reference"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_population_rounds_match_reference_simulation(eng, seed, draw):
+    rng = np.random.default_rng(seed)
+    P = 9
+    diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 40))) for i in range(P)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    try:
+        saw = set()
+        for rnd in range(6):
+            peers = (gossip.random_peers if draw == "random" else gossip.reference_peers)(rng, P, 0, P)
+            saw |= {"self"} if np.any(peers == np.arange(P)) else set()
+            saw |= {"dead"} if np.any(peers < 0) else set()
+            pop.round(peers)
+            diffs, states = _host_round(diffs, peers, states)
+            h = pop.read()
+            _same_diffs(_unpack_native(h, P), diffs)
+            assert _state_native(h, P) == states, f"round {rnd}"
+        if draw == "reference":
+            assert saw == {"self", "dead"}
+    finally:
+        pop.close()
+
+
+def test_population_round_rejects_remote_peer(eng):
+    from crdt_amd import _lib
+    rng = np.random.default_rng(3)
+    diffs = [_rand_diff(rng, 100, 5) for _ in range(3)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K, first=10)
+    try:
+        with pytest.raises(_lib.CrdtError):
+            pop.round([10, 11, 3])                       # replica 3 lives on another rank
+    finally:
+        pop.close()
+
+
+def _sharded_rounds(comm, total, seed, rounds=5):
+    rng = np.random.default_rng(seed)
+    diffs = [_rand_diff(rng, 2_000 + 11 * i, int(rng.integers(0, 35))) for i in range(total)]
+    R = comm.nranks
+    cuts = [shard.shard_range(total, R, r) for r in range(R)]
+    pops = []
+    for i in range(comm.members):
+        b, e = cuts[comm.rank0 + i]
+        pops.append(gossip.NativePopulation.on_member(comm, i, _pack(diffs[b:e]), K, b))
+    states = [{} for _ in range(total)]
+    try:
+        for rnd in range(rounds):
+            peers = (gossip.random_peers if rnd % 2 == 0 else gossip.reference_peers)(rng, total, 0, total)
+            gossip.NativePopulation.round_sharded(comm, pops, peers)
+            diffs, states = _host_round(diffs, peers, states)
+            for i, p in enumerate(pops):
+                b, e = cuts[comm.rank0 + i]
+                h = p.read()
+                _same_diffs(_unpack_native(h, e - b), diffs[b:e])
+                assert _state_native(h, e - b) == states[b:e], f"round {rnd}, member {i}"
+    finally:
+        for p in pops:
+            p.close()
+
+
+@pytest.mark.parametrize("world,total", [(2, 7), (3, 10), (5, 4)])
+def test_population_sharded_rounds_loopback(world, total):
+    """R ranks on the loopback transport (5 ranks over 4 replicas: one rank
+    holds none)."""
+    comm = shard.Comm.loopback(0, world)
+    try:
+        _sharded_rounds(comm, total, 40 + world)
+    finally:
+        comm.close()
+
+
+def test_population_sharded_round_rccl_one_rank(eng):
+    """The same protocol through a 1-member RCCL communicator (ncclCommInitRank)
+    -- self sends / receives of the point-to-point group."""
+    comm = shard.Comm.init_rank(eng)
+    try:
+        _sharded_rounds(comm, 6, 77, rounds=3)
+    finally:
+        comm.close()
