@@ -805,7 +805,8 @@ class GossipRound(Workload):
     name = "gossip_round"
     unit = "remote-entries/s"
     dtype = "int64"
-    kernel = "gossip round (refmerge over the peers' Diffs in place + the new Diffs' kv pairs)"
+    kernel = ("gossip round through crdt_population_round (refmerge over the peers' Diffs in place + the new Diffs' "
+              "kv pairs)")
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         from crdt_amd import gossip, synth
@@ -814,17 +815,30 @@ class GossipRound(Workload):
         host = {"replicas": replicas, "l_off": h["l_off"], "l_ts": h["l_ts"], "l_origin": h["l_origin"],
                 "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
                 "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
-        self.pop = gossip.Population(eng, host, 62)
-        # (A/B: CRDT_GOSSIP_PULL=assembled builds each RemoteDiff by segmented copies first)
-        self.pop.pull_inplace = os.environ.get("CRDT_GOSSIP_PULL", "inplace") != "assembled"
+        # the round behind the C-ABI (crdt_population_round: what a cgo host of
+        # main.go:226-261 calls); CRDT_GOSSIP_IMPL=python: the Python
+        # orchestration over the same kernels (gossip.Population) for the A/B
+        self.native = os.environ.get("CRDT_GOSSIP_IMPL", "native") != "python"
+        if self.native:
+            self.pop = gossip.NativePopulation(eng, host, 62)
+            self.pop.pull_inplace = True
+        else:
+            self.pop = gossip.Population(eng, host, 62)
+            # (A/B: CRDT_GOSSIP_PULL=assembled builds each RemoteDiff by segmented copies first)
+            self.pop.pull_inplace = os.environ.get("CRDT_GOSSIP_PULL", "inplace") != "assembled"
+            self.init = self.pop.snapshot()
         self.host = h
-        self.init = self.pop.snapshot()
         self.rng = np.random.default_rng(seed)
         self.gossip, self.P, self.n_l = gossip, replicas, n_l
         self.peers = gossip.random_peers(self.rng, replicas, 0, replicas)
-        out = self.step()
-        torch.cuda.synchronize()
-        self.n_out = int(out["off"][-1].item())
+        if self.native:
+            self.pop.round(self.peers)
+            self.n_out = self.pop.sizes()[1]
+            self.pop.undo()
+        else:
+            out = self.step()
+            torch.cuda.synchronize()
+            self.n_out = int(out["off"][-1].item())
         self.config = {"workload": f"gossip round: {replicas} replicas x {entries} Diff entries each pull a random "
                                    "peer's Diff and merge (BASELINE configs[0] shape at scale)",
                        "replicas": replicas, "entries": entries, "n_new_diff": self.n_out,
@@ -843,7 +857,11 @@ class GossipRound(Workload):
         return asm + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
 
     def step(self):
-        self.pop.restore(self.init)           # every step is the same round from the same Diffs
+        if self.native:                       # every step is the same round from the same Diffs:
+            self.pop.round(self.peers)        # the round, then back to the Diffs before it
+            self.pop.undo()
+            return None
+        self.pop.restore(self.init)
         return self.pop.round(self.peers)
 
     def cpu_baseline(self, seconds, threads):

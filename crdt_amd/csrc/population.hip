@@ -55,6 +55,9 @@ struct crdt_population {
     int cur = 0;
     size_t n_e = 0, n_kv = 0;                  // the current Diffs' entries / kv pairs
     std::vector<uint64_t> cnt, kvcnt;          // per replica (host)
+    std::vector<uint64_t> pcnt, pkvcnt;        // ... of the Diffs before the last round (crdt_population_undo)
+    size_t p_n_e = 0, p_n_kv = 0;
+    bool can_undo = false;
     uint8_t *str_bytes = nullptr;
     uint64_t *str_off = nullptr;
     uint64_t n_str = 0;
@@ -256,9 +259,9 @@ int upload_round(crdt_population *pop, const HostRound &h, RoundArrays *a) {
     }
     const size_t upto = (size_t)((char *)(hp.skip + P) - (char *)pop->pin);
     hipError_t e = hipMemcpyAsync(pop->dsm, pop->pin, upto, hipMemcpyHostToDevice, pop->ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(a->bounds + 2 * P + 3, 0, 8, pop->ctx->stream);
+    // (8 bytes from the 256-byte status allocation: only the low word is compared)
     if (e == hipSuccess)
-        e = hipMemcpyAsync(a->bounds + 2 * P + 3, pop->ctx->dev_status, 4, hipMemcpyDeviceToDevice, pop->ctx->stream);
+        e = hipMemcpyAsync(a->bounds + 2 * P + 3, pop->ctx->dev_status, 8, hipMemcpyDeviceToDevice, pop->ctx->stream);
     return e == hipSuccess ? CRDT_OK : hip_fail(pop->ctx, e);
 }
 
@@ -325,6 +328,13 @@ int pop_commit(crdt_population *pop) {
     const uint64_t *hb = carve_round(pop->pin, P).bounds;
     const uint32_t after = (uint32_t)hb[2 * P + 2], before = (uint32_t)hb[2 * P + 3];
     if (after & ~before) return CRDT_E_DEVICE;
+    pop->pcnt.swap(pop->cnt);
+    pop->pkvcnt.swap(pop->kvcnt);
+    pop->cnt.resize(P);
+    pop->kvcnt.resize(P);
+    pop->p_n_e = pop->n_e;
+    pop->p_n_kv = pop->n_kv;
+    pop->can_undo = true;
     for (uint32_t p = 0; p < P; ++p) {
         pop->cnt[p] = hb[p + 1] - hb[p];
         pop->kvcnt[p] = hb[P + 2 + p] - hb[P + 1 + p];
@@ -431,6 +441,24 @@ extern "C" int crdt_population_destroy(crdt_population *pop) {
         if (p) (void)hipFree(p);
     if (pop->pin) (void)hipHostFree(pop->pin);
     delete pop;
+    return CRDT_OK;
+}
+
+// Undo the last round: the Diffs and CurrentState as they were before it
+// (still in the spare buffers; valid once, until the next round).
+extern "C" int crdt_population_undo(crdt_population *pop) {
+    if (!pop_valid(pop)) return CRDT_E_INVAL;
+    if (!pop->can_undo) return CRDT_E_INVAL;
+    int rc = bind(pop->ctx);
+    if (rc) return rc;
+    hipError_t e = hipStreamSynchronize(pop->ctx->stream);
+    if (e != hipSuccess) return hip_fail(pop->ctx, e);
+    pop->cnt.swap(pop->pcnt);
+    pop->kvcnt.swap(pop->pkvcnt);
+    pop->n_e = pop->p_n_e;
+    pop->n_kv = pop->p_n_kv;
+    pop->cur = 1 - pop->cur;
+    pop->can_undo = false;
     return CRDT_OK;
 }
 

@@ -633,13 +633,17 @@ class NativePopulation:
         _lib.call("crdt_population_create", ctx, C.byref(ini), C.byref(h), ctx=ctx)
         self._h = h
         self._ctx = ctx
+        if eng is not None:
+            eng._depend(self)                  # eng.close() destroys the population first
 
     @classmethod
     def on_member(cls, comm, member: int, host: dict, keys_per_replica: int, first: int):
         from . import _lib
         ctx = C.c_void_p()
         _lib.call("crdt_shard_member_ctx", comm._h, member, C.byref(ctx))
-        return cls(None, host, keys_per_replica, first, _ctx=ctx, _owner=comm)
+        pop = cls(None, host, keys_per_replica, first, _ctx=ctx, _owner=comm)
+        comm._depend(pop)                      # (the member context dies with the communicator)
+        return pop
 
     def close(self) -> None:
         from . import _lib
@@ -661,6 +665,18 @@ class NativePopulation:
         if hasattr(self._owner, "_bind"):
             self._owner._bind()
         _lib.call("crdt_population_round", self._h, pk.ctypes.data, ctx=self._ctx)
+
+    def sizes(self):
+        """(replicas, Diff entries, kv pairs) of the current Diffs."""
+        from . import _lib
+        P, n_e, n_kv = C.c_uint32(), C.c_size_t(), C.c_size_t()
+        _lib.call("crdt_population_info", self._h, C.byref(P), C.byref(n_e), C.byref(n_kv))
+        return P.value, n_e.value, n_kv.value
+
+    def undo(self) -> None:
+        """Back to the Diffs and CurrentState before the last round."""
+        from . import _lib
+        _lib.call("crdt_population_undo", self._h, ctx=self._ctx)
 
     @staticmethod
     def round_sharded(comm, pops, peers_all) -> None:

@@ -399,7 +399,19 @@ class Comm:
         eng._depend(c)                      # eng.close() destroys the communicator first
         return c
 
+    def _depend(self, obj) -> None:
+        """obj (a population on a member context) is closed before the communicator."""
+        import weakref
+        if not hasattr(self, "_deps"):
+            self._deps = []
+        self._deps.append(weakref.ref(obj))
+
     def close(self) -> None:
+        for r in getattr(self, "_deps", []):
+            o = r()
+            if o is not None:
+                o.close()
+        self._deps = []
         if getattr(self, "_h", None):
             if self._owner is not None and not getattr(self._owner, "ctx", None):
                 raise RuntimeError("engine closed before its communicator")   # never reached via Engine.close

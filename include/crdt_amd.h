@@ -588,6 +588,10 @@ int crdt_population_read(crdt_population *pop, uint64_t *l_off, int64_t *ts, uin
  * peers' Diffs in place (crdt_refmerge_batch_pull, key slots re-based, kv
  * pairs from its own passes); one upload, one read-back.  Synchronises. */
 int crdt_population_round(crdt_population *pop, const int64_t *peers);
+/* Undo the last round (local or sharded): the Diffs and CurrentState as they
+ * were before it -- they stay in the population's spare buffers until the
+ * next round; CRDT_E_INVAL when there is nothing to undo. */
+int crdt_population_undo(crdt_population *pop);
 /* One round over a communicator (main.go:226-258 across GPUs): member i's
  * population (created on crdt_shard_member_ctx(comm, i)) holds global
  * replicas crdt_shard_range(total, nranks, rank0 + i); peers_all [total]

@@ -126,3 +126,31 @@ def test_population_sharded_round_rccl_one_rank(eng):
         _sharded_rounds(comm, 6, 77, rounds=3)
     finally:
         comm.close()
+
+
+def test_population_undo_restores_the_previous_round(eng):
+    """crdt_population_undo: the Diffs and CurrentState of before the last
+    round, once; repeating the round then gives the same result."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng(9)
+    P = 6
+    diffs = [_rand_diff(rng, 3_000 + 5 * i, int(rng.integers(1, 30))) for i in range(P)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    try:
+        peers = gossip.reference_peers(rng, P, 0, P)
+        pop.round(gossip.random_peers(rng, P, 0, P))
+        before = pop.read()
+        pop.round(peers)
+        after = pop.read()
+        pop.undo()
+        back = pop.read()
+        for k in before:
+            np.testing.assert_array_equal(back[k], before[k], err_msg=k)
+        with pytest.raises(_lib.CrdtError):
+            pop.undo()                                   # once only
+        pop.round(peers)
+        again = pop.read()
+        for k in after:
+            np.testing.assert_array_equal(again[k], after[k], err_msg=k)
+    finally:
+        pop.close()

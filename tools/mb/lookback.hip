@@ -1,0 +1,260 @@
+// lookback.hip -- does XCD-local tile placement make a single-pass decoupled
+// look-back pay on MI355X?  (the fused set merge with the
+// XCD-contiguous tile mapping)
+//
+// The fused set merge is a single-pass, look-back-chained kernel: per tile,
+// stage + merge + count, publish the count, look back for the offset, store.
+// This microbenchmark strips it to the chain itself -- an exclusive scan of
+// 16M u32 in 4096-item tiles -- and times
+//   * reduce / scan / apply (three launches, no waiting: the two-pass form);
+//   * one pass, tiles in blockIdx order (consecutive tiles on different XCDs,
+//     blocks being dealt round-robin over the 8 XCDs);
+//   * one pass, XCD-chunked: XCD x takes chunks x, x + 8, x + 16, ... of C
+//     consecutive tiles (a tile's predecessor is on its own XCD except at
+//     chunk starts; C = 512 is one contiguous range per XCD);
+//   * one pass without the look-back (timing only, wrong offsets).
+// Status words are single 8-byte {flag, value} agent-scope atomics (one
+// granule: no separate payload ordering, MI355X_MICROARCH.md "Valid forms").
+// Spins are bounded (s_sleep between polls): a tile whose predecessor never
+// publishes raises an error count instead of hanging.
+//
+// build: hipcc -O3 --offload-arch=gfx950 -o tools/mb/lookback tools/mb/lookback.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+constexpr int TB = 256, IPT = 16, TILE = TB * IPT;
+constexpr unsigned long long FLAG_A = 1ull << 62, FLAG_P = 2ull << 62, VAL = (1ull << 62) - 1;
+
+#define CK(x)                                                                       \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                \
+        }                                                                           \
+    } while (0)
+
+__device__ __forceinline__ uint32_t tile_of(uint32_t b, uint32_t chunk) {
+    if (chunk == 0) return b;                              // blockIdx order
+    const uint32_t x = b & 7u, q = b >> 3;
+    return ((q / chunk) * 8u + x) * chunk + q % chunk;
+}
+
+// block exclusive scan of one value per thread; *tot = the block total
+__device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *tot) {
+    __shared__ uint64_t s_w[TB / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint64_t off = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < TB / 64; ++k) {
+        off += k < w ? s_w[k] : 0;
+        all += s_w[k];
+    }
+    __syncthreads();
+    *tot = all;
+    return off + x - v;
+}
+
+// mode 0: look-back; mode 1: no look-back (timing only)
+template <int MODE>
+__global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                unsigned long long *st, uint32_t chunk, unsigned *err) {
+    __shared__ uint64_t s_base;
+    const uint32_t t = tile_of(blockIdx.x, chunk);
+    const size_t base = (size_t)t * TILE + (size_t)threadIdx.x * IPT;
+    uint32_t v[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; k += 4) {
+        const uint4 q = *(const uint4 *)(in + base + k);
+        v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) s += v[k];
+    uint64_t tot;
+    const uint64_t ex = block_scan(s, &tot);
+    if (threadIdx.x == 0) {
+        uint64_t pre = 0;
+        if (MODE == 0) {
+            if (t == 0) {
+                __hip_atomic_store(&st[0], FLAG_P | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(&st[t], FLAG_A | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int64_t j = (int64_t)t - 1;
+                uint32_t spins = 0;
+                while (j >= 0) {
+                    const unsigned long long w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((w & ~VAL) == 0) {
+                        if (++spins > (1u << 20)) {          // bounded: report, never hang
+                            atomicAdd(err, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    pre += w & VAL;
+                    if ((w & ~VAL) == FLAG_P) break;
+                    --j;
+                }
+                __hip_atomic_store(&st[t], FLAG_P | (pre + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        s_base = pre;
+    }
+    __syncthreads();
+    uint64_t run = s_base + ex;
+    uint64_t o[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        o[k] = run;
+        run += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; k += 2) *(ulonglong2 *)(out + base + k) = ulonglong2{o[k], o[k + 1]};
+}
+
+__global__ __launch_bounds__(TB) void k_reduce(const uint32_t *__restrict__ in, uint64_t *__restrict__ sums) {
+    const size_t base = (size_t)blockIdx.x * TILE + (size_t)threadIdx.x * IPT;
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; k += 4) {
+        const uint4 q = *(const uint4 *)(in + base + k);
+        s += (uint64_t)q.x + q.y + q.z + q.w;
+    }
+    uint64_t tot;
+    (void)block_scan(s, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_sums(uint64_t *sums, uint32_t n) {
+    __shared__ uint64_t s_w[16];
+    const uint32_t per = (n + 1023) / 1024, b = threadIdx.x * per, e = b + per < n ? b + per : n;
+    uint64_t s = 0;
+    for (uint32_t i = b; i < e && i < n; ++i) s += sums[i];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint64_t off = 0;
+    for (int k = 0; k < w; ++k) off += s_w[k];
+    uint64_t run = off + x - s;
+    for (uint32_t i = b; i < e && i < n; ++i) {
+        const uint64_t v = sums[i];
+        sums[i] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_apply(const uint32_t *__restrict__ in, const uint64_t *__restrict__ sums,
+                                              uint64_t *__restrict__ out) {
+    const size_t base = (size_t)blockIdx.x * TILE + (size_t)threadIdx.x * IPT;
+    uint32_t v[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; k += 4) {
+        const uint4 q = *(const uint4 *)(in + base + k);
+        v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) s += v[k];
+    uint64_t tot;
+    uint64_t run = sums[blockIdx.x] + block_scan(s, &tot);
+    uint64_t o[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        o[k] = run;
+        run += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; k += 2) *(ulonglong2 *)(out + base + k) = ulonglong2{o[k], o[k + 1]};
+}
+
+int main(int argc, char **argv) {
+    const uint32_t ntiles = argc > 1 ? (uint32_t)atoi(argv[1]) : 4096;     // multiple of 8 * 512
+    const size_t n = (size_t)ntiles * TILE;
+    const int reps = 20;
+    std::vector<uint32_t> h(n);
+    uint64_t seed = 88172645463325252ull;
+    for (size_t i = 0; i < n; ++i) {
+        seed ^= seed << 13, seed ^= seed >> 7, seed ^= seed << 17;
+        h[i] = (uint32_t)(seed & 1023);
+    }
+    std::vector<uint64_t> ref(n);
+    uint64_t run = 0;
+    for (size_t i = 0; i < n; ++i) ref[i] = run, run += h[i];
+    uint32_t *d_in;
+    uint64_t *d_out, *d_sums;
+    unsigned long long *d_st;
+    unsigned *d_err;
+    CK(hipMalloc(&d_in, n * 4));
+    CK(hipMalloc(&d_out, n * 8));
+    CK(hipMalloc(&d_sums, ntiles * 8));
+    CK(hipMalloc(&d_st, ntiles * 8));
+    CK(hipMalloc(&d_err, 4));
+    CK(hipMemcpy(d_in, h.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(d_err, 0, 4));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<uint64_t> got(n);
+    auto check = [&](const char *name) {
+        CK(hipMemcpy(got.data(), d_out, n * 8, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t i = 0; i < n; ++i) bad += got[i] != ref[i];
+        unsigned err = 0;
+        CK(hipMemcpy(&err, d_err, 4, hipMemcpyDeviceToHost));
+        printf("  %-28s check: %zu wrong, %u spin timeouts\n", name, bad, err);
+    };
+    auto timeit = [&](const char *name, auto fn, bool verify) {
+        fn();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) fn();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("%-30s %8.1f us  (%.2f TB/s of in + out)\n", name, ms * 1e3 / reps,
+               (double)n * 12 / (ms * 1e-3 / reps) / 1e12);
+        if (verify) check(name);
+    };
+    printf("exclusive scan of %zu u32 (%u tiles of %d), 20 reps\n", n, ntiles, TILE);
+    timeit("reduce/scan/apply (3 launches)", [&] {
+        k_reduce<<<ntiles, TB>>>(d_in, d_sums);
+        k_scan_sums<<<1, 1024>>>(d_sums, ntiles);
+        k_apply<<<ntiles, TB>>>(d_in, d_sums, d_out);
+    }, true);
+    timeit("one pass, no look-back", [&] { k_onepass<1><<<ntiles, TB>>>(d_in, d_out, d_st, 0, d_err); }, false);
+    const uint32_t chunks[] = {0, 1, 4, 16, 64, 512};
+    for (uint32_t c : chunks) {
+        if (c && ntiles % (8 * c)) continue;
+        char name[64];
+        if (c == 0) snprintf(name, sizeof name, "look-back, blockIdx order");
+        else snprintf(name, sizeof name, "look-back, XCD chunks of %u", c);
+        timeit(name, [&] {
+            hipMemsetAsync(d_st, 0, ntiles * 8);
+            k_onepass<0><<<ntiles, TB>>>(d_in, d_out, d_st, c, d_err);
+        }, true);
+    }
+    CK(hipFree(d_in));
+    CK(hipFree(d_out));
+    CK(hipFree(d_sums));
+    CK(hipFree(d_st));
+    CK(hipFree(d_err));
+    return 0;
+}
