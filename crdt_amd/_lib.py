@@ -117,6 +117,11 @@ class crdt_refmerge_acc(C.Structure):
     _fields_ = [("best", C.c_void_p), ("sum", C.c_void_p), ("npar", C.c_void_p)]
 
 
+class crdt_population_cmds(C.Structure):
+    _fields_ = [("c_off", C.c_void_p), ("c_ts", C.c_void_p), ("c_kv", C.c_void_p), ("kv_key", C.c_void_p),
+                ("kv_val", C.c_void_p)]
+
+
 class crdt_population_init(C.Structure):
     _fields_ = [("replicas", C.c_uint32), ("keys_per_replica", C.c_uint32), ("first", C.c_uint64),
                 ("n_str", C.c_uint64), ("l_off", C.c_void_p), ("l_ts", C.c_void_p), ("l_origin", C.c_void_p),
@@ -265,6 +270,7 @@ SIGNATURES = {
     "crdt_population_read": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "crdt_population_round": (_I, [_P, _P]),
     "crdt_population_undo": (_I, [_P]),
+    "crdt_population_add_commands": (_I, [_P, C.POINTER(crdt_population_cmds), _P]),
     "crdt_population_round_sharded": (_I, [_P, C.POINTER(_P), _P, _U64]),
     "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
     "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),

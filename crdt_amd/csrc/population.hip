@@ -444,6 +444,150 @@ extern "C" int crdt_population_destroy(crdt_population *pop) {
     return CRDT_OK;
 }
 
+// POST /data on every replica at once (AddCommand, main.go:173-215) through
+// crdt_local_apply: the commands (host arrays, arrival order per replica) in
+// one upload, the next Diffs and CurrentState into the spare buffers (the
+// state copied first: the apply updates it in place), the new Diffs' kv
+// pairs gathered from the old Diffs' and the commands' (by src, the entry
+// count read on the device), one read-back of the bounds, the status word
+// and every command's HTTP status.  More than kLaMax commands for one
+// replica run as several chunks, each the next kLaMax of every replica's.
+namespace crdt {
+namespace {
+constexpr uint64_t kLaMax = 4096;        // crdt_local_apply: commands per replica per call
+
+int pop_apply_chunk(crdt_population *pop, const crdt_population_cmds &c, const std::vector<uint64_t> &idx,
+                    const std::vector<uint64_t> &sub_off, uint16_t *status) {
+    crdt_ctx *ctx = pop->ctx;
+    const uint32_t P = pop->P;
+    const size_t n_c = idx.size();
+    // the chunk's commands, packed: c_off P+1 | c_ts n_c | c_kv n_c+1 (u64), kv_key | kv_val (u32)
+    std::vector<uint64_t> kv_off(n_c + 1, 0);
+    for (size_t j = 0; j < n_c; ++j) kv_off[j + 1] = kv_off[j] + (c.c_kv[idx[j] + 1] - c.c_kv[idx[j]]);
+    const size_t n_kvc = kv_off[n_c];
+    const size_t bytes = Carve::round((P + 1) * 8) + Carve::round(n_c * 8 + 8) + Carve::round((n_c + 1) * 8) +
+                         Carve::round(n_kvc * 4 + 4) * 2 + Carve::round(n_c * 2 + 2) + round_bytes(P) + 1024;
+    int rc = dev_grow(ctx, &pop->xb, &pop->xb_bytes, bytes);
+    if (!rc) rc = pin_grow(pop, bytes);
+    if (rc) return rc;
+    Carve w(pop->xb), hw(pop->pin);
+    uint64_t *d_off = w.take<uint64_t>(P + 1), *h_off = hw.take<uint64_t>(P + 1);
+    int64_t *d_ts = w.take<int64_t>(n_c + 1), *h_ts = hw.take<int64_t>(n_c + 1);
+    uint64_t *d_kv = w.take<uint64_t>(n_c + 1), *h_kv = hw.take<uint64_t>(n_c + 1);
+    uint32_t *d_key = w.take<uint32_t>(n_kvc + 1), *h_key = hw.take<uint32_t>(n_kvc + 1);
+    uint32_t *d_val = w.take<uint32_t>(n_kvc + 1), *h_val = hw.take<uint32_t>(n_kvc + 1);
+    uint16_t *d_st = w.take<uint16_t>(n_c + 1), *h_st = hw.take<uint16_t>(n_c + 1);
+    uint64_t *d_bounds = w.take<uint64_t>(2 * P + 4), *h_bounds = hw.take<uint64_t>(2 * P + 4);
+    std::copy(sub_off.begin(), sub_off.end(), h_off);
+    std::copy(kv_off.begin(), kv_off.end(), h_kv);
+    for (size_t j = 0; j < n_c; ++j) {
+        h_ts[j] = c.c_ts[idx[j]];
+        const uint64_t a = c.c_kv[idx[j]], b = c.c_kv[idx[j] + 1];
+        std::copy(c.kv_key + a, c.kv_key + b, h_key + kv_off[j]);
+        std::copy(c.kv_val + a, c.kv_val + b, h_val + kv_off[j]);
+    }
+    const size_t upto = (size_t)((char *)(h_val + n_kvc + 1) - (char *)pop->pin);
+    hipError_t e = hipMemcpyAsync(pop->xb, pop->pin, upto, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_bounds + 2 * P + 3, ctx->dev_status, 8, hipMemcpyDeviceToDevice, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    auto &nd = pop->d[1 - pop->cur];
+    rc = diff_reserve(pop, nd, pop->n_e + n_c, pop->n_kv + n_kvc, false);
+    if (rc) return rc;
+    auto &cd = pop->d[pop->cur];
+    const int so = pop->cur, sn = 1 - pop->cur;
+    const uint64_t ns = (uint64_t)P * pop->K;
+    if (ns) {
+        e = hipMemcpyAsync(pop->st_kind[sn], pop->st_kind[so], ns, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(pop->st_str[sn], pop->st_str[so], ns * 4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(pop->st_sum[sn], pop->st_sum[so], ns * 8, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
+    crdt_local_in in{};
+    in.replicas = P;
+    in.n_slots = (uint32_t)ns;
+    in.n_l = pop->n_e;
+    in.n_c = n_c;
+    in.n_kv = n_kvc;
+    in.n_str = pop->n_str;
+    in.l_off = cd.off;
+    in.l_ts = cd.ts;
+    in.l_origin = cd.origin;
+    in.c_off = d_off;
+    in.c_ts = d_ts;
+    in.c_kv = d_kv;
+    in.kv_key = d_key;
+    in.kv_val = d_val;
+    in.str_bytes = pop->str_bytes;
+    in.str_off = pop->str_off;
+    const crdt_local_out out{nd.off, nd.ts, nd.origin, nd.src, d_st, pop->st_kind[sn], pop->st_str[sn], pop->st_sum[sn]};
+    rc = crdt_local_apply(ctx, &in, &out);
+    if (rc) return rc;
+    // the new Diffs' kv pairs: an entry's from the old Diff (src >= 0) or its command (src < 0)
+    rc = seg_gather2_dev_count(ctx, pop->n_e + n_c, nd.off + P, nd.src, cd.kv_off, d_kv, nd.kv_off, cd.kv_key, d_key,
+                               nd.kv_key, cd.kv_val, d_val, nd.kv_val);
+    if (rc) return rc;
+    k_pop_bounds<<<grid_for(P + 1, 256, 64), 256, 0, ctx->stream>>>(nd.off, nd.kv_off, P, ctx->dev_status, d_bounds);
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    e = hipMemcpyAsync(h_bounds, d_bounds, (2 * P + 4) * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && n_c) e = hipMemcpyAsync(h_st, d_st, n_c * 2, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    const uint32_t after = (uint32_t)h_bounds[2 * P + 2], before = (uint32_t)h_bounds[2 * P + 3];
+    if (after & ~before) return CRDT_E_DEVICE;           // nothing swapped in
+    for (size_t j = 0; j < n_c; ++j) status[idx[j]] = h_st[j];
+    for (uint32_t p = 0; p < P; ++p) {
+        pop->cnt[p] = h_bounds[p + 1] - h_bounds[p];
+        pop->kvcnt[p] = h_bounds[P + 2 + p] - h_bounds[P + 1 + p];
+    }
+    pop->n_e = h_bounds[P];
+    pop->n_kv = h_bounds[2 * P + 1];
+    pop->cur = 1 - pop->cur;
+    pop->can_undo = false;                               // (undo is a round's)
+    return CRDT_OK;
+}
+
+}  // namespace
+}  // namespace crdt
+
+extern "C" int crdt_population_add_commands(crdt_population *pop, const crdt_population_cmds *c, uint16_t *status) {
+    if (!pop_valid(pop) || !c || !c->c_off) return CRDT_E_INVAL;
+    int rc = bind(pop->ctx);
+    if (rc) return rc;
+    const uint32_t P = pop->P;
+    if (c->c_off[0] != 0) return CRDT_E_INVAL;
+    for (uint32_t p = 0; p < P; ++p)
+        if (c->c_off[p + 1] < c->c_off[p]) return CRDT_E_INVAL;
+    const uint64_t n_c = c->c_off[P];
+    if (n_c == 0) return CRDT_OK;
+    if (!c->c_ts || !c->c_kv || !status || c->c_kv[0] != 0) return CRDT_E_INVAL;
+    for (uint64_t j = 0; j < n_c; ++j)
+        if (c->c_kv[j + 1] < c->c_kv[j]) return CRDT_E_INVAL;
+    if (c->c_kv[n_c] && (!c->kv_key || !c->kv_val)) return CRDT_E_INVAL;
+    for (uint64_t q = 0; q < c->c_kv[n_c]; ++q)          // slots of the replica's own range (checked per command below)
+        if (c->kv_val[q] >= pop->n_str) return CRDT_E_INVAL;
+    for (uint32_t p = 0; p < P; ++p)
+        for (uint64_t j = c->c_off[p]; j < c->c_off[p + 1]; ++j)
+            for (uint64_t q = c->c_kv[j]; q < c->c_kv[j + 1]; ++q)
+                if (c->kv_key[q] < (uint64_t)p * pop->K || c->kv_key[q] >= (uint64_t)(p + 1) * pop->K)
+                    return CRDT_E_INVAL;
+    uint64_t most = 0;
+    for (uint32_t p = 0; p < P; ++p) most = std::max(most, c->c_off[p + 1] - c->c_off[p]);
+    for (uint64_t r = 0; r * kLaMax < most; ++r) {       // chunk r: the commands r*kLaMax .. of every replica
+        std::vector<uint64_t> idx, sub_off(P + 1, 0);
+        for (uint32_t p = 0; p < P; ++p) {
+            const uint64_t a = std::min(c->c_off[p] + r * kLaMax, c->c_off[p + 1]);
+            const uint64_t b = std::min(a + kLaMax, c->c_off[p + 1]);
+            for (uint64_t j = a; j < b; ++j) idx.push_back(j);
+            sub_off[p + 1] = idx.size();
+        }
+        rc = pop_apply_chunk(pop, *c, idx, sub_off, status);
+        if (rc) return rc;
+    }
+    return CRDT_OK;
+}
+
 // Undo the last round: the Diffs and CurrentState as they were before it
 // (still in the spare buffers; valid once, until the next round).
 extern "C" int crdt_population_undo(crdt_population *pop) {

@@ -673,6 +673,23 @@ class NativePopulation:
         _lib.call("crdt_population_info", self._h, C.byref(P), C.byref(n_e), C.byref(n_kv))
         return P.value, n_e.value, n_kv.value
 
+    def add_commands(self, host_cmds: dict) -> np.ndarray:
+        """POST /data on every replica at once (AddCommand, main.go:173-215;
+        crdt_population_add_commands): host_cmds = {off (P+1), ts, kv_off,
+        kv_key (local slot ids), kv_val}, commands in arrival order per
+        replica.  Returns every command's HTTP status (200 / 500)."""
+        from . import _lib
+        from ._lib import crdt_population_cmds
+        a = lambda x, dt: np.ascontiguousarray(np.asarray(x).astype(dt))
+        keep = [a(host_cmds["off"], np.uint64), a(host_cmds["ts"], np.int64), a(host_cmds["kv_off"], np.uint64),
+                a(np.asarray(host_cmds["kv_key"]).astype(np.uint32), np.uint32),
+                a(np.asarray(host_cmds["kv_val"]).astype(np.uint32), np.uint32)]
+        ptr = lambda x: x.ctypes.data if x.size else None
+        cmds = crdt_population_cmds(*[ptr(x) for x in keep])
+        status = np.zeros(max(len(keep[1]), 1), np.uint16)
+        _lib.call("crdt_population_add_commands", self._h, C.byref(cmds), status.ctypes.data, ctx=self._ctx)
+        return status[:len(keep[1])].astype(np.int64)
+
     def undo(self) -> None:
         """Back to the Diffs and CurrentState before the last round."""
         from . import _lib

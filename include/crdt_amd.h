@@ -588,6 +588,23 @@ int crdt_population_read(crdt_population *pop, uint64_t *l_off, int64_t *ts, uin
  * peers' Diffs in place (crdt_refmerge_batch_pull, key slots re-based, kv
  * pairs from its own passes); one upload, one read-back.  Synchronises. */
 int crdt_population_round(crdt_population *pop, const int64_t *peers);
+/* POST /data on every replica at once (AddCommand, main.go:173-215, through
+ * crdt_local_apply): replica p's commands c_off[p] .. c_off[p+1] in ARRIVAL
+ * order (host arrays), command j = (c_ts[j], pairs [c_kv[j], c_kv[j+1]) of
+ * kv_key (local slot ids of replica p's range) / kv_val (string ids of the
+ * population's arena)).  Diff.Put of the *Command (an equal ts replaced,
+ * main.go:187), then the CurrentState apply with the early return after a
+ * new key and the 500 on an unparsable value (main.go:188-207);
+ * status[j] = 200 / 500.  Any number of commands per replica (chunks of
+ * 4096 per device call).  Synchronises. */
+typedef struct crdt_population_cmds {
+    const uint64_t *c_off;      /* [replicas + 1] */
+    const int64_t *c_ts;        /* [n_c] */
+    const uint64_t *c_kv;       /* [n_c + 1], c_kv[0] = 0 */
+    const uint32_t *kv_key;
+    const uint32_t *kv_val;
+} crdt_population_cmds;
+int crdt_population_add_commands(crdt_population *pop, const crdt_population_cmds *cmds, uint16_t *status);
 /* Undo the last round (local or sharded): the Diffs and CurrentState as they
  * were before it -- they stay in the population's spare buffers until the
  * next round; CRDT_E_INVAL when there is nothing to undo. */

@@ -154,3 +154,62 @@ def test_population_undo_restores_the_previous_round(eng):
             np.testing.assert_array_equal(again[k], after[k], err_msg=k)
     finally:
         pop.close()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_population_commands_and_rounds(eng, seed):
+    """AddCommand on every replica through crdt_population_add_commands
+    (main.go:173-215: same-ms replaces, early return after a new key, 500 on
+    an unparsable value) between reference-drawn rounds == pyref: statuses,
+    Diffs and CurrentState."""
+    from test_gpu_local_apply import _cmd_block
+    rng = np.random.default_rng(seed)
+    P = 8
+    diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 30))) for i in range(P)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    try:
+        for rnd in range(5):
+            cmds, exp = [], []
+            for i in range(P):
+                t0 = max(diffs[i]) if diffs[i] else 1_000
+                mine = [(t0 + int(rng.integers(-3, 6)), {KEYS[int(rng.integers(0, K))]: STRS[int(rng.integers(0, 12))]})
+                        for _ in range(int(rng.integers(0, 4)))]
+                exp += [pyref.add_command(diffs[i], states[i], t, d) for t, d in mine]
+                cmds.append(mine)
+            np.testing.assert_array_equal(pop.add_commands(_cmd_block(cmds)), exp)
+            h = pop.read()
+            _same_diffs(_unpack_native(h, P), diffs)
+            assert _state_native(h, P) == states, f"after commands, round {rnd}"
+            peers = gossip.reference_peers(rng, P, 0, P)
+            pop.round(peers)
+            diffs, states = _host_round(diffs, peers, states)
+            h = pop.read()
+            _same_diffs(_unpack_native(h, P), diffs)
+            assert _state_native(h, P) == states, f"round {rnd}"
+    finally:
+        pop.close()
+
+
+def test_population_commands_over_the_per_call_limit(eng):
+    """5000 commands on one replica (past crdt_local_apply's 4096 per call):
+    chunked in arrival order == pyref."""
+    from test_gpu_local_apply import _cmd_block
+    rng = np.random.default_rng(12)
+    P = 3
+    diffs = [_rand_diff(rng, 100 + i, 3) for i in range(P)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    try:
+        cmds, exp = [], []
+        for i in range(P):
+            n = 5000 if i == 1 else 7
+            mine = [(10_000 + j // 2, {KEYS[int(rng.integers(0, K))]: STRS[int(rng.integers(0, 10))]}) for j in range(n)]
+            exp += [pyref.add_command(diffs[i], states[i], t, d) for t, d in mine]
+            cmds.append(mine)
+        np.testing.assert_array_equal(pop.add_commands(_cmd_block(cmds)), exp)
+        h = pop.read()
+        _same_diffs(_unpack_native(h, P), diffs)
+        assert _state_native(h, P) == states
+    finally:
+        pop.close()
