@@ -22,6 +22,8 @@ int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within 
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
+int g_dec_small = 1;
+int g_rm_kvx = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_rdd_diag = 0;
@@ -146,6 +148,7 @@ extern "C" int crdt_ctx_create(int device, void *stream, crdt_ctx **out) {
         if (ctx->dev_status) (void)hipFree(ctx->dev_status);
     server_ctx_release(ctx);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->hio) (void)hipHostFree(ctx->hio);
     (void)crdt_strtab_destroy(ctx->keys);
     (void)crdt_strtab_destroy(ctx->vals);
         delete ctx;
@@ -188,6 +191,7 @@ extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
     if (ctx->dev_status) (void)hipFree(ctx->dev_status);
     server_ctx_release(ctx);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->hio) (void)hipHostFree(ctx->hio);
     (void)crdt_strtab_destroy(ctx->keys);
     (void)crdt_strtab_destroy(ctx->vals);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
@@ -315,6 +319,12 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.or_parts")) {     // OR-Set write-pass workgroups per 2048-item tile
         if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
         g_or_parts = (int)v;
+    } else if (!strcmp(name, "refmerge.kv_one_launch")) {   // kv tile pass: both tile kinds in one launch at any grid
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_rm_kvx = (int)v;
+    } else if (!strcmp(name, "codec.small")) {   // gossip decode of few small bodies in one pass: 0 off, 1 auto, 2 always
+        if (v < 0 || v > 2) return CRDT_E_INVAL;
+        g_dec_small = (int)v;
     } else if (!strcmp(name, "refmerge.count_dma")) {   // RefMerge count pass: ts runs staged by LDS-DMA
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_rm_count_dma = (int)v;

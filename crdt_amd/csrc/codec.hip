@@ -24,6 +24,7 @@
 // the host decodes those (crdt_server_ingest_binary), as the reference would.
 #include <string.h>
 
+#include <functional>
 #include <vector>
 
 #include "scan.hpp"
@@ -159,13 +160,18 @@ __device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, ui
 }
 
 // ---------------------------------------------------------------- bodies
-struct BodyDesc {                  // one pulled body, concatenated in one device buffer
-    uint64_t data;                 // byte offset of the body
+struct BodyDesc {                  // one pulled body
+    uint64_t data;                 // its address minus DecodeCtx::data (mod 2^64: bodies may sit in separate buffers)
     uint64_t e0, q0;               // first global entry / pair of the body
     uint64_t ne, np, nb;
     uint32_t slot_base;
     uint32_t pad;
+    uint64_t y0;                   // the body's first byte in the pair-byte scan (boff): header n_bytes before it
 };
+
+__device__ __forceinline__ const uint8_t *body_ptr(const uint8_t *data, uint64_t at) {
+    return (const uint8_t *)((uintptr_t)data + at);
+}
 
 __device__ __forceinline__ uint32_t find_body(const BodyDesc *b, uint32_t nbody, uint64_t x, bool pairs) {
     uint32_t lo = 0, hi = nbody;                     // last body whose first item <= x
@@ -190,7 +196,7 @@ struct DecodeCtx {
     __device__ void pair_bytes(uint64_t j, const uint8_t **kp, uint32_t *kn, const uint8_t **vp, uint32_t *vn) const {
         const uint32_t b = find_body(bd, nbody, j, true);
         const BodyDesc d = bd[b];
-        const uint8_t *region = data + d.data + 32 + 12 * d.ne + 8 * d.np;
+        const uint8_t *region = body_ptr(data, d.data) + 32 + 12 * d.ne + 8 * d.np;
         const uint64_t o = boff[j] - boff[d.q0];
         const uint64_t k = klen[j], v = boff[j + 1] - boff[j] - k;
         if (o > d.nb || k > d.nb - o || v > d.nb - o - k) {
@@ -207,13 +213,17 @@ struct DecodeCtx {
 };
 
 constexpr uint32_t kChunk = 1024;  // items per workgroup of the body-major grids (grid.y = body)
+// pairs per workgroup of the claim pass: one per thread -- each pair's two
+// table claims are a chain of dependent memory-side atomics and string
+// compares, so pairs run side by side, not four deep per thread
+constexpr uint32_t kClaimChunk = 256;
 
 // per entry: ts, pair count; ts must ascend strictly within a body, no nil map
 __global__ __launch_bounds__(256) void k_dec_entries(DecodeCtx c, int64_t *__restrict__ r_ts,
                                                      uint32_t *__restrict__ cnt) {
     const uint32_t b = blockIdx.y;
     const BodyDesc d = c.bd[b];
-    const uint8_t *base = c.data + d.data + 32;
+    const uint8_t *base = body_ptr(c.data, d.data) + 32;
     bool host = false;
     for (uint64_t i = (uint64_t)blockIdx.x * kChunk + threadIdx.x; i < d.ne && i < (uint64_t)(blockIdx.x + 1) * kChunk;
          i += 256) {
@@ -233,10 +243,10 @@ __global__ __launch_bounds__(256) void k_dec_entries(DecodeCtx c, int64_t *__res
 
 // per pair: klen and klen + vlen (u32; an overflow marks the body malformed)
 __global__ __launch_bounds__(256) void k_dec_pairs(DecodeCtx c, uint32_t *__restrict__ klen,
-                                                   uint32_t *__restrict__ plen) {
+                                                   uint32_t *__restrict__ plen, uint8_t *__restrict__ first) {
     const uint32_t b = blockIdx.y;
     const BodyDesc d = c.bd[b];
-    const uint8_t *base = c.data + d.data + 32 + 12 * d.ne;
+    const uint8_t *base = body_ptr(c.data, d.data) + 32 + 12 * d.ne;
     for (uint64_t q = (uint64_t)blockIdx.x * kChunk + threadIdx.x; q < d.np && q < (uint64_t)(blockIdx.x + 1) * kChunk;
          q += 256) {
         const uint32_t kl = le32(base + 4 * q), vl = le32(base + 4 * d.np + 4 * q);
@@ -244,7 +254,163 @@ __global__ __launch_bounds__(256) void k_dec_pairs(DecodeCtx c, uint32_t *__rest
         if (t > 0xFFFFFFFFull) atomicOr(&c.flag[b], kBodyMalformed);
         klen[d.q0 + q] = kl;
         plen[d.q0 + q] = t > 0xFFFFFFFFull ? 0u : (uint32_t)t;
+        first[d.q0 + q] = 0;                              // (k_dec_kv marks the entries' first pairs)
     }
+}
+
+// ---- the decode of a few small bodies in one pass (gossip_decode_at picks it
+// when every body fits kSmallItems entries and pairs): two 1024-thread
+// workgroups per body, one for its pairs (k_dec_pairs and the byte scan) and
+// one for its entries (k_dec_entries, the count scan, k_dec_kv, the `first`
+// marks), each checking its half of k_dec_bodies.  The scans are body-local:
+// r_kv and `first` are relative to the body's first pair, and boff is the
+// body's own scan based at y0 (the header byte counts of the bodies before
+// it; a body whose real lengths disagree with its header is flagged and
+// claims nothing, so its boundary slot -- written by both neighbours with the
+// same value -- never matters).  Eight launches and their host calls fewer
+// for the Server.merge() shapes; large batches keep the multi-pass form.
+constexpr int kSmallT = 1024, kSmallR = 8;
+constexpr uint64_t kSmallItems = 1u << 18;
+
+__device__ __forceinline__ uint64_t block1024_exclusive_scan(uint64_t v, uint64_t *total, uint64_t *wsum) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint64_t off = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSmallT / 64; ++k) {
+        const uint64_t s = wsum[k];
+        off += k < w ? s : 0;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + x - v;
+}
+
+template <bool AL>
+__device__ __forceinline__ void dec_small(DecodeCtx c, int64_t *__restrict__ r_ts,
+                                                       uint32_t *__restrict__ klen, uint64_t *__restrict__ boff,
+                                                       uint8_t *__restrict__ first, uint64_t n_e, uint64_t n_p,
+                                                       uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                                       uint64_t *__restrict__ r_off, const BodyDesc &d,
+                                                       uint64_t *wsum, uint32_t b, bool entries) {
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0 && entries) {
+        r_off[b] = d.e0;                                 // (the multi-pass form uploads these)
+        if (b == 0) {
+            r_off[c.nbody] = n_e;
+            r_kv[n_e] = kv_base + n_p;
+        }
+    }
+    const uint8_t *base = body_ptr(c.data, d.data) + 32;
+    auto ld32 = [&](const uint8_t *p) { return AL ? *(const uint32_t *)p : le32(p); };
+    auto ld64 = [&](const uint8_t *p) { return AL ? *(const uint64_t *)p : le64(p); };
+    bool bad = false, host = false;
+    uint64_t carry = 0;
+    if (!entries) {
+    // pairs: klen and the scan of klen + vlen into boff.  Each
+    // thread takes kSmallR consecutive items of a chunk (its own prefix in
+    // registers): one workgroup scan per chunk of kSmallT * kSmallR items
+    const uint8_t *pk = base + 12 * d.ne, *pv = pk + 4 * d.np;
+    for (uint64_t c0 = 0; c0 < d.np; c0 += (uint64_t)kSmallT * kSmallR) {
+        const uint64_t i0 = c0 + (uint64_t)tid * kSmallR;
+        uint32_t t[kSmallR];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            const uint64_t q = i0 + r;
+            t[r] = 0;
+            if (q < d.np) {
+                const uint32_t kl = ld32(pk + 4 * q), vl = ld32(pv + 4 * q);
+                const uint64_t x = (uint64_t)kl + vl;
+                if (x > 0xFFFFFFFFull) bad = true;
+                else t[r] = (uint32_t)x;
+                klen[d.q0 + q] = kl;
+            }
+            sum += t[r];
+        }
+        uint64_t tot;
+        uint64_t run = carry + block1024_exclusive_scan(sum, &tot, wsum);
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            if (i0 + r < d.np) boff[d.q0 + i0 + r] = d.y0 + run;
+            run += t[r];
+        }
+        carry += tot;
+    }
+    if (carry != d.nb) bad = true;
+    if (tid == 0) boff[d.q0 + d.np] = d.y0 + d.nb;
+    } else {
+    // entries: ts, pair counts (nil map / not ascending: the host path), the
+    // body-local scan of the counts into r_kv and `first` of every pair (1
+    // on an entry's first pair; pairs no entry covers only occur in a body
+    // whose counts disagree with its header, flagged here: it claims nothing)
+    for (uint64_t c0 = 0; c0 < d.ne; c0 += (uint64_t)kSmallT * kSmallR) {
+        const uint64_t i0 = c0 + (uint64_t)tid * kSmallR;
+        uint32_t k[kSmallR];
+        uint64_t sum = 0;
+        int64_t prev = i0 && i0 < d.ne ? (int64_t)ld64(base + 8 * (i0 - 1)) : 0;
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            const uint64_t i = i0 + r;
+            k[r] = 0;
+            if (i < d.ne) {
+                const int64_t ts = (int64_t)ld64(base + 8 * i);
+                uint32_t kk = ld32(base + 8 * d.ne + 4 * i);
+                if (kk == kNilPairs) {
+                    host = true;
+                    kk = 0;
+                }
+                if (i && prev >= ts) host = true;
+                prev = ts;
+                r_ts[d.e0 + i] = ts;
+                k[r] = kk;
+            }
+            sum += k[r];
+        }
+        uint64_t tot;
+        uint64_t run = carry + block1024_exclusive_scan(sum, &tot, wsum);
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            const uint64_t i = i0 + r;
+            if (i < d.ne) {
+                r_kv[d.e0 + i] = kv_base + d.q0 + run;
+                for (uint32_t j = 0; j < k[r] && run + j < d.np; ++j) first[d.q0 + run + j] = j == 0;
+            }
+            run += k[r];
+        }
+        carry += tot;
+    }
+    if (carry != d.np) bad = true;
+    }
+    const uint32_t fl = (bad ? kBodyMalformed : 0u) | (host ? kBodyHost : 0u);
+    uint32_t wfl = fl;
+    for (int m = 32; m >= 1; m >>= 1) wfl |= __shfl_xor(wfl, m, 64);
+    if ((tid & 63) == 0 && wfl) atomicOr(&c.flag[b], wfl);
+}
+
+__global__ __launch_bounds__(kSmallT) void k_dec_small(DecodeCtx c, int64_t *__restrict__ r_ts,
+                                                       uint32_t *__restrict__ klen, uint64_t *__restrict__ boff,
+                                                       uint8_t *__restrict__ first, uint64_t n_e, uint64_t n_p,
+                                                       uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                                       uint64_t *__restrict__ r_off) {
+    __shared__ uint64_t wsum[kSmallT / 64];
+    const uint32_t b = blockIdx.x >> 1;                  // two workgroups per body: its pairs, its entries
+    const bool entries = blockIdx.x & 1;
+    const BodyDesc d = c.bd[b];
+    // word loads for a body at an 8-byte aligned address (every body the
+    // Server path uploads), byte loads otherwise
+    if ((((uintptr_t)body_ptr(c.data, d.data)) & 7) == 0)
+        dec_small<true>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, d, wsum, b, entries);
+    else
+        dec_small<false>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, d, wsum, b, entries);
 }
 
 struct CountSrc32 {
@@ -314,7 +480,7 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
                                                    uint32_t *__restrict__ kv_val, unsigned long long *__restrict__ ctr) {
     const uint32_t b = blockIdx.y;
     const BodyDesc d = c.bd[b];
-    const uint8_t *region = c.data + d.data + 32 + 12 * d.ne + 8 * d.np;
+    const uint8_t *region = body_ptr(c.data, d.data) + 32 + 12 * d.ne + 8 * d.np;
     const uint64_t o0 = c.boff[d.q0];
     // a body the earlier passes already rejected (flag0: their flags, which
     // this pass only reads -- its own go to cflag) claims no table entries:
@@ -322,8 +488,8 @@ __global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabV
     const bool rejected = flag0[b] != 0;
     bool host = false, bad = false, full = false;
     uint32_t nk = 0, nv = 0;
-    for (uint64_t q = (uint64_t)blockIdx.x * kChunk + threadIdx.x; q < d.np && q < (uint64_t)(blockIdx.x + 1) * kChunk;
-         q += 256) {
+    for (uint64_t q = (uint64_t)blockIdx.x * kClaimChunk + threadIdx.x;
+         q < d.np && q < (uint64_t)(blockIdx.x + 1) * kClaimChunk; q += 256) {
         const uint64_t j = d.q0 + q;
         if (rejected) {
             kslot[j] = vslot[j] = kEmptyE32;
@@ -439,8 +605,11 @@ __global__ void k_dec_assign(DecodeCtx c, TabView t, bool value, const uint32_t 
 }
 
 __global__ void k_off_end(uint64_t *__restrict__ off, const uint64_t *__restrict__ n_new_dev,
-                          const uint64_t *__restrict__ bytes_new_dev, uint64_t n_old, uint64_t bytes_old) {
+                          const uint64_t *__restrict__ bytes_new_dev, uint64_t n_old, uint64_t bytes_old,
+                          unsigned long long *__restrict__ sizes) {
     off[n_old + *n_new_dev] = bytes_old + *bytes_new_dev;
+    sizes[0] = *n_new_dev;                            // (read back with the flags in one copy)
+    sizes[1] = *bytes_new_dev;
 }
 
 // pass C: ids of the pairs whose string was new in this call
@@ -475,12 +644,13 @@ __global__ void k_rehash(uint64_t *__restrict__ tab, uint64_t mask, const uint8_
 }
 
 // hdr[32 b ..] = the first 32 bytes of body b (zeros if shorter)
-__global__ void k_gather_headers(const uint8_t *__restrict__ data, const uint64_t *__restrict__ off, uint32_t nb,
-                                 uint8_t *__restrict__ hdr) {
+__global__ void k_gather_headers(const uint8_t *__restrict__ data, const uint64_t *__restrict__ at,
+                                 const uint64_t *__restrict__ len, uint32_t nb, uint8_t *__restrict__ hdr) {
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
     if (b >= nb) return;
-    const bool ok = off[b + 1] - off[b] >= 32;
-    for (int i = 0; i < 32; ++i) hdr[32 * (size_t)b + i] = ok ? data[off[b] + i] : 0;
+    const bool ok = len[b] >= 32;
+    const uint8_t *p = body_ptr(data, at[b]);
+    for (int i = 0; i < 32; ++i) hdr[32 * (size_t)b + i] = ok ? p[i] : 0;
 }
 
 uint64_t pow2_at_least(uint64_t x) {
@@ -622,60 +792,80 @@ extern "C" int crdt_strtab_get(const crdt_strtab *t, uint64_t id, const char **p
     return CRDT_OK;
 }
 
-extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, crdt_strtab *keys,
-                                  crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status) {
-    int rc = bind(ctx);
-    if (rc) return rc;
-    if (!in || !keys || !vals || !out || !body_status) return CRDT_E_INVAL;
-    if (keys->device != ctx->device || vals->device != ctx->device) return CRDT_E_INVAL;
-    const uint32_t nb = in->n_bodies;
-    if (nb == 0) return CRDT_OK;
-    if (!in->data || !in->body_off || !in->slot_base || !out->r_off) return CRDT_E_INVAL;
+namespace crdt {
+static size_t decode_ws_need(uint32_t nb, uint64_t n_e, uint64_t n_p) {
+    const size_t head = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 8) + 64;
+    return Carve::round(head) + Carve::round((n_e + 1) * 4) + Carve::round((n_e + 1) * 8) +
+           Carve::round(n_p * 4 + 4) * 4 + Carve::round((n_p + 1) * 8) * 5 + Carve::round(n_p + 1) +
+           scan_lb_tmp_bytes(std::max(n_p, n_e)) + 4096;
+}
+
+size_t gossip_decode_scratch_bytes(uint32_t nb, uint64_t n_e, uint64_t n_p) { return decode_ws_need(nb, n_e, n_p); }
+
+// The decode of nb bodies at data + at[b] (mod 2^64), len[b] bytes each.  Small
+// uploads and read-backs go through the context's pinned staging (ctx->hio):
+// one upload of the body table with the zeroed flags and counters, one
+// read-back of flags + counters per host synchronisation.
+//   spec (optional): work that consumes the decode's output, enqueued right
+//   behind the claim pass's read-back so that it runs before the host has
+//   even looked at the claims (the common case: every string already
+//   interned, nothing left to do); when new strings did arrive, their ids are
+//   written afterwards and *spec_stale says spec ran on incomplete ids.  The
+//   decode then works in `scratch` (>= gossip_decode_scratch_bytes), not in
+//   ctx->ws, which spec's own passes use.  Without scratch, spec runs after
+//   the whole decode.  Either way it has completed when this returns.
+int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
+                     uint32_t key_cap, uint64_t kv_base, const uint32_t *slot_base, const uint8_t *host_hdr,
+                     crdt_strtab *keys, crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status,
+                     const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale) {
+    if (spec_stale) *spec_stale = false;
     const hipStream_t s = ctx->stream;
+    int rc;
+    hipError_t e;
     // headers (32 B per body) to the host in one gather + one copy: the sizes
     // the decode is planned with
-    for (uint32_t b = 0; b < nb; ++b)
-        if (in->body_off[b + 1] < in->body_off[b]) return CRDT_E_INVAL;
-    std::vector<uint8_t> hdr_buf;
-    const uint8_t *hdr = in->host_hdr;
-    hipError_t e;
+    const uint8_t *hdr = host_hdr;
     if (!hdr) {
-        hdr_buf.assign(32 * (size_t)nb, 0);
-        rc = ws_reserve(ctx, Carve::round((nb + 1) * 8) + Carve::round(32 * (size_t)nb) + 512);
+        rc = ws_reserve(ctx, Carve::round(nb * 16) + Carve::round(32 * (size_t)nb) + 512);
+        if (!rc) rc = hio_reserve(ctx, (size_t)nb * 16 + 32 * (size_t)nb);
         if (rc) return rc;
         Carve w0(ctx->ws);
-        uint64_t *d_off = w0.take<uint64_t>(nb + 1);
+        uint64_t *d_al = w0.take<uint64_t>(2 * (size_t)nb);
         uint8_t *d_hdr = w0.take<uint8_t>(32 * (size_t)nb);
-        e = hipMemcpyAsync(d_off, in->body_off, (nb + 1) * 8, hipMemcpyHostToDevice, s);
+        uint64_t *h_al = (uint64_t *)ctx->hio;
+        memcpy(h_al, at, nb * 8);
+        memcpy(h_al + nb, len, nb * 8);
+        e = hipMemcpyAsync(d_al, h_al, nb * 16, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return hip_fail(ctx, e);
-        k_gather_headers<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(in->data, d_off, nb, d_hdr);
+        k_gather_headers<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(data, d_al, d_al + nb, nb, d_hdr);
         rc = check_launch(ctx);
         if (rc) return rc;
-        e = hipMemcpyAsync(hdr_buf.data(), d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
+        uint8_t *h_hdr = (uint8_t *)ctx->hio + (size_t)nb * 16;
+        e = hipMemcpyAsync(h_hdr, d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(ctx, e);
-        hdr = hdr_buf.data();
+        hdr = h_hdr;
     }
     std::vector<BodyDesc> bd(nb);
     std::vector<uint64_t> r_off(nb + 1, 0);
     uint64_t n_e = 0, n_p = 0, n_b = 0;
     static const char magic[8] = {'C', 'R', 'D', 'T', 'S', 'O', 'A', '1'};
     for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t len = in->body_off[b + 1] - in->body_off[b];
         const uint8_t *h = &hdr[32 * b];
         uint64_t ne = 0, np = 0, nby = 0;
         body_status[b] = 0;
-        if (len < 32 || memcmp(h, magic, 8) != 0) {
+        if (len[b] < 32 || memcmp(h, magic, 8) != 0) {
             body_status[b] = kBodyMalformed;
         } else {
             memcpy(&ne, h + 8, 8);
             memcpy(&np, h + 16, 8);
             memcpy(&nby, h + 24, 8);
-            if (ne > len / 12 || np > len / 8 || nby > len || 32 + ne * 12 + np * 8 + nby != len || np >= kPend)
+            const uint64_t l = len[b];
+            if (ne > l / 12 || np > l / 8 || nby > l || 32 + ne * 12 + np * 8 + nby != l || np >= kPend)
                 body_status[b] = kBodyMalformed;
         }
         if (body_status[b]) ne = np = nby = 0;           // contributes nothing
-        bd[b] = BodyDesc{in->body_off[b], n_e, n_p, ne, np, nby, in->slot_base[b], 0};
+        bd[b] = BodyDesc{at[b], n_e, n_p, ne, np, nby, slot_base[b], 0, n_b};
         n_e += ne;
         n_p += np;
         n_b += nby;
@@ -686,15 +876,20 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     rc = tab_reserve(ctx, keys, n_p, n_b);
     if (!rc) rc = tab_reserve(ctx, vals, n_p, n_b);
     if (rc) return rc;
-    // workspace
-    const size_t need = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 4) * 2 + Carve::round((n_e + 1) * 4) +
-                        Carve::round((n_e + 1) * 8) + Carve::round(n_p * 4 + 4) * 4 + Carve::round((n_p + 1) * 8) * 5 +
-                        Carve::round(n_p + 1) + scan_lb_tmp_bytes(std::max(n_p, n_e)) + Carve::round(64) + 4096;
-    rc = ws_reserve(ctx, need);
+    // workspace; the head block [body table | flags | counters] is uploaded
+    // from the pinned staging in one copy (flags and counters zeroed there)
+    const size_t bd_bytes = Carve::round(nb * sizeof(BodyDesc)), fl_bytes = Carve::round(nb * 8);
+    const size_t head = bd_bytes + fl_bytes + 64;
+    const size_t need = decode_ws_need(nb, n_e, n_p);
+    const bool early = spec && scratch && scratch_cap >= need;   // spec behind the claims, on scratch
+    rc = early ? CRDT_OK : ws_reserve(ctx, need);
+    if (!rc) rc = hio_reserve(ctx, head + (nb + 1) * 8);
     if (rc) return rc;
-    Carve w(ctx->ws);
-    BodyDesc *d_bd = w.take<BodyDesc>(nb);
-    uint32_t *d_flag = w.take<uint32_t>(2 * nb);          // [0, nb): the other passes, [nb, 2nb): the claim pass
+    Carve w(early ? scratch : ctx->ws);
+    char *d_head = w.take<char>(head);
+    BodyDesc *d_bd = (BodyDesc *)d_head;
+    uint32_t *d_flag = (uint32_t *)(d_head + bd_bytes);   // [0, nb): the other passes, [nb, 2nb): the claim pass
+    unsigned long long *ctr = (unsigned long long *)(d_head + bd_bytes + fl_bytes);   // [0..1] claims, [2..5] sizes
     uint32_t *cnt = w.take<uint32_t>(n_e + 1);
     uint64_t *pre = w.take<uint64_t>(n_e + 1);
     uint32_t *klen = w.take<uint32_t>(n_p + 1);
@@ -707,24 +902,32 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     uint64_t *kboff = w.take<uint64_t>(n_p + 1);
     uint64_t *vboff = w.take<uint64_t>(n_p + 1);
     uint8_t *first = w.take<uint8_t>(n_p + 1);
-    unsigned long long *ctr = w.take<unsigned long long>(8);
     void *tmp = w.take<char>(scan_lb_tmp_bytes(std::max(n_p, n_e)));
-    e = hipMemcpyAsync(d_bd, bd.data(), nb * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, nb * 8, s);
-    if (e == hipSuccess) e = hipMemsetAsync(first, 0, n_p + 1, s);
-    if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, 64, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(out->r_off, r_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    DecodeCtx c{in->data, d_bd, nb, d_flag, boff, klen, n_p};
+    char *h_head = (char *)ctx->hio;
+    memset(h_head, 0, head);
+    memcpy(h_head, bd.data(), nb * sizeof(BodyDesc));
+    uint64_t *h_roff = (uint64_t *)(h_head + head);
+    memcpy(h_roff, r_off.data(), (nb + 1) * 8);
+    DecodeCtx c{data, d_bd, nb, d_flag, boff, klen, n_p};
     uint64_t max_ne = 0, max_np = 0;
     for (auto &x : bd) {
         max_ne = std::max(max_ne, x.ne);
         max_np = std::max(max_np, x.np);
     }
+    const bool small = g_dec_small == 2 || (g_dec_small == 1 && nb <= (uint32_t)ctx->num_cus &&
+                                            max_ne <= kSmallItems && max_np <= kSmallItems);
+    e = hipMemcpyAsync(d_head, h_head, head, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && !small) e = hipMemcpyAsync(out->r_off, h_roff, (nb + 1) * 8, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
     const dim3 ge((unsigned)std::max<uint64_t>((max_ne + kChunk - 1) / kChunk, 1), nb);
     const dim3 gp((unsigned)std::max<uint64_t>((max_np + kChunk - 1) / kChunk, 1), nb);
     const unsigned cap = (unsigned)ctx->num_cus * 8;
-    if (n_e) {
+    if (small) {
+        k_dec_small<<<2 * nb, kSmallT, 0, s>>>(c, out->r_ts, klen, boff, first, n_e, n_p, kv_base, out->r_kv,
+                                           out->r_off);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+    } else if (n_e) {
         k_dec_entries<<<ge, 256, 0, s>>>(c, out->r_ts, cnt);
         rc = check_launch(ctx);
         if (!rc) rc = scan_lb(ctx, CountSrc32{cnt}, NoAct(), n_e, 0, pre, tmp);
@@ -733,68 +936,75 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
         e = hipMemsetAsync(pre, 0, 8, s);
         if (e != hipSuccess) return hip_fail(ctx, e);
     }
-    if (n_p) {
-        k_dec_pairs<<<gp, 256, 0, s>>>(c, klen, plen);
+    if (!small) {
+        if (n_p) {
+            k_dec_pairs<<<gp, 256, 0, s>>>(c, klen, plen, first);
+            rc = check_launch(ctx);
+            if (rc) return rc;
+        }
+        rc = scan_lb(ctx, CountSrc32{plen}, NoAct(), n_p, 0, boff, tmp);
+        if (rc) return rc;
+        k_dec_bodies<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(c, pre);
+        k_dec_kv<<<ge, 256, 0, s>>>(c, pre, n_e, n_p, kv_base, out->r_kv, first);
         rc = check_launch(ctx);
         if (rc) return rc;
     }
-    rc = scan_lb(ctx, CountSrc32{plen}, NoAct(), n_p, 0, boff, tmp);
-    if (rc) return rc;
-    k_dec_bodies<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(c, pre);
-    k_dec_kv<<<ge, 256, 0, s>>>(c, pre, n_e, n_p, in->kv_base, out->r_kv, first);
-    rc = check_launch(ctx);
-    if (rc) return rc;
     const uint64_t kn0 = keys->n, kb0 = keys->nbytes, vn0 = vals->n, vb0 = vals->nbytes;
     TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
     TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
-        k_dec_claim<<<gp, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, in->key_cap, in->kv_base, kslot, vslot,
+        const dim3 gc((unsigned)std::max<uint64_t>((max_np + kClaimChunk - 1) / kClaimChunk, 1), nb);
+        k_dec_claim<<<gc, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, key_cap, kv_base, kslot, vslot,
                                        out->kv_key, out->kv_val, ctr);
         rc = check_launch(ctx);
         if (rc) return rc;
     }
-    // claims and flags to the host: the id passes run only when new strings arrived
-    uint64_t h_ctr[8];
-    std::vector<uint32_t> flags(2 * nb);
-    e = hipMemcpyAsync(h_ctr, ctr, 64, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    // claims and flags to the host in one pinned copy: the id passes run only
+    // when new strings arrived
+    const size_t tail = fl_bytes + 64;
+    char *h_tail = h_head + bd_bytes;
+    const uint32_t *flags = (const uint32_t *)h_tail;
+    const unsigned long long *h_ctr = (const unsigned long long *)(h_tail + fl_bytes);
+    e = hipMemcpyAsync(h_tail, d_head + bd_bytes, tail, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (early) {
+        rc = (*spec)();
+        if (rc) {
+            (void)hipStreamSynchronize(s);             // (the read-back into ctx->hio is in flight)
+            return rc;
+        }
+    }
+    e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     uint64_t new_k = 0, new_kb = 0, new_v = 0, new_vb = 0;
     if (h_ctr[0] || h_ctr[1]) {
-        if (h_ctr[0]) {
+        if (early && spec_stale) *spec_stale = true;
+        const bool any_k = h_ctr[0] != 0, any_v = h_ctr[1] != 0;
+        if (any_k) {
             rc = scan_lb(ctx, RepCntSrc{kslot}, NoAct(), n_p, 0, krank, tmp);
             if (!rc) rc = scan_lb(ctx, RepLenSrc{c, kslot, false}, NoAct(), n_p, 0, kboff, tmp);
             if (rc) return rc;
             k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kt, false, kslot, krank, kboff, kn0, kb0,
                                                                 keys->bytes, keys->off);
-            k_off_end<<<1, 1, 0, s>>>(keys->off, krank + n_p, kboff + n_p, kn0, kb0);
+            k_off_end<<<1, 1, 0, s>>>(keys->off, krank + n_p, kboff + n_p, kn0, kb0, ctr + 2);
         }
-        if (h_ctr[1]) {
+        if (any_v) {
             rc = scan_lb(ctx, RepCntSrc{vslot}, NoAct(), n_p, 0, vrank, tmp);
             if (!rc) rc = scan_lb(ctx, RepLenSrc{c, vslot, true}, NoAct(), n_p, 0, vboff, tmp);
             if (rc) return rc;
             k_dec_assign<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, vt, true, vslot, vrank, vboff, vn0, vb0,
                                                                 vals->bytes, vals->off);
-            k_off_end<<<1, 1, 0, s>>>(vals->off, vrank + n_p, vboff + n_p, vn0, vb0);
+            k_off_end<<<1, 1, 0, s>>>(vals->off, vrank + n_p, vboff + n_p, vn0, vb0, ctr + 4);
         }
-        k_dec_ids<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kslot, vslot, keys->tab, vals->tab, in->key_cap,
-                                                         in->kv_base, out->kv_key, out->kv_val);
+        k_dec_ids<<<grid_for(n_p, 256, cap), 256, 0, s>>>(c, kslot, vslot, keys->tab, vals->tab, key_cap,
+                                                         kv_base, out->kv_key, out->kv_val);
         rc = check_launch(ctx);
         if (rc) return rc;
-        uint64_t sizes[4] = {0, 0, 0, 0};
-        if (h_ctr[0]) {
-            e = hipMemcpyAsync(&sizes[0], krank + n_p, 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(&sizes[1], kboff + n_p, 8, hipMemcpyDeviceToHost, s);
-        }
-        if (e == hipSuccess && h_ctr[1]) {
-            e = hipMemcpyAsync(&sizes[2], vrank + n_p, 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(&sizes[3], vboff + n_p, 8, hipMemcpyDeviceToHost, s);
-        }
-        if (e == hipSuccess) e = hipMemcpyAsync(flags.data(), d_flag, nb * 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);          // the id pass may flag a body too
+        e = hipMemcpyAsync(h_tail, d_head + bd_bytes, tail, hipMemcpyDeviceToHost, s);   // the id pass may flag a body too
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(ctx, e);
-        new_k = sizes[0], new_kb = sizes[1], new_v = sizes[2], new_vb = sizes[3];
+        if (any_k) new_k = h_ctr[2], new_kb = h_ctr[3];
+        if (any_v) new_v = h_ctr[4], new_vb = h_ctr[5];
     }
     for (uint32_t b = 0; b < nb; ++b) {
         body_status[b] |= flags[b] | flags[nb + b];
@@ -803,7 +1013,34 @@ extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, c
     rc = CRDT_OK;
     if (new_k) rc = tab_pull_new(ctx, keys, kn0 + new_k, kb0 + new_kb);
     if (!rc && new_v) rc = tab_pull_new(ctx, vals, vn0 + new_v, vb0 + new_vb);
+    if (!rc && spec && !early) {
+        rc = (*spec)();
+        if (!rc) {
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+        }
+    }
     return rc;
+}
+}  // namespace crdt
+
+extern "C" int crdt_gossip_decode(crdt_ctx *ctx, const crdt_gossip_bodies *in, crdt_strtab *keys,
+                                  crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!in || !keys || !vals || !out || !body_status) return CRDT_E_INVAL;
+    if (keys->device != ctx->device || vals->device != ctx->device) return CRDT_E_INVAL;
+    const uint32_t nb = in->n_bodies;
+    if (nb == 0) return CRDT_OK;
+    if (!in->data || !in->body_off || !in->slot_base || !out->r_off) return CRDT_E_INVAL;
+    std::vector<uint64_t> at(nb), len(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+        if (in->body_off[b + 1] < in->body_off[b]) return CRDT_E_INVAL;
+        at[b] = in->body_off[b];
+        len[b] = in->body_off[b + 1] - in->body_off[b];
+    }
+    return gossip_decode_at(ctx, nb, in->data, at.data(), len.data(), in->key_cap, in->kv_base, in->slot_base,
+                            in->host_hdr, keys, vals, out, body_status, nullptr, nullptr, 0, nullptr);
 }
 
 // Intern n strings [off[i], off[i+1]) of a device arena (host callers seeding

@@ -6,6 +6,7 @@
 #include <atomic>
 #include <stddef.h>
 #include <stdint.h>
+#include <functional>
 #include <vector>
 
 #include "../../include/crdt_amd.h"
@@ -26,6 +27,12 @@ struct crdt_ctx {
     void *srv_batch = nullptr;        // batched Server merge scratch (server.hip)
     void *pinned = nullptr;           // pinned host staging (pulled bodies on their way to HBM)
     size_t pinned_bytes = 0;
+    // Pinned host staging of a call's small uploads / read-backs (descriptors,
+    // counters, flags): a pinned copy is a DMA with no host round trip, where a
+    // pageable device-to-host copy waits for the stream (~15 us each).  Owned
+    // by one call at a time; every user synchronises before it returns.
+    void *hio = nullptr;
+    size_t hio_bytes = 0;
     // A second (non-blocking) stream for pipelined passes, created on first
     // use; every call that uses it joins it back into `stream` by an event
     // before returning, so callers only ever order against `stream`.
@@ -66,6 +73,8 @@ extern int g_rdd_diag;          // OR-Set D2 group dedup timing diagnostic (sort
 extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
 extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
 extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
+extern int g_rm_kvx;           // RefMerge kv tile pass in one launch at any grid (refmerge.kv_one_launch)
+extern int g_dec_small;        // gossip decode of few small bodies in one pass (codec.small)
 extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmerge.count_dma)
 extern int g_lww_chunk;         // set merges: tiles per count / write chunk (sets.lww_chunk, sets.or_chunk;
 extern int g_or_chunk;          //   0 = one chunk), DESIGN.md §5.4
@@ -90,6 +99,14 @@ int tuples_merge_stable(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const cr
 int seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,
                           const uint64_t *a_off, const uint64_t *b_off, uint64_t *dst_off, const uint32_t *a0,
                           const uint32_t *b0, uint32_t *dst0, const uint32_t *a1, const uint32_t *b1, uint32_t *dst1);
+// codec.hip: crdt_gossip_decode of nb bodies at data + at[b] (mod 2^64, so the
+// bodies may sit in separate device buffers), len[b] bytes each; optionally
+// with work enqueued behind the claim pass before the host waits (see there)
+int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
+                     uint32_t key_cap, uint64_t kv_base, const uint32_t *slot_base, const uint8_t *host_hdr,
+                     crdt_strtab *keys, crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status,
+                     const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale);
+size_t gossip_decode_scratch_bytes(uint32_t nb, uint64_t n_e, uint64_t n_p);
 
 // shard.hip: the communicator's collective transport for other protocols
 // (population.hip's sharded rounds).  One point-to-point transfer of a group:
@@ -110,6 +127,24 @@ int comm_rank0(const crdt_comm *c);
 crdt_ctx *comm_member_ctx(crdt_comm *c, size_t i);
 int comm_allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes);
 int comm_p2p(crdt_comm *c, const std::vector<XP2P> &ops);
+
+// ctx->hio at >= bytes (grow-only; the stream is drained before a regrow).
+inline int hio_reserve(crdt_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->hio_bytes) return CRDT_OK;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    if (ctx->hio) (void)hipHostFree(ctx->hio);
+    ctx->hio = nullptr;
+    ctx->hio_bytes = 0;
+    const size_t want = bytes + bytes / 2 > (64u << 10) ? bytes + bytes / 2 : (64u << 10);
+    e = hipHostMalloc(&ctx->hio, want, 0);
+    if (e != hipSuccess) {
+        ctx->hio = nullptr;
+        return hip_fail(ctx, e);
+    }
+    ctx->hio_bytes = want;
+    return CRDT_OK;
+}
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

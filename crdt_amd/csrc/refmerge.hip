@@ -960,6 +960,19 @@ __global__ __launch_bounds__(FB, 4) void k_rm_tile_kv(crdt_refmerge_in in, const
                                   nullptr, nullptr, err, kvo);
 }
 
+// ... and both kinds of tile in one launch, for grids that fit the chip in one
+// wave of workgroups (small batches: one launch fewer, occupancy moot)
+template <int FOLD>
+__global__ __launch_bounds__(FB, 4) void k_rm_tile_kvx(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
+                                                       const uint64_t *__restrict__ bits, const OkVal *__restrict__ okv,
+                                                       SlotAcc acc, int diag, const uint64_t *__restrict__ ic,
+                                                       crdt_refmerge_out out, uint32_t *__restrict__ err, KvOut kvo) {
+    rm_tile<FOLD, 1, true, true>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                 nullptr, nullptr, err, kvo);
+    rm_tile<FOLD, 1, true, false>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                  nullptr, nullptr, err, kvo);
+}
+
 // Delta replay, second phase: the global max holder of each slot writes its
 // string.  Every tile left one candidate (its max holder) per slot it
 // touched, so only those are checked -- unless some tile's LDS table
@@ -1332,7 +1345,9 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     }
     // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
 #define RM_TILE(F, P, KV, DIAG)                                                                                \
-    if (KV) {                                                                                                  \
+    if (KV && (g_rm_kvx || tg <= (unsigned)ctx->num_cus)) {                                                    \
+        k_rm_tile_kvx<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
+    } else if (KV) {                                                                                           \
         k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
         k_rm_tile_kv<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);       \
     } else                                                                                                       \

@@ -73,9 +73,24 @@ struct Server {
     bool host_valid = true, dev_valid = false;
     DevDiff dd, dd2;                                        // current + next (swapped per merge)
     std::vector<std::pair<int64_t, std::shared_ptr<const Value>>> pend_cmds;
-    char *pend_body = nullptr;         // pinned host copy of the parked pull (a full-rate H2D at the merge)
+    char *pend_body = nullptr;         // pinned host copy of the parked pull
     size_t pend_len = 0, pend_cap = 0;
     bool pend = false;
+    // The parked pull's H2D starts at ingest (into `pull`, on the context's
+    // stream): it overlaps the host's validation of the next pulls instead of
+    // sitting inside the merge.  pend_body is rewritten only by a later parked
+    // pull, i.e. after a merge (which synchronises) or absorb_pending (which
+    // drains the stream first).
+    bool pend_dev = false;
+    DBuf pull;
+    // CurrentState as of the last device merge, per key id: kind (0 absent,
+    // 1 string id, 2 sum), string id, sum.  While state_synced, CurrentState
+    // is exactly the map these describe, and the next merge updates only the
+    // keys whose words changed (main.go:76 rebuilds from empty: same result).
+    std::vector<uint8_t> sk;
+    std::vector<uint32_t> ss;
+    std::vector<int64_t> su;
+    bool state_synced = false;
     DBuf body, r_ts, r_kv, r_off, l_off, o_off, o_src, st_kind, st_str, st_sum, c_ts, c_kv, c_key, c_val, c_off,
         c_status;
 };
@@ -301,6 +316,7 @@ static int merge_locked(crdt_ctx *ctx, Server *const *srv, size_t n) {
         s.RemoteDiff.clear();                                    // main.go:75
         s.CurrentState.swap(st);
         s.state_view.clear();
+        s.state_synced = false;                                  // (no per-key words of this map)
         s.Alive = true;                                          // main.go:99
     }
     return CRDT_OK;
@@ -419,15 +435,18 @@ static std::string tab_str(const crdt_strtab *t, uint64_t id) {
 // H2D a body and decode it with the context's tables: entries -> r_ts /
 // r_kv (+ kv_base), pairs -> kv_key / kv_val at kv_base.  *status = the
 // body's decode status (0: taken).
-static int dev_decode(crdt_ctx *ctx, DBuf &body_dev, const char *body, size_t len, bool pinned, uint64_t kv_base,
-                      int64_t *r_ts, uint64_t *r_kv, uint64_t *r_off, uint32_t *kv_key, uint32_t *kv_val,
-                      uint32_t *status) {
-    int rc = dbuf(ctx, body_dev, len);
-    if (!rc && !pinned) rc = pinned_reserve(ctx, len);
-    if (rc) return rc;
-    if (!pinned) memcpy(ctx->pinned, body, len);
-    hipError_t e = hipMemcpyAsync(body_dev.p, pinned ? body : ctx->pinned, len, hipMemcpyHostToDevice, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
+// on_dev: body_dev already holds the body (a pull uploaded at ingest).
+static int dev_decode(crdt_ctx *ctx, DBuf &body_dev, const char *body, size_t len, bool pinned, bool on_dev,
+                      uint64_t kv_base, int64_t *r_ts, uint64_t *r_kv, uint64_t *r_off, uint32_t *kv_key,
+                      uint32_t *kv_val, uint32_t *status) {
+    if (!on_dev) {
+        int rc = dbuf(ctx, body_dev, len);
+        if (!rc && !pinned) rc = pinned_reserve(ctx, len);
+        if (rc) return rc;
+        if (!pinned) memcpy(ctx->pinned, body, len);
+        hipError_t e = hipMemcpyAsync(body_dev.p, pinned ? body : ctx->pinned, len, hipMemcpyHostToDevice, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
     const uint64_t boff[2] = {0, len};
     const uint32_t sb = 0;
     crdt_gossip_bodies gb{1, 0xFFFFFFFFu, kv_base, body_dev.as<uint8_t>(), boff, &sb,
@@ -455,7 +474,7 @@ static int dev_upload(crdt_ctx *ctx, Server &s) {
     if (!rc) rc = dbuf(ctx, s.r_off, 16);
     if (rc) return rc;
     uint32_t st = 0;
-    rc = dev_decode(ctx, s.body, body.data(), body.size(), false, 0, s.dd.ts.as<int64_t>(), s.dd.kv_off.as<uint64_t>(),
+    rc = dev_decode(ctx, s.body, body.data(), body.size(), false, false, 0, s.dd.ts.as<int64_t>(), s.dd.kv_off.as<uint64_t>(),
                     s.r_off.as<uint64_t>(), s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), &st);
     if (rc) return rc;
     if (st) return CRDT_E_UNSORTED;                   // (never: a treemap's body is ascending and nil-free)
@@ -518,7 +537,11 @@ static int make_host(Server &s) {
 static void parse_soa_into(Server &s, const char *data, size_t len);
 static void absorb_pending(Server &s) {
     if (!s.pend) return;
+    // an upload started at ingest may still read pend_body, which the next
+    // parked pull overwrites: drain it first (every merge synchronises anyway)
+    if (s.pend_dev && s.ctx && bind(s.ctx) == CRDT_OK) (void)hipStreamSynchronize(s.ctx->stream);
     s.pend = false;
+    s.pend_dev = false;
     parse_soa_into(s, s.pend_body, s.pend_len);
 }
 
@@ -544,7 +567,7 @@ static int dev_flush_chunk(crdt_ctx *ctx, Server &s, const std::map<int64_t, std
     if (!rc) rc = dbuf(ctx, s.dd2.kv_val, (s.dd.n_kv + np) * 4 + 4);
     if (rc) return rc;
     uint32_t st = 0;
-    rc = dev_decode(ctx, s.body, body.data(), body.size(), false, 0, s.c_ts.as<int64_t>(), s.c_kv.as<uint64_t>(),
+    rc = dev_decode(ctx, s.body, body.data(), body.size(), false, false, 0, s.c_ts.as<int64_t>(), s.c_kv.as<uint64_t>(),
                     s.c_off.as<uint64_t>(), s.c_key.as<uint32_t>(), s.c_val.as<uint32_t>(), &st);
     if (rc) return rc;
     if (st) return CRDT_E_UNSORTED;
@@ -605,6 +628,42 @@ static int dev_flush_cmds(crdt_ctx *ctx, Server &s) {
     return CRDT_OK;
 }
 
+// CurrentState from the merge's per-key words (main.go:76-96: rebuilt from
+// empty; kind 1 = the string id's value, 2 = Itoa(sum), else absent), kind /
+// str / sum indexed by key id, n = the key table's size.  While the previous
+// words still describe CurrentState (no AddCommand or host merge since), only
+// the keys whose words changed are touched -- the same map as a rebuild.
+static void apply_state(crdt_ctx *ctx, Server &s, const uint8_t *kind, const uint32_t *str, const int64_t *sum,
+                        uint64_t n) {
+    auto kd = [](uint8_t k) -> uint8_t { return k == 1 || k == 2 ? k : 0; };
+    auto text = [&](uint8_t k, uint32_t id, int64_t v) {
+        return k == 1 ? tab_str(ctx->vals, id) : std::to_string((long long)v);   // strconv.Itoa
+    };
+    if (!s.state_synced) {
+        std::map<std::string, std::string> st;
+        for (uint64_t k = 0; k < n; ++k)
+            if (kd(kind[k])) st.emplace(tab_str(ctx->keys, k), text(kind[k], str[k], sum[k]));
+        s.CurrentState.swap(st);
+        s.state_view.clear();
+    } else {
+        bool changed = false;
+        const uint64_t old = s.sk.size();
+        for (uint64_t k = 0; k < std::max(n, old); ++k) {
+            const uint8_t a = k < old ? s.sk[k] : 0, b = k < n ? kd(kind[k]) : 0;
+            if (a == b && (b == 0 || (b == 1 ? s.ss[k] == str[k] : s.su[k] == sum[k]))) continue;
+            changed = true;
+            if (b == 0) s.CurrentState.erase(tab_str(ctx->keys, k));
+            else s.CurrentState[tab_str(ctx->keys, k)] = text(b, str[k], sum[k]);
+        }
+        if (changed) s.state_view.clear();
+    }
+    s.sk.resize(n);
+    for (uint64_t k = 0; k < n; ++k) s.sk[k] = kd(kind[k]);
+    s.ss.assign(str, str + n);
+    s.su.assign(sum, sum + n);
+    s.state_synced = true;
+}
+
 // merge() (main.go:35-100) of one device-resident server: the pull decoded
 // on the device into R, the batched RefMerge with this Diff as L, the next
 // Diff gathered in HBM; only CurrentState (one word per key slot) comes back.
@@ -639,7 +698,8 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     if (!rc) rc = dbuf(ctx, s.dd2.kv_val, (nkv + np) * 4 + 4);
     if (rc) return rc;
     uint32_t st = 0;
-    rc = dev_decode(ctx, s.body, rp, rlen, s.pend, nkv, s.r_ts.as<int64_t>(), s.r_kv.as<uint64_t>(),
+    const bool on_dev = s.pend && s.pend_dev;
+    rc = dev_decode(ctx, on_dev ? s.pull : s.body, rp, rlen, s.pend, on_dev, nkv, s.r_ts.as<int64_t>(), s.r_kv.as<uint64_t>(),
                     s.r_off.as<uint64_t>(), s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), &st);
     if (rc) return rc;
     if (st) return CRDT_E_UNSORTED;                   // (callers route such pulls to the host path first)
@@ -652,8 +712,16 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     rc = dbuf(ctx, s.st_kind, nks + 1);
     if (!rc) rc = dbuf(ctx, s.st_str, nks * 4 + 4);
     if (!rc) rc = dbuf(ctx, s.st_sum, nks * 8 + 8);
+    // pinned staging (the decode above has synchronised: ctx->hio is free):
+    // [l_off | entry count | pair total | status | sum | str | kind]
+    const size_t h_sum = 64, h_str = h_sum + Carve::round(nks * 8 + 8), h_kind = h_str + Carve::round(nks * 4 + 4);
+    if (!rc) rc = hio_reserve(ctx, h_kind + nks + 1);
     if (rc) return rc;
-    const uint64_t loff[2] = {0, nl};
+    char *hio = (char *)ctx->hio;
+    uint64_t *loff = (uint64_t *)hio, *oo = loff + 2, *new_nkv = loff + 4;
+    uint32_t *fl = (uint32_t *)(loff + 5);
+    loff[0] = 0;
+    loff[1] = nl;
     hipError_t e = hipMemcpyAsync(s.l_off.p, loff, 16, hipMemcpyHostToDevice, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
     crdt_refmerge_in ri;
@@ -687,33 +755,27 @@ static int dev_merge_one(crdt_ctx *ctx, Server &s) {
     if (rc) return rc;
     // CurrentState (main.go:76-96: rebuilt from empty), the entry count and
     // the new pair count (every dst offset from the entry count on = the total)
-    std::vector<uint8_t> kind(nks);
-    std::vector<uint32_t> sstr(nks);
-    std::vector<int64_t> ssum(nks);
-    uint64_t oo[2] = {0, 0}, new_nkv = 0;
+    uint8_t *kind = (uint8_t *)(hio + h_kind);
+    uint32_t *sstr = (uint32_t *)(hio + h_str);
+    int64_t *ssum = (int64_t *)(hio + h_sum);
     e = hipMemcpyAsync(oo, s.o_off.p, 16, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(&new_nkv, s.dd2.kv_off.as<uint64_t>() + nl + ne, 8, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && nks) e = hipMemcpyAsync(kind.data(), s.st_kind.p, nks, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && nks) e = hipMemcpyAsync(sstr.data(), s.st_str.p, nks * 4, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && nks) e = hipMemcpyAsync(ssum.data(), s.st_sum.p, nks * 8, hipMemcpyDeviceToHost, ctx->stream);
-    uint32_t fl[3] = {0, 0, 0};
+        e = hipMemcpyAsync(new_nkv, s.dd2.kv_off.as<uint64_t>() + nl + ne, 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nks) e = hipMemcpyAsync(kind, s.st_kind.p, nks, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nks) e = hipMemcpyAsync(sstr, s.st_str.p, nks * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && nks) e = hipMemcpyAsync(ssum, s.st_sum.p, nks * 8, hipMemcpyDeviceToHost, ctx->stream);
+    fl[0] = fl[1] = fl[2] = 0;
     if (e == hipSuccess) e = sc.fetch(fl);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
     if (sc.raised(fl)) return CRDT_E_DEVICE;                // dd / RemoteDiff untouched (the swap below never ran)
-    std::map<std::string, std::string> state;
-    for (uint64_t k = 0; k < nks; ++k) {
-        if (kind[k] == 1) state.emplace(tab_str(ctx->keys, k), tab_str(ctx->vals, sstr[k]));
-        else if (kind[k] == 2) state.emplace(tab_str(ctx->keys, k), std::to_string((long long)ssum[k]));   // Itoa
-    }
+    apply_state(ctx, s, kind, sstr, ssum, nks);
     std::swap(s.dd, s.dd2);
     s.dd.n = oo[1];
-    s.dd.n_kv = new_nkv;
-    s.CurrentState.swap(state);
-    s.state_view.clear();
+    s.dd.n_kv = *new_nkv;
     s.RemoteDiff.clear();                             // main.go:75
     s.pend = false;
+    s.pend_dev = false;
     s.pend_len = 0;
     s.host_valid = false;
     return CRDT_OK;
@@ -734,10 +796,13 @@ struct SegPtrs {                       // one server's device Diff, for the conc
 };
 
 // L of the batch: every server's Diff behind the previous one; kv ranges
-// re-based into the shared arena, key ids into the server's slot range.
+// re-based into the shared arena, key ids into the server's slot range;
+// l_kv[nl] = the arena's L pair count.
 __global__ void k_srv_concat(const SegPtrs *__restrict__ sp, int64_t *__restrict__ l_ts, uint8_t *__restrict__ l_org,
-                             uint64_t *__restrict__ l_kv, uint32_t *__restrict__ kv_key, uint32_t *__restrict__ kv_val) {
+                             uint64_t *__restrict__ l_kv, uint32_t *__restrict__ kv_key, uint32_t *__restrict__ kv_val,
+                             uint64_t nl, uint64_t nkl) {
     const SegPtrs p = sp[blockIdx.y];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) l_kv[nl] = nkl;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * 256) {
         l_ts[p.e0 + i] = p.ts[i];
         l_org[p.e0 + i] = p.origin[i];
@@ -749,19 +814,27 @@ __global__ void k_srv_concat(const SegPtrs *__restrict__ sp, int64_t *__restrict
     }
 }
 
-// The batch's new Diffs back into each server's next buffers.
-// Server y's entry range is o_off[y, y+1) of the batch's new Diff and its
-// pair range kb[y, y+1): both read on the device (the destinations are sized
-// for the upper bound), so the split needs no host round trip.
+// The batch's new Diffs back into each server's next buffers.  Server y's
+// entry range is o_off[y, y+1) of the batch's new Diff and its pair range
+// [o_kv[o_off[y]], o_kv[o_off[y+1]]): both read on the device (the
+// destinations are sized for the upper bound), so the split needs no host
+// round trip; the pair ranges also go to kb[] for the host.
 __global__ void k_srv_split(const SegPtrs *__restrict__ sp, const int64_t *__restrict__ o_ts,
                             const uint8_t *__restrict__ o_org, const uint64_t *__restrict__ o_kv,
                             const uint32_t *__restrict__ kv_key, const uint32_t *__restrict__ kv_val,
-                            const uint64_t *__restrict__ o_off, const uint64_t *__restrict__ kb) {
+                            const uint64_t *__restrict__ o_off, uint64_t *__restrict__ kb,
+                            const uint32_t *__restrict__ status, uint32_t *__restrict__ status_out) {
     SegPtrs p = sp[blockIdx.y];
     p.e0 = o_off[blockIdx.y];
     p.n = o_off[blockIdx.y + 1] - p.e0;
-    p.q0 = kb[blockIdx.y];
-    p.nq = kb[blockIdx.y + 1] - p.q0;
+    p.q0 = o_kv[p.e0];
+    p.nq = o_kv[p.e0 + p.n] - p.q0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        kb[blockIdx.y] = p.q0;
+        if (blockIdx.y + 1 == gridDim.y) kb[blockIdx.y + 1] = p.q0 + p.nq;
+        if (blockIdx.y == 0)                         // the merge's status words, read back with the results
+            for (int w = 0; w < 3; ++w) status_out[w] = status[w];
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i <= p.n; i += (uint64_t)gridDim.x * 256) {
         p.dkv_off[i] = o_kv[p.e0 + i] - p.q0;
         if (i < p.n) {
@@ -775,22 +848,19 @@ __global__ void k_srv_split(const SegPtrs *__restrict__ sp, const int64_t *__res
     }
 }
 
-// out[i] = v[idx[i]]
-__global__ void k_gather_at(const uint64_t *__restrict__ v, const uint64_t *__restrict__ idx, size_t n,
-                            uint64_t *__restrict__ out) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) out[i] = v[idx[i]];
-}
-
 struct BatchBufs {                     // per-context scratch of the batched server merge
-    DBuf kb, sp, body, l_ts, l_org, l_kv, l_off, kv_key, kv_val, r_off, r_ts, r_kv, o_off, o_ts, o_org, o_src, n_kv,
-        n_key, n_val, st_kind, st_str, st_sum;
+    DBuf head, res, body, dec, l_ts, l_org, l_kv, kv_key, kv_val, r_off, r_ts, r_kv, o_ts, o_org, o_src, n_kv, n_key,
+        n_val;
+    void *hp = nullptr;                // pinned image of head (upload) and res + status (read-back)
+    size_t hp_cap = 0;
 };
 
 // merge() of several device-resident servers in ONE decode, ONE RefMerge and
-// ONE gather.  Key slots: server s owns [s*kcap, (s+1)*kcap); a pull that
+// ONE split.  Key slots: server s owns [s*kcap, (s+1)*kcap); a pull that
 // brings more new keys than the slack is reported (*retry) and the caller
-// merges one server at a time instead.
+// merges one server at a time instead.  Host traffic per call: one pinned
+// upload of the descriptors (head), the pulls not already uploaded at ingest,
+// one pinned read-back of the results (res) -- plus the decode's own.
 // CRDT_SRV_PROF=1: per-phase host wall time of each batched merge on stderr
 // (a development aid; every phase ends where the host next waits anyway).
 struct PhaseClock {
@@ -830,13 +900,14 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     uint64_t kcap = 64;
     while (kcap < nks0 + 256) kcap <<= 1;
     if (kcap * S >= 0xFFFFFFFFull) return CRDT_E_RANGE;
-    // the pulls, one body per server, staged in pinned host memory (one
-    // full-rate H2D instead of a pageable copy)
+    // the pulls: parked ones were uploaded at ingest (s.pull); the rest (a
+    // RemoteDiff built on the host, a parked pull whose upload was not
+    // started) are staged in pinned memory and uploaded into bb.body here
     std::vector<std::string> enc(S);
-    std::vector<uint64_t> boff(S + 1, 0), e0(S + 1, 0), q0(S + 1, 0), re(S + 1, 0), rq(S + 1, 0), pin_at(S, 0);
+    std::vector<uint64_t> blen(S), bat(S, 0), e0(S + 1, 0), q0(S + 1, 0), re(S + 1, 0), rq(S + 1, 0), pin_at(S, 0);
     std::vector<uint32_t> sbase(S);
     std::vector<uint8_t> hdr(32 * S);
-    uint64_t pin_used = 0;
+    uint64_t pin_used = 0, stage = 0;
     for (size_t i = 0; i < S; ++i) {
         Server &s = *srv[i];
         if (!s.pend) {
@@ -846,7 +917,11 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
         }
         const char *b = s.pend ? s.pend_body : enc[i].data();
         memcpy(&hdr[32 * i], b, 32);                    // (every body here is >= 32 bytes)
-        boff[i + 1] = boff[i] + (s.pend ? s.pend_len : enc[i].size());
+        blen[i] = s.pend ? s.pend_len : enc[i].size();
+        if (!(s.pend && s.pend_dev)) {
+            bat[i] = stage;
+            stage += (blen[i] + 15) & ~(uint64_t)15;
+        }
         uint64_t ne, np;
         memcpy(&ne, b + 8, 8);
         memcpy(&np, b + 16, 8);
@@ -862,101 +937,35 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
         if (!srv[i]->pend) memcpy((char *)ctx->pinned + pin_at[i], enc[i].data(), enc[i].size());
     pc.mark("upload+encode");
     const uint64_t nl = e0[S], nkl = q0[S], nr = re[S], nkr = rq[S], nslots = kcap * S;
-    rc = dbuf(ctx, bb.sp, S * sizeof(SegPtrs));
-    if (!rc) rc = dbuf(ctx, bb.body, boff[S] + 1);
-    if (!rc) rc = dbuf(ctx, bb.kb, (S + 1) * 8);
+    // head (device, one upload): sp | sq | l_off;  res (device, one read-back):
+    // o_off | kb | st_sum | st_str | st_kind
+    const size_t h_sq = Carve::round(S * sizeof(SegPtrs)), h_loff = h_sq + Carve::round(S * sizeof(SegPtrs));
+    const size_t h_bytes = h_loff + Carve::round((S + 1) * 8);
+    const size_t r_kb = Carve::round((S + 1) * 8), r_sum = r_kb + Carve::round((S + 1) * 8);
+    const size_t r_str = r_sum + Carve::round(nslots * 8 + 8), r_kind = r_str + Carve::round(nslots * 4 + 4);
+    const size_t r_st = r_kind + Carve::round(nslots + 1), r_bytes = r_st + 16;
+    rc = dbuf(ctx, bb.head, h_bytes);
+    if (!rc) rc = dbuf(ctx, bb.res, r_bytes);
+    if (!rc) rc = dbuf(ctx, bb.dec, gossip_decode_scratch_bytes((uint32_t)S, nr, nkr));
+    if (!rc) rc = dbuf(ctx, bb.body, stage + 16);
     if (!rc) rc = dbuf(ctx, bb.l_ts, nl * 8 + 8);
     if (!rc) rc = dbuf(ctx, bb.l_org, nl + 1);
     if (!rc) rc = dbuf(ctx, bb.l_kv, (nl + 1) * 8);
-    if (!rc) rc = dbuf(ctx, bb.l_off, (S + 1) * 8);
     if (!rc) rc = dbuf(ctx, bb.kv_key, (nkl + nkr) * 4 + 4);
     if (!rc) rc = dbuf(ctx, bb.kv_val, (nkl + nkr) * 4 + 4);
     if (!rc) rc = dbuf(ctx, bb.r_off, (S + 1) * 8);
     if (!rc) rc = dbuf(ctx, bb.r_ts, nr * 8 + 8);
     if (!rc) rc = dbuf(ctx, bb.r_kv, (nr + 1) * 8);
-    if (!rc) rc = dbuf(ctx, bb.o_off, (S + 1) * 8);
     if (!rc) rc = dbuf(ctx, bb.o_ts, (nl + nr) * 8 + 8);
     if (!rc) rc = dbuf(ctx, bb.o_org, nl + nr + 1);
     if (!rc) rc = dbuf(ctx, bb.o_src, (nl + nr) * 8 + 8);
     if (!rc) rc = dbuf(ctx, bb.n_kv, (nl + nr + 1) * 8);
     if (!rc) rc = dbuf(ctx, bb.n_key, (nkl + nkr) * 4 + 4);
     if (!rc) rc = dbuf(ctx, bb.n_val, (nkl + nkr) * 4 + 4);
-    if (!rc) rc = dbuf(ctx, bb.st_kind, nslots + 1);
-    if (!rc) rc = dbuf(ctx, bb.st_str, nslots * 4 + 4);
-    if (!rc) rc = dbuf(ctx, bb.st_sum, nslots * 8 + 8);
-    if (rc) return rc;
-    const hipStream_t st = ctx->stream;
-    // L: concat
-    std::vector<SegPtrs> sp(S);
-    uint64_t maxn = 1;
-    for (size_t i = 0; i < S; ++i) {
-        Server &s = *srv[i];
-        sp[i] = SegPtrs{s.dd.ts.as<int64_t>(), s.dd.origin.as<uint8_t>(), s.dd.kv_off.as<uint64_t>(),
-                        s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
-                        nullptr, e0[i], s.dd.n, q0[i], s.dd.n_kv, sbase[i], 0};
-        maxn = std::max<uint64_t>(maxn, std::max(s.dd.n, s.dd.n_kv));
-    }
-    hipError_t e = hipMemcpyAsync(bb.sp.p, sp.data(), S * sizeof(SegPtrs), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(bb.l_off.p, e0.data(), (S + 1) * 8, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    const dim3 grid(grid_for(maxn, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
-    k_srv_concat<<<grid, 256, 0, st>>>(bb.sp.as<SegPtrs>(), bb.l_ts.as<int64_t>(), bb.l_org.as<uint8_t>(),
-                                        bb.l_kv.as<uint64_t>(), bb.kv_key.as<uint32_t>(), bb.kv_val.as<uint32_t>());
-    rc = check_launch(ctx);
-    if (rc) return rc;
-    e = hipMemcpyAsync(bb.l_kv.as<uint64_t>() + nl, &nkl, 8, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    // R: every pull decoded at once, pairs behind L's in the arena
-    for (size_t i = 0; i < S && e == hipSuccess; ++i) {
-        const Server &s = *srv[i];
-        e = hipMemcpyAsync(bb.body.as<char>() + boff[i], s.pend ? s.pend_body : (char *)ctx->pinned + pin_at[i],
-                           boff[i + 1] - boff[i], hipMemcpyHostToDevice, st);
-    }
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    std::vector<uint32_t> bst(S, 0);
-    crdt_gossip_bodies gb{(uint32_t)S, (uint32_t)kcap, nkl, bb.body.as<uint8_t>(), boff.data(), sbase.data(),
-                          hdr.data()};
-    crdt_gossip_decoded go{bb.r_off.as<uint64_t>(), bb.r_ts.as<int64_t>(), bb.r_kv.as<uint64_t>(),
-                           bb.kv_key.as<uint32_t>(), bb.kv_val.as<uint32_t>()};
-    pc.mark("alloc+concat");
-    rc = crdt_gossip_decode(ctx, &gb, ctx->keys, ctx->vals, &go, bst.data());
-    if (rc) return rc;
-    pc.mark("decode");
-    for (auto x : bst)
-        if (x) {                                       // a key past the slot slack (or a malformed pull)
-            *retry = true;
-            return CRDT_OK;
-        }
-    uint64_t nstr = 0;
-    const uint8_t *sb = nullptr;
-    const uint64_t *so = nullptr;
-    (void)crdt_strtab_info(ctx->vals, &nstr, &b0, &sb, &so);
-    crdt_refmerge_in ri;
-    ri.replicas = (uint32_t)S;
-    ri.n_slots = (uint32_t)nslots;
-    ri.n_l = nl;
-    ri.n_r = nr;
-    ri.n_kv = nkl + nkr;
-    ri.n_str = nstr;
-    ri.l_off = bb.l_off.as<uint64_t>();
-    ri.l_ts = bb.l_ts.as<int64_t>();
-    ri.l_origin = bb.l_org.as<uint8_t>();
-    ri.l_kv = bb.l_kv.as<uint64_t>();
-    ri.r_off = bb.r_off.as<uint64_t>();
-    ri.r_ts = bb.r_ts.as<int64_t>();
-    ri.r_kv = bb.r_kv.as<uint64_t>();
-    ri.kv_key = bb.kv_key.as<uint32_t>();
-    ri.kv_val = bb.kv_val.as<uint32_t>();
-    ri.str_bytes = sb;
-    ri.str_off = so;
-    crdt_refmerge_out ro{bb.o_off.as<uint64_t>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
-                         bb.o_src.as<int64_t>(), bb.st_kind.as<uint8_t>(), bb.st_str.as<uint32_t>(),
-                         bb.st_sum.as<int64_t>()};
     // each server's next Diff buffers at their upper bound (its L + its pull),
-    // so the gather and the split run behind the merge with no host round
-    // trip for the output sizes: one synchronisation per call, for CurrentState
-    uint64_t maxs = 1;
-    std::vector<SegPtrs> sq(S);
+    // so the split runs behind the merge with no host round trip for the
+    // output sizes: one synchronisation per call after the decode's
+    uint64_t maxs = 1, maxn = 1;
     for (size_t i = 0; i < S && !rc; ++i) {
         Server &s = *srv[i];
         const uint64_t nu = s.dd.n + (re[i + 1] - re[i]), qu = s.dd.n_kv + (rq[i + 1] - rq[i]);
@@ -965,71 +974,151 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
         if (!rc) rc = dbuf(ctx, s.dd2.kv_off, (nu + 1) * 8);
         if (!rc) rc = dbuf(ctx, s.dd2.kv_key, qu * 4 + 4);
         if (!rc) rc = dbuf(ctx, s.dd2.kv_val, qu * 4 + 4);
+        maxs = std::max<uint64_t>(maxs, std::max(nu + 1, qu));
+        maxn = std::max<uint64_t>(maxn, std::max(s.dd.n, s.dd.n_kv));
+    }
+    if (!rc && bb.hp_cap < h_bytes + r_bytes + 64) {
+        const hipError_t e = hipStreamSynchronize(ctx->stream);   // (the previous image may still be in flight)
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        if (bb.hp) (void)hipHostFree(bb.hp);
+        bb.hp = nullptr;
+        bb.hp_cap = 0;
+        const size_t want = (h_bytes + r_bytes + 64) * 3 / 2;
+        if (hipHostMalloc(&bb.hp, want, 0) != hipSuccess) {
+            bb.hp = nullptr;
+            return CRDT_E_NOMEM;
+        }
+        bb.hp_cap = want;
+    }
+    if (rc) return rc;
+    char *hp = (char *)bb.hp, *hres = hp + h_bytes;
+    uint32_t *hfl = (uint32_t *)(hres + r_st);
+    SegPtrs *sp = (SegPtrs *)hp, *sq = (SegPtrs *)(hp + h_sq);
+    for (size_t i = 0; i < S; ++i) {
+        Server &s = *srv[i];
+        sp[i] = SegPtrs{s.dd.ts.as<int64_t>(), s.dd.origin.as<uint8_t>(), s.dd.kv_off.as<uint64_t>(),
+                        s.dd.kv_key.as<uint32_t>(), s.dd.kv_val.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
+                        nullptr, e0[i], s.dd.n, q0[i], s.dd.n_kv, sbase[i], 0};
         sq[i] = SegPtrs{nullptr, nullptr, nullptr, nullptr, nullptr, s.dd2.ts.as<int64_t>(),
                         s.dd2.origin.as<uint8_t>(), s.dd2.kv_off.as<uint64_t>(), s.dd2.kv_key.as<uint32_t>(),
                         s.dd2.kv_val.as<uint32_t>(), 0, 0, 0, 0, sbase[i], 0};
-        maxs = std::max<uint64_t>(maxs, std::max(nu + 1, qu));
     }
+    memcpy(hp + h_loff, e0.data(), (S + 1) * 8);
+    const hipStream_t st = ctx->stream;
+    char *dh = bb.head.as<char>(), *dr = bb.res.as<char>();
+    hipError_t e = hipMemcpyAsync(dh, hp, h_bytes, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    // L: concat
+    const dim3 grid(grid_for(maxn, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
+    k_srv_concat<<<grid, 256, 0, st>>>((const SegPtrs *)dh, bb.l_ts.as<int64_t>(), bb.l_org.as<uint8_t>(),
+                                        bb.l_kv.as<uint64_t>(), bb.kv_key.as<uint32_t>(), bb.kv_val.as<uint32_t>(), nl,
+                                        nkl);
+    rc = check_launch(ctx);
     if (rc) return rc;
-    StatusScope sc(ctx);
-    // the merge with the new Diffs' kv pairs (copied by its tile pass; the
-    // entry count stays on the device), then each server's pair range, the
-    // split into its next buffers, then CurrentState
+    // R: every pull decoded at once, pairs behind L's in the arena; bodies
+    // addressed relative to bb.body (the ones uploaded at ingest live in
+    // their servers' pull buffers)
+    const uint8_t *base = bb.body.as<uint8_t>();
+    std::vector<uint64_t> at(S);
+    for (size_t i = 0; i < S && e == hipSuccess; ++i) {
+        const Server &s = *srv[i];
+        if (s.pend && s.pend_dev) {
+            at[i] = (uint64_t)(uintptr_t)s.pull.p - (uint64_t)(uintptr_t)base;
+        } else {
+            at[i] = bat[i];
+            e = hipMemcpyAsync(bb.body.as<char>() + bat[i], s.pend ? s.pend_body : (char *)ctx->pinned + pin_at[i],
+                               blen[i], hipMemcpyHostToDevice, st);
+        }
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    std::vector<uint32_t> bst(S, 0);
+    crdt_gossip_decoded go{bb.r_off.as<uint64_t>(), bb.r_ts.as<int64_t>(), bb.r_kv.as<uint64_t>(),
+                           bb.kv_key.as<uint32_t>(), bb.kv_val.as<uint32_t>()};
+    pc.mark("alloc+concat");
+    crdt_refmerge_in ri;
+    ri.replicas = (uint32_t)S;
+    ri.n_slots = (uint32_t)nslots;
+    ri.n_l = nl;
+    ri.n_r = nr;
+    ri.n_kv = nkl + nkr;
+    ri.l_off = (const uint64_t *)(dh + h_loff);
+    ri.l_ts = bb.l_ts.as<int64_t>();
+    ri.l_origin = bb.l_org.as<uint8_t>();
+    ri.l_kv = bb.l_kv.as<uint64_t>();
+    ri.r_off = bb.r_off.as<uint64_t>();
+    ri.r_ts = bb.r_ts.as<int64_t>();
+    ri.r_kv = bb.r_kv.as<uint64_t>();
+    ri.kv_key = bb.kv_key.as<uint32_t>();
+    ri.kv_val = bb.kv_val.as<uint32_t>();
+    crdt_refmerge_out ro{(uint64_t *)dr, bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(), bb.o_src.as<int64_t>(),
+                         (uint8_t *)(dr + r_kind), (uint32_t *)(dr + r_str), (int64_t *)(dr + r_sum)};
     const crdt_refmerge_kv_out kvo{bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>(),
                                    nkl + nkr};
-    rc = crdt_refmerge_batch_kv(ctx, &ri, &ro, &kvo);
+    StatusScope sc(ctx);
+    // the merge with the new Diffs' kv pairs (copied by its tile pass; the
+    // entry count stays on the device), the split into each server's next
+    // buffers, then everything the host needs in one read-back.  Enqueued by
+    // the decode right behind its claim pass (the strings of a pull are
+    // nearly always interned already); when the pulls brought new strings the
+    // decode finishes their ids first and this runs again.
+    const std::function<int()> run_merge = [&]() -> int {
+        uint64_t nstr = 0, nb0 = 0;
+        const uint8_t *sb = nullptr;
+        const uint64_t *so = nullptr;
+        (void)crdt_strtab_info(ctx->vals, &nstr, &nb0, &sb, &so);
+        ri.n_str = nstr;
+        ri.str_bytes = sb;
+        ri.str_off = so;
+        int r = crdt_refmerge_batch_kv(ctx, &ri, &ro, &kvo);
+        if (r) return r;
+        const dim3 g2(grid_for(maxs, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
+        k_srv_split<<<g2, 256, 0, st>>>((const SegPtrs *)(dh + h_sq), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
+                                         bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>(),
+                                         (const uint64_t *)dr, (uint64_t *)(dr + r_kb), sc.saved,
+                                         (uint32_t *)(dr + r_st));
+        r = check_launch(ctx);
+        if (r) return r;
+        const hipError_t x = hipMemcpyAsync(hres, dr, r_bytes, hipMemcpyDeviceToHost, st);   // results + status words
+        return x == hipSuccess ? CRDT_OK : hip_fail(ctx, x);
+    };
+    bool stale = false;
+    rc = gossip_decode_at(ctx, (uint32_t)S, base, at.data(), blen.data(), (uint32_t)kcap, nkl, sbase.data(),
+                          hdr.data(), ctx->keys, ctx->vals, &go, bst.data(), &run_merge, bb.dec.p, bb.dec.cap, &stale);
     if (rc) return rc;
-    pc.mark("refmerge_launch");
-    k_gather_at<<<grid_for(S + 1, 256, 1u << 20), 256, 0, st>>>(bb.n_kv.as<uint64_t>(), bb.o_off.as<uint64_t>(),
-                                                                 S + 1, bb.kb.as<uint64_t>());
-    rc = check_launch(ctx);
-    if (rc) return rc;
-    e = hipMemcpyAsync(bb.sp.p, sq.data(), S * sizeof(SegPtrs), hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    const dim3 g2(grid_for(maxs, 256, (unsigned)ctx->num_cus * 2), (unsigned)S);
-    k_srv_split<<<g2, 256, 0, st>>>(bb.sp.as<SegPtrs>(), bb.o_ts.as<int64_t>(), bb.o_org.as<uint8_t>(),
-                                     bb.n_kv.as<uint64_t>(), bb.n_key.as<uint32_t>(), bb.n_val.as<uint32_t>(),
-                                     bb.o_off.as<uint64_t>(), bb.kb.as<uint64_t>());
-    rc = check_launch(ctx);
-    if (rc) return rc;
-    std::vector<uint64_t> oo(S + 1), kb(S + 1);
-    std::vector<uint8_t> kind(nslots);
-    std::vector<uint32_t> sstr(nslots);
-    std::vector<int64_t> ssum(nslots);
-    e = hipMemcpyAsync(oo.data(), bb.o_off.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(kb.data(), bb.kb.p, (S + 1) * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(kind.data(), bb.st_kind.p, nslots, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(sstr.data(), bb.st_str.p, nslots * 4, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(ssum.data(), bb.st_sum.p, nslots * 8, hipMemcpyDeviceToHost, st);
-    uint32_t fl[3] = {0, 0, 0};
-    if (e == hipSuccess) e = sc.fetch(fl);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);   // (also settles sp / sq, host vectors)
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    if (sc.raised(fl)) return CRDT_E_DEVICE;                // no server swapped in anything
-    pc.mark("gather+split+state_d2h");
+    pc.mark("decode+merge");
+    for (auto x : bst)
+        if (x) {                                       // a key past the slot slack (or a malformed pull)
+            *retry = true;
+            return CRDT_OK;
+        }
+    if (stale) {                                       // new strings: the merge again, on their ids
+        rc = run_merge();
+        if (rc) return rc;
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
+    if (sc.raised(hfl)) return CRDT_E_DEVICE;              // no server swapped in anything
+    pc.mark("split+read_back");
+    const uint64_t *oo = (const uint64_t *)hres, *kb = (const uint64_t *)(hres + r_kb);
+    const uint8_t *kind = (const uint8_t *)(hres + r_kind);
+    const uint32_t *sstr = (const uint32_t *)(hres + r_str);
+    const int64_t *ssum = (const int64_t *)(hres + r_sum);
     uint64_t nks = 0;
     (void)crdt_strtab_info(ctx->keys, &nks, &b0, nullptr, nullptr);
-    std::vector<std::string> kname(nks);
-    for (uint64_t k = 0; k < nks; ++k) kname[k] = tab_str(ctx->keys, k);
+    const uint64_t nk = std::min(nks, kcap);
     for (size_t i = 0; i < S; ++i) {
         Server &s = *srv[i];
-        std::map<std::string, std::string> state;       // main.go:76: rebuilt from empty
-        for (uint64_t k = 0; k < nks && k < kcap; ++k) {
-            const uint64_t sl = i * kcap + k;
-            if (kind[sl] == 1) state.emplace(kname[k], tab_str(ctx->vals, sstr[sl]));
-            else if (kind[sl] == 2) state.emplace(kname[k], std::to_string((long long)ssum[sl]));   // Itoa
-        }
+        apply_state(ctx, s, kind + i * kcap, sstr + i * kcap, ssum + i * kcap, nk);
         std::swap(s.dd, s.dd2);
         s.dd.n = oo[i + 1] - oo[i];
         s.dd.n_kv = kb[i + 1] - kb[i];
-        s.CurrentState.swap(state);
-        s.state_view.clear();
         s.RemoteDiff.clear();                          // main.go:75
         s.pend = false;
+        s.pend_dev = false;
         s.pend_len = 0;
         s.host_valid = false;
     }
-    pc.mark("state_rebuild");
+    pc.mark("state");
     return CRDT_OK;
 }
 
@@ -1037,10 +1126,11 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
 void server_ctx_release(crdt_ctx *ctx) {
     if (!ctx->srv_batch) return;
     BatchBufs *bb = (BatchBufs *)ctx->srv_batch;
-    for (DBuf *b : {&bb->kb, &bb->sp, &bb->body, &bb->l_ts, &bb->l_org, &bb->l_kv, &bb->l_off, &bb->kv_key, &bb->kv_val,
-                    &bb->r_off, &bb->r_ts, &bb->r_kv, &bb->o_off, &bb->o_ts, &bb->o_org, &bb->o_src, &bb->n_kv,
-                    &bb->n_key, &bb->n_val, &bb->st_kind, &bb->st_str, &bb->st_sum})
+    for (DBuf *b : {&bb->head, &bb->res, &bb->body, &bb->dec, &bb->l_ts, &bb->l_org, &bb->l_kv, &bb->kv_key, &bb->kv_val,
+                    &bb->r_off, &bb->r_ts, &bb->r_kv, &bb->o_ts, &bb->o_org, &bb->o_src, &bb->n_kv, &bb->n_key,
+                    &bb->n_val})
         dbuf_free(*b);
+    if (bb->hp) (void)hipHostFree(bb->hp);
     delete bb;
     ctx->srv_batch = nullptr;
 }
@@ -1062,7 +1152,7 @@ static void dev_free(Server &s) {
     for (DBuf *b : {&s.dd.ts, &s.dd.origin, &s.dd.kv_off, &s.dd.kv_key, &s.dd.kv_val, &s.dd2.ts, &s.dd2.origin,
                     &s.dd2.kv_off, &s.dd2.kv_key, &s.dd2.kv_val, &s.body, &s.r_ts, &s.r_kv, &s.r_off, &s.l_off,
                     &s.o_off, &s.o_src, &s.st_kind, &s.st_str, &s.st_sum, &s.c_ts, &s.c_kv, &s.c_key, &s.c_val,
-                    &s.c_off, &s.c_status})
+                    &s.c_off, &s.c_status, &s.pull})
         dbuf_free(*b);
     if (s.pend_body) (void)hipHostFree(s.pend_body);
     s.pend_body = nullptr;
@@ -1186,6 +1276,7 @@ extern "C" int crdt_server_init_state(crdt_server *srv, const char *const *keys,
     srv->s.InitialState.clear();
     for (size_t i = 0; i < n; ++i) srv->s.InitialState[std::string(keys[i], klen[i])] = std::string(vals[i], vlen[i]);
     srv->s.CurrentState = srv->s.InitialState;
+    srv->s.state_synced = false;
     srv->s.state_view.clear();
     return CRDT_OK;
 }
@@ -1206,6 +1297,7 @@ extern "C" int crdt_server_add_command(crdt_server *srv, int64_t ts_ms, const ch
     if (s.host_valid) s.Diff[ts_ms] = v;                   // same-ms writes overwrite
     if (s.dev_valid) s.pend_cmds.emplace_back(ts_ms, v);   // applied to the device Diff at the next merge
     s.state_view.clear();
+    s.state_synced = false;                                 // CurrentState now differs from the device's words
     *http_status = 200;
     for (auto &kv : v->kv) {
         auto it = s.CurrentState.find(kv.first);
@@ -1863,7 +1955,7 @@ extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, siz
     std::lock_guard<std::mutex> g(srv->s.Lock);
     Server &s = srv->s;
     if (device_form && s.ctx && !s.pend && s.RemoteDiff.empty()) {
-        if (len > s.pend_cap) {                                 // (the previous pull's H2D completed: merges sync)
+        if (len > s.pend_cap) {
             if (s.pend_body) (void)hipHostFree(s.pend_body);
             s.pend_body = nullptr;
             s.pend_cap = 0;
@@ -1875,6 +1967,10 @@ extern "C" int crdt_server_ingest_binary(crdt_server *srv, const char *data, siz
         memcpy(s.pend_body, data, len);
         s.pend_len = len;
         s.pend = true;
+        // its upload starts now, ordered before the merge on the context's
+        // stream; on any failure here the merge uploads it instead
+        s.pend_dev = bind(s.ctx) == CRDT_OK && dbuf(s.ctx, s.pull, len) == CRDT_OK &&
+                     hipMemcpyAsync(s.pull.p, s.pend_body, len, hipMemcpyHostToDevice, s.ctx->stream) == hipSuccess;
     } else {
         absorb_pending(s);
         parse_soa_into(s, data, len);

@@ -20,6 +20,16 @@ from gossip_util import K, KEYS, STRS, _host_round, _pack, _rand_diff, _same_dif
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=[2, 0], ids=["one_pass", "multi_pass"], autouse=True)
+def decode_form(request, eng):
+    """Every test under both decode forms: the one-pass small-body kernel
+    (codec.small = 2: always) and the multi-pass form (0)."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"codec.small", request.param)
+    yield request.param
+    _lib.call("crdt_set_option", b"codec.small", 1)
+
+
 def _serve(diff) -> bytes:
     """The binary gossip body of a Diff (host-only Server: main.go:153-170)."""
     s = Server(None, 8080)
@@ -201,3 +211,41 @@ def test_decode_short_string_order_and_interning(eng):
     b3 = slice(int(r_kv[r_off[3]]), int(r_kv[r_off[4]]))
     assert np.array_equal(kv[b0], kv[b3])
     assert np.array_equal(kk[b0] - 0, kk[b3] - 3000)               # key ids rebased into each body's slot range
+
+
+def test_decode_large_bodies_both_forms_agree(eng, decode_form):
+    """Bodies past one chunk of the one-pass kernel (8192 items per round of
+    its scans; 20k entries / ~60k pairs) and a body at an odd byte offset:
+    the same ids, ranges and flags from both forms, equal to the host ingest."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng(11)
+    bodies = []
+    for n in (20_000, 3, 9_000):
+        d, t = {}, 5
+        for _ in range(n):
+            t += int(rng.integers(1, 4))
+            d[t] = {f"k{int(q)}": str(int(rng.integers(-99, 99))) for q in rng.choice(40, int(rng.integers(0, 6)), replace=False)}
+        bodies.append(_serve(d))
+    bodies.insert(1, _raw_body([(1, [(b"a", b"1")])]) + b"")     # shifts the next body off 8-byte alignment
+    out = []
+    for form in (0, 2):
+        _lib.call("crdt_set_option", b"codec.small", form)
+        keys, vals = codec.StrTab(eng), codec.StrTab(eng)
+        dec, st, kk, kv = _decode(eng, bodies, keys, vals)
+        h = {x: dec[x].cpu().numpy() for x in ("r_off", "r_ts", "r_kv")}
+        ks, vs = keys.strings(), vals.strings()
+        # ids follow the claim races: compare the strings they resolve to
+        pairs = [(ks[kk[q] - 1000 * bi], vs[kv[q]]) for bi in range(len(bodies))
+                 for q in range(h["r_kv"][h["r_off"][bi]], h["r_kv"][h["r_off"][bi + 1]])]
+        out.append((st.tolist(), h, pairs, sorted(ks), sorted(vs)))
+    _lib.call("crdt_set_option", b"codec.small", decode_form)
+    a, b = out
+    assert a[0] == b[0] == [0, 0, 0, 0]
+    for x in a[1]:
+        np.testing.assert_array_equal(a[1][x], b[1][x], err_msg=x)
+    assert a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+    r_off, r_ts = a[1]["r_off"], a[1]["r_ts"]
+    host = Server(None, 9000)
+    assert host.IngestBinary(bodies[0]) == 0
+    assert r_ts[r_off[0]:r_off[1]].tolist() == host.RemoteDiff.Keys()
+    host.close()

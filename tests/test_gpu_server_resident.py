@@ -164,3 +164,52 @@ def test_self_pull_round_trip(eng, wire):
         assert s.AddCommand(200, {"k1": "-13"}) == pyref.add_command(diff, state, 200, {"k1": "-13"})
         assert s.CurrentState == state
     s.close()
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_resident_state_updates_and_double_pulls(eng, seed):
+    """Merges with no AddCommand in between (CurrentState updated only where
+    the device's per-key words changed, server.hip apply_state), pulls that
+    grow the key set, a second pull before the merge (the first one's upload
+    started at ingest, then parsed on the host) and empty pulls: CurrentState
+    and the Diff == pyref after every merge."""
+    rng = np.random.default_rng(seed)
+    P = 3
+    keys = KEYS + [f"n{i}" for i in range(8)]
+    model = [({}, {}) for _ in range(P)]
+    srv = [Server(eng, 8080 + i) for i in range(P)]
+    peers_src = [Server(None, 9100 + i) for i in range(P)]           # host-only peers serving pulls
+    clock = 5_000
+    for rnd in range(8):
+        remotes = []
+        for i in range(P):
+            pulls = []
+            for _ in range(1 if rnd % 3 else 2):                     # every third round: two pulls before the merge
+                p = peers_src[i] if rnd != 4 else Server(None, 9200)   # round 4: empty pulls
+                for _ in range(int(rng.integers(0, 6)) if rnd != 4 else 0):
+                    clock += int(rng.integers(1, 4))
+                    ks = rng.choice(len(keys) if rnd > 2 else 6, int(rng.integers(1, 3)), replace=False)
+                    p.Diff.Put(clock, {keys[int(q)]: VALS[int(rng.integers(0, len(VALS)))] for q in ks})
+                st, body = p.GossipBinary()
+                assert st == 200
+                assert srv[i].IngestBinary(body) == 0
+                pulls.append({t: dict(p.Diff.Get(t)[0]) for t in p.Diff.Keys()})
+                if rnd == 4:
+                    p.close()
+            rem = {}
+            for pl in pulls:                                         # RemoteDiff.Put: the later pull wins
+                rem.update(pl)
+            remotes.append(rem)
+        if rnd % 2 == 0:
+            merge_servers(srv)
+        else:
+            for s in srv:
+                s.merge()
+        for i in range(P):
+            model[i] = pyref.merge(model[i][0], remotes[i])
+            assert srv[i].CurrentState == model[i][1], f"round {rnd} replica {i}"
+        if rnd % 4 == 3:
+            for i in range(P):
+                assert srv[i].DiffSignature == _sig(model[i][0]), f"round {rnd} replica {i}"
+    for s in srv + peers_src:
+        s.close()
