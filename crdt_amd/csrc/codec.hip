@@ -315,32 +315,45 @@ __device__ __forceinline__ void dec_small(DecodeCtx c, int64_t *__restrict__ r_t
     bool bad = false, host = false;
     uint64_t carry = 0;
     if (!entries) {
-    // pairs: klen and the scan of klen + vlen into boff.  Each
-    // thread takes kSmallR consecutive items of a chunk (its own prefix in
-    // registers): one workgroup scan per chunk of kSmallT * kSmallR items
+    // pairs: klen and the scan of klen + vlen into boff.  Each thread takes
+    // kSmallR consecutive items of a chunk (its own prefix in registers): one
+    // workgroup scan per chunk of kSmallT * kSmallR items.  The next chunk's
+    // loads are issued before this chunk's stores, so the wait for them does
+    // not also wait for the stores (one memory counter covers both).
     const uint8_t *pk = base + 12 * d.ne, *pv = pk + 4 * d.np;
-    for (uint64_t c0 = 0; c0 < d.np; c0 += (uint64_t)kSmallT * kSmallR) {
+    constexpr uint64_t CH = (uint64_t)kSmallT * kSmallR;
+    uint32_t kl[kSmallR], vl[kSmallR];
+    auto load = [&](uint64_t c0) {
         const uint64_t i0 = c0 + (uint64_t)tid * kSmallR;
-        uint32_t t[kSmallR];
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            const bool in = i0 + r < d.np;
+            kl[r] = in ? ld32(pk + 4 * (i0 + r)) : 0;
+            vl[r] = in ? ld32(pv + 4 * (i0 + r)) : 0;
+        }
+    };
+    if (d.np) load(0);
+    for (uint64_t c0 = 0; c0 < d.np; c0 += CH) {
+        const uint64_t i0 = c0 + (uint64_t)tid * kSmallR;
+        uint32_t t[kSmallR], k0[kSmallR];
         uint64_t sum = 0;
 #pragma unroll
         for (int r = 0; r < kSmallR; ++r) {
-            const uint64_t q = i0 + r;
-            t[r] = 0;
-            if (q < d.np) {
-                const uint32_t kl = ld32(pk + 4 * q), vl = ld32(pv + 4 * q);
-                const uint64_t x = (uint64_t)kl + vl;
-                if (x > 0xFFFFFFFFull) bad = true;
-                else t[r] = (uint32_t)x;
-                klen[d.q0 + q] = kl;
-            }
+            const uint64_t x = (uint64_t)kl[r] + vl[r];
+            if (x > 0xFFFFFFFFull) bad = true;
+            t[r] = x > 0xFFFFFFFFull ? 0u : (uint32_t)x;
+            k0[r] = kl[r];
             sum += t[r];
         }
         uint64_t tot;
         uint64_t run = carry + block1024_exclusive_scan(sum, &tot, wsum);
+        if (c0 + CH < d.np) load(c0 + CH);
 #pragma unroll
         for (int r = 0; r < kSmallR; ++r) {
-            if (i0 + r < d.np) boff[d.q0 + i0 + r] = d.y0 + run;
+            if (i0 + r < d.np) {
+                klen[d.q0 + i0 + r] = k0[r];
+                boff[d.q0 + i0 + r] = d.y0 + run;
+            }
             run += t[r];
         }
         carry += tot;

@@ -14,3 +14,8 @@ cat gpurun_out/final/bench_default.json
 timeout -k 10 300 python bench.py --workload server_merge --steps 50 --warmup 5 --no-e2e --cpu-seconds 3 \
     > gpurun_out/final/bench_server_merge.json 2> gpurun_out/final/bench_server_merge.err || exit 1
 timeout -k 10 700 bash tools/profile.sh shard_fold || exit 1
+CRDT_SRV_PROF=1 timeout -k 10 120 python -u tools/server_prof.py 5 > gpurun_out/final/srv_prof5.txt 2> gpurun_out/final/srv_prof5.err || exit 1
+grep srv_ingest gpurun_out/final/srv_prof5.err | tail -5; tail -2 gpurun_out/final/srv_prof5.err
+timeout -k 10 200 python bench.py --workload gossip_round_wire --steps 10 --warmup 2 --no-e2e --no-cpu-baseline > gpurun_out/final/bench_wire.json 2> gpurun_out/final/bench_wire.err || exit 1
+timeout -k 10 600 bash tools/server_cross.sh > gpurun_out/final/server_cross.txt 2>&1 || exit 1
+cat gpurun_out/final/server_cross.txt

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Server.merge() end to end against the C restatement on the host's CPU share, by replica count.
-O=gpurun_out/srv_cross; mkdir -p $O
+O=${SRV_CROSS_OUT:-gpurun_out/srv_cross}; mkdir -p $O
 for r in 5 20 64 160; do
   timeout -k 10 240 python bench.py --workload server_merge --demo-replicas $r --steps 20 --warmup 3 --cpu-seconds 4 --no-e2e > $O/r$r.json 2> $O/r$r.err || { tail -3 $O/r$r.err; exit 1; }
   python - $O/r$r.json $r <<'PY'
