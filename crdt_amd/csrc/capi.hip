@@ -24,6 +24,7 @@ int g_rm_parts = 1;
 int g_rm_count_dma = 1;
 int g_dec_small = 1;
 int g_rm_kvx = 0;
+int g_rm_ld_all = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_rdd_diag = 0;
@@ -319,6 +320,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sets.or_parts")) {     // OR-Set write-pass workgroups per 2048-item tile
         if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
         g_or_parts = (int)v;
+    } else if (!strcmp(name, "refmerge.load_all")) {   // tile pass loads non-emitted entries too (A/B)
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_rm_ld_all = (int)v;
     } else if (!strcmp(name, "refmerge.kv_one_launch")) {   // kv tile pass: both tile kinds in one launch at any grid
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_rm_kvx = (int)v;

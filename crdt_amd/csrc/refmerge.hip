@@ -573,6 +573,7 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
 }
 
 enum { RM_FOLD_NONE = 0, RM_FOLD_FULL = 1, RM_FOLD_DELTA = 2 };
+constexpr int kDiagLoadAll = 256;          // diag bit: load every in-tile entry (refmerge.load_all A/B)
 
 // Pass 2, one workgroup per tile, in merge order: wave w's lanes take merge
 // items k = 64 (w + NWV i) + lane (i < FI), so each load instruction covers 64
@@ -729,7 +730,9 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
     uint8_t e_org[FI];
 #pragma unroll
     for (int f = 0; f < FI; ++f) {                       // every entry load issued before the first use
-        const bool in_tile = it_in(f), il = it_l(f);
+        // (only emitted entries are written or folded: an R entry whose ts L
+        // already holds loads nothing)
+        const bool in_tile = it_in(f) && ((diag & kDiagLoadAll) || it_em(f)), il = it_l(f);
         const uint64_t gi = it_gi(f);
         const uint64_t *kv = (il ? in.l_kv : in.r_kv) + gi;
         e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
@@ -898,7 +901,7 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
         }
     }
     __syncthreads();
-    if (diag == 2) return;
+    if ((diag & 255) == 2) return;
     for (int h = threadIdx.x; h < TT; h += WT) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;
@@ -1332,9 +1335,10 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     }
     // the tile pass: slice write and (with slots) the replay fold
     const unsigned tg = (unsigned)tmax;
+    const int lda = g_rm_ld_all ? kDiagLoadAll : 0;
     const KvOut kvo = kv ? KvOut{kv->kv_off, kv->kv_key, kv->kv_val, kv->kv_cap, ikv, tone} : KvOut{};
     if (delta && ns) {                                            // incremental replay: fold only the inserted R
-        k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, 0, ic, out, *delta, cand, cand_n,
+        k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, lda, ic, out, *delta, cand, cand_n,
                                                    ovf, ctx->dev_status);
         rc = check_launch(ctx);
         if (rc) return rc;
@@ -1355,16 +1359,16 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
                                                   crdt_replay_state{}, nullptr, nullptr, nullptr, ctx->dev_status)
     // (the kv output needs the whole tile in one workgroup: refmerge.tile_parts ignored)
     if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
-        if (kv) RM_TILE(RM_FOLD_NONE, 1, true, 0);
-        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, false, 0);
-        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, false, 0);
-        else RM_TILE(RM_FOLD_NONE, 1, false, 0);
+        if (kv) RM_TILE(RM_FOLD_NONE, 1, true, lda);
+        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, false, lda);
+        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, false, lda);
+        else RM_TILE(RM_FOLD_NONE, 1, false, lda);
         if (!ns || delta) return check_launch(ctx);
     } else {
-        if (kv) RM_TILE(RM_FOLD_FULL, 1, true, g_rm_diag);
-        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_FULL, 2, false, g_rm_diag);
-        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_FULL, 4, false, g_rm_diag);
-        else RM_TILE(RM_FOLD_FULL, 1, false, g_rm_diag);
+        if (kv) RM_TILE(RM_FOLD_FULL, 1, true, g_rm_diag | lda);
+        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_FULL, 2, false, g_rm_diag | lda);
+        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_FULL, 4, false, g_rm_diag | lda);
+        else RM_TILE(RM_FOLD_FULL, 1, false, g_rm_diag | lda);
     }
 #undef RM_TILE
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);
