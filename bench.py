@@ -915,7 +915,7 @@ class GossipRoundWire(GossipRound):
     and materialises the next Diffs.  Each step restarts from the same
     population and the same bodies."""
     name = "gossip_round_wire"
-    kernel = "gossip round from wire bodies (crdt_gossip_decode + refmerge + Diff materialisation)"
+    kernel = "gossip round from wire bodies through crdt_population_round_wire (device decode + refmerge + kv output)"
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         from crdt_amd import codec, gossip, synth
@@ -924,7 +924,11 @@ class GossipRoundWire(GossipRound):
         host = {"replicas": replicas, "l_off": h["l_off"], "l_ts": h["l_ts"], "l_origin": h["l_origin"],
                 "l_kv": h["l_kv"], "kv_key": h["kv_key"].view(np.uint32)[:n_l], "kv_val": h["kv_val"].view(np.uint32)[:n_l],
                 "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
-        self.pop = gossip.Population(eng, host, 62)
+        # the wire round behind the C-ABI (crdt_population_round_wire: decode +
+        # merge in one call, what a cgo host of main.go:226-261 binds);
+        # CRDT_GOSSIP_IMPL=python: Population.round_wire over the same kernels
+        self.native = os.environ.get("CRDT_GOSSIP_IMPL", "native") != "python"
+        self.pop = gossip.NativePopulation(eng, host, 62) if self.native else gossip.Population(eng, host, 62)
         self.host, self.P, self.n_l, self.gossip = h, replicas, n_l, gossip
         names = [c.encode() for c in synth.ALPHABET]
         self.keys, self.vals = codec.StrTab(eng), codec.StrTab(eng)
@@ -941,11 +945,16 @@ class GossipRoundWire(GossipRound):
         self.data = torch.frombuffer(bytearray(b"".join(bodies)), dtype=torch.uint8).to(eng.device)
         self.n_e = sum(codec.body_counts(b)[0] for b in bodies)
         self.n_p = sum(codec.body_counts(b)[1] for b in bodies)
-        self.init = self.pop.snapshot()
-        self.str0 = (self.pop.str_bytes, self.pop.str_off)
-        out = self.step()
-        torch.cuda.synchronize()
-        self.n_out = int(out["off"][-1].item())
+        if self.native:
+            self.pop.round_wire(self.data, self.body_off, self.keys, self.vals)
+            self.n_out = self.pop.sizes()[1]
+            self.pop.undo()
+        else:
+            self.init = self.pop.snapshot()
+            self.str0 = (self.pop.str_bytes, self.pop.str_off)
+            out = self.step()
+            torch.cuda.synchronize()
+            self.n_out = int(out["off"][-1].item())
         self.config = {"workload": f"gossip round from the wire: {replicas} replicas x {entries} Diff entries each "
                                    "pull a random peer's Diff as a binary gossip body in HBM, device decode + "
                                    "batched merge (BASELINE configs[0] shape at scale)",
@@ -962,6 +971,10 @@ class GossipRoundWire(GossipRound):
         return self.body_bytes + n_r * 24 + (self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17) + n_out * 24
 
     def step(self):
+        if self.native:                       # the same round from the same Diffs every step
+            self.pop.round_wire(self.data, self.body_off, self.keys, self.vals)
+            self.pop.undo()
+            return None
         self.pop.restore(self.init)
         self.pop.str_bytes, self.pop.str_off = self.str0
         return self.pop.round_wire(self.data, self.body_off.tolist(), self.keys, self.vals, self.n_e, self.n_p)

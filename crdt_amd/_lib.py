@@ -272,6 +272,7 @@ SIGNATURES = {
     "crdt_population_undo": (_I, [_P]),
     "crdt_population_add_commands": (_I, [_P, C.POINTER(crdt_population_cmds), _P]),
     "crdt_population_round_sharded": (_I, [_P, C.POINTER(_P), _P, _U64]),
+    "crdt_population_round_wire": (_I, [_P, _P, _P, _P, _P, _P]),
     "crdt_synth_counters": (_I, [_CTX, _U64, C.c_uint32, _P, _SZ, _U64]),
     "crdt_synth_vclock_pairs": (_I, [_CTX, _U64, _P, _P, _SZ, _SZ, _U64]),
     "crdt_synth_set_tuples": (_I, [_CTX, _U64, C.c_uint32, C.POINTER(crdt_tuples), _SZ, _U64]),

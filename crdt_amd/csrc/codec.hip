@@ -806,6 +806,34 @@ extern "C" int crdt_strtab_get(const crdt_strtab *t, uint64_t id, const char **p
 }
 
 namespace crdt {
+// The first 32 bytes of each body (zeros for a shorter one) to host memory:
+// one gather kernel, one read-back.  Synchronises.
+int gossip_headers(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
+                   uint8_t *hdr) {
+    if (nb == 0) return CRDT_OK;
+    const hipStream_t s = ctx->stream;
+    int rc = ws_reserve(ctx, Carve::round(nb * 16) + Carve::round(32 * (size_t)nb) + 512);
+    if (!rc) rc = hio_reserve(ctx, (size_t)nb * 16 + 32 * (size_t)nb);
+    if (rc) return rc;
+    Carve w0(ctx->ws);
+    uint64_t *d_al = w0.take<uint64_t>(2 * (size_t)nb);
+    uint8_t *d_hdr = w0.take<uint8_t>(32 * (size_t)nb);
+    uint64_t *h_al = (uint64_t *)ctx->hio;
+    memcpy(h_al, at, nb * 8);
+    memcpy(h_al + nb, len, nb * 8);
+    hipError_t e = hipMemcpyAsync(d_al, h_al, nb * 16, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    k_gather_headers<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(data, d_al, d_al + nb, nb, d_hdr);
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    uint8_t *h_hdr = (uint8_t *)ctx->hio + (size_t)nb * 16;
+    e = hipMemcpyAsync(h_hdr, d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    memcpy(hdr, h_hdr, 32 * (size_t)nb);
+    return CRDT_OK;
+}
+
 static size_t decode_ws_need(uint32_t nb, uint64_t n_e, uint64_t n_p) {
     const size_t head = Carve::round(nb * sizeof(BodyDesc)) + Carve::round(nb * 8) + 64;
     return Carve::round(head) + Carve::round((n_e + 1) * 4) + Carve::round((n_e + 1) * 8) +
@@ -837,27 +865,13 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     hipError_t e;
     // headers (32 B per body) to the host in one gather + one copy: the sizes
     // the decode is planned with
+    std::vector<uint8_t> hdr_buf;
     const uint8_t *hdr = host_hdr;
     if (!hdr) {
-        rc = ws_reserve(ctx, Carve::round(nb * 16) + Carve::round(32 * (size_t)nb) + 512);
-        if (!rc) rc = hio_reserve(ctx, (size_t)nb * 16 + 32 * (size_t)nb);
+        hdr_buf.resize(32 * (size_t)nb);
+        rc = gossip_headers(ctx, nb, data, at, len, hdr_buf.data());
         if (rc) return rc;
-        Carve w0(ctx->ws);
-        uint64_t *d_al = w0.take<uint64_t>(2 * (size_t)nb);
-        uint8_t *d_hdr = w0.take<uint8_t>(32 * (size_t)nb);
-        uint64_t *h_al = (uint64_t *)ctx->hio;
-        memcpy(h_al, at, nb * 8);
-        memcpy(h_al + nb, len, nb * 8);
-        e = hipMemcpyAsync(d_al, h_al, nb * 16, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return hip_fail(ctx, e);
-        k_gather_headers<<<grid_for(nb, 256, 1u << 30), 256, 0, s>>>(data, d_al, d_al + nb, nb, d_hdr);
-        rc = check_launch(ctx);
-        if (rc) return rc;
-        uint8_t *h_hdr = (uint8_t *)ctx->hio + (size_t)nb * 16;
-        e = hipMemcpyAsync(h_hdr, d_hdr, 32 * (size_t)nb, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(ctx, e);
-        hdr = h_hdr;
+        hdr = hdr_buf.data();
     }
     std::vector<BodyDesc> bd(nb);
     std::vector<uint64_t> r_off(nb + 1, 0);

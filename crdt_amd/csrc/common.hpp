@@ -108,6 +108,9 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
                      crdt_strtab *keys, crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status,
                      const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale);
 size_t gossip_decode_scratch_bytes(uint32_t nb, uint64_t n_e, uint64_t n_p);
+// codec.hip: the first 32 bytes of each body (zeros if shorter) into host hdr[32 nb].  Synchronises.
+int gossip_headers(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
+                   uint8_t *hdr);
 
 // shard.hip: the communicator's collective transport for other protocols
 // (population.hip's sharded rounds).  One point-to-point transfer of a group:

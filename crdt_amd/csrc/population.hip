@@ -61,6 +61,10 @@ struct crdt_population {
     uint8_t *str_bytes = nullptr;
     uint64_t *str_off = nullptr;
     uint64_t n_str = 0;
+    // after the first wire round: the value table the pulls were interned
+    // into IS the string arena (its first n_str strings checked equal to the
+    // population's own, which are then freed); refreshed before every use
+    crdt_strtab *vtab = nullptr;
     uint8_t *st_kind[2] = {nullptr, nullptr};  // CurrentState, double-buffered with the Diffs
     uint32_t *st_str[2] = {nullptr, nullptr};
     int64_t *st_sum[2] = {nullptr, nullptr};
@@ -181,6 +185,18 @@ int diff_reserve(crdt_population *pop, crdt_population::Diff &d, size_t cap_e, s
     return rc;
 }
 
+// the value arena of a population that adopted a table (the table may have
+// grown or moved since the last call)
+void pop_arena(crdt_population *pop) {
+    if (!pop->vtab) return;
+    uint64_t nb = 0;
+    const uint8_t *b = nullptr;
+    const uint64_t *o = nullptr;
+    (void)crdt_strtab_info(pop->vtab, &pop->n_str, &nb, &b, &o);
+    pop->str_bytes = const_cast<uint8_t *>(b);           // (borrowed: freed by the table)
+    pop->str_off = const_cast<uint64_t *>(o);
+}
+
 // CurrentState of the replicas whose peer was dead: put back after the batched merge rebuilt it
 __global__ void k_pop_keep_state(const uint8_t *__restrict__ skip, uint32_t K, uint64_t n_slots,
                                  const uint8_t *__restrict__ ok, const uint32_t *__restrict__ os,
@@ -274,6 +290,7 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
     crdt_ctx *ctx = pop->ctx;
     const uint32_t P = pop->P;
     if (P == 0) return CRDT_OK;                          // (a rank that holds no replica merges nothing)
+    pop_arena(pop);
     auto &nd = pop->d[1 - pop->cur];
     int rc = diff_reserve(pop, nd, pop->n_e + h.n_r, pop->n_kv + h.n_rkv, false);
     if (rc) return rc;
@@ -346,6 +363,7 @@ int pop_commit(crdt_population *pop) {
 }
 
 bool pop_valid(const crdt_population *p) { return p && p->ctx && p->d[p->cur].off; }
+
 
 // host prefix of a count vector
 std::vector<uint64_t> prefix(const std::vector<uint64_t> &c) {
@@ -437,7 +455,10 @@ extern "C" int crdt_population_destroy(crdt_population *pop) {
     for (int b = 0; b < 2; ++b)
         for (void *p : {(void *)pop->st_kind[b], (void *)pop->st_str[b], (void *)pop->st_sum[b]})
             if (p) (void)hipFree(p);
-    for (void *p : {(void *)pop->str_bytes, (void *)pop->str_off, pop->dsm, pop->xb})
+    if (!pop->vtab)
+        for (void *p : {(void *)pop->str_bytes, (void *)pop->str_off})
+            if (p) (void)hipFree(p);
+    for (void *p : {pop->dsm, pop->xb})
         if (p) (void)hipFree(p);
     if (pop->pin) (void)hipHostFree(pop->pin);
     delete pop;
@@ -555,6 +576,7 @@ extern "C" int crdt_population_add_commands(crdt_population *pop, const crdt_pop
     if (!pop_valid(pop) || !c || !c->c_off) return CRDT_E_INVAL;
     int rc = bind(pop->ctx);
     if (rc) return rc;
+    pop_arena(pop);
     const uint32_t P = pop->P;
     if (c->c_off[0] != 0) return CRDT_E_INVAL;
     for (uint32_t p = 0; p < P; ++p)
@@ -672,6 +694,111 @@ extern "C" int crdt_population_round(crdt_population *pop, const int64_t *peers)
     rc = upload_round(pop, h, &a);
     const auto &cd = pop->d[pop->cur];
     if (!rc) rc = pop_merge(pop, a, h, cd.ts, cd.kv_off, pop->n_kv);
+    if (rc) return rc;
+    return pop_commit(pop);
+}
+
+// One synchronous round whose pulls arrive on the wire (main.go:226-258 with
+// the Gossip body of main.go:159 in its binary form): body i =
+// bodies[body_off[i], body_off[i+1]) in device memory is local replica i's
+// pulled Diff; an empty body is a failed GET (the round skipped for i,
+// main.go:234-239).  The bodies are decoded on the device against the
+// context's string tables (keys: key id k of replica i -> slot i*K + k, ids
+// below K; vals: the value ids, whose arena becomes the population's), their
+// pairs behind the current Diff's in its kv arena, then merged as in
+// crdt_population_round.  A body the device decode does not take (malformed,
+// a nil map, unsorted, a key id >= K) fails the call with CRDT_E_UNSORTED and
+// its status in body_status[i] (host, P words; 0 = taken): nothing is merged.
+// The first wire round checks that vals holds the population's strings at
+// their ids (intern them first) and adopts its arena.  Synchronises.
+extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *keys, crdt_strtab *vals,
+                                          const uint8_t *bodies, const uint64_t *body_off, uint32_t *body_status) {
+    if (!pop_valid(pop) || !keys || !vals || !body_status || (!body_off && pop->P)) return CRDT_E_INVAL;
+    int rc = bind(pop->ctx);
+    if (rc) return rc;
+    const uint32_t P = pop->P;
+    if (P == 0) return CRDT_OK;
+    crdt_ctx *ctx = pop->ctx;
+    if (!bodies && body_off[P] > body_off[0]) return CRDT_E_INVAL;
+    if (pop->vtab && pop->vtab != vals) return CRDT_E_INVAL;
+    if (!pop->vtab) {                                    // adopt vals' arena: its first n_str strings must agree
+        uint64_t nv = 0, nbv = 0;
+        (void)crdt_strtab_info(vals, &nv, &nbv, nullptr, nullptr);
+        if (nv < pop->n_str) return CRDT_E_INVAL;
+        std::vector<uint64_t> off(pop->n_str + 1);
+        hipError_t e = hipMemcpy(off.data(), pop->str_off, off.size() * 8, hipMemcpyDeviceToHost);
+        std::vector<uint8_t> bytes(off.back() - off[0]);
+        if (e == hipSuccess && !bytes.empty())
+            e = hipMemcpy(bytes.data(), pop->str_bytes + off[0], bytes.size(), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        for (uint64_t i = 0; i < pop->n_str; ++i) {
+            const char *q = nullptr;
+            size_t qn = 0;
+            if (crdt_strtab_get(vals, i, &q, &qn) != CRDT_OK || qn != off[i + 1] - off[i] ||
+                (qn && memcmp(q, bytes.data() + (off[i] - off[0]), qn) != 0))
+                return CRDT_E_INVAL;
+        }
+    }
+    std::vector<uint64_t> at(P), len(P);
+    for (uint32_t i = 0; i < P; ++i) {
+        if (body_off[i + 1] < body_off[i]) return CRDT_E_INVAL;
+        at[i] = body_off[i];
+        len[i] = body_off[i + 1] - body_off[i];
+    }
+    // sizes from the headers: the decode's entries per body, pairs in total
+    std::vector<uint8_t> hdr(32 * (size_t)P);
+    rc = gossip_headers(ctx, P, bodies, at.data(), len.data(), hdr.data());
+    if (rc) return rc;
+    HostRound h(P);
+    std::vector<uint32_t> sbase(P);
+    uint64_t n_e = 0, n_p = 0;
+    for (uint32_t i = 0; i < P; ++i) {
+        uint64_t ne = 0, np = 0, nby = 0;
+        if (len[i] >= 32 && memcmp(&hdr[32 * i], "CRDTSOA1", 8) == 0) {
+            memcpy(&ne, &hdr[32 * i + 8], 8);
+            memcpy(&np, &hdr[32 * i + 16], 8);
+            memcpy(&nby, &hdr[32 * i + 24], 8);
+            if (ne > len[i] / 12 || np > len[i] / 8 || nby > len[i] || 32 + ne * 12 + np * 8 + nby != len[i])
+                ne = np = 0;                             // (malformed: the decode flags it)
+        }
+        h.r_off[i] = n_e;
+        h.r_end[i] = n_e + ne;
+        sbase[i] = (uint32_t)((uint64_t)i * pop->K);
+        if (len[i] == 0) {                               // a failed GET: no merge for i
+            h.skip[i] = 1;
+            h.any_skip = true;
+        }
+        n_e += ne;
+        n_p += np;
+    }
+    if (n_e >= 0xFFFFFFFFull) return CRDT_E_RANGE;
+    h.n_r = n_e;
+    h.n_rkv = n_p;
+    // the pulled pairs go behind the current Diff's own in its kv arena; the
+    // decoded entries into the exchange buffers
+    auto &cd = pop->d[pop->cur];
+    rc = diff_reserve(pop, cd, pop->n_e, pop->n_kv + n_p, true);
+    const size_t xb = Carve::round((P + 1) * 8) + Carve::round(n_e * 8 + 8) + Carve::round((n_e + 1) * 8) + 1024;
+    if (!rc) rc = dev_grow(ctx, &pop->xb, &pop->xb_bytes, xb);
+    if (rc) return rc;
+    Carve w(pop->xb);
+    uint64_t *r_off = w.take<uint64_t>(P + 1);
+    int64_t *r_ts = w.take<int64_t>(n_e + 1);
+    uint64_t *r_kv = w.take<uint64_t>(n_e + 1);
+    const crdt_gossip_decoded go{r_off, r_ts, r_kv, cd.kv_key, cd.kv_val};
+    rc = gossip_decode_at(ctx, P, bodies, at.data(), len.data(), pop->K, pop->n_kv, sbase.data(), hdr.data(), keys,
+                          vals, &go, body_status, nullptr, nullptr, 0, nullptr);
+    if (rc) return rc;
+    for (uint32_t i = 0; i < P; ++i)
+        if (body_status[i] && len[i]) return CRDT_E_UNSORTED;   // (nothing merged: the population is unchanged)
+    if (!pop->vtab) {                                    // the arena is vals' from now on
+        (void)dev_free(ctx, (void **)&pop->str_bytes);
+        (void)dev_free(ctx, (void **)&pop->str_off);
+        pop->vtab = vals;
+    }
+    RoundArrays a;
+    rc = upload_round(pop, h, &a);
+    if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p);
     if (rc) return rc;
     return pop_commit(pop);
 }

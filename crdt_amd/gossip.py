@@ -690,6 +690,28 @@ class NativePopulation:
         _lib.call("crdt_population_add_commands", self._h, C.byref(cmds), status.ctypes.data, ctx=self._ctx)
         return status[:len(keep[1])].astype(np.int64)
 
+    def round_wire(self, data, body_off, keys, vals) -> None:
+        """One round whose pulls arrive on the wire (crdt_population_round_wire):
+        body i = data[body_off[i]:body_off[i+1]] (a device uint8 tensor) is
+        replica i's pulled Diff in the binary gossip form, an empty body a
+        failed GET.  keys / vals: codec.StrTab of the key ids (< K) and value
+        ids (vals must hold this population's strings at their ids).
+        Raises CrdtError (CRDT_E_UNSORTED) with .body_status when a body is
+        not taken by the device decode; nothing is merged then."""
+        from . import _lib
+        bo = np.ascontiguousarray(np.asarray(body_off, dtype=np.uint64))
+        assert len(bo) == self.P + 1
+        st = np.zeros(max(self.P, 1), np.uint32)
+        if hasattr(self._owner, "_bind"):
+            self._owner._bind()
+        self._vtab = vals                      # (the population borrows its arena from now on)
+        try:
+            _lib.call("crdt_population_round_wire", self._h, keys._h, vals._h, data.data_ptr() if data.numel() else None,
+                      bo.ctypes.data, st.ctypes.data, ctx=self._ctx)
+        except _lib.CrdtError as err:
+            err.body_status = st[:self.P].copy()
+            raise
+
     def undo(self) -> None:
         """Back to the Diffs and CurrentState before the last round."""
         from . import _lib

@@ -559,6 +559,7 @@ int crdt_shard_refmerge(crdt_comm *comm, const crdt_refmerge_in *in, const crdt_
  * arena str_bytes / str_off [n_str + 1].  CurrentState starts empty
  * (NewServer with an empty initialState, main.go:102-105). */
 typedef struct crdt_population crdt_population;
+typedef struct crdt_strtab crdt_strtab;           /* (string tables: below, with the gossip decode) */
 typedef struct crdt_population_init {
     uint32_t replicas;
     uint32_t keys_per_replica;
@@ -618,6 +619,20 @@ int crdt_population_undo(crdt_population *pop);
  * Synchronises. */
 int crdt_population_round_sharded(crdt_comm *comm, crdt_population *const *pops, const int64_t *peers_all,
                                   uint64_t total);
+/* One round whose pulls arrive on the wire (main.go:226-258 with the
+ * Gossip body of main.go:159 in the binary form of crdt_server_gossip_binary):
+ * body i = bodies[body_off[i], body_off[i+1]) (device memory; body_off host,
+ * replicas + 1) is local replica i's pulled Diff, an empty body a failed GET
+ * (the round skipped for i, main.go:234-239).  Decoded on the device against
+ * the string tables (keys: key id k of replica i -> slot i*K + k, ids < K;
+ * vals: the value ids -- the first wire round checks that vals holds the
+ * population's strings at their ids and adopts its arena), the pulled pairs
+ * behind the current Diff's, then merged as crdt_population_round.  A body
+ * the device decode does not take (malformed, a nil map, unsorted, a key id
+ * >= K) fails the call with CRDT_E_UNSORTED, its status in body_status[i]
+ * (host, replicas words): nothing is merged.  Synchronises. */
+int crdt_population_round_wire(crdt_population *pop, crdt_strtab *keys, crdt_strtab *vals, const uint8_t *bodies,
+                               const uint64_t *body_off, uint32_t *body_status);
 
 /* ------------------------------------------------ synthetic state (bench/tests)
  * SplitMix64-seeded generators; identical to the numpy
@@ -697,7 +712,7 @@ int crdt_server_ingest_binary(crdt_server *srv, const char *data, size_t len, in
  * value arena the device gossip decode interns into.  A table belongs to one
  * device; calls that add strings synchronise and refresh a host mirror
  * (crdt_strtab_get). */
-typedef struct crdt_strtab crdt_strtab;
+/* (crdt_strtab: declared with crdt_population above) */
 int crdt_strtab_create(crdt_ctx *ctx, size_t cap_strings, size_t cap_bytes, crdt_strtab **out);
 int crdt_strtab_destroy(crdt_strtab *tab);
 /* counts and the device arena (bytes_dev / off_dev nullable): off_dev[0..n_str]

@@ -19,26 +19,26 @@ from oracle import pyref
 pytestmark = pytest.mark.gpu
 
 
-def _unpack_native(h, P):
+def _unpack_native(h, P, strs=STRS):
     out = []
     for i in range(P):
         d = {}
         for e in range(int(h["off"][i]), int(h["off"][i + 1])):
-            kv = {KEYS[int(h["kv_key"][q]) - i * K]: STRS[int(h["kv_val"][q])]
+            kv = {KEYS[int(h["kv_key"][q]) - i * K]: strs[int(h["kv_val"][q])]
                   for q in range(int(h["kv_off"][e]), int(h["kv_off"][e + 1]))}
             d[int(h["ts"][e])] = pyref.Command(kv) if h["origin"][e] else kv
         out.append(d)
     return out
 
 
-def _state_native(h, P):
+def _state_native(h, P, strs=STRS):
     out = []
     for i in range(P):
         st = {}
         for k in range(K):
             s = i * K + k
             if h["st_kind"][s] == 1:
-                st[KEYS[k]] = STRS[int(h["st_str"][s])]
+                st[KEYS[k]] = strs[int(h["st_str"][s])]
             elif h["st_kind"][s] == 2:
                 st[KEYS[k]] = str(int(h["st_sum"][s]))
         out.append(st)
@@ -211,5 +211,93 @@ def test_population_commands_over_the_per_call_limit(eng):
         h = pop.read()
         _same_diffs(_unpack_native(h, P), diffs)
         assert _state_native(h, P) == states
+    finally:
+        pop.close()
+
+
+def _wire_tables(eng):
+    from crdt_amd import codec
+    keys, vals = codec.StrTab(eng), codec.StrTab(eng)
+    assert keys.intern(KEYS).tolist() == list(range(K))            # key id = KEYS index
+    assert vals.intern(STRS).tolist() == list(range(len(STRS)))    # value id = the population's string id
+    return keys, vals
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_population_wire_rounds_match_reference_simulation(eng, seed):
+    """crdt_population_round_wire: every replica's pull arrives as a binary
+    gossip body in HBM (main.go:159, :245-256), decoded on the device and
+    merged == the pyref simulation; failed GETs (empty bodies) skip the
+    round, self-pulls rebuild CurrentState, a value the tables have not seen
+    is interned and lands in the population's arena (adopted from vals),
+    and AddCommand between wire rounds uses the same ids."""
+    from test_gpu_codec import _serve, _upload
+    from test_gpu_local_apply import _cmd_block
+    rng = np.random.default_rng(seed)
+    P = 7
+    diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 30))) for i in range(P)]
+    keys, vals = _wire_tables(eng)
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    try:
+        for rnd in range(6):
+            peers = (gossip.random_peers if rnd % 2 else gossip.reference_peers)(rng, P, 0, P)
+            pulls = [dict(diffs[q]) if q >= 0 else None for q in peers]
+            if rnd == 2:                                 # a value no table holds yet
+                t = 50_000 + rnd
+                pulls[0] = dict(pulls[0] or {})
+                pulls[0][t] = {KEYS[1]: "fresh-" + str(seed)}
+            bodies = [_serve(pl) if pl is not None else b"" for pl in pulls]
+            data, off = _upload(eng, bodies)
+            pop.round_wire(data, off, keys, vals)
+            strs = [x.decode() for x in vals.strings()]
+            for i in range(P):
+                if pulls[i] is None:
+                    continue                             # a failed GET: no merge (main.go:234-239)
+                diffs[i], states[i] = pyref.merge(diffs[i], {t: dict(v) for t, v in pulls[i].items()})
+            h = pop.read()
+            _same_diffs(_unpack_native(h, P, strs), diffs)
+            assert _state_native(h, P, strs) == states, f"round {rnd}"
+            if rnd == 3:                                 # AddCommand between wire rounds (main.go:173-215)
+                cmds, exp = [], []
+                for i in range(P):
+                    t0 = max(diffs[i]) if diffs[i] else 1_000
+                    mine = [(t0 + 1 + j, {KEYS[int(rng.integers(0, K))]: STRS[int(rng.integers(0, 12))]})
+                            for j in range(int(rng.integers(0, 3)))]
+                    exp += [pyref.add_command(diffs[i], states[i], t, d) for t, d in mine]
+                    cmds.append(mine)
+                np.testing.assert_array_equal(pop.add_commands(_cmd_block(cmds)), exp)
+    finally:
+        pop.close()
+
+
+def test_population_wire_round_refusals(eng):
+    """A body the device decode does not take (here: a nil map, and one
+    truncated) fails the round with CRDT_E_UNSORTED and its status, the
+    population unchanged; a value table that does not hold the population's
+    strings at their ids is refused before anything is decoded."""
+    from crdt_amd import _lib, codec
+    from test_gpu_codec import _raw_body, _serve, _upload
+    rng = np.random.default_rng(8)
+    P = 3
+    diffs = [_rand_diff(rng, 100 + i, 5) for i in range(P)]
+    keys, vals = _wire_tables(eng)
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    try:
+        before = pop.read()
+        good = _serve(diffs[1])
+        for bad in (_raw_body([(7, None)]), good[:-1]):
+            data, off = _upload(eng, [good, bad, good])
+            with pytest.raises(_lib.CrdtError) as ei:
+                pop.round_wire(data, off, keys, vals)
+            assert ei.value.body_status[1] != 0 and ei.value.body_status[0] == 0
+            after = pop.read()
+            for k in before:
+                np.testing.assert_array_equal(after[k], before[k], err_msg=k)
+        other = codec.StrTab(eng)
+        other.intern(list(reversed(STRS)))               # the same strings at other ids
+        data, off = _upload(eng, [good, good, good])
+        with pytest.raises(_lib.CrdtError):
+            pop.round_wire(data, off, keys, other)
     finally:
         pop.close()
