@@ -765,7 +765,7 @@ class RefMergeBatch(Workload):
 class RefMergeDelta(RefMergeBatch):
     """The same batch through the incremental replay:
     crdt_refmerge_delta folds only the inserted R entries into a carried
-    ts-keyed state.  Each step restores the state of L first (a 1.7 MB
+    ts-keyed state.  Each step restores the state of L first (one 1.7 MB
     device copy, inside the timed region) so every step is the same merge."""
     name = "refmerge_delta"
     kernel = "refmerge_delta (whole op: walk passes + k_rp_fold x2 + k_rp_final + state restore)"
@@ -775,8 +775,15 @@ class RefMergeDelta(RefMergeBatch):
 
     def __init__(self, eng, rank, world, replicas, entries, seed=2024):
         super().__init__(eng, rank, world, replicas, entries, seed)
-        self.st0 = eng.replay_state_init(self.dev)
-        self.st = {k: v.clone() for k, v in self.st0.items()}
+        # the five state arrays as views of one buffer: the restore is ONE copy
+        n = max(int(self.dev["n_slots"]), 1)
+        self.buf0 = torch.empty(28 * n, dtype=torch.uint8, device=eng.device)
+        self.buf = torch.empty_like(self.buf0)
+        views = lambda b: {"best_key": b[0:8 * n].view(torch.int64), "sum": b[8 * n:16 * n].view(torch.int64),
+                           "best_str": b[16 * n:20 * n].view(torch.int32), "npar": b[20 * n:24 * n].view(torch.int32),
+                           "nhold": b[24 * n:28 * n].view(torch.int32)}
+        self.st0 = eng.replay_state_init(self.dev, st=views(self.buf0))
+        self.st = views(self.buf)
         self.config["workload"] = self.config["workload"].replace("RefMerge", "RefMerge, incremental replay,", 1)
         h = self.host
         self.n_rkv = int(h["r_kv"][-1] - h["r_kv"][0])
@@ -787,8 +794,7 @@ class RefMergeDelta(RefMergeBatch):
                 + self.host["n_slots"] * (28 * 2 + 13) + int(self.host["str_off"][-1]))
 
     def step(self):
-        for k, v in self.st0.items():
-            self.st[k].copy_(v)
+        self.buf.copy_(self.buf0)
         self.eng.refmerge_delta(self.dev, self.st)
 
     def cpu_baseline(self, seconds, threads):

@@ -108,6 +108,10 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
                      crdt_strtab *keys, crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status,
                      const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale);
 size_t gossip_decode_scratch_bytes(uint32_t nb, uint64_t n_e, uint64_t n_p);
+// refmerge.hip: crdt_refmerge_batch_pull when every entry of L and of the
+// pulled ranges is known to hold exactly one kv pair
+int refmerge_batch_pull_one_pair(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                                 const crdt_refmerge_pull *pull, const crdt_refmerge_kv_out *kv);
 // codec.hip: the first 32 bytes of each body (zeros if shorter) into host hdr[32 nb].  Synchronises.
 int gossip_headers(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
                    uint8_t *hdr);

@@ -58,6 +58,13 @@ struct crdt_population {
     std::vector<uint64_t> pcnt, pkvcnt;        // ... of the Diffs before the last round (crdt_population_undo)
     size_t p_n_e = 0, p_n_kv = 0;
     bool can_undo = false;
+    // every entry of the current Diffs holds exactly one kv pair (the
+    // reference's load generator writes one key per command, main.go:282):
+    // rounds then size the kv output from entry counts alone
+    // (refmerge_batch_pull_one_pair).  Exact or false: set at creation from
+    // the host arrays, kept by local rounds, cleared by anything that may
+    // bring other entries (multi-pair commands, sharded and wire rounds).
+    bool one_pair = false, p_one_pair = false;
     uint8_t *str_bytes = nullptr;
     uint64_t *str_off = nullptr;
     uint64_t n_str = 0;
@@ -286,7 +293,7 @@ int upload_round(crdt_population *pop, const HostRound &h, RoundArrays *a) {
 // any imported behind them); the next Diffs and CurrentState into the spare
 // buffers; the read-back of their bounds into the pinned staging (async).
 int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, const int64_t *r_ts,
-              const uint64_t *r_kv, size_t n_arena) {
+              const uint64_t *r_kv, size_t n_arena, bool one_pair = false) {
     crdt_ctx *ctx = pop->ctx;
     const uint32_t P = pop->P;
     if (P == 0) return CRDT_OK;                          // (a rank that holds no replica merges nothing)
@@ -318,7 +325,8 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
                                 pop->st_sum[sn]};
     const crdt_refmerge_pull pull{a.r_end, a.sd};
     const crdt_refmerge_kv_out kv{nd.kv_off, nd.kv_key, nd.kv_val, nd.cap_kv};
-    rc = crdt_refmerge_batch_pull(ctx, &in, &out, &pull, &kv);
+    rc = one_pair ? refmerge_batch_pull_one_pair(ctx, &in, &out, &pull, &kv)
+                  : crdt_refmerge_batch_pull(ctx, &in, &out, &pull, &kv);
     if (rc) return rc;
     const uint64_t ns = (uint64_t)P * pop->K;
     if (h.any_skip && ns)
@@ -351,6 +359,7 @@ int pop_commit(crdt_population *pop) {
     pop->kvcnt.resize(P);
     pop->p_n_e = pop->n_e;
     pop->p_n_kv = pop->n_kv;
+    pop->p_one_pair = pop->one_pair;
     pop->can_undo = true;
     for (uint32_t p = 0; p < P; ++p) {
         pop->cnt[p] = hb[p + 1] - hb[p];
@@ -407,6 +416,8 @@ extern "C" int crdt_population_create(crdt_ctx *ctx, const crdt_population_init 
     pop->n_e = n_e;
     pop->n_kv = n_kv;
     pop->n_str = h->n_str;
+    pop->one_pair = true;
+    for (uint64_t e = 0; e < n_e && pop->one_pair; ++e) pop->one_pair = h->l_kv[e + 1] - h->l_kv[e] == 1;
     auto &d = pop->d[0];
     rc = diff_reserve(pop, d, n_e, n_kv, false);
     const uint64_t ns = (uint64_t)P * pop->K, nbytes = h->str_off[h->n_str];
@@ -594,6 +605,8 @@ extern "C" int crdt_population_add_commands(crdt_population *pop, const crdt_pop
             for (uint64_t q = c->c_kv[j]; q < c->c_kv[j + 1]; ++q)
                 if (c->kv_key[q] < (uint64_t)p * pop->K || c->kv_key[q] >= (uint64_t)(p + 1) * pop->K)
                     return CRDT_E_INVAL;
+    for (uint64_t j = 0; j < n_c && pop->one_pair; ++j)   // (cleared before any chunk lands)
+        if (c->c_kv[j + 1] - c->c_kv[j] != 1) pop->one_pair = false;
     uint64_t most = 0;
     for (uint32_t p = 0; p < P; ++p) most = std::max(most, c->c_off[p + 1] - c->c_off[p]);
     for (uint64_t r = 0; r * kLaMax < most; ++r) {       // chunk r: the commands r*kLaMax .. of every replica
@@ -623,6 +636,7 @@ extern "C" int crdt_population_undo(crdt_population *pop) {
     pop->kvcnt.swap(pop->pkvcnt);
     pop->n_e = pop->p_n_e;
     pop->n_kv = pop->p_n_kv;
+    pop->one_pair = pop->p_one_pair;
     pop->cur = 1 - pop->cur;
     pop->can_undo = false;
     return CRDT_OK;
@@ -693,9 +707,9 @@ extern "C" int crdt_population_round(crdt_population *pop, const int64_t *peers)
     RoundArrays a;
     rc = upload_round(pop, h, &a);
     const auto &cd = pop->d[pop->cur];
-    if (!rc) rc = pop_merge(pop, a, h, cd.ts, cd.kv_off, pop->n_kv);
+    if (!rc) rc = pop_merge(pop, a, h, cd.ts, cd.kv_off, pop->n_kv, pop->one_pair);   // (pulls: this population's own Diffs)
     if (rc) return rc;
-    return pop_commit(pop);
+    return pop_commit(pop);                              // (one_pair kept: entries of one-pair Diffs)
 }
 
 // One synchronous round whose pulls arrive on the wire (main.go:226-258 with
@@ -800,7 +814,9 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     rc = upload_round(pop, h, &a);
     if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p);
     if (rc) return rc;
-    return pop_commit(pop);
+    rc = pop_commit(pop);
+    if (!rc) pop->one_pair = false;                      // (the pulled bodies' entries: not checked)
+    return rc;
 }
 
 // One synchronous round over a communicator: member i's population holds
@@ -1018,6 +1034,7 @@ extern "C" int crdt_population_round_sharded(crdt_comm *c, crdt_population *cons
     for (size_t i = 0; i < M; ++i) {
         rc = pop_commit(pops[i]);
         if (rc) return rc;
+        pops[i]->one_pair = false;                       // (entries from other ranks' Diffs: not checked)
     }
     return CRDT_OK;
 }

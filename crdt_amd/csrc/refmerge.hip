@@ -445,7 +445,8 @@ template <int NT, bool KV = false>
 __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                  uint32_t *__restrict__ tcnt, uint64_t *__restrict__ bits,
                                                  uint32_t *__restrict__ zero, int dma, uint64_t *__restrict__ tkv,
-                                                 uint32_t *__restrict__ tone, uint32_t *__restrict__ err) {
+                                                 uint32_t *__restrict__ tone, uint32_t *__restrict__ err,
+                                                 int one_pair = 0) {
     constexpr int NI = MT / NT, LPW = 64 / NI;           // items per thread, lanes per bitmap word
     static_assert(NI * LPW == 64, "a bitmap word is LPW lanes' items");
     __shared__ alignas(16) int64_t sm[MT + 8];           // (DMA: each run from its 16-byte aligned-down start)
@@ -489,7 +490,9 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
     if (k0 < k1) ia0 = thread_merge(SA, SB, d.lprev, na, nb, k0, k1, d.has_prev, d.maxl, &isl, &emit);
     uint64_t ks = 0;                                     // KV: kv pairs of the tile's emitted entries
     int one = 1;                                         // KV: every emitted entry has exactly one pair
-    if (KV) {
+    if (KV && one_pair) {                                // (the caller's invariant: one pair per entry)
+        ks = (uint64_t)__popc(emit);
+    } else if (KV) {
         // the merge marks its emitted R entries by R index in LDS; then the
         // kv ranges are read in index order (coalesced, all loads in flight):
         // every L entry of the tile, the marked R entries
@@ -1177,7 +1180,21 @@ extern "C" int crdt_atoi_batch(crdt_ctx *ctx, const uint8_t *bytes, const uint64
 
 static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
                         const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta,
-                        const crdt_refmerge_kv_out *kv = nullptr, const crdt_refmerge_pull *pull = nullptr);
+                        const crdt_refmerge_kv_out *kv = nullptr, const crdt_refmerge_pull *pull = nullptr,
+                        bool one_pair = false);
+
+namespace crdt {
+// crdt_refmerge_batch_pull for a caller that knows every entry of L and of
+// the pulled ranges has exactly one kv pair (population.hip tracks it): the
+// kv count pass takes each tile's pair count from its emitted count instead
+// of reading every entry's kv range, and the tile pass runs as one-pair
+// tiles only.
+int refmerge_batch_pull_one_pair(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
+                                 const crdt_refmerge_pull *pull, const crdt_refmerge_kv_out *kv) {
+    if (!pull || !pull->r_end || !kv) return CRDT_E_INVAL;
+    return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr, kv, pull, true);
+}
+}  // namespace crdt
 
 extern "C" int crdt_refmerge_batch(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp) {
     return refmerge_run(ctx, inp, outp, nullptr, nullptr, nullptr);
@@ -1215,7 +1232,7 @@ extern "C" int crdt_refmerge_delta(crdt_ctx *ctx, const crdt_refmerge_in *inp, c
 
 static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_refmerge_out *outp,
                         const int64_t *maxl_dev, const crdt_refmerge_acc *acc_out, const crdt_replay_state *delta,
-                        const crdt_refmerge_kv_out *kv, const crdt_refmerge_pull *pull) {
+                        const crdt_refmerge_kv_out *kv, const crdt_refmerge_pull *pull, bool one_pair) {
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
@@ -1308,7 +1325,8 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // (count-pass shapes at 4096-item tiles: 256 x 16 51 us, 512 x 8 45 us, 1024 x 4 67 us)
     // LDS-DMA staging of the ts runs when both logs are 8-byte aligned (refmerge.count_dma)
     const int cdma = g_rm_count_dma && !((((uintptr_t)in.l_ts) | ((uintptr_t)in.r_ts)) & 7);
-    if (kv) k_rm_count<MB, true><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma, tkv, tone, ctx->dev_status);
+    if (kv) k_rm_count<MB, true><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma, tkv, tone, ctx->dev_status,
+                                                             one_pair ? 1 : 0);
     else k_rm_count<MB><<<(unsigned)tmax, MB, 0, s>>>(in, desc, tcnt, bits, ovf, cdma, nullptr, nullptr, nullptr);
     rc = check_launch(ctx);
     if (rc) return rc;
@@ -1349,7 +1367,9 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     }
     // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
 #define RM_TILE(F, P, KV, DIAG)                                                                                \
-    if (KV && (g_rm_kvx || tg <= (unsigned)ctx->num_cus)) {                                                    \
+    if (KV && one_pair) {                                   /* every tile a one-pair tile */                   \
+        k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
+    } else if (KV && (g_rm_kvx || tg <= (unsigned)ctx->num_cus)) {                                             \
         k_rm_tile_kvx<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
     } else if (KV) {                                                                                           \
         k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \

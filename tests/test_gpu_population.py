@@ -301,3 +301,53 @@ def test_population_wire_round_refusals(eng):
             pop.round_wire(data, off, keys, other)
     finally:
         pop.close()
+
+
+def _rand_diff_one(rng, t0, n):
+    """A Diff whose every entry holds exactly one pair (the reference's load
+    generator: one key per command, main.go:282)."""
+    d, t = {}, t0
+    for _ in range(n):
+        t += int(rng.integers(1, 5))
+        kv = {KEYS[int(rng.integers(0, K))]: STRS[int(rng.integers(0, len(STRS)))]}
+        d[t] = pyref.Command(kv) if rng.random() < 0.5 else kv
+    return d
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_population_one_pair_rounds(eng, seed):
+    """Populations whose entries all hold one pair take the one-pair kv
+    passes (refmerge_batch_pull_one_pair: tile pair counts from the emitted
+    counts): rounds (self-pulls, dead peers), undo, one-pair AddCommands, then
+    multi-pair AddCommands (which drop the invariant) and more rounds -- all
+    == pyref."""
+    from test_gpu_local_apply import _cmd_block
+    rng = np.random.default_rng(seed)
+    P = 9
+    diffs = [_rand_diff_one(rng, 1_000 + 17 * i, int(rng.integers(0, 60))) for i in range(P)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    states = [{} for _ in range(P)]
+    try:
+        for rnd in range(8):
+            if rnd in (3, 6):                            # AddCommand: one pair each, then (round 6) several
+                cmds, exp = [], []
+                for i in range(P):
+                    t0 = max(diffs[i]) if diffs[i] else 1_000
+                    npairs = 1 if rnd == 3 else 2
+                    mine = [(t0 + 1 + j, {KEYS[int(q)]: STRS[int(rng.integers(0, 12))]
+                                          for q in rng.choice(K, npairs, replace=False)})
+                            for j in range(int(rng.integers(0, 3)))]
+                    exp += [pyref.add_command(diffs[i], states[i], t, d) for t, d in mine]
+                    cmds.append(mine)
+                np.testing.assert_array_equal(pop.add_commands(_cmd_block(cmds)), exp)
+            peers = (gossip.random_peers if rnd % 2 else gossip.reference_peers)(rng, P, 0, P)
+            if rnd == 1:                                 # a round undone and drawn again
+                pop.round(gossip.random_peers(rng, P, 0, P))
+                pop.undo()
+            pop.round(peers)
+            diffs, states = _host_round(diffs, peers, states)
+            h = pop.read()
+            _same_diffs(_unpack_native(h, P), diffs)
+            assert _state_native(h, P) == states, f"round {rnd}"
+    finally:
+        pop.close()
