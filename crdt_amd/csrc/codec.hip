@@ -191,6 +191,7 @@ struct DecodeCtx {
     const uint64_t *boff;          // [n_pairs + 1] scan of (klen + vlen) over all pairs
     const uint32_t *klen;          // [n_pairs]
     uint64_t n_pairs;
+    unsigned long long *multi;     // entries whose pair count is not 1 (the one-pair invariant of population.hip)
     // pair j: key bytes and value bytes, clamped to the body's byte region
     // (lengths that overrun it mark the body malformed: never read past it)
     __device__ void pair_bytes(uint64_t j, const uint8_t **kp, uint32_t *kn, const uint8_t **vp, uint32_t *vn) const {
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(256) void k_dec_entries(DecodeCtx c, int64_t *__res
     const BodyDesc d = c.bd[b];
     const uint8_t *base = body_ptr(c.data, d.data) + 32;
     bool host = false;
+    uint32_t multi = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kChunk + threadIdx.x; i < d.ne && i < (uint64_t)(blockIdx.x + 1) * kChunk;
          i += 256) {
         const int64_t ts = (int64_t)le64(base + 8 * i);
@@ -234,11 +236,14 @@ __global__ __launch_bounds__(256) void k_dec_entries(DecodeCtx c, int64_t *__res
             k = 0;
         }
         if (i && (int64_t)le64(base + 8 * (i - 1)) >= ts) host = true;
+        multi += k != 1;
         r_ts[d.e0 + i] = ts;
         cnt[d.e0 + i] = k;
     }
     if (__any(host) && (threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(host)) - 1)
         atomicOr(&c.flag[b], kBodyHost);
+    for (int m = 32; m >= 1; m >>= 1) multi += __shfl_xor(multi, m, 64);
+    if ((threadIdx.x & 63) == 0 && multi && c.multi) atomicAdd(c.multi, (unsigned long long)multi);
 }
 
 // per pair: klen and klen + vlen (u32; an overflow marks the body malformed)
@@ -313,6 +318,7 @@ __device__ __forceinline__ void dec_small(DecodeCtx c, int64_t *__restrict__ r_t
     auto ld32 = [&](const uint8_t *p) { return AL ? *(const uint32_t *)p : le32(p); };
     auto ld64 = [&](const uint8_t *p) { return AL ? *(const uint64_t *)p : le64(p); };
     bool bad = false, host = false;
+    uint32_t multi = 0;                                  // entries whose pair count is not 1
     uint64_t carry = 0;
     if (!entries) {
     // pairs: klen and the scan of klen + vlen into boff.  Each thread takes
@@ -385,6 +391,7 @@ __device__ __forceinline__ void dec_small(DecodeCtx c, int64_t *__restrict__ r_t
                 prev = ts;
                 r_ts[d.e0 + i] = ts;
                 k[r] = kk;
+                multi += kk != 1;
             }
             sum += k[r];
         }
@@ -405,8 +412,12 @@ __device__ __forceinline__ void dec_small(DecodeCtx c, int64_t *__restrict__ r_t
     }
     const uint32_t fl = (bad ? kBodyMalformed : 0u) | (host ? kBodyHost : 0u);
     uint32_t wfl = fl;
-    for (int m = 32; m >= 1; m >>= 1) wfl |= __shfl_xor(wfl, m, 64);
+    for (int m = 32; m >= 1; m >>= 1) {
+        wfl |= __shfl_xor(wfl, m, 64);
+        multi += __shfl_xor(multi, m, 64);
+    }
     if ((tid & 63) == 0 && wfl) atomicOr(&c.flag[b], wfl);
+    if ((tid & 63) == 0 && multi && c.multi) atomicAdd(c.multi, (unsigned long long)multi);
 }
 
 __global__ __launch_bounds__(kSmallT) void k_dec_small(DecodeCtx c, int64_t *__restrict__ r_ts,
@@ -858,8 +869,10 @@ size_t gossip_decode_scratch_bytes(uint32_t nb, uint64_t n_e, uint64_t n_p) { re
 int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
                      uint32_t key_cap, uint64_t kv_base, const uint32_t *slot_base, const uint8_t *host_hdr,
                      crdt_strtab *keys, crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status,
-                     const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale) {
+                     const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale,
+                     uint64_t *multi_pair) {
     if (spec_stale) *spec_stale = false;
+    if (multi_pair) *multi_pair = 0;
     const hipStream_t s = ctx->stream;
     int rc;
     hipError_t e;
@@ -935,7 +948,7 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     memcpy(h_head, bd.data(), nb * sizeof(BodyDesc));
     uint64_t *h_roff = (uint64_t *)(h_head + head);
     memcpy(h_roff, r_off.data(), (nb + 1) * 8);
-    DecodeCtx c{data, d_bd, nb, d_flag, boff, klen, n_p};
+    DecodeCtx c{data, d_bd, nb, d_flag, boff, klen, n_p, ctr + 6};
     uint64_t max_ne = 0, max_np = 0;
     for (auto &x : bd) {
         max_ne = std::max(max_ne, x.ne);
@@ -1037,6 +1050,7 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
         body_status[b] |= flags[b] | flags[nb + b];
         if (body_status[b] & kBodyMalformed) body_status[b] = kBodyMalformed;   // nothing else applies then
     }
+    if (multi_pair) *multi_pair = h_ctr[6];
     rc = CRDT_OK;
     if (new_k) rc = tab_pull_new(ctx, keys, kn0 + new_k, kb0 + new_kb);
     if (!rc && new_v) rc = tab_pull_new(ctx, vals, vn0 + new_v, vb0 + new_vb);

@@ -106,7 +106,8 @@ int seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, co
 int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint64_t *at, const uint64_t *len,
                      uint32_t key_cap, uint64_t kv_base, const uint32_t *slot_base, const uint8_t *host_hdr,
                      crdt_strtab *keys, crdt_strtab *vals, const crdt_gossip_decoded *out, uint32_t *body_status,
-                     const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale);
+                     const std::function<int()> *spec, void *scratch, size_t scratch_cap, bool *spec_stale,
+                     uint64_t *multi_pair = nullptr);   // (entries whose pair count is not 1)
 size_t gossip_decode_scratch_bytes(uint32_t nb, uint64_t n_e, uint64_t n_p);
 // refmerge.hip: crdt_refmerge_batch_pull when every entry of L and of the
 // pulled ranges is known to hold exactly one kv pair

@@ -62,8 +62,9 @@ struct crdt_population {
     // reference's load generator writes one key per command, main.go:282):
     // rounds then size the kv output from entry counts alone
     // (refmerge_batch_pull_one_pair).  Exact or false: set at creation from
-    // the host arrays, kept by local rounds, cleared by anything that may
-    // bring other entries (multi-pair commands, sharded and wire rounds).
+    // the host arrays, kept by local rounds and by wire rounds whose decode
+    // counted no other entry, cleared by multi-pair commands and sharded
+    // rounds.
     bool one_pair = false, p_one_pair = false;
     uint8_t *str_bytes = nullptr;
     uint64_t *str_off = nullptr;
@@ -800,8 +801,9 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     int64_t *r_ts = w.take<int64_t>(n_e + 1);
     uint64_t *r_kv = w.take<uint64_t>(n_e + 1);
     const crdt_gossip_decoded go{r_off, r_ts, r_kv, cd.kv_key, cd.kv_val};
+    uint64_t multi = 1;
     rc = gossip_decode_at(ctx, P, bodies, at.data(), len.data(), pop->K, pop->n_kv, sbase.data(), hdr.data(), keys,
-                          vals, &go, body_status, nullptr, nullptr, 0, nullptr);
+                          vals, &go, body_status, nullptr, nullptr, 0, nullptr, &multi);
     if (rc) return rc;
     for (uint32_t i = 0; i < P; ++i)
         if (body_status[i] && len[i]) return CRDT_E_UNSORTED;   // (nothing merged: the population is unchanged)
@@ -810,12 +812,14 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
         (void)dev_free(ctx, (void **)&pop->str_off);
         pop->vtab = vals;
     }
+    // one pair per pulled entry too (counted by the decode): the one-pair passes
+    const bool one = pop->one_pair && multi == 0;
     RoundArrays a;
     rc = upload_round(pop, h, &a);
-    if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p);
+    if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, one);
     if (rc) return rc;
     rc = pop_commit(pop);
-    if (!rc) pop->one_pair = false;                      // (the pulled bodies' entries: not checked)
+    if (!rc) pop->one_pair = one;
     return rc;
 }
 

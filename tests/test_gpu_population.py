@@ -223,19 +223,22 @@ def _wire_tables(eng):
     return keys, vals
 
 
+@pytest.mark.parametrize("one", [False, True], ids=["pairs", "one_pair"])
 @pytest.mark.parametrize("seed", [5, 6])
-def test_population_wire_rounds_match_reference_simulation(eng, seed):
+def test_population_wire_rounds_match_reference_simulation(eng, seed, one):
     """crdt_population_round_wire: every replica's pull arrives as a binary
     gossip body in HBM (main.go:159, :245-256), decoded on the device and
     merged == the pyref simulation; failed GETs (empty bodies) skip the
     round, self-pulls rebuild CurrentState, a value the tables have not seen
     is interned and lands in the population's arena (adopted from vals),
-    and AddCommand between wire rounds uses the same ids."""
+    and AddCommand between wire rounds uses the same ids.  one: every
+    entry holds one pair (the one-pair kv passes, kept through the rounds)."""
     from test_gpu_codec import _serve, _upload
     from test_gpu_local_apply import _cmd_block
     rng = np.random.default_rng(seed)
     P = 7
-    diffs = [_rand_diff(rng, 1_000 + 13 * i, int(rng.integers(0, 30))) for i in range(P)]
+    gen = _rand_diff_one if one else _rand_diff
+    diffs = [gen(rng, 1_000 + 13 * i, int(rng.integers(0, 30))) for i in range(P)]
     keys, vals = _wire_tables(eng)
     pop = gossip.NativePopulation(eng, _pack(diffs), K)
     states = [{} for _ in range(P)]
