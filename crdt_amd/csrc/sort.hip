@@ -30,6 +30,7 @@
 // memory-side round trip across the 8 XCDs' non-coherent L2s; the extra
 // read of the upsweep costs less than those chains.
 #include <algorithm>
+#include <cstring>
 
 #include "scan.hpp"
 
@@ -46,6 +47,7 @@ struct SortPlan {
     uint32_t W, P, words;        // composite bits, passes, 64-bit words
     uint32_t b0;                 // bit offset of the rep field: 1 (tomb) + side bits (0 or 1)
     uint32_t s0;                 // bit of the first digit (0: the whole composite is sorted)
+    uint32_t tl, tw;             // LWW key-bucket tables: key bits per bucket table, entry bytes (4 / 8; 0: none)
     uint64_t n1;                 // composites [0, n1) come from in (side 0), [n1, n) from in2 (side 1)
     crdt_tuples in2;
 };
@@ -163,7 +165,7 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, co
 // reduces the nmm minmax partials, then thread 0 sizes the composite
 __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32_t nmm, SortPlan *plan,
                                                    uint32_t side_bits, crdt_tuples in2, uint64_t n1,
-                                                   uint32_t key_only = 0) {
+                                                   uint32_t key_only = 0, uint32_t lww_table = 0) {
     __shared__ unsigned long long sr[6][256];
     const int tid = threadIdx.x;
     unsigned long long v[6] = {~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
@@ -216,6 +218,22 @@ __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32
     if (key_only == 2) keep += (8u - p.bk % 8u) % 8u + 8u;
     p.s0 = (key_only && p.words == 1 && p.W > keep) ? p.W - keep : 0;
     p.P = p.W - p.s0 ? (p.W - p.s0 + 7) / 8 : 1;        // >= 1: the first pass composes
+    // LWW key-bucket tables (k_lww_table): one pass on the key's top 8 bits,
+    // then a table of the remaining bk - 8 key bits per bucket in LDS -- 2^15
+    // u32 entries (tag + marker <= 32 bits) or 2^14 u64 entries in 128 KB;
+    // keys of fewer than 12 bits keep the key-only sort (tiny tables would
+    // serialise the LDS atomics on a few entries)
+    p.tl = p.tw = 0;
+    const uint32_t kb = p.b0 + p.br + p.bt;
+    if (key_only == 1 && lww_table && p.words == 1 && p.bk >= 12) {
+        if (p.bk <= 8 + 15 && kb + 1 <= 32) p.tw = 4;
+        else if (p.bk <= 8 + 14 && kb + 1 <= 64) p.tw = 8;
+        if (p.tw) {
+            p.tl = p.bk - 8;
+            p.s0 = p.W - 8;
+            p.P = 1;
+        }
+    }
     *plan = p;
 }
 
@@ -384,7 +402,8 @@ __global__ __launch_bounds__(SB) void k_sort_up_vec(crdt_tuples in, size_t n, co
 // most of its 9.6 us in three serial rounds of barriers).
 constexpr int CSB = 1024;
 __global__ __launch_bounds__(CSB) void k_sort_colscan(const uint32_t *__restrict__ cnt, uint32_t ntiles,
-                                                      uint32_t *__restrict__ loc, uint32_t *__restrict__ tot) {
+                                                      uint32_t *__restrict__ loc, uint32_t *__restrict__ tot,
+                                                      unsigned long long *__restrict__ zero = nullptr) {
     constexpr int K = 8;
     constexpr int NW = CSB / 64;
     __shared__ uint32_t s_w[NW];
@@ -425,6 +444,7 @@ __global__ __launch_bounds__(CSB) void k_sort_colscan(const uint32_t *__restrict
         carry += all;
     }
     if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+    if (zero && threadIdx.x == 0) zero[blockIdx.x] = 0;   // k_lww_table's bucket flags
 }
 
 // ---------------------------------------------------------------- one pass
@@ -569,7 +589,8 @@ static void launch_pass(bool first, bool last, unsigned grid, hipStream_t st, co
 template <int WORDS>
 static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &out, const SortPlan *plan_d,
                       uint32_t P, uint64_t *bufs, uint32_t *cnt, uint32_t *loc, uint32_t *tot, bool decode = true,
-                      uint64_t **result = nullptr, bool vec_first = false) {
+                      uint64_t **result = nullptr, bool vec_first = false,
+                      unsigned long long *zero = nullptr) {
     const hipStream_t st = ctx->stream;
     const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
     uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
@@ -581,7 +602,7 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
             k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a);
         else
             k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr);
-        k_sort_colscan<<<256, CSB, 0, st>>>(cnt, ntiles, loc, tot);
+        k_sort_colscan<<<256, CSB, 0, st>>>(cnt, ntiles, loc, tot, q == 0 ? zero : nullptr);
         launch_pass<WORDS>(false, decode && q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
         std::swap(a, b);
     }
@@ -935,6 +956,147 @@ __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c,
         out.ts[o] = p.tmin + get_bits(win, p.b0 + p.br, p.bt);
         out.rep[o] = (uint32_t)(p.rmin + get_bits(win, p.b0, p.br));
         out.tomb[o] = tomb;
+    }
+}
+
+// ---------------------------------------------------------------- LWW D2: key-bucket tables
+// sort.lww_table (default 1).  LWW keeps one tuple per key, and a key's
+// winner is a MAX -- of the tag word c ^ 3 over the key's tuples (the max
+// (ts, rep), then side A (bit 1 inverted), then the least tomb (bit 0
+// inverted): the order the key-only sort's dedup takes its run maximum in)
+// -- so it needs no order among the key's tuples.  When the key offsets span
+// 12..23 bits (config D: 23) the sort is ONE radix pass on the key's top 8
+// bits, which leaves each of 256 key buckets contiguous, and one 1024-thread
+// workgroup per bucket keeps the max of each of its 2^(bk-8) keys in an LDS
+// table (<= 128 KB: one workgroup per CU): an LDS atomicMax per tuple, then
+// a walk of the table in key order that stores one tuple per present key at
+// its rank -- round-major, so consecutive lanes take consecutive keys and the
+// ballot-compacted stores are contiguous per wave.
+// A bucket's output offset is the number of present keys in the buckets
+// before it.  Each workgroup publishes its own count as soon as its table
+// is walked once (an agent-scope store of count | ready) and sums its
+// predecessors' (thread d polls bucket d's word): no chain, every count is
+// published before its workgroup waits.  Workgroups are dispatched in index
+// order, so every polled predecessor has been dispatched; the polls are
+// bounded, and a timeout raises CRDT_DEV_LOOKBACK (output invalid) instead
+// of hanging.
+constexpr int LTB = 1024;                          // threads per bucket workgroup
+constexpr int LT_WAVES = LTB / 64;
+constexpr uint32_t kLtBytes = 128u * 1024u;        // the LDS table
+constexpr unsigned long long kLtReady = 1ull << 32;
+
+__device__ __forceinline__ uint64_t lt_field(uint64_t x, uint32_t s, uint32_t b) {
+    return b == 0 ? 0 : (x >> s) & (b >= 64 ? ~0ull : ((1ull << b) - 1ull));
+}
+
+template <typename E>
+__global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
+                                                   const uint32_t *__restrict__ tot,
+                                                   unsigned long long *__restrict__ flag, crdt_tuples out,
+                                                   uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
+    constexpr uint32_t NE = kLtBytes / sizeof(E);  // 2^15 u32 / 2^14 u64 entries
+    constexpr uint32_t NR = NE / LTB;              // table rounds at most
+    static_assert(NR * LT_WAVES <= 64 * 8, "one wave scans the round counts");
+    __shared__ E tab[NE];
+    __shared__ uint32_t s_cnt[NR * LT_WAVES];      // present keys per (round, wave), then their prefix
+    __shared__ unsigned long long s_sum[3];        // bucket start, predecessors' keys, own keys
+    const SortPlan p = *plan_;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t b = blockIdx.x, L = p.tl, ne = 1u << L;
+    const uint32_t kb = p.b0 + p.br + p.bt;        // tag bits under the key (< 8 * sizeof(E))
+    const E marker = (E)1 << kb, tmask = marker - 1;
+    if (tid < 3) s_sum[tid] = 0;
+    for (uint32_t i = tid; i < ne; i += LTB) tab[i] = 0;
+    unsigned long long part = (tid < 256 && (uint32_t)tid < b) ? tot[tid] : 0u;
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
+    __syncthreads();
+    if (lane == 0 && w < 4 && part) atomicAdd(&s_sum[0], part);
+    __syncthreads();
+    const uint64_t *src = c + s_sum[0];
+    const uint32_t nb = tot[b];
+    // every tuple of the bucket into its key's entry
+    uint32_t j = tid;
+    for (; j + 3 * LTB < nb; j += 4 * LTB) {
+        uint64_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = src[j + k * LTB];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            atomicMax(&tab[(uint32_t)(x[k] >> kb) & (ne - 1)], ((E)(x[k] ^ 3u) & tmask) | marker);
+    }
+    for (; j < nb; j += LTB) {
+        const uint64_t x = src[j];
+        atomicMax(&tab[(uint32_t)(x >> kb) & (ne - 1)], ((E)(x ^ 3u) & tmask) | marker);
+    }
+    __syncthreads();
+    // present keys per (round, wave), their exclusive prefix, and the total
+    const uint32_t R = (ne + LTB - 1) / LTB, NC = R * LT_WAVES;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t e = r * LTB + tid;
+        const uint64_t m = __ballot(e < ne && tab[e] != 0);
+        if (lane == 0) s_cnt[r * LT_WAVES + w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (w == 0) {
+        uint32_t v[8], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = lane * 8 + k;
+            v[k] = i < NC ? s_cnt[i] : 0u;
+            sum += v[k];
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        uint32_t run = x - sum;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = lane * 8 + k;
+            if (i < NC) s_cnt[i] = run;
+            run += v[k];
+        }
+        if (lane == 63) {
+            s_sum[2] = x;
+            __hip_atomic_store(&flag[b], kLtReady | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // the predecessors' counts
+    unsigned long long pre = 0;
+    if ((uint32_t)tid < b) {
+        unsigned long long f;
+        uint32_t spins = 0;
+        while (!((f = __hip_atomic_load(&flag[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kLtReady)) {
+            if (++spins > (1u << 22)) {            // bounded: report, never hang
+                atomicOr(err, CRDT_DEV_LOOKBACK);
+                f = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pre = f & 0xFFFFFFFFull;
+    }
+    for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (lane == 0 && w < 4 && pre) atomicAdd(&s_sum[1], pre);
+    __syncthreads();
+    const uint64_t off = s_sum[1];
+    if (b == gridDim.x - 1 && tid == 0) *out_count = off + s_sum[2];
+    // one tuple per present key, in key order
+    const uint64_t kbase = (uint64_t)b << L;
+    const uint32_t sr = p.b0, st = p.b0 + p.br;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t e = r * LTB + tid;
+        const E v = e < ne ? tab[e] : (E)0;
+        const uint64_t m = __ballot(v != 0);
+        if (v == 0) continue;
+        const size_t o = off + s_cnt[r * LT_WAVES + w] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint64_t win = (uint64_t)(v & tmask) ^ 3u;
+        out.key[o] = p.kmin + (kbase | e);
+        out.ts[o] = p.tmin + lt_field(win, st, p.bt);
+        out.rep[o] = (uint32_t)(p.rmin + lt_field(win, sr, p.br));
+        out.tomb[o] = (uint8_t)(win & 1u);
     }
 }
 
@@ -1435,6 +1597,18 @@ static int or_run_dedup(crdt_ctx *ctx, uint64_t *c, size_t n, const SortPlan *pl
     return check_launch(ctx);
 }
 
+// the device plan back to the host through the context's pinned buffer (a
+// pageable destination costs a staged copy on every call)
+static int read_plan(crdt_ctx *ctx, const SortPlan *plan, SortPlan *h) {
+    int rc = hio_reserve(ctx, sizeof(SortPlan));
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(ctx->hio, plan, sizeof(SortPlan), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+    memcpy(h, ctx->hio, sizeof(SortPlan));
+    return CRDT_OK;
+}
+
 template <int MODE, int WORDS>
 static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPlan *plan, uint32_t *cnt,
                        uint32_t *loc, uint32_t *tot, const crdt_tuples &out, uint64_t *out_count) {
@@ -1467,7 +1641,8 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
     const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
-    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + 1024);
+    const size_t b_flag = Carve::round(256 * 8);
+    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + 1024);
     if (rc) return rc;
     Carve w(ctx->ws);
     SortMinMax *mm = w.take<SortMinMax>(2 * MM_BLOCKS);
@@ -1476,12 +1651,13 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint32_t *loc = w.take<uint32_t>(ncnt);
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
+    unsigned long long *flags = w.take<unsigned long long>(256);
     const unsigned nmm = launch_minmax(ctx, A, na, B, nb, mm);
-    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u);
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u,
+                                  MODE == DD_LWW ? (uint32_t)g_lww_table : 0u);
     SortPlan h;
-    hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
+    rc = read_plan(ctx, plan, &h);
+    if (rc) return rc;
     uint64_t *sorted = nullptr;
     if (h.words == 1) {
         auto vec_ok = [](const crdt_tuples &t, size_t m) {
@@ -1489,6 +1665,15 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
                                ((uintptr_t)t.tomb & 1));
         };
         const bool vec = vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
+        if (MODE == DD_LWW && h.tw) {                   // one pass on the key's top byte, then bucket tables
+            rc = sort_words<1>(ctx, A, n, *out, plan, 1, bufs, cnt, loc, tot, false, &sorted, vec, flags);
+            if (rc) return rc;
+            if (h.tw == 4)
+                k_lww_table<uint32_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
+            else
+                k_lww_table<uint64_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
+            return check_launch(ctx);
+        }
         rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted, vec);
         if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup
             return or_run_dedup(ctx, sorted, n, plan, sorted == bufs ? bufs + n : bufs, bufs + 2 * n, cnt, loc,
@@ -1541,9 +1726,8 @@ extern "C" int crdt_tuples_sort(crdt_ctx *ctx, const crdt_tuples *in, size_t n, 
     k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 0, crdt_tuples{nullptr, nullptr, nullptr, nullptr}, n);
     // the pass count and composite width decide the launches: one small read-back
     SortPlan h;
-    hipError_t e = hipMemcpyAsync(&h, plan, sizeof(h), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
+    rc = read_plan(ctx, plan, &h);
+    if (rc) return rc;
     if (h.words == 1) return sort_words<1>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
     if (h.words == 2) return sort_words<2>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);
     return sort_words<3>(ctx, *in, n, *out, plan, h.P, bufs, cnt, loc, tot);

@@ -154,3 +154,38 @@ def test_unsorted_orset_sort_modes(eng, mode):
         test_unsorted_single_tag(eng, 5000)
     finally:
         _lib.call("crdt_set_option", b"sort.or_key_only", 2)
+
+
+@pytest.mark.parametrize("kbits,tbits", [(11, 20), (12, 20), (16, 20), (20, 8), (23, 20), (24, 20),
+                                         (16, 40), (22, 40), (23, 40)])
+def test_unsorted_lww_key_tables(eng, kbits, tbits):
+    """LWW D2 by key-bucket LDS tables (sort.lww_table; taken when the key
+    offsets span 12..23 bits with tags of <= 31 bits, 12..22 bits with wider
+    tags; 11 / 24 key bits and 23 bits with wide tags keep the key-only
+    sort): with the tables on and off == the oracle.  Keys offset far from 0
+    and spanning their full width, 80 % of the tuples in one key bucket,
+    cross-side equal tags with differing tombs, one side shorter."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng(kbits * 100 + tbits)
+
+    def side(m):
+        key = rng.integers(0, 2**kbits, m, dtype=np.uint64)
+        hot = rng.random(m) < 0.8                                  # one hot bucket (top key byte 0)
+        key[hot] = rng.integers(0, 2**max(kbits - 8, 1), int(hot.sum()), dtype=np.uint64)
+        key[:2] = [0, 2**kbits - 1]
+        ts = rng.integers(0, 2**tbits, m, dtype=np.uint64)
+        ts[:2] = [0, 2**tbits - 1]
+        rep = rng.integers(0, 40, m, dtype=np.uint64).astype(np.uint32)
+        tomb = rng.integers(0, 2, m, dtype=np.uint8)
+        return key + np.uint64(2**61), ts + np.uint64(12345), rep + np.uint32(7), tomb
+
+    a, b = side(150_000), side(130_000)
+    for f in range(3):                                            # cross-side equal tags
+        b[f][:5000] = a[f][:5000]
+    try:
+        for on in (1, 0):
+            _lib.call("crdt_set_option", b"sort.lww_table", on)
+            _check(eng, a, b)
+            _check(eng, a, tuple(x[:0] for x in b))
+    finally:
+        _lib.call("crdt_set_option", b"sort.lww_table", 1)
