@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 // buffer) and both passes read it from HBM.
 constexpr int RT = 2048;                 // nominal tile (composites)
 constexpr int RCAP = 3072;               // LDS capacity of a run-aligned tile
-constexpr int RB = 256;                  // threads
+constexpr int RB = 512;                  // threads (6 composites each; 256 x 12: 0.985 ms, 1024 x 3: 1.10)
 constexpr uint32_t kInsMax = 32;         // runs up to this length: element-wise marks, unsorted
 
 // first run start at or after p (keys = composite >> ks): galloping, then binary search
