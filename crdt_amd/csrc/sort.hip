@@ -165,7 +165,8 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, co
 // reduces the nmm minmax partials, then thread 0 sizes the composite
 __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32_t nmm, SortPlan *plan,
                                                    uint32_t side_bits, crdt_tuples in2, uint64_t n1,
-                                                   uint32_t key_only = 0, uint32_t lww_table = 0) {
+                                                   uint32_t key_only = 0, uint32_t lww_table = 0,
+                                                   uint32_t or_table = 0, uint64_t n_all = 0) {
     __shared__ unsigned long long sr[6][256];
     const int tid = threadIdx.x;
     unsigned long long v[6] = {~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
@@ -233,6 +234,17 @@ __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32
             p.s0 = p.W - 8;
             p.P = 1;
         }
+    }
+    // OR-Set key chunks (k_or_chunk): two passes on the key's top 16 bits,
+    // then chunks of 2^10 keys sorted in LDS -- where the sorted prefix fixes
+    // the chunk (bk <= 26) and chunks hold <= 3072 tuples on average (config
+    // D: 2.4k; the LDS holds 4096)
+    if (or_table && key_only != 1 && p.words == 1 && p.bk >= 16 && p.bk <= 16 + 9 &&
+        n_all <= (1536ull << (p.bk - 9))) {
+        p.tw = 4;
+        p.tl = 9;
+        p.s0 = p.W - 16;
+        p.P = 2;
     }
     *plan = p;
 }
@@ -444,7 +456,8 @@ __global__ __launch_bounds__(CSB) void k_sort_colscan(const uint32_t *__restrict
         carry += all;
     }
     if (threadIdx.x == 0) tot[blockIdx.x] = carry;
-    if (zero && threadIdx.x == 0) zero[blockIdx.x] = 0;   // k_lww_table's bucket flags
+    if (zero && threadIdx.x == 0) zero[blockIdx.x] = 0;   // the bucket tables' flags
+    if (zero && threadIdx.x == 0 && blockIdx.x == 0) zero[256] = 0;   // k_or_chunk's fallback word
 }
 
 // ---------------------------------------------------------------- one pass
@@ -1100,6 +1113,331 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- OR-Set D2: key chunks sorted in LDS
+// sort.or_table (default 1).  The radix sort runs only TWO passes, on the
+// key's top 16 bits; the key space is then cut into chunks of 2^10 keys
+// (config D: 8192 chunks of ~2.4k tuples), each contiguous in the sorted
+// composites because a chunk is a run of top-16 buckets.  Per chunk, one
+// 512-thread workgroup holds the chunk in LDS and finishes the sort there:
+//   k_chunk_bounds: the chunk starts, one 64-ary search per chunk;
+//   k_or_chunk: the chunk's tuples into registers, a counting sort by key
+//     into LDS (count per key, scan, scatter by LDS atomics), then one thread
+//     per key finds the key's distinct tags -- a key of <= kOtRun tuples
+//     read at once and resolved in registers (element j is its tag's first
+//     copy when no other element has its tag and a smaller composite, an
+//     equal one a lower index); a longer key by the whole workgroup (marks
+//     in LDS, ranks by counting) -- and places them in tag order, tomb =
+//     the OR of the tag's copies, as composites (side bit cleared) in LDS,
+//     then copies them out at once to the chunk's own input range of `tmp`
+//     (stored straight from each key's thread they were partial-line
+//     scatters: 238 us of a 403 us pass), plus the chunk's count;
+//   k_sort_colscan over the chunk counts;
+//   k_or_emit: each chunk's tags decoded into the SoA output at its offset.
+// A chunk of more than kOcCap tuples (skewed keys) or of more than kOcLong
+// keys with over kOtRun tuples raises the fallback word and stores nothing;
+// the host then runs the radix path (inputs untouched).
+// (Round 4, first form: one radix pass on the key's top byte and a counting
+// sort of each 78k-tuple bucket through global memory -- its scattered 8-B
+// stores over 256 x 625 KB alone took 375 us)
+constexpr int OCB = 512;                 // threads per chunk workgroup
+constexpr int OC_WAVES = OCB / 64;
+constexpr uint32_t kOcBits = 9;          // keys per chunk: 2^9
+constexpr uint32_t kOcKeys = 1u << kOcBits;
+constexpr uint32_t kOcCap = 2048;        // tuples per chunk (LDS); more -> fallback
+constexpr uint32_t kOcPer = kOcCap / OCB;
+constexpr uint32_t kOtRun = 8;           // keys of up to this many tuples: one thread, registers
+constexpr uint32_t kOcLong = 256;        // longer keys per chunk (LDS list); more -> the workgroup loops
+
+// a key's <= kOtRun tuples sorted in registers (Batcher's 19-comparator
+// network; unused slots hold ~0 and sort last), so its distinct tags are the
+// slots whose tag differs from the previous slot's -- the first copy of each
+// tag its smallest composite.  (Pairwise first-copy tests and ranks over all
+// slots, 8 x 8 64-bit compares per key twice, made the pass VALU-bound: 428 us.)
+__device__ __forceinline__ void ot_cswap(uint64_t &a, uint64_t &b) {
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+__device__ __forceinline__ void ot_sort8(uint64_t *v) {
+    ot_cswap(v[0], v[1]); ot_cswap(v[2], v[3]); ot_cswap(v[4], v[5]); ot_cswap(v[6], v[7]);
+    ot_cswap(v[0], v[2]); ot_cswap(v[1], v[3]); ot_cswap(v[4], v[6]); ot_cswap(v[5], v[7]);
+    ot_cswap(v[1], v[2]); ot_cswap(v[5], v[6]);
+    ot_cswap(v[0], v[4]); ot_cswap(v[1], v[5]); ot_cswap(v[2], v[6]); ot_cswap(v[3], v[7]);
+    ot_cswap(v[2], v[4]); ot_cswap(v[3], v[5]);
+    ot_cswap(v[1], v[2]); ot_cswap(v[3], v[4]); ot_cswap(v[5], v[6]);
+}
+// bit j: slot j (< m) starts a tag in the sorted slots
+__device__ __forceinline__ uint32_t ot_firsts(const uint64_t *v, uint32_t m, uint32_t tb) {
+    uint32_t fm = m ? 1u : 0u;
+#pragma unroll
+    for (uint32_t j = 1; j < kOtRun; ++j) fm |= (j < m && (v[j] >> tb) != (v[j - 1] >> tb)) ? 1u << j : 0u;
+    return fm;
+}
+
+// bounds[i] = first composite of chunk i (0 < i < nch; bounds[0] = 0,
+// bounds[nch] = n): a 64-ary search per chunk over the chunk index c >> cs,
+// non-decreasing in the sorted composites (every index probed once the span
+// is <= 64)
+__global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict__ c, size_t n, uint32_t cs,
+                                                      uint32_t nch, uint64_t *__restrict__ bounds) {
+    const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);      // one wave per bound
+    const int lane = threadIdx.x & 63;
+    if (i > nch) return;
+    if (i == 0 || i == nch) {
+        if (lane == 0) bounds[i] = i == 0 ? 0 : n;
+        return;
+    }
+    size_t lo = 0, hi = n;                            // the answer lies in [lo, hi]
+    while (lo < hi) {
+        const size_t span = hi - lo;
+        const size_t q = lo + span * (size_t)lane / 64;
+        const uint64_t ge = __ballot((c[q] >> cs) >= i);
+        if (ge == 0) {
+            lo += span * 63 / 64 + 1;
+        } else {
+            const int t = __ffsll((long long)ge) - 1;
+            hi = lo + span * (size_t)t / 64;
+            if (t > 0) lo += span * (size_t)(t - 1) / 64 + 1;
+        }
+    }
+    if (lane == 0) bounds[i] = lo;
+}
+
+__global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
+                                                  const SortPlan *__restrict__ plan_,
+                                                  const uint64_t *__restrict__ bounds, uint32_t *__restrict__ cnt,
+                                                  uint32_t *__restrict__ fbw, int diag) {
+    constexpr uint32_t R = kOcKeys / OCB;             // keys per thread (round-major)
+    __shared__ uint32_t tab[kOcKeys];
+    __shared__ uint64_t stg[kOcCap];
+    __shared__ uint64_t ost[kOcCap];                  // the chunk's tags in order (one coalesced copy out)
+    __shared__ uint32_t s_first[kOcCap / 32];         // a long key's first-copy marks
+    __shared__ uint32_t s_cnt[R * OC_WAVES], s_wsum[OC_WAVES], s_long[kOcLong], s_lrk[kOcLong], s_nlong, s_tot;
+    const SortPlan p = *plan_;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t kb = p.b0 + p.br + p.bt, tb = p.b0;
+    const size_t s = bounds[blockIdx.x], e = bounds[blockIdx.x + 1];
+    if (e - s > kOcCap) {                             // skewed keys: the radix path instead
+        if (tid == 0) {
+            atomicOr(fbw, 1u);
+            cnt[blockIdx.x] = 0;
+        }
+        return;
+    }
+    const uint32_t len = (uint32_t)(e - s);
+    for (uint32_t i = tid; i < kOcKeys; i += OCB) tab[i] = 0;
+    for (uint32_t i = tid; i < kOcCap / 32; i += OCB) s_first[i] = 0;
+    if (tid == 0) s_nlong = 0;
+    uint64_t x[kOcPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kOcPer; ++k) {
+        const uint32_t j = k * OCB + tid;
+        x[k] = j < len ? c[s + j] : 0;
+    }
+    __syncthreads();
+    // counting sort by key into LDS
+#pragma unroll
+    for (uint32_t k = 0; k < kOcPer; ++k)
+        if (k * OCB + tid < len) atomicAdd(&tab[(uint32_t)(x[k] >> kb) & (kOcKeys - 1)], 1u);
+    __syncthreads();
+    if (diag == 1) {                                  // timing diagnostics (sort.rdd_diag): counts only
+        if (tid == 0) cnt[blockIdx.x] = 0;
+        return;
+    }
+    {                                                 // exclusive scan: wave w the contiguous entries [w P, (w+1) P)
+        constexpr uint32_t P = kOcKeys / OC_WAVES;
+        uint32_t carry = 0;
+#pragma unroll
+        for (uint32_t e0 = 0; e0 < P; e0 += 64) {
+            const uint32_t i = (uint32_t)w * P + e0 + (uint32_t)lane;
+            const uint32_t v = tab[i];
+            uint32_t y = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(y, d, 64);
+                if (lane >= d) y += t;
+            }
+            tab[i] = carry + y - v;
+            carry += (uint32_t)__shfl((int)y, 63, 64);
+        }
+        if (lane == 0) s_wsum[w] = carry;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int k = 0; k < w; ++k) woff += s_wsum[k];
+#pragma unroll
+        for (uint32_t e0 = 0; e0 < P; e0 += 64) tab[(uint32_t)w * P + e0 + (uint32_t)lane] += woff;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kOcPer; ++k)
+        if (k * OCB + tid < len) stg[atomicAdd(&tab[(uint32_t)(x[k] >> kb) & (kOcKeys - 1)], 1u)] = x[k];
+    __syncthreads();                                  // tab[k] = the end of key k
+    if (diag == 2) {                                  // + the scan and the scatter into LDS
+        if (tid == 0) cnt[blockIdx.x] = 0;
+        return;
+    }
+    // distinct tags per key (long keys listed, resolved below); each short
+    // key's slots stay sorted in registers for the stores
+    uint32_t dk[R], fk[R];
+    uint64_t sv[R][kOtRun];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t kl = r * OCB + tid;
+        const uint32_t s0 = kl ? tab[kl - 1] : 0u, m = tab[kl] - s0;
+        const uint32_t ms = m <= kOtRun ? m : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kOtRun; ++k) sv[r][k] = k < ms ? stg[s0 + k] : ~0ull;
+        if (m > kOtRun) {
+            const uint32_t q = atomicAdd(&s_nlong, 1u);
+            if (q < kOcLong) s_long[q] = kl;
+        }
+        if (ms > 1) ot_sort8(sv[r]);
+        fk[r] = ot_firsts(sv[r], ms, tb);
+        dk[r] = (uint32_t)__popc(fk[r]);
+    }
+    __syncthreads();
+    const uint32_t nl = s_nlong;
+    if (diag == 3) {                                  // + the short keys' distinct tags
+        if (tid == 0) cnt[blockIdx.x] = 0;
+        return;
+    }
+    if (nl > kOcLong) {                               // (uniform) too many long keys: the radix path
+        if (tid == 0) {
+            atomicOr(fbw, 1u);
+            cnt[blockIdx.x] = 0;
+        }
+        return;
+    }
+    for (uint32_t q = 0; q < nl; ++q) {               // a long key: first-copy marks, their count to its owner
+        const uint32_t kl = s_long[q];
+        const uint32_t s0 = kl ? tab[kl - 1] : 0u, m = tab[kl] - s0;
+        uint32_t f = 0;
+        for (uint32_t i = tid; i < m; i += OCB) {
+            const uint64_t xi = stg[s0 + i];
+            bool first = true;
+            for (uint32_t k = 0; k < m && first; ++k) {
+                const uint64_t y = stg[s0 + k];
+                if (k != i && (y >> tb) == (xi >> tb) && (y < xi || (y == xi && k < i))) first = false;
+            }
+            if (first) atomicOr(&s_first[(s0 + i) >> 5], 1u << ((s0 + i) & 31));
+            f += first ? 1u : 0u;
+        }
+        for (int o = 32; o >= 1; o >>= 1) f += __shfl_xor(f, o, 64);
+        if (lane == 0) s_wsum[w] = f;
+        __syncthreads();
+        if ((uint32_t)tid == kl % OCB) {
+            uint32_t t = 0;
+            for (int k = 0; k < OC_WAVES; ++k) t += s_wsum[k];
+#pragma unroll
+            for (uint32_t r = 0; r < R; ++r)
+                if (r == kl / OCB) dk[r] = t;
+        }
+        __syncthreads();
+    }
+    // ranks: per (round, wave) sums, their prefix, in-wave prefixes
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        uint32_t d = dk[r];
+        for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (lane == 0) s_cnt[r * OC_WAVES + w] = d;
+    }
+    __syncthreads();
+    if (w == 0) {
+        constexpr uint32_t NC = R * OC_WAVES;
+        static_assert(NC <= 64, "one wave");
+        const uint32_t c0 = lane < (int)NC ? s_cnt[lane] : 0u;
+        uint32_t y = c0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(y, o, 64);
+            if (lane >= o) y += t;
+        }
+        if (lane < (int)NC) s_cnt[lane] = y - c0;
+        if (lane == 63) {
+            cnt[blockIdx.x] = y;
+            s_tot = y;
+        }
+    }
+    __syncthreads();
+    if (diag == 4) {                                  // + the long keys and the ranks
+        if (tid == 0) cnt[blockIdx.x] = 0;
+        return;
+    }
+    // stores: composites with the side bit cleared and the tomb = the OR of the tag's copies
+    uint64_t *dst = tmp + s;
+    const uint64_t keep = ~3ull;
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t kl = r * OCB + tid;
+        const uint32_t s0 = kl ? tab[kl - 1] : 0u, m = tab[kl] - s0, d = dk[r];
+        uint32_t y = d;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(y, o, 64);
+            if (lane >= o) y += t;
+        }
+        const uint32_t rk0 = s_cnt[r * OC_WAVES + w] + y - d;   // the key's first rank in the chunk
+        if (m > kOtRun) {
+            for (uint32_t q = 0; q < nl; ++q)
+                if (s_long[q] == kl) s_lrk[q] = rk0;
+        } else if (m > 0) {
+            // the OR of each tag's tombs, from the right: run = slot j's tomb,
+            // plus the run after it while the tag continues
+            uint32_t tt = 0, run = 0;
+#pragma unroll
+            for (int j = kOtRun - 1; j >= 0; --j) {
+                const bool in = (uint32_t)j < m;
+                const bool cont = (uint32_t)j + 1 < m && !((fk[r] >> (j + 1)) & 1u);
+                run = (in ? (uint32_t)(sv[r][j] & 1u) : 0u) | (cont ? run : 0u);
+                tt |= run << j;
+            }
+            uint32_t rk = rk0;
+#pragma unroll
+            for (uint32_t j = 0; j < kOtRun; ++j)
+                if ((fk[r] >> j) & 1u) ost[rk++] = (sv[r][j] & keep) | ((tt >> j) & 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < nl; ++q) {               // long keys' stores: ranks by counting the marks
+        const uint32_t kl = s_long[q], rk0 = s_lrk[q];
+        const uint32_t s0 = kl ? tab[kl - 1] : 0u, m = tab[kl] - s0;
+        for (uint32_t i = tid; i < m; i += OCB) {
+            if (!((s_first[(s0 + i) >> 5] >> ((s0 + i) & 31)) & 1u)) continue;
+            const uint64_t xi = stg[s0 + i];
+            uint32_t rk = 0, tomb = 0;
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint64_t y = stg[s0 + k];
+                if ((y >> tb) == (xi >> tb)) tomb |= (uint32_t)(y & 1u);
+                else if (((s_first[(s0 + k) >> 5] >> ((s0 + k) & 31)) & 1u) && (y >> tb) < (xi >> tb)) ++rk;
+            }
+            ost[rk0 + rk] = (xi & keep) | tomb;
+        }
+    }
+    __syncthreads();
+    const uint32_t nt = s_tot;
+    for (uint32_t i = tid; i < nt; i += OCB) dst[i] = ost[i];
+}
+
+// chunk i's tags (tmp[bounds[i], + cnt[i])) decoded to out[loc[i], ...)
+__global__ __launch_bounds__(256) void k_or_emit(const uint64_t *__restrict__ tmp, const SortPlan *__restrict__ plan_,
+                                                 const uint64_t *__restrict__ bounds, const uint32_t *__restrict__ cnt,
+                                                 const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
+                                                 crdt_tuples out, uint64_t *__restrict__ out_count) {
+    const SortPlan p = *plan_;
+    const uint32_t i = blockIdx.x, m = cnt[i];
+    if (i == 0 && threadIdx.x == 0) *out_count = tot[0];
+    const uint64_t *src = tmp + bounds[i];
+    const size_t o = loc[i];
+    const uint32_t kb = p.b0 + p.br + p.bt, st = p.b0 + p.br;
+    for (uint32_t j = threadIdx.x; j < m; j += 256) {
+        const uint64_t x = src[j];
+        out.key[o + j] = p.kmin + lt_field(x, kb, p.bk);
+        out.ts[o + j] = p.tmin + lt_field(x, st, p.bt);
+        out.rep[o + j] = (uint32_t)(p.rmin + lt_field(x, p.b0, p.br));
+        out.tomb[o + j] = (uint8_t)(x & 1u);
+    }
+}
+
 // ---------------------------------------------------------------- OR-Set: groups put in tag order
 // The fused OR-Set merge sorts on the KEY's bits and one more tag digit
 // (sort.or_key_only = 2; config D: 32 of 51 bits, 4 passes instead of 7):
@@ -1641,8 +1979,12 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
     const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
-    const size_t b_flag = Carve::round(256 * 8);
-    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + 1024);
+    const size_t b_flag = Carve::round(257 * 8);
+    constexpr size_t kMaxChunks = 1u << 16;             // k_or_chunk: 2^(bk - 10), bk <= 26
+    const size_t b_chunk = MODE == DD_OR ? Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
+                                               Carve::round(64)
+                                         : 0;
+    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + b_chunk + 1024);
     if (rc) return rc;
     Carve w(ctx->ws);
     SortMinMax *mm = w.take<SortMinMax>(2 * MM_BLOCKS);
@@ -1651,13 +1993,19 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint32_t *loc = w.take<uint32_t>(ncnt);
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
-    unsigned long long *flags = w.take<unsigned long long>(256);
+    unsigned long long *flags = w.take<unsigned long long>(257);
+    uint64_t *cb = MODE == DD_OR ? w.take<uint64_t>(kMaxChunks + 1) : nullptr;      // chunk bounds, counts, offsets
+    uint32_t *cc = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
+    uint32_t *cl = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
+    uint32_t *ct = MODE == DD_OR ? w.take<uint32_t>(16) : nullptr;
     const unsigned nmm = launch_minmax(ctx, A, na, B, nb, mm);
-    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u,
-                                  MODE == DD_LWW ? (uint32_t)g_lww_table : 0u);
+    const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
+    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, MODE == DD_LWW ? (uint32_t)g_lww_table : 0u,
+                                  MODE == DD_OR ? (uint32_t)g_or_table : 0u, (uint64_t)n);
     SortPlan h;
     rc = read_plan(ctx, plan, &h);
     if (rc) return rc;
+
     uint64_t *sorted = nullptr;
     if (h.words == 1) {
         auto vec_ok = [](const crdt_tuples &t, size_t m) {
@@ -1673,6 +2021,27 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
             else
                 k_lww_table<uint64_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
             return check_launch(ctx);
+        }
+        if (MODE == DD_OR && h.tw) {                    // two passes on the key's top 16 bits, then chunks in LDS
+            rc = sort_words<1>(ctx, A, n, *out, plan, 2, bufs, cnt, loc, tot, false, &sorted, vec, flags);
+            if (rc) return rc;
+            const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
+            uint64_t *tmp = sorted == bufs ? bufs + n : bufs;
+            k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, cb);
+            k_or_chunk<<<nch, OCB, 0, s>>>(sorted, tmp, plan, cb, cc, (uint32_t *)&flags[256], g_rdd_diag);
+            k_sort_colscan<<<1, CSB, 0, s>>>(cc, nch, cl, ct);
+            k_or_emit<<<nch, 256, 0, s>>>(tmp, plan, cb, cc, cl, ct, *out, out_count);
+            rc = check_launch(ctx);
+            if (rc) return rc;
+            rc = hio_reserve(ctx, 8);                   // the fallback word (long keys)
+            if (rc) return rc;
+            hipError_t e = hipMemcpyAsync(ctx->hio, &flags[256], 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+            if (*(const uint32_t *)ctx->hio == 0) return CRDT_OK;
+            k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, 0u, 0u, (uint64_t)n);
+            rc = read_plan(ctx, plan, &h);              // the sort path from the untouched inputs
+            if (rc) return rc;
         }
         rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted, vec);
         if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup

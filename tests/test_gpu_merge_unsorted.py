@@ -146,6 +146,7 @@ def test_unsorted_orset_sort_modes(eng, mode):
     of equal sorted bits marked in LDS.  All == the oracle."""
     from crdt_amd import _lib
     _lib.call("crdt_set_option", b"sort.or_key_only", mode)
+    _lib.call("crdt_set_option", b"sort.or_table", 0)
     try:
         ks = 30_000
         _check(eng, synth.set_tuples(71, 0, 100_000, ks), synth.set_tuples(71, 1, 90_000, ks))
@@ -154,6 +155,7 @@ def test_unsorted_orset_sort_modes(eng, mode):
         test_unsorted_single_tag(eng, 5000)
     finally:
         _lib.call("crdt_set_option", b"sort.or_key_only", 2)
+        _lib.call("crdt_set_option", b"sort.or_table", 1)
 
 
 @pytest.mark.parametrize("kbits,tbits", [(11, 20), (12, 20), (16, 20), (20, 8), (23, 20), (24, 20),
@@ -162,9 +164,11 @@ def test_unsorted_lww_key_tables(eng, kbits, tbits):
     """LWW D2 by key-bucket LDS tables (sort.lww_table; taken when the key
     offsets span 12..23 bits with tags of <= 31 bits, 12..22 bits with wider
     tags; 11 / 24 key bits and 23 bits with wide tags keep the key-only
-    sort): with the tables on and off == the oracle.  Keys offset far from 0
-    and spanning their full width, 80 % of the tuples in one key bucket,
-    cross-side equal tags with differing tombs, one side shorter."""
+    sort) and OR-Set D2 by key chunks sorted in LDS (sort.or_table; 16..26
+    key bits, <= 3072 tuples per 2^10-key chunk on average): with both on and off == the
+    oracle.  Keys offset far from 0 and spanning their full width, 80 % of
+    the tuples in one key bucket, cross-side equal tags with differing
+    tombs, one side shorter."""
     from crdt_amd import _lib
     rng = np.random.default_rng(kbits * 100 + tbits)
 
@@ -185,7 +189,50 @@ def test_unsorted_lww_key_tables(eng, kbits, tbits):
     try:
         for on in (1, 0):
             _lib.call("crdt_set_option", b"sort.lww_table", on)
+            _lib.call("crdt_set_option", b"sort.or_table", on)
             _check(eng, a, b)
             _check(eng, a, tuple(x[:0] for x in b))
     finally:
         _lib.call("crdt_set_option", b"sort.lww_table", 1)
+        _lib.call("crdt_set_option", b"sort.or_table", 1)
+
+
+def _keyed(rng, keys, tbits=6):
+    m = len(keys)
+    ts = rng.integers(0, 2**tbits, m, dtype=np.uint64)
+    rep = rng.integers(0, 3, m, dtype=np.uint64).astype(np.uint32)
+    tomb = rng.integers(0, 2, m, dtype=np.uint8)
+    side = rng.integers(0, 2, m).astype(bool)
+    p = rng.permutation(m)
+    keys, ts, rep, tomb, side = keys[p], ts[p], rep[p], tomb[p], side[p]
+    a = tuple(np.ascontiguousarray(x[~side]) for x in (keys, ts, rep, tomb))
+    b = tuple(np.ascontiguousarray(x[side]) for x in (keys, ts, rep, tomb))
+    return a, b
+
+
+@pytest.mark.parametrize("case", ["long_keys", "key_of_2000", "too_many_long_keys", "chunk_over_cap"])
+def test_unsorted_orset_tables_long_keys(eng, case):
+    """OR-Set key chunks sorted in LDS around their limits (20 key bits:
+    1024 chunks of 2^10 keys): keys of 9..60 tuples (the workgroup's long-key
+    path, few ts values so tags repeat within a key), a key of 2000 tuples,
+    300 keys of 9 tuples in one chunk (over the 256 long keys a chunk lists)
+    and one chunk of 9000+ tuples (over its 4096 in LDS): the last two fall
+    back to the radix sort.  All == the oracle, chunks on and off."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng({"long_keys": 1, "key_of_2000": 2, "too_many_long_keys": 3, "chunk_over_cap": 4}[case])
+    bg = rng.integers(0, 2**20, 150_000, dtype=np.uint64)
+    if case == "long_keys":
+        extra = np.repeat(rng.choice(2**20, 400, replace=False).astype(np.uint64), rng.integers(9, 61, 400))
+    elif case == "key_of_2000":
+        extra = np.full(2000, 77, np.uint64)
+    elif case == "too_many_long_keys":
+        extra = np.repeat(np.arange(300, dtype=np.uint64), 9)
+    else:
+        extra = np.full(9000, 5, np.uint64)
+    a, b = _keyed(rng, np.concatenate([bg, extra, np.array([2**20 - 1], np.uint64)]))
+    try:
+        for on in (1, 0):
+            _lib.call("crdt_set_option", b"sort.or_table", on)
+            _check(eng, a, b)
+    finally:
+        _lib.call("crdt_set_option", b"sort.or_table", 1)
