@@ -173,10 +173,14 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
 /* The same two merges on UNSORTED inputs (config D2), as one device sort of
  * both sides together with a side bit between rep and tomb -- composite
  * order (key, ts, rep, side, tomb) is the stable merge of the two sorted
- * sides -- followed by a neighbour dedup of the sorted composites.  Output
- * identical to crdt_tuples_sort of each side then crdt_lww_merge /
- * crdt_orset_merge.  Synchronises the stream once (to size the passes).
- * na + nb < 2^32; out capacity >= na + nb. */
+ * sides -- followed by a neighbour dedup of the sorted composites.  Where
+ * the key offsets are dense enough the sort stops early: LWW after one pass
+ * on the key's top byte (each key's winner kept in an LDS table per
+ * bucket), OR-Set after two passes on its top 16 bits (each 2^9-key chunk
+ * sorted in LDS).  Output identical to crdt_tuples_sort of each side then
+ * crdt_lww_merge / crdt_orset_merge.  Synchronises the stream once to size
+ * the passes (the OR-Set chunk form a second time, to confirm no chunk
+ * outgrew its LDS).  na + nb < 2^32; out capacity >= na + nb. */
 int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                             size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
