@@ -1123,14 +1123,12 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 //   k_or_chunk: the chunk's tuples into registers, a counting sort by key
 //     into LDS (count per key, scan, scatter by LDS atomics), then one thread
 //     per key finds the key's distinct tags -- a key of <= kOtRun tuples
-//     read at once and resolved in registers (element j is its tag's first
-//     copy when no other element has its tag and a smaller composite, an
-//     equal one a lower index); a longer key by the whole workgroup (marks
-//     in LDS, ranks by counting) -- and places them in tag order, tomb =
-//     the OR of the tag's copies, as composites (side bit cleared) in LDS,
-//     then copies them out at once to the chunk's own input range of `tmp`
-//     (stored straight from each key's thread they were partial-line
-//     scatters: 238 us of a 403 us pass), plus the chunk's count;
+//     sorted in registers by a sorting network, <= kOtMid by an insertion
+//     sort of its own slots in LDS, a longer key by the whole workgroup
+//     (first-copy marks in LDS, ranks by counting) -- and places them in tag
+//     order, tomb = the OR of the tag's copies, as composites (side bit
+//     cleared) in LDS, then copies them out at once to the chunk's own input
+//     range of `tmp`, plus the chunk's count;
 //   k_sort_colscan over the chunk counts;
 //   k_or_emit: each chunk's tags decoded into the SoA output at its offset.
 // A chunk of more than kOcCap tuples (skewed keys) or of more than kOcLong
@@ -1146,6 +1144,7 @@ constexpr uint32_t kOcKeys = 1u << kOcBits;
 constexpr uint32_t kOcCap = 2048;        // tuples per chunk (LDS); more -> fallback
 constexpr uint32_t kOcPer = kOcCap / OCB;
 constexpr uint32_t kOtRun = 8;           // keys of up to this many tuples: one thread, registers
+constexpr uint32_t kOtMid = 32;          // up to this many: one thread, an insertion sort of its slots in LDS
 constexpr uint32_t kOcLong = 256;        // longer keys per chunk (LDS list); more -> the workgroup loops
 
 // a key's <= kOtRun tuples sorted in registers (Batcher's 19-comparator
@@ -1287,13 +1286,23 @@ __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c
         const uint32_t ms = m <= kOtRun ? m : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < kOtRun; ++k) sv[r][k] = k < ms ? stg[s0 + k] : ~0ull;
-        if (m > kOtRun) {
-            const uint32_t q = atomicAdd(&s_nlong, 1u);
-            if (q < kOcLong) s_long[q] = kl;
-        }
         if (ms > 1) ot_sort8(sv[r]);
         fk[r] = ot_firsts(sv[r], ms, tb);
         dk[r] = (uint32_t)__popc(fk[r]);
+        if (m > kOtMid) {
+            const uint32_t q = atomicAdd(&s_nlong, 1u);
+            if (q < kOcLong) s_long[q] = kl;
+        } else if (m > kOtRun) {                      // (rare: a wave with such a key waits for it)
+            for (uint32_t i = 1; i < m; ++i) {
+                const uint64_t xv = stg[s0 + i];
+                uint32_t j = i;
+                for (; j > 0 && stg[s0 + j - 1] > xv; --j) stg[s0 + j] = stg[s0 + j - 1];
+                stg[s0 + j] = xv;
+            }
+            uint32_t d = 1;
+            for (uint32_t i = 1; i < m; ++i) d += (stg[s0 + i] >> tb) != (stg[s0 + i - 1] >> tb) ? 1u : 0u;
+            dk[r] = d;
+        }
     }
     __syncthreads();
     const uint32_t nl = s_nlong;
@@ -1377,9 +1386,18 @@ __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c
             if (lane >= o) y += t;
         }
         const uint32_t rk0 = s_cnt[r * OC_WAVES + w] + y - d;   // the key's first rank in the chunk
-        if (m > kOtRun) {
+        if (m > kOtMid) {
             for (uint32_t q = 0; q < nl; ++q)
                 if (s_long[q] == kl) s_lrk[q] = rk0;
+        } else if (m > kOtRun) {                      // its sorted slots in LDS: one walk
+            uint32_t rk = rk0;
+            for (uint32_t i = 0; i < m;) {
+                const uint64_t x0 = stg[s0 + i];
+                uint32_t tomb = (uint32_t)(x0 & 1u), k = i + 1;
+                for (; k < m && (stg[s0 + k] >> tb) == (x0 >> tb); ++k) tomb |= (uint32_t)(stg[s0 + k] & 1u);
+                ost[rk++] = (x0 & keep) | tomb;
+                i = k;
+            }
         } else if (m > 0) {
             // the OR of each tag's tombs, from the right: run = slot j's tomb,
             // plus the run after it while the tag continues
