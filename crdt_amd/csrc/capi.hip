@@ -28,7 +28,7 @@ int g_rm_ld_all = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
-int g_or_table = 1;      // OR-Set D2: key-bucket counting sorts (same key spans, <= 4 tuples per key)
+int g_or_table = 1;      // OR-Set D2: 2^9-key chunks sorted in LDS after two top-16-bit passes (16..25 key bits)
 int g_rdd_diag = 0;
 int g_mm_bpc = 1;        // sort minmax: workgroups per CU per input (1: 0.716 ms LWW D2 step, 4: 0.732)
 int g_lww_parts = 4;     // LWW write pass: quarter tiles (half tiles 112 -> 105 us)
@@ -312,12 +312,12 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         g_mm_bpc = (int)v;
     } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: the D2 dedup apply (OR-Set: and count)
         if (v < 0 || v > 4) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores);
-                                                        //   OR-Set tables: 1 key counts, 2 scatter, 3 per-key tags, 4 long keys
+                                                        //   OR-Set chunks: 1 key counts, 2 LDS sort, 3 per-key tags, 4 long keys + ranks
         g_rdd_diag = (int)v;
     } else if (!strcmp(name, "sort.lww_table")) {    // LWW D2: 1 key-bucket LDS tables where they apply, 0 key-only sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_lww_table = (int)v;
-    } else if (!strcmp(name, "sort.or_table")) {     // OR-Set D2: 1 key-bucket counting sorts where they apply, 0 the radix sort
+    } else if (!strcmp(name, "sort.or_table")) {     // OR-Set D2: 1 key chunks sorted in LDS where they apply, 0 the radix sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_table = (int)v;
     } else if (!strcmp(name, "sort.vec_up")) {       // fused D2 sort: 1 vectorised composing upsweep, 0 scalar
