@@ -28,6 +28,7 @@ int g_rm_ld_all = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
+int g_or_lookback = 1;   // OR-Set D2 chunks: offsets by a decoupled look-back (0: count scan + emit pass)
 int g_or_table = 1;      // OR-Set D2: 2^9-key chunks sorted in LDS after two top-16-bit passes (16..25 key bits)
 int g_rdd_diag = 0;
 int g_mm_bpc = 1;        // sort minmax: workgroups per CU per input (1: 0.716 ms LWW D2 step, 4: 0.732)
@@ -320,6 +321,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_table")) {     // OR-Set D2: 1 key chunks sorted in LDS where they apply, 0 the radix sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_table = (int)v;
+    } else if (!strcmp(name, "sort.or_lookback")) {  // OR-Set D2 chunks: 1 look-back offsets + direct stores, 0 scan + emit
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_lookback = (int)v;
     } else if (!strcmp(name, "sort.vec_up")) {       // fused D2 sort: 1 vectorised composing upsweep, 0 scalar
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sort_vec_up = (int)v;

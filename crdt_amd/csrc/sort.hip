@@ -1178,10 +1178,12 @@ __device__ __forceinline__ uint32_t ot_firsts(const uint64_t *v, uint32_t m, uin
 // non-decreasing in the sorted composites (every index probed once the span
 // is <= 64)
 __global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict__ c, size_t n, uint32_t cs,
-                                                      uint32_t nch, uint64_t *__restrict__ bounds) {
+                                                      uint32_t nch, uint64_t *__restrict__ bounds,
+                                                      unsigned long long *__restrict__ st) {
     const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);      // one wave per bound
     const int lane = threadIdx.x & 63;
     if (i > nch) return;
+    if (st && i < nch && lane == 0) st[i] = 0;        // k_or_chunk<true>'s look-back words
     if (i == 0 || i == nch) {
         if (lane == 0) bounds[i] = i == 0 ? 0 : n;
         return;
@@ -1202,10 +1204,21 @@ __global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict
     if (lane == 0) bounds[i] = lo;
 }
 
+// LB (sort.or_lookback): the chunk finds its output offset itself by a
+// decoupled look-back over the chunks before it and stores the SoA output
+// directly (no tmp round trip, no scan, no emit).  Status word per chunk:
+// kOcA | count once counted, kOcP | inclusive prefix once resolved; wave 0
+// reads 64 predecessors per poll, nearest first, and sums back to the
+// nearest resolved one.  Chunks are dispatched in index order, so every
+// polled chunk has been dispatched; polls are bounded (CRDT_DEV_LOOKBACK).
+constexpr unsigned long long kOcA = 1ull << 62, kOcP = 2ull << 62, kOcVal = (1ull << 62) - 1;
+template <bool LB>
 __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
                                                   const SortPlan *__restrict__ plan_,
                                                   const uint64_t *__restrict__ bounds, uint32_t *__restrict__ cnt,
-                                                  uint32_t *__restrict__ fbw, int diag) {
+                                                  uint32_t *__restrict__ fbw, int diag,
+                                                  unsigned long long *__restrict__ st, crdt_tuples out,
+                                                  uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
     constexpr uint32_t R = kOcKeys / OCB;             // keys per thread (round-major)
     __shared__ uint32_t tab[kOcKeys];
     __shared__ uint64_t stg[kOcCap];
@@ -1220,6 +1233,7 @@ __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c
         if (tid == 0) {
             atomicOr(fbw, 1u);
             cnt[blockIdx.x] = 0;
+            if (LB) __hip_atomic_store(&st[blockIdx.x], kOcA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
     }
@@ -1314,6 +1328,7 @@ __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c
         if (tid == 0) {
             atomicOr(fbw, 1u);
             cnt[blockIdx.x] = 0;
+            if (LB) __hip_atomic_store(&st[blockIdx.x], kOcA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
     }
@@ -1365,6 +1380,9 @@ __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c
         if (lane == 63) {
             cnt[blockIdx.x] = y;
             s_tot = y;
+            if (LB)                                   // counted: published at once
+                __hip_atomic_store(&st[blockIdx.x], (blockIdx.x ? kOcA : kOcP) | y, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
@@ -1433,7 +1451,56 @@ __global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c
     }
     __syncthreads();
     const uint32_t nt = s_tot;
-    for (uint32_t i = tid; i < nt; i += OCB) dst[i] = ost[i];
+    if constexpr (!LB) {
+        for (uint32_t i = tid; i < nt; i += OCB) dst[i] = ost[i];
+        return;
+    }
+    // the offset: the counts of the chunks before this one
+    __shared__ unsigned long long s_off;
+    if (w == 0) {
+        unsigned long long acc = 0;
+        if (blockIdx.x > 0) {
+            long long j = (long long)blockIdx.x - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const long long q = j - lane;
+                const unsigned long long f =
+                    q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kOcP;
+                const uint64_t isp = __ballot((f >> 62) == 2), notready = __ballot((f >> 62) == 0);
+                const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
+                const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
+                if (notready & need) {
+                    if (++spins > (1u << 22)) {       // bounded: report, never hang
+                        if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long v = lane <= pl ? (f & kOcVal) : 0ull;
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                acc += v;
+                if (pl < 64) break;
+                j -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&st[blockIdx.x], kOcP | (acc + nt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_off = acc;
+            if (blockIdx.x == gridDim.x - 1) *out_count = acc + nt;
+        }
+    }
+    __syncthreads();
+    const size_t o = s_off;
+    const uint32_t sr = p.b0 + p.br;
+    for (uint32_t i = tid; i < nt; i += OCB) {
+        const uint64_t xv = ost[i];
+        out.key[o + i] = p.kmin + lt_field(xv, kb, p.bk);
+        out.ts[o + i] = p.tmin + lt_field(xv, sr, p.bt);
+        out.rep[o + i] = (uint32_t)(p.rmin + lt_field(xv, p.b0, p.br));
+        out.tomb[o + i] = (uint8_t)(xv & 1u);
+    }
 }
 
 // chunk i's tags (tmp[bounds[i], + cnt[i])) decoded to out[loc[i], ...)
@@ -1998,8 +2065,8 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
     const size_t b_flag = Carve::round(257 * 8);
-    constexpr size_t kMaxChunks = 1u << 16;             // k_or_chunk: 2^(bk - 10), bk <= 26
-    const size_t b_chunk = MODE == DD_OR ? Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
+    constexpr size_t kMaxChunks = 1u << 16;             // k_or_chunk: 2^(bk - 9), bk <= 25
+    const size_t b_chunk = MODE == DD_OR ? 2 * Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
                                                Carve::round(64)
                                          : 0;
     rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + b_chunk + 1024);
@@ -2016,6 +2083,7 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint32_t *cc = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
     uint32_t *cl = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
     uint32_t *ct = MODE == DD_OR ? w.take<uint32_t>(16) : nullptr;
+    unsigned long long *cst = MODE == DD_OR ? w.take<unsigned long long>(kMaxChunks + 1) : nullptr;   // look-back words
     const unsigned nmm = launch_minmax(ctx, A, na, B, nb, mm);
     const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
     k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, MODE == DD_LWW ? (uint32_t)g_lww_table : 0u,
@@ -2045,10 +2113,17 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
             if (rc) return rc;
             const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
             uint64_t *tmp = sorted == bufs ? bufs + n : bufs;
-            k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, cb);
-            k_or_chunk<<<nch, OCB, 0, s>>>(sorted, tmp, plan, cb, cc, (uint32_t *)&flags[256], g_rdd_diag);
-            k_sort_colscan<<<1, CSB, 0, s>>>(cc, nch, cl, ct);
-            k_or_emit<<<nch, 256, 0, s>>>(tmp, plan, cb, cc, cl, ct, *out, out_count);
+            const bool lb = g_or_lookback && !g_rdd_diag;
+            k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, cb, lb ? cst : nullptr);
+            if (lb) {
+                k_or_chunk<true><<<nch, OCB, 0, s>>>(sorted, tmp, plan, cb, cc, (uint32_t *)&flags[256], 0, cst, *out,
+                                                     out_count, ctx->dev_status);
+            } else {
+                k_or_chunk<false><<<nch, OCB, 0, s>>>(sorted, tmp, plan, cb, cc, (uint32_t *)&flags[256], g_rdd_diag,
+                                                      nullptr, *out, out_count, ctx->dev_status);
+                k_sort_colscan<<<1, CSB, 0, s>>>(cc, nch, cl, ct);
+                k_or_emit<<<nch, 256, 0, s>>>(tmp, plan, cb, cc, cl, ct, *out, out_count);
+            }
             rc = check_launch(ctx);
             if (rc) return rc;
             rc = hio_reserve(ctx, 8);                   // the fallback word (long keys)

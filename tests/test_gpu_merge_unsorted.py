@@ -217,7 +217,8 @@ def test_unsorted_orset_tables_long_keys(eng, case):
     path, few ts values so tags repeat within a key), a key of 2000 tuples,
     300 keys of 9 tuples in one chunk (over the 256 long keys a chunk lists)
     and one chunk of 9000+ tuples (over its 4096 in LDS): the last two fall
-    back to the radix sort.  All == the oracle, chunks on and off."""
+    back to the radix sort.  All == the oracle: chunks with look-back
+    offsets, chunks with the scan + emit pass, and the radix path."""
     from crdt_amd import _lib
     rng = np.random.default_rng({"long_keys": 1, "key_of_2000": 2, "too_many_long_keys": 3, "chunk_over_cap": 4}[case])
     bg = rng.integers(0, 2**20, 150_000, dtype=np.uint64)
@@ -231,8 +232,10 @@ def test_unsorted_orset_tables_long_keys(eng, case):
         extra = np.full(9000, 5, np.uint64)
     a, b = _keyed(rng, np.concatenate([bg, extra, np.array([2**20 - 1], np.uint64)]))
     try:
-        for on in (1, 0):
+        for on, lb in ((1, 1), (1, 0), (0, 1)):
             _lib.call("crdt_set_option", b"sort.or_table", on)
+            _lib.call("crdt_set_option", b"sort.or_lookback", lb)
             _check(eng, a, b)
     finally:
         _lib.call("crdt_set_option", b"sort.or_table", 1)
+        _lib.call("crdt_set_option", b"sort.or_lookback", 1)

@@ -10,8 +10,8 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_merge_unsorted.py tests/tes
     --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 cd /tmp && export TMPDIR=/tmp
-for v in d3 d4 on off on off; do
-  case $v in d?) opt="--option sort.rdd_diag=${v#d}";; on) opt="--option sort.or_table=1";; off) opt="--option sort.or_table=0";; esac
+for v in lb1 lb0 lb1 lb0; do
+  case $v in lb?) opt="--option sort.or_lookback=${v#lb}";; d?) opt="--option sort.rdd_diag=${v#d}";; on) opt="--option sort.or_table=1";; off) opt="--option sort.or_table=0";; esac
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t_$v -o run -- \
       python3 $R/bench.py --workload orset_merge_d2 --steps 20 --warmup 3 --no-e2e --no-cpu-baseline $opt \
       > $OUT/b_$v.json 2> $OUT/b_$v.err || { tail -3 $OUT/b_$v.err; exit 1; }
