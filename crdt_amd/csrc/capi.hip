@@ -28,6 +28,8 @@ int g_rm_ld_all = 0;
 int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
+int g_sample_plan = 1;   // dense-key D2 paths from a sampled plan, checked in the upsweep (sort.sample_plan)
+int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
 int g_or_lookback = 1;   // OR-Set D2 chunks: offsets by a decoupled look-back (0: count scan + emit pass)
 int g_or_table = 1;      // OR-Set D2: 2^9-key chunks sorted in LDS after two top-16-bit passes (16..25 key bits)
 int g_rdd_diag = 0;
@@ -321,6 +323,12 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_table")) {     // OR-Set D2: 1 key chunks sorted in LDS where they apply, 0 the radix sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_table = (int)v;
+    } else if (!strcmp(name, "sort.sample_plan")) {  // D2 dense-key paths: 1 plan from a sample + range check, 0 full minmax
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_sample_plan = (int)v;
+    } else if (!strcmp(name, "sort.sample_min")) {   // fewest tuples for the sampled plan
+        if (v < 0 || v > 0x7FFFFFFF) return CRDT_E_INVAL;
+        g_sample_min = (int)v;
     } else if (!strcmp(name, "sort.or_lookback")) {  // OR-Set D2 chunks: 1 look-back offsets + direct stores, 0 scan + emit
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_lookback = (int)v;

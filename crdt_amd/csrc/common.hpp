@@ -68,6 +68,8 @@ extern int g_vclock_blocks_per_cu;
 extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
 extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
 extern int g_lww_table;        // LWW D2 key-bucket tables (sort.lww_table)
+extern int g_sample_plan;      // D2 dense-key paths from a sampled plan (sort.sample_plan)
+extern int g_sample_min;       // ... from this many tuples (sort.sample_min)
 extern int g_or_lookback;      // OR-Set D2 chunk offsets by look-back (sort.or_lookback)
 extern int g_or_table;         // OR-Set D2 key chunks sorted in LDS (sort.or_table)
 extern int g_sort_vec_up;       // fused D2 sort: vectorised composing upsweep (sort.vec_up)

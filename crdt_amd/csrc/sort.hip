@@ -162,13 +162,70 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, co
     return ga + gb;
 }
 
+// A SAMPLE of both inputs' field ranges (sort.sample_plan): 32768 evenly
+// spaced tuples per side, 2 per thread, partials in the minmax format.  The
+// plan widens the sampled ranges (k_sort_plan's margin) and the composing
+// upsweep checks every tuple against them (the violation word): the dense-key
+// D2 paths then skip the full minmax read (400 MB at config D) and redo the
+// call from an exact plan only when a tuple fell outside.
+constexpr unsigned SAMPLE_WG = 64;       // workgroups per side
+__global__ __launch_bounds__(256) void k_sample_minmax(crdt_tuples in, size_t n, crdt_tuples in2, size_t n2,
+                                                       SortMinMax *mm) {
+    const bool second = blockIdx.x >= SAMPLE_WG;
+    const crdt_tuples t = second ? in2 : in;
+    const size_t m = second ? n2 : n;
+    constexpr size_t NS = (size_t)SAMPLE_WG * 256 * 2;
+    unsigned long long kmin = ~0ULL, kmax = 0, tmin = ~0ULL, tmax = 0, rmin = ~0ULL, rmax = 0;
+    const size_t s0 = ((size_t)(blockIdx.x % SAMPLE_WG) * 256 + threadIdx.x) * 2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const size_t i = m > NS ? (s0 + u) * m / NS : s0 + u;
+        if (i < m) {
+            const unsigned long long k = t.key[i], ts = t.ts[i], r = t.rep[i];
+            kmin = k < kmin ? k : kmin;
+            kmax = k > kmax ? k : kmax;
+            tmin = ts < tmin ? ts : tmin;
+            tmax = ts > tmax ? ts : tmax;
+            rmin = r < rmin ? r : rmin;
+            rmax = r > rmax ? r : rmax;
+        }
+    }
+    for (int w = 32; w >= 1; w >>= 1) {
+        kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, w, 64));
+        kmax = max(kmax, (unsigned long long)__shfl_xor(kmax, w, 64));
+        tmin = min(tmin, (unsigned long long)__shfl_xor(tmin, w, 64));
+        tmax = max(tmax, (unsigned long long)__shfl_xor(tmax, w, 64));
+        rmin = min(rmin, (unsigned long long)__shfl_xor(rmin, w, 64));
+        rmax = max(rmax, (unsigned long long)__shfl_xor(rmax, w, 64));
+    }
+    __shared__ unsigned long long sred[6][4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sred[0][w] = kmin;
+        sred[1][w] = kmax;
+        sred[2][w] = tmin;
+        sred[3][w] = tmax;
+        sred[4][w] = rmin;
+        sred[5][w] = rmax;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int f = threadIdx.x;
+        unsigned long long v = sred[f][0];
+        for (int k = 1; k < 4; ++k) v = (f & 1) ? max(v, sred[f][k]) : min(v, sred[f][k]);
+        (&mm[blockIdx.x].kmin)[f] = v;
+    }
+}
+
 // reduces the nmm minmax partials, then thread 0 sizes the composite
 __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32_t nmm, SortPlan *plan,
                                                    uint32_t side_bits, crdt_tuples in2, uint64_t n1,
                                                    uint32_t key_only = 0, uint32_t lww_table = 0,
-                                                   uint32_t or_table = 0, uint64_t n_all = 0) {
+                                                   uint32_t or_table = 0, uint64_t n_all = 0,
+                                                   uint32_t margin = 0, uint32_t *viol = nullptr) {
     __shared__ unsigned long long sr[6][256];
     const int tid = threadIdx.x;
+    if (viol && tid == 0) *viol = 0;                  // the upsweep's range check starts clean
     unsigned long long v[6] = {~0ULL, 0, ~0ULL, 0, ~0ULL, 0};
     for (uint32_t i = tid; i < nmm; i += 256)
 #pragma unroll
@@ -192,7 +249,19 @@ __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32
     const unsigned long long r = sr[tid][0];
     const SortMinMax m{__shfl(r, 0), __shfl(r, 1), __shfl(r, 2), __shfl(r, 3), __shfl(r, 4), __shfl(r, 5)};
     if (tid != 0) return;
-    const SortMinMax *mm = &m;
+    SortMinMax mw = m;
+    if (margin) {                                     // sampled ranges, widened by 1/256 of their span
+        auto widen = [](unsigned long long &lo, unsigned long long &hi, unsigned long long cap) {
+            if (lo > hi) return;                      // (no sample)
+            const unsigned long long pad = (hi - lo) >> 8;
+            lo = lo > pad ? lo - pad : 0;
+            hi = cap - hi > pad ? hi + pad : cap;
+        };
+        widen(mw.kmin, mw.kmax, ~0ULL);
+        widen(mw.tmin, mw.tmax, ~0ULL);
+        widen(mw.rmin, mw.rmax, 0xFFFFFFFFULL);
+    }
+    const SortMinMax *mm = &mw;
     SortPlan p;
     p.b0 = 1 + side_bits;
     p.n1 = n1;
@@ -364,15 +433,21 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
 // loads per tuple).  Needs key / ts 16-byte, rep 8-byte, tomb 2-byte aligned
 // sides and an even n1 (no pair straddles the two inputs); the histogram
 // counts do not depend on which lane composes which tuple.
+__device__ __forceinline__ bool outside(uint64_t off, uint32_t b) { return b < 64 && (off >> b) != 0; }
+
 __global__ __launch_bounds__(SB) void k_sort_up_vec(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                     uint32_t ntiles, uint32_t *__restrict__ cnt,
-                                                    uint64_t *__restrict__ comp) {
+                                                    uint64_t *__restrict__ comp, uint32_t *__restrict__ viol) {
     __shared__ uint32_t h[SWAVES * 256];
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
     const SortPlan p = *plan_;
     const size_t base = (size_t)blockIdx.x * ST;
     uint64_t c[SR];
+    bool bad = false;                                 // (viol) a field outside the plan's ranges
+    auto out_of = [&](uint64_t k, uint64_t t, uint32_t r) {
+        return outside(k - p.kmin, p.bk) || outside(t - p.tmin, p.bt) || outside((uint64_t)r - p.rmin, p.br);
+    };
 #pragma unroll
     for (int r = 0; r < SR / 2; ++r) {
         const size_t e = base + 2 * ((size_t)r * SB + tid);
@@ -385,14 +460,17 @@ __global__ __launch_bounds__(SB) void k_sort_up_vec(crdt_tuples in, size_t n, co
             const ulonglong2 k = *(const ulonglong2 *)(T.key + f), t = *(const ulonglong2 *)(T.ts + f);
             const uint2 rp = *(const uint2 *)(T.rep + f);
             const uint16_t tb = *(const uint16_t *)(T.tomb + f);
+            if (viol) bad = bad || out_of(k.x, t.x, rp.x) || out_of(k.y, t.y, rp.y);
             c[2 * r] = compose<1>(p, k.x, t.x, rp.x, (uint8_t)(tb & 0xFF), side).w[0];
             c[2 * r + 1] = compose<1>(p, k.y, t.y, rp.y, (uint8_t)(tb >> 8), side).w[0];
             *(ulonglong2 *)(comp + e) = ulonglong2{c[2 * r], c[2 * r + 1]};
         } else {
+            if (viol) bad = bad || out_of(T.key[f], T.ts[f], T.rep[f]);
             c[2 * r] = compose<1>(p, T.key[f], T.ts[f], T.rep[f], T.tomb[f], side).w[0];
             comp[e] = c[2 * r];
         }
     }
+    if (viol && __ballot(bad) && (tid & 63) == 0) atomicOr(viol, 1u);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
@@ -603,14 +681,14 @@ template <int WORDS>
 static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt_tuples &out, const SortPlan *plan_d,
                       uint32_t P, uint64_t *bufs, uint32_t *cnt, uint32_t *loc, uint32_t *tot, bool decode = true,
                       uint64_t **result = nullptr, bool vec_first = false,
-                      unsigned long long *zero = nullptr) {
+                      unsigned long long *zero = nullptr, uint32_t *viol = nullptr) {
     const hipStream_t st = ctx->stream;
     const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
     uint64_t *a = bufs, *b = bufs + (size_t)WORDS * n;
     for (uint32_t q = 0; q < P; ++q) {
         // pass 0's upsweep composes from the tuples and stores the composites
         if (q == 0 && WORDS == 1 && vec_first)
-            k_sort_up_vec<<<ntiles, SB, 0, st>>>(in, n, plan_d, ntiles, cnt, a);
+            k_sort_up_vec<<<ntiles, SB, 0, st>>>(in, n, plan_d, ntiles, cnt, a, viol);
         else if (q == 0)
             k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a);
         else
@@ -2047,7 +2125,7 @@ static bool tuples_full(const crdt_tuples *t) { return t && t->key && t->ts && t
 
 template <int MODE>
 static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
-                              crdt_tuples *out, uint64_t *out_count) {
+                              crdt_tuples *out, uint64_t *out_count, bool allow_sample = true) {
     int rc = bind(ctx);
     if (rc) return rc;
     if (!out_count || !tuples_full(out)) return CRDT_E_INVAL;
@@ -2064,7 +2142,7 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
     const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
-    const size_t b_flag = Carve::round(257 * 8);
+    const size_t b_flag = Carve::round(258 * 8);
     constexpr size_t kMaxChunks = 1u << 16;             // k_or_chunk: 2^(bk - 9), bk <= 25
     const size_t b_chunk = MODE == DD_OR ? 2 * Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
                                                Carve::round(64)
@@ -2078,38 +2156,62 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     uint32_t *loc = w.take<uint32_t>(ncnt);
     uint32_t *tot = w.take<uint32_t>(256);
     uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
-    unsigned long long *flags = w.take<unsigned long long>(257);
+    unsigned long long *flags = w.take<unsigned long long>(258);
+    uint32_t *viol = (uint32_t *)&flags[257];        // the sampled plan's range check
     uint64_t *cb = MODE == DD_OR ? w.take<uint64_t>(kMaxChunks + 1) : nullptr;      // chunk bounds, counts, offsets
     uint32_t *cc = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
     uint32_t *cl = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
     uint32_t *ct = MODE == DD_OR ? w.take<uint32_t>(16) : nullptr;
     unsigned long long *cst = MODE == DD_OR ? w.take<unsigned long long>(kMaxChunks + 1) : nullptr;   // look-back words
-    const unsigned nmm = launch_minmax(ctx, A, na, B, nb, mm);
+    auto vec_ok = [](const crdt_tuples &t, size_t m) {
+        return m == 0 || !((((uintptr_t)t.key | (uintptr_t)t.ts) & 15) | ((uintptr_t)t.rep & 7) |
+                           ((uintptr_t)t.tomb & 1));
+    };
+    const bool vec = vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
     const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
-    k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, MODE == DD_LWW ? (uint32_t)g_lww_table : 0u,
-                                  MODE == DD_OR ? (uint32_t)g_or_table : 0u, (uint64_t)n);
+    const uint32_t lww_t = MODE == DD_LWW ? (uint32_t)g_lww_table : 0u, or_t = MODE == DD_OR ? (uint32_t)g_or_table : 0u;
     SortPlan h;
-    rc = read_plan(ctx, plan, &h);
-    if (rc) return rc;
+    // the dense-key paths from a sampled plan (sort.sample_plan): checked by
+    // the composing upsweep, the call redone from the exact plan on a miss
+    bool sampled = false;
+    unsigned nmm = 0;
+    if (allow_sample && g_sample_plan && vec && (lww_t || or_t) && n >= (size_t)g_sample_min) {
+        nmm = 2 * SAMPLE_WG;
+        k_sample_minmax<<<nmm, 256, 0, s>>>(A, na, B, nb, mm);
+        k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n, 1u, viol);
+        rc = read_plan(ctx, plan, &h);
+        if (rc) return rc;
+        sampled = h.words == 1 && h.tw;
+    }
+    if (!sampled) {
+        nmm = launch_minmax(ctx, A, na, B, nb, mm);
+        k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n);
+        rc = read_plan(ctx, plan, &h);
+        if (rc) return rc;
+    }
+    uint32_t *vw = sampled ? viol : nullptr;          // (a miss: the call again from the exact plan)
 
     uint64_t *sorted = nullptr;
     if (h.words == 1) {
-        auto vec_ok = [](const crdt_tuples &t, size_t m) {
-            return m == 0 || !((((uintptr_t)t.key | (uintptr_t)t.ts) & 15) | ((uintptr_t)t.rep & 7) |
-                               ((uintptr_t)t.tomb & 1));
-        };
-        const bool vec = vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
         if (MODE == DD_LWW && h.tw) {                   // one pass on the key's top byte, then bucket tables
-            rc = sort_words<1>(ctx, A, n, *out, plan, 1, bufs, cnt, loc, tot, false, &sorted, vec, flags);
+            rc = sort_words<1>(ctx, A, n, *out, plan, 1, bufs, cnt, loc, tot, false, &sorted, vec, flags, vw);
             if (rc) return rc;
             if (h.tw == 4)
                 k_lww_table<uint32_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
             else
                 k_lww_table<uint64_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
-            return check_launch(ctx);
+            rc = check_launch(ctx);
+            if (rc || !sampled) return rc;
+            rc = hio_reserve(ctx, 8);                   // the range check
+            if (rc) return rc;
+            hipError_t e = hipMemcpyAsync(ctx->hio, viol, 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+            if (*(const uint32_t *)ctx->hio == 0) return CRDT_OK;
+            return set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false);
         }
         if (MODE == DD_OR && h.tw) {                    // two passes on the key's top 16 bits, then chunks in LDS
-            rc = sort_words<1>(ctx, A, n, *out, plan, 2, bufs, cnt, loc, tot, false, &sorted, vec, flags);
+            rc = sort_words<1>(ctx, A, n, *out, plan, 2, bufs, cnt, loc, tot, false, &sorted, vec, flags, vw);
             if (rc) return rc;
             const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
             uint64_t *tmp = sorted == bufs ? bufs + n : bufs;
@@ -2126,12 +2228,15 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
             }
             rc = check_launch(ctx);
             if (rc) return rc;
-            rc = hio_reserve(ctx, 8);                   // the fallback word (long keys)
+            rc = hio_reserve(ctx, 16);                  // the fallback word (long keys), the range check
             if (rc) return rc;
-            hipError_t e = hipMemcpyAsync(ctx->hio, &flags[256], 4, hipMemcpyDeviceToHost, s);
+            hipError_t e = hipMemcpyAsync(ctx->hio, &flags[256], 16, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) return hip_fail(ctx, e);
-            if (*(const uint32_t *)ctx->hio == 0) return CRDT_OK;
+            const uint32_t fb = *(const uint32_t *)ctx->hio, miss = sampled ? ((const uint32_t *)ctx->hio)[2] : 0u;
+            if (fb == 0 && miss == 0) return CRDT_OK;
+            if (miss) return set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false);
+            if (sampled) nmm = launch_minmax(ctx, A, na, B, nb, mm);   // the exact ranges for the sort path
             k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, 0u, 0u, (uint64_t)n);
             rc = read_plan(ctx, plan, &h);              // the sort path from the untouched inputs
             if (rc) return rc;

@@ -239,3 +239,34 @@ def test_unsorted_orset_tables_long_keys(eng, case):
     finally:
         _lib.call("crdt_set_option", b"sort.or_table", 1)
         _lib.call("crdt_set_option", b"sort.or_lookback", 1)
+
+
+@pytest.mark.parametrize("outlier", [False, True])
+def test_unsorted_sampled_plans(eng, outlier):
+    """The dense-key D2 paths from a sampled plan (sort.sample_plan; forced on
+    these small calls by sort.sample_min = 0): 200k / 180k tuples, keys in
+    2^20, ts in 2^24, cross-side equal tags.  With an outlier key and ts at
+    indices the 32768-tuple-per-side sample skips, the composing upsweep
+    flags the miss and the call is redone from the exact plan (the wide ts
+    then keeps LWW off its tables).  == the oracle, sampling on and off."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng(77 + outlier)
+
+    def side(m):
+        return (rng.integers(0, 2**20, m, dtype=np.uint64), rng.integers(0, 2**24, m, dtype=np.uint64),
+                rng.integers(0, 50, m, dtype=np.uint64).astype(np.uint32), rng.integers(0, 2, m, dtype=np.uint8))
+
+    a, b = side(200_000), side(180_000)
+    for f in range(3):
+        b[f][:3000] = a[f][:3000]
+    if outlier:
+        a[0][1] = 2**22            # (sampled: every ~6.1th tuple of a, ~5.5th of b, from index 0)
+        b[1][3] = 2**40
+    try:
+        _lib.call("crdt_set_option", b"sort.sample_min", 0)
+        for on in (1, 0):
+            _lib.call("crdt_set_option", b"sort.sample_plan", on)
+            _check(eng, a, b)
+    finally:
+        _lib.call("crdt_set_option", b"sort.sample_plan", 1)
+        _lib.call("crdt_set_option", b"sort.sample_min", 1 << 20)
