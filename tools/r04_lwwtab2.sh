@@ -26,7 +26,7 @@ PY
 for rep in 1 2; do
   for m in 1 2 4; do run lww_mm${m}_$rep lww_merge_d2 --option sort.mm_blocks_per_cu=$m; done
 done
-run or_2 orset_merge_d2
+
 run or_3 orset_merge_d2 --option sort.or_key_only=3
 run or_2b orset_merge_d2
 run or_3b orset_merge_d2 --option sort.or_key_only=3
