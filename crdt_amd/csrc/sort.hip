@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict
 // polled chunk has been dispatched; polls are bounded (CRDT_DEV_LOOKBACK).
 constexpr unsigned long long kOcA = 1ull << 62, kOcP = 2ull << 62, kOcVal = (1ull << 62) - 1;
 template <bool LB>
-__global__ __launch_bounds__(OCB) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
+__global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
                                                   const SortPlan *__restrict__ plan_,
                                                   const uint64_t *__restrict__ bounds, uint32_t *__restrict__ cnt,
                                                   uint32_t *__restrict__ fbw, int diag,
