@@ -495,7 +495,7 @@ struct PendGet {                   // bytes of pending reference j (key or value
 // table (an id from an earlier call) gets its ids written at once; the
 // others record their entry (bit 31: this pair claimed it) for passes B / C
 // and count the claims (ctr[0] keys, ctr[1] values).  kEmptyE slots: done.
-__global__ __launch_bounds__(256) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
                                                    const uint8_t *__restrict__ first, const uint32_t *__restrict__ flag0,
                                                    uint32_t *__restrict__ cflag,
                                                    uint32_t key_cap,
