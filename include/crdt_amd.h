@@ -177,10 +177,13 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
  * the key offsets are dense enough the sort stops early: LWW after one pass
  * on the key's top byte (each key's winner kept in an LDS table per
  * bucket), OR-Set after two passes on its top 16 bits (each 2^9-key chunk
- * sorted in LDS).  Output identical to crdt_tuples_sort of each side then
+ * sorted in LDS); on large calls those two are planned from a sample of
+ * the inputs that the first pass checks (a miss redoes the call from the
+ * exact ranges).  Output identical to crdt_tuples_sort of each side then
  * crdt_lww_merge / crdt_orset_merge.  Synchronises the stream once to size
- * the passes (the OR-Set chunk form a second time, to confirm no chunk
- * outgrew its LDS).  na + nb < 2^32; out capacity >= na + nb. */
+ * the passes, and the dense-key forms once more at the end (the sample's
+ * check; the OR-Set chunks' LDS limits).  na + nb < 2^32; out capacity >=
+ * na + nb. */
 int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                             size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
