@@ -78,6 +78,21 @@ def test_set_option_validation():
     assert lib.crdt_set_option(b"join.unroll", 1) == 0
 
 
+def test_d2_path_options():
+    """The unsorted-merge forms' switches: on / off accepted,
+    anything else refused; each left at its default."""
+    lib = _lib.lib()
+    for name, default in ((b"sort.lww_table", 1), (b"sort.or_table", 1), (b"sort.or_lookback", 1),
+                          (b"sort.sample_plan", 1)):
+        assert lib.crdt_set_option(name, 2) == -1
+        assert lib.crdt_set_option(name, -1) == -1
+        assert lib.crdt_set_option(name, 1 - default) == 0
+        assert lib.crdt_set_option(name, default) == 0
+    assert lib.crdt_set_option(b"sort.sample_min", -1) == -1
+    assert lib.crdt_set_option(b"sort.sample_min", 2**31) == -1
+    assert lib.crdt_set_option(b"sort.sample_min", 1 << 20) == 0
+
+
 def test_null_context_is_invalid_not_a_crash():
     lib = _lib.lib()
     assert lib.crdt_gcounter_join(None, None, None, None, 1, 1) == -1
