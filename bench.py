@@ -408,14 +408,22 @@ def _key_range_pieces(a, b, parts):
 
 
 class SetMergeUnsorted(SetMerge):
-    """configs[3] D2: both sides arrive UNSORTED; a step is ONE device sort
-    of both sides together (crdt_*_merge_unsorted: LSD radix over a packed
-    (key, ts, rep, side, tomb) composite, whose order is the stable merge of
-    the sorted sides) followed by a neighbour dedup of the sorted composites.
-    Algorithmic bytes are those of the merge itself (inputs read once, output
-    written once); the sort's passes are the price of unsorted input, so frac
-    reads against that."""
-    kernel = "k_sort_* (both sides at once) + k_dd_count + k_dd_apply"
+    """configs[3] D2: both sides arrive UNSORTED; a step is ONE call of
+    crdt_*_merge_unsorted over both sides together (a packed (key, ts, rep,
+    side, tomb) composite, whose order is the stable merge of the sorted
+    sides).  On config D's dense keys the sort stops early: LWW after one
+    radix pass on the key's top byte, each key's winner kept in an LDS table
+    per bucket (k_lww_table); OR-Set after two passes on the top 16 key bits,
+    each 2^9-key chunk sorted and deduplicated in LDS (k_or_chunk); both
+    planned from a sample of the inputs.  Algorithmic bytes
+    are those of the merge itself (inputs read once, output written once);
+    the sort's passes are the price of unsorted input, so frac reads against
+    that."""
+
+    @property
+    def kernel(self):
+        return ("k_sample_minmax + k_sort_up_vec + k_sort_pass + k_lww_table" if self.lww else
+                "k_sample_minmax + k_sort_up_vec + k_sort_up + 2 k_sort_pass + k_chunk_bounds + k_or_chunk")
 
     def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
         self.eng, self.n, self.lww = eng, n, lww
