@@ -1193,8 +1193,8 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 
 // ---------------------------------------------------------------- OR-Set D2: key chunks sorted in LDS
 // sort.or_table (default 1).  The radix sort runs only TWO passes, on the
-// key's top 16 bits; the key space is then cut into chunks of 2^10 keys
-// (config D: 8192 chunks of ~2.4k tuples), each contiguous in the sorted
+// key's top 16 bits; the key space is then cut into chunks of 2^9 keys
+// (config D: 16384 chunks of ~1.2k tuples), each contiguous in the sorted
 // composites because a chunk is a run of top-16 buckets.  Per chunk, one
 // 512-thread workgroup holds the chunk in LDS and finishes the sort there:
 //   k_chunk_bounds: the chunk starts, one 64-ary search per chunk;
@@ -1205,12 +1205,14 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 //     sort of its own slots in LDS, a longer key by the whole workgroup
 //     (first-copy marks in LDS, ranks by counting) -- and places them in tag
 //     order, tomb = the OR of the tag's copies, as composites (side bit
-//     cleared) in LDS, then copies them out at once to the chunk's own input
-//     range of `tmp`, plus the chunk's count;
-//   k_sort_colscan over the chunk counts;
+//     cleared) in LDS; then (sort.or_lookback, default) finds the chunk's
+//     output offset by a decoupled look-back and stores the SoA output
+//     itself, or copies the composites to the chunk's own input range of
+//     `tmp` with the chunk's count, for
+//   k_sort_colscan over the chunk counts and
 //   k_or_emit: each chunk's tags decoded into the SoA output at its offset.
 // A chunk of more than kOcCap tuples (skewed keys) or of more than kOcLong
-// keys with over kOtRun tuples raises the fallback word and stores nothing;
+// keys with over kOtMid tuples raises the fallback word and stores nothing;
 // the host then runs the radix path (inputs untouched).
 // (Round 4, first form: one radix pass on the key's top byte and a counting
 // sort of each 78k-tuple bucket through global memory -- its scattered 8-B
