@@ -162,33 +162,29 @@ static unsigned launch_minmax(crdt_ctx *ctx, const crdt_tuples &in, size_t n, co
     return ga + gb;
 }
 
-// A SAMPLE of both inputs' field ranges (sort.sample_plan): 32768 evenly
-// spaced tuples per side, 2 per thread, partials in the minmax format.  The
-// plan widens the sampled ranges (k_sort_plan's margin) and the composing
-// upsweep checks every tuple against them (the violation word): the dense-key
-// D2 paths then skip the full minmax read (400 MB at config D) and redo the
-// call from an exact plan only when a tuple fell outside.
-constexpr unsigned SAMPLE_WG = 64;       // workgroups per side
+// A SAMPLE of both inputs' field ranges (sort.sample_plan): per side 256
+// runs of 64 consecutive tuples (one wave each: coalesced 512-B loads),
+// evenly spread from the first tuple to the last, partials in the minmax
+// format.  The plan widens the sampled ranges (k_sort_plan's margin) and
+// the composing upsweep checks every tuple against them (the violation
+// word): the dense-key D2 paths then skip the full minmax read (400 MB at
+// config D) and redo the call from an exact plan only when a tuple fell
+// outside.  (32768 single tuples per side, strided: 12 us.)
+constexpr unsigned SAMPLE_WG = 64;       // workgroups per side (4 runs each)
 __global__ __launch_bounds__(256) void k_sample_minmax(crdt_tuples in, size_t n, crdt_tuples in2, size_t n2,
                                                        SortMinMax *mm) {
     const bool second = blockIdx.x >= SAMPLE_WG;
     const crdt_tuples t = second ? in2 : in;
     const size_t m = second ? n2 : n;
-    constexpr size_t NS = (size_t)SAMPLE_WG * 256 * 2;
+    constexpr size_t NR = (size_t)SAMPLE_WG * 4;      // runs per side
     unsigned long long kmin = ~0ULL, kmax = 0, tmin = ~0ULL, tmax = 0, rmin = ~0ULL, rmax = 0;
-    const size_t s0 = ((size_t)(blockIdx.x % SAMPLE_WG) * 256 + threadIdx.x) * 2;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const size_t i = m > NS ? (s0 + u) * m / NS : s0 + u;
-        if (i < m) {
-            const unsigned long long k = t.key[i], ts = t.ts[i], r = t.rep[i];
-            kmin = k < kmin ? k : kmin;
-            kmax = k > kmax ? k : kmax;
-            tmin = ts < tmin ? ts : tmin;
-            tmax = ts > tmax ? ts : tmax;
-            rmin = r < rmin ? r : rmin;
-            rmax = r > rmax ? r : rmax;
-        }
+    const size_t run = (size_t)(blockIdx.x % SAMPLE_WG) * 4 + (threadIdx.x >> 6);
+    const size_t i = (m > NR * 64 ? run * (m - 64) / (NR - 1) : run * 64) + (threadIdx.x & 63);
+    if (i < m) {
+        const unsigned long long k = t.key[i], ts = t.ts[i], r = t.rep[i];
+        kmin = kmax = k;
+        tmin = tmax = ts;
+        rmin = rmax = r;
     }
     for (int w = 32; w >= 1; w >>= 1) {
         kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, w, 64));

@@ -246,7 +246,7 @@ def test_unsorted_sampled_plans(eng, outlier):
     """The dense-key D2 paths from a sampled plan (sort.sample_plan; forced on
     these small calls by sort.sample_min = 0): 200k / 180k tuples, keys in
     2^20, ts in 2^24, cross-side equal tags.  With an outlier key and ts at
-    indices the 32768-tuple-per-side sample skips, the composing upsweep
+    an index the sample (256 runs of 64 tuples per side) skips, the upsweep
     flags the miss and the call is redone from the exact plan (the wide ts
     then keeps LWW off its tables).  == the oracle, sampling on and off."""
     from crdt_amd import _lib
@@ -260,8 +260,8 @@ def test_unsorted_sampled_plans(eng, outlier):
     for f in range(3):
         b[f][:3000] = a[f][:3000]
     if outlier:
-        a[0][1] = 2**22            # (sampled: every ~6.1th tuple of a, ~5.5th of b, from index 0)
-        b[1][3] = 2**40
+        a[0][100] = 2**22          # (sampled: 256 runs of 64 tuples per side, ~784 / ~706 apart from index 0)
+        b[1][100] = 2**40
     try:
         _lib.call("crdt_set_option", b"sort.sample_min", 0)
         for on in (1, 0):
