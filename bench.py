@@ -1235,13 +1235,19 @@ def main():
                 cpu["affinity_cpus"] = aff
                 cpu["cpu_share"] = ("threads = min(affinity mask, OMP_NUM_THREADS = "
                                     f"{os.environ.get('OMP_NUM_THREADS', 'unset')}): the GPU's host CPU share")
+        from crdt_amd import _lib
+        rccl = _lib.rccl_info()                       # the RCCL this process resolved
+        config = dict(wl.config)
+        if "parallelism" in config:
+            config["parallelism"] = f"{config['parallelism']} [RCCL {rccl['version']}]"
+        config["rccl"] = rccl
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": wl.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": getattr(wl, "scaling", "weak"),
             "vs_baseline": None, "dtype": wl.dtype,
             "data": "synthetic (SplitMix64-seeded, generated in HBM)",
-            "config": wl.config, "roofline": roof, "cpu_baseline": cpu, "e2e_pcie": e2e,
+            "config": config, "roofline": roof, "cpu_baseline": cpu, "e2e_pcie": e2e,
             "gpu_time_s": round(gpu_s, 6),
         }
         if hasattr(wl, "extra"):

@@ -240,6 +240,7 @@ SIGNATURES = {
     "crdt_shard_comm_init_rank": (_I, [_CTX, _P, _I, _I, C.POINTER(_P)]),
     "crdt_shard_comm_create_loopback": (_I, [_I, _I, C.POINTER(_P)]),
     "crdt_shard_comm_transport": (_I, [_P, C.POINTER(_I)]),
+    "crdt_rccl_info": (_I, [C.POINTER(_I), C.c_char_p, C.c_size_t]),
     "crdt_shard_comm_destroy": (_I, [_P]),
     "crdt_shard_comm_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     "crdt_shard_member_ctx": (_I, [_P, _I, C.POINTER(_P)]),
@@ -319,3 +320,12 @@ def call(fn: str, *args, ctx=None) -> int:
     if isinstance(st, int) and st < 0:
         check(fn, st, ctx)
     return st
+
+
+def rccl_info() -> dict:
+    """The RCCL this process resolved (crdt_rccl_info): version and library path."""
+    v = C.c_int(0)
+    buf = C.create_string_buffer(512)
+    call("crdt_rccl_info", C.byref(v), buf, 512)
+    x = v.value
+    return {"version": f"{x // 10000}.{x // 100 % 100}.{x % 100}", "code": x, "path": buf.value.decode()}

@@ -299,6 +299,7 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
     const uint32_t P = pop->P;
     if (P == 0) return CRDT_OK;                          // (a rank that holds no replica merges nothing)
     pop_arena(pop);
+    pop->can_undo = false;                               // the spare buffers (the undo snapshot) are rewritten below
     auto &nd = pop->d[1 - pop->cur];
     int rc = diff_reserve(pop, nd, pop->n_e + h.n_r, pop->n_kv + h.n_rkv, false);
     if (rc) return rc;
@@ -346,14 +347,22 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
 // After the stream has drained: the next Diffs / CurrentState are swapped in
 // and the host counts refreshed from the read-back -- unless a pass of this
 // round raised a device flag, which leaves the population as it was.
-int pop_commit(crdt_population *pop) {
+// (split in two so that a sharded round can check every member before it
+// swaps any in: all or nothing across the communicator's members)
+int pop_commit_check(crdt_population *pop) {
     hipError_t e = hipStreamSynchronize(pop->ctx->stream);
     if (e != hipSuccess) return hip_fail(pop->ctx, e);
     const uint32_t P = pop->P;
     if (P == 0) return CRDT_OK;
     const uint64_t *hb = carve_round(pop->pin, P).bounds;
     const uint32_t after = (uint32_t)hb[2 * P + 2], before = (uint32_t)hb[2 * P + 3];
-    if (after & ~before) return CRDT_E_DEVICE;
+    return (after & ~before) ? CRDT_E_DEVICE : CRDT_OK;
+}
+
+void pop_commit_apply(crdt_population *pop) {
+    const uint32_t P = pop->P;
+    if (P == 0) return;
+    const uint64_t *hb = carve_round(pop->pin, P).bounds;
     pop->pcnt.swap(pop->cnt);
     pop->pkvcnt.swap(pop->kvcnt);
     pop->cnt.resize(P);
@@ -369,7 +378,12 @@ int pop_commit(crdt_population *pop) {
     pop->n_e = hb[P];
     pop->n_kv = hb[2 * P + 1];
     pop->cur = 1 - pop->cur;
-    return CRDT_OK;
+}
+
+int pop_commit(crdt_population *pop) {
+    const int rc = pop_commit_check(pop);
+    if (rc == CRDT_OK) pop_commit_apply(pop);
+    return rc;
 }
 
 bool pop_valid(const crdt_population *p) { return p && p->ctx && p->d[p->cur].off; }
@@ -524,6 +538,7 @@ int pop_apply_chunk(crdt_population *pop, const crdt_population_cmds &c, const s
     if (e == hipSuccess)
         e = hipMemcpyAsync(d_bounds + 2 * P + 3, ctx->dev_status, 8, hipMemcpyDeviceToDevice, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
+    pop->can_undo = false;                               // (undo is a round's; the spare buffers are rewritten below)
     auto &nd = pop->d[1 - pop->cur];
     rc = diff_reserve(pop, nd, pop->n_e + n_c, pop->n_kv + n_kvc, false);
     if (rc) return rc;
@@ -608,6 +623,7 @@ extern "C" int crdt_population_add_commands(crdt_population *pop, const crdt_pop
                     return CRDT_E_INVAL;
     for (uint64_t j = 0; j < n_c && pop->one_pair; ++j)   // (cleared before any chunk lands)
         if (c->c_kv[j + 1] - c->c_kv[j] != 1) pop->one_pair = false;
+    std::fill(status, status + n_c, (uint16_t)0);        // 0 = not applied (a failing chunk leaves its own and later ones at 0)
     uint64_t most = 0;
     for (uint32_t p = 0; p < P; ++p) most = std::max(most, c->c_off[p + 1] - c->c_off[p]);
     for (uint64_t r = 0; r * kLaMax < most; ++r) {       // chunk r: the commands r*kLaMax .. of every replica
@@ -1035,9 +1051,13 @@ extern "C" int crdt_population_round_sharded(crdt_comm *c, crdt_population *cons
         if (!rc) rc = pop_merge(p, a, x.h, x.i_ts, x.i_kv, p->n_kv + x.K_in);
         if (rc) return rc;
     }
+    for (size_t i = 0; i < M; ++i) {                    // every member checked before any is swapped in
+        const int rc_i = pop_commit_check(pops[i]);
+        if (rc_i && !rc) rc = rc_i;
+    }
+    if (rc) return rc;
     for (size_t i = 0; i < M; ++i) {
-        rc = pop_commit(pops[i]);
-        if (rc) return rc;
+        pop_commit_apply(pops[i]);
         pops[i]->one_pair = false;                       // (entries from other ranks' Diffs: not checked)
     }
     return CRDT_OK;

@@ -37,6 +37,7 @@
 //     the same planning, offsets, tree merges and reductions at R > 1 on a
 //     one-GPU machine.
 // The compute (folds, merges, RefMerge) is the same code on either transport.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
@@ -380,6 +381,20 @@ extern "C" int crdt_shard_unique_id(void *id, size_t cap) {
     ncclResult_t r = ncclGetUniqueId(&u);
     if (r != ncclSuccess) return CRDT_E_COMM;
     memcpy(id, &u, sizeof u);
+    return CRDT_OK;
+}
+
+extern "C" int crdt_rccl_info(int *version, char *path, size_t cap) {
+    if (!version) return CRDT_E_INVAL;
+    int v = 0;
+    if (ncclGetVersion(&v) != ncclSuccess) return CRDT_E_DEVICE;
+    *version = v;
+    if (path && cap) {
+        Dl_info di{};
+        const char *f = dladdr((const void *)&ncclGetVersion, &di) && di.dli_fname ? di.dli_fname : "";
+        strncpy(path, f, cap - 1);
+        path[cap - 1] = 0;
+    }
     return CRDT_OK;
 }
 

@@ -2121,6 +2121,20 @@ static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPla
 
 static bool tuples_full(const crdt_tuples *t) { return t && t->key && t->ts && t->rep && t->tomb; }
 
+// any byte of out's four fields (cap tuples) inside any of in's (n tuples)?
+// The dense-key D2 forms store into out before they know whether the call
+// must be redone from the inputs, so out may not alias a or b.
+static bool tuples_overlap(const crdt_tuples &out, size_t cap, const crdt_tuples &in, size_t n) {
+    if (n == 0 || cap == 0) return false;
+    const uintptr_t ob[4] = {(uintptr_t)out.key, (uintptr_t)out.ts, (uintptr_t)out.rep, (uintptr_t)out.tomb};
+    const size_t ow[4] = {8, 8, 4, 1};
+    const uintptr_t ib[4] = {(uintptr_t)in.key, (uintptr_t)in.ts, (uintptr_t)in.rep, (uintptr_t)in.tomb};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            if (ob[i] < ib[j] + n * ow[j] && ib[j] < ob[i] + cap * ow[i]) return true;
+    return false;
+}
+
 template <int MODE>
 static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
                               crdt_tuples *out, uint64_t *out_count, bool allow_sample = true) {
@@ -2137,6 +2151,7 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     if (n >= (1ULL << 32)) return CRDT_E_RANGE;       // 32-bit in-tile / bucket arithmetic
     const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples A = na ? *a : none, B = nb ? *b : none;
+    if (tuples_overlap(*out, n, A, na) || tuples_overlap(*out, n, B, nb)) return CRDT_E_INVAL;
     const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
     const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);

@@ -183,7 +183,8 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
  * crdt_lww_merge / crdt_orset_merge.  Synchronises the stream once to size
  * the passes, and the dense-key forms once more at the end (the sample's
  * check; the OR-Set chunks' LDS limits).  na + nb < 2^32; out capacity >=
- * na + nb. */
+ * na + nb; out must not overlap a or b (CRDT_E_INVAL: the dense-key forms
+ * store before they know whether the call is redone from the inputs). */
 int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                             size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
@@ -467,6 +468,12 @@ int crdt_shard_comm_destroy(crdt_comm *comm);
 int crdt_shard_comm_info(const crdt_comm *comm, int *members, int *nranks, int *rank0);
 enum { CRDT_SHARD_RCCL = 0, CRDT_SHARD_LOOPBACK = 1 };
 int crdt_shard_comm_transport(const crdt_comm *comm, int *kind);
+/* The RCCL this process runs: *version = ncclGetVersion (e.g. 22606 for
+ * 2.26.6) and path (NUL-terminated, truncated to cap) = the shared object
+ * the dynamic linker resolved ncclGetVersion to.  The library is linked
+ * against /opt/rocm/lib/librccl, but in a process that already loaded
+ * another librccl of the same soname (PyTorch's) that one is used. */
+int crdt_rccl_info(int *version, char *path, size_t cap);
 int crdt_shard_member_ctx(crdt_comm *comm, int member, crdt_ctx **ctx);
 int crdt_shard_comm_last_error(const crdt_comm *comm);     /* last ncclResult_t */
 int crdt_shard_sync(crdt_comm *comm);
@@ -604,7 +611,10 @@ int crdt_population_round(crdt_population *pop, const int64_t *peers);
  * main.go:187), then the CurrentState apply with the early return after a
  * new key and the 500 on an unparsable value (main.go:188-207);
  * status[j] = 200 / 500.  Any number of commands per replica (chunks of
- * 4096 per device call).  Synchronises. */
+ * 4096 per device call: chunk r = commands r*4096 .. of every replica).  On
+ * an error the chunks before the failing one stay applied (their status
+ * 200 / 500) and every command of the failing and later chunks has status 0
+ * (not applied); a failed call leaves nothing to undo.  Synchronises. */
 typedef struct crdt_population_cmds {
     const uint64_t *c_off;      /* [replicas + 1] */
     const int64_t *c_ts;        /* [n_c] */

@@ -270,3 +270,31 @@ def test_unsorted_sampled_plans(eng, outlier):
     finally:
         _lib.call("crdt_set_option", b"sort.sample_plan", 1)
         _lib.call("crdt_set_option", b"sort.sample_min", 1 << 20)
+
+
+
+def test_unsorted_refuses_out_aliasing_an_input(eng):
+    """The dense-key D2 forms store into out before they know whether the
+    call is redone from the inputs, so out may not overlap a or b: refused
+    with CRDT_E_INVAL, the inputs untouched; a disjoint view of
+    the same allocation is fine."""
+    from crdt_amd import _lib
+    ua = synth.set_tuples(91, 0, 3000, 1000)
+    ub = synth.set_tuples(91, 1, 2000, 1000)
+    n = 5000
+    big = TupleSet.from_numpy(*(np.concatenate([x, y, x, y]) for x, y in zip(ua, ub)), eng.device)
+    A = TupleSet(big.key[:3000], big.ts[:3000], big.rep[:3000], big.tomb[:3000])
+    B = TupleSet(big.key[3000:n], big.ts[3000:n], big.rep[3000:n], big.tomb[3000:n])
+    sa, sb = _np_sorted(ua), _np_sorted(ub)
+    for name, ref in MODES:
+        fn = getattr(eng, f"{name}_merge_unsorted")
+        for lo in (0, 2000, 4999):                       # out over a, over both, over b's last tuple
+            out = TupleSet(big.key[lo:lo + n], big.ts[lo:lo + n], big.rep[lo:lo + n], big.tomb[lo:lo + n])
+            with pytest.raises(_lib.CrdtError):
+                fn(A, B, out=out)
+        np.testing.assert_array_equal(A.to_numpy()[0], ua[0])
+        np.testing.assert_array_equal(B.to_numpy()[0], ub[0])
+        out = TupleSet(big.key[n:], big.ts[n:], big.rep[n:], big.tomb[n:])   # disjoint: the second copy
+        got = fn(A, B, out=out).to_numpy()
+        for g, e in zip(got, ref(sa, sb)):
+            np.testing.assert_array_equal(g, e)

@@ -156,6 +156,35 @@ def test_population_undo_restores_the_previous_round(eng):
         pop.close()
 
 
+def test_population_failed_round_leaves_nothing_to_undo(eng):
+    """A round that fails after the previous round succeeded (fault injection
+    "fail.refmerge": its merge call returns an error) leaves the population
+    as it was, and undo is refused: the spare buffers no longer hold a
+    consistent snapshot (population.hip)."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng(19)
+    P = 5
+    diffs = [_rand_diff(rng, 4_000 + 7 * i, int(rng.integers(1, 25))) for i in range(P)]
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    try:
+        pop.round(gossip.random_peers(rng, P, 0, P))
+        after = pop.read()
+        _lib.call("crdt_set_option", b"fail.refmerge", 1)
+        try:
+            with pytest.raises(_lib.CrdtError):
+                pop.round(gossip.random_peers(rng, P, 0, P))
+        finally:
+            _lib.call("crdt_set_option", b"fail.refmerge", 0)
+        with pytest.raises(_lib.CrdtError):
+            pop.undo()
+        now = pop.read()
+        for k in after:
+            np.testing.assert_array_equal(now[k], after[k], err_msg=k)
+        eng.check_device()
+    finally:
+        pop.close()
+
+
 @pytest.mark.parametrize("seed", [3, 4])
 def test_population_commands_and_rounds(eng, seed):
     """AddCommand on every replica through crdt_population_add_commands

@@ -25,7 +25,13 @@
 #include <cstdlib>
 #include <vector>
 
-constexpr int TB = 256, IPT = 16, TILE = TB * IPT;
+#ifndef TBV
+#define TBV 256
+#endif
+#ifndef IPTV
+#define IPTV 16
+#endif
+constexpr int TB = TBV, IPT = IPTV, TILE = TB * IPT;   // -DTBV=1024 for 16k-item tiles
 constexpr unsigned long long FLAG_A = 1ull << 62, FLAG_P = 2ull << 62, VAL = (1ull << 62) - 1;
 
 #define CK(x)                                                                       \
@@ -66,7 +72,9 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *tot) {
     return off + x - v;
 }
 
-// mode 0: look-back; mode 1: no look-back (timing only)
+// mode 0: serial look-back by one thread; mode 1: no look-back (timing only);
+// mode 2: 64-lane window look-back (one status per lane, a ballot for the
+// first inclusive flag, a wave reduction; first poll without s_sleep)
 template <int MODE>
 __global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
                                                 unsigned long long *st, uint32_t chunk, unsigned *err) {
@@ -84,7 +92,43 @@ __global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in,
     for (int k = 0; k < IPT; ++k) s += v[k];
     uint64_t tot;
     const uint64_t ex = block_scan(s, &tot);
-    if (threadIdx.x == 0) {
+    if (MODE == 2) {                                        // 64-lane window look-back by wave 0
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            uint64_t pre = 0;
+            if (t == 0) {
+                if (lane == 0) __hip_atomic_store(&st[0], FLAG_P | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (lane == 0) __hip_atomic_store(&st[t], FLAG_A | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int64_t j = (int64_t)t - 1;                 // window [j - 63, j], lane l reads j - l
+                uint32_t spins = 0;
+                for (;;) {
+                    const int64_t q = j - lane;
+                    const unsigned long long w =
+                        q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FLAG_P;
+                    const uint64_t isp = __ballot((w & ~VAL) == FLAG_P), nr = __ballot((w & ~VAL) == 0);
+                    const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
+                    const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
+                    if (nr & need) {
+                        if (++spins > (1u << 20)) {
+                            if (lane == 0) atomicAdd(err, 1u);
+                            break;
+                        }
+                        if (spins > 1) __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    uint64_t v = lane <= pl ? (w & VAL) : 0;
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                    pre += v;
+                    if (pl < 64) break;
+                    j -= 64;
+                }
+                if (lane == 0) __hip_atomic_store(&st[t], FLAG_P | (pre + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) s_base = pre;
+        }
+    } else if (threadIdx.x == 0) {
         uint64_t pre = 0;
         if (MODE == 0) {
             if (t == 0) {
@@ -250,7 +294,14 @@ int main(int argc, char **argv) {
             hipMemsetAsync(d_st, 0, ntiles * 8);
             k_onepass<0><<<ntiles, TB>>>(d_in, d_out, d_st, c, d_err);
         }, true);
+        if (c == 0) snprintf(name, sizeof name, "window look-back, blockIdx");
+        else snprintf(name, sizeof name, "window look-back, XCD chunks %u", c);
+        timeit(name, [&] {
+            hipMemsetAsync(d_st, 0, ntiles * 8);
+            k_onepass<2><<<ntiles, TB>>>(d_in, d_out, d_st, c, d_err);
+        }, true);
     }
+    timeit("memset of the status words", [&] { hipMemsetAsync(d_st, 0, ntiles * 8); }, false);
     CK(hipFree(d_in));
     CK(hipFree(d_out));
     CK(hipFree(d_sums));
