@@ -613,6 +613,125 @@ class ShardSetMerge(SetMerge):
                                      "whole merged state; roofline.bytes_per_launch counts this rank's merge only"}}
 
 
+class LoopbackSetMerge(Workload):
+    """configs[3] as a distributed population over R LOOPBACK ranks on this
+    one GPU (crdt_shard_comm_create_loopback): rank r holds its own sorted
+    share of the 10M + 10M tuples; a step = crdt_shard_{lww,orset}_merge_local
+    with the final all-gather -- weighted splitters from pooled samples (one
+    all-gather), the count matrix (one all-gather), every tuple sent to its
+    key-range owner (ONE point-to-point group), the owner's rank-order merge
+    tree and set merge, the all-gather-v of the merged state to every rank.
+    The R ranks share one GPU's HBM, so the line prices the protocol itself
+    (planning, host round trips, the exchange's device copies, R-fold output)
+    before the first multi-GPU run, not xGMI.  Algorithmic bytes are the
+    merge's (inputs once, output once)."""
+    unit = "input-tuples/s"
+    scaling = "weak"
+
+    def __init__(self, eng, rank, world, n, key_space, ranks, lww=True, seed=2024):
+        from crdt_amd import shard
+        if world != 1:
+            raise SystemExit("loopback_* workloads run R ranks on ONE GPU: use --gpus 1")
+        self.eng, self.n, self.lww, self.R = eng, n, lww, ranks
+        self.name = "loopback_set_merge" if lww else "loopback_orset_merge"
+        self.kernel = f"whole op: crdt_shard_{'lww' if lww else 'orset'}_merge_local over {ranks} loopback ranks"
+        self.comm = shard.Comm.loopback(torch.device(eng.device).index or 0, ranks)
+        self.A, self.B = [], []
+        for r in range(ranks):
+            b, e = shard.shard_range(n, ranks, r)
+            self.A.append(eng.synth_set_tuples(seed * 100 + r, 0, e - b, key_space))
+            self.B.append(eng.synth_set_tuples(seed * 100 + r, 1, e - b, key_space))
+        self.cap = 2 * n
+        self.outs = [E.TupleSet.empty(self.cap, eng.device) for _ in range(ranks)]
+        self.step()
+        torch.cuda.synchronize()
+        self.n_out = len(self.last[0])
+        self.config = {"workload": f"{'LWW-Element-Set' if lww else 'OR-Set'} merge of a distributed population, "
+                                   f"{n} tuples per side split over {ranks} loopback ranks on one GPU, key space "
+                                   f"{key_space}: splitters + count matrix + one p2p group + owner merge + "
+                                   "all-gather-v (BASELINE configs[3] sharded; the protocol's cost before xGMI)",
+                       "tuples_per_side": n, "key_space": key_space, "loopback_ranks": ranks, "n_out": self.n_out,
+                       "parallelism": f"key-range shard x{ranks} loopback ranks on 1 GPU"}
+
+    def units(self):
+        return 2 * self.n
+
+    def bytes_per_launch(self):
+        return 21 * 2 * self.n + 21 * self.n_out
+
+    def step(self):
+        self.last = self.comm.set_merge_local(self.A, self.B, lww=self.lww, gather=True, cap=self.cap,
+                                              outs=self.outs)
+
+    def extra(self, avg_ms):
+        return {"exchange": {"transport": "loopback", "ranks": self.R, "n_out_total": self.n_out,
+                             "note": "R ranks on one GPU: every rank receives the whole merged state (R-fold "
+                                     "output writes); roofline.bytes_per_launch counts the merge once"}}
+
+
+class LoopbackGossipRound(Workload):
+    """crdt_population_round_sharded at the gossip_round bench's population
+    (1000 replicas x 10k entries) over R LOOPBACK ranks on this one GPU: the
+    per-replica counts all-gathered, the round's global draw planned on every
+    rank, each rank's pulled Diffs packed and delivered by ONE point-to-point
+    group, the merge over the received Diffs in place; each step the same
+    draw, undone after (as gossip_round).  Prices the sharded protocol before
+    the first multi-GPU run."""
+    unit = "remote-entries/s"
+    dtype = "int64"
+    name = "loopback_gossip_round"
+    scaling = "weak"
+
+    def __init__(self, eng, rank, world, replicas, entries, ranks, seed=2024):
+        from crdt_amd import gossip, shard, synth
+        if world != 1:
+            raise SystemExit("loopback_* workloads run R ranks on ONE GPU: use --gpus 1")
+        self.kernel = f"gossip round through crdt_population_round_sharded over {ranks} loopback ranks"
+        h = synth.refmerge_packed(seed, replicas, entries)
+        n_l = len(h["l_ts"])
+        kvk, kvv = h["kv_key"].view(np.uint32)[:n_l], h["kv_val"].view(np.uint32)[:n_l]
+        self.comm = shard.Comm.loopback(torch.device(eng.device).index or 0, ranks)
+        self.pops, self.R, self.P, self.n_l = [], ranks, replicas, n_l
+        for i in range(ranks):
+            b, e = shard.shard_range(replicas, ranks, i)
+            lb, le = int(h["l_off"][b]), int(h["l_off"][e])
+            kb, ke = int(h["l_kv"][lb]), int(h["l_kv"][le])
+            host = {"replicas": e - b, "l_off": h["l_off"][b:e + 1] - lb, "l_ts": h["l_ts"][lb:le],
+                    "l_origin": h["l_origin"][lb:le], "l_kv": h["l_kv"][lb:le + 1] - kb,
+                    "kv_key": (kvk[kb:ke].astype(np.int64) - b * 62).astype(np.uint32), "kv_val": kvv[kb:ke],
+                    "str_bytes": h["str_bytes"], "str_off": h["str_off"]}
+            self.pops.append(gossip.NativePopulation.on_member(self.comm, i, host, 62, b))
+        self.gossip = gossip
+        self.peers = gossip.random_peers(np.random.default_rng(seed), replicas, 0, replicas)
+        gossip.NativePopulation.round_sharded(self.comm, self.pops, self.peers)
+        self.n_out = sum(p.sizes()[1] for p in self.pops)
+        for p in self.pops:
+            p.undo()
+        self.config = {"workload": f"sharded gossip round: {replicas} replicas x {entries} Diff entries over "
+                                   f"{ranks} loopback ranks on one GPU, each replica pulls a random peer's Diff "
+                                   "(count all-gather + one p2p group of the pulled Diffs + in-place merge)",
+                       "replicas": replicas, "entries": entries, "loopback_ranks": ranks,
+                       "parallelism": f"replica shard x{ranks} loopback ranks on 1 GPU"}
+
+    def units(self):
+        return self.n_l
+
+    def bytes_per_launch(self):
+        # as gossip_round: the merge's compulsory bytes + the new Diffs' kv pairs
+        n_r, n_out = self.n_l, self.n_out
+        return self.n_l * 17 + n_r * 16 + n_r * 8 + n_out * 17 + n_out * 24
+
+    def step(self):
+        self.gossip.NativePopulation.round_sharded(self.comm, self.pops, self.peers)
+        for p in self.pops:
+            p.undo()
+
+    def extra(self, avg_ms):
+        return {"exchange": {"transport": "loopback", "ranks": self.R,
+                             "note": "the pulled Diffs of other ranks' replicas move as device copies on the one "
+                                     "GPU; roofline.bytes_per_launch counts the merge once, not the exchange"}}
+
+
 class ShardJoin(Workload):
     """configs[4] E2: every rank holds a DIVERGENT full copy of the
     [rows, nodes] counter state; the join is one in-place
@@ -1113,6 +1232,11 @@ def make_workload(name, eng, rank, world, args):
         return ShardFold(eng, rank, world, args.total_rows, args.nodes)
     if name == "shard_join":
         return ShardJoin(eng, rank, world, args.rows, args.nodes)
+    if name in ("loopback_set_merge", "loopback_orset_merge"):
+        return LoopbackSetMerge(eng, rank, world, args.set_n, args.key_space, args.loopback,
+                                lww=(name == "loopback_set_merge"))
+    if name == "loopback_gossip_round":
+        return LoopbackGossipRound(eng, rank, world, args.replicas, args.entries, args.loopback)
     if name in ("shard_set_merge", "shard_orset_merge"):
         return ShardSetMerge(eng, rank, world, args.set_n, args.key_space, lww=(name == "shard_set_merge"))
     raise SystemExit(f"unknown workload {name}")
@@ -1140,7 +1264,9 @@ def main():
                     choices=["gcounter_join", "pncounter_join", "vclock_classify", "lww_merge", "orset_merge",
                              "lww_merge_d2", "orset_merge_d2", "shard_fold", "shard_join", "refmerge",
                              "refmerge_delta", "gossip_round", "gossip_round_wire", "server_merge",
-                             "shard_set_merge", "shard_orset_merge"])
+                             "shard_set_merge", "shard_orset_merge", "loopback_set_merge", "loopback_orset_merge",
+                             "loopback_gossip_round"])
+    ap.add_argument("--loopback", type=int, default=8, help="ranks of the loopback_* workloads (one GPU)")
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--pairs", type=int, default=10_000_000)
@@ -1154,6 +1280,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive e2e_pcie measurement")
+    ap.add_argument("--no-peaks", action="store_true",
+                    help="skip the self-measured peak sweep (timeline traces: the trace then ends with the timed loop)")
     ap.add_argument("--option", action="append", default=[], help="name=value kernel knob (crdt_set_option)")
     args = ap.parse_args()
 
@@ -1185,9 +1313,14 @@ def main():
     torch.cuda.synchronize(dev)
 
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    mark = None
+    if os.environ.get("CRDT_TRACE_MARK"):           # tools/timeline.py: a tiny crdt_stream_copy before each step
+        mark = (torch.zeros(64, dtype=torch.int64, device=dev), torch.zeros(64, dtype=torch.int64, device=dev))
     t0 = time.perf_counter()
     evs[0].record(stream)
     for k in range(args.steps):
+        if mark is not None:
+            eng.stream_copy(mark[0], mark[1], 1, 1)
         wl.step()
         evs[k + 1].record(stream)
     torch.cuda.synchronize(dev)
@@ -1213,7 +1346,8 @@ def main():
         med_ms = float(np.median(step_ms))
         achieved = wl.bytes_per_launch() / (avg_ms / 1e3) / 1e9
         traffic = load_traffic(wl)
-        peaks = measure_peaks(eng)
+        peaks = measure_peaks(eng) if not args.no_peaks else {"copy": float("nan"), "read": float("nan"),
+                                                               "skipped": "--no-peaks"}
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "measured_peak": peaks, "frac_of_copy_peak": round(achieved / peaks["copy"], 4),

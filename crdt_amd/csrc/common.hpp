@@ -100,6 +100,15 @@ void server_ctx_release(crdt_ctx *ctx);   // server.hip: the context's Server-me
 // sets.hip: out = the stable merge of A and B, all na + nb tuples (crdt_tuples_merge)
 int tuples_merge_stable(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
                         const crdt_tuples &O);
+// ... of many independent pairs, one split + one merge launch per 16 pairs
+struct MergePairArg {
+    crdt_tuples A;
+    size_t na;
+    crdt_tuples B;
+    size_t nb;
+    crdt_tuples O;
+};
+int tuples_merge_stable_batch(crdt_ctx *ctx, const std::vector<MergePairArg> &pairs);
 // gossip.hip: crdt_seg_gather2 (4-byte elements, base 0) over n_max segments
 // of which the first *n_dev are real (a count still on the device)
 int seg_gather2_dev_count(crdt_ctx *ctx, size_t n_max, const uint64_t *n_dev, const int64_t *code,

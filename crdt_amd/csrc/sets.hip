@@ -474,10 +474,11 @@ constexpr int OCB = 512;                 // count pass threads (4 items each; 25
 constexpr int OWT = 512;                 // write pass threads (4 items each)
 constexpr int ONW = OT / 64;             // bitmap words per tile and bitmap
 
-__global__ __launch_bounds__(256) void k_or_split(crdt_tuples A, crdt_tuples B, size_t na, size_t nb, size_t ntiles,
-                                                  uint64_t *__restrict__ split) {
+// The merge-path split of diagonal t * OT (one 16-lane group per diagonal,
+// four per wave; every lane of the wave calls it: the ballots are wave-wide).
+__device__ __forceinline__ void or_split_diag(const crdt_tuples &A, const crdt_tuples &B, size_t na, size_t nb,
+                                              size_t ntiles, size_t t, uint64_t *__restrict__ split) {
     const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
-    const size_t t = ((((size_t)blockIdx.x * 256 + threadIdx.x) >> 6) << 2) + (size_t)grp;
     const size_t n = na + nb;
     const size_t d = t * OT < n ? t * OT : n;
     size_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
@@ -504,6 +505,12 @@ __global__ __launch_bounds__(256) void k_or_split(crdt_tuples A, crdt_tuples B, 
         }
     }
     if (gl == 0 && t <= ntiles) split[t] = lo;
+}
+
+__global__ __launch_bounds__(256) void k_or_split(crdt_tuples A, crdt_tuples B, size_t na, size_t nb, size_t ntiles,
+                                                  uint64_t *__restrict__ split) {
+    const size_t t = ((((size_t)blockIdx.x * 256 + threadIdx.x) >> 6) << 2) + (size_t)((threadIdx.x & 63) >> 4);
+    or_split_diag(A, B, na, nb, ntiles, t, split);
 }
 
 __device__ __forceinline__ LwwTile or_tile(const uint64_t *__restrict__ split, uint64_t t, size_t n) {
@@ -971,55 +978,161 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
 // item's output position = its index in its run + its rank in the other run
 // (B elements strictly below an A tag, A elements at or below a B tag).
 template <int NT>
-__global__ __launch_bounds__(NT) void k_tmerge(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
-                                               const uint64_t *__restrict__ split, crdt_tuples out) {
+__device__ __forceinline__ void tmerge_tile(const crdt_tuples &A, const crdt_tuples &B, size_t na, size_t nb,
+                                            const uint64_t *__restrict__ split, const crdt_tuples &out, uint64_t t,
+                                            uint64_t *sk, uint64_t *st, uint32_t *sr, uint8_t *sm) {
+    // both runs staged in LDS (A at slots [0, na), B at [na, n)); thread k
+    // merges items [k NI, (k+1) NI) of the tile after a merge-path search
+    // of its diagonal (A first on an equal tag), the merged tuples are put
+    // back into LDS in merged order, then stored coalesced.  (Round 4's form
+    // -- every item binary-searched its rank in the other run, ~11 dependent
+    // 3-field LDS compares per item -- ran at ~1.6 TB/s.)
     constexpr int NI = OT / NT;
-    __shared__ uint64_t sk[OT], st[OT];
-    __shared__ uint32_t sr[OT];
-    const uint64_t t = blockIdx.x;
     const LwwTile b = or_tile(split, t, na + nb);
-    uint64_t k[NI], ts[NI];
-    uint32_t r[NI];
-    uint8_t m[NI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {                       // A run at slots [0, na), B run at [na, n)
-        const uint32_t x = threadIdx.x + (uint32_t)j * NT;
-        const bool v = x < b.n, on_a = x < b.na;
-        const size_t g = on_a ? b.i0 + x : b.j0 + (x - b.na);
-        const crdt_tuples &S = on_a ? A : B;
-        k[j] = v ? S.key[g] : 0;
-        ts[j] = v ? S.ts[g] : 0;
-        r[j] = v ? S.rep[g] : 0;
-        m[j] = v ? S.tomb[g] : 0;
-        if (v) {
-            sk[x] = k[j];
-            st[x] = ts[j];
-            sr[x] = r[j];
-        }
-    }
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
         const uint32_t x = threadIdx.x + (uint32_t)j * NT;
         if (x >= b.n) continue;
-        const Tag me{k[j], ts[j], r[j]};
         const bool on_a = x < b.na;
-        // rank in the other run: B below an A tag (strict), A at or below a B tag
-        uint32_t lo = 0, hi = on_a ? b.nb : b.na;
-        const uint32_t base = on_a ? b.na : 0;
-        while (lo < hi) {
+        const size_t g = on_a ? b.i0 + x : b.j0 + (x - b.na);
+        const crdt_tuples &S = on_a ? A : B;
+        sk[x] = S.key[g];
+        st[x] = S.ts[g];
+        sr[x] = S.rep[g];
+        sm[x] = S.tomb[g];
+    }
+    __syncthreads();
+    auto tg = [&](uint32_t x) { return Tag{sk[x], st[x], sr[x]}; };
+    const uint32_t k0 = threadIdx.x * NI < b.n ? threadIdx.x * NI : b.n;
+    const uint32_t k1 = k0 + NI < b.n ? k0 + NI : b.n;
+    uint64_t ok[NI], ot[NI];
+    uint32_t orr[NI];
+    uint8_t om[NI];
+    {
+        uint32_t lo = k0 > b.nb ? k0 - b.nb : 0, hi = k0 < b.na ? k0 : b.na;
+        while (lo < hi) {                                // P(i) = A[i] <= B[k0-1-i]: true below the split
             const uint32_t mid = (lo + hi) >> 1;
-            const Tag o{sk[base + mid], st[base + mid], sr[base + mid]};
-            const bool before = on_a ? !tag_le(me, o) : tag_le(o, me);
-            if (before) lo = mid + 1;
+            if (tag_le(tg(mid), tg(b.na + (k0 - 1 - mid)))) lo = mid + 1;
             else hi = mid;
         }
-        const size_t pos = (size_t)t * OT + (on_a ? x : x - b.na) + lo;
-        out.key[pos] = k[j];
-        out.ts[pos] = ts[j];
-        out.rep[pos] = r[j];
-        out.tomb[pos] = m[j];
+        uint32_t ia = lo, ib = k0 - lo;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            if ((uint32_t)j >= k1 - k0) break;
+            const bool take_a = ia < b.na && (ib >= b.nb || tag_le(tg(ia), tg(b.na + ib)));
+            const uint32_t x = take_a ? ia : b.na + ib;
+            ok[j] = sk[x];
+            ot[j] = st[x];
+            orr[j] = sr[x];
+            om[j] = sm[x];
+            ia += take_a ? 1u : 0u;
+            ib += take_a ? 0u : 1u;
+        }
     }
+    __syncthreads();                                     // every staged input read
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        if ((uint32_t)j >= k1 - k0) break;
+        const uint32_t x = k0 + (uint32_t)j;
+        sk[x] = ok[j];
+        st[x] = ot[j];
+        sr[x] = orr[j];
+        sm[x] = om[j];
+    }
+    __syncthreads();
+    const size_t o0 = (size_t)t * OT;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const uint32_t x = threadIdx.x + (uint32_t)j * NT;
+        if (x >= b.n) continue;
+        out.key[o0 + x] = sk[x];
+        out.ts[o0 + x] = st[x];
+        out.rep[o0 + x] = sr[x];
+        out.tomb[o0 + x] = sm[x];
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_tmerge(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
+                                               const uint64_t *__restrict__ split, crdt_tuples out) {
+    __shared__ uint64_t sk[OT], st[OT];
+    __shared__ uint32_t sr[OT];
+    __shared__ uint8_t sm[OT];
+    tmerge_tile<NT>(A, B, na, nb, split, out, blockIdx.x, sk, st, sr, sm);
+}
+
+// Up to kMergeBatch independent stable merges in ONE split launch and ONE
+// merge launch (a level of the key-range owner's rank-order merge tree, both
+// sides: crdt_shard_*_merge_local).  Pair p's tiles are tile0[p] ..
+// tile0[p+1]; its split entries (ntiles_p + 1 of them) start at tile0[p] + p.
+// (One crdt_tuples_merge per pair paid ~27 us of fixed split + merge latency
+// each: 112 of them per distributed set merge at R = 8.)
+constexpr int kMergeBatch = 16;
+struct MergeBatch {
+    crdt_tuples A[kMergeBatch], B[kMergeBatch], O[kMergeBatch];
+    uint64_t na[kMergeBatch], nb[kMergeBatch];
+    uint32_t tile0[kMergeBatch + 1];
+    uint32_t np;
+};
+
+__device__ __forceinline__ uint32_t batch_pair(const MergeBatch &mb, uint64_t x, uint32_t per_pair_extra) {
+    uint32_t p = 0;                                      // the last p with tile0[p] + p * extra <= x
+    for (uint32_t q = 1; q < mb.np; ++q)
+        if ((uint64_t)mb.tile0[q] + (uint64_t)q * per_pair_extra <= x) p = q;
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_or_split_batch(MergeBatch mb, uint64_t *__restrict__ split) {
+    const uint64_t e = ((((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6) << 2) + (uint64_t)((threadIdx.x & 63) >> 4);
+    const uint32_t p = batch_pair(mb, e, 1);
+    const uint64_t s0 = (uint64_t)mb.tile0[p] + p, nt = mb.tile0[p + 1] - mb.tile0[p];
+    // entries past the last pair's (nt + 1) compute nothing: t > ntiles
+    const uint64_t t = e - s0;
+    or_split_diag(mb.A[p], mb.B[p], mb.na[p], mb.nb[p], nt, t, split + s0);
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_tmerge_batch(MergeBatch mb, const uint64_t *__restrict__ split) {
+    __shared__ uint64_t sk[OT], st[OT];
+    __shared__ uint32_t sr[OT];
+    __shared__ uint8_t sm[OT];
+    const uint32_t p = batch_pair(mb, blockIdx.x, 0);
+    tmerge_tile<NT>(mb.A[p], mb.B[p], mb.na[p], mb.nb[p], split + mb.tile0[p] + p, mb.O[p],
+                    blockIdx.x - mb.tile0[p], sk, st, sr, sm);
+}
+
+// Every pair's stable merge (tuples_merge_stable of each), kMergeBatch pairs
+// per pair of launches.
+int tuples_merge_stable_batch(crdt_ctx *ctx, const std::vector<MergePairArg> &pairs) {
+    for (size_t p0 = 0; p0 < pairs.size(); p0 += kMergeBatch) {
+        MergeBatch mb{};
+        uint64_t tiles = 0;
+        const size_t np = std::min(pairs.size() - p0, (size_t)kMergeBatch);
+        for (size_t q = 0; q < np; ++q) {
+            const MergePairArg &x = pairs[p0 + q];
+            const crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
+            mb.A[q] = x.na ? x.A : empty;
+            mb.B[q] = x.nb ? x.B : empty;
+            mb.O[q] = x.O;
+            mb.na[q] = x.na;
+            mb.nb[q] = x.nb;
+            mb.tile0[q] = (uint32_t)tiles;
+            tiles += (x.na + x.nb + OT - 1) / OT;
+            if (tiles >= 0x7fffffffULL) return CRDT_E_RANGE;
+        }
+        mb.tile0[np] = (uint32_t)tiles;
+        mb.np = (uint32_t)np;
+        if (tiles == 0) continue;
+        const uint64_t entries = tiles + np;
+        int rc = ws_reserve(ctx, Carve::round(entries * 8) + 1024);
+        if (rc) return rc;
+        uint64_t *split = (uint64_t *)ctx->ws;
+        k_or_split_batch<<<(unsigned)((entries + 15) / 16), 256, 0, ctx->stream>>>(mb, split);
+        k_tmerge_batch<512><<<(unsigned)tiles, 512, 0, ctx->stream>>>(mb, split);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+    }
+    return CRDT_OK;
 }
 
 int tuples_merge_stable(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,

@@ -159,10 +159,69 @@ __global__ void k_loop_allreduce(PtrTab t, int M, size_t n) {
     }
 }
 
+// One launch for a whole group of device copies (the loopback form of an
+// all-gather or a point-to-point group): segment s = (dst, src, bytes) in a
+// device table, cut into 64-KB blocks; blk[s] = the first block of segment s
+// (blk[nseg] = all blocks).  A workgroup finds its segment by binary search
+// and copies its block with the widest access the block's alignment allows.
+// (One hipMemcpyAsync per transfer cost ~8 us each on the transport stream:
+// 512 of them per distributed set merge at R = 8.)
+struct CopySeg {
+    char *dst;
+    const char *src;
+    uint64_t bytes;
+};
+constexpr uint64_t kCopyBlk = 64u << 10;
+
+__global__ __launch_bounds__(256) void k_batch_copy(const CopySeg *__restrict__ seg, const uint64_t *__restrict__ blk,
+                                                    uint32_t nseg) {
+    const uint64_t b = blockIdx.x;
+    uint32_t lo = 0, hi = nseg;                          // the last s with blk[s] <= b
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (blk[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    const CopySeg sg = seg[lo];
+    const uint64_t o0 = (b - blk[lo]) * kCopyBlk;
+    const uint64_t n = sg.bytes - o0 < kCopyBlk ? sg.bytes - o0 : kCopyBlk;
+    char *d = sg.dst + o0;
+    const char *s = sg.src + o0;
+    const uintptr_t al = (uintptr_t)d | (uintptr_t)s;
+    if ((al & 15) == 0) {
+        const uint64_t nv = n >> 4;
+        for (uint64_t i = threadIdx.x; i < nv; i += 256) ((uint4 *)d)[i] = ((const uint4 *)s)[i];
+        for (uint64_t i = (nv << 4) + threadIdx.x; i < n; i += 256) d[i] = s[i];
+    } else if ((al & 7) == 0) {
+        const uint64_t nv = n >> 3;
+        for (uint64_t i = threadIdx.x; i < nv; i += 256) ((uint64_t *)d)[i] = ((const uint64_t *)s)[i];
+        for (uint64_t i = (nv << 3) + threadIdx.x; i < n; i += 256) d[i] = s[i];
+    } else if ((al & 3) == 0) {
+        const uint64_t nv = n >> 2;
+        for (uint64_t i = threadIdx.x; i < nv; i += 256) ((uint32_t *)d)[i] = ((const uint32_t *)s)[i];
+        for (uint64_t i = (nv << 2) + threadIdx.x; i < n; i += 256) d[i] = s[i];
+    } else {
+        for (uint64_t i = threadIdx.x; i < n; i += 256) d[i] = s[i];
+    }
+}
+
 struct LoopTransport final : Transport {
     crdt_ctx *ctx = nullptr;              // the transport's own stream (a context for its errors)
     hipEvent_t done = nullptr;
     std::vector<hipEvent_t> ev;           // one per member
+    // the copy tables: built in pinned host memory, uploaded on the transport
+    // stream, read by k_batch_copy from device memory.  A ring of kTabs slots,
+    // each with an event recorded after its upload, so the host only waits
+    // when it reuses a slot whose upload (queued behind the members' work)
+    // has not run yet -- kTabs collectives later.
+    static constexpr int kTabs = 4;
+    struct Tab {
+        void *h = nullptr, *d = nullptr;
+        size_t bytes = 0;
+        hipEvent_t up = nullptr;
+        bool pending = false;
+    } tab[kTabs];
+    int next_tab = 0;
 
     ~LoopTransport() override {
         if (ctx) {
@@ -172,6 +231,11 @@ struct LoopTransport final : Transport {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
+        for (Tab &t : tab) {
+            if (t.up) (void)hipEventDestroy(t.up);
+            if (t.h) (void)hipHostFree(t.h);
+            if (t.d) (void)hipFree(t.d);
+        }
         if (ctx) (void)crdt_ctx_destroy(ctx);
     }
     int init(int device, size_t members) {
@@ -188,6 +252,8 @@ struct LoopTransport final : Transport {
         if (rc) return rc;
         ev.assign(members, nullptr);
         hipError_t e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+        for (Tab &t : tab)
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&t.up, hipEventDisableTiming);
         for (size_t i = 0; i < members && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
         return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
     }
@@ -208,10 +274,52 @@ struct LoopTransport final : Transport {
         for (size_t i = 0; i < c->m.size() && e == hipSuccess; ++i) e = hipStreamWaitEvent(c->m[i].ctx->stream, done, 0);
         return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
     }
-    int copy(void *dst, const void *src, size_t bytes) {
-        if (!bytes || dst == src) return CRDT_OK;
-        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream);
-        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    // every (dst, src, bytes) of `segs` in one k_batch_copy launch on the
+    // transport stream (after fence_in, before fence_out)
+    int copy_all(std::vector<CopySeg> &segs) {
+        size_t k = 0;
+        for (const CopySeg &g : segs)
+            if (g.bytes && g.dst != g.src) segs[k++] = g;
+        segs.resize(k);
+        if (segs.empty()) return CRDT_OK;
+        const size_t ns = segs.size();
+        const size_t need = Carve::round(ns * sizeof(CopySeg)) + (ns + 1) * 8;
+        Tab &t = tab[next_tab];
+        next_tab = (next_tab + 1) % kTabs;
+        hipError_t e = hipSuccess;
+        if (t.pending) e = hipEventSynchronize(t.up);    // this slot's last upload has left its pinned copy
+        t.pending = false;
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        if (need > t.bytes) {
+            e = hipStreamSynchronize(ctx->stream);       // (the old device table may still be read)
+            if (t.h) (void)hipHostFree(t.h);
+            if (t.d) (void)hipFree(t.d);
+            t.h = t.d = nullptr;
+            t.bytes = 0;
+            const size_t want = need * 2 > (64u << 10) ? need * 2 : (64u << 10);
+            if (e == hipSuccess) e = hipHostMalloc(&t.h, want, 0);
+            if (e == hipSuccess) e = hipMalloc(&t.d, want);
+            if (e != hipSuccess) return hip_fail(ctx, e);
+            t.bytes = want;
+        }
+        CopySeg *hs = (CopySeg *)t.h;
+        uint64_t *hb = (uint64_t *)((char *)t.h + Carve::round(ns * sizeof(CopySeg)));
+        uint64_t nb = 0;
+        for (size_t i = 0; i < ns; ++i) {
+            hs[i] = segs[i];
+            hb[i] = nb;
+            nb += (segs[i].bytes + kCopyBlk - 1) / kCopyBlk;
+        }
+        hb[ns] = nb;
+        if (nb >= (1ull << 31)) return CRDT_E_RANGE;
+        e = hipMemcpyAsync(t.d, t.h, need, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipEventRecord(t.up, ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        t.pending = true;
+        k_batch_copy<<<(unsigned)nb, 256, 0, ctx->stream>>>(
+            (const CopySeg *)t.d, (const uint64_t *)((char *)t.d + Carve::round(ns * sizeof(CopySeg))),
+            (uint32_t)ns);
+        return check_launch(ctx);
     }
     int allreduce(crdt_comm *c, void *const *buf, size_t n, XType t, XOp op) override {
         const int M = (int)c->m.size();
@@ -248,9 +356,12 @@ struct LoopTransport final : Transport {
         return rc ? rc : fence_out(c);
     }
     int allgather(crdt_comm *c, const void *const *send, void *const *recv, size_t bytes) override {
+        std::vector<CopySeg> segs;
+        for (size_t j = 0; j < c->m.size(); ++j)
+            for (size_t q = 0; q < c->m.size(); ++q)
+                segs.push_back(CopySeg{(char *)recv[j] + q * bytes, (const char *)send[q], bytes});
         int rc = fence_in(c);
-        for (size_t j = 0; j < c->m.size() && !rc; ++j)
-            for (size_t q = 0; q < c->m.size() && !rc; ++q) rc = copy((char *)recv[j] + q * bytes, send[q], bytes);
+        if (!rc) rc = copy_all(segs);
         return rc ? rc : fence_out(c);
     }
     int p2p(crdt_comm *c, const std::vector<XP2P> &ops) override {
@@ -265,9 +376,12 @@ struct LoopTransport final : Transport {
             for (size_t j = 0; j < snd[k].size(); ++j)
                 if (snd[k][j]->bytes != rcv[k][j]->bytes) return nccl_fail(c, ncclInvalidUsage);
         }
+        std::vector<CopySeg> segs;
+        for (size_t k = 0; k < M * M; ++k)
+            for (size_t j = 0; j < snd[k].size(); ++j)
+                segs.push_back(CopySeg{(char *)rcv[k][j]->rbuf, (const char *)snd[k][j]->sbuf, snd[k][j]->bytes});
         int rc = fence_in(c);
-        for (size_t k = 0; k < M * M && !rc; ++k)
-            for (size_t j = 0; j < snd[k].size() && !rc; ++j) rc = copy(rcv[k][j]->rbuf, snd[k][j]->sbuf, snd[k][j]->bytes);
+        if (!rc) rc = copy_all(segs);
         return rc ? rc : fence_out(c);
     }
 };
@@ -1100,17 +1214,19 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
             return crdt_tuples{t.key + off, t.ts + off, t.rep + off, t.tomb + off};
         };
         int cur = 0;
-        while (ru[0].size() > 1) {
+        while (ru[0].size() > 1) {                       // one level of both sides: one batched launch pair
+            std::vector<MergePairArg> lvl;
             for (int side = 0; side < 2; ++side) {
                 std::vector<Run> nx;
                 for (size_t k = 0; k < ru[side].size(); k += 2) {
                     const Run x = ru[side][k], y = k + 1 < ru[side].size() ? ru[side][k + 1] : Run{x.off + x.n, 0};
-                    rc = tuples_merge_stable(mb.ctx, view(cur, x.off), x.n, view(cur, y.off), y.n, view(1 - cur, x.off));
-                    if (rc) return rc;
+                    lvl.push_back(MergePairArg{view(cur, x.off), x.n, view(cur, y.off), y.n, view(1 - cur, x.off)});
                     nx.push_back(Run{x.off, x.n + y.n});
                 }
                 ru[side].swap(nx);
             }
+            rc = tuples_merge_stable_batch(mb.ctx, lvl);
+            if (rc) return rc;
             cur = 1 - cur;
         }
         uint64_t *count = n_dev ? n_dev[i] : (uint64_t *)mb.scratch;   // (the head's word 0)

@@ -8,7 +8,10 @@ host over 1-GB D2H slices of the same device population:
   * an 8-way crdt_shard_range split (the 8-GPU sharding) folded per shard and
     max-combined -- the join the RCCL all-reduce(max) performs across GPUs;
   * the native communicator path crdt_shard_fold_max_u64 (1-rank RCCL
-    ncclAllReduce(ncclUint64, ncclMax)) over the whole population.
+    ncclAllReduce(ncclUint64, ncclMax)) over the whole population;
+  * the same protocol over 8 LOOPBACK ranks on the one GPU (each rank its
+    crdt_shard_range shard, the all-reduce(max) a reduction kernel over the
+    eight members' folds): every rank's result == the oracle.
 """
 from concurrent.futures import ThreadPoolExecutor
 
@@ -57,8 +60,13 @@ def test_configs4_population_generator(population):
     np.testing.assert_array_equal(as_u64(flat[-n:]), synth.counters(2024, 1, n, ROWS * NODES - n))
 
 
-def test_configs4_fold_and_8way_shards_match_oracle(eng, population):
-    exp = _host_fold(population)
+@pytest.fixture(scope="module")
+def expected_fold(population):
+    return _host_fold(population)
+
+
+def test_configs4_fold_and_8way_shards_match_oracle(eng, population, expected_fold):
+    exp = expected_fold
     whole = as_u64(eng.gcounter_fold(population))
     np.testing.assert_array_equal(whole, exp)
     parts = []
@@ -71,5 +79,23 @@ def test_configs4_fold_and_8way_shards_match_oracle(eng, population):
     try:
         got = c.fold_max([population])[0]
         np.testing.assert_array_equal(as_u64(got), exp)
+    finally:
+        c.close()
+
+
+def test_configs4_fold_max_over_8_loopback_ranks(population, expected_fold):
+    """configs[4] through crdt_shard_fold_max_u64 over R = 8 loopback ranks:
+    the 8-GPU sharding of the north_star's scaling config, each rank's
+    12.5M-row shard folded on its own stream, the 512-B folds all-reduced."""
+    c = shard.Comm.loopback(0, 8)
+    try:
+        shards = []
+        for r in range(8):
+            b, e = shard.shard_range(ROWS, 8, r)
+            shards.append(population[b:e])
+        outs = c.fold_max(shards)
+        c.sync()
+        for r, o in enumerate(outs):
+            np.testing.assert_array_equal(as_u64(o), expected_fold, err_msg=f"rank {r}")
     finally:
         c.close()
