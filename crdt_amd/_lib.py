@@ -53,6 +53,11 @@ class CrdtError(RuntimeError):
         super().__init__(msg)
 
 
+class crdt_set_plan(C.Structure):
+    """Opaque plan of a stream-ordered D2 merge (crdt_set_merge_plan)."""
+    _fields_ = [("w", C.c_uint64 * 24)]
+
+
 class crdt_tuples(C.Structure):
     _fields_ = [("key", C.c_void_p), ("ts", C.c_void_p), ("rep", C.c_void_p), ("tomb", C.c_void_p)]
 
@@ -172,6 +177,12 @@ SIGNATURES = {
                                      C.POINTER(crdt_tuples), _P]),
     "crdt_orset_merge_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ,
                                        C.POINTER(crdt_tuples), _P]),
+    "crdt_set_merge_plan": (_I, [_CTX, _I, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _SZ, C.c_uint32,
+                                 C.POINTER(crdt_set_plan)]),
+    "crdt_lww_merge_unsorted_planned": (_I, [_CTX, C.POINTER(crdt_set_plan), C.POINTER(crdt_tuples), _SZ,
+                                             C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _P]),
+    "crdt_orset_merge_unsorted_planned": (_I, [_CTX, C.POINTER(crdt_set_plan), C.POINTER(crdt_tuples), _SZ,
+                                               C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples), _P]),
     "crdt_tuples_sort": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, C.POINTER(crdt_tuples)]),
     "crdt_u64_lower_bound": (_I, [_CTX, _P, _SZ, _P, _SZ, _P]),
     "crdt_tuples_count_unsorted": (_I, [_CTX, C.POINTER(crdt_tuples), _SZ, _P]),

@@ -393,10 +393,13 @@ __device__ __forceinline__ void sort_load(const crdt_tuples &in, const uint64_t 
 }
 
 // cnt[d * ntiles + t] = composites of tile t with digit d in this pass
+__device__ __forceinline__ bool outside(uint64_t off, uint32_t b) { return b < 64 && (off >> b) != 0; }
+
 template <int WORDS, bool FIRST>
 __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
                                                 const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
-                                                uint32_t *__restrict__ cnt, uint64_t *__restrict__ comp) {
+                                                uint32_t *__restrict__ cnt, uint64_t *__restrict__ comp,
+                                                uint32_t *__restrict__ viol = nullptr) {
     __shared__ uint32_t h[SWAVES * 256];          // one histogram per wave: fewer LDS atomic collisions
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
@@ -404,6 +407,20 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
     const size_t base = (size_t)blockIdx.x * ST;
     CKey<WORDS> c[SR];
     sort_load<WORDS, FIRST>(in, src, n, p, base, c);
+    if (FIRST && viol) {                          // a planned call: every tuple inside the plan's ranges?
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+            const size_t e = base + (size_t)r * SB + tid;
+            if (e >= n) continue;
+            const bool side = e >= p.n1;
+            const crdt_tuples &T = side ? p.in2 : in;
+            const size_t f = side ? e - p.n1 : e;
+            bad = bad || outside(T.key[f] - p.kmin, p.bk) || outside(T.ts[f] - p.tmin, p.bt) ||
+                  outside((uint64_t)T.rep[f] - p.rmin, p.br);
+        }
+        if (__ballot(bad) && (tid & 63) == 0) atomicOr(viol, 1u);
+    }
     if constexpr (FIRST) {                        // the composites, so pass 0 reads 8 B instead of a tuple
 #pragma unroll
         for (int r = 0; r < SR; ++r) {
@@ -429,8 +446,6 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
 // loads per tuple).  Needs key / ts 16-byte, rep 8-byte, tomb 2-byte aligned
 // sides and an even n1 (no pair straddles the two inputs); the histogram
 // counts do not depend on which lane composes which tuple.
-__device__ __forceinline__ bool outside(uint64_t off, uint32_t b) { return b < 64 && (off >> b) != 0; }
-
 __global__ __launch_bounds__(SB) void k_sort_up_vec(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                     uint32_t ntiles, uint32_t *__restrict__ cnt,
                                                     uint64_t *__restrict__ comp, uint32_t *__restrict__ viol) {
@@ -686,7 +701,7 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
         if (q == 0 && WORDS == 1 && vec_first)
             k_sort_up_vec<<<ntiles, SB, 0, st>>>(in, n, plan_d, ntiles, cnt, a, viol);
         else if (q == 0)
-            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a);
+            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a, viol);
         else
             k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr);
         k_sort_colscan<<<256, CSB, 0, st>>>(cnt, ntiles, loc, tot, q == 0 ? zero : nullptr);
@@ -2135,137 +2150,321 @@ static bool tuples_overlap(const crdt_tuples &out, size_t cap, const crdt_tuples
     return false;
 }
 
+// ---------------------------------------------------------------- the D2 merge's workspace
+constexpr size_t kMaxChunks = 1u << 16;             // k_or_chunk: 2^(bk - 9), bk <= 25
+struct D2Ws {
+    SortMinMax *mm;
+    SortPlan *plan;
+    uint32_t *cnt, *loc, *tot;
+    uint64_t *bufs;
+    unsigned long long *flags;                      // [0, 256) bucket / look-back words, [256] the OR chunk fallback
+    uint32_t *viol;                                 // the plan's range check (the upsweep raises it)
+    uint64_t *cb;                                   // OR-Set chunk bounds, counts, offsets, look-back words
+    uint32_t *cc, *cl, *ct;
+    unsigned long long *cst;
+};
+
+template <int MODE>
+static size_t d2_ws_bytes(size_t n) {
+    const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;
+    const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
+    const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
+    const size_t b_flag = Carve::round(258 * 8);
+    const size_t b_chunk = MODE == DD_OR ? 2 * Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
+                                               Carve::round(64)
+                                         : 0;
+    return b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + b_chunk + 1024;
+}
+
+template <int MODE>
+static D2Ws d2_carve(void *ws, size_t n) {
+    const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
+    Carve w(ws);
+    D2Ws d{};
+    d.mm = w.take<SortMinMax>(2 * MM_BLOCKS);
+    d.plan = w.take<SortPlan>(1);
+    d.cnt = w.take<uint32_t>(ncnt);
+    d.loc = w.take<uint32_t>(ncnt);
+    d.tot = w.take<uint32_t>(256);
+    d.bufs = w.take<uint64_t>(2 * 3 * n);
+    d.flags = w.take<unsigned long long>(258);
+    d.viol = (uint32_t *)&d.flags[257];
+    if (MODE == DD_OR) {
+        d.cb = w.take<uint64_t>(kMaxChunks + 1);
+        d.cc = w.take<uint32_t>(kMaxChunks);
+        d.cl = w.take<uint32_t>(kMaxChunks);
+        d.ct = w.take<uint32_t>(16);
+        d.cst = w.take<unsigned long long>(kMaxChunks + 1);
+    }
+    return d;
+}
+
+// A planned call's plan on the device (by value: the launch captures it, so
+// a graph replays it) and its range check cleared.
+__global__ void k_put_plan(SortPlan h, SortPlan *plan, uint32_t *viol) {
+    if (threadIdx.x == 0) {
+        *plan = h;
+        *viol = 0;
+    }
+}
+
+// A planned call's end: a tuple outside the plan (the upsweep's range check)
+// or an OR-Set chunk over its LDS limits leaves the output invalid -- raise
+// CRDT_DEV_PLAN and set the count to ~0 (no host synchronisation).
+__global__ void k_d2_check(const uint32_t *__restrict__ viol, const uint32_t *__restrict__ fb,
+                           uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
+    if (threadIdx.x == 0 && ((viol && *viol) || (fb && *fb))) {
+        atomicOr(err, CRDT_DEV_PLAN);
+        *out_count = ~0ull;
+    }
+}
+
+static bool d2_vec(const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb) {
+    auto vec_ok = [](const crdt_tuples &t, size_t m) {
+        return m == 0 || !((((uintptr_t)t.key | (uintptr_t)t.ts) & 15) | ((uintptr_t)t.rep & 7) |
+                           ((uintptr_t)t.tomb & 1));
+    };
+    return vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
+}
+
+// The passes of a D2 merge whose plan h is known on the host (w.plan holds
+// it on the device).  vw: the range check of a sampled or given plan
+// (nullptr: the plan is exact for these inputs).
+//   planned (crdt_*_merge_unsorted_planned): no host synchronisation at all
+//     -- a tuple outside the plan, or an OR-Set chunk over its LDS limits,
+//     raises CRDT_DEV_PLAN and sets *out_count = ~0 (k_d2_check);
+//   otherwise the dense-key forms read their check words back at the end:
+//     *miss = the call must be redone from the exact plan (the caller does);
+//     the OR-Set chunk fallback runs the radix path here.
+template <int MODE>
+static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
+                   const crdt_tuples &out, uint64_t *out_count, const D2Ws &w, SortPlan h, uint32_t *vw, bool vec,
+                   bool planned, bool *miss) {
+    const size_t n = na + nb;
+    const hipStream_t s = ctx->stream;
+    const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
+    *miss = false;
+    auto read_words = [&](const void *src, size_t bytes) -> int {   // the end-of-call check words
+        int rc = hio_reserve(ctx, 16);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(ctx->hio, src, bytes, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
+    };
+    auto finish = [&](const uint32_t *fb) -> int {     // after the last pass: the range check
+        int rc = check_launch(ctx);
+        if (rc || !vw) return rc;
+        if (planned) {
+            k_d2_check<<<1, 64, 0, s>>>(vw, fb, out_count, ctx->dev_status);
+            return check_launch(ctx);
+        }
+        rc = read_words(vw, 4);
+        if (!rc) *miss = *(const uint32_t *)ctx->hio != 0;
+        return rc;
+    };
+    uint64_t *sorted = nullptr;
+    int rc;
+    if (h.words == 1) {
+        if (MODE == DD_LWW && h.tw) {                   // one pass on the key's top byte, then bucket tables
+            rc = sort_words<1>(ctx, A, n, out, w.plan, 1, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec, w.flags,
+                               vw);
+            if (rc) return rc;
+            if (h.tw == 4)
+                k_lww_table<uint32_t><<<256, LTB, 0, s>>>(sorted, w.plan, w.tot, w.flags, out, out_count,
+                                                          ctx->dev_status);
+            else
+                k_lww_table<uint64_t><<<256, LTB, 0, s>>>(sorted, w.plan, w.tot, w.flags, out, out_count,
+                                                          ctx->dev_status);
+            return finish(nullptr);
+        }
+        if (MODE == DD_OR && h.tw) {                    // two passes on the key's top 16 bits, then chunks in LDS
+            rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec, w.flags,
+                               vw);
+            if (rc) return rc;
+            const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
+            uint64_t *tmp = sorted == w.bufs ? w.bufs + n : w.bufs;
+            const bool lb = g_or_lookback && !g_rdd_diag;
+            uint32_t *fbw = (uint32_t *)&w.flags[256];
+            k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, w.cb, lb ? w.cst : nullptr);
+            if (lb) {
+                k_or_chunk<true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, 0, w.cst, out, out_count,
+                                                     ctx->dev_status);
+            } else {
+                k_or_chunk<false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, nullptr, out,
+                                                      out_count, ctx->dev_status);
+                k_sort_colscan<<<1, CSB, 0, s>>>(w.cc, nch, w.cl, w.ct);
+                k_or_emit<<<nch, 256, 0, s>>>(tmp, w.plan, w.cb, w.cc, w.cl, w.ct, out, out_count);
+            }
+            rc = check_launch(ctx);
+            if (rc) return rc;
+            if (planned) {
+                k_d2_check<<<1, 64, 0, s>>>(vw, fbw, out_count, ctx->dev_status);
+                return check_launch(ctx);
+            }
+            rc = read_words(&w.flags[256], 16);        // the fallback word (long keys), the range check
+            if (rc) return rc;
+            const uint32_t fb = *(const uint32_t *)ctx->hio, mw = vw ? ((const uint32_t *)ctx->hio)[2] : 0u;
+            if (mw) {
+                *miss = true;
+                return CRDT_OK;
+            }
+            if (fb == 0) return CRDT_OK;
+            // the sort path from the untouched inputs, on the exact ranges
+            const unsigned nmm = launch_minmax(ctx, A, na, B, nb, w.mm);
+            k_sort_plan<<<1, 256, 0, s>>>(w.mm, nmm, w.plan, 1, B, na, key_only, 0u, 0u, (uint64_t)n);
+            rc = read_plan(ctx, w.plan, &h);
+            if (rc) return rc;
+            vw = nullptr;
+        }
+        rc = sort_words<1>(ctx, A, n, out, w.plan, h.P, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec, nullptr, vw);
+        if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup
+            rc = or_run_dedup(ctx, sorted, n, w.plan, sorted == w.bufs ? w.bufs + n : w.bufs, w.bufs + 2 * n, w.cnt,
+                              w.loc, w.tot, out, out_count);
+        else if (!rc)
+            rc = dedup_words<MODE, 1>(ctx, sorted, n, w.plan, w.cnt, w.loc, w.tot, out, out_count);
+        return rc ? rc : finish(nullptr);
+    }
+    if (h.words == 2) {
+        rc = sort_words<2>(ctx, A, n, out, w.plan, h.P, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, false, nullptr, vw);
+        if (!rc) rc = dedup_words<MODE, 2>(ctx, sorted, n, w.plan, w.cnt, w.loc, w.tot, out, out_count);
+        return rc ? rc : finish(nullptr);
+    }
+    rc = sort_words<3>(ctx, A, n, out, w.plan, h.P, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, false, nullptr, vw);
+    if (!rc) rc = dedup_words<MODE, 3>(ctx, sorted, n, w.plan, w.cnt, w.loc, w.tot, out, out_count);
+    return rc ? rc : finish(nullptr);
+}
+
+// argument checks shared by the planned and unplanned calls
+static int d2_args(const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb, const crdt_tuples *out,
+                   const uint64_t *out_count) {
+    if (!out_count || !tuples_full(out)) return CRDT_E_INVAL;
+    if ((na && !tuples_full(a)) || (nb && !tuples_full(b))) return CRDT_E_INVAL;
+    if (na + nb >= (1ULL << 32)) return CRDT_E_RANGE;  // 32-bit in-tile / bucket arithmetic
+    const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
+    if (tuples_overlap(*out, na + nb, na ? *a : none, na) || tuples_overlap(*out, na + nb, nb ? *b : none, nb))
+        return CRDT_E_INVAL;
+    return CRDT_OK;
+}
+
 template <int MODE>
 static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
                               crdt_tuples *out, uint64_t *out_count, bool allow_sample = true) {
     int rc = bind(ctx);
     if (rc) return rc;
-    if (!out_count || !tuples_full(out)) return CRDT_E_INVAL;
-    if ((na && !tuples_full(a)) || (nb && !tuples_full(b))) return CRDT_E_INVAL;
+    rc = d2_args(a, na, b, nb, out, out_count);
+    if (rc) return rc;
     const size_t n = na + nb;
     const hipStream_t s = ctx->stream;
     if (n == 0) {
         hipError_t e = hipMemsetAsync(out_count, 0, sizeof(uint64_t), s);
         return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
     }
-    if (n >= (1ULL << 32)) return CRDT_E_RANGE;       // 32-bit in-tile / bucket arithmetic
     const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples A = na ? *a : none, B = nb ? *b : none;
-    if (tuples_overlap(*out, n, A, na) || tuples_overlap(*out, n, B, nb)) return CRDT_E_INVAL;
-    const size_t ntiles = (n + ST - 1) / ST, ncnt = ntiles * 256;   // >= the dedup's tile count
-    const size_t b_mm = Carve::round(2 * MM_BLOCKS * sizeof(SortMinMax)), b_plan = Carve::round(sizeof(SortPlan));
-    const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
-    const size_t b_flag = Carve::round(258 * 8);
-    constexpr size_t kMaxChunks = 1u << 16;             // k_or_chunk: 2^(bk - 9), bk <= 25
-    const size_t b_chunk = MODE == DD_OR ? 2 * Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
-                                               Carve::round(64)
-                                         : 0;
-    rc = ws_reserve(ctx, b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + b_chunk + 1024);
+    rc = ws_reserve(ctx, d2_ws_bytes<MODE>(n));
     if (rc) return rc;
-    Carve w(ctx->ws);
-    SortMinMax *mm = w.take<SortMinMax>(2 * MM_BLOCKS);
-    SortPlan *plan = w.take<SortPlan>(1);
-    uint32_t *cnt = w.take<uint32_t>(ncnt);
-    uint32_t *loc = w.take<uint32_t>(ncnt);
-    uint32_t *tot = w.take<uint32_t>(256);
-    uint64_t *bufs = w.take<uint64_t>(2 * 3 * n);
-    unsigned long long *flags = w.take<unsigned long long>(258);
-    uint32_t *viol = (uint32_t *)&flags[257];        // the sampled plan's range check
-    uint64_t *cb = MODE == DD_OR ? w.take<uint64_t>(kMaxChunks + 1) : nullptr;      // chunk bounds, counts, offsets
-    uint32_t *cc = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
-    uint32_t *cl = MODE == DD_OR ? w.take<uint32_t>(kMaxChunks) : nullptr;
-    uint32_t *ct = MODE == DD_OR ? w.take<uint32_t>(16) : nullptr;
-    unsigned long long *cst = MODE == DD_OR ? w.take<unsigned long long>(kMaxChunks + 1) : nullptr;   // look-back words
-    auto vec_ok = [](const crdt_tuples &t, size_t m) {
-        return m == 0 || !((((uintptr_t)t.key | (uintptr_t)t.ts) & 15) | ((uintptr_t)t.rep & 7) |
-                           ((uintptr_t)t.tomb & 1));
-    };
-    const bool vec = vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
+    const D2Ws w = d2_carve<MODE>(ctx->ws, n);
+    const bool vec = d2_vec(A, na, B, nb);
     const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
     const uint32_t lww_t = MODE == DD_LWW ? (uint32_t)g_lww_table : 0u, or_t = MODE == DD_OR ? (uint32_t)g_or_table : 0u;
     SortPlan h;
     // the dense-key paths from a sampled plan (sort.sample_plan): checked by
     // the composing upsweep, the call redone from the exact plan on a miss
     bool sampled = false;
-    unsigned nmm = 0;
     if (allow_sample && g_sample_plan && vec && (lww_t || or_t) && n >= (size_t)g_sample_min) {
-        nmm = 2 * SAMPLE_WG;
-        k_sample_minmax<<<nmm, 256, 0, s>>>(A, na, B, nb, mm);
-        k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n, 1u, viol);
-        rc = read_plan(ctx, plan, &h);
+        k_sample_minmax<<<2 * SAMPLE_WG, 256, 0, s>>>(A, na, B, nb, w.mm);
+        k_sort_plan<<<1, 256, 0, s>>>(w.mm, 2 * SAMPLE_WG, w.plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n, 1u,
+                                      w.viol);
+        rc = read_plan(ctx, w.plan, &h);
         if (rc) return rc;
         sampled = h.words == 1 && h.tw;
     }
     if (!sampled) {
-        nmm = launch_minmax(ctx, A, na, B, nb, mm);
-        k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n);
-        rc = read_plan(ctx, plan, &h);
+        const unsigned nmm = launch_minmax(ctx, A, na, B, nb, w.mm);
+        k_sort_plan<<<1, 256, 0, s>>>(w.mm, nmm, w.plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n);
+        rc = read_plan(ctx, w.plan, &h);
         if (rc) return rc;
     }
-    uint32_t *vw = sampled ? viol : nullptr;          // (a miss: the call again from the exact plan)
+    bool miss = false;
+    rc = d2_body<MODE>(ctx, A, na, B, nb, *out, out_count, w, h, sampled ? w.viol : nullptr, vec, false, &miss);
+    if (rc) return rc;
+    return miss ? set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false) : CRDT_OK;
+}
 
-    uint64_t *sorted = nullptr;
-    if (h.words == 1) {
-        if (MODE == DD_LWW && h.tw) {                   // one pass on the key's top byte, then bucket tables
-            rc = sort_words<1>(ctx, A, n, *out, plan, 1, bufs, cnt, loc, tot, false, &sorted, vec, flags, vw);
-            if (rc) return rc;
-            if (h.tw == 4)
-                k_lww_table<uint32_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
-            else
-                k_lww_table<uint64_t><<<256, LTB, 0, s>>>(sorted, plan, tot, flags, *out, out_count, ctx->dev_status);
-            rc = check_launch(ctx);
-            if (rc || !sampled) return rc;
-            rc = hio_reserve(ctx, 8);                   // the range check
-            if (rc) return rc;
-            hipError_t e = hipMemcpyAsync(ctx->hio, viol, 4, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return hip_fail(ctx, e);
-            if (*(const uint32_t *)ctx->hio == 0) return CRDT_OK;
-            return set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false);
-        }
-        if (MODE == DD_OR && h.tw) {                    // two passes on the key's top 16 bits, then chunks in LDS
-            rc = sort_words<1>(ctx, A, n, *out, plan, 2, bufs, cnt, loc, tot, false, &sorted, vec, flags, vw);
-            if (rc) return rc;
-            const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
-            uint64_t *tmp = sorted == bufs ? bufs + n : bufs;
-            const bool lb = g_or_lookback && !g_rdd_diag;
-            k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, cb, lb ? cst : nullptr);
-            if (lb) {
-                k_or_chunk<true><<<nch, OCB, 0, s>>>(sorted, tmp, plan, cb, cc, (uint32_t *)&flags[256], 0, cst, *out,
-                                                     out_count, ctx->dev_status);
-            } else {
-                k_or_chunk<false><<<nch, OCB, 0, s>>>(sorted, tmp, plan, cb, cc, (uint32_t *)&flags[256], g_rdd_diag,
-                                                      nullptr, *out, out_count, ctx->dev_status);
-                k_sort_colscan<<<1, CSB, 0, s>>>(cc, nch, cl, ct);
-                k_or_emit<<<nch, 256, 0, s>>>(tmp, plan, cb, cc, cl, ct, *out, out_count);
-            }
-            rc = check_launch(ctx);
-            if (rc) return rc;
-            rc = hio_reserve(ctx, 16);                  // the fallback word (long keys), the range check
-            if (rc) return rc;
-            hipError_t e = hipMemcpyAsync(ctx->hio, &flags[256], 16, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return hip_fail(ctx, e);
-            const uint32_t fb = *(const uint32_t *)ctx->hio, miss = sampled ? ((const uint32_t *)ctx->hio)[2] : 0u;
-            if (fb == 0 && miss == 0) return CRDT_OK;
-            if (miss) return set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false);
-            if (sampled) nmm = launch_minmax(ctx, A, na, B, nb, mm);   // the exact ranges for the sort path
-            k_sort_plan<<<1, 256, 0, s>>>(mm, nmm, plan, 1, B, na, key_only, 0u, 0u, (uint64_t)n);
-            rc = read_plan(ctx, plan, &h);              // the sort path from the untouched inputs
-            if (rc) return rc;
-        }
-        rc = sort_words<1>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted, vec);
-        if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup
-            return or_run_dedup(ctx, sorted, n, plan, sorted == bufs ? bufs + n : bufs, bufs + 2 * n, cnt, loc,
-                                tot, *out, out_count);
-        return rc ? rc : dedup_words<MODE, 1>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
+// ---------------------------------------------------------------- planned D2 merges
+// crdt_set_merge_plan's opaque result: the plan of one (mode, na, nb) shape.
+struct PlanBlob {
+    uint32_t magic, mode;
+    uint64_t na, nb;
+    SortPlan h;
+};
+constexpr uint32_t kPlanMagic = 0x43524450u;     // "CRDP"
+static_assert(sizeof(PlanBlob) <= sizeof(crdt_set_plan), "crdt_set_plan holds the plan");
+
+static int set_merge_plan(crdt_ctx *ctx, int mode, const crdt_tuples *a, size_t na, const crdt_tuples *b, size_t nb,
+                          uint32_t widen, crdt_set_plan *plan) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!plan || (mode != DD_LWW && mode != DD_OR)) return CRDT_E_INVAL;
+    if ((na && !tuples_full(a)) || (nb && !tuples_full(b))) return CRDT_E_INVAL;
+    const size_t n = na + nb;
+    if (n >= (1ULL << 32)) return CRDT_E_RANGE;
+    const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
+    const crdt_tuples A = na ? *a : none, B = nb ? *b : none;
+    // the planned calls run in the workspace reserved here (no allocation
+    // inside a captured graph)
+    rc = ws_reserve(ctx, mode == DD_LWW ? d2_ws_bytes<DD_LWW>(n) : d2_ws_bytes<DD_OR>(n));
+    if (!rc) rc = hio_reserve(ctx, 16);
+    if (rc) return rc;
+    PlanBlob pb{};
+    pb.magic = kPlanMagic;
+    pb.mode = (uint32_t)mode;
+    pb.na = na;
+    pb.nb = nb;
+    if (n) {
+        const D2Ws w = mode == DD_LWW ? d2_carve<DD_LWW>(ctx->ws, n) : d2_carve<DD_OR>(ctx->ws, n);
+        const uint32_t key_only = mode == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
+        const uint32_t lww_t = mode == DD_LWW ? (uint32_t)g_lww_table : 0u, or_t = mode == DD_OR ? (uint32_t)g_or_table : 0u;
+        const unsigned nmm = launch_minmax(ctx, A, na, B, nb, w.mm);
+        k_sort_plan<<<1, 256, 0, ctx->stream>>>(w.mm, nmm, w.plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n,
+                                                widen ? 1u : 0u);
+        rc = read_plan(ctx, w.plan, &pb.h);
+        if (rc) return rc;
     }
-    if (h.words == 2) {
-        rc = sort_words<2>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
-        return rc ? rc : dedup_words<MODE, 2>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
+    memset(plan, 0, sizeof *plan);
+    memcpy(plan, &pb, sizeof pb);
+    return CRDT_OK;
+}
+
+template <int MODE>
+static int set_merge_planned(crdt_ctx *ctx, const crdt_set_plan *plan, const crdt_tuples *a, size_t na,
+                             const crdt_tuples *b, size_t nb, crdt_tuples *out, uint64_t *out_count) {
+    int rc = bind(ctx);
+    if (rc) return rc;
+    if (!plan) return CRDT_E_INVAL;
+    PlanBlob pb;
+    memcpy(&pb, plan, sizeof pb);
+    if (pb.magic != kPlanMagic || pb.mode != (uint32_t)MODE || pb.na != na || pb.nb != nb) return CRDT_E_INVAL;
+    rc = d2_args(a, na, b, nb, out, out_count);
+    if (rc) return rc;
+    const size_t n = na + nb;
+    const hipStream_t s = ctx->stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(out_count, 0, sizeof(uint64_t), s);
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
     }
-    rc = sort_words<3>(ctx, A, n, *out, plan, h.P, bufs, cnt, loc, tot, false, &sorted);
-    return rc ? rc : dedup_words<MODE, 3>(ctx, sorted, n, plan, cnt, loc, tot, *out, out_count);
+    if (ctx->ws_bytes < d2_ws_bytes<MODE>(n)) return CRDT_E_INVAL;   // (the plan call reserved it)
+    const crdt_tuples none{nullptr, nullptr, nullptr, nullptr};
+    const crdt_tuples A = na ? *a : none, B = nb ? *b : none;
+    const D2Ws w = d2_carve<MODE>(ctx->ws, n);
+    SortPlan h = pb.h;
+    h.in2 = B;                                          // (the plan's shape, these inputs)
+    h.n1 = na;
+    k_put_plan<<<1, 64, 0, s>>>(h, w.plan, w.viol);
+    rc = check_launch(ctx);
+    if (rc) return rc;
+    bool miss = false;
+    return d2_body<MODE>(ctx, A, na, B, nb, *out, out_count, w, h, w.viol, d2_vec(A, na, B, nb), true, &miss);
 }
 }  // namespace crdt
 
@@ -2321,4 +2520,21 @@ extern "C" int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size
 extern "C" int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                                          size_t nb, crdt_tuples *out, uint64_t *out_count_dev) {
     return set_merge_unsorted<DD_OR>(ctx, a, na, b, nb, out, out_count_dev);
+}
+
+extern "C" int crdt_set_merge_plan(crdt_ctx *ctx, int mode, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                                   size_t nb, uint32_t widen, crdt_set_plan *plan) {
+    return set_merge_plan(ctx, mode, a, na, b, nb, widen, plan);
+}
+
+extern "C" int crdt_lww_merge_unsorted_planned(crdt_ctx *ctx, const crdt_set_plan *plan, const crdt_tuples *a,
+                                               size_t na, const crdt_tuples *b, size_t nb, crdt_tuples *out,
+                                               uint64_t *out_count_dev) {
+    return set_merge_planned<DD_LWW>(ctx, plan, a, na, b, nb, out, out_count_dev);
+}
+
+extern "C" int crdt_orset_merge_unsorted_planned(crdt_ctx *ctx, const crdt_set_plan *plan, const crdt_tuples *a,
+                                                 size_t na, const crdt_tuples *b, size_t nb, crdt_tuples *out,
+                                                 uint64_t *out_count_dev) {
+    return set_merge_planned<DD_OR>(ctx, plan, a, na, b, nb, out, out_count_dev);
 }

@@ -257,6 +257,29 @@ class Engine:
         """OR-Set merge of UNSORTED sides (D2): one fused device sort + dedup."""
         return self._set_merge("crdt_orset_merge_unsorted", a, b, out, count, trim)
 
+    def set_merge_plan(self, lww: bool, a: TupleSet, b: TupleSet, widen: bool = False):
+        """crdt_set_merge_plan: the exact plan of a D2 merge of this shape
+        (one synchronisation); reserves the workspace its planned calls use."""
+        from ._lib import crdt_set_plan
+        plan = crdt_set_plan()
+        ca, cb = a.c(), b.c()
+        self._call("crdt_set_merge_plan", 0 if lww else 1, C.byref(ca), len(a), C.byref(cb), len(b),
+                   1 if widen else 0, C.byref(plan))
+        return plan
+
+    def merge_unsorted_planned(self, lww: bool, plan, a: TupleSet, b: TupleSet, out: TupleSet,
+                               count: torch.Tensor) -> None:
+        """crdt_{lww,orset}_merge_unsorted_planned: the D2 merge enqueued with
+        no host synchronisation (graph-capturable); *count = 2^64 - 1 and the
+        CRDT_DEV_PLAN flag when the inputs left the plan."""
+        for s in (a, b, out):
+            self._check(s.key, s.ts, itemsize=8)
+            self._check(s.rep, itemsize=4)
+            self._check(s.tomb, itemsize=1)
+        ca, cb, co = a.c(), b.c(), out.c()
+        fn = "crdt_lww_merge_unsorted_planned" if lww else "crdt_orset_merge_unsorted_planned"
+        self._call(fn, C.byref(plan), C.byref(ca), len(a), C.byref(cb), len(b), C.byref(co), count.data_ptr())
+
     def sort_tuples(self, t: TupleSet, out: TupleSet | None = None) -> TupleSet:
         """Device sort into ascending (key, ts, rep, tomb) order (config D2)."""
         n = len(t)

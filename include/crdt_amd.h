@@ -70,6 +70,8 @@ int crdt_ctx_sync(crdt_ctx *ctx);
 #define CRDT_DEV_LOOKBACK 1u
 #define CRDT_DEV_RANGE 2u          /* a batch exceeded a per-replica kernel limit, or a pass found its
                                       inputs inconsistent (merge bitmaps): the output is invalid */
+#define CRDT_DEV_PLAN 4u           /* a planned D2 merge's inputs fell outside its plan (or an OR-Set key
+                                      chunk outgrew its LDS): that call's output is invalid, its count ~0 */
 int crdt_ctx_device_status(crdt_ctx *ctx, uint32_t *flags, int clear);
 int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 /* Pre-size the context's device workspace so that later calls never
@@ -189,6 +191,30 @@ int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, cons
                             size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                               size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
+/* Stream-ordered D2 merges (no host synchronisation: a HIP graph can capture
+ * them).  The calls above read their plan -- field ranges, composite layout,
+ * which dense-key form applies -- back from the device (one synchronisation)
+ * and check the sampled ranges at the end (a second).  A host that merges
+ * the same shape repeatedly (a replica population's key space; the gossip
+ * loop of main.go:226-258 calls merge() every round) plans once:
+ * crdt_set_merge_plan (mode 0 = LWW, 1 = OR-Set; synchronises once) computes
+ * the exact plan of a, b -- widen != 0 widens each field range by 1/256 of
+ * its span, for later inputs that drift -- and reserves the context's
+ * workspace for it.  The _planned calls then enqueue the merge with no
+ * read-back, for inputs of the same na / nb (CRDT_E_INVAL otherwise): the
+ * composing pass checks every tuple against the plan, and a tuple outside it
+ * (or an OR-Set key chunk over its LDS limits) raises CRDT_DEV_PLAN in the
+ * context's status word and sets *out_count_dev = ~0 -- run the unplanned
+ * call then.  Otherwise the output is the unplanned call's, bit for bit. */
+typedef struct crdt_set_plan {
+    uint64_t w[24];
+} crdt_set_plan;
+int crdt_set_merge_plan(crdt_ctx *ctx, int mode, const crdt_tuples *a, size_t na, const crdt_tuples *b,
+                        size_t nb, uint32_t widen, crdt_set_plan *plan);
+int crdt_lww_merge_unsorted_planned(crdt_ctx *ctx, const crdt_set_plan *plan, const crdt_tuples *a, size_t na,
+                                    const crdt_tuples *b, size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
+int crdt_orset_merge_unsorted_planned(crdt_ctx *ctx, const crdt_set_plan *plan, const crdt_tuples *a, size_t na,
+                                      const crdt_tuples *b, size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 /* Sort n SoA tuples (device) into ascending (key, ts, rep, tomb) order --
  * the merge input order, with tomb (0/1) breaking exact tag ties so the
  * result does not depend on the input order (config D2: unsorted state).
