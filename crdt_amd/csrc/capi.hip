@@ -29,6 +29,9 @@ int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
 int g_sample_plan = 1;   // dense-key D2 paths from a sampled plan, checked in the upsweep (sort.sample_plan)
+int g_plan_cache = 1;    // ... launched from the last such plan's shape, checked on the device (sort.plan_cache)
+int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
+int g_or_narrow = 1;     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
 int g_or_lookback = 1;   // OR-Set D2 chunks: offsets by a decoupled look-back (0: count scan + emit pass)
 int g_or_table = 1;      // OR-Set D2: 2^9-key chunks sorted in LDS after two top-16-bit passes (16..25 key bits)
@@ -326,6 +329,15 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.sample_plan")) {  // D2 dense-key paths: 1 plan from a sample + range check, 0 full minmax
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sample_plan = (int)v;
+    } else if (!strcmp(name, "sort.lww_gather")) {   // LWW D2 tables: 1 runs gathered from bucket-grouped tiles, 0 a scatter pass
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_lww_gather = (int)v;
+    } else if (!strcmp(name, "sort.or_narrow")) {    // OR-Set D2 chunks: 1 u32 sorting networks where the tag fits 32 bits
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_narrow = (int)v;
+    } else if (!strcmp(name, "sort.plan_cache")) {   // D2 sampled plans: 1 launch from the cached shape (no read-back)
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_plan_cache = (int)v;
     } else if (!strcmp(name, "sort.sample_min")) {   // fewest tuples for the sampled plan
         if (v < 0 || v > 0x7FFFFFFF) return CRDT_E_INVAL;
         g_sample_min = (int)v;

@@ -39,6 +39,14 @@ struct crdt_ctx {
     hipStream_t aux = nullptr;
     hipEvent_t *ev = nullptr;         // event pool of the pipelined passes (timing disabled)
     size_t n_ev = 0;
+    // D2 merges (sort.hip): the last sampled dense-key plan, by (mode, n,
+    // knobs).  The next such call launches its passes from this shape with no
+    // read-back; the device compares the fresh sampled plan with it and a
+    // difference counts as a range miss (the call is redone exactly, the
+    // entry dropped).
+    alignas(8) unsigned char d2_plan[2][128];   // [mode: LWW, OR-Set]
+    uint64_t d2_key[2][2] = {{0, 0}, {0, 0}};
+    bool d2_ok[2] = {false, false};
 };
 
 namespace crdt {
@@ -69,6 +77,9 @@ extern int g_rm_diag;           // timing diagnostic: refmerge replay fold varia
 extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
 extern int g_lww_table;        // LWW D2 key-bucket tables (sort.lww_table)
 extern int g_sample_plan;      // D2 dense-key paths from a sampled plan (sort.sample_plan)
+extern int g_plan_cache;       // ... launched from the context's cached plan shape (sort.plan_cache)
+extern int g_lww_gather;       // LWW D2 tables fed by gathers from bucket-grouped tiles (sort.lww_gather)
+extern int g_or_narrow;        // OR-Set D2 chunks: u32 sorting networks (sort.or_narrow)
 extern int g_sample_min;       // ... from this many tuples (sort.sample_min)
 extern int g_or_lookback;      // OR-Set D2 chunk offsets by look-back (sort.or_lookback)
 extern int g_or_table;         // OR-Set D2 key chunks sorted in LDS (sort.or_table)

@@ -1202,6 +1202,209 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- LWW D2: bucket tables fed by gathers
+// sort.lww_gather (default 1, vector-aligned inputs).  The table form above
+// needs each key bucket's composites contiguous, which cost a radix scatter
+// pass (composites read and written once more, 320 MB at config D) and its
+// column scan.  A bucket's winner is a MAX, so its composites may arrive in
+// any order: here the composing pass groups each 4096-tuple tile's
+// composites by bucket in LDS (an unstable counting sort) and stores the
+// tile in that order, with each (bucket, tile) count and start; the bucket's
+// workgroup then gathers its ~16-composite run from every tile -- 16 lanes
+// per run, four runs per wave-instruction, so every load is a contiguous
+// 128-B piece -- into its LDS table.  No scatter pass, no column scan.
+__global__ __launch_bounds__(SB) void k_lww_up_tiled(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
+                                                     uint32_t ntiles, uint32_t *__restrict__ run,
+                                                     uint64_t *__restrict__ comp, uint32_t *__restrict__ viol,
+                                                     unsigned long long *__restrict__ zero) {
+    __shared__ uint32_t h[256], hs[256];
+    __shared__ uint64_t stage[ST];
+    const int tid = threadIdx.x;
+    h[tid] = 0;
+    if (zero && blockIdx.x == 0) zero[tid] = 0;        // the bucket tables' flags (k_lww_table_g)
+    const SortPlan p = *plan_;
+    const size_t base = (size_t)blockIdx.x * ST;
+    uint64_t c[SR];
+    uint32_t vm = 0;                                  // bit r: c[r] holds a tuple (e < n)
+    bool bad = false;                                 // (viol) a field outside the plan's ranges
+    auto out_of = [&](uint64_t k, uint64_t t, uint32_t r) {
+        return outside(k - p.kmin, p.bk) || outside(t - p.tmin, p.bt) || outside((uint64_t)r - p.rmin, p.br);
+    };
+#pragma unroll
+    for (int r = 0; r < SR / 2; ++r) {               // two tuples per lane per round (16-B key / ts loads)
+        const size_t e = base + 2 * ((size_t)r * SB + tid);
+        c[2 * r] = c[2 * r + 1] = 0;
+        if (e >= n) continue;
+        vm |= (e + 1 < n ? 3u : 1u) << (2 * r);
+        const bool side = e >= p.n1;
+        const crdt_tuples &T = side ? p.in2 : in;
+        const size_t f = side ? e - p.n1 : e;
+        if (e + 1 < n) {
+            const ulonglong2 k = *(const ulonglong2 *)(T.key + f), t = *(const ulonglong2 *)(T.ts + f);
+            const uint2 rp = *(const uint2 *)(T.rep + f);
+            const uint16_t tb = *(const uint16_t *)(T.tomb + f);
+            if (viol) bad = bad || out_of(k.x, t.x, rp.x) || out_of(k.y, t.y, rp.y);
+            c[2 * r] = compose<1>(p, k.x, t.x, rp.x, (uint8_t)(tb & 0xFF), side).w[0];
+            c[2 * r + 1] = compose<1>(p, k.y, t.y, rp.y, (uint8_t)(tb >> 8), side).w[0];
+        } else {
+            if (viol) bad = bad || out_of(T.key[f], T.ts[f], T.rep[f]);
+            c[2 * r] = compose<1>(p, T.key[f], T.ts[f], T.rep[f], T.tomb[f], side).w[0];
+        }
+    }
+    if (viol && __ballot(bad) && (tid & 63) == 0) atomicOr(viol, 1u);
+    __syncthreads();
+    const uint32_t sh = p.s0;                         // the bucket: the composite's top byte (bits s0 .. s0 + 8)
+    uint32_t d[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+        d[r] = ((vm >> r) & 1u) ? (uint32_t)(c[r] >> sh) & 255u : 256u;
+        if (d[r] < 256) atomicAdd(&h[d[r]], 1u);
+    }
+    __syncthreads();
+    {                                                 // exclusive scan of the 256 bucket counts
+        const uint32_t v = h[tid];
+        uint64_t all;
+        const uint32_t ex = (uint32_t)block_exclusive_scan_u64(v, &all);
+        hs[tid] = ex;
+        run[(size_t)tid * ntiles + blockIdx.x] = ex << 16 | v;   // (bucket, tile) run: start | count (<= 4096 each)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SR; ++r)
+        if (d[r] < 256) stage[atomicAdd(&hs[d[r]], 1u)] = c[r];
+    __syncthreads();
+    const uint32_t m = n - base < (size_t)ST ? (uint32_t)(n - base) : (uint32_t)ST;
+    for (uint32_t i = 2 * tid; i < m; i += 2 * SB) {   // the tile, bucket by bucket (16-B stores)
+        if (i + 1 < m) *(ulonglong2 *)(comp + base + i) = ulonglong2{stage[i], stage[i + 1]};
+        else comp[base + i] = stage[i];
+    }
+}
+
+constexpr uint32_t kRunLds = 6144;                 // (bucket, tile) runs staged in LDS (24 KB; config D: 4883)
+template <typename E>
+__global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
+                                                     const uint32_t *__restrict__ run, uint32_t ntiles,
+                                                     unsigned long long *__restrict__ flag, crdt_tuples out,
+                                                     uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
+    constexpr uint32_t NE = kLtBytes / sizeof(E);  // 2^15 u32 / 2^14 u64 entries
+    constexpr uint32_t NR = NE / LTB;
+    static_assert(NR * LT_WAVES <= 64 * 8, "one wave scans the round counts");
+    __shared__ E tab[NE];
+    __shared__ uint32_t s_run[kRunLds];
+    __shared__ uint32_t s_cnt[NR * LT_WAVES];
+    __shared__ unsigned long long s_sum[3];
+    const SortPlan p = *plan_;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t b = blockIdx.x, L = p.tl, ne = 1u << L;
+    const uint32_t kb = p.b0 + p.br + p.bt;
+    const E marker = (E)1 << kb, tmask = marker - 1;
+    if (tid < 3) s_sum[tid] = 0;
+    for (uint32_t i = tid; i < ne; i += LTB) tab[i] = 0;
+    const uint32_t *rg = run + (size_t)b * ntiles;    // this bucket's run in every tile
+    const bool lds = ntiles <= kRunLds;
+    if (lds)
+        for (uint32_t i = tid; i < ntiles; i += LTB) s_run[i] = rg[i];
+    __syncthreads();
+    // lane group g (16 lanes) takes KT tiles per iteration, t = t0 + g +
+    // 64 k, its lanes elements l and l + 16 of each run: 2 KT loads in
+    // flight per lane, every load instruction four contiguous 128-B pieces
+    constexpr uint32_t KT = 4, NG = 4 * LT_WAVES;     // tiles per group per iteration, lane groups
+    const uint32_t g = (uint32_t)tid >> 4, l = (uint32_t)lane & 15;
+    auto put = [&](uint64_t x) { atomicMax(&tab[(uint32_t)(x >> kb) & (ne - 1)], ((E)(x ^ 3u) & tmask) | marker); };
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += NG * KT) {
+        uint32_t rn[KT];
+        const uint64_t *rp[KT];
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            const uint32_t t = t0 + g + NG * k;
+            rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
+            rp[k] = c + (size_t)t * ST + (rn[k] >> 16);
+            rn[k] &= 0xFFFFu;
+        }
+        uint64_t x[2 * KT];
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            x[2 * k] = l < rn[k] ? rp[k][l] : 0;
+            x[2 * k + 1] = l + 16 < rn[k] ? rp[k][l + 16] : 0;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            if (l < rn[k]) put(x[2 * k]);
+            if (l + 16 < rn[k]) put(x[2 * k + 1]);
+            for (uint32_t i = l + 32; i < rn[k]; i += 16) put(rp[k][i]);   // (rare: runs over 32)
+        }
+    }
+    __syncthreads();
+    // present keys per (round, wave), their exclusive prefix, and the total
+    const uint32_t R = (ne + LTB - 1) / LTB, NC = R * LT_WAVES;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t e = r * LTB + tid;
+        const uint64_t m = __ballot(e < ne && tab[e] != 0);
+        if (lane == 0) s_cnt[r * LT_WAVES + w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (w == 0) {
+        uint32_t v[8], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = lane * 8 + k;
+            v[k] = i < NC ? s_cnt[i] : 0u;
+            sum += v[k];
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t y = __shfl_up(x, dd, 64);
+            if (lane >= dd) x += y;
+        }
+        uint32_t run = x - sum;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = lane * 8 + k;
+            if (i < NC) s_cnt[i] = run;
+            run += v[k];
+        }
+        if (lane == 63) {
+            s_sum[2] = x;
+            __hip_atomic_store(&flag[b], kLtReady | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // the predecessors' counts (as k_lww_table: every count is published before its workgroup waits)
+    unsigned long long pre = 0;
+    if ((uint32_t)tid < b) {
+        unsigned long long f;
+        uint32_t spins = 0;
+        while (!((f = __hip_atomic_load(&flag[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kLtReady)) {
+            if (++spins > (1u << 22)) {            // bounded: report, never hang
+                atomicOr(err, CRDT_DEV_LOOKBACK);
+                f = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pre = f & 0xFFFFFFFFull;
+    }
+    for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (lane == 0 && w < 4 && pre) atomicAdd(&s_sum[1], pre);
+    __syncthreads();
+    const uint64_t off = s_sum[1];
+    if (b == gridDim.x - 1 && tid == 0) *out_count = off + s_sum[2];
+    const uint64_t kbase = (uint64_t)b << L;
+    const uint32_t sr = p.b0, st = p.b0 + p.br;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t e = r * LTB + tid;
+        const E v = e < ne ? tab[e] : (E)0;
+        const uint64_t m = __ballot(v != 0);
+        if (v == 0) continue;
+        const size_t o = off + s_cnt[r * LT_WAVES + w] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint64_t win = (uint64_t)(v & tmask) ^ 3u;
+        out.key[o] = p.kmin + (kbase | e);
+        out.ts[o] = p.tmin + lt_field(win, st, p.bt);
+        out.rep[o] = (uint32_t)(p.rmin + lt_field(win, sr, p.br));
+        out.tomb[o] = (uint8_t)(win & 1u);
+    }
+}
+
 // ---------------------------------------------------------------- OR-Set D2: key chunks sorted in LDS
 // sort.or_table (default 1).  The radix sort runs only TWO passes, on the
 // key's top 16 bits; the key space is then cut into chunks of 2^9 keys
@@ -1256,6 +1459,29 @@ __device__ __forceinline__ void ot_sort8(uint64_t *v) {
     ot_cswap(v[2], v[4]); ot_cswap(v[3], v[5]);
     ot_cswap(v[1], v[2]); ot_cswap(v[3], v[4]); ot_cswap(v[5], v[6]);
 }
+// the same on the low 32 bits, when every tag bit lies below bit 32 (kb <=
+// 32: the bits above are the key's, equal over a key's slots) -- u32 min /
+// max instead of 64-bit compares and selects
+__device__ __forceinline__ void ot_cswap32(uint32_t &a, uint32_t &b) {
+    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+__device__ __forceinline__ void ot_sort8_32(uint32_t *v) {
+    ot_cswap32(v[0], v[1]); ot_cswap32(v[2], v[3]); ot_cswap32(v[4], v[5]); ot_cswap32(v[6], v[7]);
+    ot_cswap32(v[0], v[2]); ot_cswap32(v[1], v[3]); ot_cswap32(v[4], v[6]); ot_cswap32(v[5], v[7]);
+    ot_cswap32(v[1], v[2]); ot_cswap32(v[5], v[6]);
+    ot_cswap32(v[0], v[4]); ot_cswap32(v[1], v[5]); ot_cswap32(v[2], v[6]); ot_cswap32(v[3], v[7]);
+    ot_cswap32(v[2], v[4]); ot_cswap32(v[3], v[5]);
+    ot_cswap32(v[1], v[2]); ot_cswap32(v[3], v[4]); ot_cswap32(v[5], v[6]);
+}
+__device__ __forceinline__ uint32_t ot_firsts32(const uint32_t *v, uint32_t m, uint32_t tb) {
+    uint32_t fm = m ? 1u : 0u;
+#pragma unroll
+    for (uint32_t j = 1; j < kOtRun; ++j) fm |= (j < m && (v[j] >> tb) != (v[j - 1] >> tb)) ? 1u << j : 0u;
+    return fm;
+}
+
 // bit j: slot j (< m) starts a tag in the sorted slots
 __device__ __forceinline__ uint32_t ot_firsts(const uint64_t *v, uint32_t m, uint32_t tb) {
     uint32_t fm = m ? 1u : 0u;
@@ -1303,7 +1529,7 @@ __global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict
 // nearest resolved one.  Chunks are dispatched in index order, so every
 // polled chunk has been dispatched; polls are bounded (CRDT_DEV_LOOKBACK).
 constexpr unsigned long long kOcA = 1ull << 62, kOcP = 2ull << 62, kOcVal = (1ull << 62) - 1;
-template <bool LB>
+template <bool LB, bool NARROW>
 __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
                                                   const SortPlan *__restrict__ plan_,
                                                   const uint64_t *__restrict__ bounds, uint32_t *__restrict__ cnt,
@@ -1382,17 +1608,35 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     }
     // distinct tags per key (long keys listed, resolved below); each short
     // key's slots stay sorted in registers for the stores
+    // (NARROW: kb <= 32, every tag bit in the low word -- the key's slots are
+    // sorted on their low words, the high word kept once per key)
     uint32_t dk[R], fk[R];
-    uint64_t sv[R][kOtRun];
+    uint64_t sv[NARROW ? 1 : R][NARROW ? 1 : kOtRun];
+    uint32_t sl[NARROW ? R : 1][NARROW ? kOtRun : 1], sh[NARROW ? R : 1];
+    auto slot = [&](uint32_t r, uint32_t j) -> uint64_t {   // slot j of key r's sorted slots (the full composite)
+        if constexpr (NARROW) return (uint64_t)sh[r] << 32 | sl[r][j];
+        else return sv[r][j];
+    };
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
         const uint32_t kl = r * OCB + tid;
         const uint32_t s0 = kl ? tab[kl - 1] : 0u, m = tab[kl] - s0;
         const uint32_t ms = m <= kOtRun ? m : 0u;
+        if constexpr (NARROW) {
 #pragma unroll
-        for (uint32_t k = 0; k < kOtRun; ++k) sv[r][k] = k < ms ? stg[s0 + k] : ~0ull;
-        if (ms > 1) ot_sort8(sv[r]);
-        fk[r] = ot_firsts(sv[r], ms, tb);
+            for (uint32_t k = 0; k < kOtRun; ++k) {
+                const uint64_t v = k < ms ? stg[s0 + k] : ~0ull;
+                sl[r][k] = (uint32_t)v;
+                if (k == 0) sh[r] = (uint32_t)(v >> 32);
+            }
+            if (ms > 1) ot_sort8_32(sl[r]);
+            fk[r] = ot_firsts32(sl[r], ms, tb);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < kOtRun; ++k) sv[r][k] = k < ms ? stg[s0 + k] : ~0ull;
+            if (ms > 1) ot_sort8(sv[r]);
+            fk[r] = ot_firsts(sv[r], ms, tb);
+        }
         dk[r] = (uint32_t)__popc(fk[r]);
         if (m > kOtMid) {
             const uint32_t q = atomicAdd(&s_nlong, 1u);
@@ -1481,6 +1725,45 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         if (tid == 0) cnt[blockIdx.x] = 0;
         return;
     }
+    // LB: the offset -- the counts of the chunks before this one -- found by
+    // wave 0 while the other waves place their keys' tags (the barrier after
+    // the placement joins them)
+    __shared__ unsigned long long s_off;
+    if (LB && w == 0) {
+        const uint32_t nt0 = s_tot;
+        unsigned long long acc = 0;
+        if (blockIdx.x > 0) {
+            long long j = (long long)blockIdx.x - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const long long q = j - lane;
+                const unsigned long long f =
+                    q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kOcP;
+                const uint64_t isp = __ballot((f >> 62) == 2), notready = __ballot((f >> 62) == 0);
+                const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
+                const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
+                if (notready & need) {
+                    if (++spins > (1u << 22)) {       // bounded: report, never hang
+                        if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long v = lane <= pl ? (f & kOcVal) : 0ull;
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                acc += v;
+                if (pl < 64) break;
+                j -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&st[blockIdx.x], kOcP | (acc + nt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_off = acc;
+            if (blockIdx.x == gridDim.x - 1) *out_count = acc + nt0;
+        }
+    }
     // stores: composites with the side bit cleared and the tomb = the OR of the tag's copies
     uint64_t *dst = tmp + s;
     const uint64_t keep = ~3ull;
@@ -1515,13 +1798,13 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
             for (int j = kOtRun - 1; j >= 0; --j) {
                 const bool in = (uint32_t)j < m;
                 const bool cont = (uint32_t)j + 1 < m && !((fk[r] >> (j + 1)) & 1u);
-                run = (in ? (uint32_t)(sv[r][j] & 1u) : 0u) | (cont ? run : 0u);
+                run = (in ? (uint32_t)(slot(r, (uint32_t)j) & 1u) : 0u) | (cont ? run : 0u);
                 tt |= run << j;
             }
             uint32_t rk = rk0;
 #pragma unroll
             for (uint32_t j = 0; j < kOtRun; ++j)
-                if ((fk[r] >> j) & 1u) ost[rk++] = (sv[r][j] & keep) | ((tt >> j) & 1u);
+                if ((fk[r] >> j) & 1u) ost[rk++] = (slot(r, j) & keep) | ((tt >> j) & 1u);
         }
     }
     __syncthreads();
@@ -1546,44 +1829,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         for (uint32_t i = tid; i < nt; i += OCB) dst[i] = ost[i];
         return;
     }
-    // the offset: the counts of the chunks before this one
-    __shared__ unsigned long long s_off;
-    if (w == 0) {
-        unsigned long long acc = 0;
-        if (blockIdx.x > 0) {
-            long long j = (long long)blockIdx.x - 1;
-            uint32_t spins = 0;
-            for (;;) {
-                const long long q = j - lane;
-                const unsigned long long f =
-                    q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kOcP;
-                const uint64_t isp = __ballot((f >> 62) == 2), notready = __ballot((f >> 62) == 0);
-                const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
-                const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
-                if (notready & need) {
-                    if (++spins > (1u << 22)) {       // bounded: report, never hang
-                        if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                unsigned long long v = lane <= pl ? (f & kOcVal) : 0ull;
-                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-                acc += v;
-                if (pl < 64) break;
-                j -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(&st[blockIdx.x], kOcP | (acc + nt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_off = acc;
-            if (blockIdx.x == gridDim.x - 1) *out_count = acc + nt;
-        }
-    }
-    __syncthreads();
-    const size_t o = s_off;
+    const size_t o = s_off;                          // (wave 0's look-back above; the barriers since publish it)
     const uint32_t sr = p.b0 + p.br;
     for (uint32_t i = tid; i < nt; i += OCB) {
         const uint64_t xv = ost[i];
@@ -2219,6 +2465,17 @@ __global__ void k_d2_check(const uint32_t *__restrict__ viol, const uint32_t *__
     }
 }
 
+// The fresh (sampled) plan against the cached one the host launched from:
+// any difference in the launch shape raises the range check (a miss).
+__global__ void k_plan_match(const SortPlan *__restrict__ fresh, SortPlan c, uint32_t *__restrict__ viol) {
+    if (threadIdx.x != 0) return;
+    const SortPlan f = *fresh;
+    if (f.words != c.words || f.P != c.P || f.s0 != c.s0 || f.tl != c.tl || f.tw != c.tw || f.bk != c.bk ||
+        f.bt != c.bt || f.br != c.br || f.b0 != c.b0 || f.W != c.W)
+        *viol = 1;
+}
+static_assert(sizeof(SortPlan) <= sizeof(((crdt_ctx *)nullptr)->d2_plan[0]), "the context caches a plan per mode");
+
 static bool d2_vec(const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb) {
     auto vec_ok = [](const crdt_tuples &t, size_t m) {
         return m == 0 || !((((uintptr_t)t.key | (uintptr_t)t.ts) & 15) | ((uintptr_t)t.rep & 7) |
@@ -2265,6 +2522,17 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
     uint64_t *sorted = nullptr;
     int rc;
     if (h.words == 1) {
+        if (MODE == DD_LWW && h.tw && vec && g_lww_gather) {   // tiles grouped by bucket, tables gather their runs
+            const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
+            k_lww_up_tiled<<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+            if (h.tw == 4)
+                k_lww_table_g<uint32_t><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count,
+                                                            ctx->dev_status);
+            else
+                k_lww_table_g<uint64_t><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count,
+                                                            ctx->dev_status);
+            return finish(nullptr);
+        }
         if (MODE == DD_LWW && h.tw) {                   // one pass on the key's top byte, then bucket tables
             rc = sort_words<1>(ctx, A, n, out, w.plan, 1, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec, w.flags,
                                vw);
@@ -2286,12 +2554,21 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             const bool lb = g_or_lookback && !g_rdd_diag;
             uint32_t *fbw = (uint32_t *)&w.flags[256];
             k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, w.cb, lb ? w.cst : nullptr);
+            const bool narrow = kb <= 32 && g_or_narrow;
             if (lb) {
-                k_or_chunk<true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, 0, w.cst, out, out_count,
-                                                     ctx->dev_status);
+                if (narrow)
+                    k_or_chunk<true, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, 0, w.cst, out,
+                                                               out_count, ctx->dev_status);
+                else
+                    k_or_chunk<true, false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, 0, w.cst, out,
+                                                                out_count, ctx->dev_status);
             } else {
-                k_or_chunk<false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, nullptr, out,
-                                                      out_count, ctx->dev_status);
+                if (narrow)
+                    k_or_chunk<false, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag,
+                                                                nullptr, out, out_count, ctx->dev_status);
+                else
+                    k_or_chunk<false, false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag,
+                                                                 nullptr, out, out_count, ctx->dev_status);
                 k_sort_colscan<<<1, CSB, 0, s>>>(w.cc, nch, w.cl, w.ct);
                 k_or_emit<<<nch, 256, 0, s>>>(tmp, w.plan, w.cb, w.cc, w.cl, w.ct, out, out_count);
             }
@@ -2375,9 +2652,25 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
         k_sample_minmax<<<2 * SAMPLE_WG, 256, 0, s>>>(A, na, B, nb, w.mm);
         k_sort_plan<<<1, 256, 0, s>>>(w.mm, 2 * SAMPLE_WG, w.plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n, 1u,
                                       w.viol);
-        rc = read_plan(ctx, w.plan, &h);
-        if (rc) return rc;
-        sampled = h.words == 1 && h.tw;
+        // the launch shape of the last call of this kind, checked on the
+        // device: no read-back (sort.plan_cache)
+        const uint64_t key0 = (uint64_t)n, key1 = (uint64_t)MODE | (uint64_t)key_only << 8 | (uint64_t)lww_t << 16 |
+                                                  (uint64_t)or_t << 24 | (uint64_t)na << 32;
+        if (g_plan_cache && ctx->d2_ok[MODE] && ctx->d2_key[MODE][0] == key0 && ctx->d2_key[MODE][1] == key1) {
+            memcpy(&h, ctx->d2_plan[MODE], sizeof h);
+            k_plan_match<<<1, 64, 0, s>>>(w.plan, h, w.viol);
+            sampled = true;
+        } else {
+            rc = read_plan(ctx, w.plan, &h);
+            if (rc) return rc;
+            sampled = h.words == 1 && h.tw;
+            ctx->d2_ok[MODE] = sampled && g_plan_cache;
+            if (ctx->d2_ok[MODE]) {
+                memcpy(ctx->d2_plan[MODE], &h, sizeof h);
+                ctx->d2_key[MODE][0] = key0;
+                ctx->d2_key[MODE][1] = key1;
+            }
+        }
     }
     if (!sampled) {
         const unsigned nmm = launch_minmax(ctx, A, na, B, nb, w.mm);
@@ -2388,7 +2681,9 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     bool miss = false;
     rc = d2_body<MODE>(ctx, A, na, B, nb, *out, out_count, w, h, sampled ? w.viol : nullptr, vec, false, &miss);
     if (rc) return rc;
-    return miss ? set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false) : CRDT_OK;
+    if (!miss) return CRDT_OK;
+    ctx->d2_ok[MODE] = false;                           // (a shape change: the next call reads its plan back)
+    return set_merge_unsorted<MODE>(ctx, a, na, b, nb, out, out_count, false);
 }
 
 // ---------------------------------------------------------------- planned D2 merges

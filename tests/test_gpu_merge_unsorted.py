@@ -298,3 +298,27 @@ def test_unsorted_refuses_out_aliasing_an_input(eng):
         got = fn(A, B, out=out).to_numpy()
         for g, e in zip(got, ref(sa, sb)):
             np.testing.assert_array_equal(g, e)
+
+
+def test_unsorted_plan_cache_shape_changes(eng):
+    """sort.plan_cache: a sampled dense-key call launches from the last such
+    call's plan shape with no read-back, the device checking the fresh plan
+    against it.  Calls of one size whose key / ts widths change between calls
+    (a shape mismatch: the call is redone from the exact plan and the cache
+    dropped), alternating modes, and a repeat of each == the oracle."""
+    from crdt_amd import _lib
+    rng = np.random.default_rng(123)
+
+    def side(m, kbits, tbits):
+        return (rng.integers(0, 2**kbits, m, dtype=np.uint64), rng.integers(0, 2**tbits, m, dtype=np.uint64),
+                rng.integers(0, 50, m, dtype=np.uint64).astype(np.uint32), rng.integers(0, 2, m, dtype=np.uint8))
+
+    try:
+        _lib.call("crdt_set_option", b"sort.sample_min", 0)
+        for kbits, tbits in ((20, 20), (20, 20), (21, 20), (18, 24), (18, 24), (20, 20)):
+            a, b = side(120_000, kbits, tbits), side(120_000, kbits, tbits)
+            for f in range(3):
+                b[f][:2000] = a[f][:2000]
+            _check(eng, a, b)
+    finally:
+        _lib.call("crdt_set_option", b"sort.sample_min", 1 << 20)
