@@ -30,6 +30,7 @@ int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
 int g_sample_plan = 1;   // dense-key D2 paths from a sampled plan, checked in the upsweep (sort.sample_plan)
 int g_plan_cache = 1;    // ... launched from the last such plan's shape, checked on the device (sort.plan_cache)
+int g_rm_affine = 1;     // one-pair populations: RefMerge pair indices computed, no kv range loads (refmerge.affine_kv)
 int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
 int g_or_narrow = 1;     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -317,8 +318,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v < 1 || v > 16) return CRDT_E_INVAL;
         g_mm_bpc = (int)v;
     } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: the D2 dedup apply (OR-Set: and count)
-        if (v < 0 || v > 4) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores);
-                                                        //   OR-Set chunks: 1 key counts, 2 LDS sort, 3 per-key tags, 4 long keys + ranks
+        if (v < 0 || v > 6) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores);
+                                                        //   OR-Set chunks: 1 key counts, 2 LDS sort, 3 per-key tags, 4 long keys + ranks,
+                                                        //   5 all but the output stores, 6 no look-back (fake offsets)
         g_rdd_diag = (int)v;
     } else if (!strcmp(name, "sort.lww_table")) {    // LWW D2: 1 key-bucket LDS tables where they apply, 0 key-only sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
@@ -329,6 +331,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.sample_plan")) {  // D2 dense-key paths: 1 plan from a sample + range check, 0 full minmax
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_sample_plan = (int)v;
+    } else if (!strcmp(name, "refmerge.affine_kv")) { // one-pair populations: 1 pair index = kv[0] + entry (no range loads)
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_rm_affine = (int)v;
     } else if (!strcmp(name, "sort.lww_gather")) {   // LWW D2 tables: 1 runs gathered from bucket-grouped tiles, 0 a scatter pass
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_lww_gather = (int)v;

@@ -166,6 +166,7 @@ struct KvOut {
     uint64_t cap;
     const uint64_t *ikv;                  // per-tile kv base (exclusive scan of tkv)
     const uint32_t *tone;                 // per tile: every emitted entry has exactly one pair
+    uint32_t affine = 0;                  // one-pair population: every entry one pair, entry e's at kv[0] + e
 };
 
 // kv pairs of an entry's range [kb, ke), clamped to the arena (malformed
@@ -731,6 +732,16 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
     uint32_t e_cnt[FI], e_slot[FI], e_v[FI];
     uint32_t cmask = 0;                                  // KV: bit f = replay candidate (its count is k_c[f])
     uint8_t e_org[FI];
+    // ONE (one-pair populations): every entry of L and of the pulled ranges
+    // holds exactly one pair and the pairs lie in entry order -- entry gi's
+    // pair at kv[0] + gi -- so no range is loaded: the pair loads issue with
+    // the ts loads instead of behind a kv range load
+    uint64_t kl0 = 0, kr0 = 0;
+    const bool aff = ONE && kvo.affine;                  // (uniform)
+    if (aff) {
+        kl0 = in.n_l ? in.l_kv[0] : 0;
+        kr0 = in.n_r ? in.r_kv[0] : 0;
+    }
 #pragma unroll
     for (int f = 0; f < FI; ++f) {                       // every entry load issued before the first use
         // (only emitted entries are written or folded: an R entry whose ts L
@@ -740,7 +751,8 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
         const uint64_t *kv = (il ? in.l_kv : in.r_kv) + gi;
         e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
         e_org[f] = (in_tile && il) ? in.l_origin[gi] : 0;
-        e_kb[f] = ((FOLDS || KV) && in_tile) ? kv[0] : 0;
+        if (aff) e_kb[f] = (il ? kl0 : kr0) + gi;
+        else e_kb[f] = ((FOLDS || KV) && in_tile) ? kv[0] : 0;
         e_ke[f] = ((FOLDS || KV) && !ONE && in_tile) ? kv[1] : 0;   // (ONE: every emitted range has one pair)
     }
     if (FOLDS || KV) {
@@ -1354,7 +1366,12 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // the tile pass: slice write and (with slots) the replay fold
     const unsigned tg = (unsigned)tmax;
     const int lda = g_rm_ld_all ? kDiagLoadAll : 0;
-    const KvOut kvo = kv ? KvOut{kv->kv_off, kv->kv_key, kv->kv_val, kv->kv_cap, ikv, tone} : KvOut{};
+    // (one_pair: the caller's population keeps one pair per entry in entry
+    // order -- refmerge_batch_pull_one_pair; the tile pass then computes
+    // each entry's pair index instead of loading its kv range)
+    const KvOut kvo = kv ? KvOut{kv->kv_off, kv->kv_key, kv->kv_val, kv->kv_cap, ikv, tone,
+                                 one_pair && g_rm_affine ? 1u : 0u}
+                         : KvOut{};
     if (delta && ns) {                                            // incremental replay: fold only the inserted R
         k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, lda, ic, out, *delta, cand, cand_n,
                                                    ovf, ctx->dev_status);

@@ -1729,7 +1729,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     // wave 0 while the other waves place their keys' tags (the barrier after
     // the placement joins them)
     __shared__ unsigned long long s_off;
-    if (LB && w == 0) {
+    if (LB && w == 0 && diag == 6 && lane == 0) s_off = s;   // (timing only: no look-back, a disjoint fake offset)
+    if (LB && w == 0 && diag != 6) {
         const uint32_t nt0 = s_tot;
         unsigned long long acc = 0;
         if (blockIdx.x > 0) {
@@ -1830,6 +1831,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         return;
     }
     const size_t o = s_off;                          // (wave 0's look-back above; the barriers since publish it)
+    if (diag == 5) return;                            // (timing only: everything but the output stores)
     const uint32_t sr = p.b0 + p.br;
     for (uint32_t i = tid; i < nt; i += OCB) {
         const uint64_t xv = ost[i];
@@ -2551,17 +2553,17 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             if (rc) return rc;
             const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
             uint64_t *tmp = sorted == w.bufs ? w.bufs + n : w.bufs;
-            const bool lb = g_or_lookback && !g_rdd_diag;
+            const bool lb = g_or_lookback && (!g_rdd_diag || g_rdd_diag >= 5);   // (diag 5 / 6: the look-back form's timings)
             uint32_t *fbw = (uint32_t *)&w.flags[256];
             k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, w.cb, lb ? w.cst : nullptr);
             const bool narrow = kb <= 32 && g_or_narrow;
             if (lb) {
                 if (narrow)
-                    k_or_chunk<true, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, 0, w.cst, out,
-                                                               out_count, ctx->dev_status);
+                    k_or_chunk<true, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, w.cst,
+                                                               out, out_count, ctx->dev_status);
                 else
-                    k_or_chunk<true, false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, 0, w.cst, out,
-                                                                out_count, ctx->dev_status);
+                    k_or_chunk<true, false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, w.cst,
+                                                                out, out_count, ctx->dev_status);
             } else {
                 if (narrow)
                     k_or_chunk<false, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag,
