@@ -1529,32 +1529,49 @@ __global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict
 // nearest resolved one.  Chunks are dispatched in index order, so every
 // polled chunk has been dispatched; polls are bounded (CRDT_DEV_LOOKBACK).
 constexpr unsigned long long kOcA = 1ull << 62, kOcP = 2ull << 62, kOcVal = (1ull << 62) - 1;
-template <bool LB, bool NARROW>
+// K (sort.or_pair): chunks per workgroup.  K = 2 processes two consecutive
+// chunks in turn, each into its own LDS output buffer, and looks back ONCE,
+// for the first, after both are placed -- by then its predecessors have had
+// a whole chunk's time to publish -- then stores both (the second's offset
+// is the first's plus its count).
+// (wave-uniform returns / continues only: every barrier below is reached by
+// the whole workgroup or by none of it)
+template <bool LB, bool NARROW, int K>
 __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
                                                   const SortPlan *__restrict__ plan_,
                                                   const uint64_t *__restrict__ bounds, uint32_t *__restrict__ cnt,
                                                   uint32_t *__restrict__ fbw, int diag,
                                                   unsigned long long *__restrict__ st, crdt_tuples out,
-                                                  uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
+                                                  uint64_t *__restrict__ out_count, uint32_t *__restrict__ err,
+                                                  uint32_t nch) {
     constexpr uint32_t R = kOcKeys / OCB;             // keys per thread (round-major)
     __shared__ uint32_t tab[kOcKeys];
     __shared__ uint64_t stg[kOcCap];
-    __shared__ uint64_t ost[kOcCap];                  // the chunk's tags in order (one coalesced copy out)
+    __shared__ uint64_t ostb[K][kOcCap];              // each chunk's tags in order (one coalesced copy out)
     __shared__ uint32_t s_first[kOcCap / 32];         // a long key's first-copy marks
-    __shared__ uint32_t s_cnt[R * OC_WAVES], s_wsum[OC_WAVES], s_long[kOcLong], s_lrk[kOcLong], s_nlong, s_tot;
+    __shared__ uint32_t s_cnt[R * OC_WAVES], s_wsum[OC_WAVES], s_long[kOcLong], s_lrk[kOcLong], s_nlong, s_totk[K];
+    __shared__ unsigned long long s_off;
     const SortPlan p = *plan_;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t kb = p.b0 + p.br + p.bt, tb = p.b0;
-    const size_t s = bounds[blockIdx.x], e = bounds[blockIdx.x + 1];
+    bool fb = false;                                  // (uniform) a chunk of this workgroup fell back
+    size_t sk[K];
+    for (int kk = 0; kk < K; ++kk) {
+    const uint32_t ci = blockIdx.x * K + (uint32_t)kk;
+    uint64_t *ost = ostb[kk];
+    const size_t s = bounds[ci], e = bounds[ci + 1];
+    sk[kk] = s;
     if (e - s > kOcCap) {                             // skewed keys: the radix path instead
         if (tid == 0) {
             atomicOr(fbw, 1u);
-            cnt[blockIdx.x] = 0;
-            if (LB) __hip_atomic_store(&st[blockIdx.x], kOcA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cnt[ci] = 0;
+            if (LB) __hip_atomic_store(&st[ci], kOcA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        return;
+        fb = true;
+        continue;
     }
     const uint32_t len = (uint32_t)(e - s);
+    __syncthreads();                                  // (the previous chunk's LDS reads are done)
     for (uint32_t i = tid; i < kOcKeys; i += OCB) tab[i] = 0;
     for (uint32_t i = tid; i < kOcCap / 32; i += OCB) s_first[i] = 0;
     if (tid == 0) s_nlong = 0;
@@ -1571,7 +1588,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         if (k * OCB + tid < len) atomicAdd(&tab[(uint32_t)(x[k] >> kb) & (kOcKeys - 1)], 1u);
     __syncthreads();
     if (diag == 1) {                                  // timing diagnostics (sort.rdd_diag): counts only
-        if (tid == 0) cnt[blockIdx.x] = 0;
+        if (tid == 0) cnt[ci] = 0;
         return;
     }
     {                                                 // exclusive scan: wave w the contiguous entries [w P, (w+1) P)
@@ -1603,7 +1620,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         if (k * OCB + tid < len) stg[atomicAdd(&tab[(uint32_t)(x[k] >> kb) & (kOcKeys - 1)], 1u)] = x[k];
     __syncthreads();                                  // tab[k] = the end of key k
     if (diag == 2) {                                  // + the scan and the scatter into LDS
-        if (tid == 0) cnt[blockIdx.x] = 0;
+        if (tid == 0) cnt[ci] = 0;
         return;
     }
     // distinct tags per key (long keys listed, resolved below); each short
@@ -1656,16 +1673,17 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     __syncthreads();
     const uint32_t nl = s_nlong;
     if (diag == 3) {                                  // + the short keys' distinct tags
-        if (tid == 0) cnt[blockIdx.x] = 0;
+        if (tid == 0) cnt[ci] = 0;
         return;
     }
     if (nl > kOcLong) {                               // (uniform) too many long keys: the radix path
         if (tid == 0) {
             atomicOr(fbw, 1u);
-            cnt[blockIdx.x] = 0;
-            if (LB) __hip_atomic_store(&st[blockIdx.x], kOcA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cnt[ci] = 0;
+            if (LB) __hip_atomic_store(&st[ci], kOcA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        return;
+        fb = true;
+        continue;
     }
     for (uint32_t q = 0; q < nl; ++q) {               // a long key: first-copy marks, their count to its owner
         const uint32_t kl = s_long[q];
@@ -1713,28 +1731,26 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         }
         if (lane < (int)NC) s_cnt[lane] = y - c0;
         if (lane == 63) {
-            cnt[blockIdx.x] = y;
-            s_tot = y;
+            cnt[ci] = y;
+            s_totk[kk] = y;
             if (LB)                                   // counted: published at once
-                __hip_atomic_store(&st[blockIdx.x], (blockIdx.x ? kOcA : kOcP) | y, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&st[ci], (ci ? kOcA : kOcP) | y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
     if (diag == 4) {                                  // + the long keys and the ranks
-        if (tid == 0) cnt[blockIdx.x] = 0;
+        if (tid == 0) cnt[ci] = 0;
         return;
     }
     // LB: the offset -- the counts of the chunks before this one -- found by
     // wave 0 while the other waves place their keys' tags (the barrier after
     // the placement joins them)
-    __shared__ unsigned long long s_off;
-    if (LB && w == 0 && diag == 6 && lane == 0) s_off = s;   // (timing only: no look-back, a disjoint fake offset)
-    if (LB && w == 0 && diag != 6) {
-        const uint32_t nt0 = s_tot;
+    if (K == 1 && LB && w == 0 && diag == 6 && lane == 0) s_off = s;   // (timing only: no look-back, a fake offset)
+    if (K == 1 && LB && w == 0 && diag != 6) {
+        const uint32_t nt0 = s_totk[0];
         unsigned long long acc = 0;
-        if (blockIdx.x > 0) {
-            long long j = (long long)blockIdx.x - 1;
+        if (ci > 0) {
+            long long j = (long long)ci - 1;
             uint32_t spins = 0;
             for (;;) {
                 const long long q = j - lane;
@@ -1758,15 +1774,14 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
                 j -= 64;
             }
             if (lane == 0)
-                __hip_atomic_store(&st[blockIdx.x], kOcP | (acc + nt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&st[ci], kOcP | (acc + nt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) {
             s_off = acc;
-            if (blockIdx.x == gridDim.x - 1) *out_count = acc + nt0;
+            if (ci == nch - 1) *out_count = acc + nt0;
         }
     }
-    // stores: composites with the side bit cleared and the tomb = the OR of the tag's copies
-    uint64_t *dst = tmp + s;
+    // placement: composites with the side bit cleared and the tomb = the OR of the tag's copies
     const uint64_t keep = ~3ull;
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
@@ -1824,21 +1839,66 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
             ost[rk0 + rk] = (xi & keep) | tomb;
         }
     }
+    }                                                 // (the next chunk of this workgroup)
     __syncthreads();
-    const uint32_t nt = s_tot;
+    if (fb) return;                                   // (uniform; the call falls back to the radix path)
     if constexpr (!LB) {
-        for (uint32_t i = tid; i < nt; i += OCB) dst[i] = ost[i];
+        for (int kk = 0; kk < K; ++kk)
+            for (uint32_t i = tid; i < s_totk[kk]; i += OCB) tmp[sk[kk] + i] = ostb[kk][i];
         return;
     }
-    const size_t o = s_off;                          // (wave 0's look-back above; the barriers since publish it)
+    if (K == 2 && w == 0 && diag == 6 && lane == 0) s_off = sk[0];
+    if (K == 2 && w == 0 && diag != 6) {              // one look-back for both chunks, after both are placed
+        const uint32_t ci = blockIdx.x * K, n0 = s_totk[0], n1 = K == 2 ? s_totk[K - 1] : 0u;
+        unsigned long long acc = 0;
+        if (ci > 0) {
+            long long j = (long long)ci - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const long long q = j - lane;
+                const unsigned long long f =
+                    q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kOcP;
+                const uint64_t isp = __ballot((f >> 62) == 2), notready = __ballot((f >> 62) == 0);
+                const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
+                const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
+                if (notready & need) {
+                    if (++spins > (1u << 22)) {       // bounded: report, never hang
+                        if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long v = lane <= pl ? (f & kOcVal) : 0ull;
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                acc += v;
+                if (pl < 64) break;
+                j -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&st[ci], kOcP | (acc + n0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            __hip_atomic_store(&st[ci + 1], kOcP | (acc + n0 + n1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_off = acc;
+            if (ci + 1 == nch - 1) *out_count = acc + n0 + n1;
+        }
+    }
+    __syncthreads();
     if (diag == 5) return;                            // (timing only: everything but the output stores)
     const uint32_t sr = p.b0 + p.br;
-    for (uint32_t i = tid; i < nt; i += OCB) {
-        const uint64_t xv = ost[i];
-        out.key[o + i] = p.kmin + lt_field(xv, kb, p.bk);
-        out.ts[o + i] = p.tmin + lt_field(xv, sr, p.bt);
-        out.rep[o + i] = (uint32_t)(p.rmin + lt_field(xv, p.b0, p.br));
-        out.tomb[o + i] = (uint8_t)(xv & 1u);
+    size_t o = s_off;
+    for (int kk = 0; kk < K; ++kk) {
+        const uint32_t nt = s_totk[kk];
+        const uint64_t *ost = ostb[kk];
+        for (uint32_t i = tid; i < nt; i += OCB) {
+            const uint64_t xv = ost[i];
+            out.key[o + i] = p.kmin + lt_field(xv, kb, p.bk);
+            out.ts[o + i] = p.tmin + lt_field(xv, sr, p.bt);
+            out.rep[o + i] = (uint32_t)(p.rmin + lt_field(xv, p.b0, p.br));
+            out.tomb[o + i] = (uint8_t)(xv & 1u);
+        }
+        o += nt;
     }
 }
 
@@ -2557,20 +2617,28 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             uint32_t *fbw = (uint32_t *)&w.flags[256];
             k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, w.cb, lb ? w.cst : nullptr);
             const bool narrow = kb <= 32 && g_or_narrow;
+            const int kpair = g_or_pair && nch % 2 == 0 ? 2 : 1;
+            const unsigned grid = nch / (unsigned)kpair;
+#define OR_CHUNK(LBV, NAR, KV)                                                                                 \
+    k_or_chunk<LBV, NAR, KV><<<grid, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, LBV ? w.cst : nullptr, \
+                                                   out, out_count, ctx->dev_status, nch)
             if (lb) {
-                if (narrow)
-                    k_or_chunk<true, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, w.cst,
-                                                               out, out_count, ctx->dev_status);
-                else
-                    k_or_chunk<true, false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, w.cst,
-                                                                out, out_count, ctx->dev_status);
+                if (narrow) {
+                    if (kpair == 2) OR_CHUNK(true, true, 2);
+                    else OR_CHUNK(true, true, 1);
+                } else {
+                    if (kpair == 2) OR_CHUNK(true, false, 2);
+                    else OR_CHUNK(true, false, 1);
+                }
             } else {
-                if (narrow)
-                    k_or_chunk<false, true><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag,
-                                                                nullptr, out, out_count, ctx->dev_status);
-                else
-                    k_or_chunk<false, false><<<nch, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag,
-                                                                 nullptr, out, out_count, ctx->dev_status);
+                if (narrow) {
+                    if (kpair == 2) OR_CHUNK(false, true, 2);
+                    else OR_CHUNK(false, true, 1);
+                } else {
+                    if (kpair == 2) OR_CHUNK(false, false, 2);
+                    else OR_CHUNK(false, false, 1);
+                }
+#undef OR_CHUNK
                 k_sort_colscan<<<1, CSB, 0, s>>>(w.cc, nch, w.cl, w.ct);
                 k_or_emit<<<nch, 256, 0, s>>>(tmp, w.plan, w.cb, w.cc, w.cl, w.ct, out, out_count);
             }
