@@ -33,6 +33,7 @@ int g_plan_cache = 1;    // ... launched from the last such plan's shape, checke
 int g_rm_affine = 1;     // one-pair populations: RefMerge pair indices computed, no kv range loads (refmerge.affine_kv)
 int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
 int g_or_narrow = 1;
+int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
 int g_or_lookback = 1;   // OR-Set D2 chunks: offsets by a decoupled look-back (0: count scan + emit pass)
@@ -338,6 +339,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.lww_gather")) {   // LWW D2 tables: 1 runs gathered from bucket-grouped tiles, 0 a scatter pass
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_lww_gather = (int)v;
+    } else if (!strcmp(name, "sort.or_bucket")) {    // OR-Set D2: 1 tile groups + bucket gathers, 0 two radix passes
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_bucket = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

@@ -1221,7 +1221,10 @@ __global__ __launch_bounds__(SB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
     __shared__ uint64_t stage[ST];
     const int tid = threadIdx.x;
     h[tid] = 0;
-    if (zero && blockIdx.x == 0) zero[tid] = 0;        // the bucket tables' flags (k_lww_table_g)
+    if (zero && blockIdx.x == 0) {                    // the buckets' flags (k_lww_table_g, k_or_bucket), the
+        zero[tid] = 0;                                //   OR-Set chunks' fallback word
+        if (tid == 0) zero[256] = 0;
+    }
     const SortPlan p = *plan_;
     const size_t base = (size_t)blockIdx.x * ST;
     uint64_t c[SR];
@@ -1253,7 +1256,7 @@ __global__ __launch_bounds__(SB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
     }
     if (viol && __ballot(bad) && (tid & 63) == 0) atomicOr(viol, 1u);
     __syncthreads();
-    const uint32_t sh = p.s0;                         // the bucket: the composite's top byte (bits s0 .. s0 + 8)
+    const uint32_t sh = p.W - 8;                      // the bucket: the composite's (the key's) top byte
     uint32_t d[SR];
 #pragma unroll
     for (int r = 0; r < SR; ++r) {
@@ -1403,6 +1406,137 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
         out.rep[o] = (uint32_t)(p.rmin + lt_field(win, sr, p.br));
         out.tomb[o] = (uint8_t)(win & 1u);
     }
+}
+
+// OR-Set D2 without radix passes (sort.or_bucket): the composing pass groups
+// each tile by the key's top byte T (k_lww_up_tiled); one 1024-thread
+// workgroup per T then gathers T's runs from every tile TWICE -- first to
+// count them by the chunk-id bits under T (chunks of 2^9 keys: 2^(bk-17)
+// per T), then to place each into its chunk's contiguous range of T's
+// region (LDS cursors; any order within a chunk: the chunk kernel sorts
+// it) -- and writes the chunk bounds.  T's region starts after the regions
+// of T' < T: each workgroup publishes its total and sums its predecessors'
+// (all 256 are co-resident; polls bounded).  Replaces two radix passes
+// (upsweep, column scan, scatter each) and the chunk-bounds search.
+constexpr int OBB = 1024;                          // threads per bucket workgroup
+constexpr int OB_WAVES = OBB / 64;
+constexpr uint32_t kObSub = 256;                   // chunks per top-byte bucket at most (bk <= 25)
+__global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
+                                                   const uint32_t *__restrict__ run, uint32_t ntiles, size_t n,
+                                                   unsigned long long *__restrict__ flag, uint64_t *__restrict__ dst,
+                                                   uint64_t *__restrict__ bounds, unsigned long long *__restrict__ cst,
+                                                   uint32_t nch, uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_run[kRunLds];
+    __shared__ uint32_t s_h[OB_WAVES][kObSub];        // per-wave counts by sub-bucket, then the cursors (row 0)
+    __shared__ unsigned long long s_sum[3];
+    const SortPlan p = *plan_;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t T = blockIdx.x;
+    const uint32_t kb = p.b0 + p.br + p.bt;           // the key's bits start here
+    const uint32_t s6 = p.bk > 17 ? p.bk - 17 : 0;    // chunk-id bits under the top byte
+    const uint32_t nsub = 1u << s6, ssh = kb + 9;     // sub-bucket = (x >> ssh) & (nsub - 1)
+    const uint32_t *rg = run + (size_t)T * ntiles;
+    const bool lds = ntiles <= kRunLds;
+    if (tid < 3) s_sum[tid] = 0;
+    for (uint32_t i = tid; i < OB_WAVES * kObSub; i += OBB) (&s_h[0][0])[i] = 0;
+    unsigned long long tot = 0;                       // this bucket's tuples
+    for (uint32_t i = tid; i < ntiles; i += OBB) {
+        const uint32_t r = rg[i];
+        if (lds) s_run[i] = r;
+        tot += r & 0xFFFFu;
+    }
+    for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    __syncthreads();
+    if (lane == 0 && tot) atomicAdd(&s_sum[2], tot);
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&flag[T], kLtReady | s_sum[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // gather the runs (as k_lww_table_g: 16-lane groups, KT tiles each per round, 2 elements per lane per tile)
+    constexpr uint32_t KT = 4, NG = 4 * OB_WAVES;
+    const uint32_t g = (uint32_t)tid >> 4, l = (uint32_t)lane & 15;
+    auto sweep = [&](auto &&put) {
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += NG * KT) {
+            uint32_t rn[KT];
+            const uint64_t *rp[KT];
+#pragma unroll
+            for (uint32_t k = 0; k < KT; ++k) {
+                const uint32_t t = t0 + g + NG * k;
+                rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
+                rp[k] = c + (size_t)t * ST + (rn[k] >> 16);
+                rn[k] &= 0xFFFFu;
+            }
+            uint64_t x[2 * KT];
+#pragma unroll
+            for (uint32_t k = 0; k < KT; ++k) {
+                x[2 * k] = l < rn[k] ? rp[k][l] : 0;
+                x[2 * k + 1] = l + 16 < rn[k] ? rp[k][l + 16] : 0;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < KT; ++k) {
+                if (l < rn[k]) put(x[2 * k]);
+                if (l + 16 < rn[k]) put(x[2 * k + 1]);
+                for (uint32_t i = l + 32; i < rn[k]; i += 16) put(rp[k][i]);   // (rare: runs over 32)
+            }
+        }
+    };
+    // 1. counts by sub-bucket (a row per wave: fewer same-address LDS atomics)
+    sweep([&](uint64_t x) { atomicAdd(&s_h[w][(uint32_t)(x >> ssh) & (nsub - 1)], 1u); });
+    // the predecessors' totals (every bucket published its own above)
+    unsigned long long pre = 0;
+    if ((uint32_t)tid < T) {
+        unsigned long long f;
+        uint32_t spins = 0;
+        while (!((f = __hip_atomic_load(&flag[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kLtReady)) {
+            if (++spins > (1u << 22)) {            // bounded: report, never hang
+                atomicOr(err, CRDT_DEV_LOOKBACK);
+                f = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pre = f & 0xFFFFFFFFull;
+    }
+    for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    __syncthreads();                                  // every wave's counts
+    if (lane == 0 && w < 4 && pre) atomicAdd(&s_sum[1], pre);
+    if (w == 0) {                                     // sub-bucket totals -> exclusive prefix -> cursors (row 0)
+        uint32_t v[kObSub / 64], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kObSub / 64; ++k) {
+            const uint32_t b = (uint32_t)lane * (kObSub / 64) + k;
+            uint32_t t = 0;
+            for (int q = 0; q < OB_WAVES; ++q) t += s_h[q][b];
+            v[k] = t;
+            sum += t;
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        uint32_t run0 = x - sum;
+#pragma unroll
+        for (uint32_t k = 0; k < kObSub / 64; ++k) {
+            s_h[0][(uint32_t)lane * (kObSub / 64) + k] = run0;
+            run0 += v[k];
+        }
+    }
+    __syncthreads();
+    const uint64_t base = s_sum[1];
+    // the chunk bounds (chunk = 2^9 keys: sub-buckets of T, or runs of 2^(17 - bk) buckets) and
+    // the chunk kernel's look-back words
+    if (s6 > 0 || (T & ((1u << (17 - p.bk)) - 1u)) == 0) {
+        for (uint32_t b = tid; b < nsub; b += OBB) {
+            const uint32_t ch = s6 > 0 ? (T << s6) + b : T >> (17 - p.bk);
+            bounds[ch] = base + s_h[0][b];
+            if (cst) cst[ch] = 0;
+        }
+    }
+    if (T == gridDim.x - 1 && tid == 0) bounds[nch] = n;
+    __syncthreads();
+    // 2. each tuple into its chunk's range of T's region (any order within it)
+    uint64_t *out = dst + base;
+    sweep([&](uint64_t x) { out[atomicAdd(&s_h[0][(uint32_t)(x >> ssh) & (nsub - 1)], 1u)] = x; });
 }
 
 // ---------------------------------------------------------------- OR-Set D2: key chunks sorted in LDS
@@ -2607,15 +2741,25 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
                                                           ctx->dev_status);
             return finish(nullptr);
         }
-        if (MODE == DD_OR && h.tw) {                    // two passes on the key's top 16 bits, then chunks in LDS
-            rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec, w.flags,
-                               vw);
-            if (rc) return rc;
+        if (MODE == DD_OR && h.tw) {                    // the key's top 16 bits grouped, then chunks in LDS
             const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
-            uint64_t *tmp = sorted == w.bufs ? w.bufs + n : w.bufs;
             const bool lb = g_or_lookback && (!g_rdd_diag || g_rdd_diag >= 5);   // (diag 5 / 6: the look-back form's timings)
+            const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
+            if (vec && g_or_bucket) {                   // tiles grouped by top byte, buckets gathered into chunks
+                k_lww_up_tiled<<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+                k_or_bucket<<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, n, w.flags, w.bufs + n, w.cb,
+                                                lb ? w.cst : nullptr, nch, ctx->dev_status);
+                sorted = w.bufs + n;
+            } else {                                    // two radix passes on the top 16 bits
+                rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec,
+                                   w.flags, vw);
+                if (rc) return rc;
+            }
+            uint64_t *tmp = sorted == w.bufs ? w.bufs + n : w.bufs;
             uint32_t *fbw = (uint32_t *)&w.flags[256];
-            k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, w.cb, lb ? w.cst : nullptr);
+            if (!(vec && g_or_bucket))
+                k_chunk_bounds<<<(nch + 1 + 3) / 4, 256, 0, s>>>(sorted, n, kb + kOcBits, nch, w.cb,
+                                                                  lb ? w.cst : nullptr);
             const bool narrow = kb <= 32 && g_or_narrow;
             const int kpair = g_or_pair && nch % 2 == 0 ? 2 : 1;
             const unsigned grid = nch / (unsigned)kpair;
