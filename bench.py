@@ -411,19 +411,20 @@ class SetMergeUnsorted(SetMerge):
     """configs[3] D2: both sides arrive UNSORTED; a step is ONE call of
     crdt_*_merge_unsorted over both sides together (a packed (key, ts, rep,
     side, tomb) composite, whose order is the stable merge of the sorted
-    sides).  On config D's dense keys the sort stops early: LWW after one
-    radix pass on the key's top byte, each key's winner kept in an LDS table
-    per bucket (k_lww_table); OR-Set after two passes on the top 16 key bits,
-    each 2^9-key chunk sorted and deduplicated in LDS (k_or_chunk); both
-    planned from a sample of the inputs.  Algorithmic bytes
+    sides).  On config D's dense keys no radix pass runs: the composing pass
+    groups each tile by the key's top byte (k_lww_up_tiled); LWW gathers each
+    byte's runs into an LDS table of per-key winners (k_lww_table_g), OR-Set
+    gathers them into 2^9-key chunk ranges (k_or_bucket), each chunk sorted
+    and deduplicated in LDS (k_or_chunk); both planned from a sample of the
+    inputs, launched from the context's cached plan.  Algorithmic bytes
     are those of the merge itself (inputs read once, output written once);
     the sort's passes are the price of unsorted input, so frac reads against
     that."""
 
     @property
     def kernel(self):
-        return ("k_sample_minmax + k_sort_up_vec + k_sort_pass + k_lww_table" if self.lww else
-                "k_sample_minmax + k_sort_up_vec + k_sort_up + 2 k_sort_pass + k_chunk_bounds + k_or_chunk")
+        return ("k_sample_minmax + k_plan_match + k_lww_up_tiled + k_lww_table_g" if self.lww else
+                "k_sample_minmax + k_plan_match + k_lww_up_tiled + k_or_bucket + k_or_chunk")
 
     def __init__(self, eng, rank, world, n, key_space, lww=True, seed=2024):
         self.eng, self.n, self.lww = eng, n, lww

@@ -31,7 +31,7 @@ for wl in $wls; do
     for v in $va $vb; do
       t=$O/${wl}_${v}_$p
       timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $t -o run -- \
-          python3 $R/bench.py --workload $wl --steps 10 --warmup 2 --no-e2e --no-cpu-baseline --option $knob=$v \
+          python3 $R/bench.py --workload $wl --steps 10 --warmup 2 --no-e2e --no-cpu-baseline --no-peaks --option $knob=$v \
           > $t.json 2> $t.err || { tail -3 $t.err; exit 1; }
       python3 - $t/run_kernel_stats.csv $t.json "$wl $knob=$v #$p" "$kre" <<'PY'
 import csv, json, re, sys

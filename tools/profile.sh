@@ -14,7 +14,7 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 "$ROOT/bench.py" --workload "$WL" --steps 20 --warmup 3 --no-cpu-baseline --no-e2e "$@" > "$OUT/bench_trace.json"
+    python3 "$ROOT/bench.py" --workload "$WL" --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-peaks "$@" > "$OUT/bench_trace.json"
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
     python3 "$ROOT/bench.py" --workload "$WL" --steps 5 --warmup 1 --no-cpu-baseline --no-e2e "$@" > "$OUT/bench_fetch.json"
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
