@@ -33,6 +33,7 @@ int g_plan_cache = 1;    // ... launched from the last such plan's shape, checke
 int g_rm_affine = 1;     // one-pair populations: RefMerge pair indices computed, no kv range loads (refmerge.affine_kv)
 int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
 int g_or_narrow = 1;
+int g_pop_direct = 1;    // population rounds: staging kernel + polled host bounds, no copy engine (pop.direct)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -342,6 +343,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_bucket")) {    // OR-Set D2: 1 tile groups + bucket gathers, 0 two radix passes
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_bucket = (int)v;
+    } else if (!strcmp(name, "pop.direct")) {        // population rounds: 1 staging kernel + polled host bounds, 0 copies + sync
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_pop_direct = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

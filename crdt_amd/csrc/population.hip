@@ -76,8 +76,11 @@ struct crdt_population {
     uint8_t *st_kind[2] = {nullptr, nullptr};  // CurrentState, double-buffered with the Diffs
     uint32_t *st_str[2] = {nullptr, nullptr};
     int64_t *st_sum[2] = {nullptr, nullptr};
-    void *pin = nullptr;                       // pinned staging (uploads, the end-of-round read-back)
+    void *pin = nullptr;                       // pinned staging (uploads, the end-of-round read-back; coherent)
+    void *pin_d = nullptr;                     // ... its device address (kernels read / write it directly)
     size_t pin_bytes = 0;
+    uint64_t *hflag = nullptr, *hflag_d = nullptr;   // the round's completion word (coherent host memory)
+    uint64_t seq = 0;                          // ... the value the current round's last kernel writes
     void *dsm = nullptr;                       // device staging of the per-replica arrays
     size_t dsm_bytes = 0;
     void *xb = nullptr;                        // sharded rounds: send and import buffers
@@ -119,15 +122,31 @@ int pin_grow(crdt_population *pop, size_t bytes) {
     hipError_t e = hipStreamSynchronize(pop->ctx->stream);
     if (e != hipSuccess) return hip_fail(pop->ctx, e);
     if (pop->pin) (void)hipHostFree(pop->pin);
-    pop->pin = nullptr;
+    pop->pin = pop->pin_d = nullptr;
     pop->pin_bytes = 0;
     const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
-    e = hipHostMalloc(&pop->pin, want, hipHostMallocDefault);
+    // coherent (fine-grained): the round's staging kernel reads it and the
+    // bounds kernel writes it directly, no copy-engine transfers
+    e = hipHostMalloc(&pop->pin, want, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&pop->pin_d, pop->pin, 0);
     if (e != hipSuccess) {
-        pop->pin = nullptr;
+        if (pop->pin) (void)hipHostFree(pop->pin);
+        pop->pin = pop->pin_d = nullptr;
         return hip_fail(pop->ctx, e);
     }
     pop->pin_bytes = want;
+    if (!pop->hflag) {
+        void *f = nullptr, *fd = nullptr;
+        e = hipHostMalloc(&f, 64, hipHostMallocCoherent | hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&fd, f, 0);
+        if (e != hipSuccess) {
+            if (f) (void)hipHostFree(f);
+            return hip_fail(pop->ctx, e);
+        }
+        pop->hflag = (uint64_t *)f;
+        pop->hflag_d = (uint64_t *)fd;
+        *(volatile uint64_t *)pop->hflag = 0;
+    }
     return CRDT_OK;
 }
 
@@ -231,6 +250,37 @@ __global__ void k_pop_bounds(const uint64_t *__restrict__ off, const uint64_t *_
 }
 
 
+// pop.direct (default 1): the round's per-replica arrays come from the
+// coherent pinned staging by this kernel (no copy-engine upload, no separate
+// status copy), and the end-of-round bounds go straight into it with a
+// completion word the host polls (no copy-engine read-back, no interrupt
+// wake-up).  Measured in DESIGN.md §5.8.
+__global__ void k_pop_stage(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst, size_t nw,
+                            const uint32_t *__restrict__ status, uint64_t *__restrict__ snap) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *snap = *status;
+}
+
+// as k_pop_bounds, one workgroup, into host memory; then the completion word
+// (system-scope release: the bounds are visible to the host before it)
+__global__ __launch_bounds__(256) void k_pop_bounds_host(const uint64_t *__restrict__ off,
+                                                         const uint64_t *__restrict__ kv_off, uint32_t P,
+                                                         const uint32_t *__restrict__ status,
+                                                         const uint64_t *__restrict__ snap, uint64_t *__restrict__ out,
+                                                         uint64_t *__restrict__ flag, uint64_t seq) {
+    for (uint32_t p = threadIdx.x; p <= P; p += 256) {
+        const uint64_t o = off[p];
+        out[p] = o;
+        out[P + 1 + p] = kv_off[o];
+    }
+    if (threadIdx.x == 0) {
+        out[2 * P + 2] = *status;
+        out[2 * P + 3] = *snap;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Per-replica arrays of one round's merge, one carve in both the device
 // staging and the pinned staging: r_off P | r_end P | bounds 2P + 4 (u64) |
 // slot delta P (u32) | skip P (u8).  bounds: the next Diffs' entry offsets
@@ -282,6 +332,13 @@ int upload_round(crdt_population *pop, const HostRound &h, RoundArrays *a) {
         memcpy(hp.skip, h.skip.data(), P);
     }
     const size_t upto = (size_t)((char *)(hp.skip + P) - (char *)pop->pin);
+    if (g_pop_direct) {
+        const size_t nw = (upto + 7) / 8;                // (the carve's slack covers the rounding)
+        k_pop_stage<<<grid_for(nw, 256, 64), 256, 0, pop->ctx->stream>>>((const uint64_t *)pop->pin_d,
+                                                                          (uint64_t *)pop->dsm, nw,
+                                                                          pop->ctx->dev_status, a->bounds + 2 * P + 3);
+        return check_launch(pop->ctx);
+    }
     hipError_t e = hipMemcpyAsync(pop->dsm, pop->pin, upto, hipMemcpyHostToDevice, pop->ctx->stream);
     // (8 bytes from the 256-byte status allocation: only the low word is compared)
     if (e == hipSuccess)
@@ -335,6 +392,12 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
         k_pop_keep_state<<<grid_for(ns, 256, (unsigned)ctx->num_cus * 4), 256, 0, ctx->stream>>>(
             a.skip, pop->K, ns, pop->st_kind[so], pop->st_str[so], pop->st_sum[so], pop->st_kind[sn],
             pop->st_str[sn], pop->st_sum[sn]);
+    if (g_pop_direct) {
+        pop->seq += 1;
+        k_pop_bounds_host<<<1, 256, 0, ctx->stream>>>(nd.off, nd.kv_off, P, ctx->dev_status, a.bounds + 2 * P + 3,
+                                                       carve_round(pop->pin_d, P).bounds, pop->hflag_d, pop->seq);
+        return check_launch(ctx);
+    }
     k_pop_bounds<<<grid_for(P + 1, 256, 64), 256, 0, ctx->stream>>>(nd.off, nd.kv_off, P, ctx->dev_status,
                                                                       a.bounds);
     rc = check_launch(ctx);
@@ -350,9 +413,22 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
 // (split in two so that a sharded round can check every member before it
 // swaps any in: all or nothing across the communicator's members)
 int pop_commit_check(crdt_population *pop) {
-    hipError_t e = hipStreamSynchronize(pop->ctx->stream);
-    if (e != hipSuccess) return hip_fail(pop->ctx, e);
     const uint32_t P = pop->P;
+    if (g_pop_direct && P) {
+        // poll the completion word; the stream's own state ends the wait when
+        // the round's kernels did not all run (a launch or device error)
+        const volatile uint64_t *f = pop->hflag;
+        while (*f != pop->seq) {
+            const hipError_t q = hipStreamQuery(pop->ctx->stream);
+            if (q == hipErrorNotReady) continue;
+            if (*f == pop->seq) break;
+            return hip_fail(pop->ctx, q == hipSuccess ? hipErrorUnknown : q);
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    } else {
+        hipError_t e = hipStreamSynchronize(pop->ctx->stream);
+        if (e != hipSuccess) return hip_fail(pop->ctx, e);
+    }
     if (P == 0) return CRDT_OK;
     const uint64_t *hb = carve_round(pop->pin, P).bounds;
     const uint32_t after = (uint32_t)hb[2 * P + 2], before = (uint32_t)hb[2 * P + 3];
@@ -487,6 +563,7 @@ extern "C" int crdt_population_destroy(crdt_population *pop) {
     for (void *p : {pop->dsm, pop->xb})
         if (p) (void)hipFree(p);
     if (pop->pin) (void)hipHostFree(pop->pin);
+    if (pop->hflag) (void)hipHostFree(pop->hflag);
     delete pop;
     return CRDT_OK;
 }
@@ -647,8 +724,8 @@ extern "C" int crdt_population_undo(crdt_population *pop) {
     if (!pop->can_undo) return CRDT_E_INVAL;
     int rc = bind(pop->ctx);
     if (rc) return rc;
-    hipError_t e = hipStreamSynchronize(pop->ctx->stream);
-    if (e != hipSuccess) return hip_fail(pop->ctx, e);
+    // (no synchronisation: the swap is host bookkeeping, and every later use of
+    // either buffer set is ordered behind the round on the population's stream)
     pop->cnt.swap(pop->pcnt);
     pop->kvcnt.swap(pop->pkvcnt);
     pop->n_e = pop->p_n_e;

@@ -627,7 +627,11 @@ int crdt_population_read(crdt_population *pop, uint64_t *l_off, int64_t *ts, uin
  * replica peers[i] (host array of P; == first + i: a self-pull, merge() runs
  * and rebuilds CurrentState, main.go:76; -1: dead).  The merge reads the
  * peers' Diffs in place (crdt_refmerge_batch_pull, key slots re-based, kv
- * pairs from its own passes); one upload, one read-back.  Synchronises. */
+ * pairs from its own passes).  The per-replica arrays go up through a
+ * staging kernel that reads them from coherent pinned memory, and the last
+ * kernel writes the next Diffs' bounds back into it with a completion word
+ * the call polls (no copy-engine transfers; option pop.direct = 0 restores
+ * hipMemcpyAsync + hipStreamSynchronize).  Returns once the round is done. */
 int crdt_population_round(crdt_population *pop, const int64_t *peers);
 /* POST /data on every replica at once (AddCommand, main.go:173-215, through
  * crdt_local_apply): replica p's commands c_off[p] .. c_off[p+1] in ARRIVAL
@@ -651,7 +655,8 @@ typedef struct crdt_population_cmds {
 int crdt_population_add_commands(crdt_population *pop, const crdt_population_cmds *cmds, uint16_t *status);
 /* Undo the last round (local or sharded): the Diffs and CurrentState as they
  * were before it -- they stay in the population's spare buffers until the
- * next round; CRDT_E_INVAL when there is nothing to undo. */
+ * next round; CRDT_E_INVAL when there is nothing to undo.  Host bookkeeping
+ * only (no synchronisation: later work is ordered on the population's stream). */
 int crdt_population_undo(crdt_population *pop);
 /* One round over a communicator (main.go:226-258 across GPUs): member i's
  * population (created on crdt_shard_member_ctx(comm, i)) holds global

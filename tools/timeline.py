@@ -2,13 +2,14 @@
 """Where a bench step's wall time goes, from a rocprofv3 run with
 --kernel-trace --memory-copy-trace --output-format csv:
 
-    python tools/timeline.py <dir with run_kernel_trace.csv [, run_memory_copy_trace.csv]> [steps]
+    python tools/timeline.py <dir with run_kernel_trace.csv [, run_memory_copy_trace.csv]> [steps] [--seq]
 
 Takes the last complete step (between the marker kernels bench.py launches
 under CRDT_TRACE_MARK=1; else about the last 1/steps of the trace), and prints
 its span, the time some kernel or copy was running (busy), the idle gaps,
 the number of kernels / copies, and the top kernels and copy kinds by total
-time in that window."""
+time in that window; --seq also lists the window's events in order (start
+offset, idle gap before it, duration, name)."""
 import collections
 import csv
 import os
@@ -28,8 +29,10 @@ def rows(path, kind):
 
 
 def main():
-    d = sys.argv[1]
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    args = [a for a in sys.argv[1:] if a != "--seq"]
+    seq = "--seq" in sys.argv
+    d = args[0]
+    steps = int(args[1]) if len(args) > 1 else 10
     ev = rows(os.path.join(d, "run_kernel_trace.csv"), "kernel") + rows(os.path.join(d, "run_memory_copy_trace.csv"),
                                                                          "copy")
     ev.sort()
@@ -66,6 +69,11 @@ def main():
           f"{nk} kernels, {nc} copies")
     for n, t in tot.most_common(25):
         print(f"  {t / 1e3:9.1f} us  x{cnt[n]:<5} {n[:90]}")
+    if seq:
+        prev_end = w0
+        for s, e, k, n in win:
+            print(f"  +{(s - w0) / 1e3:8.1f} us  gap {(s - prev_end) / 1e3:7.1f}  {(e - s) / 1e3:8.1f} us  {n[:80]}")
+            prev_end = max(prev_end, e)
 
 
 if __name__ == "__main__":
