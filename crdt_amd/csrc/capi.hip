@@ -34,6 +34,7 @@ int g_rm_affine = 1;     // one-pair populations: RefMerge pair indices computed
 int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
 int g_or_narrow = 1;
 int g_pop_direct = 1;    // population rounds: staging kernel + polled host bounds, no copy engine (pop.direct)
+int g_or_place_batch = 1;  // OR-Set D2 buckets: placement sorted per round in LDS, stored in pieces (sort.or_place_batch)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -321,9 +322,10 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v < 1 || v > 16) return CRDT_E_INVAL;
         g_mm_bpc = (int)v;
     } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: the D2 dedup apply (OR-Set: and count)
-        if (v < 0 || v > 6) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores);
+        if (v < 0 || v > 8) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores);
                                                         //   OR-Set chunks: 1 key counts, 2 LDS sort, 3 per-key tags, 4 long keys + ranks,
-                                                        //   5 all but the output stores, 6 no look-back (fake offsets)
+                                                        //   5 all but the output stores, 6 no look-back (fake offsets);
+                                                        //   OR-Set buckets: 7 no placement stores, 8 no placement sweep
         g_rdd_diag = (int)v;
     } else if (!strcmp(name, "sort.lww_table")) {    // LWW D2: 1 key-bucket LDS tables where they apply, 0 key-only sort
         if (v != 0 && v != 1) return CRDT_E_INVAL;
@@ -346,6 +348,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "pop.direct")) {        // population rounds: 1 staging kernel + polled host bounds, 0 copies + sync
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_pop_direct = (int)v;
+    } else if (!strcmp(name, "sort.or_place_batch")) {   // OR-Set D2 buckets: 1 placement batched in LDS, 0 one by one
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_place_batch = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

@@ -1421,13 +1421,17 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
 constexpr int OBB = 1024;                          // threads per bucket workgroup
 constexpr int OB_WAVES = OBB / 64;
 constexpr uint32_t kObSub = 256;                   // chunks per top-byte bucket at most (bk <= 25)
+constexpr uint32_t kObBatch = 4 * OB_WAVES * 4 * 32;   // a placement round's tuples at most (256 runs x 32)
 __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
                                                    const uint32_t *__restrict__ run, uint32_t ntiles, size_t n,
                                                    unsigned long long *__restrict__ flag, uint64_t *__restrict__ dst,
                                                    uint64_t *__restrict__ bounds, unsigned long long *__restrict__ cst,
-                                                   uint32_t nch, uint32_t *__restrict__ err) {
+                                                   uint32_t nch, uint32_t *__restrict__ err, int diag,
+                                                   bool place_batch) {
     __shared__ uint32_t s_run[kRunLds];
     __shared__ uint32_t s_h[OB_WAVES][kObSub];        // per-wave counts by sub-bucket, then the cursors (row 0)
+    __shared__ uint64_t s_buf[kObBatch];              // (batched placement) one round's tuples by sub-bucket
+    __shared__ uint32_t s_nb;
     __shared__ unsigned long long s_sum[3];
     const SortPlan p = *plan_;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1536,7 +1540,98 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
     __syncthreads();
     // 2. each tuple into its chunk's range of T's region (any order within it)
     uint64_t *out = dst + base;
-    sweep([&](uint64_t x) { out[atomicAdd(&s_h[0][(uint32_t)(x >> ssh) & (nsub - 1)], 1u)] = x; });
+    if (diag == 8) return;                            // (timing only: the chunk ranges left unfilled)
+    if (diag == 7) {                                  // (timing only: placement ranks, no stores)
+        sweep([&](uint64_t x) { atomicAdd(&s_h[0][(uint32_t)(x >> ssh) & (nsub - 1)], 1u); });
+        return;
+    }
+    if (!place_batch) {
+        sweep([&](uint64_t x) { out[atomicAdd(&s_h[0][(uint32_t)(x >> ssh) & (nsub - 1)], 1u)] = x; });
+        return;
+    }
+    // batched placement (sort.or_place_batch): a round's tuples (256 runs)
+    // ranked per sub-bucket in LDS (row 1 of s_h), the round's ranges
+    // reserved from the cursors (row 0) by one wave, the tuples sorted by
+    // sub-bucket in s_buf, then stored in order -- each sub-bucket's part one
+    // contiguous piece of its chunk range (one-by-one 8-B stores to 64
+    // ranges cost 65 of the pass's 153 us).  Row 2: the round's offsets in
+    // s_buf, row 3: its bases in the chunk ranges.  Tuples past 32 in a run
+    // (rare) are placed one by one from the cursors directly.  (Issuing the
+    // next round's loads before this round's stores: no faster.)
+    uint32_t *bc = s_h[1], *bo = s_h[2], *gb = s_h[3];
+    for (uint32_t i = tid; i < kObSub; i += OBB) bc[i] = 0;
+    __syncthreads();
+    auto load = [&](uint32_t t0, uint32_t *rn, const uint64_t **rp, uint64_t *x) {
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            const uint32_t t = t0 + g + NG * k;
+            rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
+            rp[k] = c + (size_t)t * ST + (rn[k] >> 16);
+            rn[k] &= 0xFFFFu;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            x[2 * k] = l < rn[k] ? rp[k][l] : 0;
+            x[2 * k + 1] = l + 16 < rn[k] ? rp[k][l + 16] : 0;
+        }
+    };
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += NG * KT) {
+        uint32_t rn[KT], rk[2 * KT];
+        const uint64_t *rp[KT];
+        uint64_t x[2 * KT];
+        load(t0, rn, rp, x);
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            if (l < rn[k]) rk[2 * k] = atomicAdd(&bc[(uint32_t)(x[2 * k] >> ssh) & (nsub - 1)], 1u);
+            if (l + 16 < rn[k]) rk[2 * k + 1] = atomicAdd(&bc[(uint32_t)(x[2 * k + 1] >> ssh) & (nsub - 1)], 1u);
+            for (uint32_t i = l + 32; i < rn[k]; i += 16) {   // (rare: runs over 32)
+                const uint64_t y = rp[k][i];
+                out[atomicAdd(&s_h[0][(uint32_t)(y >> ssh) & (nsub - 1)], 1u)] = y;
+            }
+        }
+        __syncthreads();
+        if (w == 0) {                                 // the round's counts -> offsets in s_buf, ranges reserved
+            uint32_t v[kObSub / 64], sum = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kObSub / 64; ++k) {
+                const uint32_t b = (uint32_t)lane * (kObSub / 64) + k;
+                v[k] = b < nsub ? bc[b] : 0u;
+                sum += v[k];
+            }
+            uint32_t y = sum;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(y, d, 64);
+                if (lane >= d) y += t;
+            }
+            uint32_t o = y - sum;
+#pragma unroll
+            for (uint32_t k = 0; k < kObSub / 64; ++k) {
+                const uint32_t b = (uint32_t)lane * (kObSub / 64) + k;
+                if (b < nsub) {
+                    bo[b] = o;
+                    gb[b] = s_h[0][b];
+                    s_h[0][b] += v[k];
+                    bc[b] = 0;
+                }
+                o += v[k];
+            }
+            if (lane == 63) s_nb = y;                 // the round's tuples
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            if (l < rn[k]) s_buf[bo[(uint32_t)(x[2 * k] >> ssh) & (nsub - 1)] + rk[2 * k]] = x[2 * k];
+            if (l + 16 < rn[k]) s_buf[bo[(uint32_t)(x[2 * k + 1] >> ssh) & (nsub - 1)] + rk[2 * k + 1]] = x[2 * k + 1];
+        }
+        __syncthreads();
+        const uint32_t nb = s_nb;
+        for (uint32_t i = tid; i < nb; i += OBB) {
+            const uint64_t y = s_buf[i];
+            const uint32_t b = (uint32_t)(y >> ssh) & (nsub - 1);
+            out[gb[b] + (i - bo[b])] = y;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- OR-Set D2: key chunks sorted in LDS
@@ -2748,7 +2843,8 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             if (vec && g_or_bucket) {                   // tiles grouped by top byte, buckets gathered into chunks
                 k_lww_up_tiled<<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
                 k_or_bucket<<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, n, w.flags, w.bufs + n, w.cb,
-                                                lb ? w.cst : nullptr, nch, ctx->dev_status);
+                                                lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
+                                                g_or_place_batch != 0);
                 sorted = w.bufs + n;
             } else {                                    // two radix passes on the top 16 bits
                 rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec,
