@@ -2757,13 +2757,23 @@ __global__ void k_d2_check(const uint32_t *__restrict__ viol, const uint32_t *__
 }
 
 // The fresh (sampled) plan against the cached one the host launched from:
-// any difference in the launch shape raises the range check (a miss).
-__global__ void k_plan_match(const SortPlan *__restrict__ fresh, SortPlan c, uint32_t *__restrict__ viol) {
+// any difference in the launch shape raises the range check (a miss) AND
+// puts the cached shape into the device plan, so the passes launched on the
+// cached grids index their tables, buckets and chunks by the shape those
+// grids were sized for (the fresh plan's own shape -- e.g. a sample that
+// caught a far key: 41 key bits -- would send the bucket pass past its 256
+// sub-buckets and the chunk bounds).  The call's own fields (side pointer,
+// n1, the range minima) stay; the output is discarded and the call redone.
+__global__ void k_plan_match(SortPlan *__restrict__ fresh, SortPlan c, uint32_t *__restrict__ viol) {
     if (threadIdx.x != 0) return;
-    const SortPlan f = *fresh;
+    SortPlan f = *fresh;
     if (f.words != c.words || f.P != c.P || f.s0 != c.s0 || f.tl != c.tl || f.tw != c.tw || f.bk != c.bk ||
-        f.bt != c.bt || f.br != c.br || f.b0 != c.b0 || f.W != c.W)
+        f.bt != c.bt || f.br != c.br || f.b0 != c.b0 || f.W != c.W) {
+        f.words = c.words, f.P = c.P, f.s0 = c.s0, f.tl = c.tl, f.tw = c.tw;
+        f.bk = c.bk, f.bt = c.bt, f.br = c.br, f.b0 = c.b0, f.W = c.W;
+        *fresh = f;
         *viol = 1;
+    }
 }
 static_assert(sizeof(SortPlan) <= sizeof(((crdt_ctx *)nullptr)->d2_plan[0]), "the context caches a plan per mode");
 
