@@ -35,6 +35,7 @@ int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped 
 int g_or_narrow = 1;
 int g_pop_direct = 1;    // population rounds: staging kernel + polled host bounds, no copy engine (pop.direct)
 int g_or_place_batch = 1;  // OR-Set D2 buckets: placement sorted per round in LDS, stored in pieces (sort.or_place_batch)
+int g_up_threads = 512;  // D2 tile grouping pass: threads per 4096-tuple tile, 256 or 512 (sort.up_threads)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -351,6 +352,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_place_batch")) {   // OR-Set D2 buckets: 1 placement batched in LDS, 0 one by one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_place_batch = (int)v;
+    } else if (!strcmp(name, "sort.up_threads")) {   // D2 tile grouping pass: 256 / 512 threads per 4096-tuple tile
+        if (v != 256 && v != 512) return CRDT_E_INVAL;
+        g_up_threads = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

@@ -1213,29 +1213,31 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 // workgroup then gathers its ~16-composite run from every tile -- 16 lanes
 // per run, four runs per wave-instruction, so every load is a contiguous
 // 128-B piece -- into its LDS table.  No scatter pass, no column scan.
-__global__ __launch_bounds__(SB) void k_lww_up_tiled(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
+template <int UB>
+__global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                      uint32_t ntiles, uint32_t *__restrict__ run,
                                                      uint64_t *__restrict__ comp, uint32_t *__restrict__ viol,
                                                      unsigned long long *__restrict__ zero) {
+    constexpr int UR = ST / UB;                       // composites per thread
     __shared__ uint32_t h[256], hs[256];
     __shared__ uint64_t stage[ST];
     const int tid = threadIdx.x;
-    h[tid] = 0;
-    if (zero && blockIdx.x == 0) {                    // the buckets' flags (k_lww_table_g, k_or_bucket), the
+    if (tid < 256) h[tid] = 0;
+    if (zero && blockIdx.x == 0 && tid < 256) {       // the buckets' flags (k_lww_table_g, k_or_bucket), the
         zero[tid] = 0;                                //   OR-Set chunks' fallback word
         if (tid == 0) zero[256] = 0;
     }
     const SortPlan p = *plan_;
     const size_t base = (size_t)blockIdx.x * ST;
-    uint64_t c[SR];
+    uint64_t c[UR];
     uint32_t vm = 0;                                  // bit r: c[r] holds a tuple (e < n)
     bool bad = false;                                 // (viol) a field outside the plan's ranges
     auto out_of = [&](uint64_t k, uint64_t t, uint32_t r) {
         return outside(k - p.kmin, p.bk) || outside(t - p.tmin, p.bt) || outside((uint64_t)r - p.rmin, p.br);
     };
 #pragma unroll
-    for (int r = 0; r < SR / 2; ++r) {               // two tuples per lane per round (16-B key / ts loads)
-        const size_t e = base + 2 * ((size_t)r * SB + tid);
+    for (int r = 0; r < UR / 2; ++r) {               // two tuples per lane per round (16-B key / ts loads)
+        const size_t e = base + 2 * ((size_t)r * UB + tid);
         c[2 * r] = c[2 * r + 1] = 0;
         if (e >= n) continue;
         vm |= (e + 1 < n ? 3u : 1u) << (2 * r);
@@ -1257,27 +1259,42 @@ __global__ __launch_bounds__(SB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
     if (viol && __ballot(bad) && (tid & 63) == 0) atomicOr(viol, 1u);
     __syncthreads();
     const uint32_t sh = p.W - 8;                      // the bucket: the composite's (the key's) top byte
-    uint32_t d[SR];
+    uint32_t d[UR];
 #pragma unroll
-    for (int r = 0; r < SR; ++r) {
+    for (int r = 0; r < UR; ++r) {
         d[r] = ((vm >> r) & 1u) ? (uint32_t)(c[r] >> sh) & 255u : 256u;
         if (d[r] < 256) atomicAdd(&h[d[r]], 1u);
     }
     __syncthreads();
-    {                                                 // exclusive scan of the 256 bucket counts
-        const uint32_t v = h[tid];
-        uint64_t all;
-        const uint32_t ex = (uint32_t)block_exclusive_scan_u64(v, &all);
-        hs[tid] = ex;
-        run[(size_t)tid * ntiles + blockIdx.x] = ex << 16 | v;   // (bucket, tile) run: start | count (<= 4096 each)
+    if (tid < 64) {                                   // exclusive scan of the 256 bucket counts (wave 0, 4 per lane)
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = h[tid * 4 + k];
+            sum += v[k];
+        }
+        uint32_t y = sum;
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t t = __shfl_up(y, dd, 64);
+            if (tid >= dd) y += t;
+        }
+        uint32_t ex = y - sum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = (uint32_t)tid * 4 + k;
+            hs[b] = ex;
+            run[(size_t)b * ntiles + blockIdx.x] = ex << 16 | v[k];   // (bucket, tile) run: start | count (<= 4096 each)
+            ex += v[k];
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < SR; ++r)
+    for (int r = 0; r < UR; ++r)
         if (d[r] < 256) stage[atomicAdd(&hs[d[r]], 1u)] = c[r];
     __syncthreads();
     const uint32_t m = n - base < (size_t)ST ? (uint32_t)(n - base) : (uint32_t)ST;
-    for (uint32_t i = 2 * tid; i < m; i += 2 * SB) {   // the tile, bucket by bucket (16-B stores)
+    for (uint32_t i = 2 * tid; i < m; i += 2 * UB) {   // the tile, bucket by bucket (16-B stores)
         if (i + 1 < m) *(ulonglong2 *)(comp + base + i) = ulonglong2{stage[i], stage[i + 1]};
         else comp[base + i] = stage[i];
     }
@@ -2825,7 +2842,8 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
     if (h.words == 1) {
         if (MODE == DD_LWW && h.tw && vec && g_lww_gather) {   // tiles grouped by bucket, tables gather their runs
             const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
-            k_lww_up_tiled<<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+            if (g_up_threads == 512) k_lww_up_tiled<512><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+            else k_lww_up_tiled<SB><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
             if (h.tw == 4)
                 k_lww_table_g<uint32_t><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count,
                                                             ctx->dev_status);
@@ -2851,7 +2869,10 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             const bool lb = g_or_lookback && (!g_rdd_diag || g_rdd_diag >= 5);   // (diag 5 / 6: the look-back form's timings)
             const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
             if (vec && g_or_bucket) {                   // tiles grouped by top byte, buckets gathered into chunks
-                k_lww_up_tiled<<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+                if (g_up_threads == 512)
+                    k_lww_up_tiled<512><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+                else
+                    k_lww_up_tiled<SB><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
                 k_or_bucket<<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, n, w.flags, w.bufs + n, w.cb,
                                                 lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
                                                 g_or_place_batch != 0);
