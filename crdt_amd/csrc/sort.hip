@@ -300,12 +300,12 @@ __global__ __launch_bounds__(256) void k_sort_plan(const SortMinMax *mms, uint32
             p.P = 1;
         }
     }
-    // OR-Set key chunks (k_or_chunk): two passes on the key's top 16 bits,
-    // then chunks of 2^10 keys sorted in LDS -- where the sorted prefix fixes
-    // the chunk (bk <= 26) and chunks hold <= 3072 tuples on average (config
-    // D: 2.4k; the LDS holds 4096)
+    // OR-Set key chunks (k_or_chunk): the key's top bits grouped, then
+    // chunks of 2^9 keys sorted in LDS -- where the grouped prefix fixes the
+    // chunk (bk <= 25) and chunks hold <= 1280 tuples on average (config D:
+    // 1.2k; the LDS holds 1536 -- sized for four workgroups per CU)
     if (or_table && key_only != 1 && p.words == 1 && p.bk >= 16 && p.bk <= 16 + 9 &&
-        n_all <= (1536ull << (p.bk - 9))) {
+        n_all <= (1280ull << (p.bk - 9))) {
         p.tw = 4;
         p.tl = 9;
         p.s0 = p.W - 16;
@@ -1681,11 +1681,11 @@ constexpr int OCB = 512;                 // threads per chunk workgroup
 constexpr int OC_WAVES = OCB / 64;
 constexpr uint32_t kOcBits = 9;          // keys per chunk: 2^9
 constexpr uint32_t kOcKeys = 1u << kOcBits;
-constexpr uint32_t kOcCap = 2048;        // tuples per chunk (LDS); more -> fallback
+constexpr uint32_t kOcCap = 1536;        // tuples per chunk (LDS); more -> fallback
 constexpr uint32_t kOcPer = kOcCap / OCB;
 constexpr uint32_t kOtRun = 8;           // keys of up to this many tuples: one thread, registers
 constexpr uint32_t kOtMid = 32;          // up to this many: one thread, an insertion sort of its slots in LDS
-constexpr uint32_t kOcLong = 256;        // longer keys per chunk (LDS list); more -> the workgroup loops
+constexpr uint32_t kOcLong = 64;         // longer keys per chunk (LDS list); more -> fallback
 
 // a key's <= kOtRun tuples sorted in registers (Batcher's 19-comparator
 // network; unused slots hold ~0 and sort last), so its distinct tags are the
