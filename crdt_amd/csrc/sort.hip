@@ -1213,14 +1213,15 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 // workgroup then gathers its ~16-composite run from every tile -- 16 lanes
 // per run, four runs per wave-instruction, so every load is a contiguous
 // 128-B piece -- into its LDS table.  No scatter pass, no column scan.
-template <int UB>
+template <int UB, int TILE>
 __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                      uint32_t ntiles, uint32_t *__restrict__ run,
                                                      uint64_t *__restrict__ comp, uint32_t *__restrict__ viol,
                                                      unsigned long long *__restrict__ zero) {
-    constexpr int UR = ST / UB;                       // composites per thread
+    constexpr int UR = TILE / UB;                     // composites per thread
+    static_assert(TILE < 65536, "16-bit run starts and counts");
     __shared__ uint32_t h[256], hs[256];
-    __shared__ uint64_t stage[ST];
+    __shared__ uint64_t stage[TILE];
     const int tid = threadIdx.x;
     if (tid < 256) h[tid] = 0;
     if (zero && blockIdx.x == 0 && tid < 256) {       // the buckets' flags (k_lww_table_g, k_or_bucket), the
@@ -1228,7 +1229,7 @@ __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
         if (tid == 0) zero[256] = 0;
     }
     const SortPlan p = *plan_;
-    const size_t base = (size_t)blockIdx.x * ST;
+    const size_t base = (size_t)blockIdx.x * TILE;
     uint64_t c[UR];
     uint32_t vm = 0;                                  // bit r: c[r] holds a tuple (e < n)
     bool bad = false;                                 // (viol) a field outside the plan's ranges
@@ -1293,15 +1294,15 @@ __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
     for (int r = 0; r < UR; ++r)
         if (d[r] < 256) stage[atomicAdd(&hs[d[r]], 1u)] = c[r];
     __syncthreads();
-    const uint32_t m = n - base < (size_t)ST ? (uint32_t)(n - base) : (uint32_t)ST;
+    const uint32_t m = n - base < (size_t)TILE ? (uint32_t)(n - base) : (uint32_t)TILE;
     for (uint32_t i = 2 * tid; i < m; i += 2 * UB) {   // the tile, bucket by bucket (16-B stores)
         if (i + 1 < m) *(ulonglong2 *)(comp + base + i) = ulonglong2{stage[i], stage[i + 1]};
         else comp[base + i] = stage[i];
     }
 }
 
-constexpr uint32_t kRunLds = 6144;                 // (bucket, tile) runs staged in LDS (24 KB; config D: 4883)
-template <typename E>
+constexpr uint32_t kRunLds = 6144;                 // (bucket, tile) runs staged in LDS (24 KB; config D: 2442 tiles of 8192)
+template <typename E, uint32_t GL>
 __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
                                                      const uint32_t *__restrict__ run, uint32_t ntiles,
                                                      unsigned long long *__restrict__ flag, crdt_tuples out,
@@ -1326,9 +1327,11 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
         for (uint32_t i = tid; i < ntiles; i += LTB) s_run[i] = rg[i];
     __syncthreads();
     // lane group g (16 lanes) takes KT tiles per iteration, t = t0 + g +
-    // 64 k, its lanes elements l and l + 16 of each run: 2 KT loads in
+    // 64 k, its lanes elements l + 16 j (j < GL) of each run: 8 loads in
     // flight per lane, every load instruction four contiguous 128-B pieces
-    constexpr uint32_t KT = 4, NG = 4 * LT_WAVES;     // tiles per group per iteration, lane groups
+    // (GL = 2: 4096-tuple tiles, runs of ~16; GL = 4: 8192, runs of ~32)
+    constexpr uint32_t KT = 8 / GL, NG = 4 * LT_WAVES;  // tiles per group per iteration, lane groups
+    constexpr uint32_t TILE = 2048 * GL;
     const uint32_t g = (uint32_t)tid >> 4, l = (uint32_t)lane & 15;
     auto put = [&](uint64_t x) { atomicMax(&tab[(uint32_t)(x >> kb) & (ne - 1)], ((E)(x ^ 3u) & tmask) | marker); };
     for (uint32_t t0 = 0; t0 < ntiles; t0 += NG * KT) {
@@ -1338,20 +1341,20 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
         for (uint32_t k = 0; k < KT; ++k) {
             const uint32_t t = t0 + g + NG * k;
             rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
-            rp[k] = c + (size_t)t * ST + (rn[k] >> 16);
+            rp[k] = c + (size_t)t * TILE + (rn[k] >> 16);
             rn[k] &= 0xFFFFu;
         }
-        uint64_t x[2 * KT];
+        uint64_t x[GL * KT];
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k)
+#pragma unroll
+            for (uint32_t j = 0; j < GL; ++j) x[GL * k + j] = l + 16 * j < rn[k] ? rp[k][l + 16 * j] : 0;
 #pragma unroll
         for (uint32_t k = 0; k < KT; ++k) {
-            x[2 * k] = l < rn[k] ? rp[k][l] : 0;
-            x[2 * k + 1] = l + 16 < rn[k] ? rp[k][l + 16] : 0;
-        }
 #pragma unroll
-        for (uint32_t k = 0; k < KT; ++k) {
-            if (l < rn[k]) put(x[2 * k]);
-            if (l + 16 < rn[k]) put(x[2 * k + 1]);
-            for (uint32_t i = l + 32; i < rn[k]; i += 16) put(rp[k][i]);   // (rare: runs over 32)
+            for (uint32_t j = 0; j < GL; ++j)
+                if (l + 16 * j < rn[k]) put(x[GL * k + j]);
+            for (uint32_t i = l + 16 * GL; i < rn[k]; i += 16) put(rp[k][i]);   // (rare: longer runs)
         }
     }
     __syncthreads();
@@ -1438,7 +1441,8 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
 constexpr int OBB = 1024;                          // threads per bucket workgroup
 constexpr int OB_WAVES = OBB / 64;
 constexpr uint32_t kObSub = 256;                   // chunks per top-byte bucket at most (bk <= 25)
-constexpr uint32_t kObBatch = 4 * OB_WAVES * 4 * 32;   // a placement round's tuples at most (256 runs x 32)
+constexpr uint32_t kObBatch = 4 * OB_WAVES * 8 * 16;   // a placement round's tuples at most (8 loads x 16 lanes per group)
+template <uint32_t GL>
 __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
                                                    const uint32_t *__restrict__ run, uint32_t ntiles, size_t n,
                                                    unsigned long long *__restrict__ flag, uint64_t *__restrict__ dst,
@@ -1471,31 +1475,35 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
     if (lane == 0 && tot) atomicAdd(&s_sum[2], tot);
     __syncthreads();
     if (tid == 0) __hip_atomic_store(&flag[T], kLtReady | s_sum[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // gather the runs (as k_lww_table_g: 16-lane groups, KT tiles each per round, 2 elements per lane per tile)
-    constexpr uint32_t KT = 4, NG = 4 * OB_WAVES;
+    // gather the runs (as k_lww_table_g: 16-lane groups, KT tiles each per round, GL elements per lane per tile)
+    constexpr uint32_t KT = 8 / GL, NG = 4 * OB_WAVES;
+    constexpr uint32_t TILE = 2048 * GL;
     const uint32_t g = (uint32_t)tid >> 4, l = (uint32_t)lane & 15;
+    auto load = [&](uint32_t t0, uint32_t *rn, const uint64_t **rp, uint64_t *x) {
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k) {
+            const uint32_t t = t0 + g + NG * k;
+            rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
+            rp[k] = c + (size_t)t * TILE + (rn[k] >> 16);
+            rn[k] &= 0xFFFFu;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KT; ++k)
+#pragma unroll
+            for (uint32_t j = 0; j < GL; ++j) x[GL * k + j] = l + 16 * j < rn[k] ? rp[k][l + 16 * j] : 0;
+    };
     auto sweep = [&](auto &&put) {
         for (uint32_t t0 = 0; t0 < ntiles; t0 += NG * KT) {
             uint32_t rn[KT];
             const uint64_t *rp[KT];
+            uint64_t x[GL * KT];
+            load(t0, rn, rp, x);
 #pragma unroll
             for (uint32_t k = 0; k < KT; ++k) {
-                const uint32_t t = t0 + g + NG * k;
-                rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
-                rp[k] = c + (size_t)t * ST + (rn[k] >> 16);
-                rn[k] &= 0xFFFFu;
-            }
-            uint64_t x[2 * KT];
 #pragma unroll
-            for (uint32_t k = 0; k < KT; ++k) {
-                x[2 * k] = l < rn[k] ? rp[k][l] : 0;
-                x[2 * k + 1] = l + 16 < rn[k] ? rp[k][l + 16] : 0;
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < KT; ++k) {
-                if (l < rn[k]) put(x[2 * k]);
-                if (l + 16 < rn[k]) put(x[2 * k + 1]);
-                for (uint32_t i = l + 32; i < rn[k]; i += 16) put(rp[k][i]);   // (rare: runs over 32)
+                for (uint32_t j = 0; j < GL; ++j)
+                    if (l + 16 * j < rn[k]) put(x[GL * k + j]);
+                for (uint32_t i = l + 16 * GL; i < rn[k]; i += 16) put(rp[k][i]);   // (rare: longer runs)
             }
         }
     };
@@ -1578,30 +1586,17 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
     uint32_t *bc = s_h[1], *bo = s_h[2], *gb = s_h[3];
     for (uint32_t i = tid; i < kObSub; i += OBB) bc[i] = 0;
     __syncthreads();
-    auto load = [&](uint32_t t0, uint32_t *rn, const uint64_t **rp, uint64_t *x) {
-#pragma unroll
-        for (uint32_t k = 0; k < KT; ++k) {
-            const uint32_t t = t0 + g + NG * k;
-            rn[k] = t < ntiles ? (lds ? s_run[t] : rg[t]) : 0u;
-            rp[k] = c + (size_t)t * ST + (rn[k] >> 16);
-            rn[k] &= 0xFFFFu;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < KT; ++k) {
-            x[2 * k] = l < rn[k] ? rp[k][l] : 0;
-            x[2 * k + 1] = l + 16 < rn[k] ? rp[k][l + 16] : 0;
-        }
-    };
     for (uint32_t t0 = 0; t0 < ntiles; t0 += NG * KT) {
-        uint32_t rn[KT], rk[2 * KT];
+        uint32_t rn[KT], rk[GL * KT];
         const uint64_t *rp[KT];
-        uint64_t x[2 * KT];
+        uint64_t x[GL * KT];
         load(t0, rn, rp, x);
 #pragma unroll
         for (uint32_t k = 0; k < KT; ++k) {
-            if (l < rn[k]) rk[2 * k] = atomicAdd(&bc[(uint32_t)(x[2 * k] >> ssh) & (nsub - 1)], 1u);
-            if (l + 16 < rn[k]) rk[2 * k + 1] = atomicAdd(&bc[(uint32_t)(x[2 * k + 1] >> ssh) & (nsub - 1)], 1u);
-            for (uint32_t i = l + 32; i < rn[k]; i += 16) {   // (rare: runs over 32)
+#pragma unroll
+            for (uint32_t j = 0; j < GL; ++j)
+                if (l + 16 * j < rn[k]) rk[GL * k + j] = atomicAdd(&bc[(uint32_t)(x[GL * k + j] >> ssh) & (nsub - 1)], 1u);
+            for (uint32_t i = l + 16 * GL; i < rn[k]; i += 16) {   // (rare: longer runs)
                 const uint64_t y = rp[k][i];
                 out[atomicAdd(&s_h[0][(uint32_t)(y >> ssh) & (nsub - 1)], 1u)] = y;
             }
@@ -1637,10 +1632,11 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t k = 0; k < KT; ++k) {
-            if (l < rn[k]) s_buf[bo[(uint32_t)(x[2 * k] >> ssh) & (nsub - 1)] + rk[2 * k]] = x[2 * k];
-            if (l + 16 < rn[k]) s_buf[bo[(uint32_t)(x[2 * k + 1] >> ssh) & (nsub - 1)] + rk[2 * k + 1]] = x[2 * k + 1];
-        }
+        for (uint32_t k = 0; k < KT; ++k)
+#pragma unroll
+            for (uint32_t j = 0; j < GL; ++j)
+                if (l + 16 * j < rn[k])
+                    s_buf[bo[(uint32_t)(x[GL * k + j] >> ssh) & (nsub - 1)] + rk[GL * k + j]] = x[GL * k + j];
         __syncthreads();
         const uint32_t nb = s_nb;
         for (uint32_t i = tid; i < nb; i += OBB) {
@@ -2802,6 +2798,21 @@ static bool d2_vec(const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t
     return vec_ok(A, na) && vec_ok(B, nb) && na % 2 == 0 && g_sort_vec_up;
 }
 
+// The tile grouping pass of the gather forms (k_lww_up_tiled): tiles of
+// sort.group_tile tuples (4096 or 8192) grouped by the key's top byte;
+// returns the tile count.
+static unsigned group_tiles(hipStream_t s, const crdt_tuples &A, size_t n, const D2Ws &w, uint32_t *vw) {
+    const unsigned tile = g_group_tile == 8192 ? 8192u : 4096u;
+    const unsigned ntiles = (unsigned)((n + tile - 1) / tile);
+    if (tile == 8192)
+        k_lww_up_tiled<1024, 8192><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+    else if (g_up_threads == 512)
+        k_lww_up_tiled<512, ST><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+    else
+        k_lww_up_tiled<SB, ST><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+    return ntiles;
+}
+
 // The passes of a D2 merge whose plan h is known on the host (w.plan holds
 // it on the device).  vw: the range check of a sampled or given plan
 // (nullptr: the plan is exact for these inputs).
@@ -2841,15 +2852,17 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
     int rc;
     if (h.words == 1) {
         if (MODE == DD_LWW && h.tw && vec && g_lww_gather) {   // tiles grouped by bucket, tables gather their runs
-            const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
-            if (g_up_threads == 512) k_lww_up_tiled<512><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
-            else k_lww_up_tiled<SB><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
-            if (h.tw == 4)
-                k_lww_table_g<uint32_t><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count,
-                                                            ctx->dev_status);
-            else
-                k_lww_table_g<uint64_t><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count,
-                                                            ctx->dev_status);
+            const unsigned ntiles = group_tiles(s, A, n, w, vw);
+#define LWW_G(E, GLV) \
+    k_lww_table_g<E, GLV><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count, ctx->dev_status)
+            if (h.tw == 4) {
+                if (g_group_tile == 8192) LWW_G(uint32_t, 4);
+                else LWW_G(uint32_t, 2);
+            } else {
+                if (g_group_tile == 8192) LWW_G(uint64_t, 4);
+                else LWW_G(uint64_t, 2);
+            }
+#undef LWW_G
             return finish(nullptr);
         }
         if (MODE == DD_LWW && h.tw) {                   // one pass on the key's top byte, then bucket tables
@@ -2869,13 +2882,15 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             const bool lb = g_or_lookback && (!g_rdd_diag || g_rdd_diag >= 5);   // (diag 5 / 6: the look-back form's timings)
             const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
             if (vec && g_or_bucket) {                   // tiles grouped by top byte, buckets gathered into chunks
-                if (g_up_threads == 512)
-                    k_lww_up_tiled<512><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+                const unsigned gt = group_tiles(s, A, n, w, vw);
+                if (g_group_tile == 8192)
+                    k_or_bucket<4><<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, gt, n, w.flags, w.bufs + n, w.cb,
+                                                       lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
+                                                       g_or_place_batch != 0);
                 else
-                    k_lww_up_tiled<SB><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
-                k_or_bucket<<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, n, w.flags, w.bufs + n, w.cb,
-                                                lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
-                                                g_or_place_batch != 0);
+                    k_or_bucket<2><<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, gt, n, w.flags, w.bufs + n, w.cb,
+                                                       lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
+                                                       g_or_place_batch != 0);
                 sorted = w.bufs + n;
             } else {                                    // two radix passes on the top 16 bits
                 rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec,
