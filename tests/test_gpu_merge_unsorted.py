@@ -164,8 +164,8 @@ def test_unsorted_lww_key_tables(eng, kbits, tbits):
     """LWW D2 by key-bucket LDS tables (sort.lww_table; taken when the key
     offsets span 12..23 bits with tags of <= 31 bits, 12..22 bits with wider
     tags; 11 / 24 key bits and 23 bits with wide tags keep the key-only
-    sort) and OR-Set D2 by key chunks sorted in LDS (sort.or_table; 16..26
-    key bits, <= 3072 tuples per 2^10-key chunk on average): with both on and off == the
+    sort) and OR-Set D2 by key chunks sorted in LDS (sort.or_table; 16..25
+    key bits, <= 1280 tuples per 2^9-key chunk on average): with both on and off == the
     oracle.  Keys offset far from 0 and spanning their full width, 80 % of
     the tuples in one key bucket, cross-side equal tags with differing
     tombs, one side shorter."""
@@ -213,10 +213,11 @@ def _keyed(rng, keys, tbits=6):
 @pytest.mark.parametrize("case", ["long_keys", "key_of_2000", "too_many_long_keys", "chunk_over_cap"])
 def test_unsorted_orset_tables_long_keys(eng, case):
     """OR-Set key chunks sorted in LDS around their limits (20 key bits:
-    1024 chunks of 2^10 keys): keys of 9..60 tuples (the workgroup's long-key
-    path, few ts values so tags repeat within a key), a key of 2000 tuples,
-    300 keys of 9 tuples in one chunk (over the 256 long keys a chunk lists)
-    and one chunk of 9000+ tuples (over its 4096 in LDS): the last two fall
+    2048 chunks of 2^9 keys, 1536 tuples and 64 keys of over 32 tuples per
+    chunk in LDS): keys of 9..60 tuples (the insertion-sorted and the
+    workgroup's long-key paths, few ts values so tags repeat within a key), a
+    key of 2000 tuples, 300 keys of 9 tuples in one chunk and one chunk of
+    9000+ tuples: the last three chunks are over the LDS capacity and fall
     back to the radix sort.  All == the oracle: chunks with look-back
     offsets, chunks with the scan + emit pass, and the radix path."""
     from crdt_amd import _lib
