@@ -11,8 +11,8 @@
 namespace crdt {
 JoinTuning g_join;
 FoldTuning g_fold;
-int g_vclock_pairs_per_wave = 8;   // tools/tune_vclock.py at 10M x 128: 8 x 1 block/CU 6.50 TB/s
-int g_vclock_blocks_per_cu = 1;    //   against 6.19 TB/s for 4 x 8
+int g_vclock_pairs_per_wave = 32;  // 10M x 128, one block/CU: 32 pairs 0.858-0.860 of 8 TB/s, 16 0.852-0.854,
+int g_vclock_blocks_per_cu = 1;    //   8 0.833 (profiles/r05/ab/vclock_*.txt; 4 x 8 blocks/CU: 6.19 TB/s)
 int g_lww_chunk = 0;      // LWW tiles per chunk, 0 = one chunk (chunked schedules measured slower: DESIGN.md §5.4)
 int g_or_chunk = 0;       // OR-Set tiles per chunk (likewise)
 int g_set_streams = 1;
@@ -285,7 +285,7 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v < 1 || v > 64) return CRDT_E_INVAL;
         g_join.blocks_per_cu = (int)v;
     } else if (!strcmp(name, "fold.unroll")) {
-        if (v != 1 && v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
+        if (v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32) return CRDT_E_INVAL;
         g_fold.unroll = (int)v;
     } else if (!strcmp(name, "fold.nontemporal")) {
         if (v != 0 && v != 1) return CRDT_E_INVAL;
@@ -294,7 +294,7 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v < 1 || v > 64) return CRDT_E_INVAL;
         g_fold.blocks_per_cu = (int)v;
     } else if (!strcmp(name, "vclock.pairs_per_wave")) {
-        if (v != 1 && v != 2 && v != 4 && v != 8) return CRDT_E_INVAL;
+        if (v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32) return CRDT_E_INVAL;
         g_vclock_pairs_per_wave = (int)v;
     } else if (!strcmp(name, "vclock.blocks_per_cu")) {
         if (v < 1 || v > 64) return CRDT_E_INVAL;

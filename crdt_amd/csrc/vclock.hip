@@ -9,8 +9,10 @@
 // Layout: a, b row-major [pairs x nodes].  A pair's row is spread over
 // NODES/2 lanes (16 B per lane), so one wave-load of a 128-node clock is the
 // whole 1 KiB row; the "for all" is a 64-bit wave ballot.  U pairs-groups
-// are loaded before any is reduced, so each lane keeps 2*U 16-B loads in
-// flight.  HBM-bound: 2 * nodes * 8 + 1 bytes per pair.
+// are loaded before any is reduced (all of a's rows, then all of b's), so
+// each lane keeps 2*U 16-B loads in flight -- at U = 32 (the default) 256
+// VGPRs, one wave per SIMD and 256 KiB in flight per CU.  HBM-bound:
+// 2 * nodes * 8 + 1 bytes per pair.
 #include "common.hpp"
 
 namespace crdt {
@@ -34,16 +36,17 @@ __global__ __launch_bounds__(256) void k_vclock(const u64x2 *__restrict__ a, con
     const size_t nwaves = ((size_t)gridDim.x * 256) >> 6;
     for (size_t p0 = wave * PPW; p0 < pairs; p0 += nwaves * PPW) {
         u64x2 x[U], y[U];
+        // all of a's rows, then all of b's: each operand's U rows (U KiB at
+        // 128 nodes) one contiguous burst
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t p = p0 + (size_t)u * PPL + sub;
-            if (p < pairs) {
-                x[u] = __builtin_nontemporal_load(a + p * LPR + col);
-                y[u] = __builtin_nontemporal_load(b + p * LPR + col);
-            } else {
-                x[u] = (u64x2){0, 0};
-                y[u] = (u64x2){0, 0};
-            }
+            x[u] = p < pairs ? __builtin_nontemporal_load(a + p * LPR + col) : (u64x2){0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t p = p0 + (size_t)u * PPL + sub;
+            y[u] = p < pairs ? __builtin_nontemporal_load(b + p * LPR + col) : (u64x2){0, 0};
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -84,6 +87,8 @@ static void launch_vc(int ppw, unsigned grid, hipStream_t s, const u64x2 *a, con
         case 1: k_vclock<NODES, 1><<<grid, 256, 0, s>>>(a, b, c, pairs); break;
         case 2: k_vclock<NODES, 2><<<grid, 256, 0, s>>>(a, b, c, pairs); break;
         case 8: k_vclock<NODES, 8><<<grid, 256, 0, s>>>(a, b, c, pairs); break;
+        case 16: k_vclock<NODES, 16><<<grid, 256, 0, s>>>(a, b, c, pairs); break;
+        case 32: k_vclock<NODES, 32><<<grid, 256, 0, s>>>(a, b, c, pairs); break;
         default: k_vclock<NODES, 4><<<grid, 256, 0, s>>>(a, b, c, pairs); break;
     }
 }
