@@ -911,19 +911,23 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     std::vector<uint64_t> blen(S), bat(S, 0), e0(S + 1, 0), q0(S + 1, 0), re(S + 1, 0), rq(S + 1, 0), pin_at(S, 0);
     std::vector<uint32_t> sbase(S);
     std::vector<uint8_t> hdr(32 * S);
-    uint64_t pin_used = 0, stage = 0;
+    // bodies encoded here are staged in pinned memory at their offsets in
+    // bb.body, so one copy uploads all of them (a copy per body waited
+    // ~24 us each on the copy engine)
+    uint64_t stage = 0;
+    bool any_enc = false;
     for (size_t i = 0; i < S; ++i) {
         Server &s = *srv[i];
         if (!s.pend) {
             encode_soa(s.RemoteDiff, enc[i]);
-            pin_at[i] = pin_used;
-            pin_used += enc[i].size();
+            any_enc = true;
         }
         const char *b = s.pend ? s.pend_body : enc[i].data();
         memcpy(&hdr[32 * i], b, 32);                    // (every body here is >= 32 bytes)
         blen[i] = s.pend ? s.pend_len : enc[i].size();
         if (!(s.pend && s.pend_dev)) {
             bat[i] = stage;
+            if (!s.pend) pin_at[i] = stage;
             stage += (blen[i] + 15) & ~(uint64_t)15;
         }
         uint64_t ne, np;
@@ -935,7 +939,7 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
         q0[i + 1] = q0[i] + s.dd.n_kv;
         sbase[i] = (uint32_t)(i * kcap);
     }
-    rc = pinned_reserve(ctx, pin_used);               // bodies encoded here; parked pulls are pinned already
+    rc = pinned_reserve(ctx, any_enc ? stage : 0);    // bodies encoded here; parked pulls are pinned already
     if (rc) return rc;
     for (size_t i = 0; i < S; ++i)
         if (!srv[i]->pend) memcpy((char *)ctx->pinned + pin_at[i], enc[i].data(), enc[i].size());
@@ -1024,14 +1028,15 @@ static int dev_merge_batch(crdt_ctx *ctx, Server *const *srv, size_t S, bool *re
     // their servers' pull buffers)
     const uint8_t *base = bb.body.as<uint8_t>();
     std::vector<uint64_t> at(S);
+    if (any_enc) e = hipMemcpyAsync(bb.body.as<char>(), ctx->pinned, stage, hipMemcpyHostToDevice, st);
     for (size_t i = 0; i < S && e == hipSuccess; ++i) {
         const Server &s = *srv[i];
         if (s.pend && s.pend_dev) {
             at[i] = (uint64_t)(uintptr_t)s.pull.p - (uint64_t)(uintptr_t)base;
         } else {
             at[i] = bat[i];
-            e = hipMemcpyAsync(bb.body.as<char>() + bat[i], s.pend ? s.pend_body : (char *)ctx->pinned + pin_at[i],
-                               blen[i], hipMemcpyHostToDevice, st);
+            if (s.pend)                                // (after the bulk copy: its slot there held no body)
+                e = hipMemcpyAsync(bb.body.as<char>() + bat[i], s.pend_body, blen[i], hipMemcpyHostToDevice, st);
         }
     }
     if (e != hipSuccess) return hip_fail(ctx, e);
