@@ -37,6 +37,7 @@ int g_pop_direct = 1;    // population rounds: staging kernel + polled host boun
 int g_or_place_batch = 1;  // OR-Set D2 buckets: placement sorted per round in LDS, stored in pieces (sort.or_place_batch)
 int g_up_threads = 512;  // D2 tile grouping pass: threads per 4096-tuple tile, 256 or 512 (sort.up_threads)
 int g_group_tile = 8192;  // D2 gather forms: tuples per grouping tile, 4096 or 8192 (sort.group_tile)
+int g_or_sub_hist = 1;   // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -359,6 +360,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.group_tile")) {   // D2 gather forms: 4096 / 8192 tuples per grouping tile
         if (v != 4096 && v != 8192) return CRDT_E_INVAL;
         g_group_tile = (int)v;
+    } else if (!strcmp(name, "sort.or_sub_hist")) {  // OR-Set D2 buckets: 1 chunk counts from per-run rows, 0 a counting gather
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_or_sub_hist = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

@@ -84,6 +84,7 @@ extern int g_pop_direct;       // population rounds without copy-engine staging 
 extern int g_or_place_batch;   // OR-Set D2 bucket placement batched in LDS (sort.or_place_batch)
 extern int g_up_threads;       // D2 tile grouping pass: threads per tile (sort.up_threads)
 extern int g_group_tile;       // D2 gather forms: tuples per grouping tile (sort.group_tile)
+extern int g_or_sub_hist;      // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
 extern int g_or_bucket;        // OR-Set D2: bucket gathers instead of radix passes (sort.or_bucket)
 extern int g_or_pair;          // OR-Set D2 chunks: two per workgroup (sort.or_pair)
 extern int g_or_narrow;        // OR-Set D2 chunks: u32 sorting networks (sort.or_narrow)

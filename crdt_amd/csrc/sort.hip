@@ -1213,17 +1213,33 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
 // workgroup then gathers its ~16-composite run from every tile -- 16 lanes
 // per run, four runs per wave-instruction, so every load is a contiguous
 // 128-B piece -- into its LDS table.  No scatter pass, no column scan.
-template <int UB, int TILE>
+//
+// HIST (OR-Set, <= 64 chunks per top byte): also each run's counts by chunk
+// (the 6 key bits under the top byte), one byte per chunk, 64 B per run, at
+// sh_.rows[(bucket * ntiles + tile) * 16 ..] (u32 words of four byte
+// counts): the bucket pass then sums 64-B rows instead of gathering every
+// composite once more to count it.  A run of more than 255 composites
+// (a byte could wrap) sets sh_.flag[bucket]: that bucket counts by gathers.
+struct SubHist {
+    uint32_t *rows;
+    uint32_t *flag;
+};
+template <int UB, int TILE, bool HIST = false>
 __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                      uint32_t ntiles, uint32_t *__restrict__ run,
                                                      uint64_t *__restrict__ comp, uint32_t *__restrict__ viol,
-                                                     unsigned long long *__restrict__ zero) {
+                                                     unsigned long long *__restrict__ zero, SubHist sh_ = {}) {
     constexpr int UR = TILE / UB;                     // composites per thread
     static_assert(TILE < 65536, "16-bit run starts and counts");
     __shared__ uint32_t h[256], hs[256];
     __shared__ uint64_t stage[TILE];
+    static_assert(!HIST || TILE * 2 >= 256 * 16, "the run counts fit the staging area");
+    uint32_t *const hr = reinterpret_cast<uint32_t *>(stage);   // HIST: each run's byte counts by chunk (written
+                                                                //   out before the tile is staged)
     const int tid = threadIdx.x;
     if (tid < 256) h[tid] = 0;
+    if (HIST)
+        for (int i = tid; i < 256 * 16; i += UB) hr[i] = 0;
     if (zero && blockIdx.x == 0 && tid < 256) {       // the buckets' flags (k_lww_table_g, k_or_bucket), the
         zero[tid] = 0;                                //   OR-Set chunks' fallback word
         if (tid == 0) zero[256] = 0;
@@ -1260,13 +1276,26 @@ __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
     if (viol && __ballot(bad) && (tid & 63) == 0) atomicOr(viol, 1u);
     __syncthreads();
     const uint32_t sh = p.W - 8;                      // the bucket: the composite's (the key's) top byte
+    const uint32_t ssh = p.b0 + p.br + p.bt + 9;      // HIST: the chunk bits under it (as k_or_bucket's sub-bucket)
+    const uint32_t smask = (p.bk > 17 ? 1u << (p.bk - 17) : 1u) - 1u;
     uint32_t d[UR];
 #pragma unroll
     for (int r = 0; r < UR; ++r) {
         d[r] = ((vm >> r) & 1u) ? (uint32_t)(c[r] >> sh) & 255u : 256u;
-        if (d[r] < 256) atomicAdd(&h[d[r]], 1u);
+        if (d[r] < 256) {
+            atomicAdd(&h[d[r]], 1u);
+            if (HIST) {
+                const uint32_t sb = (uint32_t)(c[r] >> ssh) & smask;   // (<= 63: HIST only for <= 64 chunks)
+                atomicAdd(&hr[d[r] * 16 + (sb >> 2)], 1u << (8 * (sb & 3)));
+            }
+        }
     }
     __syncthreads();
+    if (HIST) {                                       // the rows out (16 lanes per 64-B row); wide runs flagged
+        for (int i = tid; i < 256 * 16; i += UB)
+            sh_.rows[((size_t)(i >> 4) * ntiles + blockIdx.x) * 16 + (i & 15)] = hr[i];
+        if (tid < 256 && h[tid] > 255) sh_.flag[tid] = 1;
+    }
     if (tid < 64) {                                   // exclusive scan of the 256 bucket counts (wave 0, 4 per lane)
         uint32_t v[4], sum = 0;
 #pragma unroll
@@ -1448,7 +1477,7 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
                                                    unsigned long long *__restrict__ flag, uint64_t *__restrict__ dst,
                                                    uint64_t *__restrict__ bounds, unsigned long long *__restrict__ cst,
                                                    uint32_t nch, uint32_t *__restrict__ err, int diag,
-                                                   bool place_batch) {
+                                                   bool place_batch, SubHist shist) {
     __shared__ uint32_t s_run[kRunLds];
     __shared__ uint32_t s_h[OB_WAVES][kObSub];        // per-wave counts by sub-bucket, then the cursors (row 0)
     __shared__ uint64_t s_buf[kObBatch];              // (batched placement) one round's tuples by sub-bucket
@@ -1507,8 +1536,31 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
             }
         }
     };
-    // 1. counts by sub-bucket (a row per wave: fewer same-address LDS atomics)
-    sweep([&](uint64_t x) { atomicAdd(&s_h[w][(uint32_t)(x >> ssh) & (nsub - 1)], 1u); });
+    // 1. counts by sub-bucket: from the grouping pass's per-run chunk counts
+    // (shist: four lanes per 64-B row, sixteen byte counts each), else by a
+    // gather of every run (a row per wave: fewer same-address LDS atomics)
+    bool rows = shist.rows != nullptr && nsub <= 64;
+    if (rows) {
+        rows = shist.flag[T] == 0;                    // (uniform) no run of T over 255
+        __syncthreads();                              // (every lane has read the flag)
+        if (tid == 0) shist.flag[T] = 0;              // clean for the next call
+    }
+    if (rows) {
+        const uint32_t q = (uint32_t)tid & 3;
+        uint32_t cnt[16] = {};
+        const uint4 *rp4 = (const uint4 *)shist.rows + (size_t)T * ntiles * 4;
+        for (uint32_t t = (uint32_t)tid >> 2; t < ntiles; t += OBB / 4) {
+            const uint4 v = rp4[(size_t)t * 4 + q];
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) cnt[j] += (wv[j >> 2] >> (8 * (j & 3))) & 255u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (cnt[j]) atomicAdd(&s_h[w][16 * q + j], cnt[j]);
+    } else {
+        sweep([&](uint64_t x) { atomicAdd(&s_h[w][(uint32_t)(x >> ssh) & (nsub - 1)], 1u); });
+    }
     // the predecessors' totals (every bucket published its own above)
     unsigned long long pre = 0;
     if ((uint32_t)tid < T) {
@@ -2712,6 +2764,7 @@ struct D2Ws {
     uint64_t *cb;                                   // OR-Set chunk bounds, counts, offsets, look-back words
     uint32_t *cc, *cl, *ct;
     unsigned long long *cst;
+    uint32_t *hrows, *hflag;                        // OR-Set: per-run chunk counts (SubHist), 64 B per (bucket, tile)
 };
 
 template <int MODE>
@@ -2721,7 +2774,7 @@ static size_t d2_ws_bytes(size_t n) {
     const size_t b_cnt = Carve::round(ncnt * 4), b_tot = Carve::round(256 * 4), b_bufs = Carve::round(2 * 3 * n * 8);
     const size_t b_flag = Carve::round(258 * 8);
     const size_t b_chunk = MODE == DD_OR ? 2 * Carve::round((kMaxChunks + 1) * 8) + 2 * Carve::round(kMaxChunks * 4) +
-                                               Carve::round(64)
+                                               Carve::round(64) + Carve::round(ntiles * 256 * 64) + Carve::round(256 * 4)
                                          : 0;
     return b_mm + b_plan + 2 * b_cnt + b_tot + b_bufs + b_flag + b_chunk + 1024;
 }
@@ -2745,6 +2798,8 @@ static D2Ws d2_carve(void *ws, size_t n) {
         d.cl = w.take<uint32_t>(kMaxChunks);
         d.ct = w.take<uint32_t>(16);
         d.cst = w.take<unsigned long long>(kMaxChunks + 1);
+        d.hrows = w.take<uint32_t>(ntiles * 256 * 16);   // (ntiles of 4096: enough for either grouping tile)
+        d.hflag = w.take<uint32_t>(256);
     }
     return d;
 }
@@ -2801,10 +2856,15 @@ static bool d2_vec(const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t
 // The tile grouping pass of the gather forms (k_lww_up_tiled): tiles of
 // sort.group_tile tuples (4096 or 8192) grouped by the key's top byte;
 // returns the tile count.
-static unsigned group_tiles(hipStream_t s, const crdt_tuples &A, size_t n, const D2Ws &w, uint32_t *vw) {
+static unsigned group_tiles(hipStream_t s, const crdt_tuples &A, size_t n, const D2Ws &w, uint32_t *vw,
+                            const SubHist &hist = {}) {
     const unsigned tile = g_group_tile == 8192 ? 8192u : 4096u;
     const unsigned ntiles = (unsigned)((n + tile - 1) / tile);
-    if (tile == 8192)
+    if (hist.rows && tile == 8192)
+        k_lww_up_tiled<1024, 8192, true><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, hist);
+    else if (hist.rows)
+        k_lww_up_tiled<512, ST, true><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, hist);
+    else if (tile == 8192)
         k_lww_up_tiled<1024, 8192><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
     else if (g_up_threads == 512)
         k_lww_up_tiled<512, ST><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
@@ -2882,15 +2942,17 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             const bool lb = g_or_lookback && (!g_rdd_diag || g_rdd_diag >= 5);   // (diag 5 / 6: the look-back form's timings)
             const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
             if (vec && g_or_bucket) {                   // tiles grouped by top byte, buckets gathered into chunks
-                const unsigned gt = group_tiles(s, A, n, w, vw);
+                // per-run chunk counts from the grouping pass (<= 64 chunks per top byte)
+                const SubHist hist = (g_or_sub_hist && h.bk <= 23) ? SubHist{w.hrows, w.hflag} : SubHist{};
+                const unsigned gt = group_tiles(s, A, n, w, vw, hist);
                 if (g_group_tile == 8192)
                     k_or_bucket<4><<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, gt, n, w.flags, w.bufs + n, w.cb,
                                                        lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
-                                                       g_or_place_batch != 0);
+                                                       g_or_place_batch != 0, hist);
                 else
                     k_or_bucket<2><<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, gt, n, w.flags, w.bufs + n, w.cb,
                                                        lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
-                                                       g_or_place_batch != 0);
+                                                       g_or_place_batch != 0, hist);
                 sorted = w.bufs + n;
             } else {                                    // two radix passes on the top 16 bits
                 rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec,
