@@ -176,15 +176,18 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
  * both sides together with a side bit between rep and tomb -- composite
  * order (key, ts, rep, side, tomb) is the stable merge of the two sorted
  * sides -- followed by a neighbour dedup of the sorted composites.  Where
- * the key offsets are dense enough the sort stops early: LWW after one pass
- * on the key's top byte (each key's winner kept in an LDS table per
- * bucket), OR-Set after two passes on its top 16 bits (each 2^9-key chunk
- * sorted in LDS); on large calls those two are planned from a sample of
- * the inputs that the first pass checks (a miss redoes the call from the
- * exact ranges).  Output identical to crdt_tuples_sort of each side then
- * crdt_lww_merge / crdt_orset_merge.  Synchronises the stream once to size
- * the passes, and the dense-key forms once more at the end (the sample's
- * check; the OR-Set chunks' LDS limits).  na + nb < 2^32; out capacity >=
+ * the key offsets are dense enough no radix pass runs: the tuples are
+ * grouped per tile by the key's top byte, then LWW gathers each byte's runs
+ * into an LDS table of per-key winners and OR-Set gathers them into 2^9-key
+ * chunks sorted in LDS; on large calls those forms are planned from a
+ * sample of the inputs that the grouping pass checks (a miss redoes the
+ * call from the exact ranges), and a context keeps the last sampled shape
+ * per mode and size (launched from it without reading the plan back; a
+ * different fresh sample counts as a miss).  Output identical to
+ * crdt_tuples_sort of each side then crdt_lww_merge / crdt_orset_merge.
+ * Synchronises once at the end in the dense-key forms (the sample's check,
+ * the OR-Set chunks' LDS limits), once more to read a plan the context does
+ * not hold, and once to size the radix passes otherwise.  na + nb < 2^32; out capacity >=
  * na + nb; out must not overlap a or b (CRDT_E_INVAL: the dense-key forms
  * store before they know whether the call is redone from the inputs). */
 int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
@@ -192,9 +195,9 @@ int crdt_lww_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, cons
 int crdt_orset_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_tuples *b,
                               size_t nb, crdt_tuples *out, uint64_t *out_count_dev);
 /* Stream-ordered D2 merges (no host synchronisation: a HIP graph can capture
- * them).  The calls above read their plan -- field ranges, composite layout,
- * which dense-key form applies -- back from the device (one synchronisation)
- * and check the sampled ranges at the end (a second).  A host that merges
+ * them).  The calls above may read their plan -- field ranges, composite
+ * layout, which dense-key form applies -- back from the device and check the
+ * sampled ranges at the end (one synchronisation each).  A host that merges
  * the same shape repeatedly (a replica population's key space; the gossip
  * loop of main.go:226-258 calls merge() every round) plans once:
  * crdt_set_merge_plan (mode 0 = LWW, 1 = OR-Set; synchronises once) computes
