@@ -29,7 +29,7 @@ int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
 int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
 int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
 int g_sample_plan = 1;   // dense-key D2 paths from a sampled plan, checked in the upsweep (sort.sample_plan)
-int g_plan_cache = 1;    // ... launched from the last such plan's shape, checked on the device (sort.plan_cache)
+int g_plan_cache = 2;    // ... launched from the last such plan (2: as it is, no sample; 1: its shape, a fresh sample checked on the device) (sort.plan_cache)
 int g_rm_affine = 1;     // one-pair populations: RefMerge pair indices computed, no kv range loads (refmerge.affine_kv)
 int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
 int g_or_narrow = 1;
@@ -369,8 +369,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_narrow")) {    // OR-Set D2 chunks: 1 u32 sorting networks where the tag fits 32 bits
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_narrow = (int)v;
-    } else if (!strcmp(name, "sort.plan_cache")) {   // D2 sampled plans: 1 launch from the cached shape (no read-back)
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "sort.plan_cache")) {   // D2 sampled plans: 2 the cached plan (no sample), 1 its shape + a sample, 0 none
+        if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_plan_cache = (int)v;
     } else if (!strcmp(name, "sort.sample_min")) {   // fewest tuples for the sampled plan
         if (v < 0 || v > 0x7FFFFFFF) return CRDT_E_INVAL;

@@ -3067,11 +3067,29 @@ static int set_merge_unsorted(crdt_ctx *ctx, const crdt_tuples *a, size_t na, co
     // the composing upsweep, the call redone from the exact plan on a miss
     bool sampled = false;
     if (allow_sample && g_sample_plan && vec && (lww_t || or_t) && n >= (size_t)g_sample_min) {
+        const uint64_t key0 = (uint64_t)n, key1 = (uint64_t)MODE | (uint64_t)key_only << 8 | (uint64_t)lww_t << 16 |
+                                                  (uint64_t)or_t << 24 | (uint64_t)na << 32;
+        const bool cached =
+            g_plan_cache && ctx->d2_ok[MODE] && ctx->d2_key[MODE][0] == key0 && ctx->d2_key[MODE][1] == key1;
+        if (cached && g_plan_cache == 2) {
+            // sort.plan_cache = 2 (default): the last call's plan as it is --
+            // these inputs' pointers, its shape and ranges -- no sample; the
+            // grouping pass checks every tuple against its ranges, and one
+            // outside redoes the call (as the planned calls, the plan a
+            // shape validated by the whole of the last call's inputs)
+            memcpy(&h, ctx->d2_plan[MODE], sizeof h);
+            h.n1 = na;
+            h.in2 = B;
+            k_put_plan<<<1, 64, 0, s>>>(h, w.plan, w.viol);
+            sampled = true;
+        }
+    }
+    if (!sampled && allow_sample && g_sample_plan && vec && (lww_t || or_t) && n >= (size_t)g_sample_min) {
         k_sample_minmax<<<2 * SAMPLE_WG, 256, 0, s>>>(A, na, B, nb, w.mm);
         k_sort_plan<<<1, 256, 0, s>>>(w.mm, 2 * SAMPLE_WG, w.plan, 1, B, na, key_only, lww_t, or_t, (uint64_t)n, 1u,
                                       w.viol);
         // the launch shape of the last call of this kind, checked on the
-        // device: no read-back (sort.plan_cache)
+        // device: no read-back (sort.plan_cache = 1)
         const uint64_t key0 = (uint64_t)n, key1 = (uint64_t)MODE | (uint64_t)key_only << 8 | (uint64_t)lww_t << 16 |
                                                   (uint64_t)or_t << 24 | (uint64_t)na << 32;
         if (g_plan_cache && ctx->d2_ok[MODE] && ctx->d2_key[MODE][0] == key0 && ctx->d2_key[MODE][1] == key1) {

@@ -181,9 +181,9 @@ int crdt_orset_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
  * into an LDS table of per-key winners and OR-Set gathers them into 2^9-key
  * chunks sorted in LDS; on large calls those forms are planned from a
  * sample of the inputs that the grouping pass checks (a miss redoes the
- * call from the exact ranges), and a context keeps the last sampled shape
- * per mode and size (launched from it without reading the plan back; a
- * different fresh sample counts as a miss).  Output identical to
+ * call from the exact ranges), and a context keeps the last sampled plan
+ * per mode and size (later calls of that size launch from it with no
+ * sample and no read-back; a tuple outside its ranges is a miss).  Output identical to
  * crdt_tuples_sort of each side then crdt_lww_merge / crdt_orset_merge.
  * Synchronises once at the end in the dense-key forms (the sample's check,
  * the OR-Set chunks' LDS limits), once more to read a plan the context does
