@@ -79,10 +79,11 @@ int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
 /* Kernel tuning knobs (process-wide), for A/B runs: "join.unroll" (1,2,4,8),
  * "join.nontemporal" (0/1), "join.blocks_per_cu" (1..64),
- * "vclock.pairs_per_wave" (1,2,4,8), "sets.lww_chunk" / "sets.or_chunk"
+ * "vclock.pairs_per_wave" (1,2,4,8,16,32), "sets.lww_chunk" / "sets.or_chunk"
  * (tiles per count / write chunk of the set merges, 0 = one chunk),
  * "sets.streams" (1, 2), "sets.lww_parts", "sets.or_parts",
- * "refmerge.tile_parts", "refmerge.count_dma";
+ * "refmerge.tile_parts", "refmerge.count_dma", the D2 forms' "sort.*"
+ * (e.g. "sort.plan_cache" 0/1/2, "sort.group_tile" 4096/8192), "pop.direct";
  * fault injection: "fail.refmerge" (n: the next n RefMerge calls return
  * CRDT_E_NOMEM before touching the device -- error-path tests),
  * "fail.zero_bits" (n: the next n two-pass merges -- set merges, RefMerge --
