@@ -38,6 +38,7 @@ int g_or_place_batch = 1;  // OR-Set D2 buckets: placement sorted per round in L
 int g_up_threads = 512;  // D2 tile grouping pass: threads per 4096-tuple tile, 256 or 512 (sort.up_threads)
 int g_group_tile = 8192;  // D2 gather forms: tuples per grouping tile, 4096 or 8192 (sort.group_tile)
 int g_or_sub_hist = 1;   // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
+int g_read_poll = 1;     // small read-backs polled from coherent host memory (ctx.read_poll)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -199,10 +200,64 @@ extern "C" int crdt_stream_destroy(void *stream) {
     return e == hipSuccess ? CRDT_OK : CRDT_E_HIP;
 }
 
+namespace crdt {
+__global__ __launch_bounds__(256) void k_read_words(const uint32_t *__restrict__ src, uint32_t n,
+                                                    uint32_t *__restrict__ dst, uint64_t *__restrict__ flag,
+                                                    uint64_t seq) {
+    for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void **host) {
+    if (bytes > kCioBytes || (bytes & 3)) return CRDT_E_INVAL;
+    if (!g_read_poll) {
+        int rc = hio_reserve(ctx, bytes ? bytes : 4);
+        if (rc) return rc;
+        hipError_t e = bytes ? hipMemcpyAsync(ctx->hio, dev_src, bytes, hipMemcpyDeviceToHost, ctx->stream)
+                             : hipSuccess;
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        *host = ctx->hio;
+        return CRDT_OK;
+    }
+    if (!ctx->cio) {                                  // words | completion word (64 B after them)
+        void *h = nullptr, *d = nullptr;
+        hipError_t e = hipHostMalloc(&h, kCioBytes + 64, hipHostMallocCoherent | hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&d, h, 0);
+        if (e != hipSuccess) {
+            if (h) (void)hipHostFree(h);
+            return hip_fail(ctx, e);
+        }
+        ctx->cio = h;
+        ctx->cio_d = d;
+        *(volatile uint64_t *)((char *)h + kCioBytes) = 0;
+        ctx->cio_seq = 0;
+    }
+    const uint64_t seq = ++ctx->cio_seq;
+    k_read_words<<<1, 256, 0, ctx->stream>>>((const uint32_t *)dev_src, (uint32_t)(bytes / 4),
+                                              (uint32_t *)ctx->cio_d, (uint64_t *)((char *)ctx->cio_d + kCioBytes),
+                                              seq);
+    int rc = check_launch(ctx);
+    if (rc) return rc;
+    const volatile uint64_t *f = (const volatile uint64_t *)((char *)ctx->cio + kCioBytes);
+    while (*f != seq) {
+        const hipError_t q = hipStreamQuery(ctx->stream);
+        if (q == hipErrorNotReady) continue;
+        if (*f == seq) break;
+        return hip_fail(ctx, q == hipSuccess ? hipErrorUnknown : q);
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    *host = ctx->cio;
+    return CRDT_OK;
+}
+}  // namespace crdt
+
 extern "C" int crdt_ctx_destroy(crdt_ctx *ctx) {
     if (!ctx) return CRDT_OK;
     (void)bind(ctx);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->cio) (void)hipHostFree(ctx->cio);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->io) (void)hipFree(ctx->io);
     if (ctx->dev_status) (void)hipFree(ctx->dev_status);
@@ -363,6 +418,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "sort.or_sub_hist")) {  // OR-Set D2 buckets: 1 chunk counts from per-run rows, 0 a counting gather
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_sub_hist = (int)v;
+    } else if (!strcmp(name, "ctx.read_poll")) {     // small read-backs: 1 kernel + polled coherent memory, 0 copy + sync
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_read_poll = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

@@ -47,6 +47,10 @@ struct crdt_ctx {
     alignas(8) unsigned char d2_plan[2][128];   // [mode: LWW, OR-Set]
     uint64_t d2_key[2][2] = {{0, 0}, {0, 0}};
     bool d2_ok[2] = {false, false};
+    // Polled small read-backs (ctx_read_words): coherent pinned host memory
+    // a kernel writes the words into, then a completion word (kCioWords on).
+    void *cio = nullptr, *cio_d = nullptr;
+    uint64_t cio_seq = 0;
 };
 
 namespace crdt {
@@ -85,6 +89,7 @@ extern int g_or_place_batch;   // OR-Set D2 bucket placement batched in LDS (sor
 extern int g_up_threads;       // D2 tile grouping pass: threads per tile (sort.up_threads)
 extern int g_group_tile;       // D2 gather forms: tuples per grouping tile (sort.group_tile)
 extern int g_or_sub_hist;      // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
+extern int g_read_poll;        // small read-backs polled from coherent host memory (ctx.read_poll)
 extern int g_or_bucket;        // OR-Set D2: bucket gathers instead of radix passes (sort.or_bucket)
 extern int g_or_pair;          // OR-Set D2 chunks: two per workgroup (sort.or_pair)
 extern int g_or_narrow;        // OR-Set D2 chunks: u32 sorting networks (sort.or_narrow)
@@ -187,6 +192,15 @@ inline int hio_reserve(crdt_ctx *ctx, size_t bytes) {
     ctx->hio_bytes = want;
     return CRDT_OK;
 }
+
+// Up to kCioBytes of device memory to the host, stream-ordered, without the
+// copy engine or an interrupt-driven wait: one one-workgroup kernel copies
+// the words into coherent pinned memory and then releases a completion
+// word that the host polls (the stream's own state ends the wait if the
+// kernel never ran).  *host = the pinned copy, valid until the next call.
+// (ctx.read_poll = 0: hipMemcpyAsync + hipStreamSynchronize into ctx->hio.)
+constexpr size_t kCioBytes = 4096;
+int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void **host);
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

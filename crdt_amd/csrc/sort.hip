@@ -2716,12 +2716,11 @@ static int or_run_dedup(crdt_ctx *ctx, uint64_t *c, size_t n, const SortPlan *pl
 // the device plan back to the host through the context's pinned buffer (a
 // pageable destination costs a staged copy on every call)
 static int read_plan(crdt_ctx *ctx, const SortPlan *plan, SortPlan *h) {
-    int rc = hio_reserve(ctx, sizeof(SortPlan));
+    static_assert(sizeof(SortPlan) % 4 == 0, "whole words");
+    const void *hp = nullptr;
+    int rc = ctx_read_words(ctx, plan, sizeof(SortPlan), &hp);
     if (rc) return rc;
-    hipError_t e = hipMemcpyAsync(ctx->hio, plan, sizeof(SortPlan), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    memcpy(h, ctx->hio, sizeof(SortPlan));
+    memcpy(h, hp, sizeof(SortPlan));
     return CRDT_OK;
 }
 
@@ -2890,13 +2889,8 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
     const hipStream_t s = ctx->stream;
     const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
     *miss = false;
-    auto read_words = [&](const void *src, size_t bytes) -> int {   // the end-of-call check words
-        int rc = hio_reserve(ctx, 16);
-        if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(ctx->hio, src, bytes, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
-    };
+    const void *hw = nullptr;                          // the end-of-call check words, on the host
+    auto read_words = [&](const void *src, size_t bytes) -> int { return ctx_read_words(ctx, src, bytes, &hw); };
     auto finish = [&](const uint32_t *fb) -> int {     // after the last pass: the range check
         int rc = check_launch(ctx);
         if (rc || !vw) return rc;
@@ -2905,7 +2899,7 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             return check_launch(ctx);
         }
         rc = read_words(vw, 4);
-        if (!rc) *miss = *(const uint32_t *)ctx->hio != 0;
+        if (!rc) *miss = *(const uint32_t *)hw != 0;
         return rc;
     };
     uint64_t *sorted = nullptr;
@@ -2998,7 +2992,7 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             }
             rc = read_words(&w.flags[256], 16);        // the fallback word (long keys), the range check
             if (rc) return rc;
-            const uint32_t fb = *(const uint32_t *)ctx->hio, mw = vw ? ((const uint32_t *)ctx->hio)[2] : 0u;
+            const uint32_t fb = *(const uint32_t *)hw, mw = vw ? ((const uint32_t *)hw)[2] : 0u;
             if (mw) {
                 *miss = true;
                 return CRDT_OK;
