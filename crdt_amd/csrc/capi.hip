@@ -39,6 +39,7 @@ int g_up_threads = 512;  // D2 tile grouping pass: threads per 4096-tuple tile, 
 int g_group_tile = 8192;  // D2 gather forms: tuples per grouping tile, 4096 or 8192 (sort.group_tile)
 int g_or_sub_hist = 1;   // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
 int g_read_poll = 1;     // small read-backs polled from coherent host memory (ctx.read_poll)
+int g_pop_wire_early = 1;  // wire rounds: the merge enqueued behind the decode's claim pass (pop.wire_early)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -421,6 +422,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "ctx.read_poll")) {     // small read-backs: 1 kernel + polled coherent memory, 0 copy + sync
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_read_poll = (int)v;
+    } else if (!strcmp(name, "pop.wire_early")) {    // wire rounds: 1 merge enqueued behind the claim pass, 0 after the decode
+        if (v != 0 && v != 1) return CRDT_E_INVAL;
+        g_pop_wire_early = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <new>
 #include <vector>
 
@@ -85,6 +86,8 @@ struct crdt_population {
     size_t dsm_bytes = 0;
     void *xb = nullptr;                        // sharded rounds: send and import buffers
     size_t xb_bytes = 0;
+    void *dscr = nullptr;                      // wire rounds: the device decode's own scratch (the merge
+    size_t dscr_bytes = 0;                     //   runs behind its claim pass in ctx->ws)
 };
 
 namespace crdt {
@@ -560,7 +563,7 @@ extern "C" int crdt_population_destroy(crdt_population *pop) {
     if (!pop->vtab)
         for (void *p : {(void *)pop->str_bytes, (void *)pop->str_off})
             if (p) (void)hipFree(p);
-    for (void *p : {pop->dsm, pop->xb})
+    for (void *p : {pop->dsm, pop->xb, pop->dscr})
         if (p) (void)hipFree(p);
     if (pop->pin) (void)hipHostFree(pop->pin);
     if (pop->hflag) (void)hipHostFree(pop->hflag);
@@ -895,11 +898,32 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     uint64_t *r_kv = w.take<uint64_t>(n_e + 1);
     const crdt_gossip_decoded go{r_off, r_ts, r_kv, cd.kv_key, cd.kv_val};
     uint64_t multi = 1;
+    // The merge is enqueued by the decode right behind its claim pass
+    // (pop.wire_early, default 1): the pulled strings are nearly always
+    // interned already, so the host does not wait for the claims before the
+    // merge starts.  Its guesses -- the one-pair passes when the population
+    // is one-pair, the ids as the claim pass left them -- are checked after
+    // the decode; a wrong one (new strings, a multi-pair pull) runs the merge
+    // again.  Either way it writes only the spare buffers: a refused body
+    // still leaves the population as it was (with nothing to undo).
+    const bool guess_one = pop->one_pair;
+    RoundArrays a;
+    bool merged = false;
+    const std::function<int()> run_merge = [&]() -> int {
+        int r = upload_round(pop, h, &a);
+        if (!r) r = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, guess_one);
+        merged = r == CRDT_OK;
+        return r;
+    };
+    bool stale = false;
+    const size_t need = gossip_decode_scratch_bytes(P, n_e, n_p);
+    const bool early = g_pop_wire_early && dev_grow(ctx, &pop->dscr, &pop->dscr_bytes, need) == CRDT_OK;
     rc = gossip_decode_at(ctx, P, bodies, at.data(), len.data(), pop->K, pop->n_kv, sbase.data(), hdr.data(), keys,
-                          vals, &go, body_status, nullptr, nullptr, 0, nullptr, &multi);
+                          vals, &go, body_status, early ? &run_merge : nullptr, early ? pop->dscr : nullptr,
+                          early ? pop->dscr_bytes : 0, &stale, &multi);
     if (rc) return rc;
     for (uint32_t i = 0; i < P; ++i)
-        if (body_status[i] && len[i]) return CRDT_E_UNSORTED;   // (nothing merged: the population is unchanged)
+        if (body_status[i] && len[i]) return CRDT_E_UNSORTED;   // (nothing committed: the population is unchanged)
     if (!pop->vtab) {                                    // the arena is vals' from now on
         (void)dev_free(ctx, (void **)&pop->str_bytes);
         (void)dev_free(ctx, (void **)&pop->str_off);
@@ -907,10 +931,11 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     }
     // one pair per pulled entry too (counted by the decode): the one-pair passes
     const bool one = pop->one_pair && multi == 0;
-    RoundArrays a;
-    rc = upload_round(pop, h, &a);
-    if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, one);
-    if (rc) return rc;
+    if (!merged || stale || one != guess_one) {
+        rc = upload_round(pop, h, &a);
+        if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, one);
+        if (rc) return rc;
+    }
     rc = pop_commit(pop);
     if (!rc) pop->one_pair = one;
     return rc;
