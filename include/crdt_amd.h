@@ -682,7 +682,9 @@ int crdt_population_round_sharded(crdt_comm *comm, crdt_population *const *pops,
  * behind the current Diff's, then merged as crdt_population_round.  A body
  * the device decode does not take (malformed, a nil map, unsorted, a key id
  * >= K) fails the call with CRDT_E_UNSORTED, its status in body_status[i]
- * (host, replicas words): nothing is merged.  Synchronises. */
+ * (host, replicas words): nothing is committed (the previous round can no
+ * longer be undone: the merge may already have run into the spare buffers).
+ * Synchronises. */
 int crdt_population_round_wire(crdt_population *pop, crdt_strtab *keys, crdt_strtab *vals, const uint8_t *bodies,
                                const uint64_t *body_off, uint32_t *body_status);
 
