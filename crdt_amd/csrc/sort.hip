@@ -1849,6 +1849,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t kb = p.b0 + p.br + p.bt, tb = p.b0;
     bool fb = false;                                  // (uniform) a chunk of this workgroup fell back
+    bool stop = false;                                // (timing diagnostics 1..4: every chunk stops at that phase)
     size_t sk[K];
     for (int kk = 0; kk < K; ++kk) {
     const uint32_t ci = blockIdx.x * K + (uint32_t)kk;
@@ -1883,7 +1884,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     __syncthreads();
     if (diag == 1) {                                  // timing diagnostics (sort.rdd_diag): counts only
         if (tid == 0) cnt[ci] = 0;
-        return;
+        stop = true;
+        continue;
     }
     {                                                 // exclusive scan: wave w the contiguous entries [w P, (w+1) P)
         constexpr uint32_t P = kOcKeys / OC_WAVES;
@@ -1915,7 +1917,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     __syncthreads();                                  // tab[k] = the end of key k
     if (diag == 2) {                                  // + the scan and the scatter into LDS
         if (tid == 0) cnt[ci] = 0;
-        return;
+        stop = true;
+        continue;
     }
     // distinct tags per key (long keys listed, resolved below); each short
     // key's slots stay sorted in registers for the stores
@@ -1968,7 +1971,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     const uint32_t nl = s_nlong;
     if (diag == 3) {                                  // + the short keys' distinct tags
         if (tid == 0) cnt[ci] = 0;
-        return;
+        stop = true;
+        continue;
     }
     if (nl > kOcLong) {                               // (uniform) too many long keys: the radix path
         if (tid == 0) {
@@ -2034,7 +2038,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     __syncthreads();
     if (diag == 4) {                                  // + the long keys and the ranks
         if (tid == 0) cnt[ci] = 0;
-        return;
+        stop = true;
+        continue;
     }
     // LB: the offset -- the counts of the chunks before this one -- found by
     // wave 0 while the other waves place their keys' tags (the barrier after
@@ -2135,6 +2140,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     }
     }                                                 // (the next chunk of this workgroup)
     __syncthreads();
+    if (stop) return;
     if (fb) return;                                   // (uniform; the call falls back to the radix path)
     if constexpr (!LB) {
         for (int kk = 0; kk < K; ++kk)
