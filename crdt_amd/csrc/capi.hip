@@ -40,6 +40,7 @@ int g_group_tile = 8192;  // D2 gather forms: tuples per grouping tile, 4096 or 
 int g_or_sub_hist = 1;   // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
 int g_read_poll = 1;     // small read-backs polled from coherent host memory (ctx.read_poll)
 int g_pop_wire_early = 1;  // wire rounds: the merge enqueued behind the decode's claim pass (pop.wire_early)
+int g_or_lb_words = 1;   // OR-Set D2 chunk look-back: status words per lane per window, 1 or 4 (sort.or_lb_words)
 int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
 int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
 int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
@@ -425,6 +426,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "pop.wire_early")) {    // wire rounds: 1 merge enqueued behind the claim pass, 0 after the decode
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_pop_wire_early = (int)v;
+    } else if (!strcmp(name, "sort.or_lb_words")) {  // OR-Set D2 chunk look-back: 1 / 4 status words per lane per window
+        if (v != 1 && v != 4) return CRDT_E_INVAL;
+        g_or_lb_words = (int)v;
     } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_or_pair = (int)v;

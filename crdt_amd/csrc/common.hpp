@@ -91,6 +91,7 @@ extern int g_group_tile;       // D2 gather forms: tuples per grouping tile (sor
 extern int g_or_sub_hist;      // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
 extern int g_read_poll;        // small read-backs polled from coherent host memory (ctx.read_poll)
 extern int g_pop_wire_early;   // wire rounds: merge behind the claim pass (pop.wire_early)
+extern int g_or_lb_words;      // OR-Set D2 chunk look-back window words per lane (sort.or_lb_words)
 extern int g_or_bucket;        // OR-Set D2: bucket gathers instead of radix passes (sort.or_bucket)
 extern int g_or_pair;          // OR-Set D2 chunks: two per workgroup (sort.or_pair)
 extern int g_or_narrow;        // OR-Set D2 chunks: u32 sorting networks (sort.or_narrow)
