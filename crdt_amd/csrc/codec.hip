@@ -107,8 +107,24 @@ __device__ __forceinline__ bool short_lt(uint64_t a, uint32_t na, uint64_t b, ui
     return A != B ? A < B : na < nb;
 }
 
+// A table's H entries are followed by H short forms: entry i's string, when
+// it has an id and at most 7 bytes, packed as load_short does with its length
+// in the top byte (kNoShort otherwise), so a lookup of a short string that
+// hits a resolved entry compares one word loaded beside the entry instead of
+// walking entry -> offsets -> bytes (codec.short_tab).
+constexpr uint64_t kNoShort = ~0ull;
+__device__ __forceinline__ uint64_t short_form(uint64_t packed, uint32_t n) {
+    return n <= 7 ? packed | (uint64_t)n << 56 : kNoShort;
+}
+__device__ __forceinline__ uint64_t short_form_bytes(const uint8_t *p, uint32_t n) {
+    if (n > 7) return kNoShort;
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < n; ++i) v |= (uint64_t)p[i] << (8 * i);
+    return v | (uint64_t)n << 56;
+}
+
 struct TabView {
-    uint64_t *tab;
+    uint64_t *tab;                 // [mask + 1] entries, then [mask + 1] short forms
     uint64_t mask;
     const uint8_t *bytes;
     const uint64_t *off;
@@ -119,16 +135,25 @@ struct TabView {
 // Returns the entry index (kEmptyE as uint64 on a full table); *rep = claimed.
 template <class Get>
 __device__ uint64_t tab_claim(const TabView &t, uint32_t h, const uint8_t *s, uint32_t len, uint32_t self,
-                              const Get &get, bool *rep, uint64_t *ent, uint64_t sv) {
+                              const Get &get, bool *rep, uint64_t *ent, uint64_t sv, bool use_short = false) {
     // sv: the string packed by load_short when len <= 8 (compares then load
     // the candidate's bytes as one word too)
     *rep = false;
     uint64_t i = h & t.mask;
+    const uint64_t want_s = use_short ? short_form(sv, len) : kNoShort;
     for (uint64_t probe = 0; probe <= t.mask; ++probe, i = (i + 1) & t.mask) {
         // a plain load first: ids from earlier calls never change inside a
         // pass; an entry it shows empty may have been claimed meanwhile (the
-        // CAS then returns the claim)
+        // CAS then returns the claim).  Its short form is loaded beside it.
         uint64_t e = t.tab[i];
+        const uint64_t es = want_s != kNoShort ? t.tab[t.mask + 1 + i] : kNoShort;
+        if (es != kNoShort && e != kEmptyE && !((uint32_t)e & kPend)) {   // a resolved short string: one compare
+            if (es == want_s) {
+                *ent = e;
+                return i;
+            }
+            continue;
+        }
         if (e == kEmptyE) {
             const uint64_t want = (uint64_t)h << 32 | kPend | self;
             const uint64_t old = atomicCAS((unsigned long long *)&t.tab[i], (unsigned long long)kEmptyE,
@@ -495,6 +520,7 @@ struct PendGet {                   // bytes of pending reference j (key or value
 // table (an id from an earlier call) gets its ids written at once; the
 // others record their entry (bit 31: this pair claimed it) for passes B / C
 // and count the claims (ctr[0] keys, ctr[1] values).  kEmptyE slots: done.
+template <bool SHORT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
                                                    const uint8_t *__restrict__ first, const uint32_t *__restrict__ flag0,
                                                    uint32_t *__restrict__ cflag,
@@ -537,32 +563,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                     if (!lt) host = true;
                 }
             }
-            bool r;
-            uint64_t e;
             const uint32_t kh = k <= 8 ? hash32_short(ksv, (uint32_t)k) : hash32(kp, (uint32_t)k);
-            const uint64_t si = tab_claim(kt, kh, kp, (uint32_t)k, (uint32_t)j, PendGet{c, false}, &r, &e, ksv);
+            const uint32_t vh = v <= 8 ? hash32_short(vsv, (uint32_t)v) : hash32(vp, (uint32_t)v);
+            bool rk = false, rv = false;
+            uint64_t ek = 0, ev = 0;
+            const uint64_t si = tab_claim(kt, kh, kp, (uint32_t)k, (uint32_t)j, PendGet{c, false}, &rk, &ek, ksv, SHORT);
             if (si == kEmptyE) {
                 full = true;
             } else {
-                if (!r && !((uint32_t)e & kPend)) {          // an existing id
-                    const uint32_t kid = (uint32_t)e & kIdMask;
+                if (!rk && !((uint32_t)ek & kPend)) {        // an existing id
+                    const uint32_t kid = (uint32_t)ek & kIdMask;
                     if (kid >= key_cap) host = true;
                     kv_key[kv_base + j] = d.slot_base + kid;
                 } else {
-                    ks = (uint32_t)si | (r ? kRepBit : 0u);
-                    nk += r;
+                    ks = (uint32_t)si | (rk ? kRepBit : 0u);
+                    nk += rk;
                 }
             }
-            const uint32_t vh = v <= 8 ? hash32_short(vsv, (uint32_t)v) : hash32(vp, (uint32_t)v);
-            const uint64_t sv = tab_claim(vt, vh, vp, (uint32_t)v, (uint32_t)j, PendGet{c, true}, &r, &e, vsv);
+            const uint64_t sv = tab_claim(vt, vh, vp, (uint32_t)v, (uint32_t)j, PendGet{c, true}, &rv, &ev, vsv, SHORT);
             if (sv == kEmptyE) {
                 full = true;
             } else {
-                if (!r && !((uint32_t)e & kPend)) {
-                    kv_val[kv_base + j] = (uint32_t)e & kIdMask;
+                if (!rv && !((uint32_t)ev & kPend)) {
+                    kv_val[kv_base + j] = (uint32_t)ev & kIdMask;
                 } else {
-                    vs = (uint32_t)sv | (r ? kRepBit : 0u);
-                    nv += r;
+                    vs = (uint32_t)sv | (rv ? kRepBit : 0u);
+                    nv += rv;
                 }
             }
         }
@@ -625,6 +651,7 @@ __global__ void k_dec_assign(DecodeCtx c, TabView t, bool value, const uint32_t 
         off[id] = o;
         const uint64_t si = sl & ~kRepBit;
         t.tab[si] = (t.tab[si] & 0xFFFFFFFF00000000ull) | (uint32_t)id;   // keep the hash, drop the pending tag
+        t.tab[t.mask + 1 + si] = short_form_bytes(p, n);
     }
 }
 
@@ -656,7 +683,8 @@ __global__ void k_dec_ids(DecodeCtx c, const uint32_t *__restrict__ kslot, const
 __global__ void k_rehash(uint64_t *__restrict__ tab, uint64_t mask, const uint8_t *__restrict__ bytes,
                          const uint64_t *__restrict__ off, uint64_t n) {
     for (uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (uint64_t)gridDim.x * 256) {
-        const uint32_t h = hash32(bytes + off[id], (uint32_t)(off[id + 1] - off[id]));
+        const uint32_t n = (uint32_t)(off[id + 1] - off[id]);
+        const uint32_t h = hash32(bytes + off[id], n);
         uint64_t i = h & mask;
         for (;;) {
             const uint64_t old = atomicCAS((unsigned long long *)&tab[i], (unsigned long long)kEmptyE,
@@ -664,6 +692,7 @@ __global__ void k_rehash(uint64_t *__restrict__ tab, uint64_t mask, const uint8_
             if (old == kEmptyE) break;
             i = (i + 1) & mask;
         }
+        tab[mask + 1 + i] = short_form_bytes(bytes + off[id], n);
     }
 }
 
@@ -719,9 +748,9 @@ int tab_reserve(crdt_ctx *ctx, crdt_strtab *t, uint64_t more, uint64_t more_byte
     if (2 * (t->n + more) > t->H) {
         const uint64_t H = pow2_at_least(4 * (t->n + more));
         uint64_t *nt = nullptr;
-        hipError_t e = hipMalloc(&nt, H * 8);
+        hipError_t e = hipMalloc(&nt, 2 * H * 8);       // entries, then short forms
         if (e != hipSuccess) return hip_fail(ctx, e);
-        e = hipMemsetAsync(nt, 0xFF, H * 8, ctx->stream);
+        e = hipMemsetAsync(nt, 0xFF, 2 * H * 8, ctx->stream);
         if (e != hipSuccess) {
             (void)hipFree(nt);
             return hip_fail(ctx, e);
@@ -994,8 +1023,12 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
         const dim3 gc((unsigned)std::max<uint64_t>((max_np + kClaimChunk - 1) / kClaimChunk, 1), nb);
-        k_dec_claim<<<gc, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, key_cap, kv_base, kslot, vslot,
-                                       out->kv_key, out->kv_val, ctr);
+#define DEC_CLAIM(SM)                                                                                          \
+        k_dec_claim<SM><<<gc, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, key_cap, kv_base, kslot, vslot, \
+                                           out->kv_key, out->kv_val, ctr)
+        if (g_short_tab) DEC_CLAIM(true);
+        else DEC_CLAIM(false);
+#undef DEC_CLAIM
         rc = check_launch(ctx);
         if (rc) return rc;
     }

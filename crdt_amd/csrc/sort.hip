@@ -2941,7 +2941,6 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
         if (MODE == DD_OR && h.tw) {                    // the key's top 16 bits grouped, then chunks in LDS
             const uint32_t nch = 1u << (h.bk - kOcBits), kb = h.b0 + h.br + h.bt;
             const bool lb = g_or_lookback && (!g_rdd_diag || g_rdd_diag >= 5);   // (diag 5 / 6: the look-back form's timings)
-            const unsigned ntiles = (unsigned)((n + ST - 1) / ST);
             if (vec && g_or_bucket) {                   // tiles grouped by top byte, buckets gathered into chunks
                 // per-run chunk counts from the grouping pass (<= 64 chunks per top byte)
                 const SubHist hist = (g_or_sub_hist && h.bk <= 23) ? SubHist{w.hrows, w.hflag} : SubHist{};

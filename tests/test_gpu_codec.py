@@ -249,3 +249,38 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
     assert host.IngestBinary(bodies[0]) == 0
     assert r_ts[r_off[0]:r_off[1]].tolist() == host.RemoteDiff.Keys()
     host.close()
+
+
+@pytest.mark.parametrize("short_tab", [1, 0])
+def test_decode_resolved_short_forms_across_calls_and_rehash(eng, short_tab):
+    """Strings of <= 7 bytes resolved in an earlier call are found by the
+    short form stored beside their table entry (codec.short_tab, written with
+    the id and again by a rehash): a later call -- before and after the table
+    grows -- maps every string to the id the first call gave it, NUL bytes
+    and equal-padded strings of different lengths ("a" / "a\\x00") apart,
+    8-byte and longer strings by the byte walk, and interns nothing new."""
+    from crdt_amd import _lib
+    _lib.call("crdt_set_option", b"codec.short_tab", short_tab)
+    try:
+        keys, vals = codec.StrTab(eng, 4, 64), codec.StrTab(eng, 4, 64)       # tiny: grows in the first call
+        strs = [b"", b"a", b"a\x00", b"a\x00\x00", b"\x00", b"x" * 7, b"x" * 8, b"x" * 9, b"7", b"-12", b"\xff" * 6]
+        body = _raw_body([(i + 1, [(b"k%02d" % i, s)]) for i, s in enumerate(strs)] +
+                         [(100 + i, [(s, b"v")]) for i, s in enumerate(sorted(set(strs) - {b""}))])
+        dec1, st1, kk1, kv1 = _decode(eng, [body], keys, vals)
+        assert st1.tolist() == [0]
+        n_k, n_v = len(keys), len(vals)
+        for step in range(2):
+            if step:                                                     # grow both tables: a rehash
+                keys.intern([b"g%d" % i for i in range(300)])
+                vals.intern([b"h%d" % i for i in range(300)])
+                n_k, n_v = n_k + 300, n_v + 300
+            dec2, st2, kk2, kv2 = _decode(eng, [body], keys, vals)
+            assert st2.tolist() == [0]
+            assert (len(keys), len(vals)) == (n_k, n_v)                 # nothing new interned
+            assert np.array_equal(kk1, kk2) and np.array_equal(kv1, kv2)
+        ks, vs = keys.strings(), vals.strings()
+        n = len(strs)
+        assert [vs[kv1[3 + i]] for i in range(n)] == strs              # kv_base 3: pair i of entry i
+        assert [ks[kk1[3 + n + i]] for i in range(n - 1)] == sorted(set(strs) - {b""})
+    finally:
+        _lib.call("crdt_set_option", b"codec.short_tab", 1)
