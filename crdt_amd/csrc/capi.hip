@@ -22,7 +22,7 @@ int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within 
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
-int g_short_tab = 1;
+int g_short_tab = 2;
 int g_dec_small = 1;
 int g_rm_kvx = 0;
 int g_rm_ld_all = 0;
@@ -460,8 +460,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "refmerge.kv_one_launch")) {   // kv tile pass: both tile kinds in one launch at any grid
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_rm_kvx = (int)v;
-    } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry (2: + both home probes first)
+        if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_short_tab = (int)v;
     } else if (!strcmp(name, "codec.small")) {   // gossip decode of few small bodies in one pass: 0 off, 1 auto, 2 always
         if (v < 0 || v > 2) return CRDT_E_INVAL;

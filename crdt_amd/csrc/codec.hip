@@ -89,10 +89,11 @@ __device__ __forceinline__ bool bytes_lt(const uint8_t *a, uint32_t na, const ui
 // aligned word that holds a byte of the string never leaves its page.
 __device__ __forceinline__ uint64_t load_short(const uint8_t *p, uint32_t n) {
     if (n == 0) return 0;
-    const uintptr_t a = (uintptr_t)p, base = a & ~(uintptr_t)7;
-    const uint32_t sh = (uint32_t)(a - base);
-    uint64_t v = *(const uint64_t *)base >> (8 * sh);
-    if (sh + n > 8) v |= *(const uint64_t *)(base + 8) << (8 * (8 - sh));
+    // (pointer arithmetic, not integer casts: the loads stay global loads)
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 7);
+    const uint64_t *base = reinterpret_cast<const uint64_t *>(p - sh);
+    uint64_t v = base[0] >> (8 * sh);
+    if (sh + n > 8) v |= base[1] << (8 * (8 - sh));
     return n == 8 ? v : (v & ((1ull << (8 * n)) - 1));
 }
 __device__ __forceinline__ uint32_t hash32_short(uint64_t v, uint32_t n) {   // == hash32 of the n bytes
@@ -195,7 +196,7 @@ struct BodyDesc {                  // one pulled body
 };
 
 __device__ __forceinline__ const uint8_t *body_ptr(const uint8_t *data, uint64_t at) {
-    return (const uint8_t *)((uintptr_t)data + at);
+    return data + at;                                  // (mod 2^64, as the offsets are)
 }
 
 __device__ __forceinline__ uint32_t find_body(const BodyDesc *b, uint32_t nbody, uint64_t x, bool pairs) {
@@ -520,7 +521,14 @@ struct PendGet {                   // bytes of pending reference j (key or value
 // table (an id from an earlier call) gets its ids written at once; the
 // others record their entry (bit 31: this pair claimed it) for passes B / C
 // and count the claims (ctr[0] keys, ctr[1] values).  kEmptyE slots: done.
-template <bool SHORT>
+// SM (codec.short_tab): 0 -- the byte walk for every candidate entry; 1 --
+// a resolved short string compares the short form beside its entry; 2 -- as
+// 1, and a pair whose key and value both have at most 7 bytes first probes
+// both home entries at once (one round trip instead of one per table); the
+// pairs that do not resolve there (new or pending strings, probe chains,
+// longer strings) are listed in LDS and claimed by the loop of form 1 after
+// a barrier -- kept out of the first loop so that its registers stay few.
+template <int SM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_dec_claim(DecodeCtx c, TabView kt, TabView vt,
                                                    const uint8_t *__restrict__ first, const uint32_t *__restrict__ flag0,
                                                    uint32_t *__restrict__ cflag,
@@ -528,6 +536,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                                                    uint64_t kv_base, uint32_t *__restrict__ kslot,
                                                    uint32_t *__restrict__ vslot, uint32_t *__restrict__ kv_key,
                                                    uint32_t *__restrict__ kv_val, unsigned long long *__restrict__ ctr) {
+    static_assert(kClaimChunk == 256, "one pair per thread: the slow list holds a workgroup's pairs");
+    __shared__ uint32_t s_slow[SM == 2 ? kClaimChunk : 1];
+    __shared__ uint32_t s_ns;
     const uint32_t b = blockIdx.y;
     const BodyDesc d = c.bd[b];
     const uint8_t *region = body_ptr(c.data, d.data) + 32 + 12 * d.ne + 8 * d.np;
@@ -538,6 +549,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const bool rejected = flag0[b] != 0;
     bool host = false, bad = false, full = false;
     uint32_t nk = 0, nv = 0;
+    // both claims of pair j (key, then value): ids written for strings known
+    // from earlier calls, claimed / pending entries recorded for passes B / C
+    auto claim = [&](uint64_t j, const uint8_t *kp, uint32_t k, uint64_t ksv, const uint8_t *vp, uint32_t v,
+                     uint64_t vsv) {
+        uint32_t ks = kEmptyE32, vs = kEmptyE32;
+        const uint32_t kh = k <= 8 ? hash32_short(ksv, k) : hash32(kp, k);
+        const uint32_t vh = v <= 8 ? hash32_short(vsv, v) : hash32(vp, v);
+        bool rk = false, rv = false;
+        uint64_t ek = 0, ev = 0;
+        const uint64_t si = tab_claim(kt, kh, kp, k, (uint32_t)j, PendGet{c, false}, &rk, &ek, ksv, SM != 0);
+        if (si == kEmptyE) {
+            full = true;
+        } else {
+            if (!rk && !((uint32_t)ek & kPend)) {            // an existing id
+                const uint32_t kid = (uint32_t)ek & kIdMask;
+                if (kid >= key_cap) host = true;
+                kv_key[kv_base + j] = d.slot_base + kid;
+            } else {
+                ks = (uint32_t)si | (rk ? kRepBit : 0u);
+                nk += rk;
+            }
+        }
+        const uint64_t sv = tab_claim(vt, vh, vp, v, (uint32_t)j, PendGet{c, true}, &rv, &ev, vsv, SM != 0);
+        if (sv == kEmptyE) {
+            full = true;
+        } else {
+            if (!rv && !((uint32_t)ev & kPend)) {
+                kv_val[kv_base + j] = (uint32_t)ev & kIdMask;
+            } else {
+                vs = (uint32_t)sv | (rv ? kRepBit : 0u);
+                nv += rv;
+            }
+        }
+        kslot[j] = ks;
+        vslot[j] = vs;
+    };
+    if (SM == 2) {
+        if (threadIdx.x == 0) s_ns = 0;
+        __syncthreads();
+    }
     for (uint64_t q = (uint64_t)blockIdx.x * kClaimChunk + threadIdx.x;
          q < d.np && q < (uint64_t)(blockIdx.x + 1) * kClaimChunk; q += 256) {
         const uint64_t j = d.q0 + q;
@@ -546,54 +597,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             continue;
         }
         const uint64_t o = c.boff[j] - o0, k = c.klen[j], v = c.boff[j + 1] - c.boff[j] - k;
-        uint32_t ks = kEmptyE32, vs = kEmptyE32;
         if (o > d.nb || k > d.nb - o || v > d.nb - o - k) {
             bad = true;
-        } else {
-            const uint8_t *kp = region + o, *vp = region + o + k;
-            // short strings (the reference's one-byte keys and short values)
-            // packed in registers: one word load each, hash and compares on it
-            const uint64_t ksv = k <= 8 ? load_short(kp, (uint32_t)k) : 0, vsv = v <= 8 ? load_short(vp, (uint32_t)v) : 0;
-            if (q && !first[j]) {                            // keys of an entry strictly ascending
-                const uint64_t po = c.boff[j - 1] - o0, pk = c.klen[j - 1];
-                if (po + pk <= o) {
-                    const bool lt = pk <= 8 && k <= 8
-                                        ? short_lt(load_short(region + po, (uint32_t)pk), (uint32_t)pk, ksv, (uint32_t)k)
-                                        : bytes_lt(region + po, (uint32_t)pk, kp, (uint32_t)k);
-                    if (!lt) host = true;
-                }
-            }
-            const uint32_t kh = k <= 8 ? hash32_short(ksv, (uint32_t)k) : hash32(kp, (uint32_t)k);
-            const uint32_t vh = v <= 8 ? hash32_short(vsv, (uint32_t)v) : hash32(vp, (uint32_t)v);
-            bool rk = false, rv = false;
-            uint64_t ek = 0, ev = 0;
-            const uint64_t si = tab_claim(kt, kh, kp, (uint32_t)k, (uint32_t)j, PendGet{c, false}, &rk, &ek, ksv, SHORT);
-            if (si == kEmptyE) {
-                full = true;
-            } else {
-                if (!rk && !((uint32_t)ek & kPend)) {        // an existing id
-                    const uint32_t kid = (uint32_t)ek & kIdMask;
-                    if (kid >= key_cap) host = true;
-                    kv_key[kv_base + j] = d.slot_base + kid;
-                } else {
-                    ks = (uint32_t)si | (rk ? kRepBit : 0u);
-                    nk += rk;
-                }
-            }
-            const uint64_t sv = tab_claim(vt, vh, vp, (uint32_t)v, (uint32_t)j, PendGet{c, true}, &rv, &ev, vsv, SHORT);
-            if (sv == kEmptyE) {
-                full = true;
-            } else {
-                if (!rv && !((uint32_t)ev & kPend)) {
-                    kv_val[kv_base + j] = (uint32_t)ev & kIdMask;
-                } else {
-                    vs = (uint32_t)sv | (rv ? kRepBit : 0u);
-                    nv += rv;
-                }
+            kslot[j] = vslot[j] = kEmptyE32;
+            continue;
+        }
+        const uint8_t *kp = region + o, *vp = region + o + k;
+        // short strings (the reference's one-byte keys and short values)
+        // packed in registers: one word load each, hash and compares on it
+        const uint64_t ksv = k <= 8 ? load_short(kp, (uint32_t)k) : 0, vsv = v <= 8 ? load_short(vp, (uint32_t)v) : 0;
+        if (q && !first[j]) {                                // keys of an entry strictly ascending
+            const uint64_t po = c.boff[j - 1] - o0, pk = c.klen[j - 1];
+            if (po + pk <= o) {
+                const bool lt = pk <= 8 && k <= 8
+                                    ? short_lt(load_short(region + po, (uint32_t)pk), (uint32_t)pk, ksv, (uint32_t)k)
+                                    : bytes_lt(region + po, (uint32_t)pk, kp, (uint32_t)k);
+                if (!lt) host = true;
             }
         }
-        kslot[j] = ks;
-        vslot[j] = vs;
+        if constexpr (SM == 2) {
+            bool done = false;
+            if (k <= 7 && v <= 7) {                          // both home entries, one round trip
+                const uint64_t wk = short_form(ksv, (uint32_t)k), wv = short_form(vsv, (uint32_t)v);
+                const uint64_t ik = hash32_short(ksv, (uint32_t)k) & kt.mask, iv = hash32_short(vsv, (uint32_t)v) & vt.mask;
+                const uint64_t hk = kt.tab[ik], sk = kt.tab[kt.mask + 1 + ik];
+                const uint64_t hv = vt.tab[iv], sw = vt.tab[vt.mask + 1 + iv];
+                // (a short form is written with its entry's id: a match is a resolved entry)
+                if (sk == wk && sw == wv) {
+                    const uint32_t kid = (uint32_t)hk & kIdMask;
+                    if (kid >= key_cap) host = true;
+                    kv_key[kv_base + j] = d.slot_base + kid;
+                    kv_val[kv_base + j] = (uint32_t)hv & kIdMask;
+                    kslot[j] = vslot[j] = kEmptyE32;
+                    done = true;
+                }
+            }
+            if (!done) s_slow[atomicAdd(&s_ns, 1u)] = (uint32_t)(q - (uint64_t)blockIdx.x * kClaimChunk);
+        } else {
+            claim(j, kp, (uint32_t)k, ksv, vp, (uint32_t)v, vsv);
+        }
+    }
+    if constexpr (SM == 2) {                                 // the listed pairs, claimed as form 1 claims them
+        __syncthreads();
+        const uint32_t ns = s_ns;
+        for (uint32_t i = threadIdx.x; i < ns; i += 256) {
+            const uint64_t q = (uint64_t)blockIdx.x * kClaimChunk + s_slow[i], j = d.q0 + q;
+            const uint64_t o = c.boff[j] - o0, k = c.klen[j], v = c.boff[j + 1] - c.boff[j] - k;   // (in range: checked above)
+            const uint8_t *kp = region + o, *vp = region + o + k;
+            const uint64_t ksv = k <= 8 ? load_short(kp, (uint32_t)k) : 0, vsv = v <= 8 ? load_short(vp, (uint32_t)v) : 0;
+            claim(j, kp, (uint32_t)k, ksv, vp, (uint32_t)v, vsv);
+        }
     }
     const uint32_t fl = (bad ? kBodyMalformed : 0u) | (host ? kBodyHost : 0u) | (full ? kBodyFull : 0u);
     for (int m = 32; m >= 1; m >>= 1) {
@@ -1026,8 +1079,9 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
 #define DEC_CLAIM(SM)                                                                                          \
         k_dec_claim<SM><<<gc, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, key_cap, kv_base, kslot, vslot, \
                                            out->kv_key, out->kv_val, ctr)
-        if (g_short_tab) DEC_CLAIM(true);
-        else DEC_CLAIM(false);
+        if (g_short_tab == 2) DEC_CLAIM(2);
+        else if (g_short_tab == 1) DEC_CLAIM(1);
+        else DEC_CLAIM(0);
 #undef DEC_CLAIM
         rc = check_launch(ctx);
         if (rc) return rc;
