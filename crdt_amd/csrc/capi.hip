@@ -463,8 +463,8 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry (2: + both home probes first)
         if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_short_tab = (int)v;
-    } else if (!strcmp(name, "codec.small")) {   // gossip decode of few small bodies in one pass: 0 off, 1 auto, 2 always
-        if (v < 0 || v > 2) return CRDT_E_INVAL;
+    } else if (!strcmp(name, "codec.small")) {   // gossip decode in one pass: 0 off, 1 auto, 2 always, 3 always (coalesced form)
+        if (v < 0 || v > 3) return CRDT_E_INVAL;
         g_dec_small = (int)v;
     } else if (!strcmp(name, "refmerge.count_dma")) {   // RefMerge count pass: ts runs staged by LDS-DMA
         if (v != 0 && v != 1) return CRDT_E_INVAL;

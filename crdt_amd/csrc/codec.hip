@@ -463,6 +463,154 @@ __global__ __launch_bounds__(kSmallT) void k_dec_small(DecodeCtx c, int64_t *__r
         dec_small<false>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, d, wsum, b, entries);
 }
 
+// The same one-pass decode for large batches (codec.small = 3): dec_small's
+// per-thread item runs (kSmallR consecutive items, so its scans stay
+// thread-local) are uncoalesced -- each load and store instruction spans
+// 64 x kSmallR items.  Here every global access is coalesced (item
+// c0 + r kSmallT + tid) and only the scanned values change layout, through
+// one padded LDS buffer: the counts in, the prefixes out.
+constexpr uint32_t kBigCH = (uint32_t)kSmallT * kSmallR;
+__device__ __forceinline__ uint32_t big_pad(uint32_t i) { return i + (i >> 3); }
+
+template <bool AL, bool entries>
+__device__ __forceinline__ void dec_big(DecodeCtx c, int64_t *__restrict__ r_ts, uint32_t *__restrict__ klen,
+                                        uint64_t *__restrict__ boff, uint8_t *__restrict__ first, uint64_t n_e,
+                                        uint64_t n_p, uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                        uint64_t *__restrict__ r_off, const BodyDesc &d, uint64_t *wsum,
+                                        uint64_t *buf, uint32_t b) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    uint32_t *buf32 = reinterpret_cast<uint32_t *>(buf);
+    if (tid == 0 && entries) {
+        r_off[b] = d.e0;
+        if (b == 0) {
+            r_off[c.nbody] = n_e;
+            r_kv[n_e] = kv_base + n_p;
+        }
+    }
+    const uint8_t *base = body_ptr(c.data, d.data) + 32;
+    auto ld32 = [&](const uint8_t *p) { return AL ? *(const uint32_t *)p : le32(p); };
+    auto ld64 = [&](const uint8_t *p) { return AL ? *(const uint64_t *)p : le64(p); };
+    bool bad = false, host = false;
+    uint32_t multi = 0;
+    uint64_t carry = 0;
+    const uint64_t n = entries ? d.ne : d.np;
+    const uint8_t *pk = base + 12 * d.ne, *pv = pk + 4 * d.np;
+    for (uint64_t c0 = 0; c0 < n; c0 += kBigCH) {
+        // coalesced: the chunk's items, the outputs that need no scan, the counts into LDS
+        // (two rounds unrolled: a body at an unaligned address loads bytewise)
+#pragma unroll 2
+        for (int r = 0; r < kSmallR; ++r) {
+            const uint32_t li = (uint32_t)r * kSmallT + tid;
+            const uint64_t i = c0 + li;
+            uint32_t cnt = 0;
+            if constexpr (!entries) {
+                if (i < n) {
+                    const uint32_t kl = ld32(pk + 4 * i), vl = ld32(pv + 4 * i);
+                    const uint64_t x = (uint64_t)kl + vl;
+                    if (x > 0xFFFFFFFFull) bad = true;
+                    cnt = x > 0xFFFFFFFFull ? 0u : (uint32_t)x;
+                    klen[d.q0 + i] = kl;
+                }
+            } else {
+                int64_t ts = 0;
+                if (i < n) {
+                    ts = (int64_t)ld64(base + 8 * i);
+                    uint32_t kk = ld32(base + 8 * d.ne + 4 * i);
+                    if (kk == kNilPairs) {
+                        host = true;
+                        kk = 0;
+                    }
+                    r_ts[d.e0 + i] = ts;
+                    cnt = kk;
+                    multi += kk != 1;
+                }
+                // ts ascending: the previous item is the previous lane's (lane 0: a reload)
+                const int64_t up = (int64_t)__shfl_up((long long)ts, 1, 64);
+                if (i < n && i > 0) {
+                    const int64_t prev = lane ? up : (int64_t)ld64(base + 8 * (i - 1));
+                    if (prev >= ts) host = true;
+                }
+            }
+            buf32[big_pad(li)] = cnt;
+        }
+        __syncthreads();
+        // thread-consecutive: the counts, their block scan, the prefixes
+        uint32_t t[kSmallR];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            t[r] = buf32[big_pad(tid * kSmallR + r)];
+            sum += t[r];
+        }
+        uint64_t tot;
+        uint64_t run = carry + block1024_exclusive_scan(sum, &tot, wsum);   // (its barriers order the reads above)
+        const uint64_t i0 = c0 + (uint64_t)tid * kSmallR;
+        if constexpr (entries) {                          // each entry's pairs: 1 on its first (not unrolled)
+            uint64_t rr = run;
+#pragma unroll 1
+            for (int r = 0; r < kSmallR; ++r) {
+                if (i0 + r < n)
+                    for (uint32_t j = 0; j < t[r] && rr + j < d.np; ++j) first[d.q0 + rr + j] = j == 0;
+                rr += t[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kSmallR; ++r) {
+            buf[big_pad(tid * kSmallR + r)] = entries ? kv_base + d.q0 + run : d.y0 + run;
+            run += t[r];
+        }
+        carry += tot;
+        __syncthreads();
+        // coalesced: the prefixes out
+#pragma unroll 4
+        for (int r = 0; r < kSmallR; ++r) {
+            const uint32_t li = (uint32_t)r * kSmallT + tid;
+            const uint64_t i = c0 + li;
+            if (i < n) {
+                if (entries) r_kv[d.e0 + i] = buf[big_pad(li)];
+                else boff[d.q0 + i] = buf[big_pad(li)];
+            }
+        }
+        __syncthreads();                                 // (the buffer is the next chunk's)
+    }
+    if (!entries) {
+        if (carry != d.nb) bad = true;
+        if (tid == 0) boff[d.q0 + d.np] = d.y0 + d.nb;
+    } else if (carry != d.np) {
+        bad = true;
+    }
+    const uint32_t fl = (bad ? kBodyMalformed : 0u) | (host ? kBodyHost : 0u);
+    uint32_t wfl = fl;
+    for (int m = 32; m >= 1; m >>= 1) {
+        wfl |= __shfl_xor(wfl, m, 64);
+        multi += __shfl_xor(multi, m, 64);
+    }
+    if (lane == 0 && wfl) atomicOr(&c.flag[b], wfl);
+    if (lane == 0 && multi && c.multi) atomicAdd(c.multi, (unsigned long long)multi);
+}
+
+__global__ __launch_bounds__(kSmallT) void k_dec_big(DecodeCtx c, int64_t *__restrict__ r_ts,
+                                                     uint32_t *__restrict__ klen, uint64_t *__restrict__ boff,
+                                                     uint8_t *__restrict__ first, uint64_t n_e, uint64_t n_p,
+                                                     uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                                     uint64_t *__restrict__ r_off) {
+    __shared__ uint64_t wsum[kSmallT / 64];
+    __shared__ uint64_t buf[kBigCH + kBigCH / 8];
+    const uint32_t b = blockIdx.x >> 1;                  // two workgroups per body: its pairs, its entries
+    const bool entries = blockIdx.x & 1;
+    const BodyDesc d = c.bd[b];
+#define DEC_BIG(AL, EN) dec_big<AL, EN>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, d, wsum, buf, b)
+    const bool al = (((uintptr_t)body_ptr(c.data, d.data)) & 7) == 0;
+    if (entries) {
+        if (al) DEC_BIG(true, true);
+        else DEC_BIG(false, true);
+    } else {
+        if (al) DEC_BIG(true, false);
+        else DEC_BIG(false, false);
+    }
+#undef DEC_BIG
+}
+
 struct CountSrc32 {
     const uint32_t *in;
     struct Item {
@@ -1036,15 +1184,29 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
         max_ne = std::max(max_ne, x.ne);
         max_np = std::max(max_np, x.np);
     }
-    const bool small = g_dec_small == 2 || (g_dec_small == 1 && nb <= (uint32_t)ctx->num_cus &&
-                                            max_ne <= kSmallItems && max_np <= kSmallItems);
+    // decode form (codec.small): 0 the multi-pass kernels, 2 the one-pass
+    // kernel, 3 its coalesced form; 1 (auto): the one-pass kernel for a few
+    // small bodies (the Server path), the coalesced form for many bodies of
+    // up to two chunks each (the population wire rounds: DESIGN.md §5.10),
+    // the multi-pass kernels otherwise
+    int form = g_dec_small;
+    if (form == 1)
+        form = nb <= (uint32_t)ctx->num_cus && max_ne <= kSmallItems && max_np <= kSmallItems ? 2
+               : max_ne <= 2 * kBigCH && max_np <= 2 * kBigCH                                ? 3
+                                                                                              : 0;
+    const bool small = form >= 2;
     e = hipMemcpyAsync(d_head, h_head, head, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && !small) e = hipMemcpyAsync(out->r_off, h_roff, (nb + 1) * 8, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(ctx, e);
     const dim3 ge((unsigned)std::max<uint64_t>((max_ne + kChunk - 1) / kChunk, 1), nb);
     const dim3 gp((unsigned)std::max<uint64_t>((max_np + kChunk - 1) / kChunk, 1), nb);
     const unsigned cap = (unsigned)ctx->num_cus * 8;
-    if (small) {
+    if (form == 3) {
+        k_dec_big<<<2 * nb, kSmallT, 0, s>>>(c, out->r_ts, klen, boff, first, n_e, n_p, kv_base, out->r_kv,
+                                         out->r_off);
+        rc = check_launch(ctx);
+        if (rc) return rc;
+    } else if (small) {
         k_dec_small<<<2 * nb, kSmallT, 0, s>>>(c, out->r_ts, klen, boff, first, n_e, n_p, kv_base, out->r_kv,
                                            out->r_off);
         rc = check_launch(ctx);

@@ -20,10 +20,11 @@ from gossip_util import K, KEYS, STRS, _host_round, _pack, _rand_diff, _same_dif
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[2, 0], ids=["one_pass", "multi_pass"], autouse=True)
+@pytest.fixture(params=[2, 0, 3], ids=["one_pass", "multi_pass", "one_pass_coalesced"], autouse=True)
 def decode_form(request, eng):
-    """Every test under both decode forms: the one-pass small-body kernel
-    (codec.small = 2: always) and the multi-pass form (0)."""
+    """Every test under each decode form: the one-pass small-body kernel
+    (codec.small = 2: always), the multi-pass form (0) and the one-pass form
+    with coalesced accesses (3)."""
     from crdt_amd import _lib
     _lib.call("crdt_set_option", b"codec.small", request.param)
     yield request.param
@@ -228,7 +229,7 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
         bodies.append(_serve(d))
     bodies.insert(1, _raw_body([(1, [(b"a", b"1")])]) + b"")     # shifts the next body off 8-byte alignment
     out = []
-    for form in (0, 2):
+    for form in (0, 2, 3):
         _lib.call("crdt_set_option", b"codec.small", form)
         keys, vals = codec.StrTab(eng), codec.StrTab(eng)
         dec, st, kk, kv = _decode(eng, bodies, keys, vals)
@@ -239,11 +240,13 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
                  for q in range(h["r_kv"][h["r_off"][bi]], h["r_kv"][h["r_off"][bi + 1]])]
         out.append((st.tolist(), h, pairs, sorted(ks), sorted(vs)))
     _lib.call("crdt_set_option", b"codec.small", decode_form)
-    a, b = out
-    assert a[0] == b[0] == [0, 0, 0, 0]
-    for x in a[1]:
-        np.testing.assert_array_equal(a[1][x], b[1][x], err_msg=x)
-    assert a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+    a = out[0]
+    assert a[0] == [0, 0, 0, 0]
+    for b in out[1:]:
+        assert b[0] == a[0]
+        for x in a[1]:
+            np.testing.assert_array_equal(a[1][x], b[1][x], err_msg=x)
+        assert a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
     r_off, r_ts = a[1]["r_off"], a[1]["r_ts"]
     host = Server(None, 9000)
     assert host.IngestBinary(bodies[0]) == 0
