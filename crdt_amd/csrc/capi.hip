@@ -23,6 +23,7 @@ int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
 int g_short_tab = 2;
+int g_dec_big_r = 4;
 int g_dec_small = 1;
 int g_rm_kvx = 0;
 int g_rm_ld_all = 0;
@@ -463,6 +464,9 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
     } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry (2: + both home probes first)
         if (v < 0 || v > 2) return CRDT_E_INVAL;
         g_short_tab = (int)v;
+    } else if (!strcmp(name, "codec.big_r")) {   // the coalesced one-pass decode: items per thread per chunk
+        if (v != 4 && v != 8) return CRDT_E_INVAL;
+        g_dec_big_r = (int)v;
     } else if (!strcmp(name, "codec.small")) {   // gossip decode in one pass: 0 off, 1 auto, 2 always, 3 always (coalesced form)
         if (v < 0 || v > 3) return CRDT_E_INVAL;
         g_dec_small = (int)v;

@@ -469,15 +469,41 @@ __global__ __launch_bounds__(kSmallT) void k_dec_small(DecodeCtx c, int64_t *__r
 // 64 x kSmallR items.  Here every global access is coalesced (item
 // c0 + r kSmallT + tid) and only the scanned values change layout, through
 // one padded LDS buffer: the counts in, the prefixes out.
-constexpr uint32_t kBigCH = (uint32_t)kSmallT * kSmallR;
+constexpr uint32_t kBigCH = (uint32_t)kSmallT * kSmallR;   // items per chunk at R = kSmallR (the LDS buffer's size)
 __device__ __forceinline__ uint32_t big_pad(uint32_t i) { return i + (i >> 3); }
+// block1024_exclusive_scan with the per-wave sums combined by shuffles (the
+// sixteen sums in lanes, not in sixteen registers of every thread)
+__device__ __forceinline__ uint64_t big_exclusive_scan(uint64_t v, uint64_t *total, uint64_t *wsum) {
+    constexpr int NW = kSmallT / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    const uint64_t ws = lane < NW ? wsum[lane] : 0;
+    uint64_t z = ws;
+#pragma unroll
+    for (int d = 1; d < NW; d <<= 1) {
+        const uint64_t y = __shfl_up(z, d, 64);
+        if (lane >= d) z += y;
+    }
+    const uint64_t off = __shfl(z - ws, w, 64);         // the sums of the waves before this one
+    *total = __shfl(z, NW - 1, 64);
+    __syncthreads();                                     // (wsum is the next call's)
+    return off + x - v;
+}
 
-template <bool AL, bool entries>
+template <int R, bool AL, bool entries>
 __device__ __forceinline__ void dec_big(DecodeCtx c, int64_t *__restrict__ r_ts, uint32_t *__restrict__ klen,
                                         uint64_t *__restrict__ boff, uint8_t *__restrict__ first, uint64_t n_e,
                                         uint64_t n_p, uint64_t kv_base, uint64_t *__restrict__ r_kv,
                                         uint64_t *__restrict__ r_off, const BodyDesc &d, uint64_t *wsum,
                                         uint64_t *buf, uint32_t b) {
+    constexpr uint32_t CH = (uint32_t)kSmallT * R;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     uint32_t *buf32 = reinterpret_cast<uint32_t *>(buf);
     if (tid == 0 && entries) {
@@ -495,11 +521,11 @@ __device__ __forceinline__ void dec_big(DecodeCtx c, int64_t *__restrict__ r_ts,
     uint64_t carry = 0;
     const uint64_t n = entries ? d.ne : d.np;
     const uint8_t *pk = base + 12 * d.ne, *pv = pk + 4 * d.np;
-    for (uint64_t c0 = 0; c0 < n; c0 += kBigCH) {
+    for (uint64_t c0 = 0; c0 < n; c0 += CH) {
         // coalesced: the chunk's items, the outputs that need no scan, the counts into LDS
         // (two rounds unrolled: a body at an unaligned address loads bytewise)
 #pragma unroll 2
-        for (int r = 0; r < kSmallR; ++r) {
+        for (int r = 0; r < R; ++r) {
             const uint32_t li = (uint32_t)r * kSmallT + tid;
             const uint64_t i = c0 + li;
             uint32_t cnt = 0;
@@ -535,35 +561,35 @@ __device__ __forceinline__ void dec_big(DecodeCtx c, int64_t *__restrict__ r_ts,
         }
         __syncthreads();
         // thread-consecutive: the counts, their block scan, the prefixes
-        uint32_t t[kSmallR];
+        uint32_t t[R];
         uint64_t sum = 0;
 #pragma unroll
-        for (int r = 0; r < kSmallR; ++r) {
-            t[r] = buf32[big_pad(tid * kSmallR + r)];
+        for (int r = 0; r < R; ++r) {
+            t[r] = buf32[big_pad(tid * R + r)];
             sum += t[r];
         }
         uint64_t tot;
-        uint64_t run = carry + block1024_exclusive_scan(sum, &tot, wsum);   // (its barriers order the reads above)
-        const uint64_t i0 = c0 + (uint64_t)tid * kSmallR;
+        uint64_t run = carry + big_exclusive_scan(sum, &tot, wsum);   // (its barriers order the reads above)
+        const uint64_t i0 = c0 + (uint64_t)tid * R;
         if constexpr (entries) {                          // each entry's pairs: 1 on its first (not unrolled)
             uint64_t rr = run;
 #pragma unroll 1
-            for (int r = 0; r < kSmallR; ++r) {
+            for (int r = 0; r < R; ++r) {
                 if (i0 + r < n)
                     for (uint32_t j = 0; j < t[r] && rr + j < d.np; ++j) first[d.q0 + rr + j] = j == 0;
                 rr += t[r];
             }
         }
 #pragma unroll
-        for (int r = 0; r < kSmallR; ++r) {
-            buf[big_pad(tid * kSmallR + r)] = entries ? kv_base + d.q0 + run : d.y0 + run;
+        for (int r = 0; r < R; ++r) {
+            buf[big_pad(tid * R + r)] = entries ? kv_base + d.q0 + run : d.y0 + run;
             run += t[r];
         }
         carry += tot;
         __syncthreads();
         // coalesced: the prefixes out
 #pragma unroll 4
-        for (int r = 0; r < kSmallR; ++r) {
+        for (int r = 0; r < R; ++r) {
             const uint32_t li = (uint32_t)r * kSmallT + tid;
             const uint64_t i = c0 + li;
             if (i < n) {
@@ -589,17 +615,16 @@ __device__ __forceinline__ void dec_big(DecodeCtx c, int64_t *__restrict__ r_ts,
     if (lane == 0 && multi && c.multi) atomicAdd(c.multi, (unsigned long long)multi);
 }
 
-__global__ __launch_bounds__(kSmallT) void k_dec_big(DecodeCtx c, int64_t *__restrict__ r_ts,
-                                                     uint32_t *__restrict__ klen, uint64_t *__restrict__ boff,
-                                                     uint8_t *__restrict__ first, uint64_t n_e, uint64_t n_p,
-                                                     uint64_t kv_base, uint64_t *__restrict__ r_kv,
-                                                     uint64_t *__restrict__ r_off) {
-    __shared__ uint64_t wsum[kSmallT / 64];
-    __shared__ uint64_t buf[kBigCH + kBigCH / 8];
+// R = 4 fits 64 VGPRs (two workgroups per CU); R = 8 takes 79 (one)
+template <int R>
+__device__ __forceinline__ void dec_big_body(DecodeCtx c, int64_t *__restrict__ r_ts, uint32_t *__restrict__ klen,
+                                             uint64_t *__restrict__ boff, uint8_t *__restrict__ first, uint64_t n_e,
+                                             uint64_t n_p, uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                             uint64_t *__restrict__ r_off, uint64_t *wsum, uint64_t *buf) {
     const uint32_t b = blockIdx.x >> 1;                  // two workgroups per body: its pairs, its entries
     const bool entries = blockIdx.x & 1;
     const BodyDesc d = c.bd[b];
-#define DEC_BIG(AL, EN) dec_big<AL, EN>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, d, wsum, buf, b)
+#define DEC_BIG(AL, EN) dec_big<R, AL, EN>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, d, wsum, buf, b)
     const bool al = (((uintptr_t)body_ptr(c.data, d.data)) & 7) == 0;
     if (entries) {
         if (al) DEC_BIG(true, true);
@@ -609,6 +634,23 @@ __global__ __launch_bounds__(kSmallT) void k_dec_big(DecodeCtx c, int64_t *__res
         else DEC_BIG(false, false);
     }
 #undef DEC_BIG
+}
+__global__ __launch_bounds__(kSmallT) __attribute__((amdgpu_waves_per_eu(8))) void k_dec_big4(
+    DecodeCtx c, int64_t *__restrict__ r_ts, uint32_t *__restrict__ klen, uint64_t *__restrict__ boff,
+    uint8_t *__restrict__ first, uint64_t n_e, uint64_t n_p, uint64_t kv_base, uint64_t *__restrict__ r_kv,
+    uint64_t *__restrict__ r_off) {
+    __shared__ uint64_t wsum[kSmallT / 64];
+    __shared__ uint64_t buf[kBigCH / 2 + kBigCH / 16];
+    dec_big_body<4>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, wsum, buf);
+}
+__global__ __launch_bounds__(kSmallT) void k_dec_big8(DecodeCtx c, int64_t *__restrict__ r_ts,
+                                                      uint32_t *__restrict__ klen, uint64_t *__restrict__ boff,
+                                                      uint8_t *__restrict__ first, uint64_t n_e, uint64_t n_p,
+                                                      uint64_t kv_base, uint64_t *__restrict__ r_kv,
+                                                      uint64_t *__restrict__ r_off) {
+    __shared__ uint64_t wsum[kSmallT / 64];
+    __shared__ uint64_t buf[kBigCH + kBigCH / 8];
+    dec_big_body<8>(c, r_ts, klen, boff, first, n_e, n_p, kv_base, r_kv, r_off, wsum, buf);
 }
 
 struct CountSrc32 {
@@ -1202,8 +1244,12 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     const dim3 gp((unsigned)std::max<uint64_t>((max_np + kChunk - 1) / kChunk, 1), nb);
     const unsigned cap = (unsigned)ctx->num_cus * 8;
     if (form == 3) {
-        k_dec_big<<<2 * nb, kSmallT, 0, s>>>(c, out->r_ts, klen, boff, first, n_e, n_p, kv_base, out->r_kv,
-                                         out->r_off);
+        if (g_dec_big_r == 8)
+            k_dec_big8<<<2 * nb, kSmallT, 0, s>>>(c, out->r_ts, klen, boff, first, n_e, n_p, kv_base, out->r_kv,
+                                              out->r_off);
+        else
+            k_dec_big4<<<2 * nb, kSmallT, 0, s>>>(c, out->r_ts, klen, boff, first, n_e, n_p, kv_base, out->r_kv,
+                                              out->r_off);
         rc = check_launch(ctx);
         if (rc) return rc;
     } else if (small) {

@@ -107,6 +107,7 @@ extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refme
 extern int g_rm_ld_all;        // RefMerge tile pass: load non-emitted entries too (refmerge.load_all, A/B)
 extern int g_rm_kvx;           // RefMerge kv tile pass in one launch at any grid (refmerge.kv_one_launch)
 extern int g_short_tab;        // string-table lookups compare the short form beside the entry (codec.short_tab)
+extern int g_dec_big_r;        // the coalesced one-pass decode: items per thread per chunk, 4 or 8 (codec.big_r)
 extern int g_dec_small;        // gossip decode of few small bodies in one pass (codec.small)
 extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmerge.count_dma)
 extern int g_lww_chunk;         // set merges: tiles per count / write chunk (sets.lww_chunk, sets.or_chunk;

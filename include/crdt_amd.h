@@ -85,7 +85,7 @@ int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
  * "refmerge.tile_parts", "refmerge.count_dma", the D2 forms' "sort.*"
  * (e.g. "sort.plan_cache" 0/1/2, "sort.group_tile" 4096/8192,
  * "sort.or_lb_words" 1/4), "pop.direct", "codec.small" (0 multi-pass,
- * 1 auto, 2 one-pass, 3 one-pass coalesced),
+ * 1 auto, 2 one-pass, 3 one-pass coalesced), "codec.big_r" (4/8),
  * "codec.short_tab" (0/1/2: string-table lookups compare the short form
  * stored beside the entry; 2 probes a pair's key and value homes at once);
  * fault injection: "fail.refmerge" (n: the next n RefMerge calls return
