@@ -22,7 +22,7 @@ int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within 
 int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
 int g_rm_parts = 1;
 int g_rm_count_dma = 1;
-int g_short_tab = 2;
+int g_short_tab = 3;
 int g_dec_big_r = 4;
 int g_dec_small = 1;
 int g_rm_kvx = 0;
@@ -462,7 +462,7 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_rm_kvx = (int)v;
     } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry (2: + both home probes first)
-        if (v < 0 || v > 2) return CRDT_E_INVAL;
+        if (v < 0 || v > 3) return CRDT_E_INVAL;
         g_short_tab = (int)v;
     } else if (!strcmp(name, "codec.big_r")) {   // the coalesced one-pass decode: items per thread per chunk
         if (v != 4 && v != 8) return CRDT_E_INVAL;

@@ -726,8 +726,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                                                    uint64_t kv_base, uint32_t *__restrict__ kslot,
                                                    uint32_t *__restrict__ vslot, uint32_t *__restrict__ kv_key,
                                                    uint32_t *__restrict__ kv_val, unsigned long long *__restrict__ ctr) {
-    static_assert(kClaimChunk == 256, "one pair per thread: the slow list holds a workgroup's pairs");
-    __shared__ uint32_t s_slow[SM == 2 ? kClaimChunk : 1];
+    static_assert(kClaimChunk == 256, "one pair per thread (form 3: two)");
+    constexpr uint32_t CC = SM == 3 ? 2 * kClaimChunk : kClaimChunk;   // pairs per workgroup
+    __shared__ uint32_t s_slow[SM >= 2 ? CC : 1];
     __shared__ uint32_t s_ns;
     const uint32_t b = blockIdx.y;
     const BodyDesc d = c.bd[b];
@@ -775,12 +776,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         kslot[j] = ks;
         vslot[j] = vs;
     };
-    if (SM == 2) {
+    if (SM >= 2) {
         if (threadIdx.x == 0) s_ns = 0;
         __syncthreads();
     }
+    if constexpr (SM == 3) {
+        // form 3: two pairs per thread, each step's loads issued for both
+        // before either is used (the chain is paid once for two pairs)
+        constexpr int PP = 2;
+        const uint64_t qb = (uint64_t)blockIdx.x * CC + threadIdx.x;
+        bool act[PP];
+        uint64_t b0[PP], b1[PP], ksv[PP], vsv[PP], hk[PP], sk[PP], hv[PP], sw[PP];
+        uint32_t kl[PP], vl[PP];
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {
+            const uint64_t q = qb + 256 * p, j = d.q0 + q;
+            act[p] = q < d.np && !rejected;
+            if (q < d.np && rejected) kslot[j] = vslot[j] = kEmptyE32;
+            b0[p] = act[p] ? c.boff[j] : 0;
+            b1[p] = act[p] ? c.boff[j + 1] : 0;
+            kl[p] = act[p] ? c.klen[j] : 0;
+        }
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {
+            const uint64_t j = d.q0 + qb + 256 * p;
+            const uint64_t o = b0[p] - o0, k = kl[p], v = b1[p] - b0[p] - k;
+            if (act[p] && (o > d.nb || k > d.nb - o || v > d.nb - o - k)) {
+                bad = true;
+                kslot[j] = vslot[j] = kEmptyE32;
+                act[p] = false;
+            }
+            vl[p] = (uint32_t)v;
+            ksv[p] = act[p] && k <= 8 ? load_short(region + o, (uint32_t)k) : 0;
+            vsv[p] = act[p] && v <= 8 ? load_short(region + o + k, (uint32_t)v) : 0;
+        }
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {
+            const uint64_t q = qb + 256 * p, j = d.q0 + q;
+            if (act[p] && q && !first[j]) {                  // keys of an entry strictly ascending
+                const uint64_t o = b0[p] - o0, k = kl[p];
+                const uint64_t po = c.boff[j - 1] - o0, pk = c.klen[j - 1];
+                if (po + pk <= o) {
+                    const bool lt = pk <= 8 && k <= 8
+                                        ? short_lt(load_short(region + po, (uint32_t)pk), (uint32_t)pk, ksv[p], (uint32_t)k)
+                                        : bytes_lt(region + po, (uint32_t)pk, region + o, (uint32_t)k);
+                    if (!lt) host = true;
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {                       // both pairs' home entries, one round trip
+            hk[p] = sk[p] = hv[p] = sw[p] = kNoShort;
+            if (act[p] && kl[p] <= 7 && vl[p] <= 7) {
+                const uint64_t ik = hash32_short(ksv[p], kl[p]) & kt.mask, iv = hash32_short(vsv[p], vl[p]) & vt.mask;
+                hk[p] = kt.tab[ik];
+                sk[p] = kt.tab[kt.mask + 1 + ik];
+                hv[p] = vt.tab[iv];
+                sw[p] = vt.tab[vt.mask + 1 + iv];
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PP; ++p) {
+            if (!act[p]) continue;
+            const uint64_t j = d.q0 + qb + 256 * p;
+            // (a short form is written with its entry's id: a match is a resolved entry)
+            if (kl[p] <= 7 && vl[p] <= 7 && sk[p] == short_form(ksv[p], kl[p]) && sw[p] == short_form(vsv[p], vl[p])) {
+                const uint32_t kid = (uint32_t)hk[p] & kIdMask;
+                if (kid >= key_cap) host = true;
+                kv_key[kv_base + j] = d.slot_base + kid;
+                kv_val[kv_base + j] = (uint32_t)hv[p] & kIdMask;
+                kslot[j] = vslot[j] = kEmptyE32;
+            } else {
+                s_slow[atomicAdd(&s_ns, 1u)] = threadIdx.x + 256u * p;
+            }
+        }
+    }
     for (uint64_t q = (uint64_t)blockIdx.x * kClaimChunk + threadIdx.x;
-         q < d.np && q < (uint64_t)(blockIdx.x + 1) * kClaimChunk; q += 256) {
+         SM != 3 && q < d.np && q < (uint64_t)(blockIdx.x + 1) * kClaimChunk; q += 256) {
         const uint64_t j = d.q0 + q;
         if (rejected) {
             kslot[j] = vslot[j] = kEmptyE32;
@@ -827,11 +899,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             claim(j, kp, (uint32_t)k, ksv, vp, (uint32_t)v, vsv);
         }
     }
-    if constexpr (SM == 2) {                                 // the listed pairs, claimed as form 1 claims them
+    if constexpr (SM >= 2) {                                 // the listed pairs, claimed as form 1 claims them
         __syncthreads();
         const uint32_t ns = s_ns;
         for (uint32_t i = threadIdx.x; i < ns; i += 256) {
-            const uint64_t q = (uint64_t)blockIdx.x * kClaimChunk + s_slow[i], j = d.q0 + q;
+            const uint64_t q = (uint64_t)blockIdx.x * CC + s_slow[i], j = d.q0 + q;
             const uint64_t o = c.boff[j] - o0, k = c.klen[j], v = c.boff[j + 1] - c.boff[j] - k;   // (in range: checked above)
             const uint8_t *kp = region + o, *vp = region + o + k;
             const uint64_t ksv = k <= 8 ? load_short(kp, (uint32_t)k) : 0, vsv = v <= 8 ? load_short(vp, (uint32_t)v) : 0;
@@ -1283,11 +1355,13 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
     TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
-        const dim3 gc((unsigned)std::max<uint64_t>((max_np + kClaimChunk - 1) / kClaimChunk, 1), nb);
+        const uint64_t cc = g_short_tab == 3 ? 2 * kClaimChunk : kClaimChunk;   // pairs per claim workgroup
+        const dim3 gc((unsigned)std::max<uint64_t>((max_np + cc - 1) / cc, 1), nb);
 #define DEC_CLAIM(SM)                                                                                          \
         k_dec_claim<SM><<<gc, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, key_cap, kv_base, kslot, vslot, \
                                            out->kv_key, out->kv_val, ctr)
-        if (g_short_tab == 2) DEC_CLAIM(2);
+        if (g_short_tab == 3) DEC_CLAIM(3);
+        else if (g_short_tab == 2) DEC_CLAIM(2);
         else if (g_short_tab == 1) DEC_CLAIM(1);
         else DEC_CLAIM(0);
 #undef DEC_CLAIM

@@ -254,7 +254,7 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
     host.close()
 
 
-@pytest.mark.parametrize("short_tab", [2, 1, 0])
+@pytest.mark.parametrize("short_tab", [2, 3, 1, 0])
 def test_decode_resolved_short_forms_across_calls_and_rehash(eng, short_tab):
     """Strings of <= 7 bytes resolved in an earlier call are found by the
     short form stored beside their table entry (codec.short_tab, written with
@@ -287,4 +287,4 @@ def test_decode_resolved_short_forms_across_calls_and_rehash(eng, short_tab):
         assert [vs[kv1[3 + i]] for i in range(n)] == strs              # kv_base 3: pair i of entry i
         assert [ks[kk1[3 + n + i]] for i in range(n - 1)] == sorted(set(strs) - {b""})
     finally:
-        _lib.call("crdt_set_option", b"codec.short_tab", 2)
+        _lib.call("crdt_set_option", b"codec.short_tab", 3)
