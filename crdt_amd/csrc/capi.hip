@@ -462,7 +462,7 @@ extern "C" int crdt_set_option(const char *name, int64_t v) {
         if (v != 0 && v != 1) return CRDT_E_INVAL;
         g_rm_kvx = (int)v;
     } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry (2: + both home probes first)
-        if (v < 0 || v > 3) return CRDT_E_INVAL;
+        if (v < 0 || v > 4) return CRDT_E_INVAL;
         g_short_tab = (int)v;
     } else if (!strcmp(name, "codec.big_r")) {   // the coalesced one-pass decode: items per thread per chunk
         if (v != 4 && v != 8) return CRDT_E_INVAL;

@@ -726,8 +726,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                                                    uint64_t kv_base, uint32_t *__restrict__ kslot,
                                                    uint32_t *__restrict__ vslot, uint32_t *__restrict__ kv_key,
                                                    uint32_t *__restrict__ kv_val, unsigned long long *__restrict__ ctr) {
-    static_assert(kClaimChunk == 256, "one pair per thread (form 3: two)");
-    constexpr uint32_t CC = SM == 3 ? 2 * kClaimChunk : kClaimChunk;   // pairs per workgroup
+    static_assert(kClaimChunk == 256, "one pair per thread (forms 3 / 4: two / three)");
+    constexpr int PP = SM == 4 ? 3 : 2;                      // forms 3 / 4: pairs per thread
+    constexpr uint32_t CC = SM >= 3 ? PP * kClaimChunk : kClaimChunk;   // pairs per workgroup
     __shared__ uint32_t s_slow[SM >= 2 ? CC : 1];
     __shared__ uint32_t s_ns;
     const uint32_t b = blockIdx.y;
@@ -780,10 +781,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         if (threadIdx.x == 0) s_ns = 0;
         __syncthreads();
     }
-    if constexpr (SM == 3) {
-        // form 3: two pairs per thread, each step's loads issued for both
-        // before either is used (the chain is paid once for two pairs)
-        constexpr int PP = 2;
+    if constexpr (SM >= 3) {
+        // forms 3 / 4: two / three pairs per thread, each step's loads issued
+        // for all of them before any is used (the chain is paid once for all)
         const uint64_t qb = (uint64_t)blockIdx.x * CC + threadIdx.x;
         bool act[PP];
         uint64_t b0[PP], b1[PP], ksv[PP], vsv[PP], hk[PP], sk[PP], hv[PP], sw[PP];
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         }
     }
     for (uint64_t q = (uint64_t)blockIdx.x * kClaimChunk + threadIdx.x;
-         SM != 3 && q < d.np && q < (uint64_t)(blockIdx.x + 1) * kClaimChunk; q += 256) {
+         SM < 3 && q < d.np && q < (uint64_t)(blockIdx.x + 1) * kClaimChunk; q += 256) {
         const uint64_t j = d.q0 + q;
         if (rejected) {
             kslot[j] = vslot[j] = kEmptyE32;
@@ -1355,12 +1355,13 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     TabView kt{keys->tab, keys->H - 1, keys->bytes, keys->off};
     TabView vt{vals->tab, vals->H - 1, vals->bytes, vals->off};
     if (n_p) {
-        const uint64_t cc = g_short_tab == 3 ? 2 * kClaimChunk : kClaimChunk;   // pairs per claim workgroup
+        const uint64_t cc = (g_short_tab == 4 ? 3 : g_short_tab == 3 ? 2 : 1) * kClaimChunk;   // pairs per claim workgroup
         const dim3 gc((unsigned)std::max<uint64_t>((max_np + cc - 1) / cc, 1), nb);
 #define DEC_CLAIM(SM)                                                                                          \
         k_dec_claim<SM><<<gc, 256, 0, s>>>(c, kt, vt, first, d_flag, d_flag + nb, key_cap, kv_base, kslot, vslot, \
                                            out->kv_key, out->kv_val, ctr)
-        if (g_short_tab == 3) DEC_CLAIM(3);
+        if (g_short_tab == 4) DEC_CLAIM(4);
+        else if (g_short_tab == 3) DEC_CLAIM(3);
         else if (g_short_tab == 2) DEC_CLAIM(2);
         else if (g_short_tab == 1) DEC_CLAIM(1);
         else DEC_CLAIM(0);

@@ -86,9 +86,9 @@ int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
  * (e.g. "sort.plan_cache" 0/1/2, "sort.group_tile" 4096/8192,
  * "sort.or_lb_words" 1/4), "pop.direct", "codec.small" (0 multi-pass,
  * 1 auto, 2 one-pass, 3 one-pass coalesced), "codec.big_r" (4/8),
- * "codec.short_tab" (0/1/2/3: string-table lookups compare the short form
+ * "codec.short_tab" (0..4: string-table lookups compare the short form
  * stored beside the entry; 2 probes a pair's key and value homes at once;
- * 3 does so for two pairs per thread);
+ * 3 / 4 do so for two / three pairs per thread);
  * fault injection: "fail.refmerge" (n: the next n RefMerge calls return
  * CRDT_E_NOMEM before touching the device -- error-path tests),
  * "fail.zero_bits" (n: the next n two-pass merges -- set merges, RefMerge --

@@ -254,7 +254,7 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
     host.close()
 
 
-@pytest.mark.parametrize("short_tab", [2, 3, 1, 0])
+@pytest.mark.parametrize("short_tab", [2, 3, 4, 1, 0])
 def test_decode_resolved_short_forms_across_calls_and_rehash(eng, short_tab):
     """Strings of <= 7 bytes resolved in an earlier call are found by the
     short form stored beside their table entry (codec.short_tab, written with
