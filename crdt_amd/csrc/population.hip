@@ -266,12 +266,12 @@ __global__ void k_pop_stage(const uint64_t *__restrict__ src, uint64_t *__restri
 
 // as k_pop_bounds, one workgroup, into host memory; then the completion word
 // (system-scope release: the bounds are visible to the host before it)
-__global__ __launch_bounds__(256) void k_pop_bounds_host(const uint64_t *__restrict__ off,
+__global__ __launch_bounds__(1024) void k_pop_bounds_host(const uint64_t *__restrict__ off,
                                                          const uint64_t *__restrict__ kv_off, uint32_t P,
                                                          const uint32_t *__restrict__ status,
                                                          const uint64_t *__restrict__ snap, uint64_t *__restrict__ out,
                                                          uint64_t *__restrict__ flag, uint64_t seq) {
-    for (uint32_t p = threadIdx.x; p <= P; p += 256) {
+    for (uint32_t p = threadIdx.x; p <= P; p += 1024) {
         const uint64_t o = off[p];
         out[p] = o;
         out[P + 1 + p] = kv_off[o];
@@ -397,7 +397,7 @@ int pop_merge(crdt_population *pop, const RoundArrays &a, const HostRound &h, co
             pop->st_str[sn], pop->st_sum[sn]);
     if (g_pop_direct) {
         pop->seq += 1;
-        k_pop_bounds_host<<<1, 256, 0, ctx->stream>>>(nd.off, nd.kv_off, P, ctx->dev_status, a.bounds + 2 * P + 3,
+        k_pop_bounds_host<<<1, 1024, 0, ctx->stream>>>(nd.off, nd.kv_off, P, ctx->dev_status, a.bounds + 2 * P + 3,
                                                        carve_round(pop->pin_d, P).bounds, pop->hflag_d, pop->seq);
         return check_launch(ctx);
     }
