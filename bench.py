@@ -1283,7 +1283,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive e2e_pcie measurement")
     ap.add_argument("--no-peaks", action="store_true",
                     help="skip the self-measured peak sweep (timeline traces: the trace then ends with the timed loop)")
-    ap.add_argument("--option", action="append", default=[], help="name=value kernel knob (crdt_set_option)")
+    ap.add_argument("--option", action="append", default=[],
+                    help="name=value kernel knob (crdt_set_option; loads the diagnostic build, A/B runs only)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1297,10 +1298,12 @@ def main():
     world, rank, local = dist_init()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a mismatched n_gpus")
-    for o in args.option:
-        k, v = o.split("=")
+    if args.option:                               # knobs: the diagnostic build (the product has none)
         from crdt_amd import _lib
-        _lib.call("crdt_set_option", k.encode(), int(v))
+        _lib.use_diag_build()
+        for o in args.option:
+            k, v = o.split("=")
+            _lib.set_option(k, int(v))
 
     eng = E.Engine(local)
     wl = make_workload(args.workload, eng, rank, world, args)
@@ -1370,12 +1373,19 @@ def main():
                 cpu["affinity_cpus"] = aff
                 cpu["cpu_share"] = ("threads = min(affinity mask, OMP_NUM_THREADS = "
                                     f"{os.environ.get('OMP_NUM_THREADS', 'unset')}): the GPU's host CPU share")
+                if aff > threads:                     # the same restatement on the whole host
+                    whole = wl.cpu_baseline(args.cpu_seconds, aff)
+                    if whole is not None:
+                        cpu["whole_host"] = {"value": round(whole["value"], 1), "unit": whole["unit"],
+                                             "cores": whole["cores"], "sample": whole["sample"],
+                                             "cgroup_cpu_max": _cgroup_cpu_max()}
         from crdt_amd import _lib
         rccl = _lib.rccl_info()                       # the RCCL this process resolved
         config = dict(wl.config)
         if "parallelism" in config:
             config["parallelism"] = f"{config['parallelism']} [RCCL {rccl['version']}]"
         config["rccl"] = rccl
+        config["build"] = ("diag: " + ",".join(args.option)) if args.option else "product (libcrdt_amd.so)"
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": wl.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
@@ -1395,6 +1405,16 @@ def main():
         import torch.distributed as dist
         dist.destroy_process_group()
     eng.close()
+
+
+def _cgroup_cpu_max():
+    """This process's cgroup CPU quota ("quota period" or "max"): on a shared
+    box the threads of the whole-host baseline may only get this much time."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 def _cpu_model():

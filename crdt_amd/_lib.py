@@ -18,9 +18,15 @@ import threading
 
 import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
-# CRDT_AMD_LIB: another build of the same library (A/B timing of two builds
-# in one GPU call, tools/ab_build.sh); never set for tests, smoke or bench lines.
-LIB_PATH = os.environ.get("CRDT_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcrdt_amd.so")
+# CRDT_AMD_DIAG=1: the diagnostic build (libcrdt_amd_diag.so, -DCRDT_DIAG:
+# settable kernel knobs, timing diagnostics, failpoints) -- the knob-variant
+# tests (tests/test_gpu_diag_build.py runs them in a child process) and A/B
+# tools.  CRDT_AMD_LIB: another build of the same library (A/B timing of two
+# builds in one GPU call, tools/ab_build.sh).  Neither is set for the product
+# tests, smoke or bench lines.
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CRDT_AMD_LIB") or os.path.join(
+    _HERE, "libcrdt_amd_diag.so" if os.environ.get("CRDT_AMD_DIAG") == "1" else "libcrdt_amd.so")
 
 CRDT_OK = 0
 STATUS_NAMES = {
@@ -155,6 +161,7 @@ SIGNATURES = {
     "crdt_ctx_last_hip_error": (_I, [_CTX]),
     "crdt_ctx_reserve": (_I, [_CTX, _SZ]),
     "crdt_set_option": (_I, [C.c_char_p, C.c_int64]),
+    "crdt_get_option": (_I, [C.c_char_p, C.POINTER(C.c_int64)]),
     "crdt_dev_alloc": (_I, [_CTX, _SZ, C.POINTER(_P)]),
     "crdt_dev_free": (_I, [_CTX, _P]),
     "crdt_memcpy_h2d": (_I, [_CTX, _P, _P, _SZ]),
@@ -331,6 +338,33 @@ def call(fn: str, *args, ctx=None) -> int:
     if isinstance(st, int) and st < 0:
         check(fn, st, ctx)
     return st
+
+
+def use_diag_build() -> None:
+    """Load libcrdt_amd_diag.so instead of the product (A/B tools, bench
+    --option); must run before the library is first opened."""
+    global LIB_PATH
+    diag = os.path.join(_HERE, "libcrdt_amd_diag.so")
+    if _lib is not None and LIB_PATH != diag:
+        raise CrdtLibraryError(f"{LIB_PATH} is already loaded")
+    LIB_PATH = diag
+
+
+def get_option(name) -> int:
+    """A kernel knob's value in the loaded build (crdt_get_option)."""
+    v = C.c_int64(0)
+    call("crdt_get_option", name if isinstance(name, bytes) else name.encode(), C.byref(v))
+    return v.value
+
+
+def is_diag() -> bool:
+    """True when the diagnostic build (settable knobs, failpoints) is loaded."""
+    return get_option(b"build.diag") == 1
+
+
+def set_option(name, value: int) -> None:
+    """crdt_set_option: diagnostic build only (the product refuses every name)."""
+    call("crdt_set_option", name if isinstance(name, bytes) else name.encode(), int(value))
 
 
 def rccl_info() -> dict:

@@ -9,58 +9,21 @@
 #include "common.hpp"
 
 namespace crdt {
-JoinTuning g_join;
-FoldTuning g_fold;
-int g_vclock_pairs_per_wave = 32;  // 10M x 128, one block/CU: 32 pairs 0.858-0.860 of 8 TB/s, 16 0.852-0.854,
-int g_vclock_blocks_per_cu = 1;    //   8 0.833 (profiles/r05/ab/vclock_*.txt; 4 x 8 blocks/CU: 6.19 TB/s)
-int g_lww_chunk = 0;      // LWW tiles per chunk, 0 = one chunk (chunked schedules measured slower: DESIGN.md §5.4)
-int g_or_chunk = 0;       // OR-Set tiles per chunk (likewise)
-int g_set_streams = 1;
-int g_shard_exchange_always = 0;
-int g_or_count_dma = 1;  // OR-Set count pass staged by LDS-DMA (sets.or_count_dma)
-int g_or_key_sort = 2;   // OR-Set D2: 2 key + one more tag digit, marks within groups; 1 key only; 0 the 7-pass tag sort
-int g_or_parts = 2;     // OR-Set write pass: half tiles (whole tiles 159 -> 152 us)
-int g_rm_parts = 1;
-int g_rm_count_dma = 1;
-int g_short_tab = 3;
-int g_dec_big_r = 4;
-int g_dec_small = 1;
-int g_rm_kvx = 0;
-int g_rm_ld_all = 0;
-int g_sort_xcd = 1;      // radix scatter: XCD-contiguous tiles
-int g_sort_vec_up = 1;   // fused D2: vectorised composing upsweep
-int g_lww_table = 1;     // LWW D2: key-bucket LDS tables when the key offsets span 12..23 bits
-int g_sample_plan = 1;   // dense-key D2 paths from a sampled plan, checked in the upsweep (sort.sample_plan)
-int g_plan_cache = 2;    // ... launched from the last such plan (2: as it is, no sample; 1: its shape, a fresh sample checked on the device) (sort.plan_cache)
-int g_rm_affine = 1;     // one-pair populations: RefMerge pair indices computed, no kv range loads (refmerge.affine_kv)
-int g_lww_gather = 1;    // LWW D2 tables gather their runs from bucket-grouped tiles, no scatter pass (sort.lww_gather)
-int g_or_narrow = 1;
-int g_pop_direct = 1;    // population rounds: staging kernel + polled host bounds, no copy engine (pop.direct)
-int g_or_place_batch = 1;  // OR-Set D2 buckets: placement sorted per round in LDS, stored in pieces (sort.or_place_batch)
-int g_up_threads = 512;  // D2 tile grouping pass: threads per 4096-tuple tile, 256 or 512 (sort.up_threads)
-int g_group_tile = 8192;  // D2 gather forms: tuples per grouping tile, 4096 or 8192 (sort.group_tile)
-int g_or_sub_hist = 1;   // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
-int g_read_poll = 1;     // small read-backs polled from coherent host memory (ctx.read_poll)
-int g_pop_wire_early = 1;  // wire rounds: the merge enqueued behind the decode's claim pass (pop.wire_early)
-int g_or_lb_words = 1;   // OR-Set D2 chunk look-back: status words per lane per window, 1 or 4 (sort.or_lb_words)
-int g_or_bucket = 1;     // OR-Set D2: top-byte tile groups gathered into chunks, no radix passes (sort.or_bucket)
-int g_or_pair = 1;       // OR-Set D2 chunks: two per workgroup, one look-back for both (sort.or_pair)     // OR-Set D2 chunks: keys' slots sorted on their low words when the tags fit 32 bits (sort.or_narrow)
-int g_sample_min = 1 << 20;   // ... for calls of at least this many tuples (sort.sample_min)
-int g_or_lookback = 1;   // OR-Set D2 chunks: offsets by a decoupled look-back (0: count scan + emit pass)
-int g_or_table = 1;      // OR-Set D2: 2^9-key chunks sorted in LDS after two top-16-bit passes (16..25 key bits)
-int g_rdd_diag = 0;
-int g_mm_bpc = 1;        // sort minmax: workgroups per CU per input (1: 0.716 ms LWW D2 step, 4: 0.732)
-int g_lww_parts = 4;     // LWW write pass: quarter tiles (half tiles 112 -> 105 us)
-int g_rm_diag = 0;
-int g_scan_items = 8;
+#ifdef CRDT_DIAG
+#define KNOB(var, def, name, valid) int var = (def);
+#include "knobs.inc"
+#undef KNOB
 std::atomic<int> g_fail_refmerge{0};
 std::atomic<int> g_fail_zero_bits{0};
 
-bool take_fail_zero_bits() {
-    for (int f = g_fail_zero_bits.load(); f > 0;)
-        if (g_fail_zero_bits.compare_exchange_weak(f, f - 1)) return true;
+static bool take_count(std::atomic<int> &c) {
+    for (int f = c.load(); f > 0;)
+        if (c.compare_exchange_weak(f, f - 1)) return true;
     return false;
 }
+bool take_fail_zero_bits() { return take_count(g_fail_zero_bits); }
+bool take_fail_refmerge() { return take_count(g_fail_refmerge); }
+#endif
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return CRDT_OK;
@@ -209,6 +172,7 @@ __global__ __launch_bounds__(256) void k_read_words(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ dst, uint64_t *__restrict__ flag,
                                                     uint64_t seq) {
     for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    __threadfence_system();                    // each wave's stores, before the flag
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -333,165 +297,56 @@ extern "C" int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes) {
     return ws_reserve(ctx, bytes);
 }
 
+// The knob table (knobs.inc): name, current value, validity of a new value.
+struct KnobEntry {
+    const char *name;
+    int64_t (*get)();
+    int (*set)(int64_t v);   // CRDT_E_INVAL when invalid (or in the product build)
+};
+#ifdef CRDT_DIAG
+#define KNOB(var, def, kname, valid) \
+    {kname, [] { return (int64_t)var; }, [](int64_t v) { if (!(valid)) return (int)CRDT_E_INVAL; var = (int)v; return (int)CRDT_OK; }},
+#else
+#define KNOB(var, def, kname, valid) \
+    {kname, [] { return (int64_t)var; }, [](int64_t) { return (int)CRDT_E_INVAL; }},
+#endif
+static const KnobEntry kKnobs[] = {
+#include "knobs.inc"
+};
+#undef KNOB
+
+extern "C" int crdt_get_option(const char *name, int64_t *v) {
+    if (!name || !v) return CRDT_E_INVAL;
+    if (!strcmp(name, "build.diag")) {
+#ifdef CRDT_DIAG
+        *v = 1;
+#else
+        *v = 0;
+#endif
+        return CRDT_OK;
+    }
+    for (const KnobEntry &k : kKnobs)
+        if (!strcmp(name, k.name)) {
+            *v = k.get();
+            return CRDT_OK;
+        }
+    return CRDT_E_INVAL;
+}
+
+// Product build: every name is refused (the knobs are compile-time constants).
+// Diagnostic build: the knobs, validated, and the failpoints.
 extern "C" int crdt_set_option(const char *name, int64_t v) {
     if (!name) return CRDT_E_INVAL;
-    if (!strcmp(name, "join.unroll")) {
-        if (v != 1 && v != 2 && v != 4 && v != 8) return CRDT_E_INVAL;
-        g_join.unroll = (int)v;
-    } else if (!strcmp(name, "join.nontemporal")) {
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_join.nontemporal = (int)v;
-    } else if (!strcmp(name, "join.blocks_per_cu")) {
-        if (v < 1 || v > 64) return CRDT_E_INVAL;
-        g_join.blocks_per_cu = (int)v;
-    } else if (!strcmp(name, "fold.unroll")) {
-        if (v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32) return CRDT_E_INVAL;
-        g_fold.unroll = (int)v;
-    } else if (!strcmp(name, "fold.nontemporal")) {
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_fold.nontemporal = (int)v;
-    } else if (!strcmp(name, "fold.blocks_per_cu")) {
-        if (v < 1 || v > 64) return CRDT_E_INVAL;
-        g_fold.blocks_per_cu = (int)v;
-    } else if (!strcmp(name, "vclock.pairs_per_wave")) {
-        if (v != 1 && v != 2 && v != 4 && v != 8 && v != 16 && v != 32) return CRDT_E_INVAL;
-        g_vclock_pairs_per_wave = (int)v;
-    } else if (!strcmp(name, "vclock.blocks_per_cu")) {
-        if (v < 1 || v > 64) return CRDT_E_INVAL;
-        g_vclock_blocks_per_cu = (int)v;
-    } else if (!strcmp(name, "sets.lww_chunk")) {    // LWW tiles per count / write chunk (0: one chunk)
-        if (v < 0 || v > 16384) return CRDT_E_INVAL;
-        g_lww_chunk = (int)v;
-    } else if (!strcmp(name, "sets.or_chunk")) {     // OR-Set tiles per count / write chunk (0: one chunk)
-        if (v < 0 || v > 16384) return CRDT_E_INVAL;
-        g_or_chunk = (int)v;
-    } else if (!strcmp(name, "sets.streams")) {      // 1: one stream; 2: chunk c+1's count beside chunk c's write
-        if (v != 1 && v != 2) return CRDT_E_INVAL;
-        g_set_streams = (int)v;
-    } else if (!strcmp(name, "shard.exchange_always")) {   // tests: the keyed-set exchange protocol even on 1 rank
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_shard_exchange_always = (int)v;
-    } else if (!strcmp(name, "sets.or_count_dma")) { // OR-Set count pass: 1 LDS-DMA staging, 0 register staging
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_count_dma = (int)v;
-    } else if (!strcmp(name, "sort.or_key_only")) {  // OR-Set D2: 2 key + 1-2 tag digits, 1 key-only sort, 0 full tag sort
-        if (v < 0 || v > 2) return CRDT_E_INVAL;
-        g_or_key_sort = (int)v;
-    } else if (!strcmp(name, "sort.xcd_tiles")) {    // radix scatter pass: 1 XCD-contiguous tile ranges, 0 blockIdx order
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_sort_xcd = (int)v;
-    } else if (!strcmp(name, "sort.mm_blocks_per_cu")) {   // sort minmax grid: workgroups per CU per input
-        if (v < 1 || v > 16) return CRDT_E_INVAL;
-        g_mm_bpc = (int)v;
-    } else if (!strcmp(name, "sort.rdd_diag")) {     // timing diagnostic: the D2 dedup apply (OR-Set: and count)
-        if (v < 0 || v > 8) return CRDT_E_INVAL;       //   stops after 1 staging, 2 marks, 3 counts (no stores);
-                                                        //   OR-Set chunks: 1 key counts, 2 LDS sort, 3 per-key tags, 4 long keys + ranks,
-                                                        //   5 all but the output stores, 6 no look-back (fake offsets);
-                                                        //   OR-Set buckets: 7 no placement stores, 8 no placement sweep
-        g_rdd_diag = (int)v;
-    } else if (!strcmp(name, "sort.lww_table")) {    // LWW D2: 1 key-bucket LDS tables where they apply, 0 key-only sort
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_lww_table = (int)v;
-    } else if (!strcmp(name, "sort.or_table")) {     // OR-Set D2: 1 key chunks sorted in LDS where they apply, 0 the radix sort
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_table = (int)v;
-    } else if (!strcmp(name, "sort.sample_plan")) {  // D2 dense-key paths: 1 plan from a sample + range check, 0 full minmax
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_sample_plan = (int)v;
-    } else if (!strcmp(name, "refmerge.affine_kv")) { // one-pair populations: 1 pair index = kv[0] + entry (no range loads)
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_rm_affine = (int)v;
-    } else if (!strcmp(name, "sort.lww_gather")) {   // LWW D2 tables: 1 runs gathered from bucket-grouped tiles, 0 a scatter pass
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_lww_gather = (int)v;
-    } else if (!strcmp(name, "sort.or_bucket")) {    // OR-Set D2: 1 tile groups + bucket gathers, 0 two radix passes
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_bucket = (int)v;
-    } else if (!strcmp(name, "pop.direct")) {        // population rounds: 1 staging kernel + polled host bounds, 0 copies + sync
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_pop_direct = (int)v;
-    } else if (!strcmp(name, "sort.or_place_batch")) {   // OR-Set D2 buckets: 1 placement batched in LDS, 0 one by one
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_place_batch = (int)v;
-    } else if (!strcmp(name, "sort.up_threads")) {   // D2 tile grouping pass: 256 / 512 threads per 4096-tuple tile
-        if (v != 256 && v != 512) return CRDT_E_INVAL;
-        g_up_threads = (int)v;
-    } else if (!strcmp(name, "sort.group_tile")) {   // D2 gather forms: 4096 / 8192 tuples per grouping tile
-        if (v != 4096 && v != 8192) return CRDT_E_INVAL;
-        g_group_tile = (int)v;
-    } else if (!strcmp(name, "sort.or_sub_hist")) {  // OR-Set D2 buckets: 1 chunk counts from per-run rows, 0 a counting gather
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_sub_hist = (int)v;
-    } else if (!strcmp(name, "ctx.read_poll")) {     // small read-backs: 1 kernel + polled coherent memory, 0 copy + sync
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_read_poll = (int)v;
-    } else if (!strcmp(name, "pop.wire_early")) {    // wire rounds: 1 merge enqueued behind the claim pass, 0 after the decode
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_pop_wire_early = (int)v;
-    } else if (!strcmp(name, "sort.or_lb_words")) {  // OR-Set D2 chunk look-back: 1 / 4 status words per lane per window
-        if (v != 1 && v != 4) return CRDT_E_INVAL;
-        g_or_lb_words = (int)v;
-    } else if (!strcmp(name, "sort.or_pair")) {      // OR-Set D2 chunks: 1 two per workgroup (one look-back), 0 one
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_pair = (int)v;
-    } else if (!strcmp(name, "sort.or_narrow")) {    // OR-Set D2 chunks: 1 u32 sorting networks where the tag fits 32 bits
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_narrow = (int)v;
-    } else if (!strcmp(name, "sort.plan_cache")) {   // D2 sampled plans: 2 the cached plan (no sample), 1 its shape + a sample, 0 none
-        if (v < 0 || v > 2) return CRDT_E_INVAL;
-        g_plan_cache = (int)v;
-    } else if (!strcmp(name, "sort.sample_min")) {   // fewest tuples for the sampled plan
-        if (v < 0 || v > 0x7FFFFFFF) return CRDT_E_INVAL;
-        g_sample_min = (int)v;
-    } else if (!strcmp(name, "sort.or_lookback")) {  // OR-Set D2 chunks: 1 look-back offsets + direct stores, 0 scan + emit
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_or_lookback = (int)v;
-    } else if (!strcmp(name, "sort.vec_up")) {       // fused D2 sort: 1 vectorised composing upsweep, 0 scalar
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_sort_vec_up = (int)v;
-    } else if (!strcmp(name, "sets.lww_parts")) {    // LWW write-pass workgroups per 4096-item tile
-        if (v != 2 && v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
-        g_lww_parts = (int)v;
-    } else if (!strcmp(name, "sets.or_parts")) {     // OR-Set write-pass workgroups per 2048-item tile
-        if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
-        g_or_parts = (int)v;
-    } else if (!strcmp(name, "refmerge.load_all")) {   // tile pass loads non-emitted entries too (A/B)
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_rm_ld_all = (int)v;
-    } else if (!strcmp(name, "refmerge.kv_one_launch")) {   // kv tile pass: both tile kinds in one launch at any grid
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_rm_kvx = (int)v;
-    } else if (!strcmp(name, "codec.short_tab")) {   // string-table lookups: the short form beside the entry (2: + both home probes first)
-        if (v < 0 || v > 4) return CRDT_E_INVAL;
-        g_short_tab = (int)v;
-    } else if (!strcmp(name, "codec.big_r")) {   // the coalesced one-pass decode: items per thread per chunk
-        if (v != 4 && v != 8) return CRDT_E_INVAL;
-        g_dec_big_r = (int)v;
-    } else if (!strcmp(name, "codec.small")) {   // gossip decode in one pass: 0 off, 1 auto, 2 always, 3 always (coalesced form)
-        if (v < 0 || v > 3) return CRDT_E_INVAL;
-        g_dec_small = (int)v;
-    } else if (!strcmp(name, "refmerge.count_dma")) {   // RefMerge count pass: ts runs staged by LDS-DMA
-        if (v != 0 && v != 1) return CRDT_E_INVAL;
-        g_rm_count_dma = (int)v;
-    } else if (!strcmp(name, "refmerge.tile_parts")) {   // RefMerge tile-pass workgroups per 4096-item tile
-        if (v != 1 && v != 2 && v != 4) return CRDT_E_INVAL;
-        g_rm_parts = (int)v;
-    } else if (!strcmp(name, "refmerge.diag_fold")) {   // timing diagnostic: 1 skip the replay fold; 2 no flush, 4 no table, 5 no Atoi gather
-        if (v < 0 || v > 5) return CRDT_E_INVAL;
-        g_rm_diag = (int)v;
-    } else if (!strcmp(name, "scan.items")) {        // items per lane of the single-pass scan
-        if (v != 4 && v != 8 && v != 16) return CRDT_E_INVAL;
-        g_scan_items = (int)v;
-    } else if (!strcmp(name, "fail.refmerge")) {     // fault injection: the next v RefMerge calls fail (CRDT_E_NOMEM)
+#ifdef CRDT_DIAG
+    if (!strcmp(name, "fail.refmerge") || !strcmp(name, "fail.zero_bits")) {
         if (v < 0 || v > 1000) return CRDT_E_INVAL;
-        g_fail_refmerge = (int)v;
-    } else if (!strcmp(name, "fail.zero_bits")) {    // fault injection: the next v two-pass merges zero their
-        if (v < 0 || v > 1000) return CRDT_E_INVAL;    //   merge bitmaps between the passes (CRDT_DEV_RANGE)
-        g_fail_zero_bits = (int)v;
-    } else {
-        return CRDT_E_INVAL;
+        (name[5] == 'r' ? g_fail_refmerge : g_fail_zero_bits) = (int)v;
+        return CRDT_OK;
     }
-    return CRDT_OK;
+#endif
+    for (const KnobEntry &k : kKnobs)
+        if (!strcmp(name, k.name)) return k.set(v);
+    return CRDT_E_INVAL;
 }
 
 extern "C" int crdt_dev_alloc(crdt_ctx *ctx, size_t bytes, void **dev) {

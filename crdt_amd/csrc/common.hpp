@@ -62,63 +62,27 @@ inline int hip_fail(crdt_ctx *ctx, hipError_t e) {
     return e == hipErrorOutOfMemory ? CRDT_E_NOMEM : CRDT_E_HIP;
 }
 
-// Process-wide kernel tuning knobs (crdt_set_option); defined in capi.hip.
-struct JoinTuning {
-    int unroll = 1;         // 16-B vectors in flight per lane per operand (tuned: tools/tune_join.py)
-    int nontemporal = 1;    // nt loads/stores for once-touched streams
-    int blocks_per_cu = 2;  // grid = CUs * blocks_per_cu (grid-stride beyond); ~16 KiB in flight per CU
-};
-extern JoinTuning g_join;
-struct FoldTuning {
-    int unroll = 8;         // 16-B vectors in flight per lane (tools/tune_fold.py: 8 x 1 block/CU
-    int nontemporal = 1;    //   = 32 KiB in flight per CU, 7.06 TB/s at 100M x 64, against
-    int blocks_per_cu = 1;  //   6.18 TB/s for 4 x 4)
-};
-extern FoldTuning g_fold;
-extern int g_vclock_pairs_per_wave;
-extern int g_vclock_blocks_per_cu;
-extern int g_rm_diag;           // timing diagnostic: refmerge replay fold variants (wrong state)
-extern int g_sort_xcd;          // radix scatter pass: XCD-contiguous tile ranges (sort.xcd_tiles)
-extern int g_lww_table;        // LWW D2 key-bucket tables (sort.lww_table)
-extern int g_sample_plan;      // D2 dense-key paths from a sampled plan (sort.sample_plan)
-extern int g_plan_cache;       // ... launched from the context's cached plan shape (sort.plan_cache)
-extern int g_rm_affine;        // one-pair populations: no kv range loads in the tile pass (refmerge.affine_kv)
-extern int g_lww_gather;       // LWW D2 tables fed by gathers from bucket-grouped tiles (sort.lww_gather)
-extern int g_pop_direct;       // population rounds without copy-engine staging (pop.direct)
-extern int g_or_place_batch;   // OR-Set D2 bucket placement batched in LDS (sort.or_place_batch)
-extern int g_up_threads;       // D2 tile grouping pass: threads per tile (sort.up_threads)
-extern int g_group_tile;       // D2 gather forms: tuples per grouping tile (sort.group_tile)
-extern int g_or_sub_hist;      // OR-Set D2 buckets: chunk counts from per-run histograms (sort.or_sub_hist)
-extern int g_read_poll;        // small read-backs polled from coherent host memory (ctx.read_poll)
-extern int g_pop_wire_early;   // wire rounds: merge behind the claim pass (pop.wire_early)
-extern int g_or_lb_words;      // OR-Set D2 chunk look-back window words per lane (sort.or_lb_words)
-extern int g_or_bucket;        // OR-Set D2: bucket gathers instead of radix passes (sort.or_bucket)
-extern int g_or_pair;          // OR-Set D2 chunks: two per workgroup (sort.or_pair)
-extern int g_or_narrow;        // OR-Set D2 chunks: u32 sorting networks (sort.or_narrow)
-extern int g_sample_min;       // ... from this many tuples (sort.sample_min)
-extern int g_or_lookback;      // OR-Set D2 chunk offsets by look-back (sort.or_lookback)
-extern int g_or_table;         // OR-Set D2 key chunks sorted in LDS (sort.or_table)
-extern int g_sort_vec_up;       // fused D2 sort: vectorised composing upsweep (sort.vec_up)
-extern int g_mm_bpc;            // sort minmax: workgroups per CU per input (sort.mm_blocks_per_cu)
-extern int g_rdd_diag;          // OR-Set D2 group dedup timing diagnostic (sort.rdd_diag; 0 = off)
-extern int g_lww_parts;         // LWW write-pass workgroups per tile (sets.lww_parts: 2, 4, 8, 16)
-extern int g_or_parts;          // OR-Set write-pass workgroups per tile (sets.or_parts: 1, 2, 4)
-extern int g_rm_parts;          // RefMerge tile-pass workgroups per tile (refmerge.tile_parts: 1, 2, 4)
-extern int g_rm_ld_all;        // RefMerge tile pass: load non-emitted entries too (refmerge.load_all, A/B)
-extern int g_rm_kvx;           // RefMerge kv tile pass in one launch at any grid (refmerge.kv_one_launch)
-extern int g_short_tab;        // string-table lookups compare the short form beside the entry (codec.short_tab)
-extern int g_dec_big_r;        // the coalesced one-pass decode: items per thread per chunk, 4 or 8 (codec.big_r)
-extern int g_dec_small;        // gossip decode of few small bodies in one pass (codec.small)
-extern int g_rm_count_dma;      // RefMerge count pass staged by LDS-DMA (refmerge.count_dma)
-extern int g_lww_chunk;         // set merges: tiles per count / write chunk (sets.lww_chunk, sets.or_chunk;
-extern int g_or_chunk;          //   0 = one chunk), DESIGN.md §5.4
-extern int g_shard_exchange_always;   // keyed-set shard merges run the exchange protocol on 1 rank too (tests)
-extern int g_set_streams;       // set merges: 1 = one stream, 2 = counts beside writes (sets.streams)
-extern int g_or_count_dma;      // OR-Set count pass staging (sets.or_count_dma)
-extern int g_or_key_sort;       // OR-Set D2 key-only sort (sort.or_key_only)
-extern std::atomic<int> g_fail_refmerge;   // fault injection (crdt_set_option "fail.refmerge"): error-path tests
-extern std::atomic<int> g_fail_zero_bits;  // fault injection ("fail.zero_bits"): bitmaps zeroed between passes
+// Kernel-shape knobs (knobs.inc): constexpr defaults in the product build,
+// process-wide variables (crdt_set_option) in the diagnostic build only.
+#ifdef CRDT_DIAG
+#define KNOB(var, def, name, valid) extern int var;
+#else
+#define KNOB(var, def, name, valid) constexpr int var = (def);
+#endif
+#include "knobs.inc"
+#undef KNOB
+#ifdef CRDT_DIAG
+// Failpoints (crdt_set_option "fail.*", diagnostic build only): error-path tests.
+extern std::atomic<int> g_fail_refmerge;   // the next n RefMerge calls return CRDT_E_NOMEM
+extern std::atomic<int> g_fail_zero_bits;  // the next n two-pass merges zero their bitmaps between the passes
 bool take_fail_zero_bits();                // consumes one "fail.zero_bits" count
+bool take_fail_refmerge();                 // consumes one "fail.refmerge" count
+inline bool fail_refmerge_armed() { return g_fail_refmerge.load() != 0; }
+#else
+constexpr bool take_fail_zero_bits() { return false; }
+constexpr bool take_fail_refmerge() { return false; }
+constexpr bool fail_refmerge_armed() { return false; }
+#endif
 
 // The context's aux stream / an event pool of at least n events (capi.hip).
 int ctx_aux(crdt_ctx *ctx);

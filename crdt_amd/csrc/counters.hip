@@ -176,13 +176,13 @@ static void launch_join(unsigned grid, hipStream_t s, const u64x2 *a, const u64x
 
 static int join_impl(crdt_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *o, size_t n) {
     const size_t n2 = n / 2;
-    const unsigned grid = grid_for(n2, 256, (unsigned)(ctx->num_cus * g_join.blocks_per_cu));
+    const unsigned grid = grid_for(n2, 256, (unsigned)(ctx->num_cus * g_join_blocks_per_cu));
     const hipStream_t s = ctx->stream;
     if (n2) {
         const u64x2 *va = (const u64x2 *)a, *vb = (const u64x2 *)b;
         u64x2 *vo = (u64x2 *)o;
-        const bool nt = g_join.nontemporal != 0;
-        switch (g_join.unroll) {
+        const bool nt = g_join_nontemporal != 0;
+        switch (g_join_unroll) {
             case 1: nt ? launch_join<1, true>(grid, s, va, vb, vo, n2) : launch_join<1, false>(grid, s, va, vb, vo, n2); break;
             case 2: nt ? launch_join<2, true>(grid, s, va, vb, vo, n2) : launch_join<2, false>(grid, s, va, vb, vo, n2); break;
             case 8: nt ? launch_join<8, true>(grid, s, va, vb, vo, n2) : launch_join<8, false>(grid, s, va, vb, vo, n2); break;
@@ -327,8 +327,8 @@ extern "C" int crdt_gcounter_fold(crdt_ctx *ctx, const uint64_t *a, size_t rows,
     if (!a) return CRDT_E_INVAL;
     const bool pow2 = nodes >= 2 && nodes <= 512 && (nodes & (nodes - 1)) == 0 && aligned16(a);
     unsigned grid;
-    const unsigned bpc = (unsigned)g_fold.blocks_per_cu;
-    if (pow2) grid = grid_for(rows * nodes / 2, 256 * (unsigned)g_fold.unroll, (unsigned)ctx->num_cus * bpc);
+    const unsigned bpc = (unsigned)g_fold_blocks_per_cu;
+    if (pow2) grid = grid_for(rows * nodes / 2, 256 * (unsigned)g_fold_unroll, (unsigned)ctx->num_cus * bpc);
     else grid = grid_for(rows, 1, (unsigned)(ctx->num_cus * 4));
     const size_t part_bytes = (size_t)grid * nodes * sizeof(uint64_t);
     rc = ws_reserve(ctx, part_bytes);
@@ -338,10 +338,10 @@ extern "C" int crdt_gcounter_fold(crdt_ctx *ctx, const uint64_t *a, size_t rows,
         const u64x2 *va = (const u64x2 *)a;
         const size_t n2 = rows * nodes / 2;
         const hipStream_t s = ctx->stream;
-        const bool nt = g_fold.nontemporal != 0;
+        const bool nt = g_fold_nontemporal != 0;
 #define FOLD(U) (nt ? k_fold_pow2<U, true><<<grid, 256, 0, s>>>(va, n2, (int)nodes, partial) \
                     : k_fold_pow2<U, false><<<grid, 256, 0, s>>>(va, n2, (int)nodes, partial))
-        switch (g_fold.unroll) {
+        switch (g_fold_unroll) {
             case 1: FOLD(1); break;
             case 2: FOLD(2); break;
             case 8: FOLD(8); break;

@@ -280,6 +280,9 @@ __global__ __launch_bounds__(1024) void k_pop_bounds_host(const uint64_t *__rest
         out[2 * P + 2] = *status;
         out[2 * P + 3] = *snap;
     }
+    // every writing wave releases its own stores at system scope before the
+    // barrier: thread 0's release below covers only its own wave
+    __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -917,7 +920,13 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     };
     bool stale = false;
     const size_t need = gossip_decode_scratch_bytes(P, n_e, n_p);
-    const bool early = g_pop_wire_early && dev_grow(ctx, &pop->dscr, &pop->dscr_bytes, need) == CRDT_OK;
+    // Not on a population's first wire round (no vtab yet): the early merge
+    // would fold with the population's own arena and n_str, while vals may
+    // already hold strings past them (a refused earlier round interned them,
+    // or vals is shared), and a pulled id in [n_str, vals->n) would skip the
+    // replay fold without the rerun below noticing.
+    const bool early = g_pop_wire_early && pop->vtab &&
+                       dev_grow(ctx, &pop->dscr, &pop->dscr_bytes, need) == CRDT_OK;
     rc = gossip_decode_at(ctx, P, bodies, at.data(), len.data(), pop->K, pop->n_kv, sbase.data(), hdr.data(), keys,
                           vals, &go, body_status, early ? &run_merge : nullptr, early ? pop->dscr : nullptr,
                           early ? pop->dscr_bytes : 0, &stale, &multi);

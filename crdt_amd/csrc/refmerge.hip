@@ -1248,8 +1248,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     int rc = bind(ctx);
     if (rc) return rc;
     if (!inp || !outp) return CRDT_E_INVAL;
-    for (int f = g_fail_refmerge.load(); f > 0;)                  // injected failure (error-path tests)
-        if (g_fail_refmerge.compare_exchange_weak(f, f - 1)) return CRDT_E_NOMEM;
+    if (take_fail_refmerge()) return CRDT_E_NOMEM;              // injected failure (diagnostic build)
     if (delta && inp->n_slots && (!delta->best_key || !delta->best_str || !delta->sum || !delta->npar ||
                                   !delta->nhold))
         return CRDT_E_INVAL;

@@ -64,7 +64,7 @@ __device__ __forceinline__ uint32_t block_rank_flag(bool f, uint32_t *total) {
 // Items are loaded striped (coalesced), summed blocked through LDS, and the
 // offsets stored striped again.  Src::load(i) returns an Item with a .len.
 constexpr int kLbMinItems = 4;      // workspace is sized for the smallest tile
-extern int g_scan_items;            // items per lane (crdt_set_option "scan.items": 4, 8, 16)
+// items per lane: g_scan_items (knobs.inc "scan.items": 4, 8, 16)
 
 struct NoAct {
     template <int N, class Item>

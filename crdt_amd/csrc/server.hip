@@ -1244,7 +1244,7 @@ extern "C" int crdt_servers_merge(crdt_server *const *srvs, size_t n) {
     // Device-resident path: every server's Diff stays in HBM, its pull is
     // decoded on the device; the host path (pack, H2D, merge, D2H, rebuild)
     // takes batches holding a nil map (no device representation).
-    bool dev = g_fail_refmerge.load() == 0;                     // (fault injection exercises the host path)
+    bool dev = !fail_refmerge_armed();                     // (fault injection exercises the host path)
     for (auto *s : v) dev = dev && dev_ok(*s) && s->ctx == ctx;
     if (dev) rc = ctx_tables(ctx);
     if (dev && !rc) {

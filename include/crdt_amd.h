@@ -77,25 +77,24 @@ int crdt_ctx_last_hip_error(const crdt_ctx *ctx);
 /* Pre-size the context's device workspace so that later calls never
  * allocate (needed before graph capture). */
 int crdt_ctx_reserve(crdt_ctx *ctx, size_t bytes);
-/* Kernel tuning knobs (process-wide), for A/B runs: "join.unroll" (1,2,4,8),
- * "join.nontemporal" (0/1), "join.blocks_per_cu" (1..64),
- * "vclock.pairs_per_wave" (1,2,4,8,16,32), "sets.lww_chunk" / "sets.or_chunk"
- * (tiles per count / write chunk of the set merges, 0 = one chunk),
- * "sets.streams" (1, 2), "sets.lww_parts", "sets.or_parts",
- * "refmerge.tile_parts", "refmerge.count_dma", the D2 forms' "sort.*"
- * (e.g. "sort.plan_cache" 0/1/2, "sort.group_tile" 4096/8192,
- * "sort.or_lb_words" 1/4), "pop.direct", "codec.small" (0 multi-pass,
- * 1 auto, 2 one-pass, 3 one-pass coalesced), "codec.big_r" (4/8),
- * "codec.short_tab" (0..4: string-table lookups compare the short form
- * stored beside the entry; 2 probes a pair's key and value homes at once;
- * 3 / 4 do so for two / three pairs per thread);
- * fault injection: "fail.refmerge" (n: the next n RefMerge calls return
- * CRDT_E_NOMEM before touching the device -- error-path tests),
- * "fail.zero_bits" (n: the next n two-pass merges -- set merges, RefMerge --
+/* Kernel-shape knobs (crdt_amd/csrc/knobs.inc: "join.unroll", "sets.lww_parts",
+ * "sort.plan_cache", "codec.short_tab", ...).  In the product library
+ * (libcrdt_amd.so) they are compile-time constants at their measured
+ * defaults: crdt_set_option refuses every name with CRDT_E_INVAL, so no
+ * process-global state is shared between contexts and no timing diagnostic
+ * or failpoint can reach a caller.  The diagnostic build (libcrdt_amd_diag.so,
+ * -DCRDT_DIAG; linked by tests and tools only) accepts them process-wide for
+ * A/B runs, plus the timing diagnostics ("sort.rdd_diag",
+ * "refmerge.diag_fold": kernels skip work, output wrong) and the failpoints
+ * "fail.refmerge" (n: the next n RefMerge calls return CRDT_E_NOMEM before
+ * touching the device) and "fail.zero_bits" (n: the next n two-pass merges
  * zero their merge bitmaps between the passes: the write pass must raise
- * CRDT_DEV_RANGE, never read out of range).
- * Returns CRDT_E_INVAL for an unknown name or value. */
+ * CRDT_DEV_RANGE, never read out of range).  CRDT_E_INVAL for an unknown
+ * name or value. */
 int crdt_set_option(const char *name, int64_t value);
+/* The knob's value in this build; "build.diag" reads 1 in the diagnostic
+ * build, 0 in the product.  CRDT_E_INVAL for an unknown name. */
+int crdt_get_option(const char *name, int64_t *value);
 
 /* Device memory for hosts without an allocator of their own (the Go side). */
 int crdt_dev_alloc(crdt_ctx *ctx, size_t bytes, void **dev);

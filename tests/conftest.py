@@ -10,6 +10,8 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built libcrdt_amd.so")
+    config.addinivalue_line("markers", "diag: sets kernel knobs or failpoints (tests/knobs.py): non-default variants "
+                            "run under the diagnostic build, in the child suite of tests/test_gpu_diag_build.py")
 
 
 @pytest.fixture(scope="session")
@@ -20,9 +22,9 @@ def eng():
     e = Engine(0)
     # CRDT_TEST_OPTIONS="sets.streams=1,join.unroll=2": run the GPU suite
     # under non-default kernel knobs (crdt_set_option)
-    from crdt_amd import _lib
+    from knobs import set_knob
     for opt in filter(None, os.environ.get("CRDT_TEST_OPTIONS", "").split(",")):
         k, v = opt.split("=")
-        _lib.call("crdt_set_option", k.strip().encode(), int(v))
+        set_knob(k.strip().encode(), int(v))
     yield e
     e.close()

@@ -71,17 +71,54 @@ def test_shard_range_rejects_bad_args():
     assert lib.crdt_shard_range(10, 2, 2, C.byref(b), C.byref(e)) == -1
 
 
-def test_set_option_validation():
+def _diag_lib():
+    path = os.path.join(ROOT, "crdt_amd", "libcrdt_amd_diag.so")
+    lib = C.CDLL(path, mode=C.RTLD_LOCAL)
+    lib.crdt_set_option.argtypes = [C.c_char_p, C.c_int64]
+    lib.crdt_get_option.argtypes = [C.c_char_p, C.POINTER(C.c_int64)]
+    return lib
+
+
+def _knob_names():
+    with open(os.path.join(ROOT, "crdt_amd", "csrc", "knobs.inc")) as f:
+        return re.findall(r'^KNOB\(\w+, ([^,]+), "([\w.]+)"', f.read(), flags=re.M)
+
+
+def test_product_refuses_every_option():
+    """the product ABI carries no knobs, timing
+    diagnostics or failpoints -- crdt_set_option refuses every name, even at
+    the default value; crdt_get_option reports the compiled-in defaults."""
     lib = _lib.lib()
+    assert _lib.get_option(b"build.diag") == 0
+    knobs = _knob_names()
+    assert len(knobs) > 40
+    for default, name in knobs:
+        assert _lib.get_option(name.encode()) == eval(default), name
+        assert lib.crdt_set_option(name.encode(), eval(default)) == -1, name
+    for name in (b"sort.rdd_diag", b"refmerge.diag_fold", b"fail.refmerge", b"fail.zero_bits", b"no.such.knob"):
+        assert lib.crdt_set_option(name, 1) == -1
+        assert lib.crdt_set_option(name, 0) == -1
+
+
+def test_diag_build_option_validation():
+    lib = _diag_lib()
+    v = C.c_int64()
+    assert lib.crdt_get_option(b"build.diag", C.byref(v)) == 0 and v.value == 1
     assert lib.crdt_set_option(b"join.unroll", 3) == -1
     assert lib.crdt_set_option(b"no.such.knob", 1) == -1
+    assert lib.crdt_set_option(b"join.unroll", 2) == 0
+    assert lib.crdt_get_option(b"join.unroll", C.byref(v)) == 0 and v.value == 2
     assert lib.crdt_set_option(b"join.unroll", 1) == 0
+    assert lib.crdt_set_option(b"fail.refmerge", 1001) == -1
+    assert lib.crdt_set_option(b"fail.refmerge", 0) == 0
+    for default, name in _knob_names():          # every default is valid in its own table entry
+        assert lib.crdt_set_option(name.encode(), eval(default)) == 0, name
 
 
-def test_d2_path_options():
-    """The unsorted-merge forms' switches: on / off accepted,
-    anything else refused; each left at its default."""
-    lib = _lib.lib()
+def test_diag_build_d2_path_options():
+    """The unsorted-merge forms' switches, diagnostic build:
+    on / off accepted, anything else refused; each left at its default."""
+    lib = _diag_lib()
     for name, default in ((b"sort.lww_table", 1), (b"sort.or_table", 1), (b"sort.or_lookback", 1),
                           (b"sort.sample_plan", 1)):
         assert lib.crdt_set_option(name, 2) == -1
@@ -91,6 +128,12 @@ def test_d2_path_options():
     assert lib.crdt_set_option(b"sort.sample_min", -1) == -1
     assert lib.crdt_set_option(b"sort.sample_min", 2**31) == -1
     assert lib.crdt_set_option(b"sort.sample_min", 1 << 20) == 0
+
+
+def test_diag_build_exports_the_same_symbols():
+    lib = _diag_lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
 
 
 def test_null_context_is_invalid_not_a_crash():

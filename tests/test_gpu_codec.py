@@ -10,6 +10,7 @@ import struct
 
 import numpy as np
 import pytest
+from knobs import set_knob
 import torch
 
 from crdt_amd import codec, gossip
@@ -17,18 +18,18 @@ from crdt_amd.refmerge import Command
 from crdt_amd.server import Server
 from gossip_util import K, KEYS, STRS, _host_round, _pack, _rand_diff, _same_diffs, _state, _unpack
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.diag]
 
 
-@pytest.fixture(params=[2, 0, 3], ids=["one_pass", "multi_pass", "one_pass_coalesced"], autouse=True)
+@pytest.fixture(params=[1, 2, 0, 3], ids=["auto", "one_pass", "multi_pass", "one_pass_coalesced"], autouse=True)
 def decode_form(request, eng):
-    """Every test under each decode form: the one-pass small-body kernel
-    (codec.small = 2: always), the multi-pass form (0) and the one-pass form
+    """Every test under each decode form: the product's choice by size
+    (codec.small = 1), the one-pass small-body kernel (2: always), the multi-pass form (0) and the one-pass form
     with coalesced accesses (3)."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"codec.small", request.param)
+    set_knob(b"codec.small", request.param)
     yield request.param
-    _lib.call("crdt_set_option", b"codec.small", 1)
+    set_knob(b"codec.small", 1)
 
 
 def _serve(diff) -> bytes:
@@ -230,7 +231,7 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
     bodies.insert(1, _raw_body([(1, [(b"a", b"1")])]) + b"")     # shifts the next body off 8-byte alignment
     out = []
     for form in (0, 2, 3):
-        _lib.call("crdt_set_option", b"codec.small", form)
+        set_knob(b"codec.small", form)
         keys, vals = codec.StrTab(eng), codec.StrTab(eng)
         dec, st, kk, kv = _decode(eng, bodies, keys, vals)
         h = {x: dec[x].cpu().numpy() for x in ("r_off", "r_ts", "r_kv")}
@@ -239,7 +240,7 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
         pairs = [(ks[kk[q] - 1000 * bi], vs[kv[q]]) for bi in range(len(bodies))
                  for q in range(h["r_kv"][h["r_off"][bi]], h["r_kv"][h["r_off"][bi + 1]])]
         out.append((st.tolist(), h, pairs, sorted(ks), sorted(vs)))
-    _lib.call("crdt_set_option", b"codec.small", decode_form)
+    set_knob(b"codec.small", decode_form)
     a = out[0]
     assert a[0] == [0, 0, 0, 0]
     for b in out[1:]:
@@ -264,7 +265,7 @@ def test_decode_resolved_short_forms_across_calls_and_rehash(eng, short_tab):
     and equal-padded strings of different lengths ("a" / "a\\x00") apart,
     8-byte and longer strings by the byte walk, and interns nothing new."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"codec.short_tab", short_tab)
+    set_knob(b"codec.short_tab", short_tab)
     try:
         keys, vals = codec.StrTab(eng, 4, 64), codec.StrTab(eng, 4, 64)       # tiny: grows in the first call
         strs = [b"", b"a", b"a\x00", b"a\x00\x00", b"\x00", b"x" * 7, b"x" * 8, b"x" * 9, b"7", b"-12", b"\xff" * 6]
@@ -287,4 +288,4 @@ def test_decode_resolved_short_forms_across_calls_and_rehash(eng, short_tab):
         assert [vs[kv1[3 + i]] for i in range(n)] == strs              # kv_base 3: pair i of entry i
         assert [ks[kk1[3 + n + i]] for i in range(n - 1)] == sorted(set(strs) - {b""})
     finally:
-        _lib.call("crdt_set_option", b"codec.short_tab", 3)
+        set_knob(b"codec.short_tab", 3)

@@ -7,12 +7,13 @@ oracle's merge of the lexsorted sides, and (pop.* knobs) two population
 rounds == the same rounds with the knob at its default."""
 import numpy as np
 import pytest
+from knobs import set_knob
 
 from crdt_amd import _lib, gossip, synth
 from crdt_amd.engine import TupleSet
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.diag]
 
 D2_KNOBS = [("sort.plan_cache", 0), ("sort.plan_cache", 1), ("sort.group_tile", 4096), ("sort.up_threads", 256),
             ("sort.or_sub_hist", 0), ("sort.or_place_batch", 0), ("sort.or_bucket", 0), ("sort.lww_gather", 0),
@@ -23,7 +24,7 @@ DEFAULTS = {"sort.plan_cache": 2, "sort.group_tile": 8192, "sort.up_threads": 51
 
 
 def _set(name, v):
-    _lib.call("crdt_set_option", name.encode(), v)
+    set_knob(name.encode(), v)
 
 
 def _np_sorted(t):

@@ -6,6 +6,7 @@ of 1, 2 and 3 words, dedup tile edges, empty sides, cross-side duplicate tags
 with differing tombs, and a full config-D pair checked by the two-sort path."""
 import numpy as np
 import pytest
+from knobs import set_knob
 
 from crdt_amd import synth
 from crdt_amd.engine import TupleSet
@@ -139,14 +140,15 @@ def test_unsorted_run_lengths_around_the_mark_limit(eng):
     _check(eng, a, b)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_unsorted_orset_sort_modes(eng, mode):
     """sort.or_key_only: 0 the full tag sort + neighbour dedup; 1 key bits only,
     key runs marked in LDS; 2 (default) the key and one more tag digit, groups
     of equal sorted bits marked in LDS.  All == the oracle."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"sort.or_key_only", mode)
-    _lib.call("crdt_set_option", b"sort.or_table", 0)
+    set_knob(b"sort.or_key_only", mode)
+    set_knob(b"sort.or_table", 0)
     try:
         ks = 30_000
         _check(eng, synth.set_tuples(71, 0, 100_000, ks), synth.set_tuples(71, 1, 90_000, ks))
@@ -154,10 +156,11 @@ def test_unsorted_orset_sort_modes(eng, mode):
         test_unsorted_run_lengths_around_the_mark_limit(eng)
         test_unsorted_single_tag(eng, 5000)
     finally:
-        _lib.call("crdt_set_option", b"sort.or_key_only", 2)
-        _lib.call("crdt_set_option", b"sort.or_table", 1)
+        set_knob(b"sort.or_key_only", 2)
+        set_knob(b"sort.or_table", 1)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("kbits,tbits", [(11, 20), (12, 20), (16, 20), (20, 8), (23, 20), (24, 20),
                                          (16, 40), (22, 40), (23, 40)])
 def test_unsorted_lww_key_tables(eng, kbits, tbits):
@@ -188,13 +191,13 @@ def test_unsorted_lww_key_tables(eng, kbits, tbits):
         b[f][:5000] = a[f][:5000]
     try:
         for on in (1, 0):
-            _lib.call("crdt_set_option", b"sort.lww_table", on)
-            _lib.call("crdt_set_option", b"sort.or_table", on)
+            set_knob(b"sort.lww_table", on)
+            set_knob(b"sort.or_table", on)
             _check(eng, a, b)
             _check(eng, a, tuple(x[:0] for x in b))
     finally:
-        _lib.call("crdt_set_option", b"sort.lww_table", 1)
-        _lib.call("crdt_set_option", b"sort.or_table", 1)
+        set_knob(b"sort.lww_table", 1)
+        set_knob(b"sort.or_table", 1)
 
 
 def _keyed(rng, keys, tbits=6):
@@ -210,6 +213,7 @@ def _keyed(rng, keys, tbits=6):
     return a, b
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("case", ["long_keys", "key_of_2000", "too_many_long_keys", "chunk_over_cap"])
 def test_unsorted_orset_tables_long_keys(eng, case):
     """OR-Set key chunks sorted in LDS around their limits (20 key bits:
@@ -234,14 +238,15 @@ def test_unsorted_orset_tables_long_keys(eng, case):
     a, b = _keyed(rng, np.concatenate([bg, extra, np.array([2**20 - 1], np.uint64)]))
     try:
         for on, lb in ((1, 1), (1, 0), (0, 1)):
-            _lib.call("crdt_set_option", b"sort.or_table", on)
-            _lib.call("crdt_set_option", b"sort.or_lookback", lb)
+            set_knob(b"sort.or_table", on)
+            set_knob(b"sort.or_lookback", lb)
             _check(eng, a, b)
     finally:
-        _lib.call("crdt_set_option", b"sort.or_table", 1)
-        _lib.call("crdt_set_option", b"sort.or_lookback", 1)
+        set_knob(b"sort.or_table", 1)
+        set_knob(b"sort.or_lookback", 1)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("outlier", [False, True])
 def test_unsorted_sampled_plans(eng, outlier):
     """The dense-key D2 paths from a sampled plan (sort.sample_plan; forced on
@@ -264,13 +269,13 @@ def test_unsorted_sampled_plans(eng, outlier):
         a[0][100] = 2**22          # (sampled: 256 runs of 64 tuples per side, ~784 / ~706 apart from index 0)
         b[1][100] = 2**40
     try:
-        _lib.call("crdt_set_option", b"sort.sample_min", 0)
+        set_knob(b"sort.sample_min", 0)
         for on in (1, 0):
-            _lib.call("crdt_set_option", b"sort.sample_plan", on)
+            set_knob(b"sort.sample_plan", on)
             _check(eng, a, b)
     finally:
-        _lib.call("crdt_set_option", b"sort.sample_plan", 1)
-        _lib.call("crdt_set_option", b"sort.sample_min", 1 << 20)
+        set_knob(b"sort.sample_plan", 1)
+        set_knob(b"sort.sample_min", 1 << 20)
 
 
 
@@ -301,6 +306,7 @@ def test_unsorted_refuses_out_aliasing_an_input(eng):
             np.testing.assert_array_equal(g, e)
 
 
+@pytest.mark.diag
 def test_unsorted_plan_cache_shape_changes(eng):
     """sort.plan_cache: a sampled dense-key call launches from the last such
     call's plan shape with no read-back, the device checking the fresh plan
@@ -315,11 +321,11 @@ def test_unsorted_plan_cache_shape_changes(eng):
                 rng.integers(0, 50, m, dtype=np.uint64).astype(np.uint32), rng.integers(0, 2, m, dtype=np.uint8))
 
     try:
-        _lib.call("crdt_set_option", b"sort.sample_min", 0)
+        set_knob(b"sort.sample_min", 0)
         for kbits, tbits in ((20, 20), (20, 20), (21, 20), (18, 24), (18, 24), (20, 20)):
             a, b = side(120_000, kbits, tbits), side(120_000, kbits, tbits)
             for f in range(3):
                 b[f][:2000] = a[f][:2000]
             _check(eng, a, b)
     finally:
-        _lib.call("crdt_set_option", b"sort.sample_min", 1 << 20)
+        set_knob(b"sort.sample_min", 1 << 20)

@@ -11,6 +11,7 @@ CurrentState, dead peers (-1) skip the round.
 """
 import numpy as np
 import pytest
+from knobs import set_knob
 
 from crdt_amd import gossip, shard
 from gossip_util import K, KEYS, STRS, _host_round, _pack, _rand_diff, _same_diffs
@@ -156,6 +157,7 @@ def test_population_undo_restores_the_previous_round(eng):
         pop.close()
 
 
+@pytest.mark.diag
 def test_population_failed_round_leaves_nothing_to_undo(eng):
     """A round that fails after the previous round succeeded (fault injection
     "fail.refmerge": its merge call returns an error) leaves the population
@@ -169,12 +171,12 @@ def test_population_failed_round_leaves_nothing_to_undo(eng):
     try:
         pop.round(gossip.random_peers(rng, P, 0, P))
         after = pop.read()
-        _lib.call("crdt_set_option", b"fail.refmerge", 1)
+        set_knob(b"fail.refmerge", 1)
         try:
             with pytest.raises(_lib.CrdtError):
                 pop.round(gossip.random_peers(rng, P, 0, P))
         finally:
-            _lib.call("crdt_set_option", b"fail.refmerge", 0)
+            set_knob(b"fail.refmerge", 0)
         with pytest.raises(_lib.CrdtError):
             pop.undo()
         now = pop.read()
@@ -331,6 +333,48 @@ def test_population_wire_round_refusals(eng):
         data, off = _upload(eng, [good, good, good])
         with pytest.raises(_lib.CrdtError):
             pop.round_wire(data, off, keys, other)
+    finally:
+        pop.close()
+
+
+@pytest.mark.parametrize("how", ["refused_first", "shared_vals"])
+def test_population_first_wire_round_with_strings_past_the_arena(eng, how):
+    """ADVICE r05 (population.hip, pop.wire_early): on a population's FIRST
+    wire round vals may already hold strings past the population's own
+    arena -- interned by a refused earlier round's good bodies, or by another
+    user of a shared table.  A pulled value resolving to such an id must take
+    part in the replay fold (main.go:75-98) == pyref."""
+    from crdt_amd import _lib
+    from test_gpu_codec import _raw_body, _serve, _upload
+    rng = np.random.default_rng(31)
+    P = 3
+    diffs = [_rand_diff(rng, 100 + 7 * i, 6) for i in range(P)]
+    keys, vals = _wire_tables(eng)
+    pop = gossip.NativePopulation(eng, _pack(diffs), K)
+    try:
+        # below every puller's max(L) (t0 >= 100), new strings only
+        pull = {50: {KEYS[2]: "17"}, 51: {KEYS[2]: "past-the-arena"}, 52: {KEYS[3]: "40"}, 53: {KEYS[3]: "2"}}
+        if how == "shared_vals":
+            vals.intern([b"40", b"past-the-arena", b"2", b"17"])
+        else:
+            good = _serve(pull)
+            data, off = _upload(eng, [good, _raw_body([(7, None)]), good])
+            with pytest.raises(_lib.CrdtError):
+                pop.round_wire(data, off, keys, vals)
+        if how == "shared_vals":
+            assert len(vals) > len(STRS)
+        pulls = [pull, None, pull]
+        data, off = _upload(eng, [_serve(p) if p is not None else b"" for p in pulls])
+        pop.round_wire(data, off, keys, vals)
+        strs = [x.decode() for x in vals.strings()]
+        states = [{} for _ in range(P)]
+        for i in range(P):
+            if pulls[i] is not None:
+                diffs[i], states[i] = pyref.merge(diffs[i], {t: dict(v) for t, v in pulls[i].items()})
+        h = pop.read()
+        _same_diffs(_unpack_native(h, P, strs), diffs)
+        assert _state_native(h, P, strs)[0] == states[0]
+        assert _state_native(h, P, strs) == states
     finally:
         pop.close()
 

@@ -7,6 +7,7 @@ keys, same value objects), same CurrentState strings.
 """
 import numpy as np
 import pytest
+from knobs import set_knob
 import torch
 
 from crdt_amd import refmerge, synth
@@ -221,6 +222,7 @@ def test_slice_write_without_slots(eng):
         np.testing.assert_array_equal(bare[k][:n].cpu().numpy(), full[k][:n].cpu().numpy())
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("parts", [2, 4])
 def test_tile_parts_match_oracle(eng, parts):
     """The tile pass at every workgroup shape (refmerge.tile_parts: 1/parts of
@@ -228,7 +230,7 @@ def test_tile_parts_match_oracle(eng, parts):
     batch with LDS-staged and global Atoi tables, the KATs and multi-key
     config-A replicas, every replica against the oracle."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"refmerge.tile_parts", parts)
+    set_knob(b"refmerge.tile_parts", parts)
     try:
         for n_str in (0, 257):
             test_packed_batch_matches_oracle(eng, n_str)
@@ -236,20 +238,21 @@ def test_tile_parts_match_oracle(eng, parts):
         test_config_a_demo_matches_oracle(eng, 1)
         test_large_batch_matches_oracle(eng)
     finally:
-        _lib.call("crdt_set_option", b"refmerge.tile_parts", 1)
+        set_knob(b"refmerge.tile_parts", 1)
 
 
+@pytest.mark.diag
 def test_count_pass_register_staging(eng):
     """refmerge.count_dma=0: the count pass stages the tile's ts through
     registers instead of LDS-DMA (also the path for logs that are not 8-byte
     aligned); same outputs on the packed batch and the KATs."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"refmerge.count_dma", 0)
+    set_knob(b"refmerge.count_dma", 0)
     try:
         test_packed_batch_matches_oracle(eng, 0)
         test_all_kats_in_one_batch(eng)
     finally:
-        _lib.call("crdt_set_option", b"refmerge.count_dma", 1)
+        set_knob(b"refmerge.count_dma", 1)
 
 
 def _expected_kv(h, src, n_out):

@@ -15,6 +15,7 @@
 import ctypes as C
 
 import pytest
+from knobs import set_knob
 import torch
 
 from crdt_amd import _lib
@@ -33,12 +34,13 @@ def _server_from(eng, diff, remote, port=8080):
     return s
 
 
+@pytest.mark.diag
 def test_failed_merge_leaves_server_untouched(eng):
     kat = next(k for k in load_kats() if k["name"].startswith("KAT-1"))
     diff, remote = kat_inputs(kat)
     s = _server_from(eng, diff, remote)
     before = (s.DiffSignature, s.RemoteDiff.Keys(), s.CurrentState, [s.RemoteDiff.Get(t) for t in remote])
-    _lib.call("crdt_set_option", b"fail.refmerge", 1)
+    set_knob(b"fail.refmerge", 1)
     with pytest.raises(_lib.CrdtError) as ei:
         s.merge()
     assert ei.value.status == -3                                   # CRDT_E_NOMEM, as injected
@@ -82,6 +84,7 @@ def test_null_ingest_is_reserved_as_null(eng):
     b.close()
 
 
+@pytest.mark.diag
 def test_inconsistent_bitmaps_fail_merge_cleanly(eng):
     """fail.zero_bits: the RefMerge bitmaps zeroed between its count and tile
     passes.  The tile pass raises CRDT_DEV_RANGE instead of reading past the
@@ -93,7 +96,7 @@ def test_inconsistent_bitmaps_fail_merge_cleanly(eng):
     s = _server_from(eng, diff, remote)
     for resident in (False, True):
         before = (s.DiffSignature, s.RemoteDiff.Keys(), s.CurrentState, [s.RemoteDiff.Get(t) for t in remote])
-        _lib.call("crdt_set_option", b"fail.zero_bits", 1)
+        set_knob(b"fail.zero_bits", 1)
         with pytest.raises(_lib.CrdtError) as ei:
             s.merge()
         assert ei.value.status == -8                               # CRDT_E_DEVICE
@@ -108,12 +111,13 @@ def test_inconsistent_bitmaps_fail_merge_cleanly(eng):
     s.close()
 
 
+@pytest.mark.diag
 def test_refmerge_batch_inconsistent_bitmaps_flag(eng):
     """The batched call: the flag is raised (crdt_ctx_device_status), no fault."""
     from crdt_amd import refmerge, synth
     h = synth.refmerge_packed(17, 6, 9000)
     d = refmerge.to_device(h, eng.device)
-    _lib.call("crdt_set_option", b"fail.zero_bits", 1)
+    set_knob(b"fail.zero_bits", 1)
     eng.refmerge_batch(d)
     assert eng.device_status(clear=True) == 2
     eng.refmerge_batch(d)

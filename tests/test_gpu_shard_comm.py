@@ -4,6 +4,7 @@ ncclCommInitRank one.  Outputs are checked against the oracle
 (oc_gcounter_fold, oc_lww_merge, oc_orset_merge)."""
 import numpy as np
 import pytest
+from knobs import set_knob
 import torch
 
 from crdt_amd import shard, synth
@@ -106,6 +107,7 @@ def test_comm_refmerge_matches_oracle(comm, eng, replicas, entries):
     _check_refmerge_vs_oracle(h, out)
 
 
+@pytest.mark.diag
 def test_init_rank_refmerge_and_local_sets(eng):
     """The same calls through ncclCommInitRank (nranks = 1) on the engine's
     own context and stream: crdt_shard_refmerge == oracle, and the
@@ -123,11 +125,11 @@ def test_init_rank_refmerge_and_local_sets(eng):
         A, B = TupleSet.from_numpy(*sa, eng.device), TupleSet.from_numpy(*sb, eng.device)
         from crdt_amd import _lib
         for lww in (True, False):
-            _lib.call("crdt_set_option", b"shard.exchange_always", 1)
+            set_knob(b"shard.exchange_always", 1)
             try:
                 got = c.set_merge_local([A], [B], lww=lww)[0].to_numpy()
             finally:
-                _lib.call("crdt_set_option", b"shard.exchange_always", 0)
+                set_knob(b"shard.exchange_always", 0)
             exp = (oracle.lww_merge if lww else oracle.orset_merge)(sa, sb)
             for g, e in zip(got, exp):
                 np.testing.assert_array_equal(g, e)
@@ -135,6 +137,7 @@ def test_init_rank_refmerge_and_local_sets(eng):
         c.close()
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("lww", [True, False])
 @pytest.mark.parametrize("gather", [True, False])
 @pytest.mark.parametrize("na,nb", [(200_000, 180_000), (0, 5000), (7, 0), (0, 0)])
@@ -149,11 +152,11 @@ def test_comm_set_merge_local_matches_oracle(comm, lww, gather, na, nb, exchange
     sb = synth.sort_tuples_np(*synth.set_tuples(91, 1, nb, 50_000))
     A, B = TupleSet.from_numpy(*sa, "cuda:0"), TupleSet.from_numpy(*sb, "cuda:0")
     torch.cuda.synchronize()
-    _lib.call("crdt_set_option", b"shard.exchange_always", exchange)
+    set_knob(b"shard.exchange_always", exchange)
     try:
         got = comm.set_merge_local([A], [B], lww=lww, gather=gather)[0].to_numpy()
     finally:
-        _lib.call("crdt_set_option", b"shard.exchange_always", 0)
+        set_knob(b"shard.exchange_always", 0)
     exp = (oracle.lww_merge if lww else oracle.orset_merge)(sa, sb)
     for g, e in zip(got, exp):
         np.testing.assert_array_equal(g, e)

@@ -5,6 +5,7 @@ oracle/crdt_oracle.c, whose semantics are pinned by tests/golden KATs.
 """
 import numpy as np
 import pytest
+from knobs import set_knob
 import torch
 
 from crdt_amd import synth
@@ -152,6 +153,7 @@ def test_sets_unaligned_views(eng, off_a, off_b):
             np.testing.assert_array_equal(g, e, err_msg=f"{fn.__name__}.{f}")
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("chunk,streams", [(0, 1), (1, 2), (3, 1), (7, 2), (64, 2)])
 def test_sets_chunked_schedules(eng, chunk, streams):
     """The count / write passes over chunks of tiles (sets.lww_chunk,
@@ -160,7 +162,7 @@ def test_sets_chunked_schedules(eng, chunk, streams):
     tile edges, unaligned views; == the oracle."""
     from crdt_amd import _lib
     for name, v in ((b"sets.lww_chunk", chunk), (b"sets.or_chunk", chunk), (b"sets.streams", streams)):
-        _lib.call("crdt_set_option", name, v)
+        set_knob(name, v)
     try:
         _check(eng, *_sets(77, 100_000, 100_000, 50_000))
         _check(eng, *_sets(78, 4097, 4095, 1000))
@@ -170,9 +172,10 @@ def test_sets_chunked_schedules(eng, chunk, streams):
         assert eng.device_status(clear=True) == 0
     finally:
         for name, v in ((b"sets.lww_chunk", 0), (b"sets.or_chunk", 0), (b"sets.streams", 1)):
-            _lib.call("crdt_set_option", name, v)
+            set_knob(name, v)
 
 
+@pytest.mark.diag
 def test_sets_inconsistent_bitmaps_raise_range(eng):
     """fail.zero_bits: the merge bitmaps zeroed between the count and write
     passes (the GPU fault of DESIGN.md §5.4's timing build): every write-pass
@@ -185,20 +188,21 @@ def test_sets_inconsistent_bitmaps_raise_range(eng):
     A = TupleSet.from_numpy(*sa, eng.device)
     B = TupleSet.from_numpy(*sb, eng.device)
     for fn in (eng.lww_merge, eng.orset_merge):
-        _lib.call("crdt_set_option", b"fail.zero_bits", 1)
+        set_knob(b"fail.zero_bits", 1)
         with pytest.raises(CrdtLibraryError, match="0x2"):
             fn(A, B)
         assert eng.device_status(clear=True) == 0
     _check(eng, sa, sb)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("parts", [2, 8, 16])
 def test_lww_write_parts(eng, parts):
     """The LWW write pass at every workgroup shape (sets.lww_parts: 1/parts of
     a 4096-item tile per workgroup; default 4): tile and part edges, long key
     runs across parts, unaligned views (register staging)."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"sets.lww_parts", parts)
+    set_knob(b"sets.lww_parts", parts)
     try:
         _check(eng, *_sets(91, 100_000, 90_000, 40_000))
         for na, nb in ((4095, 1), (4096, 4096), (1023, 1025), (255, 257), (0, 5000)):
@@ -206,16 +210,17 @@ def test_lww_write_parts(eng, parts):
         test_sets_long_runs_cross_tiles(eng)
         test_sets_unaligned_views(eng, 3, 5)
     finally:
-        _lib.call("crdt_set_option", b"sets.lww_parts", 4)
+        set_knob(b"sets.lww_parts", 4)
 
 
+@pytest.mark.diag
 @pytest.mark.parametrize("parts", [1, 2, 4])
 def test_orset_write_parts(eng, parts):
     """The OR-Set write pass at every workgroup shape (sets.or_parts: 1/parts
     of a 2048-item tile per workgroup): tile and part edges, tag copies that
     run past a part (the global-memory walk), unaligned views."""
     from crdt_amd import _lib
-    _lib.call("crdt_set_option", b"sets.or_parts", parts)
+    set_knob(b"sets.or_parts", parts)
     try:
         _check(eng, *_sets(93, 100_000, 90_000, 40_000))
         for na, nb in ((2047, 1), (2048, 2048), (511, 513), (1023, 1025), (0, 3000)):
@@ -225,4 +230,4 @@ def test_orset_write_parts(eng, parts):
         test_sets_unaligned_views(eng, 3, 5)
         test_sets_unaligned_views(eng, 13, 11)
     finally:
-        _lib.call("crdt_set_option", b"sets.or_parts", 2)
+        set_knob(b"sets.or_parts", 2)

@@ -21,7 +21,7 @@ knob=$1; va=$2; vb=$3; wls=$4; pairs=${5:-2}; tests=${6:-}; kre=${7:-}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/ab_${knob//./_}; mkdir -p $O
 if [ -n "$tests" ]; then
-  (cd $R && CRDT_TEST_OPTIONS="$knob=$vb" timeout -k 10 600 python -u -m pytest $tests -m gpu -x -q \
+  (cd $R && CRDT_AMD_DIAG=1 CRDT_TEST_OPTIONS="$knob=$vb" timeout -k 10 600 python -u -m pytest $tests -m gpu -x -q \
       --timeout 300 --timeout-method thread > $O/tests_$vb.log 2>&1) || { tail -30 $O/tests_$vb.log; exit 1; }
   tail -1 $O/tests_$vb.log
 fi
