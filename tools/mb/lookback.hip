@@ -72,6 +72,73 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *tot) {
     return off + x - v;
 }
 
+// Striped tile layout (round 6, VERDICT r05: the blocked layout above ran
+// the no-look-back pass at half the copy rate -- each uint4 load touched 16 B
+// of every 64 B across the wave): item (k, lane-major) = tile + (k * TB +
+// tid) * 4 + j, so every load and store instruction covers a contiguous
+// span of the wave.  The block scan runs over the IPT / 4 groups in k-major
+// order: wave scans of the four group sums at once, one barrier.
+constexpr int G = IPT / 4;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void load_striped(const uint32_t *__restrict__ in, size_t tile0, uint32_t (&v)[IPT],
+                                             uint64_t (&s)[G]) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const u32x4 q = __builtin_nontemporal_load((const u32x4 *)(in + tile0 + ((size_t)k * TB + threadIdx.x) * 4));
+        v[4 * k] = q.x, v[4 * k + 1] = q.y, v[4 * k + 2] = q.z, v[4 * k + 3] = q.w;
+        s[k] = (uint64_t)q.x + q.y + q.z + q.w;
+    }
+}
+// ex[k] = exclusive prefix of (k, tid) within the tile; returns the tile total
+__device__ __forceinline__ uint64_t block_scan_g(const uint64_t (&s)[G], uint64_t (&ex)[G]) {
+    __shared__ uint64_t s_w[G][TB / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) x[k] = s[k];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const uint64_t y = __shfl_up(x[k], o);
+            if (lane >= o) x[k] += y;
+        }
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) s_w[k][w] = x[k];
+    }
+    __syncthreads();
+    uint64_t run = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        uint64_t before = 0, all = 0;
+#pragma unroll
+        for (int q = 0; q < TB / 64; ++q) {
+            before += q < w ? s_w[k][q] : 0;
+            all += s_w[k][q];
+        }
+        ex[k] = run + before + x[k] - s[k];
+        run += all;
+    }
+    __syncthreads();
+    return run;
+}
+__device__ __forceinline__ void store_striped(uint64_t *__restrict__ out, size_t tile0, const uint32_t (&v)[IPT],
+                                              const uint64_t (&ex)[G], uint64_t base) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        uint64_t r = base + ex[k];
+        uint64_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = r, r += v[4 * k + j];
+        u64x2v *p = (u64x2v *)(out + tile0 + ((size_t)k * TB + threadIdx.x) * 4);
+        __builtin_nontemporal_store((u64x2v){o[0], o[1]}, p);
+        __builtin_nontemporal_store((u64x2v){o[2], o[3]}, p + 1);
+    }
+}
+
 // mode 0: serial look-back by one thread; mode 1: no look-back (timing only);
 // mode 2: 64-lane window look-back (one status per lane, a ballot for the
 // first inclusive flag, a wave reduction; first poll without s_sleep)
@@ -80,18 +147,11 @@ __global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in,
                                                 unsigned long long *st, uint32_t chunk, unsigned *err) {
     __shared__ uint64_t s_base;
     const uint32_t t = tile_of(blockIdx.x, chunk);
-    const size_t base = (size_t)t * TILE + (size_t)threadIdx.x * IPT;
+    const size_t tile0 = (size_t)t * TILE;
     uint32_t v[IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; k += 4) {
-        const uint4 q = *(const uint4 *)(in + base + k);
-        v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
-    }
-    uint64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) s += v[k];
-    uint64_t tot;
-    const uint64_t ex = block_scan(s, &tot);
+    uint64_t gs[G], ex[G];
+    load_striped(in, tile0, v, gs);
+    const uint64_t tot = block_scan_g(gs, ex);
     if (MODE == 2) {                                        // 64-lane window look-back by wave 0
         if (threadIdx.x < 64) {
             const int lane = threadIdx.x;
@@ -157,27 +217,14 @@ __global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in,
         s_base = pre;
     }
     __syncthreads();
-    uint64_t run = s_base + ex;
-    uint64_t o[IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        o[k] = run;
-        run += v[k];
-    }
-#pragma unroll
-    for (int k = 0; k < IPT; k += 2) *(ulonglong2 *)(out + base + k) = ulonglong2{o[k], o[k + 1]};
+    store_striped(out, tile0, v, ex, s_base);
 }
 
 __global__ __launch_bounds__(TB) void k_reduce(const uint32_t *__restrict__ in, uint64_t *__restrict__ sums) {
-    const size_t base = (size_t)blockIdx.x * TILE + (size_t)threadIdx.x * IPT;
-    uint64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < IPT; k += 4) {
-        const uint4 q = *(const uint4 *)(in + base + k);
-        s += (uint64_t)q.x + q.y + q.z + q.w;
-    }
-    uint64_t tot;
-    (void)block_scan(s, &tot);
+    uint32_t v[IPT];
+    uint64_t gs[G], ex[G];
+    load_striped(in, (size_t)blockIdx.x * TILE, v, gs);
+    const uint64_t tot = block_scan_g(gs, ex);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
@@ -206,26 +253,23 @@ __global__ __launch_bounds__(1024) void k_scan_sums(uint64_t *sums, uint32_t n) 
 
 __global__ __launch_bounds__(TB) void k_apply(const uint32_t *__restrict__ in, const uint64_t *__restrict__ sums,
                                               uint64_t *__restrict__ out) {
-    const size_t base = (size_t)blockIdx.x * TILE + (size_t)threadIdx.x * IPT;
     uint32_t v[IPT];
+    uint64_t gs[G], ex[G];
+    const size_t tile0 = (size_t)blockIdx.x * TILE;
+    load_striped(in, tile0, v, gs);
+    (void)block_scan_g(gs, ex);
+    store_striped(out, tile0, v, ex, sums[blockIdx.x]);
+}
+
+// the copy-rate reference of this access pattern: read the u32s, write u64s
+__global__ __launch_bounds__(TB) void k_copy(const uint32_t *__restrict__ in, uint64_t *__restrict__ out) {
+    uint32_t v[IPT];
+    uint64_t gs[G], ex[G];
+    const size_t tile0 = (size_t)blockIdx.x * TILE;
+    load_striped(in, tile0, v, gs);
 #pragma unroll
-    for (int k = 0; k < IPT; k += 4) {
-        const uint4 q = *(const uint4 *)(in + base + k);
-        v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
-    }
-    uint64_t s = 0;
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) s += v[k];
-    uint64_t tot;
-    uint64_t run = sums[blockIdx.x] + block_scan(s, &tot);
-    uint64_t o[IPT];
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-        o[k] = run;
-        run += v[k];
-    }
-#pragma unroll
-    for (int k = 0; k < IPT; k += 2) *(ulonglong2 *)(out + base + k) = ulonglong2{o[k], o[k + 1]};
+    for (int k = 0; k < G; ++k) ex[k] = 0;
+    store_striped(out, tile0, v, ex, gs[0]);
 }
 
 int main(int argc, char **argv) {
@@ -283,6 +327,7 @@ int main(int argc, char **argv) {
         k_scan_sums<<<1, 1024>>>(d_sums, ntiles);
         k_apply<<<ntiles, TB>>>(d_in, d_sums, d_out);
     }, true);
+    timeit("copy (no scan: the access-pattern peak)", [&] { k_copy<<<ntiles, TB>>>(d_in, d_out); }, false);
     timeit("one pass, no look-back", [&] { k_onepass<1><<<ntiles, TB>>>(d_in, d_out, d_st, 0, d_err); }, false);
     const uint32_t chunks[] = {0, 1, 4, 16, 64, 512};
     for (uint32_t c : chunks) {
@@ -291,17 +336,17 @@ int main(int argc, char **argv) {
         if (c == 0) snprintf(name, sizeof name, "look-back, blockIdx order");
         else snprintf(name, sizeof name, "look-back, XCD chunks of %u", c);
         timeit(name, [&] {
-            hipMemsetAsync(d_st, 0, ntiles * 8);
+            (void)hipMemsetAsync(d_st, 0, ntiles * 8);
             k_onepass<0><<<ntiles, TB>>>(d_in, d_out, d_st, c, d_err);
         }, true);
         if (c == 0) snprintf(name, sizeof name, "window look-back, blockIdx");
         else snprintf(name, sizeof name, "window look-back, XCD chunks %u", c);
         timeit(name, [&] {
-            hipMemsetAsync(d_st, 0, ntiles * 8);
+            (void)hipMemsetAsync(d_st, 0, ntiles * 8);
             k_onepass<2><<<ntiles, TB>>>(d_in, d_out, d_st, c, d_err);
         }, true);
     }
-    timeit("memset of the status words", [&] { hipMemsetAsync(d_st, 0, ntiles * 8); }, false);
+    timeit("memset of the status words", [&] { (void)hipMemsetAsync(d_st, 0, ntiles * 8); }, false);
     CK(hipFree(d_in));
     CK(hipFree(d_out));
     CK(hipFree(d_sums));
