@@ -78,10 +78,12 @@ extern std::atomic<int> g_fail_zero_bits;  // the next n two-pass merges zero th
 bool take_fail_zero_bits();                // consumes one "fail.zero_bits" count
 bool take_fail_refmerge();                 // consumes one "fail.refmerge" count
 inline bool fail_refmerge_armed() { return g_fail_refmerge.load() != 0; }
+inline bool fail_zero_bits_armed() { return g_fail_zero_bits.load() != 0; }
 #else
 constexpr bool take_fail_zero_bits() { return false; }
 constexpr bool take_fail_refmerge() { return false; }
 constexpr bool fail_refmerge_armed() { return false; }
+constexpr bool fail_zero_bits_armed() { return false; }
 #endif
 
 // The context's aux stream / an event pool of at least n events (capi.hip).

@@ -206,4 +206,55 @@ struct CountSrc {
     __device__ Item load(uint64_t i) const { return Item{in[i]}; }
 };
 
+
+// Decoupled look-back (OR-Set D2 chunks, the fused D1 set merges): status
+// word per tile / chunk -- kOcA | count once counted, kOcP | inclusive prefix
+// once resolved, 0 not yet published.  Tiles are dispatched in index order,
+// so every polled one has been dispatched; polls are bounded
+// (CRDT_DEV_LOOKBACK).
+constexpr unsigned long long kOcA = 1ull << 62, kOcP = 2ull << 62, kOcVal = (1ull << 62) - 1;
+// The sum of chunk counts from chunk j back to the nearest inclusive prefix
+// (that prefix included): one wave, each lane loading U consecutive status
+// words per window (64 U chunks per round trip; the aggregates are all
+// published early, so a walk that has to reach far back costs round trips,
+// not waits).  Polls bounded: CRDT_DEV_LOOKBACK, never a hang.
+template <int U>
+__device__ unsigned long long lookback_sum(const unsigned long long *st, long long j, int lane, uint32_t *err) {
+    unsigned long long acc = 0;
+    uint32_t spins = 0;
+    for (;;) {
+        unsigned long long f[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long q = j - (long long)(lane * U + u);
+            f[u] = q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kOcP;
+        }
+        int fu = U;                                   // this lane's nearest inclusive prefix
+#pragma unroll
+        for (int u = U - 1; u >= 0; --u)
+            if ((f[u] >> 62) == 2) fu = u;
+        const uint64_t isp = __ballot(fu < U);
+        const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
+        const int upto = lane < pl ? U - 1 : lane == pl ? fu : -1;   // this lane's words in the sum
+        bool nr = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) nr = nr || (u <= upto && (f[u] >> 62) == 0);
+        if (__ballot(nr)) {
+            if (++spins > (1u << 22)) {               // bounded: report, never hang
+                if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
+                return acc;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        unsigned long long v = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) v += u <= upto ? (f[u] & kOcVal) : 0ull;
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc += v;
+        if (pl < 64) return acc;
+        j -= 64 * U;
+    }
+}
+
 }  // namespace crdt

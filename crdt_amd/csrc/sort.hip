@@ -1822,50 +1822,6 @@ __global__ __launch_bounds__(256) void k_chunk_bounds(const uint64_t *__restrict
 // reads 64 predecessors per poll, nearest first, and sums back to the
 // nearest resolved one.  Chunks are dispatched in index order, so every
 // polled chunk has been dispatched; polls are bounded (CRDT_DEV_LOOKBACK).
-constexpr unsigned long long kOcA = 1ull << 62, kOcP = 2ull << 62, kOcVal = (1ull << 62) - 1;
-// The sum of chunk counts from chunk j back to the nearest inclusive prefix
-// (that prefix included): one wave, each lane loading U consecutive status
-// words per window (64 U chunks per round trip; the aggregates are all
-// published early, so a walk that has to reach far back costs round trips,
-// not waits).  Polls bounded: CRDT_DEV_LOOKBACK, never a hang.
-template <int U>
-__device__ unsigned long long or_lookback(const unsigned long long *st, long long j, int lane, uint32_t *err) {
-    unsigned long long acc = 0;
-    uint32_t spins = 0;
-    for (;;) {
-        unsigned long long f[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const long long q = j - (long long)(lane * U + u);
-            f[u] = q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kOcP;
-        }
-        int fu = U;                                   // this lane's nearest inclusive prefix
-#pragma unroll
-        for (int u = U - 1; u >= 0; --u)
-            if ((f[u] >> 62) == 2) fu = u;
-        const uint64_t isp = __ballot(fu < U);
-        const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
-        const int upto = lane < pl ? U - 1 : lane == pl ? fu : -1;   // this lane's words in the sum
-        bool nr = false;
-#pragma unroll
-        for (int u = 0; u < U; ++u) nr = nr || (u <= upto && (f[u] >> 62) == 0);
-        if (__ballot(nr)) {
-            if (++spins > (1u << 22)) {               // bounded: report, never hang
-                if (lane == 0) atomicOr(err, CRDT_DEV_LOOKBACK);
-                return acc;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        unsigned long long v = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) v += u <= upto ? (f[u] & kOcVal) : 0ull;
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        acc += v;
-        if (pl < 64) return acc;
-        j -= 64 * U;
-    }
-}
 // K (sort.or_pair): chunks per workgroup.  K = 2 processes two consecutive
 // chunks in turn, each into its own LDS output buffer, and looks back ONCE,
 // for the first, after both are placed -- by then its predecessors have had
@@ -2092,8 +2048,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         const uint32_t nt0 = s_totk[0];
         unsigned long long acc = 0;
         if (ci > 0) {
-            acc = lbw == 4 ? or_lookback<4>(st, (long long)ci - 1, lane, err)
-                           : or_lookback<1>(st, (long long)ci - 1, lane, err);
+            acc = lbw == 4 ? lookback_sum<4>(st, (long long)ci - 1, lane, err)
+                           : lookback_sum<1>(st, (long long)ci - 1, lane, err);
             if (lane == 0)
                 __hip_atomic_store(&st[ci], kOcP | (acc + nt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2174,8 +2130,8 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         const uint32_t ci = blockIdx.x * K, n0 = s_totk[0], n1 = K == 2 ? s_totk[K - 1] : 0u;
         unsigned long long acc = 0;
         if (ci > 0) {
-            acc = lbw == 4 ? or_lookback<4>(st, (long long)ci - 1, lane, err)
-                           : or_lookback<1>(st, (long long)ci - 1, lane, err);
+            acc = lbw == 4 ? lookback_sum<4>(st, (long long)ci - 1, lane, err)
+                           : lookback_sum<1>(st, (long long)ci - 1, lane, err);
             if (lane == 0)
                 __hip_atomic_store(&st[ci], kOcP | (acc + n0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }

@@ -1,8 +1,8 @@
 #!/bin/bash
 # rocprofv3 --kernel-trace --stats of one bench workload (no counters): per-kernel averages.
-# Usage: tools/kstats.sh <workload> [extra bench args...]
+# Usage: [KS_TAG=_x] tools/kstats.sh <workload> [extra bench args...]
 wl=$1; shift
-O=$GRAFT_REPO_ROOT/gpurun_out/ks_$wl; mkdir -p $O
+O=$GRAFT_REPO_ROOT/gpurun_out/ks_${wl}${KS_TAG}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- \
   python3 $GRAFT_REPO_ROOT/bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-e2e "$@" > $O/bench.json 2> $O/bench.err || exit 1
