@@ -15,6 +15,7 @@ namespace crdt {
 #undef KNOB
 std::atomic<int> g_fail_refmerge{0};
 std::atomic<int> g_fail_zero_bits{0};
+std::atomic<int> g_fail_d2_plan{0};
 
 static bool take_count(std::atomic<int> &c) {
     for (int f = c.load(); f > 0;)
@@ -23,6 +24,7 @@ static bool take_count(std::atomic<int> &c) {
 }
 bool take_fail_zero_bits() { return take_count(g_fail_zero_bits); }
 bool take_fail_refmerge() { return take_count(g_fail_refmerge); }
+bool take_fail_d2_plan() { return take_count(g_fail_d2_plan); }
 #endif
 
 int ws_reserve(crdt_ctx *ctx, size_t bytes) {
@@ -338,9 +340,13 @@ extern "C" int crdt_get_option(const char *name, int64_t *v) {
 extern "C" int crdt_set_option(const char *name, int64_t v) {
     if (!name) return CRDT_E_INVAL;
 #ifdef CRDT_DIAG
-    if (!strcmp(name, "fail.refmerge") || !strcmp(name, "fail.zero_bits")) {
+    std::atomic<int> *fp = !strcmp(name, "fail.refmerge")    ? &g_fail_refmerge
+                           : !strcmp(name, "fail.zero_bits") ? &g_fail_zero_bits
+                           : !strcmp(name, "fail.d2_plan")   ? &g_fail_d2_plan
+                                                             : nullptr;
+    if (fp) {
         if (v < 0 || v > 1000) return CRDT_E_INVAL;
-        (name[5] == 'r' ? g_fail_refmerge : g_fail_zero_bits) = (int)v;
+        *fp = (int)v;
         return CRDT_OK;
     }
 #endif

@@ -75,13 +75,16 @@ inline int hip_fail(crdt_ctx *ctx, hipError_t e) {
 // Failpoints (crdt_set_option "fail.*", diagnostic build only): error-path tests.
 extern std::atomic<int> g_fail_refmerge;   // the next n RefMerge calls return CRDT_E_NOMEM
 extern std::atomic<int> g_fail_zero_bits;  // the next n two-pass merges zero their bitmaps between the passes
+extern std::atomic<int> g_fail_d2_plan;    // the next n checked D2 calls find their device plan changed
 bool take_fail_zero_bits();                // consumes one "fail.zero_bits" count
 bool take_fail_refmerge();                 // consumes one "fail.refmerge" count
+bool take_fail_d2_plan();                  // consumes one "fail.d2_plan" count
 inline bool fail_refmerge_armed() { return g_fail_refmerge.load() != 0; }
 inline bool fail_zero_bits_armed() { return g_fail_zero_bits.load() != 0; }
 #else
 constexpr bool take_fail_zero_bits() { return false; }
 constexpr bool take_fail_refmerge() { return false; }
+constexpr bool take_fail_d2_plan() { return false; }
 constexpr bool fail_refmerge_armed() { return false; }
 constexpr bool fail_zero_bits_armed() { return false; }
 #endif

@@ -52,6 +52,38 @@ struct SortPlan {
     crdt_tuples in2;
 };
 
+// The launch shape a pass was sized for, by value: a
+// pass launched from a host-known plan (cached, sampled, planned) compares
+// the device plan with it first and, on any difference, raises the plan's
+// check word and stores nothing -- its grids, tables, buckets and chunks
+// are never indexed by a shape they were not sized for (the fault of commit
+// 01a0e59).  The unplanned calls redo from the exact plan on a raised check;
+// the planned ones raise CRDT_DEV_PLAN (k_d2_check).  viol == nullptr: an
+// exact plan the host read back, nothing to check.
+struct PlanGuard {
+    uint32_t bk, bt, br, W, P, words, b0, s0, tl, tw;
+    uint32_t *viol;
+};
+__device__ __forceinline__ bool plan_guard_ok(const SortPlan &p, const PlanGuard &g) {
+    if (!g.viol) return true;
+    if (p.bk == g.bk && p.bt == g.bt && p.br == g.br && p.W == g.W && p.P == g.P && p.words == g.words &&
+        p.b0 == g.b0 && p.s0 == g.s0 && p.tl == g.tl && p.tw == g.tw)
+        return true;
+    if (threadIdx.x == 0) atomicOr(g.viol, 1u);
+    return false;
+}
+// The guard of the D2 call this host thread is launching (GuardScope in
+// d2_body); none outside one.
+static thread_local PlanGuard t_guard{};
+static PlanGuard cur_guard() { return t_guard; }
+struct GuardScope {
+    explicit GuardScope(const SortPlan &h, uint32_t *viol) { set(h, viol); }
+    ~GuardScope() { t_guard = PlanGuard{}; }
+    void set(const SortPlan &h, uint32_t *viol) {
+        t_guard = viol ? PlanGuard{h.bk, h.bt, h.br, h.W, h.P, h.words, h.b0, h.s0, h.tl, h.tw, viol} : PlanGuard{};
+    }
+};
+
 struct SortMinMax {              // one per minmax workgroup, reduced by k_sort_plan
     unsigned long long kmin, kmax, tmin, tmax, rmin, rmax;
 };
@@ -399,11 +431,12 @@ template <int WORDS, bool FIRST>
 __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
                                                 const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
                                                 uint32_t *__restrict__ cnt, uint64_t *__restrict__ comp,
-                                                uint32_t *__restrict__ viol = nullptr) {
+                                                uint32_t *__restrict__ viol = nullptr, PlanGuard pg = {}) {
     __shared__ uint32_t h[SWAVES * 256];          // one histogram per wave: fewer LDS atomic collisions
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const size_t base = (size_t)blockIdx.x * ST;
     CKey<WORDS> c[SR];
     sort_load<WORDS, FIRST>(in, src, n, p, base, c);
@@ -448,11 +481,12 @@ __global__ __launch_bounds__(SB) void k_sort_up(crdt_tuples in, const uint64_t *
 // counts do not depend on which lane composes which tuple.
 __global__ __launch_bounds__(SB) void k_sort_up_vec(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                     uint32_t ntiles, uint32_t *__restrict__ cnt,
-                                                    uint64_t *__restrict__ comp, uint32_t *__restrict__ viol) {
+                                                    uint64_t *__restrict__ comp, uint32_t *__restrict__ viol, PlanGuard pg = {}) {
     __shared__ uint32_t h[SWAVES * 256];
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < SWAVES * 256; i += SB) h[i] = 0;
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const size_t base = (size_t)blockIdx.x * ST;
     uint64_t c[SR];
     bool bad = false;                                 // (viol) a field outside the plan's ranges
@@ -555,7 +589,7 @@ template <int WORDS, bool FIRST, bool LAST>
 __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t *__restrict__ src, size_t n,
                                                   const SortPlan *__restrict__ plan_, uint32_t pass, uint32_t ntiles,
                                                   const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
-                                                  uint64_t *__restrict__ dst, crdt_tuples out, int xcd) {
+                                                  uint64_t *__restrict__ dst, crdt_tuples out, int xcd, PlanGuard pg = {}) {
     // wc: per (round, wave, digit) counts, then their exclusive prefix;
     // reused (after the ranks are taken) as the staging area of the tile
     constexpr int WC_BYTES = SR * SWAVES * 256 * 2;
@@ -566,6 +600,7 @@ __global__ __launch_bounds__(SB) void k_sort_pass(crdt_tuples in, const uint64_t
     uint16_t *wc = (uint16_t *)lds;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     // each XCD's workgroups take one contiguous range of tiles: tile t's and
     // t + 1's runs of a digit are adjacent in the output, so their partial
     // lines meet in one L2 instead of two (sort.xcd_tiles; speed only)
@@ -677,13 +712,17 @@ static void launch_pass(bool first, bool last, unsigned grid, hipStream_t st, co
                         const uint32_t *tot, uint64_t *dst, const crdt_tuples &out) {
     const int x = g_sort_xcd;
     if (first && last)
-        k_sort_pass<WORDS, true, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
+        k_sort_pass<WORDS, true, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x,
+                                                             cur_guard());
     else if (first)
-        k_sort_pass<WORDS, true, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
+        k_sort_pass<WORDS, true, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x,
+                                                             cur_guard());
     else if (last)
-        k_sort_pass<WORDS, false, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
+        k_sort_pass<WORDS, false, true><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x,
+                                                             cur_guard());
     else
-        k_sort_pass<WORDS, false, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x);
+        k_sort_pass<WORDS, false, false><<<grid, SB, 0, st>>>(in, src, n, plan, pass, grid, loc, tot, dst, out, x,
+                                                             cur_guard());
 }
 
 // P passes; the last decodes into `out`, or (decode = false) leaves the
@@ -699,11 +738,12 @@ static int sort_words(crdt_ctx *ctx, const crdt_tuples &in, size_t n, const crdt
     for (uint32_t q = 0; q < P; ++q) {
         // pass 0's upsweep composes from the tuples and stores the composites
         if (q == 0 && WORDS == 1 && vec_first)
-            k_sort_up_vec<<<ntiles, SB, 0, st>>>(in, n, plan_d, ntiles, cnt, a, viol);
+            k_sort_up_vec<<<ntiles, SB, 0, st>>>(in, n, plan_d, ntiles, cnt, a, viol, cur_guard());
         else if (q == 0)
-            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a, viol);
+            k_sort_up<WORDS, true><<<ntiles, SB, 0, st>>>(in, nullptr, n, plan_d, q, ntiles, cnt, a, viol, cur_guard());
         else
-            k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr);
+            k_sort_up<WORDS, false><<<ntiles, SB, 0, st>>>(in, a, n, plan_d, q, ntiles, cnt, nullptr, nullptr,
+                                                              cur_guard());
         k_sort_colscan<<<256, CSB, 0, st>>>(cnt, ntiles, loc, tot, q == 0 ? zero : nullptr);
         launch_pass<WORDS>(false, decode && q + 1 == P, ntiles, st, in, a, n, plan_d, q, loc, tot, b, out);
         std::swap(a, b);
@@ -888,10 +928,11 @@ __device__ __forceinline__ void dd_load(const uint64_t *__restrict__ c, size_t n
 
 template <int MODE, int WORDS>
 __global__ __launch_bounds__(DB) void k_dd_count(const uint64_t *__restrict__ c, size_t n,
-                                                 const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt) {
+                                                 const SortPlan *__restrict__ plan_, uint32_t *__restrict__ cnt, PlanGuard pg = {}) {
     __shared__ uint32_t s_w[DB / 64];
     __shared__ DdEdges<WORDS> s_x;
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const size_t base = (size_t)blockIdx.x * DT;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t m = 0;
@@ -924,11 +965,12 @@ template <int MODE, int WORDS>
 __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c, size_t n,
                                                  const SortPlan *__restrict__ plan_, const uint32_t *__restrict__ loc,
                                                  const uint32_t *__restrict__ tot, crdt_tuples out,
-                                                 uint64_t *__restrict__ out_count, int diag = 0) {
+                                                 uint64_t *__restrict__ out_count, int diag = 0, PlanGuard pg = {}) {
     __shared__ uint32_t s_c[DI * (DB / 64)];      // emits per (round, wave), then their exclusive prefix
     __shared__ uint64_t s_v[MODE == DD_LWW ? DT * WORDS : 1];   // LWW: the tile's composites (run walks)
     __shared__ DdEdges<WORDS> s_x;
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const size_t base = (size_t)blockIdx.x * DT;
     if (blockIdx.x == 0 && tid == 0) *out_count = tot[0];
@@ -1095,7 +1137,7 @@ template <typename E>
 __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
                                                    const uint32_t *__restrict__ tot,
                                                    unsigned long long *__restrict__ flag, crdt_tuples out,
-                                                   uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
+                                                   uint64_t *__restrict__ out_count, uint32_t *__restrict__ err, PlanGuard pg = {}) {
     constexpr uint32_t NE = kLtBytes / sizeof(E);  // 2^15 u32 / 2^14 u64 entries
     constexpr uint32_t NR = NE / LTB;              // table rounds at most
     static_assert(NR * LT_WAVES <= 64 * 8, "one wave scans the round counts");
@@ -1103,6 +1145,7 @@ __global__ __launch_bounds__(LTB) void k_lww_table(const uint64_t *__restrict__ 
     __shared__ uint32_t s_cnt[NR * LT_WAVES];      // present keys per (round, wave), then their prefix
     __shared__ unsigned long long s_sum[3];        // bucket start, predecessors' keys, own keys
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x, L = p.tl, ne = 1u << L;
     const uint32_t kb = p.b0 + p.br + p.bt;        // tag bits under the key (< 8 * sizeof(E))
@@ -1228,7 +1271,8 @@ template <int UB, int TILE, bool HIST = false>
 __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, const SortPlan *__restrict__ plan_,
                                                      uint32_t ntiles, uint32_t *__restrict__ run,
                                                      uint64_t *__restrict__ comp, uint32_t *__restrict__ viol,
-                                                     unsigned long long *__restrict__ zero, SubHist sh_ = {}) {
+                                                     unsigned long long *__restrict__ zero, SubHist sh_ = {},
+                                                     PlanGuard pg = {}) {
     constexpr int UR = TILE / UB;                     // composites per thread
     static_assert(TILE < 65536, "16-bit run starts and counts");
     __shared__ uint32_t h[256], hs[256];
@@ -1245,6 +1289,7 @@ __global__ __launch_bounds__(UB) void k_lww_up_tiled(crdt_tuples in, size_t n, c
         if (tid == 0) zero[256] = 0;
     }
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const size_t base = (size_t)blockIdx.x * TILE;
     uint64_t c[UR];
     uint32_t vm = 0;                                  // bit r: c[r] holds a tuple (e < n)
@@ -1335,7 +1380,7 @@ template <typename E, uint32_t GL>
 __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
                                                      const uint32_t *__restrict__ run, uint32_t ntiles,
                                                      unsigned long long *__restrict__ flag, crdt_tuples out,
-                                                     uint64_t *__restrict__ out_count, uint32_t *__restrict__ err) {
+                                                     uint64_t *__restrict__ out_count, uint32_t *__restrict__ err, PlanGuard pg = {}) {
     constexpr uint32_t NE = kLtBytes / sizeof(E);  // 2^15 u32 / 2^14 u64 entries
     constexpr uint32_t NR = NE / LTB;
     static_assert(NR * LT_WAVES <= 64 * 8, "one wave scans the round counts");
@@ -1344,6 +1389,7 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
     __shared__ uint32_t s_cnt[NR * LT_WAVES];
     __shared__ unsigned long long s_sum[3];
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x, L = p.tl, ne = 1u << L;
     const uint32_t kb = p.b0 + p.br + p.bt;
@@ -1477,13 +1523,14 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
                                                    unsigned long long *__restrict__ flag, uint64_t *__restrict__ dst,
                                                    uint64_t *__restrict__ bounds, unsigned long long *__restrict__ cst,
                                                    uint32_t nch, uint32_t *__restrict__ err, int diag,
-                                                   bool place_batch, SubHist shist) {
+                                                   bool place_batch, SubHist shist, PlanGuard pg = {}) {
     __shared__ uint32_t s_run[kRunLds];
     __shared__ uint32_t s_h[OB_WAVES][kObSub];        // per-wave counts by sub-bucket, then the cursors (row 0)
     __shared__ uint64_t s_buf[kObBatch];              // (batched placement) one round's tuples by sub-bucket
     __shared__ uint32_t s_nb;
     __shared__ unsigned long long s_sum[3];
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t T = blockIdx.x;
     const uint32_t kb = p.b0 + p.br + p.bt;           // the key's bits start here
@@ -1836,7 +1883,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
                                                   uint32_t *__restrict__ fbw, int diag,
                                                   unsigned long long *__restrict__ st, crdt_tuples out,
                                                   uint64_t *__restrict__ out_count, uint32_t *__restrict__ err,
-                                                  uint32_t nch, int lbw) {
+                                                  uint32_t nch, int lbw, PlanGuard pg = {}) {
     constexpr uint32_t R = kOcKeys / OCB;             // keys per thread (round-major)
     __shared__ uint32_t tab[kOcKeys];
     __shared__ uint64_t stg[kOcCap];
@@ -1845,6 +1892,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     __shared__ uint32_t s_cnt[R * OC_WAVES], s_wsum[OC_WAVES], s_long[kOcLong], s_lrk[kOcLong], s_nlong, s_totk[K];
     __shared__ unsigned long long s_off;
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t kb = p.b0 + p.br + p.bt, tb = p.b0;
     bool fb = false;                                  // (uniform) a chunk of this workgroup fell back
@@ -2163,8 +2211,9 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
 __global__ __launch_bounds__(256) void k_or_emit(const uint64_t *__restrict__ tmp, const SortPlan *__restrict__ plan_,
                                                  const uint64_t *__restrict__ bounds, const uint32_t *__restrict__ cnt,
                                                  const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
-                                                 crdt_tuples out, uint64_t *__restrict__ out_count) {
+                                                 crdt_tuples out, uint64_t *__restrict__ out_count, PlanGuard pg = {}) {
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const uint32_t i = blockIdx.x, m = cnt[i];
     if (i == 0 && threadIdx.x == 0) *out_count = tot[0];
     const uint64_t *src = tmp + bounds[i];
@@ -2233,9 +2282,9 @@ __device__ __forceinline__ size_t run_start_from(const uint64_t *__restrict__ c,
 }
 
 __global__ void k_run_bounds(const uint64_t *__restrict__ c, size_t n, const SortPlan *__restrict__ plan_,
-                             size_t ntiles, uint64_t *__restrict__ bounds) {
+                             size_t ntiles, uint64_t *__restrict__ bounds, PlanGuard pg = {}) {
     const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (t > ntiles) return;
+    if (t > ntiles || !plan_guard_ok(*plan_, pg)) return;
     const size_t a = t * (size_t)RT;
     bounds[t] = run_start_from(c, n, a < n ? a : n, plan_->s0);
 }
@@ -2470,10 +2519,11 @@ __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, s
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       uint64_t *__restrict__ scratch, uint32_t *__restrict__ cnt,
-                                                      int diag) {
+                                                      int diag, PlanGuard pg = {}) {
     __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const uint32_t ks = p.s0, tb = p.b0;                 // group bits from ks; tag bits from b0
     const size_t t = blockIdx.x, start = bounds[t], end = bounds[t + 1];
     const size_t len = end > start ? end - start : 0;
@@ -2518,11 +2568,12 @@ __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict_
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
-                                                      crdt_tuples out, uint64_t *__restrict__ out_count, int diag) {
+                                                      crdt_tuples out, uint64_t *__restrict__ out_count, int diag, PlanGuard pg = {}) {
     __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
     __shared__ uint32_t s_c[RR * (RB / 64)];             // outputs per (round, wave), then their exclusive prefix
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
+    if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
     const uint32_t ks = p.s0, tb = p.b0, sk = p.b0 + p.br + p.bt;
     const size_t t = blockIdx.x, start = bounds[t], end = bounds[t + 1];
     if (t == 0 && threadIdx.x == 0) *out_count = tot[0];
@@ -2669,10 +2720,11 @@ static int or_run_dedup(crdt_ctx *ctx, uint64_t *c, size_t n, const SortPlan *pl
                         uint64_t *out_count) {
     const hipStream_t st = ctx->stream;
     const size_t nt = (n + RT - 1) / RT;
-    k_run_bounds<<<(unsigned)((nt + 1 + 255) / 256), 256, 0, st>>>(c, n, plan, nt, bounds);
-    k_or_rdd_count<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, scratch, cnt, g_rdd_diag);
+    k_run_bounds<<<(unsigned)((nt + 1 + 255) / 256), 256, 0, st>>>(c, n, plan, nt, bounds, cur_guard());
+    k_or_rdd_count<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, scratch, cnt, g_rdd_diag, cur_guard());
     k_sort_colscan<<<1, CSB, 0, st>>>(cnt, (uint32_t)nt, loc, tot);
-    k_or_rdd_apply<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, loc, tot, out, out_count, g_rdd_diag);
+    k_or_rdd_apply<<<(unsigned)nt, RB, 0, st>>>(c, n, plan, bounds, loc, tot, out, out_count, g_rdd_diag,
+                                                 cur_guard());
     return check_launch(ctx);
 }
 
@@ -2692,9 +2744,9 @@ static int dedup_words(crdt_ctx *ctx, const uint64_t *c, size_t n, const SortPla
                        uint32_t *loc, uint32_t *tot, const crdt_tuples &out, uint64_t *out_count) {
     const hipStream_t st = ctx->stream;
     const unsigned nt = (unsigned)((n + DT - 1) / DT);
-    k_dd_count<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, cnt);
+    k_dd_count<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, cnt, cur_guard());
     k_sort_colscan<<<1, CSB, 0, st>>>(cnt, nt, loc, tot);
-    k_dd_apply<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, loc, tot, out, out_count, g_rdd_diag);
+    k_dd_apply<MODE, WORDS><<<nt, DB, 0, st>>>(c, n, plan, loc, tot, out, out_count, g_rdd_diag, cur_guard());
     return check_launch(ctx);
 }
 
@@ -2775,6 +2827,13 @@ __global__ void k_put_plan(SortPlan h, SortPlan *plan, uint32_t *viol) {
     }
 }
 
+// Failpoint "fail.d2_plan": the device plan's shape changed behind the
+// host's back (more key bits: the bucket / chunk indices of the fault of
+// commit 01a0e59).
+__global__ void k_corrupt_plan(SortPlan *plan) {
+    if (threadIdx.x == 0) plan->bk += 7;
+}
+
 // A planned call's end: a tuple outside the plan (the upsweep's range check)
 // or an OR-Set chunk over its LDS limits leaves the output invalid -- raise
 // CRDT_DEV_PLAN and set the count to ~0 (no host synchronisation).
@@ -2823,15 +2882,20 @@ static unsigned group_tiles(hipStream_t s, const crdt_tuples &A, size_t n, const
     const unsigned tile = g_group_tile == 8192 ? 8192u : 4096u;
     const unsigned ntiles = (unsigned)((n + tile - 1) / tile);
     if (hist.rows && tile == 8192)
-        k_lww_up_tiled<1024, 8192, true><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, hist);
+        k_lww_up_tiled<1024, 8192, true><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, hist,
+                                                                     cur_guard());
     else if (hist.rows)
-        k_lww_up_tiled<512, ST, true><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, hist);
+        k_lww_up_tiled<512, ST, true><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, hist,
+                                                                     cur_guard());
     else if (tile == 8192)
-        k_lww_up_tiled<1024, 8192><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+        k_lww_up_tiled<1024, 8192><<<ntiles, 1024, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, SubHist{},
+                                                                     cur_guard());
     else if (g_up_threads == 512)
-        k_lww_up_tiled<512, ST><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+        k_lww_up_tiled<512, ST><<<ntiles, 512, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, SubHist{},
+                                                                     cur_guard());
     else
-        k_lww_up_tiled<SB, ST><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags);
+        k_lww_up_tiled<SB, ST><<<ntiles, SB, 0, s>>>(A, n, w.plan, ntiles, w.cnt, w.bufs, vw, w.flags, SubHist{},
+                                                                     cur_guard());
     return ntiles;
 }
 
@@ -2852,6 +2916,12 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
     const hipStream_t s = ctx->stream;
     const uint32_t key_only = MODE == DD_LWW ? 1u : g_or_key_sort ? (uint32_t)g_or_key_sort : 0u;
     *miss = false;
+    GuardScope guard(h, vw);                           // every pass below checks the device plan against h
+    if (vw && take_fail_d2_plan()) {                   // failpoint (diagnostic build): a plan of another shape
+        k_corrupt_plan<<<1, 64, 0, s>>>(w.plan);       //   in device memory -- the guards must catch it
+        int rc0 = check_launch(ctx);
+        if (rc0) return rc0;
+    }
     const void *hw = nullptr;                          // the end-of-call check words, on the host
     auto read_words = [&](const void *src, size_t bytes) -> int { return ctx_read_words(ctx, src, bytes, &hw); };
     auto finish = [&](const uint32_t *fb) -> int {     // after the last pass: the range check
@@ -2871,7 +2941,8 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
         if (MODE == DD_LWW && h.tw && vec && g_lww_gather) {   // tiles grouped by bucket, tables gather their runs
             const unsigned ntiles = group_tiles(s, A, n, w, vw);
 #define LWW_G(E, GLV) \
-    k_lww_table_g<E, GLV><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count, ctx->dev_status)
+    k_lww_table_g<E, GLV><<<256, LTB, 0, s>>>(w.bufs, w.plan, w.cnt, ntiles, w.flags, out, out_count, ctx->dev_status, \
+                                              cur_guard())
             if (h.tw == 4) {
                 if (g_group_tile == 8192) LWW_G(uint32_t, 4);
                 else LWW_G(uint32_t, 2);
@@ -2888,10 +2959,10 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             if (rc) return rc;
             if (h.tw == 4)
                 k_lww_table<uint32_t><<<256, LTB, 0, s>>>(sorted, w.plan, w.tot, w.flags, out, out_count,
-                                                          ctx->dev_status);
+                                                          ctx->dev_status, cur_guard());
             else
                 k_lww_table<uint64_t><<<256, LTB, 0, s>>>(sorted, w.plan, w.tot, w.flags, out, out_count,
-                                                          ctx->dev_status);
+                                                          ctx->dev_status, cur_guard());
             return finish(nullptr);
         }
         if (MODE == DD_OR && h.tw) {                    // the key's top 16 bits grouped, then chunks in LDS
@@ -2904,11 +2975,11 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
                 if (g_group_tile == 8192)
                     k_or_bucket<4><<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, gt, n, w.flags, w.bufs + n, w.cb,
                                                        lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
-                                                       g_or_place_batch != 0, hist);
+                                                       g_or_place_batch != 0, hist, cur_guard());
                 else
                     k_or_bucket<2><<<256, OBB, 0, s>>>(w.bufs, w.plan, w.cnt, gt, n, w.flags, w.bufs + n, w.cb,
                                                        lb ? w.cst : nullptr, nch, ctx->dev_status, g_rdd_diag,
-                                                       g_or_place_batch != 0, hist);
+                                                       g_or_place_batch != 0, hist, cur_guard());
                 sorted = w.bufs + n;
             } else {                                    // two radix passes on the top 16 bits
                 rc = sort_words<1>(ctx, A, n, out, w.plan, 2, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec,
@@ -2925,7 +2996,7 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             const unsigned grid = nch / (unsigned)kpair;
 #define OR_CHUNK(LBV, NAR, KV)                                                                                 \
     k_or_chunk<LBV, NAR, KV><<<grid, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, LBV ? w.cst : nullptr, \
-                                                   out, out_count, ctx->dev_status, nch, g_or_lb_words)
+                                                   out, out_count, ctx->dev_status, nch, g_or_lb_words, cur_guard())
             if (lb) {
                 if (narrow) {
                     if (kpair == 2) OR_CHUNK(true, true, 2);
@@ -2944,7 +3015,7 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
                 }
 #undef OR_CHUNK
                 k_sort_colscan<<<1, CSB, 0, s>>>(w.cc, nch, w.cl, w.ct);
-                k_or_emit<<<nch, 256, 0, s>>>(tmp, w.plan, w.cb, w.cc, w.cl, w.ct, out, out_count);
+                k_or_emit<<<nch, 256, 0, s>>>(tmp, w.plan, w.cb, w.cc, w.cl, w.ct, out, out_count, cur_guard());
             }
             rc = check_launch(ctx);
             if (rc) return rc;
@@ -2966,6 +3037,7 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             rc = read_plan(ctx, w.plan, &h);
             if (rc) return rc;
             vw = nullptr;
+            guard.set(h, nullptr);                      // (the exact plan, read back: nothing to check)
         }
         rc = sort_words<1>(ctx, A, n, out, w.plan, h.P, w.bufs, w.cnt, w.loc, w.tot, false, &sorted, vec, nullptr, vw);
         if (!rc && MODE == DD_OR && h.s0)                 // key-only sort: key runs ordered in the dedup

@@ -14,6 +14,7 @@ HIP graph can capture the whole merge (VERDICT r04 "Next round" item 3).
 import numpy as np
 import pytest
 import torch
+from knobs import set_knob
 
 from crdt_amd import _lib, synth
 from crdt_amd.engine import TupleSet, as_u64
@@ -108,6 +109,48 @@ def test_planned_eager_and_graph_replays(eng, lww, shape):
     for g_, e in zip(got, _expect(lww, bad, nb_)):
         np.testing.assert_array_equal(g_, e)
     del g
+
+
+@pytest.mark.diag
+@pytest.mark.parametrize("lww", [True, False])
+def test_device_plan_changed_behind_the_launch(eng, lww):
+    """VERDICT r05 item 6 (the fault of commit 01a0e59): the device plan's
+    shape differs from the one the passes were launched for (failpoint
+    fail.d2_plan: more key bits in device memory).  Every pass compares the
+    device plan with its launch shape first and stores nothing: the planned
+    call raises CRDT_DEV_PLAN with count 2^64 - 1, the unplanned call
+    (sampled plan, then the context's cached plan) redoes from the exact plan
+    == the oracle, and the next planned call == the oracle."""
+    ua, ub = _dense(17, 400_000, 300_000)
+    A = TupleSet.from_numpy(*ua, eng.device)
+    B = TupleSet.from_numpy(*ub, eng.device)
+    out = TupleSet.empty(len(A) + len(B), eng.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=eng.device)
+    exp = _expect(lww, ua, ub)
+    plan = eng.set_merge_plan(lww, A, B, widen=True)
+    assert eng.device_status() == 0
+    try:
+        set_knob(b"fail.d2_plan", 1)
+        eng.merge_unsorted_planned(lww, plan, A, B, out, cnt)
+        torch.cuda.synchronize()
+        assert int(as_u64(cnt)[0]) == 2**64 - 1
+        assert eng.device_status(clear=True) & DEV_PLAN
+        set_knob(b"sort.sample_min", 0)                  # the sampled / cached dense-key forms at this size
+        fn = eng.lww_merge_unsorted if lww else eng.orset_merge_unsorted
+        for _ in range(2):                               # a fresh sampled plan, then the context's cached one
+            set_knob(b"fail.d2_plan", 1)
+            got = fn(A, B).to_numpy()
+            assert len(got[0]) == len(exp[0])
+            for g, e in zip(got, exp):
+                np.testing.assert_array_equal(g, e)
+            assert eng.device_status() == 0              # (the redo is silent)
+    finally:
+        set_knob(b"fail.d2_plan", 0)
+        set_knob(b"sort.sample_min", 1 << 20)
+    eng.merge_unsorted_planned(lww, plan, A, B, out, cnt)
+    torch.cuda.synchronize()
+    _same(out, cnt, exp)
+    assert eng.device_status() == 0
 
 
 def test_planned_refuses_another_shape(eng):
