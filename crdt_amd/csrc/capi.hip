@@ -179,17 +179,14 @@ __global__ __launch_bounds__(256) void k_read_words(const uint32_t *__restrict__
     if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void **host) {
+int ctx_read_begin(crdt_ctx *ctx, const void *dev_src, size_t bytes) {
     if (bytes > kCioBytes || (bytes & 3)) return CRDT_E_INVAL;
     if (!g_read_poll) {
         int rc = hio_reserve(ctx, bytes ? bytes : 4);
         if (rc) return rc;
         hipError_t e = bytes ? hipMemcpyAsync(ctx->hio, dev_src, bytes, hipMemcpyDeviceToHost, ctx->stream)
                              : hipSuccess;
-        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-        if (e != hipSuccess) return hip_fail(ctx, e);
-        *host = ctx->hio;
-        return CRDT_OK;
+        return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e);
     }
     if (!ctx->cio) {                                  // words | completion word (64 B after them)
         void *h = nullptr, *d = nullptr;
@@ -208,8 +205,17 @@ int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void 
     k_read_words<<<1, 256, 0, ctx->stream>>>((const uint32_t *)dev_src, (uint32_t)(bytes / 4),
                                               (uint32_t *)ctx->cio_d, (uint64_t *)((char *)ctx->cio_d + kCioBytes),
                                               seq);
-    int rc = check_launch(ctx);
-    if (rc) return rc;
+    return check_launch(ctx);
+}
+
+int ctx_read_end(crdt_ctx *ctx, const void **host) {
+    if (!g_read_poll) {
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+        *host = ctx->hio;
+        return CRDT_OK;
+    }
+    const uint64_t seq = ctx->cio_seq;
     const volatile uint64_t *f = (const volatile uint64_t *)((char *)ctx->cio + kCioBytes);
     while (*f != seq) {
         const hipError_t q = hipStreamQuery(ctx->stream);
@@ -220,6 +226,11 @@ int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void 
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     *host = ctx->cio;
     return CRDT_OK;
+}
+
+int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void **host) {
+    int rc = ctx_read_begin(ctx, dev_src, bytes);
+    return rc ? rc : ctx_read_end(ctx, host);
 }
 }  // namespace crdt
 
@@ -275,11 +286,14 @@ extern "C" int crdt_ctx_device_status(crdt_ctx *ctx, uint32_t *flags, int clear)
     int rc = bind(ctx);
     if (rc) return rc;
     if (!flags) return CRDT_E_INVAL;
-    uint32_t v = 0;
-    hipError_t e = hipMemcpyAsync(&v, ctx->dev_status, sizeof(v), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e == hipSuccess && clear && v) e = hipMemsetAsync(ctx->dev_status, 0, sizeof(v), ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
+    const void *hw = nullptr;                         // (stream-ordered: every earlier pass has finished)
+    rc = ctx_read_words(ctx, ctx->dev_status, sizeof(uint32_t), &hw);
+    if (rc) return rc;
+    const uint32_t v = *(const uint32_t *)hw;
+    if (clear && v) {
+        hipError_t e = hipMemsetAsync(ctx->dev_status, 0, sizeof(v), ctx->stream);
+        if (e != hipSuccess) return hip_fail(ctx, e);
+    }
     *flags = v;
     return CRDT_OK;
 }

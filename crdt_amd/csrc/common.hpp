@@ -174,6 +174,10 @@ inline int hio_reserve(crdt_ctx *ctx, size_t bytes) {
 // (ctx.read_poll = 0: hipMemcpyAsync + hipStreamSynchronize into ctx->hio.)
 constexpr size_t kCioBytes = 4096;
 int ctx_read_words(crdt_ctx *ctx, const void *dev_src, size_t bytes, const void **host);
+// The same in two halves, so several contexts' reads can be in flight at once
+// (one outstanding read per context; end returns its words).
+int ctx_read_begin(crdt_ctx *ctx, const void *dev_src, size_t bytes);
+int ctx_read_end(crdt_ctx *ctx, const void **host);
 
 // Make the context's device current for this host thread.
 inline int bind(crdt_ctx *ctx) {

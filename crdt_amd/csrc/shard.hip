@@ -42,6 +42,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <new>
 #include <vector>
 
@@ -418,14 +420,28 @@ int sync_all(crdt_comm *c) {
     return CRDT_OK;
 }
 
+// Every member's device status word (cleared when raised): all members'
+// polled reads in flight at once, then collected -- one wait for the slowest
+// member instead of one synchronising copy per member.
 int check_devices(crdt_comm *c) {
     for (auto &mb : c->m) {
-        uint32_t flags = 0;
-        int rc = crdt_ctx_device_status(mb.ctx, &flags, 1);
+        int rc = bind(mb.ctx);
+        if (!rc) rc = ctx_read_begin(mb.ctx, mb.ctx->dev_status, sizeof(uint32_t));
         if (rc) return rc;
-        if (flags) return CRDT_E_DEVICE;
     }
-    return CRDT_OK;
+    bool raised = false;
+    for (auto &mb : c->m) {
+        int rc = bind(mb.ctx);
+        const void *hw = nullptr;
+        if (!rc) rc = ctx_read_end(mb.ctx, &hw);
+        if (rc) return rc;
+        if (*(const uint32_t *)hw) {
+            raised = true;
+            hipError_t e = hipMemsetAsync(mb.ctx->dev_status, 0, sizeof(uint32_t), mb.ctx->stream);
+            if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        }
+    }
+    return raised ? CRDT_E_DEVICE : CRDT_OK;
 }
 
 // Copy n words of member 0's device buffer to the host (synchronises member 0).
@@ -433,6 +449,12 @@ int read_member0(crdt_comm *c, const uint64_t *src, uint64_t *dst, size_t n) {
     auto &mb = c->m[0];
     int rc = bind(mb.ctx);
     if (rc || n == 0) return rc;
+    if (n * 8 <= kCioBytes) {                          // small: the polled pinned read (no pageable copy)
+        const void *hw = nullptr;
+        rc = ctx_read_words(mb.ctx, src, n * 8, &hw);
+        if (!rc) memcpy(dst, hw, n * 8);
+        return rc;
+    }
     hipError_t e = hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToHost, mb.ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
     return e == hipSuccess ? CRDT_OK : hip_fail(mb.ctx, e);
@@ -987,26 +1009,45 @@ namespace {
 // at which the cumulative weight reaches q / R of the total.  Rank r owns
 // keys [spl[r], spl[r+1]); crdt_amd/shard.py weighted_splitters is the same rule.
 std::vector<uint64_t> weighted_splitters(const uint64_t *blocks, size_t R, size_t S) {
-    std::vector<std::pair<uint64_t, uint64_t>> e;       // (key, weight)
-    e.reserve(2 * S * R);
+    // the samples of every non-empty side, walked in key order by a k-way
+    // merge of the (sorted) sample lists: each crossing of q / R of the total
+    // weight names splitter q.  Among equal keys the walk order does not
+    // matter: a crossing inside a run of equal keys names that key.
+    struct List {
+        const uint64_t *k;
+        uint64_t w;
+        size_t i;
+    };
+    std::vector<List> ls;
+    unsigned __int128 W = 0;
     for (size_t p = 0; p < R; ++p) {
         const uint64_t *b = blocks + p * (2 + 2 * S);
         for (int side = 0; side < 2; ++side)
-            if (b[side])
-                for (size_t i = 0; i < S; ++i) e.emplace_back(b[2 + side * S + i], b[side]);
+            if (b[side] && S) {
+                ls.push_back(List{b + 2 + side * S, b[side], 0});
+                W += (unsigned __int128)S * b[side];
+            }
     }
-    std::sort(e.begin(), e.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
-    unsigned __int128 W = 0;
-    for (auto &x : e) W += x.second;
     std::vector<uint64_t> spl(R + 1, 0);
     spl[R] = kKeyEnd;
+    if (W == 0) return spl;
+    auto later = [&](int x, int y) { return ls[x].k[ls[x].i] > ls[y].k[ls[y].i]; };
+    std::vector<int> h(ls.size());
+    for (size_t x = 0; x < ls.size(); ++x) h[x] = (int)x;
+    std::make_heap(h.begin(), h.end(), later);
     unsigned __int128 cum = 0;
-    size_t k = 0;
-    for (size_t q = 1; q < R; ++q) {
-        const unsigned __int128 target = (unsigned __int128)q * W;
-        while (k < e.size() && (cum + e[k].second) * R < target) cum += e[k++].second;
-        spl[q] = W == 0 ? 0 : (k < e.size() ? e[k].first : e.back().first);
+    uint64_t last = 0;
+    size_t q = 1;
+    while (q < R && !h.empty()) {
+        std::pop_heap(h.begin(), h.end(), later);
+        List &l = ls[h.back()];
+        last = l.k[l.i];
+        cum += l.w;
+        while (q < R && cum * R >= (unsigned __int128)q * W) spl[q++] = last;
+        if (++l.i < S) std::push_heap(h.begin(), h.end(), later);
+        else h.pop_back();
     }
+    for (; q < R; ++q) spl[q] = last;                  // (not reached: the walk ends at cum = W)
     return spl;
 }
 
@@ -1036,6 +1077,65 @@ __global__ void k_cut_counts(const uint64_t *__restrict__ lb, unsigned R, size_t
     out[q] = a1 - a0;
     out[R + q] = b1 - b0;
 }
+
+// A member's row of the count matrix in ONE launch (round 6): the R - 1
+// inner splitters by value (no host-to-device copy), one wave per 64-ary
+// lower-bound search of a side's sorted keys, then the cuts' differences.
+constexpr unsigned kCutMaxR = 64;
+struct Splitters {
+    uint64_t v[kCutMaxR - 1];
+};
+__global__ __launch_bounds__(1024) void k_member_cuts(const uint64_t *__restrict__ ka, size_t na,
+                                                      const uint64_t *__restrict__ kb, size_t nb, Splitters sp,
+                                                      unsigned R, uint64_t *__restrict__ row) {
+    __shared__ uint64_t s_lb[2][kCutMaxR];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    for (unsigned j = (unsigned)wv; j < 2 * (R - 1); j += (unsigned)nwv) {
+        const int side = j >= R - 1;
+        const unsigned q = side ? j - (R - 1) : j;
+        const uint64_t *k = side ? kb : ka;
+        const uint64_t pr = sp.v[q];
+        size_t lo = 0, hi = side ? nb : na;           // first index with k >= pr lies in [lo, hi]
+        while (lo < hi) {
+            const size_t span = hi - lo;
+            const size_t x = lo + span * (size_t)lane / 64;
+            const uint64_t ge = __ballot(k[x] >= pr);
+            if (ge == 0) {
+                lo += span * 63 / 64 + 1;
+            } else {
+                const int t = __ffsll((long long)ge) - 1;
+                hi = lo + span * (size_t)t / 64;
+                if (t > 0) lo += span * (size_t)(t - 1) / 64 + 1;
+            }
+        }
+        if (lane == 0) s_lb[side][q] = lo;
+    }
+    __syncthreads();
+    for (unsigned q = threadIdx.x; q < R; q += blockDim.x) {
+        const uint64_t a0 = q ? s_lb[0][q - 1] : 0, a1 = q + 1 < R ? s_lb[0][q] : na;
+        const uint64_t b0 = q ? s_lb[1][q - 1] : 0, b1 = q + 1 < R ? s_lb[1][q] : nb;
+        row[q] = a1 - a0;
+        row[R + q] = b1 - b0;
+    }
+}
+
+// Host-side phase timing of the distributed set merge (diagnostic build,
+// "shard.host_timing" = 1): microseconds since the call started, per phase,
+// to stderr -- where the host waits or works while the GPU idles.
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    char buf[512];
+    int len = 0;
+    void mark(const char *what) {
+        if (!g_shard_host_timing) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        len += snprintf(buf + len, sizeof buf - (size_t)len, " %s %.0f", what, us);
+        if (len >= (int)sizeof buf) len = (int)sizeof buf - 1;
+    }
+    ~PhaseClock() {
+        if (g_shard_host_timing && len) fprintf(stderr, "[shard] us:%s\n", buf);
+    }
+};
 
 int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const size_t *na, const crdt_tuples *b,
                           const size_t *nb, const crdt_tuples *out, size_t cap, size_t *n_out,
@@ -1087,6 +1187,7 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
         if (rc) return rc;
         carve_ctrl(c->m[i], &ct[i]);
     }
+    PhaseClock pc;
     // 1. samples + sizes, all-gathered; every rank derives the same splitters (read-back 1)
     std::vector<const void *> snd(M);
     std::vector<void *> rcv(M);
@@ -1104,36 +1205,48 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
     }
     int rc = c->x->allgather(c, snd.data(), rcv.data(), blk * 8);
     if (rc) return rc;
+    pc.mark("ag1");
     std::vector<uint64_t> h_smp(R * blk);
     rc = read_member0(c, ct[0].smp, h_smp.data(), R * blk);
     if (rc) return rc;
+    pc.mark("rb1");
     const std::vector<uint64_t> spl = weighted_splitters(h_smp.data(), R, S);
+    pc.mark("spl");
     // 2. each member's cuts (device lower_bound of the inner splitters) -> its
     //    row of the count matrix on the device; the matrix all-gathered (read-back 2)
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
         rc = bind(mb.ctx);
         if (rc) return rc;
-        if (R > 1) {
+        uint64_t *row = ct[i].cnt + (c->rank0 + i) * 2 * R;
+        if (R <= kCutMaxR) {                             // splitters by value, one launch
+            Splitters sp{};
+            for (size_t q = 1; q < R; ++q) sp.v[q - 1] = spl[q];
+            const unsigned th = (unsigned)std::min<size_t>(1024, std::max<size_t>(64, 64 * 2 * (R - 1)));
+            k_member_cuts<<<1, th, 0, mb.ctx->stream>>>(a[i].key, na[i], b[i].key, nb[i], sp, (unsigned)R, row);
+        } else {
             hipError_t e = hipMemcpyAsync(ct[i].prb, spl.data() + 1, (R - 1) * 8, hipMemcpyHostToDevice,
                                           mb.ctx->stream);
             if (e != hipSuccess) return hip_fail(mb.ctx, e);
             rc = crdt_u64_lower_bound(mb.ctx, a[i].key, na[i], ct[i].prb, R - 1, ct[i].lb);
             if (!rc) rc = crdt_u64_lower_bound(mb.ctx, b[i].key, nb[i], ct[i].prb, R - 1, ct[i].lb + (R - 1));
             if (rc) return rc;
+            k_cut_counts<<<(unsigned)((R + 255) / 256), 256, 0, mb.ctx->stream>>>(ct[i].lb, (unsigned)R, na[i], nb[i],
+                                                                                 row);
         }
-        uint64_t *row = ct[i].cnt + (c->rank0 + i) * 2 * R;
-        k_cut_counts<<<(unsigned)((R + 255) / 256), 256, 0, mb.ctx->stream>>>(ct[i].lb, (unsigned)R, na[i], nb[i], row);
         rc = check_launch(mb.ctx);
         if (rc) return rc;
         snd[i] = row;
         rcv[i] = ct[i].cnt;
     }
+    pc.mark("cuts");
     rc = c->x->allgather(c, snd.data(), rcv.data(), 2 * R * 8);
     if (rc) return rc;
+    pc.mark("ag2");
     std::vector<uint64_t> mat(2 * R * R);               // row p = rank p's [A counts | B counts] by destination
     rc = read_member0(c, ct[0].cnt, mat.data(), mat.size());
     if (rc) return rc;
+    pc.mark("rb2");
     std::vector<size_t> tot_a(M, 0), tot_b(M, 0);
     for (size_t i = 0; i < M; ++i) {
         const size_t g = (size_t)c->rank0 + i;
@@ -1163,6 +1276,7 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
             t->tomb = w.take<uint8_t>(n + 1);
         }
     }
+    pc.mark("arenas");
     // 4. the exchange: every field of both sides to its key-range owner, ONE
     //    point-to-point group; arena 0 receives A's runs then B's, rank order
     {
@@ -1189,6 +1303,7 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
         rc = c->x->p2p(c, ops);
         if (rc) return rc;
     }
+    pc.mark("xchg");
     // 5. per member: each side's R runs merged stably in rank order (lower rank
     //    left) by a tree of crdt_tuples_merge levels -- every length known on
     //    the host, so no read-back -- then ONE set merge of the two sides.
@@ -1235,24 +1350,34 @@ int shard_set_merge_local(crdt_comm *c, bool lww, const crdt_tuples *a, const si
         rc = set_merge(mb.ctx, A, tot_a[i], B, tot_b[i], fin[i], count);
         if (rc) return rc;
     }
+    pc.mark("merges");
     if (n_dev) return CRDT_OK;                           // enqueued; counts on the device
     // 6. the whole merged state on every member, or each member's own range
     if (gather) {
         size_t tot = 0;
         rc = allgather_v_head(c, fin.data(), out, cap, &tot);
         if (rc) return rc;
+        pc.mark("gather");
         for (size_t i = 0; i < M; ++i) n_out[i] = tot;
-        return check_devices(c);
+        rc = check_devices(c);
+        pc.mark("done");
+        return rc;
+    }
+    for (size_t i = 0; i < M; ++i) {                   // every member's count read in flight at once
+        auto &mb = c->m[i];
+        rc = bind(mb.ctx);
+        if (!rc) rc = ctx_read_begin(mb.ctx, mb.scratch, 8);
+        if (rc) return rc;
     }
     for (size_t i = 0; i < M; ++i) {
         auto &mb = c->m[i];
         rc = bind(mb.ctx);
+        const void *hw = nullptr;
+        if (!rc) rc = ctx_read_end(mb.ctx, &hw);
         if (rc) return rc;
-        uint64_t h = 0;
-        hipError_t e = hipMemcpyAsync(&h, mb.scratch, 8, hipMemcpyDeviceToHost, mb.ctx->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(mb.ctx->stream);
-        if (e != hipSuccess) return hip_fail(mb.ctx, e);
+        const uint64_t h = *(const uint64_t *)hw;
         n_out[i] = h;
+        hipError_t e = hipSuccess;
         if (direct[i] || !h) continue;
         if (h > cap) return CRDT_E_RANGE;
         e = hipMemcpyAsync(out[i].key, fin[i].key, h * 8, hipMemcpyDeviceToDevice, mb.ctx->stream);
