@@ -218,7 +218,8 @@ def test_decode_short_string_order_and_interning(eng):
 def test_decode_large_bodies_both_forms_agree(eng, decode_form):
     """Bodies past one chunk of the one-pass kernel (8192 items per round of
     its scans; 20k entries / ~60k pairs) and a body at an odd byte offset:
-    the same ids, ranges and flags from both forms, equal to the host ingest."""
+    the same ids, ranges and flags from every form (multi-pass, one-pass,
+    coalesced one-pass at 4 and 8 items per thread)."""
     from crdt_amd import _lib
     rng = np.random.default_rng(11)
     bodies = []
@@ -230,8 +231,11 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
         bodies.append(_serve(d))
     bodies.insert(1, _raw_body([(1, [(b"a", b"1")])]) + b"")     # shifts the next body off 8-byte alignment
     out = []
-    for form in (0, 2, 3):
+    # (3, 8): the coalesced one-pass form with 8 items per thread per chunk
+    # (codec.big_r = 8, k_dec_big8)
+    for form, big_r in ((0, 4), (2, 4), (3, 4), (3, 8)):
         set_knob(b"codec.small", form)
+        set_knob(b"codec.big_r", big_r)
         keys, vals = codec.StrTab(eng), codec.StrTab(eng)
         dec, st, kk, kv = _decode(eng, bodies, keys, vals)
         h = {x: dec[x].cpu().numpy() for x in ("r_off", "r_ts", "r_kv")}
@@ -241,6 +245,7 @@ def test_decode_large_bodies_both_forms_agree(eng, decode_form):
                  for q in range(h["r_kv"][h["r_off"][bi]], h["r_kv"][h["r_off"][bi + 1]])]
         out.append((st.tolist(), h, pairs, sorted(ks), sorted(vs)))
     set_knob(b"codec.small", decode_form)
+    set_knob(b"codec.big_r", 4)
     a = out[0]
     assert a[0] == [0, 0, 0, 0]
     for b in out[1:]:
