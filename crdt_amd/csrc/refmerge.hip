@@ -577,7 +577,6 @@ __global__ __launch_bounds__(NT) void k_rm_count(crdt_refmerge_in in, const Tile
 }
 
 enum { RM_FOLD_NONE = 0, RM_FOLD_FULL = 1, RM_FOLD_DELTA = 2 };
-constexpr int kDiagLoadAll = 256;          // diag bit: load every in-tile entry (refmerge.load_all A/B)
 
 // Pass 2, one workgroup per tile, in merge order: wave w's lanes take merge
 // items k = 64 (w + NWV i) + lane (i < FI), so each load instruction covers 64
@@ -746,7 +745,7 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
     for (int f = 0; f < FI; ++f) {                       // every entry load issued before the first use
         // (only emitted entries are written or folded: an R entry whose ts L
         // already holds loads nothing)
-        const bool in_tile = it_in(f) && ((diag & kDiagLoadAll) || it_em(f)), il = it_l(f);
+        const bool in_tile = it_in(f) && it_em(f), il = it_l(f);
         const uint64_t gi = it_gi(f);
         const uint64_t *kv = (il ? in.l_kv : in.r_kv) + gi;
         e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
@@ -1364,7 +1363,6 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     }
     // the tile pass: slice write and (with slots) the replay fold
     const unsigned tg = (unsigned)tmax;
-    const int lda = g_rm_ld_all ? kDiagLoadAll : 0;
     // (one_pair: the caller's population keeps one pair per entry in entry
     // order -- refmerge_batch_pull_one_pair; the tile pass then computes
     // each entry's pair index instead of loading its kv range)
@@ -1372,7 +1370,7 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
                                  one_pair && g_rm_affine ? 1u : 0u}
                          : KvOut{};
     if (delta && ns) {                                            // incremental replay: fold only the inserted R
-        k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, lda, ic, out, *delta, cand, cand_n,
+        k_rm_tile<RM_FOLD_DELTA><<<tg, FB, 0, s>>>(in, desc, bits, r_dk, okv, acc, 0, ic, out, *delta, cand, cand_n,
                                                    ovf, ctx->dev_status);
         rc = check_launch(ctx);
         if (rc) return rc;
@@ -1381,11 +1379,11 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
         if (rc) return rc;
         return rp_delta_fold(ctx, in, r_dk, okv, *delta, &out, true);
     }
-    // workgroups per tile (refmerge.tile_parts): 1/P of the tile's items each
+    // one workgroup per tile (1/P of a tile per workgroup measured slower: DESIGN.md §5.4)
 #define RM_TILE(F, P, KV, DIAG)                                                                                \
     if (KV && one_pair) {                                   /* every tile a one-pair tile */                   \
         k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
-    } else if (KV && (g_rm_kvx || tg <= (unsigned)ctx->num_cus)) {                                             \
+    } else if (KV && tg <= (unsigned)ctx->num_cus) {                                                           \
         k_rm_tile_kvx<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
     } else if (KV) {                                                                                           \
         k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
@@ -1393,18 +1391,13 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     } else                                                                                                       \
         k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out,            \
                                                   crdt_replay_state{}, nullptr, nullptr, nullptr, ctx->dev_status)
-    // (the kv output needs the whole tile in one workgroup: refmerge.tile_parts ignored)
     if (!ns || g_rm_diag == 1) {                                  // (diag 1: timing without the replay fold)
-        if (kv) RM_TILE(RM_FOLD_NONE, 1, true, lda);
-        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_NONE, 2, false, lda);
-        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_NONE, 4, false, lda);
-        else RM_TILE(RM_FOLD_NONE, 1, false, lda);
+        if (kv) RM_TILE(RM_FOLD_NONE, 1, true, 0);
+        else RM_TILE(RM_FOLD_NONE, 1, false, 0);
         if (!ns || delta) return check_launch(ctx);
     } else {
-        if (kv) RM_TILE(RM_FOLD_FULL, 1, true, g_rm_diag | lda);
-        else if (g_rm_parts == 2) RM_TILE(RM_FOLD_FULL, 2, false, g_rm_diag | lda);
-        else if (g_rm_parts == 4) RM_TILE(RM_FOLD_FULL, 4, false, g_rm_diag | lda);
-        else RM_TILE(RM_FOLD_FULL, 1, false, g_rm_diag | lda);
+        if (kv) RM_TILE(RM_FOLD_FULL, 1, true, g_rm_diag);
+        else RM_TILE(RM_FOLD_FULL, 1, false, g_rm_diag);
     }
 #undef RM_TILE
     if (ns && !acc_out) k_slot_final<<<grid_for(ns, 256, cap), 256, 0, s>>>(out, acc, okv, (uint32_t)ns);

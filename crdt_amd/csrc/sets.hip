@@ -22,14 +22,12 @@
 //   write  : per part of a tile, the runs staged in LDS by LDS-DMA, every
 //            index a prefix popcount of the bitmaps, outputs stored at their
 //            rank.
-// The tiles run in CHUNKS (sets.chunk_tiles): chunk c's count + scan, then
-// its write pass, so the keys the count pass read are still in the 256 MiB
-// Infinity Cache when the write pass reads them again (MI355X_MICROARCH.md
-// "Infinity Cache": a line stays resident while fewer than ~256 MiB move
-// between its two uses).  With two streams (sets.streams = 2) chunk c+1's
-// latency-bound count pass runs beside chunk c's write pass; the count pass
-// of chunk c+2 waits for write c, so at most one chunk's keys are in
-// flight ahead of their re-read.
+// The tiles run in chunks of at most 16384 (one scan workgroup each): chunk
+// c's count, scan and write pass in turn on the context's stream.  (Smaller
+// chunks, so that the keys the count pass read were still in the Infinity
+// Cache for the write pass, and a second stream running chunk c+1's count
+// beside chunk c's write, measured slower: DESIGN.md §5.4.1.  So did one
+// pass with a decoupled look-back, §5.4.4.)
 #include <algorithm>
 #include <atomic>
 
@@ -456,239 +454,6 @@ __global__ __launch_bounds__(WT) void k_lww_write(crdt_tuples A, crdt_tuples B, 
     }
 }
 
-// ---------------------------------------------------------------- LWW, one pass (round 6)
-// k_lww_fused: the count pass, the scan and the write pass in ONE launch,
-// one workgroup per TT-item tile.  The tile's A and B
-// runs -- every field, A from two elements before the run, B from one -- are
-// staged in LDS by LDS-DMA once; the key merge runs on the staged keys (no
-// second read of the keys from HBM), its bitmaps stay in LDS, the tile's
-// emit count is published for a decoupled look-back (lookback_sum: one wave,
-// 64 predecessors per poll) and the winners are stored at their ranks from
-// the same staging.  HBM traffic = the algorithmic bytes (+ the split's
-// searches); the look-back round trips of one workgroup overlap the staging
-// and merges of the other workgroups on its CU.
-template <int TT, int NT>
-__global__ __launch_bounds__(NT) void k_lww_fused(crdt_tuples A, crdt_tuples B, size_t na, size_t nb,
-                                                  const uint64_t *__restrict__ split,
-                                                  unsigned long long *__restrict__ st, crdt_tuples out,
-                                                  uint64_t *__restrict__ out_count, uint32_t *__restrict__ err,
-                                                  int diag) {
-    constexpr int NWV = NT / 64, NW = TT / 64, NI = TT / NT, LPW = 64 / NI, CAP = TT + 3, FI = NW / NWV;
-    static_assert(NW <= 64 && NI * NT == TT && LPW * NI == 64 && FI * NWV == NW, "shape");
-    __shared__ alignas(16) uint64_t s_key[CAP + 8];
-    __shared__ alignas(16) uint64_t s_ts[CAP + 8];
-    __shared__ alignas(16) uint32_t s_rep[CAP + 16];
-    __shared__ alignas(16) uint8_t s_tomb[CAP + 64];
-    __shared__ uint64_t s_wa[NW], s_we[NW];
-    __shared__ uint32_t s_cw[NWV];
-    __shared__ uint64_t s_off;
-    const uint64_t t = blockIdx.x;
-    const size_t n = na + nb;
-    const LwwTile b = lww_tile<TT>(split, t, n);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const size_t ra = b.i0, rb = b.j0;
-    const uint32_t ca = b.na, cb = b.nb, na2 = ca + 2;   // staged A: ra-2 .. ra+ca-1 (slots 0 .. ca+1)
-    // slot x of field f sits at LDS element x + (x < na2 ? oa[f] : ob[f])
-    int oa_k, ob_k, oa_t, ob_t, oa_r, ob_r, oa_m, ob_m;
-    {
-        const size_t ga = ra >= 2 ? ra - 2 : 0, gb = rb >= 1 ? rb - 1 : 0;   // first staged element of each side
-        const uint32_t ka = (uint32_t)(ra + ca - ga), kb = (uint32_t)(rb + cb - gb);
-        const int sa = (int)(ga - (ra - 2)), sb = (int)(gb - (rb - 1)) + (int)na2;
-        uint32_t at = 0;
-        oa_k = dma_run<uint64_t, NWV>(A.key, ga, ka, s_key, &at, wv, lane) - sa;
-        ob_k = dma_run<uint64_t, NWV>(B.key, gb, kb, s_key, &at, wv, lane) - sb;
-        at = 0;
-        oa_t = dma_run<uint64_t, NWV>(A.ts, ga, ka, s_ts, &at, wv, lane) - sa;
-        ob_t = dma_run<uint64_t, NWV>(B.ts, gb, kb, s_ts, &at, wv, lane) - sb;
-        at = 0;
-        oa_r = dma_run<uint32_t, NWV>(A.rep, ga, ka, s_rep, &at, wv, lane) - sa;
-        ob_r = dma_run<uint32_t, NWV>(B.rep, gb, kb, s_rep, &at, wv, lane) - sb;
-        at = 0;
-        oa_m = dma_run<uint8_t, NWV>(A.tomb, ga, ka, s_tomb, &at, wv, lane) - sa;
-        ob_m = dma_run<uint8_t, NWV>(B.tomb, gb, kb, s_tomb, &at, wv, lane) - sb;
-    }
-    // the keys after the tile: the next merged key past its last item
-    const bool ha_next = b.i1 < na, hb_next = b.j1 < nb;
-    const uint64_t ka_next = ha_next ? A.key[b.i1] : 0, kb_next = hb_next ? B.key[b.j1] : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
-    __syncthreads();
-    // ---- the key merge (A first on an equal key): bitmaps isa / emit
-    const uint64_t *SA = s_key + 2 + oa_k, *SB = s_key + na2 + 1 + ob_k;
-    const uint32_t k0 = threadIdx.x * NI < b.n ? threadIdx.x * NI : b.n;
-    const uint32_t k1 = k0 + NI < b.n ? k0 + NI : b.n;
-    uint32_t isa = 0, emit = 0;
-    if (k0 < k1) {
-        uint32_t lo = k0 > b.nb ? k0 - b.nb : 0, hi = k0 < b.na ? k0 : b.na;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (SA[mid] <= SB[k0 - 1 - mid]) lo = mid + 1;
-            else hi = mid;
-        }
-        uint32_t ia = lo, ib = k0 - lo;
-        uint64_t ha = ia < b.na ? SA[ia] : 0, hb = ib < b.nb ? SB[ib] : 0;
-        uint64_t prev = 0;
-        for (uint32_t i = 0; i < k1 - k0; ++i) {
-            const bool take_a = ia < b.na && (ib >= b.nb || ha <= hb);
-            const uint64_t key = take_a ? ha : hb;
-            if (i > 0 && key != prev) emit |= 1u << (i - 1);
-            prev = key;
-            if (take_a) {
-                isa |= 1u << i;
-                ++ia;
-                if (ia < b.na) ha = SA[ia];
-            } else {
-                ++ib;
-                if (ib < b.nb) hb = SB[ib];
-            }
-        }
-        bool has_next;
-        uint64_t nk;
-        if (ia < b.na || ib < b.nb) {
-            has_next = true;
-            nk = (ia < b.na && (ib >= b.nb || ha <= hb)) ? ha : hb;
-        } else {
-            has_next = ha_next || hb_next;
-            nk = (ha_next && (!hb_next || ka_next <= kb_next)) ? ka_next : kb_next;
-        }
-        if (!has_next || nk != prev) emit |= 1u << (k1 - k0 - 1);
-    }
-    {
-        const int sh = (lane % LPW) * NI;
-        uint64_t wl = (uint64_t)isa << sh, we = (uint64_t)emit << sh;
-#pragma unroll
-        for (int o = 1; o < LPW; o <<= 1) {
-            wl |= (uint64_t)__shfl_xor((unsigned long long)wl, o);
-            we |= (uint64_t)__shfl_xor((unsigned long long)we, o);
-        }
-        if (lane % LPW == 0) {
-            s_wa[threadIdx.x / LPW] = wl;
-            s_we[threadIdx.x / LPW] = we;
-        }
-        uint32_t x = (uint32_t)__popc(emit);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-        if (lane == 0) s_cw[wv] = x;
-    }
-    __syncthreads();
-    // ---- the tile's output offset: publish the count, look back (wave 0)
-    // while every wave prefixes the bitmaps
-    if (wv == 0 && diag == 1) {                 // timing diagnostic: no look-back (wrong offsets)
-        if (lane == 0) s_off = t * (TT / 4);
-    } else if (wv == 0) {
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int k = 0; k < NWV; ++k) cnt += s_cw[k];
-        unsigned long long acc = 0;
-        if (t == 0) {
-            if (lane == 0) __hip_atomic_store(&st[0], kOcP | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&st[t], kOcA | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            acc = lookback_sum<1>(st, (long long)t - 1, lane, err);
-            if (lane == 0) __hip_atomic_store(&st[t], kOcP | (acc + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_off = acc;
-            if (t + 1 == gridDim.x) *out_count = acc + cnt;
-        }
-    }
-    const uint64_t word_a = lane < NW ? s_wa[lane] : 0, word_e = lane < NW ? s_we[lane] : 0;
-    uint32_t pre_a = (uint32_t)__popcll(word_a), pre_e = (uint32_t)__popcll(word_e);
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t ya = __shfl_up(pre_a, o), ye = __shfl_up(pre_e, o);
-        if (lane >= o) {
-            pre_a += ya;
-            pre_e += ye;
-        }
-    }
-    pre_a -= (uint32_t)__popcll(word_a);
-    pre_e -= (uint32_t)__popcll(word_e);
-    __syncthreads();
-    const uint64_t ob = s_off;
-    auto below = [&](uint64_t msk) -> uint32_t {        // set bits of msk below this lane
-        return __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-    };
-    auto tag_at = [&](uint32_t sl, uint64_t &k, uint64_t &ts, uint32_t &r) {
-        const bool sa = sl < na2;
-        k = s_key[(int)sl + (sa ? oa_k : ob_k)];
-        ts = s_ts[(int)sl + (sa ? oa_t : ob_t)];
-        r = s_rep[(int)sl + (sa ? oa_r : ob_r)];
-    };
-    auto tomb_at = [&](uint32_t sl) -> uint8_t { return s_tomb[(int)sl + (sl < na2 ? oa_m : ob_m)]; };
-    // ---- the winners, as k_lww_write (one part per tile)
-#pragma unroll
-    for (int f = 0; f < FI; ++f) {
-        const int w = wv + NWV * f;                      // the tile's word
-        const uint64_t wa = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_a >> 32), w) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_a, w);
-        const uint64_t we = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(word_e >> 32), w) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)word_e, w);
-        if (!((we >> lane) & 1)) continue;
-        const uint32_t la = (uint32_t)__builtin_amdgcn_readlane(pre_a, w) + below(wa);   // A items before
-        const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane(pre_e, w) + below(we);   // output rank
-        const uint32_t k = 64u * (uint32_t)w + (uint32_t)lane;
-        const uint32_t lb = k - la;
-        const bool is_a = (wa >> lane) & 1;
-        const size_t ai = ra + la;
-        uint64_t key, ts;
-        uint32_t rep, xs;
-        bool on_a;
-        size_t wi;
-        if (is_a) {                                      // an A run end whose key B does not hold
-            xs = la + 2;
-            tag_at(xs, key, ts, rep);
-            on_a = true;
-            wi = ai;
-        } else {                                         // B's run end; A's run end of the key just before it
-            const uint32_t bs = na2 + 1 + lb;
-            uint64_t kb_, tb, ka_ = 0, ta = 0;
-            uint32_t rb_, ra_ = 0;
-            tag_at(bs, kb_, tb, rb_);
-            const bool a_has = ai > 0 && (tag_at(la + 1, ka_, ta, ra_), ka_ == kb_);
-            const bool ya = a_has && (ta > tb || (ta == tb && ra_ >= rb_));   // A wins an equal tag
-            key = kb_;
-            on_a = ya;
-            xs = ya ? la + 1 : bs;
-            ts = ya ? ta : tb;
-            rep = ya ? ra_ : rb_;
-            wi = ya ? ai - 1 : rb + lb;
-        }
-        uint8_t tomb = tomb_at(xs);
-        const uint32_t lo = on_a ? 0u : na2;
-        bool more = wi > 0;
-        uint32_t sl = xs;
-        while (more && sl > lo) {
-            uint64_t pk, pt;
-            uint32_t pr;
-            tag_at(sl - 1, pk, pt, pr);
-            if (pk != key || pt != ts || pr != rep) {
-                more = false;
-                break;
-            }
-            --sl;
-            --wi;
-            tomb = tomb_at(sl);
-            more = wi > 0;
-        }
-        if (more && sl == lo) {                          // the run of copies reaches past the staging
-            const size_t fc = first_copy(on_a ? A.key : B.key, on_a ? A.ts : B.ts, on_a ? A.rep : B.rep, wi, key, ts,
-                                         rep);
-            tomb = (on_a ? A.tomb : B.tomb)[fc];
-        }
-        const uint64_t o = ob + rk;
-        if (diag == 1 && o >= n) continue;
-        if (o >= n) {                                    // (a look-back timeout's offset: flagged, never stored)
-            atomicOr(err, CRDT_DEV_RANGE);
-            continue;
-        }
-        out.key[o] = key;
-        out.ts[o] = ts;
-        out.rep[o] = rep;
-        out.tomb[o] = tomb;
-    }
-}
-
 // ---------------------------------------------------------------- OR-Set, two passes
 // The same structure for the OR-Set, over TAGS: one output per distinct tag
 // (key, ts, rep) in tag order, its tomb the OR over every copy; in the
@@ -1075,18 +840,15 @@ __global__ __launch_bounds__(WT) void k_or_write(crdt_tuples A, crdt_tuples B, s
     }
 }
 
-// The chunked two-pass schedule (file comment).  count(t0, n, s) /
-// scan(t0, n, count_out, s) / write(t0, n, s) enqueue one chunk's pass on
-// stream s.  On two streams the counts and scans run on the context's aux
-// stream, the writes on its stream, chained by events: write c waits for
-// scan c; count c + 2 waits for write c.  The last scan precedes the last
-// write on the main stream, so every aux pass has finished when the main
-// stream's work has (ws_reserve / the caller's sync see a drained context).
+// The chunked two-pass schedule.  count(t0, n, s) / scan(t0, n, count_out,
+// s) / write(t0, n, s) enqueue one chunk's pass on the context's stream; a
+// chunk is at most kScanMax tiles (one scan workgroup), or `chunk` tiles
+// (sets.lww_chunk / sets.or_chunk, diagnostic build: smaller chunks measured
+// slower; so did a second stream for the counts).
 template <class CountF, class ScanF, class WriteF>
 static int two_pass(crdt_ctx *ctx, size_t ntiles, uint64_t *out_count, CountF count, ScanF scan, WriteF write,
                     size_t chunk, bool fail_bits, uint64_t *bits, size_t bits_bytes) {
     if (chunk == 0 || chunk > kScanMax) chunk = kScanMax;
-    const size_t nchunks = (ntiles + chunk - 1) / chunk;
     const hipStream_t s = ctx->stream;
     if (fail_bits) {                                     // failpoint: one chunk, bitmaps zeroed before the writes
         for (size_t t0 = 0; t0 < ntiles; t0 += chunk) {
@@ -1099,35 +861,12 @@ static int two_pass(crdt_ctx *ctx, size_t ntiles, uint64_t *out_count, CountF co
         for (size_t t0 = 0; t0 < ntiles; t0 += chunk) write(t0, (uint32_t)std::min(chunk, ntiles - t0), s);
         return check_launch(ctx);
     }
-    if (g_set_streams < 2 || nchunks == 1) {
-        for (size_t t0 = 0; t0 < ntiles; t0 += chunk) {
-            const uint32_t n = (uint32_t)std::min(chunk, ntiles - t0);
-            count(t0, n, s);
-            scan(t0, n, t0 + n == ntiles ? out_count : nullptr, s);
-            write(t0, n, s);
-        }
-        return check_launch(ctx);
-    }
-    int rc = ctx_events(ctx, 2 * nchunks + 1);
-    if (rc) return rc;
-    hipEvent_t *ev = ctx->ev;                            // ev[0]: fork; 1 + 2c: scan c done; 2 + 2c: write c done
-    const hipStream_t a = ctx->aux;
-    hipError_t e = hipEventRecord(ev[0], s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(a, ev[0], 0);
-    for (size_t c = 0; c < nchunks && e == hipSuccess; ++c) {
-        const size_t t0 = c * chunk;
+    for (size_t t0 = 0; t0 < ntiles; t0 += chunk) {
         const uint32_t n = (uint32_t)std::min(chunk, ntiles - t0);
-        if (c >= 2) e = hipStreamWaitEvent(a, ev[2 + 2 * (c - 2)], 0);
-        if (e != hipSuccess) break;
-        count(t0, n, a);
-        scan(t0, n, c + 1 == nchunks ? out_count : nullptr, a);
-        e = hipEventRecord(ev[1 + 2 * c], a);
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, ev[1 + 2 * c], 0);
-        if (e != hipSuccess) break;
+        count(t0, n, s);
+        scan(t0, n, t0 + n == ntiles ? out_count : nullptr, s);
         write(t0, n, s);
-        e = hipEventRecord(ev[2 + 2 * c], s);
     }
-    if (e != hipSuccess) return hip_fail(ctx, e);
     return check_launch(ctx);
 }
 
@@ -1139,7 +878,6 @@ static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, con
     const size_t need = Carve::round((ntiles + 1) * 8) + Carve::round(ntiles * 4 + 4) + Carve::round((ntiles + 1) * 8) +
                         Carve::round(ntiles * 2 * LNW * 8) + 1024;
     int rc = ws_reserve(ctx, need);
-    if (!rc && g_set_streams >= 2) rc = ctx_aux(ctx);
     if (rc) return rc;
     Carve w(ctx->ws);
     uint64_t *split = w.take<uint64_t>(ntiles + 1);
@@ -1168,30 +906,6 @@ static int lww_merge_keyruns(crdt_ctx *ctx, const crdt_tuples &A, size_t na, con
                     ntiles * 2 * LNW * 8);
 }
 
-// The one-pass LWW merge (k_lww_fused): split, the look-back words zeroed,
-// one launch.  TT-item tiles of NT threads (sets.fused_shape); 2048 x 512:
-// 43 KB of LDS staging, three workgroups per CU.
-template <int TT, int NT>
-static int lww_merge_fused(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
-                           const crdt_tuples &O, uint64_t *out_count) {
-    const size_t n = na + nb;
-    const size_t ntiles = (n + TT - 1) / TT;
-    if (ntiles >= 0x7fffffffULL || n >= (1ULL << 62)) return CRDT_E_RANGE;
-    const size_t need = Carve::round((ntiles + 1) * 8) * 2 + 1024;
-    int rc = ws_reserve(ctx, need);
-    if (rc) return rc;
-    Carve w(ctx->ws);
-    uint64_t *split = w.take<uint64_t>(ntiles + 1);
-    unsigned long long *st = w.take<unsigned long long>(ntiles + 1);
-    const hipStream_t s = ctx->stream;
-    hipError_t e = hipMemsetAsync(st, 0, ntiles * 8, s);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-    k_lww_split<TT><<<(unsigned)((ntiles + 1 + 15) / 16), 256, 0, s>>>(A.key, B.key, na, nb, ntiles, split);
-    k_lww_fused<TT, NT><<<(unsigned)ntiles, NT, 0, s>>>(A, B, na, nb, split, st, O, out_count, ctx->dev_status,
-                                                               g_fused_diag);
-    return check_launch(ctx);
-}
-
 static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tuples &B, size_t nb,
                                const crdt_tuples &O, uint64_t *out_count) {
     const size_t n = na + nb;
@@ -1200,7 +914,6 @@ static int orset_merge_twopass(crdt_ctx *ctx, const crdt_tuples &A, size_t na, c
     const size_t need = Carve::round((ntiles + 1) * 8) + Carve::round(ntiles * 4 + 4) + Carve::round((ntiles + 1) * 8) +
                         Carve::round(ntiles * 2 * ONW * 8) + 1024;
     int rc = ws_reserve(ctx, need);
-    if (!rc && g_set_streams >= 2) rc = ctx_aux(ctx);
     if (rc) return rc;
     Carve w(ctx->ws);
     uint64_t *split = w.take<uint64_t>(ntiles + 1);
@@ -1442,13 +1155,6 @@ static int set_merge(crdt_ctx *ctx, const crdt_tuples *a, size_t na, const crdt_
     crdt_tuples empty{nullptr, nullptr, nullptr, nullptr};
     const crdt_tuples &A = na ? *a : empty;
     const crdt_tuples &B = nb ? *b : empty;
-    // (the bitmap failpoint exercises the two-pass form's consistency checks)
-    if (LWW && g_lww_fused && !fail_zero_bits_armed()) {
-        if (g_fused_shape == 1) return lww_merge_fused<1024, 256>(ctx, A, na, B, nb, *out, out_count);
-        if (g_fused_shape == 2) return lww_merge_fused<2048, 256>(ctx, A, na, B, nb, *out, out_count);
-        if (g_fused_shape == 3) return lww_merge_fused<4096, 1024>(ctx, A, na, B, nb, *out, out_count);
-        return lww_merge_fused<2048, 512>(ctx, A, na, B, nb, *out, out_count);
-    }
     return LWW ? lww_merge_keyruns(ctx, A, na, B, nb, *out, out_count)
                : orset_merge_twopass(ctx, A, na, B, nb, *out, out_count);
 }

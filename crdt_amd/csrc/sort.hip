@@ -1883,7 +1883,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
                                                   uint32_t *__restrict__ fbw, int diag,
                                                   unsigned long long *__restrict__ st, crdt_tuples out,
                                                   uint64_t *__restrict__ out_count, uint32_t *__restrict__ err,
-                                                  uint32_t nch, int lbw, PlanGuard pg = {}) {
+                                                  uint32_t nch, PlanGuard pg = {}) {
     constexpr uint32_t R = kOcKeys / OCB;             // keys per thread (round-major)
     __shared__ uint32_t tab[kOcKeys];
     __shared__ uint64_t stg[kOcCap];
@@ -2096,8 +2096,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         const uint32_t nt0 = s_totk[0];
         unsigned long long acc = 0;
         if (ci > 0) {
-            acc = lbw == 4 ? lookback_sum<4>(st, (long long)ci - 1, lane, err)
-                           : lookback_sum<1>(st, (long long)ci - 1, lane, err);
+            acc = lookback_sum<1>(st, (long long)ci - 1, lane, err);
             if (lane == 0)
                 __hip_atomic_store(&st[ci], kOcP | (acc + nt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2178,8 +2177,7 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
         const uint32_t ci = blockIdx.x * K, n0 = s_totk[0], n1 = K == 2 ? s_totk[K - 1] : 0u;
         unsigned long long acc = 0;
         if (ci > 0) {
-            acc = lbw == 4 ? lookback_sum<4>(st, (long long)ci - 1, lane, err)
-                           : lookback_sum<1>(st, (long long)ci - 1, lane, err);
+            acc = lookback_sum<1>(st, (long long)ci - 1, lane, err);
             if (lane == 0)
                 __hip_atomic_store(&st[ci], kOcP | (acc + n0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2996,7 +2994,7 @@ static int d2_body(crdt_ctx *ctx, const crdt_tuples &A, size_t na, const crdt_tu
             const unsigned grid = nch / (unsigned)kpair;
 #define OR_CHUNK(LBV, NAR, KV)                                                                                 \
     k_or_chunk<LBV, NAR, KV><<<grid, OCB, 0, s>>>(sorted, tmp, w.plan, w.cb, w.cc, fbw, g_rdd_diag, LBV ? w.cst : nullptr, \
-                                                   out, out_count, ctx->dev_status, nch, g_or_lb_words, cur_guard())
+                                                   out, out_count, ctx->dev_status, nch, cur_guard())
             if (lb) {
                 if (narrow) {
                     if (kpair == 2) OR_CHUNK(true, true, 2);

@@ -20,7 +20,7 @@ def eng():
     from crdt_amd.engine import Engine
     assert torch.cuda.is_available(), "gpu-marked test without a GPU"
     e = Engine(0)
-    # CRDT_TEST_OPTIONS="sets.streams=1,join.unroll=2": run the GPU suite
+    # CRDT_TEST_OPTIONS="sets.lww_parts=2,join.unroll=2": run the GPU suite
     # under non-default kernel knobs (crdt_set_option)
     from knobs import set_knob
     for opt in filter(None, os.environ.get("CRDT_TEST_OPTIONS", "").split(",")):

@@ -223,25 +223,6 @@ def test_slice_write_without_slots(eng):
 
 
 @pytest.mark.diag
-@pytest.mark.parametrize("parts", [2, 4])
-def test_tile_parts_match_oracle(eng, parts):
-    """The tile pass at every workgroup shape (refmerge.tile_parts: 1/parts of
-    a 4096-item tile per workgroup, each with its own slot table): the packed
-    batch with LDS-staged and global Atoi tables, the KATs and multi-key
-    config-A replicas, every replica against the oracle."""
-    from crdt_amd import _lib
-    set_knob(b"refmerge.tile_parts", parts)
-    try:
-        for n_str in (0, 257):
-            test_packed_batch_matches_oracle(eng, n_str)
-        test_all_kats_in_one_batch(eng)
-        test_config_a_demo_matches_oracle(eng, 1)
-        test_large_batch_matches_oracle(eng)
-    finally:
-        set_knob(b"refmerge.tile_parts", 1)
-
-
-@pytest.mark.diag
 def test_count_pass_register_staging(eng):
     """refmerge.count_dma=0: the count pass stages the tile's ts through
     registers instead of LDS-DMA (also the path for logs that are not 8-byte

@@ -154,14 +154,13 @@ def test_sets_unaligned_views(eng, off_a, off_b):
 
 
 @pytest.mark.diag
-@pytest.mark.parametrize("chunk,streams", [(0, 1), (1, 2), (3, 1), (7, 2), (64, 2)])
-def test_sets_chunked_schedules(eng, chunk, streams):
+@pytest.mark.parametrize("chunk", [0, 1, 3, 7, 64])
+def test_sets_chunked_schedules(eng, chunk):
     """The count / write passes over chunks of tiles (sets.lww_chunk,
-    sets.or_chunk; 0 = one chunk) on one stream or with the counts on the
-    context's aux stream (sets.streams = 2): chunk edges inside key runs,
-    tile edges, unaligned views; == the oracle."""
-    from crdt_amd import _lib
-    for name, v in ((b"sets.lww_chunk", chunk), (b"sets.or_chunk", chunk), (b"sets.streams", streams)):
+    sets.or_chunk; 0 = one chunk of up to 16384 tiles, the schedule of any
+    larger call): chunk edges inside key runs, tile edges, unaligned views;
+    == the oracle."""
+    for name, v in ((b"sets.lww_chunk", chunk), (b"sets.or_chunk", chunk)):
         set_knob(name, v)
     try:
         _check(eng, *_sets(77, 100_000, 100_000, 50_000))
@@ -171,7 +170,7 @@ def test_sets_chunked_schedules(eng, chunk, streams):
         test_sets_unaligned_views(eng, 3, 5)
         assert eng.device_status(clear=True) == 0
     finally:
-        for name, v in ((b"sets.lww_chunk", 0), (b"sets.or_chunk", 0), (b"sets.streams", 1)):
+        for name, v in ((b"sets.lww_chunk", 0), (b"sets.or_chunk", 0)):
             set_knob(name, v)
 
 
