@@ -1300,14 +1300,22 @@ int gossip_decode_at(crdt_ctx *ctx, uint32_t nb, const uint8_t *data, const uint
     }
     // decode form (codec.small): 0 the multi-pass kernels, 2 the one-pass
     // kernel, 3 its coalesced form; 1 (auto): the one-pass kernel for a few
-    // small bodies (the Server path), the coalesced form for many bodies of
-    // up to two chunks each (the population wire rounds: DESIGN.md §5.10),
-    // the multi-pass kernels otherwise
+    // bodies of one chunk, the coalesced form for a few larger bodies (the
+    // Server path) and for many bodies of up to two chunks each (the
+    // population wire rounds: DESIGN.md §5.10), the multi-pass kernels
+    // otherwise
+    // (round 6: a few bodies of more than one 4096-item chunk -- the Server
+    // path at config A, 10k entries per pull -- take the coalesced form too:
+    // k_dec_big4 21.7 us against k_dec_small's 26.1 us for 5 x 10k,
+    // profiles/r06/ab/server_decode_form.txt)
     int form = g_dec_small;
-    if (form == 1)
-        form = nb <= (uint32_t)ctx->num_cus && max_ne <= kSmallItems && max_np <= kSmallItems ? 2
-               : max_ne <= 2 * kBigCH && max_np <= 2 * kBigCH                                ? 3
-                                                                                              : 0;
+    if (form == 1) {
+        const uint64_t mx = std::max(max_ne, max_np);
+        form = nb <= (uint32_t)ctx->num_cus && mx <= 4096          ? 2
+               : nb <= (uint32_t)ctx->num_cus && mx <= kSmallItems ? 3
+               : mx <= 2 * kBigCH                                  ? 3
+                                                                   : 0;
+    }
     const bool small = form >= 2;
     e = hipMemcpyAsync(d_head, h_head, head, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && !small) e = hipMemcpyAsync(out->r_off, h_roff, (nb + 1) * 8, hipMemcpyHostToDevice, s);
