@@ -190,6 +190,42 @@ def test_set_merge_local(comm, lww, case):
         np.testing.assert_array_equal(x, e)
 
 
+def _dup_sets(seed, R, n):
+    """Every rank's sorted sides drawn from 40 keys x 4 ts x 2 replicas: exact
+    duplicate tags within and across ranks and sides, with random tombs -- the
+    stable rank order and the first-copy tomb rules decide every output."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in range(R):
+        sides = []
+        for _ in range(2):
+            m = int(rng.integers(0, n))
+            t = (rng.integers(0, 40, m).astype(np.uint64), rng.integers(0, 4, m).astype(np.uint64),
+                 rng.integers(0, 2, m).astype(np.uint32), rng.integers(0, 2, m).astype(np.uint8))
+            o = np.lexsort((t[2], t[1], t[0]))          # stable: equal tags keep their (random) tomb order
+            sides.append(tuple(np.ascontiguousarray(x[o]) for x in t))
+        out.append(sides)
+    return out
+
+
+@pytest.mark.parametrize("lww", [True, False])
+@pytest.mark.parametrize("n", [300, 5000])
+def test_set_merge_local_duplicate_tags(comm, lww, n):
+    """The owners' rank-order merge tree of the received runs under heavy
+    exact-tag duplication == the oracle of the stable rank-order merges (equal
+    tags: lower rank first, input order within a rank)."""
+    R = comm.nranks
+    sets = _dup_sets(50 + n, R, n)
+    A = [TupleSet.from_numpy(*s[0], "cuda:0") for s in sets]
+    B = [TupleSet.from_numpy(*s[1], "cuda:0") for s in sets]
+    exp = (oracle.lww_merge if lww else oracle.orset_merge)(stable_rank_merge([s[0] for s in sets]),
+                                                            stable_rank_merge([s[1] for s in sets]))
+    torch.cuda.synchronize()
+    for g in comm.set_merge_local(A, B, lww=lww, gather=True):
+        for x, e in zip(g.to_numpy(), exp):
+            np.testing.assert_array_equal(x, e)
+
+
 def test_refmerge_ts_range_shards(comm, eng):
     """crdt_shard_refmerge over R ts-range shards of one batch (rank r holds
     the r-th ts range of every replica): each member's slice of the new Diff
