@@ -75,23 +75,28 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *tot) {
 // Striped tile layout (round 6, VERDICT r05: the blocked layout above ran
 // the no-look-back pass at half the copy rate -- each uint4 load touched 16 B
 // of every 64 B across the wave): item (k, lane-major) = tile + (k * TB +
-// tid) * 4 + j, so every load and store instruction covers a contiguous
-// span of the wave.  The block scan runs over the IPT / 4 groups in k-major
-// order: wave scans of the four group sums at once, one barrier.
-constexpr int G = IPT / 4;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// tid) * 2 + j, so every load (u32x2) and store (u64x2) instruction covers a
+// contiguous span of the wave.  Late round 6 (tools/mb/copy_shapes.hip,
+// profiles/r06/copy_shapes.txt): the earlier u32x4 loads with two u64x2
+// nontemporal stores 32 B apart ran the copy at 3.3 TB/s; this shape with
+// default-policy stores runs it at 5.7-5.9 TB/s.  The block scan runs over the
+// IPT / 2 groups in k-major order: wave scans of the group sums at once, one
+// barrier.
+constexpr int G = IPT / 2;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void load_striped(const uint32_t *__restrict__ in, size_t tile0, uint32_t (&v)[IPT],
                                              uint64_t (&s)[G]) {
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        const u32x4 q = __builtin_nontemporal_load((const u32x4 *)(in + tile0 + ((size_t)k * TB + threadIdx.x) * 4));
-        v[4 * k] = q.x, v[4 * k + 1] = q.y, v[4 * k + 2] = q.z, v[4 * k + 3] = q.w;
-        s[k] = (uint64_t)q.x + q.y + q.z + q.w;
+        const u32x2 q = __builtin_nontemporal_load((const u32x2 *)(in + tile0 + ((size_t)k * TB + threadIdx.x) * 2));
+        v[2 * k] = q.x, v[2 * k + 1] = q.y;
+        s[k] = (uint64_t)q.x + q.y;
     }
 }
-// ex[k] = exclusive prefix of (k, tid) within the tile; returns the tile total
-__device__ __forceinline__ uint64_t block_scan_g(const uint64_t (&s)[G], uint64_t (&ex)[G]) {
+// in place: s[k] (the group sum of (k, tid)) -> its exclusive prefix within
+// the tile; returns the tile total
+__device__ __forceinline__ uint64_t block_scan_g(uint64_t (&s)[G]) {
     __shared__ uint64_t s_w[G][TB / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t x[G];
@@ -110,16 +115,21 @@ __device__ __forceinline__ uint64_t block_scan_g(const uint64_t (&s)[G], uint64_
         for (int k = 0; k < G; ++k) s_w[k][w] = x[k];
     }
     __syncthreads();
+    // the wave sums of group k scanned by the first TB / 64 lanes of every
+    // wave (shuffles, no unrolled LDS sweep: at TB = 1024 that spilled)
+    constexpr int NW = TB / 64;
     uint64_t run = 0;
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        uint64_t before = 0, all = 0;
+        const uint64_t ws = lane < NW ? s_w[k][lane] : 0;
+        uint64_t inc = ws;
 #pragma unroll
-        for (int q = 0; q < TB / 64; ++q) {
-            before += q < w ? s_w[k][q] : 0;
-            all += s_w[k][q];
+        for (int o = 1; o < NW; o <<= 1) {
+            const uint64_t y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
         }
-        ex[k] = run + before + x[k] - s[k];
+        const uint64_t before = __shfl(inc - ws, w), all = __shfl(inc, NW - 1);
+        s[k] = run + before + x[k] - s[k];
         run += all;
     }
     __syncthreads();
@@ -129,13 +139,90 @@ __device__ __forceinline__ void store_striped(uint64_t *__restrict__ out, size_t
                                               const uint64_t (&ex)[G], uint64_t base) {
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        uint64_t r = base + ex[k];
-        uint64_t o[4];
+        const uint64_t r = base + ex[k];
+        *(u64x2v *)(out + tile0 + ((size_t)k * TB + threadIdx.x) * 2) = (u64x2v){r, r + v[2 * k]};
+    }
+}
+
+// the 64-lane window look-back of status word t (wave 0 calls it, every
+// lane): publishes tot, returns the exclusive prefix
+__device__ __forceinline__ uint64_t window_lookback(unsigned long long *st, uint32_t t, uint64_t tot, int lane,
+                                                    unsigned *err) {
+    uint64_t pre = 0;
+    if (t == 0) {
+        if (lane == 0) __hip_atomic_store(&st[0], FLAG_P | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&st[t], FLAG_A | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t j = (int64_t)t - 1;                             // window [j - 63, j], lane l reads j - l
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t q = j - lane;
+        const unsigned long long w =
+            q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FLAG_P;
+        const uint64_t isp = __ballot((w & ~VAL) == FLAG_P), nr = __ballot((w & ~VAL) == 0);
+        const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
+        const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
+        if (nr & need) {
+            if (++spins > (1u << 20)) {
+                if (lane == 0) atomicAdd(err, 1u);
+                break;
+            }
+            if (spins > 1) __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = lane <= pl ? (w & VAL) : 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = r, r += v[4 * k + j];
-        u64x2v *p = (u64x2v *)(out + tile0 + ((size_t)k * TB + threadIdx.x) * 4);
-        __builtin_nontemporal_store((u64x2v){o[0], o[1]}, p);
-        __builtin_nontemporal_store((u64x2v){o[2], o[3]}, p + 1);
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        pre += v;
+        if (pl < 64) break;
+        j -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(&st[t], FLAG_P | (pre + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return pre;
+}
+
+// VERDICT r05 item 1's form: one workgroup per chunk of C consecutive tiles.
+// Phase 1 loads and sums the C tiles; wave 0 publishes the chunk total and
+// looks back ONCE (64-lane window; LB = false: no look-back, wrong offsets,
+// timing only); phase 2 loads the C tiles again (served by L2 / MALL when
+// they are still there), scans and stores them.  Reads 2x the input.
+template <bool LB>
+__global__ __launch_bounds__(TB) void k_chunked(const uint32_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                unsigned long long *st, uint32_t C, unsigned *err) {
+    __shared__ uint64_t s_base, s_red[TB / 64];
+    const uint32_t ch = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t sum = 0;
+    for (uint32_t c = 0; c < C; ++c) {
+        const size_t tile0 = ((size_t)ch * C + c) * TILE;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const u32x2 q = __builtin_nontemporal_load((const u32x2 *)(in + tile0 + ((size_t)k * TB + threadIdx.x) * 2));
+            sum += (uint64_t)q.x + q.y;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) s_red[w] = sum;
+    __syncthreads();
+    if (w == 0) {
+        uint64_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < TB / 64; ++k) tot += s_red[k];
+        const uint64_t pre = LB ? window_lookback(st, ch, tot, lane, err) : (uint64_t)ch * C * TILE * 512;
+        if (lane == 0) s_base = pre;
+    }
+    __syncthreads();
+    uint64_t base = s_base;
+    for (uint32_t c = 0; c < C; ++c) {
+        const size_t tile0 = ((size_t)ch * C + c) * TILE;
+        uint32_t v[IPT];
+        uint64_t ex[G];
+        load_striped(in, tile0, v, ex);
+        const uint64_t tt = block_scan_g(ex);
+        store_striped(out, tile0, v, ex, base);
+        base += tt;
     }
 }
 
@@ -149,44 +236,13 @@ __global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in,
     const uint32_t t = tile_of(blockIdx.x, chunk);
     const size_t tile0 = (size_t)t * TILE;
     uint32_t v[IPT];
-    uint64_t gs[G], ex[G];
-    load_striped(in, tile0, v, gs);
-    const uint64_t tot = block_scan_g(gs, ex);
+    uint64_t ex[G];
+    load_striped(in, tile0, v, ex);
+    const uint64_t tot = block_scan_g(ex);
     if (MODE == 2) {                                        // 64-lane window look-back by wave 0
         if (threadIdx.x < 64) {
-            const int lane = threadIdx.x;
-            uint64_t pre = 0;
-            if (t == 0) {
-                if (lane == 0) __hip_atomic_store(&st[0], FLAG_P | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                if (lane == 0) __hip_atomic_store(&st[t], FLAG_A | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                int64_t j = (int64_t)t - 1;                 // window [j - 63, j], lane l reads j - l
-                uint32_t spins = 0;
-                for (;;) {
-                    const int64_t q = j - lane;
-                    const unsigned long long w =
-                        q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FLAG_P;
-                    const uint64_t isp = __ballot((w & ~VAL) == FLAG_P), nr = __ballot((w & ~VAL) == 0);
-                    const int pl = isp ? __ffsll((long long)isp) - 1 : 64;
-                    const uint64_t need = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
-                    if (nr & need) {
-                        if (++spins > (1u << 20)) {
-                            if (lane == 0) atomicAdd(err, 1u);
-                            break;
-                        }
-                        if (spins > 1) __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    uint64_t v = lane <= pl ? (w & VAL) : 0;
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-                    pre += v;
-                    if (pl < 64) break;
-                    j -= 64;
-                }
-                if (lane == 0) __hip_atomic_store(&st[t], FLAG_P | (pre + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (lane == 0) s_base = pre;
+            const uint64_t pre = window_lookback(st, t, tot, threadIdx.x, err);
+            if (threadIdx.x == 0) s_base = pre;
         }
     } else if (threadIdx.x == 0) {
         uint64_t pre = 0;
@@ -222,9 +278,9 @@ __global__ __launch_bounds__(TB) void k_onepass(const uint32_t *__restrict__ in,
 
 __global__ __launch_bounds__(TB) void k_reduce(const uint32_t *__restrict__ in, uint64_t *__restrict__ sums) {
     uint32_t v[IPT];
-    uint64_t gs[G], ex[G];
-    load_striped(in, (size_t)blockIdx.x * TILE, v, gs);
-    const uint64_t tot = block_scan_g(gs, ex);
+    uint64_t ex[G];
+    load_striped(in, (size_t)blockIdx.x * TILE, v, ex);
+    const uint64_t tot = block_scan_g(ex);
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
@@ -254,22 +310,23 @@ __global__ __launch_bounds__(1024) void k_scan_sums(uint64_t *sums, uint32_t n) 
 __global__ __launch_bounds__(TB) void k_apply(const uint32_t *__restrict__ in, const uint64_t *__restrict__ sums,
                                               uint64_t *__restrict__ out) {
     uint32_t v[IPT];
-    uint64_t gs[G], ex[G];
+    uint64_t ex[G];
     const size_t tile0 = (size_t)blockIdx.x * TILE;
-    load_striped(in, tile0, v, gs);
-    (void)block_scan_g(gs, ex);
+    load_striped(in, tile0, v, ex);
+    (void)block_scan_g(ex);
     store_striped(out, tile0, v, ex, sums[blockIdx.x]);
 }
 
 // the copy-rate reference of this access pattern: read the u32s, write u64s
 __global__ __launch_bounds__(TB) void k_copy(const uint32_t *__restrict__ in, uint64_t *__restrict__ out) {
     uint32_t v[IPT];
-    uint64_t gs[G], ex[G];
+    uint64_t ex[G];
     const size_t tile0 = (size_t)blockIdx.x * TILE;
-    load_striped(in, tile0, v, gs);
+    load_striped(in, tile0, v, ex);
+    const uint64_t b = ex[0];
 #pragma unroll
     for (int k = 0; k < G; ++k) ex[k] = 0;
-    store_striped(out, tile0, v, ex, gs[0]);
+    store_striped(out, tile0, v, ex, b);
 }
 
 int main(int argc, char **argv) {
@@ -344,6 +401,18 @@ int main(int argc, char **argv) {
         timeit(name, [&] {
             (void)hipMemsetAsync(d_st, 0, ntiles * 8);
             k_onepass<2><<<ntiles, TB>>>(d_in, d_out, d_st, c, d_err);
+        }, true);
+    }
+    const uint32_t cs[] = {1, 2, 4, 8};
+    for (uint32_t c : cs) {
+        if (ntiles % c) continue;
+        char name[64];
+        snprintf(name, sizeof name, "chunks of %u tiles, no look-back", c);
+        timeit(name, [&] { k_chunked<false><<<ntiles / c, TB>>>(d_in, d_out, d_st, c, d_err); }, false);
+        snprintf(name, sizeof name, "chunks of %u tiles, look-back", c);
+        timeit(name, [&] {
+            (void)hipMemsetAsync(d_st, 0, ntiles * 8);
+            k_chunked<true><<<ntiles / c, TB>>>(d_in, d_out, d_st, c, d_err);
         }, true);
     }
     timeit("memset of the status words", [&] { (void)hipMemsetAsync(d_st, 0, ntiles * 8); }, false);
