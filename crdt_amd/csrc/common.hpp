@@ -72,6 +72,11 @@ inline int hip_fail(crdt_ctx *ctx, hipError_t e) {
 #include "knobs.inc"
 #undef KNOB
 #ifdef CRDT_DIAG
+constexpr bool kDiagBuild = true;          // kernels keep their timing-diagnostic branches
+#else
+constexpr bool kDiagBuild = false;         // kernels fold their timing-diagnostic branches away
+#endif
+#ifdef CRDT_DIAG
 // Failpoints (crdt_set_option "fail.*", diagnostic build only): error-path tests.
 extern std::atomic<int> g_fail_refmerge;   // the next n RefMerge calls return CRDT_E_NOMEM
 extern std::atomic<int> g_fail_zero_bits;  // the next n two-pass merges zero their bitmaps between the passes

@@ -915,7 +915,7 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
         }
     }
     __syncthreads();
-    if ((diag & 255) == 2) return;
+    if (kDiagBuild && (diag & 255) == 2) return;     // (timing diagnostic: diagnostic build only)
     for (int h = threadIdx.x; h < TT; h += WT) {
         const uint32_t slot = t_slot[h];
         if (slot == kEmpty) continue;

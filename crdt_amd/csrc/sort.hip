@@ -965,7 +965,8 @@ template <int MODE, int WORDS>
 __global__ __launch_bounds__(DB) void k_dd_apply(const uint64_t *__restrict__ c, size_t n,
                                                  const SortPlan *__restrict__ plan_, const uint32_t *__restrict__ loc,
                                                  const uint32_t *__restrict__ tot, crdt_tuples out,
-                                                 uint64_t *__restrict__ out_count, int diag = 0, PlanGuard pg = {}) {
+                                                 uint64_t *__restrict__ out_count, int diag_ = 0, PlanGuard pg = {}) {
+    const int diag = kDiagBuild ? diag_ : 0;          // (the product build has no timing diagnostics)
     __shared__ uint32_t s_c[DI * (DB / 64)];      // emits per (round, wave), then their exclusive prefix
     __shared__ uint64_t s_v[MODE == DD_LWW ? DT * WORDS : 1];   // LWW: the tile's composites (run walks)
     __shared__ DdEdges<WORDS> s_x;
@@ -1522,8 +1523,9 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
                                                    const uint32_t *__restrict__ run, uint32_t ntiles, size_t n,
                                                    unsigned long long *__restrict__ flag, uint64_t *__restrict__ dst,
                                                    uint64_t *__restrict__ bounds, unsigned long long *__restrict__ cst,
-                                                   uint32_t nch, uint32_t *__restrict__ err, int diag,
+                                                   uint32_t nch, uint32_t *__restrict__ err, int diag_,
                                                    bool place_batch, SubHist shist, PlanGuard pg = {}) {
+    const int diag = kDiagBuild ? diag_ : 0;          // (the product build has no timing diagnostics)
     __shared__ uint32_t s_run[kRunLds];
     __shared__ uint32_t s_h[OB_WAVES][kObSub];        // per-wave counts by sub-bucket, then the cursors (row 0)
     __shared__ uint64_t s_buf[kObBatch];              // (batched placement) one round's tuples by sub-bucket
@@ -1880,7 +1882,7 @@ template <bool LB, bool NARROW, int K>
 __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k_or_chunk(const uint64_t *__restrict__ c, uint64_t *__restrict__ tmp,
                                                   const SortPlan *__restrict__ plan_,
                                                   const uint64_t *__restrict__ bounds, uint32_t *__restrict__ cnt,
-                                                  uint32_t *__restrict__ fbw, int diag,
+                                                  uint32_t *__restrict__ fbw, int diag_,
                                                   unsigned long long *__restrict__ st, crdt_tuples out,
                                                   uint64_t *__restrict__ out_count, uint32_t *__restrict__ err,
                                                   uint32_t nch, PlanGuard pg = {}) {
@@ -1893,16 +1895,15 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     __shared__ unsigned long long s_off;
     const SortPlan p = *plan_;
     if (!plan_guard_ok(p, pg)) return;                 // (uniform: before any barrier)
+    const int diag = kDiagBuild ? diag_ : 0;          // (the product build has no timing diagnostics)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t kb = p.b0 + p.br + p.bt, tb = p.b0;
     bool fb = false;                                  // (uniform) a chunk of this workgroup fell back
     bool stop = false;                                // (timing diagnostics 1..4: every chunk stops at that phase)
-    size_t sk[K];
     for (int kk = 0; kk < K; ++kk) {
     const uint32_t ci = blockIdx.x * K + (uint32_t)kk;
     uint64_t *ost = ostb[kk];
     const size_t s = bounds[ci], e = bounds[ci + 1];
-    sk[kk] = s;
     if (e - s > kOcCap) {                             // skewed keys: the radix path instead
         if (tid == 0) {
             atomicOr(fbw, 1u);
@@ -2169,10 +2170,10 @@ __global__ __launch_bounds__(OCB) __attribute__((amdgpu_waves_per_eu(8))) void k
     if (fb) return;                                   // (uniform; the call falls back to the radix path)
     if constexpr (!LB) {
         for (int kk = 0; kk < K; ++kk)
-            for (uint32_t i = tid; i < s_totk[kk]; i += OCB) tmp[sk[kk] + i] = ostb[kk][i];
+            for (uint32_t i = tid; i < s_totk[kk]; i += OCB) tmp[bounds[blockIdx.x * K + kk] + i] = ostb[kk][i];
         return;
     }
-    if (K == 2 && w == 0 && diag == 6 && lane == 0) s_off = sk[0];
+    if (K == 2 && w == 0 && diag == 6 && lane == 0) s_off = bounds[blockIdx.x * K];
     if (K == 2 && w == 0 && diag != 6) {              // one look-back for both chunks, after both are placed
         const uint32_t ci = blockIdx.x * K, n0 = s_totk[0], n1 = K == 2 ? s_totk[K - 1] : 0u;
         unsigned long long acc = 0;
@@ -2517,7 +2518,8 @@ __global__ __launch_bounds__(RB) void k_or_rdd_count(uint64_t *__restrict__ c, s
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       uint64_t *__restrict__ scratch, uint32_t *__restrict__ cnt,
-                                                      int diag, PlanGuard pg = {}) {
+                                                      int diag_, PlanGuard pg = {}) {
+    const int diag = kDiagBuild ? diag_ : 0;          // (the product build has no timing diagnostics)
     __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
     const SortPlan p = *plan_;
@@ -2566,7 +2568,8 @@ __global__ __launch_bounds__(RB) void k_or_rdd_apply(const uint64_t *__restrict_
                                                       const SortPlan *__restrict__ plan_,
                                                       const uint64_t *__restrict__ bounds,
                                                       const uint32_t *__restrict__ loc, const uint32_t *__restrict__ tot,
-                                                      crdt_tuples out, uint64_t *__restrict__ out_count, int diag, PlanGuard pg = {}) {
+                                                      crdt_tuples out, uint64_t *__restrict__ out_count, int diag_, PlanGuard pg = {}) {
+    const int diag = kDiagBuild ? diag_ : 0;          // (the product build has no timing diagnostics)
     __shared__ alignas(16) uint64_t s_raw[RCAP + 2];
     __shared__ uint32_t s_c[RR * (RB / 64)];             // outputs per (round, wave), then their exclusive prefix
     __shared__ uint32_t s_big[RCAP / (kInsMax + 1) + 1], s_nbig, s_w[RB / 64];
