@@ -1517,7 +1517,8 @@ __global__ __launch_bounds__(LTB) void k_lww_table_g(const uint64_t *__restrict_
 constexpr int OBB = 1024;                          // threads per bucket workgroup
 constexpr int OB_WAVES = OBB / 64;
 constexpr uint32_t kObSub = 256;                   // chunks per top-byte bucket at most (bk <= 25)
-constexpr uint32_t kObBatch = 4 * OB_WAVES * 8 * 16;   // a placement round's tuples at most (8 loads x 16 lanes per group)
+constexpr uint32_t kObLoads = 12;                  // gathered elements per lane per round (KT tiles x GL)
+constexpr uint32_t kObBatch = 4 * OB_WAVES * kObLoads * 16;   // a placement round's tuples at most (16 lanes per group)
 template <uint32_t GL>
 __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ c, const SortPlan *__restrict__ plan_,
                                                    const uint32_t *__restrict__ run, uint32_t ntiles, size_t n,
@@ -1554,7 +1555,7 @@ __global__ __launch_bounds__(OBB) void k_or_bucket(const uint64_t *__restrict__ 
     __syncthreads();
     if (tid == 0) __hip_atomic_store(&flag[T], kLtReady | s_sum[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // gather the runs (as k_lww_table_g: 16-lane groups, KT tiles each per round, GL elements per lane per tile)
-    constexpr uint32_t KT = 8 / GL, NG = 4 * OB_WAVES;
+    constexpr uint32_t KT = kObLoads / GL, NG = 4 * OB_WAVES;
     constexpr uint32_t TILE = 2048 * GL;
     const uint32_t g = (uint32_t)tid >> 4, l = (uint32_t)lane & 15;
     auto load = [&](uint32_t t0, uint32_t *rn, const uint64_t **rp, uint64_t *x) {
