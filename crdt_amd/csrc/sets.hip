@@ -240,46 +240,60 @@ __global__ __launch_bounds__(LCB) void k_lww_count(const uint64_t *__restrict__ 
 }
 
 // Exclusive scan of the n <= kScanMax tile counts of one chunk (tiles t0 ..
-// t0 + n) by one workgroup (a contiguous run per thread), on top of the
-// offset the previous chunk's scan left at ic[t0] (0 for t0 == 0); ic[t0 +
-// n] = the running total, also written to *count when count != nullptr.
-// (Chunks held in registers: 6.9 / 11.5 us at 4.9k / 9.8k tiles; 16
-// coalesced rows per wave: 11.9 / 12.0; this loop 5.5 / 11.9.)
+// t0 + n) by one workgroup, on top of the offset the previous chunk's scan
+// left at ic[t0] (0 for t0 == 0); ic[t0 + n] = the running total, also
+// written to *count when count != nullptr.  Over 8k counts, striped rows
+// (scan.hpp wg_scan_rows, every access coalesced): 11.7 -> 8.4 us at 9.8k
+// tiles; up to 8k a contiguous run per thread in registers is quicker (4.7
+// us at 4.9k; striped ~7-10 us at that size).  (16 coalesced rows per wave
+// with a serial carry: 11.9 / 12.0 us.)
 __global__ __launch_bounds__(1024) void k_chunk_scan(const uint32_t *__restrict__ tcnt, uint64_t t0, uint32_t n,
                                                      uint64_t *__restrict__ ic, uint64_t *__restrict__ count) {
+    __shared__ uint64_t s_pre[16 * 16 + 1];
     __shared__ uint64_t s_w[16];
-    __shared__ uint64_t s_base;
-    if (threadIdx.x == 0) s_base = t0 ? ic[t0] : 0;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t b = threadIdx.x * per < n ? threadIdx.x * per : n;
-    const uint32_t e = b + per < n ? b + per : n;
-    const uint32_t *tc = tcnt + t0;
-    uint64_t sum = 0;
-    for (uint32_t i = b; i < e; ++i) sum += tc[i];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_w[w] = x;
-    __syncthreads();                                     // (also publishes s_base before ic[t0] is rewritten)
-    uint64_t base = s_base, tot = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        base += k < w ? s_w[k] : 0;
-        tot += s_w[k];
-    }
-    uint64_t run = base + x - sum;
+    static_assert(kScanMax <= 16 * 1024, "striped rows: 16 per thread");
+    const uint64_t base = t0 ? ic[t0] : 0;               // (read before any thread rewrites ic[t0]: the
+    const uint32_t *tc = tcnt + t0;                      //  scan's first barrier lies between)
     uint64_t *o = ic + t0;
-    for (uint32_t i = b; i < e; ++i) {
-        o[i] = run;
-        run += tc[i];
+    uint64_t tot = 0;
+    if (n > 8u * 1024) {                                 // (uniform) striped rows
+        tot = wg_scan_rows<1024, 16, uint32_t>([&](uint32_t i) { return tc[i]; }, n,
+                                               [&](uint32_t i, uint64_t x) { o[i] = base + x; }, s_pre);
+    } else {                                             // <= 8 counts per thread: a contiguous run each
+        const uint32_t per = (n + 1023) / 1024;
+        const uint32_t b = threadIdx.x * per < n ? threadIdx.x * per : n;
+        const uint32_t e = b + per < n ? b + per : n;
+        uint32_t v[8];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            v[k] = b + k < e ? tc[b + k] : 0u;
+            sum += v[k];
+        }
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint64_t x = sum;
+#pragma unroll
+        for (int o2 = 1; o2 < 64; o2 <<= 1) {
+            const uint64_t y = __shfl_up(x, o2);
+            if (lane >= o2) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint64_t run = base + x - sum;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            run += k < w ? s_w[k] : 0;
+            tot += s_w[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (b + k < e) o[b + k] = run;
+            run += v[k];
+        }
     }
     if (threadIdx.x == 0) {
-        o[n] = s_base + tot;
-        if (count) *count = s_base + tot;
+        o[n] = base + tot;
+        if (count) *count = base + tot;
     }
 }
 
