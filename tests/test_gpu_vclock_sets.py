@@ -127,6 +127,26 @@ def test_sets_full_config_d(eng):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("tiles", [8192, 8193, 9216, 16385])
+def test_sets_tile_count_scan_shapes(eng, tiles):
+    """The tile-count scan's shapes (k_chunk_scan): up to 8k counts a run per
+    thread, above that striped rows (16 per thread), and past kScanMax
+    (16384) a second scan chunk on top of the first's total.  OR-Set tiles
+    are 2048 merge items, LWW tiles 4096: `tiles` OR tiles (half as many
+    LWW ones) plus one item, device-generated sorted sides == the oracle."""
+    n = tiles * 2048 + 1
+    na, ks = n // 2 + 1, n // 3
+    A = eng.synth_set_tuples(77 + tiles, 0, na, ks)
+    B = eng.synth_set_tuples(77 + tiles, 1, n - na, ks)
+    sa, sb = A.to_numpy(), B.to_numpy()
+    for fn, ref in ((eng.orset_merge, oracle.orset_merge), (eng.lww_merge, oracle.lww_merge)):
+        got = fn(A, B).to_numpy()
+        exp = ref(sa, sb)
+        for g, e, f in zip(got, exp, ("key", "ts", "rep", "tomb")):
+            np.testing.assert_array_equal(g, e, err_msg=f"{fn.__name__}.{f}")
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("na,nb", [(1535, 1), (1536, 1536), (1537, 1535), (3071, 3073), (4608, 0), (0, 4609)])
 def test_sets_tile_boundaries(eng, na, nb):
     """Sizes around the 1536-element merge tile."""
