@@ -749,10 +749,17 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
         const uint64_t gi = it_gi(f);
         const uint64_t *kv = (il ? in.l_kv : in.r_kv) + gi;
         e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
-        e_org[f] = (in_tile && il) ? in.l_origin[gi] : 0;
+        // nontemporal hints on the once-touched origin and kv-range loads and on
+        // the slice / kv stores (profiles/r06/ab/refmerge_nontemporal.txt: gossip
+        // round -12 %, delta -3 %, RefMerge -1 %; the wire round, whose R side the
+        // decode has just written, +2.5 %).  Not on the pair loads: they lose
+        // their Infinity Cache hits (the gossip round's gain halves).  A run-time
+        // choice between hinted and plain accesses is no choice: the compiler
+        // merges the two loads of one address and drops the hint.
+        e_org[f] = (in_tile && il) ? __builtin_nontemporal_load(in.l_origin + gi) : 0;
         if (aff) e_kb[f] = (il ? kl0 : kr0) + gi;
-        else e_kb[f] = ((FOLDS || KV) && in_tile) ? kv[0] : 0;
-        e_ke[f] = ((FOLDS || KV) && !ONE && in_tile) ? kv[1] : 0;   // (ONE: every emitted range has one pair)
+        else e_kb[f] = ((FOLDS || KV) && in_tile) ? __builtin_nontemporal_load(kv) : 0;
+        e_ke[f] = ((FOLDS || KV) && !ONE && in_tile) ? __builtin_nontemporal_load(kv + 1) : 0;   // (ONE: every emitted range has one pair)
     }
     if (FOLDS || KV) {
 #pragma unroll
@@ -833,17 +840,17 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
                 atomicOr(err, CRDT_DEV_RANGE);
                 continue;
             }
-            out.ts[o] = e_ts[f];                         // (nontemporal stores: no change, 153 us)
-            out.src[o] = il ? (int64_t)gi : -(int64_t)gi - 1;
-            out.origin[o] = e_org[f];
+            __builtin_nontemporal_store(e_ts[f], &out.ts[o]);
+            __builtin_nontemporal_store(il ? (int64_t)gi : -(int64_t)gi - 1, &out.src[o]);
+            __builtin_nontemporal_store(e_org[f], &out.origin[o]);
             if (KV) {
                 const uint64_t pos = ONE ? ikt + it_rk(f) : ikt + wb + lp;
-                kvo.off[o] = pos;
+                __builtin_nontemporal_store(pos, &kvo.off[o]);
                 if (k_c[f] && pos + k_c[f] > kvo.cap) {
                     atomicOr(err, CRDT_DEV_RANGE);
                 } else if (k_c[f]) {
-                    kvo.key[pos] = e_slot[f];
-                    kvo.val[pos] = e_v[f];
+                    __builtin_nontemporal_store(e_slot[f], &kvo.key[pos]);
+                    __builtin_nontemporal_store(e_v[f], &kvo.val[pos]);
                     for (uint32_t j = 1; j < k_c[f]; ++j) {   // further kvs of the entry (rare)
                         kvo.key[pos + j] = in.kv_key[e_kb[f] + j] + (il ? 0u : d.rsd);
                         kvo.val[pos + j] = in.kv_val[e_kb[f] + j];
