@@ -22,6 +22,8 @@ struct crdt_ctx {
     void *io = nullptr;      // device staging for host-facing calls (crdt_server_*)
     size_t io_bytes = 0;
     uint32_t *dev_status = nullptr;   // device-side failure flags (CRDT_DEV_*), read by crdt_ctx_device_status
+    bool rm_nt = true;                // RefMerge kv tile passes with nontemporal hints (cleared around the
+                                      // wire round's merge, whose R side the device decode has just written)
     crdt_strtab *keys = nullptr;      // device string tables of the context's Servers (key ids, value ids)
     crdt_strtab *vals = nullptr;
     void *srv_batch = nullptr;        // batched Server merge scratch (server.hip)

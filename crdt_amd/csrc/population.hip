@@ -914,7 +914,11 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     bool merged = false;
     const std::function<int()> run_merge = [&]() -> int {
         int r = upload_round(pop, h, &a);
-        if (!r) r = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, guess_one);
+        if (!r) {                                        // (R just written by the decode: crdt_ctx::rm_nt)
+            ctx->rm_nt = false;
+            r = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, guess_one);
+            ctx->rm_nt = true;
+        }
         merged = r == CRDT_OK;
         return r;
     };
@@ -942,7 +946,11 @@ extern "C" int crdt_population_round_wire(crdt_population *pop, crdt_strtab *key
     const bool one = pop->one_pair && multi == 0;
     if (!merged || stale || one != guess_one) {
         rc = upload_round(pop, h, &a);
-        if (!rc) rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, one);
+        if (!rc) {
+            ctx->rm_nt = false;
+            rc = pop_merge(pop, a, h, r_ts, r_kv, pop->n_kv + n_p, one);
+            ctx->rm_nt = true;
+        }
         if (rc) return rc;
     }
     rc = pop_commit(pop);

@@ -601,7 +601,7 @@ enum { RM_FOLD_NONE = 0, RM_FOLD_FULL = 1, RM_FOLD_DELTA = 2 };
 //        (max, holder count, wrapped sum, parsable count); each R entry's
 //        rank (0: not inserted) goes to r_dk for the holder pass's
 //        overflow walk.
-template <int FOLD, int PARTS, bool KV, bool ONE = false>
+template <int FOLD, int PARTS, bool KV, bool ONE = false, bool NTH = true>
 __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDesc *__restrict__ desc,
                                         const uint64_t *__restrict__ bits, uint16_t *__restrict__ r_dk,
                                         const OkVal *__restrict__ okv, const SlotAcc &acc, int diag,
@@ -751,15 +751,16 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
         e_ts[f] = in_tile ? (il ? in.l_ts[gi] : in.r_ts[gi]) : 0;
         // nontemporal hints on the once-touched origin and kv-range loads and on
         // the slice / kv stores (profiles/r06/ab/refmerge_nontemporal.txt: gossip
-        // round -12 %, delta -3 %, RefMerge -1 %; the wire round, whose R side the
-        // decode has just written, +2.5 %).  Not on the pair loads: they lose
-        // their Infinity Cache hits (the gossip round's gain halves).  A run-time
-        // choice between hinted and plain accesses is no choice: the compiler
-        // merges the two loads of one address and drops the hint.
-        e_org[f] = (in_tile && il) ? __builtin_nontemporal_load(in.l_origin + gi) : 0;
+        // round -12 %, delta -3 %, RefMerge -1 %).  Not on the pair loads: they
+        // lose their Infinity Cache hits (the gossip round's gain halves).  NTH =
+        // false for a merge whose R side the device has just written (the wire
+        // round's decode, crdt_ctx::rm_nt; hinted there: +2.5 %).  The choice is
+        // a template parameter: a run-time select between a hinted and a plain
+        // access of one address is merged by the compiler into a plain one.
+        e_org[f] = (in_tile && il) ? (NTH ? __builtin_nontemporal_load(in.l_origin + gi) : in.l_origin[gi]) : 0;
         if (aff) e_kb[f] = (il ? kl0 : kr0) + gi;
-        else e_kb[f] = ((FOLDS || KV) && in_tile) ? __builtin_nontemporal_load(kv) : 0;
-        e_ke[f] = ((FOLDS || KV) && !ONE && in_tile) ? __builtin_nontemporal_load(kv + 1) : 0;   // (ONE: every emitted range has one pair)
+        else e_kb[f] = ((FOLDS || KV) && in_tile) ? (NTH ? __builtin_nontemporal_load(kv) : kv[0]) : 0;
+        e_ke[f] = ((FOLDS || KV) && !ONE && in_tile) ? (NTH ? __builtin_nontemporal_load(kv + 1) : kv[1]) : 0;   // (ONE: every emitted range has one pair)
     }
     if (FOLDS || KV) {
 #pragma unroll
@@ -840,17 +841,29 @@ __device__ __forceinline__ void rm_tile(const crdt_refmerge_in &in, const TileDe
                 atomicOr(err, CRDT_DEV_RANGE);
                 continue;
             }
-            __builtin_nontemporal_store(e_ts[f], &out.ts[o]);
-            __builtin_nontemporal_store(il ? (int64_t)gi : -(int64_t)gi - 1, &out.src[o]);
-            __builtin_nontemporal_store(e_org[f], &out.origin[o]);
+            if constexpr (NTH) {
+                __builtin_nontemporal_store(e_ts[f], &out.ts[o]);
+                __builtin_nontemporal_store(il ? (int64_t)gi : -(int64_t)gi - 1, &out.src[o]);
+                __builtin_nontemporal_store(e_org[f], &out.origin[o]);
+            } else {
+                out.ts[o] = e_ts[f];
+                out.src[o] = il ? (int64_t)gi : -(int64_t)gi - 1;
+                out.origin[o] = e_org[f];
+            }
             if (KV) {
                 const uint64_t pos = ONE ? ikt + it_rk(f) : ikt + wb + lp;
-                __builtin_nontemporal_store(pos, &kvo.off[o]);
+                if constexpr (NTH) __builtin_nontemporal_store(pos, &kvo.off[o]);
+                else kvo.off[o] = pos;
                 if (k_c[f] && pos + k_c[f] > kvo.cap) {
                     atomicOr(err, CRDT_DEV_RANGE);
                 } else if (k_c[f]) {
-                    __builtin_nontemporal_store(e_slot[f], &kvo.key[pos]);
-                    __builtin_nontemporal_store(e_v[f], &kvo.val[pos]);
+                    if constexpr (NTH) {
+                        __builtin_nontemporal_store(e_slot[f], &kvo.key[pos]);
+                        __builtin_nontemporal_store(e_v[f], &kvo.val[pos]);
+                    } else {
+                        kvo.key[pos] = e_slot[f];
+                        kvo.val[pos] = e_v[f];
+                    }
                     for (uint32_t j = 1; j < k_c[f]; ++j) {   // further kvs of the entry (rare)
                         kvo.key[pos + j] = in.kv_key[e_kb[f] + j] + (il ? 0u : d.rsd);
                         kvo.val[pos + j] = in.kv_val[e_kb[f] + j];
@@ -964,37 +977,37 @@ __global__ __launch_bounds__(FB / PARTS, 8) void k_rm_tile(crdt_refmerge_in in, 
 }
 
 // the tile pass with the kv output, one-pair tiles (two workgroups per CU)
-template <int FOLD>
+template <int FOLD, bool NTH = true>
 __global__ __launch_bounds__(FB, 8) void k_rm_tile_kv1(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                        const uint64_t *__restrict__ bits, const OkVal *__restrict__ okv,
                                                        SlotAcc acc, int diag, const uint64_t *__restrict__ ic,
                                                        crdt_refmerge_out out, uint32_t *__restrict__ err, KvOut kvo) {
-    rm_tile<FOLD, 1, true, true>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
-                                 nullptr, nullptr, err, kvo);
+    rm_tile<FOLD, 1, true, true, NTH>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                      nullptr, nullptr, err, kvo);
 }
 
 // ... and the other tiles: one workgroup per CU (the kv prefix pass needs
 // more than the 64 registers two resident tiles leave a thread)
-template <int FOLD>
+template <int FOLD, bool NTH = true>
 __global__ __launch_bounds__(FB, 4) void k_rm_tile_kv(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                       const uint64_t *__restrict__ bits, const OkVal *__restrict__ okv,
                                                       SlotAcc acc, int diag, const uint64_t *__restrict__ ic,
                                                       crdt_refmerge_out out, uint32_t *__restrict__ err, KvOut kvo) {
-    rm_tile<FOLD, 1, true, false>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
-                                  nullptr, nullptr, err, kvo);
+    rm_tile<FOLD, 1, true, false, NTH>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                       nullptr, nullptr, err, kvo);
 }
 
 // ... and both kinds of tile in one launch, for grids that fit the chip in one
 // wave of workgroups (small batches: one launch fewer, occupancy moot)
-template <int FOLD>
+template <int FOLD, bool NTH = true>
 __global__ __launch_bounds__(FB, 4) void k_rm_tile_kvx(crdt_refmerge_in in, const TileDesc *__restrict__ desc,
                                                        const uint64_t *__restrict__ bits, const OkVal *__restrict__ okv,
                                                        SlotAcc acc, int diag, const uint64_t *__restrict__ ic,
                                                        crdt_refmerge_out out, uint32_t *__restrict__ err, KvOut kvo) {
-    rm_tile<FOLD, 1, true, true>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
-                                 nullptr, nullptr, err, kvo);
-    rm_tile<FOLD, 1, true, false>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
-                                  nullptr, nullptr, err, kvo);
+    rm_tile<FOLD, 1, true, true, NTH>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                      nullptr, nullptr, err, kvo);
+    rm_tile<FOLD, 1, true, false, NTH>(in, desc, bits, nullptr, okv, acc, diag, ic, out, crdt_replay_state{}, nullptr,
+                                       nullptr, nullptr, err, kvo);
 }
 
 // Delta replay, second phase: the global max holder of each slot writes its
@@ -1389,12 +1402,19 @@ static int refmerge_run(crdt_ctx *ctx, const crdt_refmerge_in *inp, const crdt_r
     // one workgroup per tile (1/P of a tile per workgroup measured slower: DESIGN.md §5.4)
 #define RM_TILE(F, P, KV, DIAG)                                                                                \
     if (KV && one_pair) {                                   /* every tile a one-pair tile */                   \
-        k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
+        if (ctx->rm_nt) k_rm_tile_kv1<F, true><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
+        else k_rm_tile_kv1<F, false><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
     } else if (KV && tg <= (unsigned)ctx->num_cus) {                                                           \
-        k_rm_tile_kvx<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
+        if (ctx->rm_nt) k_rm_tile_kvx<F, true><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
+        else k_rm_tile_kvx<F, false><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
     } else if (KV) {                                                                                           \
-        k_rm_tile_kv1<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);      \
-        k_rm_tile_kv<F><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo);       \
+        if (ctx->rm_nt) {                                                                                      \
+            k_rm_tile_kv1<F, true><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
+            k_rm_tile_kv<F, true><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
+        } else {                                                                                               \
+            k_rm_tile_kv1<F, false><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
+            k_rm_tile_kv<F, false><<<tg, FB, 0, s>>>(in, desc, bits, okv, acc, DIAG, ic, out, ctx->dev_status, kvo); \
+        }                                                                                                      \
     } else                                                                                                       \
         k_rm_tile<F, P><<<tg * P, FB / P, 0, s>>>(in, desc, bits, nullptr, okv, acc, DIAG, ic, out,            \
                                                   crdt_replay_state{}, nullptr, nullptr, nullptr, ctx->dev_status)
