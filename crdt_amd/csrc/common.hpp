@@ -270,7 +270,7 @@ __device__ __forceinline__ uint32_t xcd_contig(uint32_t b, uint32_t G) {
 // turn.  Returns the element index in dst of element g0; *at advances past
 // the chunks.  (Reads at most 15 bytes before / past the run, inside its
 // first / last 16-byte block.)
-template <typename E, int NWV>
+template <typename E, int NWV, int AUX = 0>           // AUX: cache policy bits (2: nontemporal)
 __device__ __forceinline__ int dma_run(const E *src, size_t g0, uint32_t cnt, void *dst, uint32_t *at, int wv,
                                        int lane) {
     const char *p = (const char *)(src + g0);
@@ -283,7 +283,7 @@ __device__ __forceinline__ int dma_run(const E *src, size_t g0, uint32_t cnt, vo
     for (uint32_t off = (uint32_t)wv * 1024u; off < bytes; off += NWV * 1024u)
         if (off + 16u * (uint32_t)lane < bytes)
             __builtin_amdgcn_global_load_lds((const void *)(g + off + 16 * lane),
-                                             (__attribute__((address_space(3))) void *)(d + off), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void *)(d + off), 16, 0, AUX);
     *at += bytes;
     return idx;
 }

@@ -372,14 +372,16 @@ __global__ __launch_bounds__(WT) void k_lww_write(crdt_tuples A, crdt_tuples B, 
         oa_k = dma_run<uint64_t, NWV>(A.key, ga, ka, s_key, &at, wv, lane) - sa;
         ob_k = dma_run<uint64_t, NWV>(B.key, gb, kb, s_key, &at, wv, lane) - sb;
         at = 0;
-        oa_t = dma_run<uint64_t, NWV>(A.ts, ga, ka, s_ts, &at, wv, lane) - sa;
-        ob_t = dma_run<uint64_t, NWV>(B.ts, gb, kb, s_ts, &at, wv, lane) - sb;
+        // (ts / rep / tomb read once, nontemporal: they do not evict the keys
+        // the count pass left in the Infinity Cache)
+        oa_t = dma_run<uint64_t, NWV, 2>(A.ts, ga, ka, s_ts, &at, wv, lane) - sa;
+        ob_t = dma_run<uint64_t, NWV, 2>(B.ts, gb, kb, s_ts, &at, wv, lane) - sb;
         at = 0;
-        oa_r = dma_run<uint32_t, NWV>(A.rep, ga, ka, s_rep, &at, wv, lane) - sa;
-        ob_r = dma_run<uint32_t, NWV>(B.rep, gb, kb, s_rep, &at, wv, lane) - sb;
+        oa_r = dma_run<uint32_t, NWV, 2>(A.rep, ga, ka, s_rep, &at, wv, lane) - sa;
+        ob_r = dma_run<uint32_t, NWV, 2>(B.rep, gb, kb, s_rep, &at, wv, lane) - sb;
         at = 0;
-        oa_m = dma_run<uint8_t, NWV>(A.tomb, ga, ka, s_tomb, &at, wv, lane) - sa;
-        ob_m = dma_run<uint8_t, NWV>(B.tomb, gb, kb, s_tomb, &at, wv, lane) - sb;
+        oa_m = dma_run<uint8_t, NWV, 2>(A.tomb, ga, ka, s_tomb, &at, wv, lane) - sa;
+        ob_m = dma_run<uint8_t, NWV, 2>(B.tomb, gb, kb, s_tomb, &at, wv, lane) - sb;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
     }
     __syncthreads();
