@@ -15,10 +15,10 @@ from oracle import oracle
 
 pytestmark = [pytest.mark.gpu, pytest.mark.diag]
 
-D2_KNOBS = [("sort.plan_cache", 0), ("sort.plan_cache", 1), ("sort.group_tile", 4096), ("sort.up_threads", 256),
+D2_KNOBS = [("sort.plan_cache", 0), ("sort.plan_cache", 1), ("sort.group_tile", 8192), ("sort.up_threads", 256),
             ("sort.or_sub_hist", 0), ("sort.or_place_batch", 0), ("sort.or_bucket", 0), ("sort.lww_gather", 0),
             ("sort.or_pair", 0), ("sort.or_narrow", 0), ("ctx.read_poll", 0)]
-DEFAULTS = {"sort.plan_cache": 2, "sort.group_tile": 8192, "sort.up_threads": 512, "sort.or_sub_hist": 1,
+DEFAULTS = {"sort.plan_cache": 2, "sort.group_tile": 4096, "sort.up_threads": 512, "sort.or_sub_hist": 1,
             "sort.or_place_batch": 1, "sort.or_bucket": 1, "sort.lww_gather": 1, "sort.or_pair": 1,
             "sort.or_narrow": 1, "ctx.read_poll": 1, "pop.direct": 1, "pop.wire_early": 1}
 
